@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Benchmark: utterances/sec of the full ESPnet2 Conformer CTC/attention training step.
+
+    python bench.py [--gpus N --steps K --warmup W --batch B]
+    (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+Workload (BASELINE.json configs[1]): 80-dim fbank x 1500 frames,
+Conformer encoder d=256, 4 heads, FF 1024, 12 blocks (macaron, rel-pos latest, cnn k=31),
+Transformer decoder 6 x (4 heads, FF 2048), V=600, ctc_weight 0.3, lsm 0.1, dropout 0.1
+everywhere (SLURP YAML), SpecAug on (time warp 5, 2 freq masks <30, 2 time masks <40),
+UtteranceMVN, Adam + WarmupLR(25k) + grad clip 5.  A step = fwd + bwd + RCCL grad average
+(N>1) + clip + Adam + LR step, on a resident synthetic batch per GPU (weak scaling).
+Prints ONE JSON line (rank 0) with the roofline of the dominant kernel family (the MFMA
+GEMM) measured live with HIP events, and a CPU baseline (the oracle restatement timed on
+the host cores, rank 0 at N=1 only).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+HBM_PEAK_GBS = 8000.0
+
+
+def conformer_flops_per_utt(D, H, FF, L_enc, FF_dec, L_dec, V, T=1500, F=80, U1=41):
+    """Algorithmic forward FLOPs per utterance (SURVEY.md §8(d) formula, 2 FLOP/MAC)."""
+    T1, F1 = (T - 3) // 2 + 1, (F - 3) // 2 + 1
+    Tp, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
+    conv1 = 2 * 9 * D * T1 * F1
+    embed = conv1 + 2 * 9 * D * D * Tp * F2 + 2 * Tp * F2 * D * D
+    blk = (8 * Tp * D * FF + 8 * Tp * D * D + 2 * (2 * Tp - 1) * D * D + 2 * Tp * Tp * D
+           + 2 * Tp * (2 * Tp - 1) * D + 2 * Tp * Tp * D + 4 * Tp * D * D + 2 * Tp * D * 31 + 2 * Tp * D * D)
+    dec = L_dec * (8 * U1 * D * D + 4 * U1 * D * D + 4 * Tp * D * D + 4 * U1 * D * FF_dec + 4 * U1 * U1 * D
+                   + 4 * U1 * Tp * D) + 2 * U1 * D * V
+    ctc = 2 * Tp * D * V
+    fwd = embed + L_enc * blk + dec + ctc
+    return fwd, 3 * fwd - conv1
+
+
+def build(args, device):
+    from espnet_slurp_amd.asr.ctc import CTC
+    from espnet_slurp_amd.asr.decoder.transformer_decoder import TransformerDecoder
+    from espnet_slurp_amd.asr.encoder.conformer_encoder import ConformerEncoder
+    from espnet_slurp_amd.asr.espnet_model import ESPnetASRModel
+    from espnet_slurp_amd.asr.specaug.specaug import SpecAug
+    from espnet_slurp_amd.layers.utterance_mvn import UtteranceMVN
+    V = args.vocab
+    tokens = ["<blank>", "<unk>"] + [f"t{i}" for i in range(V - 3)] + ["<sos/eos>"]
+    enc = ConformerEncoder(input_size=80, output_size=args.d, attention_heads=args.heads, linear_units=args.ff,
+                           num_blocks=args.layers, dropout_rate=0.1, positional_dropout_rate=0.1,
+                           attention_dropout_rate=0.1, input_layer="conv2d", normalize_before=True,
+                           macaron_style=True, rel_pos_type=args.rel_pos, pos_enc_layer_type="rel_pos",
+                           selfattention_layer_type="rel_selfattn", activation_type="swish", use_cnn_module=True,
+                           cnn_module_kernel=31)
+    dec = TransformerDecoder(vocab_size=V, encoder_output_size=args.d, attention_heads=args.heads,
+                             linear_units=2048, num_blocks=6, dropout_rate=0.1, positional_dropout_rate=0.1,
+                             self_attention_dropout_rate=0.1, src_attention_dropout_rate=0.1)
+    specaug = SpecAug(apply_time_warp=True, time_warp_window=5, time_warp_mode="bicubic", apply_freq_mask=True,
+                      freq_mask_width_range=[0, 30], num_freq_mask=2, apply_time_mask=True,
+                      time_mask_width_range=[0, 40], num_time_mask=2)
+    model = ESPnetASRModel(vocab_size=V, token_list=tokens, frontend=None, specaug=specaug,
+                           normalize=UtteranceMVN(), preencoder=None, encoder=enc, postencoder=None, decoder=dec,
+                           ctc=CTC(V, args.d), joint_network=None, ctc_weight=0.3, lsm_weight=0.1,
+                           length_normalized_loss=False)
+    model = model.to(device)
+    model.flatten()
+    return model
+
+
+def synthetic_batch(B, V, rank, device):
+    g = torch.Generator().manual_seed(1234 + rank)
+    speech = torch.randn(B, 1500, 80, generator=g).to(device)
+    speech_lengths = torch.full((B,), 1500, dtype=torch.long)
+    tl = torch.randint(20, 41, (B,), generator=g)
+    text = torch.full((B, int(tl.max())), -1, dtype=torch.long)
+    for i in range(B):
+        text[i, : tl[i]] = torch.randint(2, V - 1, (int(tl[i]),), generator=g)
+    return dict(speech=speech, speech_lengths=speech_lengths, text=text, text_lengths=tl)
+
+
+def cpu_baseline(args):
+    """The oracle (plain PyTorch CPU restatement, oracle/espnet_cpu.py) timed on the host
+    cores: same C2 model shape, fp32, B=4 x 1500 frames, dropout 0.1, no SpecAug draws,
+    1 warmup + 3 timed steps of fwd + bwd + clip + torch Adam."""
+    from oracle import espnet_cpu as O
+    n = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(n)
+    cfg = O.ModelCfg(vocab_size=args.vocab, enc=O.EncCfg(output_size=args.d, attention_heads=args.heads,
+                                                          linear_units=args.ff, num_blocks=args.layers,
+                                                          dropout_rate=0.1, positional_dropout_rate=0.1,
+                                                          attention_dropout_rate=0.1, rel_pos_type=args.rel_pos),
+                     dec=O.DecCfg(attention_heads=args.heads, linear_units=2048, num_blocks=6, dropout_rate=0.1,
+                                  positional_dropout_rate=0.1, self_attention_dropout_rate=0.1,
+                                  src_attention_dropout_rate=0.1))
+    P = {k: v.requires_grad_(v.is_floating_point() and "running" not in k)
+         for k, v in O.deterministic_params(cfg, 0).items()}
+    params = [v for v in P.values() if v.requires_grad]
+    opt = torch.optim.Adam(params, lr=2e-4)
+    B = 4
+    speech, slen, text, tlen = O.synthetic_batch(B, 1500, 80, args.vocab, [1500] * B, [40, 33, 27, 20], 7)
+    bn = {}
+    times = []
+    for it in range(4):
+        t0 = time.perf_counter()
+        loss, _, _ = O.asr_forward(P, speech, slen, text, tlen, cfg, bn_state=bn)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(params, 5.0)
+        opt.step()
+        opt.zero_grad()
+        times.append(time.perf_counter() - t0)
+    t = sum(times[1:]) / len(times[1:])
+    return {"value": round(B / t, 4), "unit": "utt/s", "cores": n, "kind": "port",
+            "sample": f"oracle/espnet_cpu.py C2 step (fwd+bwd+clip+Adam), B=4 x 1500 frames, fp32, "
+                      f"1 warmup + 3 timed steps, {t:.2f} s/step on {n} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=64, help="utterances per GPU")
+    ap.add_argument("--d", type=int, default=256)
+    ap.add_argument("--heads", type=int, default=4)
+    ap.add_argument("--ff", type=int, default=1024)
+    ap.add_argument("--layers", type=int, default=12)
+    ap.add_argument("--vocab", type=int, default=600)
+    ap.add_argument("--rel-pos", default="latest", choices=["latest", "legacy"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    torch.manual_seed(0)
+
+    from espnet_slurp_amd import kernels as K
+    from espnet_slurp_amd.optimizers.fused_adam import FusedAdam
+    from espnet_slurp_amd.schedulers.warmup_lr import WarmupLR
+    from espnet_slurp_amd.train.trainer import Trainer, TrainerOptions
+
+    model = build(args, device)
+    model.train()
+    opt = FusedAdam(model.parameters(), model.flat, lr=2e-4)
+    sched = WarmupLR(opt, warmup_steps=25000)
+    trainer = Trainer(model, opt, sched, TrainerOptions(grad_clip=5.0), distributed=world > 1)
+    batch = synthetic_batch(args.batch, args.vocab, rank, device)
+
+    for _ in range(args.warmup):
+        trainer.train_one_step(batch)
+    torch.cuda.synchronize()
+
+    K.profile_gemm_start()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        trainer.train_one_step(batch)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    gemm_flops, gemm_ms, gemm_launches = K.profile_gemm_stop()
+
+    el = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+
+    if rank == 0:
+        fwd, train = conformer_flops_per_utt(args.d, args.heads, args.ff, args.layers, 2048, 6, args.vocab)
+        value = world * args.batch * args.steps / elapsed
+        achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args)
+        out = {
+            "metric": "utterances/sec (fbank80x1500, Conformer-12L CTC+attn)",
+            "value": round(value, 3),
+            "unit": "utt/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (N(0,1) fbank, random tokens U[20,40], random-init weights)",
+            "config": {"workload": f"C2 SLURP Conformer-medium d={args.d} H={args.heads} FF={args.ff} "
+                                   f"{args.layers}L enc / 6L dec, V={args.vocab}, rel_pos={args.rel_pos}, "
+                                   "ctc 0.3, lsm 0.1, dropout 0.1, SpecAug on",
+                       "global_batch": world * args.batch, "seq_len": 1500, "parallelism": f"dp{world}"},
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                         "kernel": "gemm_f32_kernel (all MFMA GEMM launches in the timed region)",
+                         "launches": gemm_launches,
+                         "avg_launch_us": round(1e3 * gemm_ms / max(1, gemm_launches), 2)},
+            "step_roofline": {"train_gflop_per_utt": round(train / 1e9, 2),
+                              "achieved_tflops": round(value / world * train / 1e12, 2),
+                              "frac_of_fp32_mfma_peak": round(value / world * train / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,93 @@
+"""ctypes loader for libespnet_mi355.so (the C ABI in include/espnet_mi355.h).
+
+There is no CPU fallback: if the library is missing or cannot be loaded, importing the
+compute path raises.  Build it with `make -C espnet_slurp_amd/csrc` (or
+`__graft_entry__.build()`).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libespnet_mi355.so")
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L = ctypes.c_long
+F = ctypes.c_float
+U64 = ctypes.c_ulonglong
+
+# name -> argtypes (all return int status unless listed in _RESTYPES)
+SIGNATURES = {
+    "esp_last_error": [],
+    "esp_abi_version": [],
+    "esp_gemm_f32": [I, I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, L, P, F, F, P, I, P, F, U64, P, P, P],
+    "esp_act_bwd": [P, P, P, L, I, F, U64, L, P],
+    "esp_scale_dropout": [P, P, L, F, F, U64, P, F, P],
+    "esp_scale_by_dev": [P, L, P, P],
+    "esp_embed_fwd": [P, P, P, P, I, I, I, F, F, U64, P],
+    "esp_embed_bwd": [P, P, P, I, I, I, F, F, U64, P],
+    "esp_specaug": [P, P, I, I, I, P, P, P, I, P, I, P],
+    "esp_utterance_mvn": [P, I, I, I, P, P],
+    "esp_grad_norm": [P, L, F, P, P, P],
+    "esp_adam": [P, P, P, P, L, P, F, F, F, F, F, I, P],
+    "esp_layernorm_fwd": [P, P, P, P, P, P, I, I, F, P],
+    "esp_layernorm_bwd": [P, P, P, P, P, P, I, P, P, I, I, P, P],
+    "esp_colsum": [P, I, I, L, P, I, P, P],
+    "esp_glu_fwd": [P, P, L, I, P],
+    "esp_glu_bwd": [P, P, P, L, I, P],
+    "esp_dwconv1d": [P, P, P, P, I, I, I, I, I, P],
+    "esp_dwconv1d_wgrad": [P, P, P, I, I, I, I, P, P],
+    "esp_bn_swish_fwd": [P, P, P, P, P, P, P, P, F, F, I, I, P, P],
+    "esp_bn_swish_bwd": [P, P, P, P, P, P, P, P, P, I, I, P, P, P],
+    "esp_heads_split": [P, L, I, I, I, I, I, P, P, P],
+    "esp_add2d": [P, L, P, L, I, I, P],
+    "esp_attn_softmax_fwd": [P, P, I, I, F, P, I, I, P, P, F, U64, I, I, I, P],
+    "esp_attn_softmax_bwd": [P, P, P, F, U64, F, L, I, P],
+    "esp_relshift_bwd": [P, P, I, I, I, I, P],
+    "esp_conv1_fwd": [P, P, P, P, I, I, I, I, P],
+    "esp_col2im_relu": [P, P, P, I, I, I, I, P],
+    "esp_conv1_wgrad": [P, P, P, P, I, I, I, I, P, P],
+    "esp_permute3": [P, P, I, I, I, I, P],
+    "esp_log_softmax": [P, P, L, I, P],
+    "esp_ctc_loss": [P, P, I, P, P, I, I, I, I, F, I, P, P, P, P],
+    "esp_label_smoothing": [P, P, L, I, I, F, F, P, P, P, P],
+    "esp_reduce_losses": [P, I, I, P, P, I, F, F, P, P],
+    "esp_argmax": [P, P, L, I, P],
+    "esp_ctc_forced_align": [P, I, I, P, I, I, P, P, P],
+}
+_RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load the native library once; raise loudly when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"espnet_slurp_amd: native library not found at {LIB_PATH}; "
+            "build it with `make -C espnet_slurp_amd/csrc` (no CPU fallback exists)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = _RESTYPES.get(name, I)
+    _lib = lib
+    return lib
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def call(name: str, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.esp_last_error().decode(errors="replace")
+        raise NativeError(f"{name} failed ({rc}): {msg}")
+    return rc

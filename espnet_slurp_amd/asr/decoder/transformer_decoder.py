@@ -1,0 +1,133 @@
+"""TransformerDecoder — drop-in for espnet2/asr/decoder/transformer_decoder.py:28-145,232-280.
+
+Embedding(V,D) -> x*sqrt(D)+PE (dropout) -> num_blocks x [LN -> causal self-MHA -> +res;
+LN -> source MHA over the encoder output -> +res; LN -> FFN(ReLU) -> +res]
+(transformer/decoder_layer.py:63-134) -> after_norm -> Linear(D, V).
+Masks: tgt (j < ys_in_len_b and j <= i), memory (j < hlen_b) — applied inside the softmax
+kernel, nothing materialised.  Explicit backward; the memory gradient of every layer is
+accumulated into one dhs buffer.
+"""
+from __future__ import annotations
+
+import math
+from typing import Tuple
+
+import torch
+from torch import nn
+
+from ... import kernels as K
+from ...blocks import Ctx, LayerNorm, Linear, MultiHeadedAttention, PositionwiseFeedForward, Seeds, empty
+from ..encoder.abs_encoder import pos_table
+
+
+class AbsDecoder(nn.Module):
+    """espnet2/asr/decoder/abs_decoder.py:9-18."""
+
+    def forward(self, hs_pad, hlens, ys_in_pad, ys_in_lens):
+        raise NotImplementedError
+
+
+class DecoderLayer(nn.Module):
+    def __init__(self, size, self_attn, src_attn, feed_forward, dropout_rate):
+        super().__init__()
+        self.size = size
+        self.self_attn = self_attn
+        self.src_attn = src_attn
+        self.feed_forward = feed_forward
+        self.norm1 = LayerNorm(size)
+        self.norm2 = LayerNorm(size)
+        self.norm3 = LayerNorm(size)
+        self.p = dropout_rate
+
+    def fwd(self, x, mem, B, L, Tm, tgt_klen, mem_klen, seeds, training):
+        c = Ctx()
+        h, c.ln1 = self.norm1.fwd(x)
+        x, c.sa = self.self_attn.fwd(h, x, B, L, tgt_klen, True, self.p, seeds, training)
+        h, c.ln2 = self.norm2.fwd(x)
+        x, c.src = self.src_attn.fwd(h, x, B, L, mem_klen, False, self.p, seeds, training, mem=mem, Tk=Tm)
+        h, c.ln3 = self.norm3.fwd(x)
+        x, c.ff = self.feed_forward.fwd(h, x, 1.0, self.p, seeds, training)
+        return x, c
+
+    def bwd(self, c, d, dmem):
+        self.norm3.bwd(c.ln3, self.feed_forward.bwd(c.ff, d), d)
+        self.norm2.bwd(c.ln2, self.src_attn.bwd(c.src, d, dmem), d)
+        self.norm1.bwd(c.ln1, self.self_attn.bwd(c.sa, d), d)
+        return d
+
+
+class TransformerDecoder(AbsDecoder):
+    def __init__(self, vocab_size: int, encoder_output_size: int, attention_heads: int = 4,
+                 linear_units: int = 2048, num_blocks: int = 6, dropout_rate: float = 0.1,
+                 positional_dropout_rate: float = 0.1, self_attention_dropout_rate: float = 0.0,
+                 src_attention_dropout_rate: float = 0.0, input_layer: str = "embed",
+                 use_output_layer: bool = True, pos_enc_class=None, normalize_before: bool = True,
+                 concat_after: bool = False, layer_drop_rate: float = 0.0):
+        super().__init__()
+        if input_layer != "embed" or not use_output_layer or not normalize_before or concat_after or layer_drop_rate:
+            raise NotImplementedError("espnet_slurp_amd TransformerDecoder: embed/pre-LN/output-layer form only")
+        D = encoder_output_size
+        self.embed = nn.Sequential(nn.Embedding(vocab_size, D))
+        self.after_norm = LayerNorm(D)
+        self.output_layer = Linear(D, vocab_size)
+        self.decoders = nn.ModuleList([
+            DecoderLayer(D, MultiHeadedAttention(attention_heads, D, self_attention_dropout_rate),
+                         MultiHeadedAttention(attention_heads, D, src_attention_dropout_rate),
+                         PositionwiseFeedForward(D, linear_units, dropout_rate, K.ACT_RELU), dropout_rate)
+            for _ in range(num_blocks)])
+        self.dropout_rate = dropout_rate
+        self.positional_dropout_rate = positional_dropout_rate
+        self.vocab_size = vocab_size
+        self.D = D
+        self.flat = None
+
+    def attach_flat(self, flat):
+        self.flat = flat
+        for l in self.decoders:
+            l.self_attn.flat = flat
+            l.src_attn.flat = flat
+
+    def run_forward(self, hs, hlens_i32, ys_in, ys_in_lens_i32, seeds: Seeds, training: bool):
+        B, Tm, D = hs.shape
+        L = ys_in.shape[1]
+        mem = hs.reshape(B * Tm, D)
+        pe = pos_table("abs", L, D, hs.device)
+        x = empty(B * L, D, like=hs)
+        pp = self.positional_dropout_rate if training else 0.0
+        sp = seeds.next()
+        E = self.embed[0].weight
+        K.embed_fwd(ys_in, E, pe, x, L, math.sqrt(D), pp, sp)
+        ctxs = []
+        for layer in self.decoders:
+            x, c = layer.fwd(x, mem, B, L, Tm, ys_in_lens_i32, hlens_i32, seeds, training)
+            ctxs.append(c)
+        y, c_after = self.after_norm.fwd(x)
+        logits = self.output_layer.fwd(y)
+        return logits, Ctx(ys_in=ys_in, pp=pp, sp=sp, layers=ctxs, after=c_after, y=y, B=B, L=L, Tm=Tm, mem=mem)
+
+    def run_backward(self, saved, dlogits, dmem, grad_hook=None):
+        """dlogits (B*L, V); dmem (B*Tm, D) accumulated (+=)."""
+        dy = self.output_layer.bwd(dlogits, saved.y)
+        d = self.after_norm.bwd_new(saved.after, dy)
+        if grad_hook is not None:
+            grad_hook(self.output_layer)
+            grad_hook(self.after_norm)
+        for i in range(len(self.decoders) - 1, -1, -1):
+            d = self.decoders[i].bwd(saved.layers[i], d, dmem)
+            saved.layers[i] = None
+            if grad_hook is not None:
+                grad_hook(self.decoders[i])
+        K.embed_bwd(saved.ys_in, d, self.embed[0].weight.grad, math.sqrt(self.D), saved.pp, saved.sp)
+        if grad_hook is not None:
+            grad_hook(self.embed)
+
+    def forward(self, hs_pad: torch.Tensor, hlens: torch.Tensor, ys_in_pad: torch.Tensor,
+                ys_in_lens: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Inference-style forward (no parameter gradients): returns (logits, olens)."""
+        from ..encoder.abs_encoder import draw_seed
+        with torch.no_grad():
+            logits, _ = self.run_forward(hs_pad.contiguous(), hlens.to(torch.int32).to(hs_pad.device),
+                                         ys_in_pad.to(hs_pad.device), ys_in_lens.to(torch.int32).to(hs_pad.device),
+                                         Seeds(draw_seed()), self.training)
+        B, L = ys_in_pad.shape
+        return logits.view(B, L, -1), ys_in_lens

@@ -1,0 +1,223 @@
+"""ConformerEncoder — drop-in for espnet2/asr/encoder/conformer_encoder.py:47-368.
+
+Same constructor kwargs and state_dict keys; forward(xs_pad, ilens) -> (out, olens, None).
+Computation: Conv2dSubsampling (implicit-im2col MFMA GEMM) -> x*sqrt(D) + rel-pos table
+-> num_blocks macaron Conformer blocks -> after_norm, all in libespnet_mi355.so kernels
+with an explicit backward (EncoderFn).  Supported configuration space = the one the
+SLURP / LibriSpeech Conformer recipes use; anything else raises NotImplementedError.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional, Tuple, Union
+
+import torch
+from torch import nn
+
+from ... import kernels as K
+from ...blocks import (ConvolutionModule, Conv2dSubsampling, Ctx, LayerNorm, PositionwiseFeedForward,
+                       RelPositionMultiHeadedAttention, Seeds, empty)
+from .abs_encoder import (AbsEncoder, EncoderFn, TooShortUttError, draw_seed, lengths_to_device, pos_table,
+                          subsampled_lengths)
+
+
+class EncoderLayer(nn.Module):
+    """Conformer block (conformer/encoder_layer.py:17-157), normalize_before=True,
+    concat_after=False:  x += ff_scale*drop(FFN_mac(LN(x))); x += drop(MHA(LN(x)));
+    x += drop(Conv(LN(x))); x += ff_scale*drop(FFN(LN(x))); x = LN_final(x)."""
+
+    def __init__(self, size, self_attn, feed_forward, feed_forward_macaron, conv_module, dropout_rate):
+        super().__init__()
+        self.self_attn = self_attn
+        self.feed_forward = feed_forward
+        self.feed_forward_macaron = feed_forward_macaron
+        self.conv_module = conv_module
+        self.norm_ff = LayerNorm(size)
+        self.norm_mha = LayerNorm(size)
+        if feed_forward_macaron is not None:
+            self.norm_ff_macaron = LayerNorm(size)
+            self.ff_scale = 0.5
+        else:
+            self.ff_scale = 1.0
+        if conv_module is not None:
+            self.norm_conv = LayerNorm(size)
+            self.norm_final = LayerNorm(size)
+        self.p = dropout_rate
+        self.size = size
+
+    def fwd(self, x, pos, klen, B, T, seeds: Seeds, training: bool):
+        c = Ctx()
+        p = self.p
+        if self.feed_forward_macaron is not None:
+            h, c.ln_mac = self.norm_ff_macaron.fwd(x)
+            x, c.ffm = self.feed_forward_macaron.fwd(h, x, self.ff_scale, p, seeds, training)
+        h, c.ln_mha = self.norm_mha.fwd(x)
+        x, c.mha = self.self_attn.fwd(h, x, pos, klen, B, T, p, seeds, training)
+        if self.conv_module is not None:
+            h, c.ln_conv = self.norm_conv.fwd(x)
+            x, c.conv = self.conv_module.fwd(h, x, B, T, p, seeds, training)
+        h, c.ln_ff = self.norm_ff.fwd(x)
+        x, c.ff = self.feed_forward.fwd(h, x, self.ff_scale, p, seeds, training)
+        if self.conv_module is not None:
+            x, c.ln_final = self.norm_final.fwd(x)
+        return x, c
+
+    def bwd(self, c, d):
+        if self.conv_module is not None:
+            d = self.norm_final.bwd_new(c.ln_final, d)
+        self.norm_ff.bwd(c.ln_ff, self.feed_forward.bwd(c.ff, d), d)
+        if self.conv_module is not None:
+            self.norm_conv.bwd(c.ln_conv, self.conv_module.bwd(c.conv, d), d)
+        self.norm_mha.bwd(c.ln_mha, self.self_attn.bwd(c.mha, d), d)
+        if self.feed_forward_macaron is not None:
+            self.norm_ff_macaron.bwd(c.ln_mac, self.feed_forward_macaron.bwd(c.ffm, d), d)
+        return d
+
+
+class ConformerEncoder(AbsEncoder):
+    def __init__(
+        self,
+        input_size: int,
+        output_size: int = 256,
+        attention_heads: int = 4,
+        linear_units: int = 2048,
+        num_blocks: int = 6,
+        dropout_rate: float = 0.1,
+        positional_dropout_rate: float = 0.1,
+        attention_dropout_rate: float = 0.0,
+        input_layer: str = "conv2d",
+        normalize_before: bool = True,
+        concat_after: bool = False,
+        positionwise_layer_type: str = "linear",
+        positionwise_conv_kernel_size: int = 3,
+        macaron_style: bool = False,
+        rel_pos_type: str = "legacy",
+        pos_enc_layer_type: str = "rel_pos",
+        selfattention_layer_type: str = "rel_selfattn",
+        activation_type: str = "swish",
+        use_cnn_module: bool = True,
+        zero_triu: bool = False,
+        cnn_module_kernel: int = 31,
+        padding_idx: int = -1,
+        interctc_layer_idx: List[int] = [],
+        interctc_use_conditioning: bool = False,
+        stochastic_depth_rate: Union[float, List[float]] = 0.0,
+        layer_drop_rate: float = 0.0,
+        max_pos_emb_len: int = 5000,
+    ):
+        super().__init__()
+        self._output_size = output_size
+        # rel_pos_type remap, conformer_encoder.py:116-125
+        if rel_pos_type == "legacy":
+            if pos_enc_layer_type == "rel_pos":
+                pos_enc_layer_type = "legacy_rel_pos"
+            if selfattention_layer_type == "rel_selfattn":
+                selfattention_layer_type = "legacy_rel_selfattn"
+        elif rel_pos_type == "latest":
+            assert selfattention_layer_type != "legacy_rel_selfattn"
+            assert pos_enc_layer_type != "legacy_rel_pos"
+        else:
+            raise ValueError("unknown rel_pos_type: " + rel_pos_type)
+        unsupported = []
+        if input_layer != "conv2d":
+            unsupported.append(f"input_layer={input_layer}")
+        if not normalize_before or concat_after:
+            unsupported.append("normalize_before=False/concat_after=True")
+        if positionwise_layer_type != "linear":
+            unsupported.append(f"positionwise_layer_type={positionwise_layer_type}")
+        if (pos_enc_layer_type, selfattention_layer_type) not in (("rel_pos", "rel_selfattn"),
+                                                                  ("legacy_rel_pos", "legacy_rel_selfattn")):
+            unsupported.append(f"{pos_enc_layer_type}/{selfattention_layer_type}")
+        if activation_type != "swish":
+            unsupported.append(f"activation_type={activation_type}")
+        if zero_triu or interctc_layer_idx or interctc_use_conditioning or layer_drop_rate:
+            unsupported.append("zero_triu/interctc/layer_drop")
+        sdr = stochastic_depth_rate if isinstance(stochastic_depth_rate, list) else [stochastic_depth_rate]
+        if any(r != 0.0 for r in sdr):
+            unsupported.append("stochastic_depth_rate")
+        if unsupported:
+            raise NotImplementedError("espnet_slurp_amd ConformerEncoder: unsupported " + ", ".join(unsupported))
+        self.legacy = pos_enc_layer_type == "legacy_rel_pos"
+        self.embed = Conv2dSubsampling(input_size, output_size)
+        self.encoders = nn.ModuleList([
+            EncoderLayer(
+                output_size,
+                RelPositionMultiHeadedAttention(attention_heads, output_size, attention_dropout_rate, self.legacy),
+                PositionwiseFeedForward(output_size, linear_units, dropout_rate, K.ACT_SWISH),
+                PositionwiseFeedForward(output_size, linear_units, dropout_rate, K.ACT_SWISH) if macaron_style else None,
+                ConvolutionModule(output_size, cnn_module_kernel) if use_cnn_module else None,
+                dropout_rate,
+            ) for _ in range(num_blocks)
+        ])
+        self.after_norm = LayerNorm(output_size)
+        self.dropout_rate = dropout_rate
+        self.positional_dropout_rate = positional_dropout_rate
+        self.max_pos_emb_len = max_pos_emb_len
+        self.interctc_layer_idx = interctc_layer_idx
+        self.interctc_use_conditioning = interctc_use_conditioning
+        self.flat = None
+        self._seed_counter = 0
+
+    def output_size(self) -> int:
+        return self._output_size
+
+    def attach_flat(self, flat):
+        self.flat = flat
+        for l in self.encoders:
+            l.self_attn.flat = flat
+
+    # ---------------------------------------------------------------- explicit passes
+    def run_forward(self, feats, ilens_cpu, seeds: Seeds, training: bool):
+        B, T, _ = feats.shape
+        if T < 7:
+            raise TooShortUttError(
+                f"has {T} frames and is too short for subsampling (it needs more than 7 frames), return empty results",
+                T, 7)
+        D = self._output_size
+        olens = subsampled_lengths(ilens_cpu, T)
+        klen = lengths_to_device(olens, feats.device)
+        x, c_emb = self.embed.fwd(feats, math.sqrt(D), self.positional_dropout_rate, seeds, training)
+        T2 = c_emb.T2
+        tab = pos_table("legacy" if self.legacy else "latest", T2, D, feats.device, self.max_pos_emb_len)
+        pp = self.positional_dropout_rate if training else 0.0
+        sp = seeds.next()
+        if pp > 0:
+            pos = torch.empty_like(tab)
+            K.scale_dropout(tab, pos, drop_p=pp, seed=sp)
+        else:
+            pos = tab
+        ctxs = []
+        for layer in self.encoders:
+            x, c = layer.fwd(x, pos, klen, B, T2, seeds, training)
+            ctxs.append(c)
+        hs, c_after = self.after_norm.fwd(x)
+        return hs.view(B, T2, D), olens, Ctx(emb=c_emb, layers=ctxs, after=c_after)
+
+    def run_backward(self, saved, dhs, grad_hook=None):
+        B, T2, D = dhs.shape
+        d = self.after_norm.bwd_new(saved.after, dhs.view(B * T2, D))
+        if grad_hook is not None:
+            grad_hook(self.after_norm)
+        for i in range(len(self.encoders) - 1, -1, -1):
+            d = self.encoders[i].bwd(saved.layers[i], d)
+            saved.layers[i] = None
+            if grad_hook is not None:
+                grad_hook(self.encoders[i])
+        self.embed.bwd(saved.emb, d)
+        if grad_hook is not None:
+            grad_hook(self.embed)
+
+    def forward(self, xs_pad: torch.Tensor, ilens: torch.Tensor, prev_states: torch.Tensor = None,
+                ctc=None) -> Tuple[torch.Tensor, torch.Tensor, Optional[torch.Tensor]]:
+        assert self.flat is not None, "call espnet_slurp_amd.flatten_model(model) before running"
+        ilens_cpu = ilens.detach().cpu()
+        feats = xs_pad.contiguous().float()
+        seed = draw_seed()
+        anchor = self.after_norm.weight
+        hook = getattr(self, "_grad_hook", None)
+        if torch.is_grad_enabled() and anchor.requires_grad:
+            hs = EncoderFn.apply(feats, anchor, self, ilens_cpu, seed, hook)
+            olens = subsampled_lengths(ilens_cpu, feats.shape[1])
+        else:
+            hs, olens, _ = self.run_forward(feats, ilens_cpu, Seeds(seed), self.training)
+        return hs, olens.to(xs_pad.device), None

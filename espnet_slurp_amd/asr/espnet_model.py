@@ -1,0 +1,223 @@
+"""ESPnetASRModel — drop-in for espnet2/asr/espnet_model.py:36-297 (CTC/attention hybrid).
+
+forward(speech, speech_lengths, text, text_lengths) -> (loss[1], stats, weight[1]) exactly
+like the reference (stat keys loss_ctc / loss_att / acc / loss, plus cer/wer = None).
+The step runs as two autograd nodes whose backward passes are explicit kernel sequences:
+  EncoderFn (asr/encoder/abs_encoder.py): SpecAug/MVN'd fbank -> encoder output hs
+  HeadsFn (below): CTC branch + decoder branch + label-smoothing loss, fused loss
+    gradients (computed in the forward, scaled by grad_output in the backward), one dhs.
+Parameter gradients are written into the flat gradient buffer (flat.py).
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple, Union
+
+import torch
+from torch import nn
+
+from .. import kernels as K
+from ..blocks import Seeds, empty
+from ..flat import FlatParams
+from .encoder.abs_encoder import draw_seed
+
+
+class AbsESPnetModel(nn.Module):
+    """espnet2/train/abs_espnet_model.py:7-40."""
+
+    def forward(self, **batch):
+        raise NotImplementedError
+
+    def collect_feats(self, **batch):
+        raise NotImplementedError
+
+
+def add_sos_eos(ys_pad_cpu: torch.Tensor, ys_lens_cpu: torch.Tensor, sos: int, eos: int, ignore_id: int):
+    """add_sos_eos.py:12-31 on the host (integer bookkeeping): ys_in padded with eos,
+    ys_out padded with ignore_id."""
+    B = ys_pad_cpu.shape[0]
+    ys = [ys_pad_cpu[i][ys_pad_cpu[i] != ignore_id] for i in range(B)]
+    L = max(int(y.numel()) for y in ys) + 1
+    ys_in = torch.full((B, L), eos, dtype=torch.long)
+    ys_out = torch.full((B, L), ignore_id, dtype=torch.long)
+    for i, y in enumerate(ys):
+        n = int(y.numel())
+        ys_in[i, 0] = sos
+        ys_in[i, 1:n + 1] = y
+        ys_out[i, :n] = y
+        ys_out[i, n] = eos
+    return ys_in, ys_out, torch.tensor([int(y.numel()) + 1 for y in ys], dtype=torch.long)
+
+
+class HeadsFn(torch.autograd.Function):
+    """CTC + attention-decoder losses of one batch; backward returns d loss / d hs."""
+
+    @staticmethod
+    def forward(ctx, hs, anchor, model, hlens_cpu, text_cpu, text_lengths_cpu, seed):
+        out4, state = model._heads_forward(hs, hlens_cpu, text_cpu, text_lengths_cpu, Seeds(seed), True)
+        ctx.model = model
+        ctx.state = state
+        loss = out4[3:4].clone()
+        others = out4[0:3].clone()
+        ctx.mark_non_differentiable(others)
+        return loss, others
+
+    @staticmethod
+    def backward(ctx, g_loss, g_others):
+        dhs = ctx.model._heads_backward(ctx.state, g_loss.contiguous())
+        ctx.state = None
+        return dhs, None, None, None, None, None, None
+
+
+class ESPnetASRModel(AbsESPnetModel):
+    def __init__(self, vocab_size: int, token_list: Union[Tuple[str, ...], List[str]], frontend, specaug,
+                 normalize, preencoder, encoder, postencoder, decoder, ctc, joint_network=None,
+                 ctc_weight: float = 0.5, interctc_weight: float = 0.0, ignore_id: int = -1,
+                 lsm_weight: float = 0.0, length_normalized_loss: bool = False, report_cer: bool = True,
+                 report_wer: bool = True, sym_space: str = "<space>", sym_blank: str = "<blank>",
+                 sym_sos: str = "<sos/eos>", sym_eos: str = "<sos/eos>", extract_feats_in_collect_stats: bool = True,
+                 lang_token_id: int = -1):
+        assert 0.0 <= ctc_weight <= 1.0, ctc_weight
+        super().__init__()
+        if frontend is not None or preencoder is not None or postencoder is not None or joint_network is not None:
+            raise NotImplementedError("frontend/pre-/post-encoder/transducer are not on the fbank hot path")
+        if interctc_weight != 0.0 or lang_token_id != -1:
+            raise NotImplementedError("interctc / lang_token_id")
+        self.blank_id = token_list.index(sym_blank)
+        self.sos = token_list.index(sym_sos) if sym_sos in token_list else vocab_size - 1
+        self.eos = token_list.index(sym_eos) if sym_eos in token_list else vocab_size - 1
+        self.vocab_size = vocab_size
+        self.ignore_id = ignore_id
+        self.ctc_weight = ctc_weight
+        self.interctc_weight = interctc_weight
+        self.token_list = list(token_list).copy()
+        self.frontend = frontend
+        self.specaug = specaug
+        self.normalize = normalize
+        self.preencoder = preencoder
+        self.postencoder = postencoder
+        self.encoder = encoder
+        self.decoder = None if ctc_weight == 1.0 else decoder
+        self.ctc = None if ctc_weight == 0.0 else ctc
+        self.lsm_weight = lsm_weight
+        self.length_normalized_loss = length_normalized_loss
+        self.error_calculator = None
+        self.extract_feats_in_collect_stats = extract_feats_in_collect_stats
+        self.flat: Optional[FlatParams] = None
+        if self.blank_id != 0:
+            raise NotImplementedError("blank must be token 0 (torch CTCLoss default used by espnet2)")
+
+    # ------------------------------------------------------------------ setup
+    def flatten(self, device=None) -> FlatParams:
+        """Move parameters into one flat HBM buffer (+ flat grads).  Call once, after .to(device)."""
+        device = device or next(self.parameters()).device
+        self.flat = FlatParams(self, device)
+        for m in (self.encoder, self.decoder):
+            if m is not None and hasattr(m, "attach_flat"):
+                m.attach_flat(self.flat)
+        return self.flat
+
+    # ------------------------------------------------------------------ heads
+    def _heads_forward(self, hs, hlens_cpu, text_cpu, text_lengths_cpu, seeds: Seeds, want_grad: bool):
+        B, T, D = hs.shape
+        dev = hs.device
+        hs2d = hs.reshape(B * T, D)
+        hlens_i32 = hlens_cpu.to(torch.int32).to(dev, non_blocking=True)
+        state = {"hs2d": hs2d, "B": B, "T": T}
+        nll = grad_ctc = None
+        if self.ctc is not None:
+            Umax = text_cpu.shape[1]
+            ys = text_cpu.to(dev, non_blocking=True)
+            tl = text_lengths_cpu.to(torch.int32).to(dev, non_blocking=True)
+            nll, grad_ctc, _ = self.ctc.loss_and_grad(hs2d, B, T, hlens_i32, ys, tl, Umax,
+                                                      self.ctc_weight / B, want_grad=want_grad)
+            state["grad_ctc"] = grad_ctc
+        row_loss = row_stat = None
+        R = 0
+        denom = float(B)
+        if self.decoder is not None:
+            ys_in, ys_out, ys_in_lens = add_sos_eos(text_cpu, text_lengths_cpu, self.sos, self.eos, self.ignore_id)
+            L = ys_in.shape[1]
+            R = B * L
+            if self.length_normalized_loss:
+                denom = float(int((ys_out != self.ignore_id).sum()))
+            ys_in_d = ys_in.to(dev, non_blocking=True)
+            ys_out_d = ys_out.to(dev, non_blocking=True)
+            logits, dsaved = self.decoder.run_forward(hs, hlens_i32, ys_in_d,
+                                                      ys_in_lens.to(torch.int32).to(dev, non_blocking=True),
+                                                      seeds, self.training)
+            V = self.vocab_size
+            grad_att = empty(R, V, like=hs) if want_grad else None
+            row_loss = empty(R, like=hs)
+            row_stat = torch.empty(2 * R, dtype=torch.int32, device=dev)
+            K.label_smoothing(logits, ys_out_d, V, self.ignore_id, self.lsm_weight,
+                              (1.0 - self.ctc_weight) / denom, grad_att, row_loss, row_stat)
+            state["grad_att"] = grad_att
+            state["dec"] = dsaved
+        out4 = empty(4, like=hs)
+        K.reduce_losses(nll, B, self.ctc.zero_infinity if self.ctc is not None else True, row_loss, row_stat, R,
+                        denom, self.ctc_weight, out4)
+        return out4, state
+
+    def _heads_backward(self, state, g_loss):
+        hs2d = state["hs2d"]
+        dhs = torch.zeros_like(hs2d) if self.ctc is None else torch.empty_like(hs2d)
+        hook = getattr(self, "_grad_hook", None)
+        if self.ctc is not None:
+            g = state["grad_ctc"]
+            K.scale_by_dev(g, g_loss)
+            self.ctc.backward_from_logits(g, hs2d, dhs)
+            if hook is not None:
+                hook(self.ctc)
+        if self.decoder is not None:
+            g = state["grad_att"]
+            K.scale_by_dev(g, g_loss)
+            self.decoder.run_backward(state["dec"], g, dhs, hook)
+        return dhs.view(state["B"], state["T"], -1)
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, speech: torch.Tensor, speech_lengths: torch.Tensor, text: torch.Tensor,
+                text_lengths: torch.Tensor, specaug_draws: Optional[dict] = None, **kwargs):
+        assert text_lengths.dim() == 1, text_lengths.shape
+        assert speech.shape[0] == speech_lengths.shape[0] == text.shape[0] == text_lengths.shape[0], (
+            speech.shape, speech_lengths.shape, text.shape, text_lengths.shape)
+        assert self.flat is not None, "call model.flatten() after moving the model to the GPU"
+        B = speech.shape[0]
+        text[text == -1] = self.ignore_id
+        sl_cpu = speech_lengths.detach().cpu()
+        tl_cpu = text_lengths.detach().cpu()
+        text_cpu = text.detach().cpu()[:, : int(tl_cpu.max())]
+        encoder_out, encoder_out_lens = self.encode(speech, speech_lengths, sl_cpu, specaug_draws)
+        hlens_cpu = encoder_out_lens.detach().cpu()
+        seed = draw_seed()
+        anchor = next(p for p in (self.ctc or self.decoder).parameters())
+        if torch.is_grad_enabled() and anchor.requires_grad:
+            loss, others = HeadsFn.apply(encoder_out, anchor, self, hlens_cpu, text_cpu, tl_cpu, seed)
+        else:
+            out4, _ = self._heads_forward(encoder_out, hlens_cpu, text_cpu, tl_cpu, Seeds(seed), False)
+            loss, others = out4[3:4], out4[0:3]
+        stats = dict(
+            loss_ctc=others[0:1].detach() if self.ctc is not None else None,
+            cer_ctc=None,
+            loss_att=others[1:2].detach() if self.decoder is not None else None,
+            acc=others[2:3].detach() if self.decoder is not None else None,
+            cer=None, wer=None,
+            loss=loss.detach(),
+        )
+        weight = torch.tensor([B], dtype=torch.long, device=loss.device)
+        return loss, stats, weight
+
+    def encode(self, speech: torch.Tensor, speech_lengths: torch.Tensor, sl_cpu: Optional[torch.Tensor] = None,
+               specaug_draws: Optional[dict] = None):
+        """espnet_model.py:319-377 (frontend=None: feats = speech[:, :max_len])."""
+        if sl_cpu is None:
+            sl_cpu = speech_lengths.detach().cpu()
+        feats = speech[:, : int(sl_cpu.max())].contiguous().float()
+        feats_lengths = sl_cpu
+        if self.specaug is not None and self.training:
+            feats, _ = self.specaug(feats, feats_lengths, draws=specaug_draws)
+        if self.normalize is not None:
+            feats, _ = self.normalize(feats, feats_lengths)
+        return self.encoder(feats, feats_lengths)[:2]
+
+    def collect_feats(self, speech, speech_lengths, text, text_lengths, **kwargs) -> Dict[str, torch.Tensor]:
+        return {"feats": speech[:, : int(speech_lengths.max())], "feats_lengths": speech_lengths}

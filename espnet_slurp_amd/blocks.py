@@ -1,0 +1,488 @@
+"""Building blocks of the hot path with explicit forward and backward passes.
+
+Each block mirrors a reference module (same submodule/parameter names, so state_dict keys
+match) and exposes `fwd(...) -> (out, ctx)` / `bwd(ctx, dout) -> dinput`.  Gradients
+are accumulated straight into the flat gradient views (flat.py).  Activations are
+row-major [B*T, D] device tensors.  All arithmetic is in libespnet_mi355.so (kernels.py).
+
+Reference: espnet/nets/pytorch_backend/{conformer,transformer}/*.py (cited per class).
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import torch
+from torch import nn
+
+from . import kernels as K
+
+
+def _mix64(x: int) -> int:
+    x &= 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return x ^ (x >> 31)
+
+
+class Seeds:
+    """Per-forward stream of dropout seeds (stateless counter RNG keys)."""
+
+    def __init__(self, base: int):
+        self.base = base & 0xFFFFFFFFFFFFFFFF
+        self.i = 0
+
+    def next(self) -> int:
+        self.i += 1
+        return _mix64(self.base + 0x9E3779B97F4A7C15 * self.i)
+
+
+class Ctx(dict):
+    __getattr__ = dict.__getitem__
+    __setattr__ = dict.__setitem__
+
+
+def empty(*shape, like: torch.Tensor):
+    return torch.empty(*shape, dtype=torch.float32, device=like.device)
+
+
+class Linear(nn.Module):
+    """Parameter container with torch.nn.Linear's names/shapes/init (weight (out,in), bias)."""
+
+    def __init__(self, idim: int, odim: int, bias: bool = True):
+        super().__init__()
+        ref = nn.Linear(idim, odim, bias=bias)
+        self.weight = ref.weight
+        if bias:
+            self.bias = ref.bias
+        else:
+            self.register_parameter("bias", None)
+
+    def fwd(self, x2d, out=None, **kw):
+        if out is None:
+            out = empty(x2d.shape[0], self.weight.shape[0], like=x2d)
+        return K.linear_fwd(x2d, self.weight, self.bias, out, **kw)
+
+    def bwd(self, dy, x2d, dx=None, accumulate=False, need_dx=True):
+        K.linear_bwd_weight(dy, x2d, self.weight.grad, self.bias.grad if self.bias is not None else None)
+        if not need_dx:
+            return None
+        if dx is None:
+            dx = empty(dy.shape[0], self.weight.shape[1], like=dy)
+            accumulate = False
+        return K.linear_bwd_data(dy, self.weight, dx, accumulate=accumulate)
+
+
+class LayerNorm(nn.Module):
+    """espnet LayerNorm (torch.nn.LayerNorm(size, eps=1e-12)), layer_norm.py:12-38."""
+
+    def __init__(self, size: int, eps: float = 1e-12):
+        super().__init__()
+        ref = nn.LayerNorm(size, eps=eps)
+        self.weight = ref.weight
+        self.bias = ref.bias
+        self.eps = eps
+
+    def fwd(self, x2d):
+        M, D = x2d.shape
+        y = empty(M, D, like=x2d)
+        mean = empty(M, like=x2d)
+        rstd = empty(M, like=x2d)
+        K.layernorm_fwd(x2d, self.weight, self.bias, y, mean, rstd, self.eps)
+        return y, Ctx(x=x2d, mean=mean, rstd=rstd)
+
+    def bwd(self, ctx, dy, dx_acc):
+        """dx_acc += LN'(dy)  (dx_acc is the residual-stream gradient buffer)."""
+        K.layernorm_bwd(dy, ctx.x, self.weight, ctx.mean, ctx.rstd, dx_acc, self.weight.grad, self.bias.grad,
+                        accumulate=True)
+
+    def bwd_new(self, ctx, dy):
+        dx = torch.empty_like(dy)
+        K.layernorm_bwd(dy, ctx.x, self.weight, ctx.mean, ctx.rstd, dx, self.weight.grad, self.bias.grad,
+                        accumulate=False)
+        return dx
+
+
+class PositionwiseFeedForward(nn.Module):
+    """positionwise_feed_forward.py:12-32: w_2(dropout(act(w_1(x))))."""
+
+    def __init__(self, idim: int, hidden: int, dropout_rate: float, act: int):
+        super().__init__()
+        self.w_1 = Linear(idim, hidden)
+        self.w_2 = Linear(hidden, idim)
+        self.p = dropout_rate
+        self.act = act
+
+    def fwd(self, x2d, resid, alpha, p_res, seeds: Seeds, training: bool):
+        """returns resid + alpha * drop_res(w_2(drop(act(w_1 x))))  (new buffer)."""
+        M = x2d.shape[0]
+        H = self.w_1.weight.shape[0]
+        pre = empty(M, H, like=x2d)
+        h = empty(M, H, like=x2d)
+        p_in = self.p if training else 0.0
+        s1, s2 = seeds.next(), seeds.next()
+        self.w_1.fwd(x2d, h, act=self.act, aux=pre, drop_p=p_in, seed=s1)
+        out = empty(M, x2d.shape[1], like=x2d)
+        pr = p_res if training else 0.0
+        self.w_2.fwd(h, out, alpha=alpha, drop_p=pr, seed=s2, R=resid, beta=1.0)
+        return out, Ctx(x=x2d, pre=pre, h=h, s1=s1, s2=s2, p_in=p_in, pr=pr, alpha=alpha)
+
+    def bwd(self, c, dout):
+        """dout: grad w.r.t. the residual output; returns grad w.r.t. x2d (new buffer)."""
+        dz = torch.empty_like(dout)
+        K.scale_dropout(dout, dz, alpha=c.alpha, drop_p=c.pr, seed=c.s2)
+        dh = self.w_2.bwd(dz, c.h)
+        K.act_bwd(dh, c.pre, dh, self.act, drop_p=c.p_in, seed=c.s1)
+        return self.w_1.bwd(dh, c.x)
+
+
+class RelPositionMultiHeadedAttention(nn.Module):
+    """(Legacy)RelPositionMultiHeadedAttention, attention.py:117-308 (zero_triu=False).
+
+    Scores are materialised per (head, utterance) in head-major order z = h*B + b."""
+
+    def __init__(self, n_head: int, n_feat: int, dropout_rate: float, legacy: bool):
+        super().__init__()
+        assert n_feat % n_head == 0
+        self.h, self.d_k = n_head, n_feat // n_head
+        self.linear_q = Linear(n_feat, n_feat)
+        self.linear_k = Linear(n_feat, n_feat)
+        self.linear_v = Linear(n_feat, n_feat)
+        self.linear_out = Linear(n_feat, n_feat)
+        self.linear_pos = Linear(n_feat, n_feat, bias=False)
+        self.pos_bias_u = nn.Parameter(torch.Tensor(self.h, self.d_k))
+        self.pos_bias_v = nn.Parameter(torch.Tensor(self.h, self.d_k))
+        nn.init.xavier_uniform_(self.pos_bias_u)
+        nn.init.xavier_uniform_(self.pos_bias_v)
+        self.p = dropout_rate
+        self.legacy = legacy
+        self.flat = None  # set by the model after flattening
+
+    def _wqkv(self, grad=False):
+        f = self.flat
+        D = self.h * self.d_k
+        w = f.fused([self.linear_q.weight, self.linear_k.weight, self.linear_v.weight], (3 * D, D), grad)
+        b = f.fused([self.linear_q.bias, self.linear_k.bias, self.linear_v.bias], (3 * D,), grad)
+        return w, b
+
+    def fwd(self, x2d, resid, pos_emb, klen, B, T, p_res, seeds: Seeds, training: bool):
+        H, dk = self.h, self.d_k
+        D = H * dk
+        M = B * T
+        Z = H * B
+        P = pos_emb.shape[0]
+        relpos = 2 if self.legacy else 1
+        w, b = self._wqkv()
+        qkv = empty(M, 3 * D, like=x2d)
+        K.linear_fwd(x2d, w, b, qkv)
+        p = empty(P, D, like=x2d)
+        K.linear_fwd(pos_emb, self.linear_pos.weight, None, p)
+        q_u = empty(Z * T * dk, like=x2d)
+        q_v = empty(Z * T * dk, like=x2d)
+        K.heads_split(qkv, 3 * D, 0, B, T, H, dk, self.pos_bias_u, q_u)
+        K.heads_split(qkv, 3 * D, 0, B, T, H, dk, self.pos_bias_v, q_v)
+        ac = empty(Z * T * T, like=x2d)
+        # ac[z] = q_u[z] k[b,h]^T
+        K.gemm(T, T, dk, q_u, qkv, ac, mode_a=K.KC, lda=dk, mode_b=K.KC, ldb=3 * D, ldc=T, b_off=D,
+               batch=Z, nb2=B, sa=(B * T * dk, T * dk), sb=(dk, T * 3 * D), sc=(B * T * T, T * T))
+        bd = empty(Z * T * P, like=x2d)
+        K.gemm(T, P, dk, q_v, p, bd, mode_a=K.KC, lda=dk, mode_b=K.KC, ldb=D, ldc=P,
+               batch=Z, nb2=B, sa=(B * T * dk, T * dk), sb=(dk, 0), sc=(B * T * P, T * P))
+        pa = self.p if training else 0.0
+        sa = seeds.next()
+        pdrop = empty(Z * T * T, like=x2d) if pa > 0 else None
+        K.attn_softmax_fwd(ac, bd, relpos, P, math.sqrt(dk), klen, B, False, ac, pdrop, pa, sa, Z, T, T)
+        del bd
+        attn = ac
+        pv = pdrop if pdrop is not None else attn
+        ctx_ = empty(M, D, like=x2d)
+        K.gemm(T, dk, T, pv, qkv, ctx_, mode_a=K.KC, lda=T, mode_b=K.RC, ldb=3 * D, ldc=D, b_off=2 * D,
+               batch=Z, nb2=B, sa=(B * T * T, T * T), sb=(dk, T * 3 * D), sc=(dk, T * D))
+        out = empty(M, D, like=x2d)
+        pr = p_res if training else 0.0
+        so = seeds.next()
+        self.linear_out.fwd(ctx_, out, drop_p=pr, seed=so, R=resid, beta=1.0)
+        return out, Ctx(x=x2d, qkv=qkv, p=p, pos=pos_emb, q_u=q_u, q_v=q_v, attn=attn, pv=pv, ctx=ctx_,
+                        pa=pa, sa=sa, pr=pr, so=so, B=B, T=T, P=P)
+
+    def bwd(self, c, dout):
+        H, dk = self.h, self.d_k
+        D = H * dk
+        B, T, P = c.B, c.T, c.P
+        M, Z = B * T, H * B
+        relpos = 2 if self.legacy else 1
+        dz = torch.empty_like(dout)
+        K.scale_dropout(dout, dz, drop_p=c.pr, seed=c.so)
+        dctx = self.linear_out.bwd(dz, c.ctx)
+        dqkv = empty(M, 3 * D, like=dout)
+        # dP = dctx v^T  (into a (Z,T,T) buffer)
+        dS = empty(Z * T * T, like=dout)
+        K.gemm(T, T, dk, dctx, c.qkv, dS, mode_a=K.KC, lda=D, mode_b=K.KC, ldb=3 * D, ldc=T, b_off=2 * D,
+               batch=Z, nb2=B, sa=(dk, T * D), sb=(dk, T * 3 * D), sc=(B * T * T, T * T))
+        # dV = pv^T dctx -> dqkv[:, 2D:3D]
+        K.gemm(T, dk, T, c.pv, dctx, dqkv, mode_a=K.RC, lda=T, mode_b=K.RC, ldb=D, ldc=3 * D, c_off=2 * D,
+               batch=Z, nb2=B, sa=(B * T * T, T * T), sb=(dk, T * D), sc=(dk, T * 3 * D))
+        K.attn_softmax_bwd(c.attn, dS, dS, c.pa, c.sa, math.sqrt(dk), Z * T, T)
+        dbd = empty(Z * T * P, like=dout)
+        K.relshift_bwd(dS, dbd, relpos, Z, T, P)
+        # dq_u = dS k -> dqkv[:, 0:D]
+        K.gemm(T, dk, T, dS, c.qkv, dqkv, mode_a=K.KC, lda=T, mode_b=K.RC, ldb=3 * D, ldc=3 * D, b_off=D,
+               batch=Z, nb2=B, sa=(B * T * T, T * T), sb=(dk, T * 3 * D), sc=(dk, T * 3 * D))
+        # dk = dS^T q_u -> dqkv[:, D:2D]
+        K.gemm(T, dk, T, dS, c.q_u, dqkv, mode_a=K.RC, lda=T, mode_b=K.RC, ldb=dk, ldc=3 * D, c_off=D,
+               batch=Z, nb2=B, sa=(B * T * T, T * T), sb=(B * T * dk, T * dk), sc=(dk, T * 3 * D))
+        K.colsum(dqkv, self.pos_bias_u.grad.view(-1), accumulate=True, M=M, N=D, ld=3 * D)
+        # dq_v = dbd p -> tmp
+        tmp = empty(M, D, like=dout)
+        K.gemm(T, dk, P, dbd, c.p, tmp, mode_a=K.KC, lda=P, mode_b=K.RC, ldb=D, ldc=D,
+               batch=Z, nb2=B, sa=(B * T * P, T * P), sb=(dk, 0), sc=(dk, T * D))
+        K.colsum(tmp, self.pos_bias_v.grad.view(-1), accumulate=True)
+        K.add2d(tmp, D, dqkv, 3 * D, M, D)
+        # dp[:, h] = sum_b dbd[h,b]^T q_v[h,b]   (K = B*T)
+        dp = empty(P, D, like=dout)
+        K.gemm(P, dk, B * T, dbd, c.q_v, dp, mode_a=K.RC, lda=P, mode_b=K.RC, ldb=dk, ldc=D,
+               batch=H, nb2=1, sa=(B * T * P, 0), sb=(B * T * dk, 0), sc=(dk, 0))
+        # linear_pos weight grad only (pos_emb is a constant table)
+        K.gemm(D, D, P, dp, c.pos, self.linear_pos.weight.grad, mode_a=K.RC, lda=D, mode_b=K.RC, ldb=D, ldc=D,
+               R=self.linear_pos.weight.grad, beta=1.0)
+        w, _ = self._wqkv()
+        gw, gb = self._wqkv(grad=True)
+        K.linear_bwd_weight(dqkv, c.x, gw, gb)
+        dx = empty(M, D, like=dout)
+        K.linear_bwd_data(dqkv, w, dx)
+        return dx
+
+
+class MultiHeadedAttention(nn.Module):
+    """attention.py:16-114 (self- or source-attention), head-major z = h*B + b."""
+
+    def __init__(self, n_head: int, n_feat: int, dropout_rate: float):
+        super().__init__()
+        self.h, self.d_k = n_head, n_feat // n_head
+        self.linear_q = Linear(n_feat, n_feat)
+        self.linear_k = Linear(n_feat, n_feat)
+        self.linear_v = Linear(n_feat, n_feat)
+        self.linear_out = Linear(n_feat, n_feat)
+        self.p = dropout_rate
+        self.flat = None
+
+    def _w(self, names, grad=False):
+        f = self.flat
+        D = self.h * self.d_k
+        mods = [getattr(self, n) for n in names]
+        w = f.fused([m.weight for m in mods], (len(mods) * D, D), grad)
+        b = f.fused([m.bias for m in mods], (len(mods) * D,), grad)
+        return w, b
+
+    def fwd(self, xq, resid, B, Tq, klen, causal, p_res, seeds: Seeds, training: bool, mem=None, Tk=None):
+        """self-attention when mem is None (q,k,v from xq), else source attention over mem."""
+        H, dk = self.h, self.d_k
+        D = H * dk
+        Z = H * B
+        if mem is None:
+            Tk = Tq
+            w, b = self._w(("linear_q", "linear_k", "linear_v"))
+            qkv = empty(B * Tq, 3 * D, like=xq)
+            K.linear_fwd(xq, w, b, qkv)
+            qb, qld, qoff = qkv, 3 * D, 0
+            kvb, kvld, koff, voff = qkv, 3 * D, D, 2 * D
+            kv = None
+        else:
+            qkv = empty(B * Tq, D, like=xq)
+            self.linear_q.fwd(xq, qkv)
+            w, b = self._w(("linear_k", "linear_v"))
+            kv = empty(B * Tk, 2 * D, like=xq)
+            K.linear_fwd(mem, w, b, kv)
+            qb, qld, qoff = qkv, D, 0
+            kvb, kvld, koff, voff = kv, 2 * D, 0, D
+        sc = empty(Z * Tq * Tk, like=xq)
+        K.gemm(Tq, Tk, dk, qb, kvb, sc, mode_a=K.KC, lda=qld, mode_b=K.KC, ldb=kvld, ldc=Tk, a_off=qoff, b_off=koff,
+               batch=Z, nb2=B, sa=(dk, Tq * qld), sb=(dk, Tk * kvld), sc=(B * Tq * Tk, Tq * Tk))
+        pa = self.p if training else 0.0
+        sa = seeds.next()
+        pdrop = empty(Z * Tq * Tk, like=xq) if pa > 0 else None
+        K.attn_softmax_fwd(sc, None, 0, 0, math.sqrt(dk), klen, B, causal, sc, pdrop, pa, sa, Z, Tq, Tk)
+        pv = pdrop if pdrop is not None else sc
+        ctx_ = empty(B * Tq, D, like=xq)
+        K.gemm(Tq, dk, Tk, pv, kvb, ctx_, mode_a=K.KC, lda=Tk, mode_b=K.RC, ldb=kvld, ldc=D, b_off=voff,
+               batch=Z, nb2=B, sa=(B * Tq * Tk, Tq * Tk), sb=(dk, Tk * kvld), sc=(dk, Tq * D))
+        out = empty(B * Tq, D, like=xq)
+        pr = p_res if training else 0.0
+        so = seeds.next()
+        self.linear_out.fwd(ctx_, out, drop_p=pr, seed=so, R=resid, beta=1.0)
+        return out, Ctx(xq=xq, mem=mem, qkv=qkv, kv=kv, attn=sc, pv=pv, ctx=ctx_, pa=pa, sa=sa, pr=pr, so=so,
+                        B=B, Tq=Tq, Tk=Tk)
+
+    def bwd(self, c, dout, dmem=None):
+        """returns dxq (new); accumulates the memory gradient into dmem for source attention."""
+        H, dk = self.h, self.d_k
+        D = H * dk
+        B, Tq, Tk = c.B, c.Tq, c.Tk
+        Z = H * B
+        dz = torch.empty_like(dout)
+        K.scale_dropout(dout, dz, drop_p=c.pr, seed=c.so)
+        dctx = self.linear_out.bwd(dz, c.ctx)
+        if c.mem is None:
+            dq_buf = empty(B * Tq, 3 * D, like=dout)
+            dqld, dqoff = 3 * D, 0
+            dkv, dkvld, dkoff, dvoff = dq_buf, 3 * D, D, 2 * D
+            kvb, kvld, koff, voff = c.qkv, 3 * D, D, 2 * D
+            qb, qld, qoff = c.qkv, 3 * D, 0
+        else:
+            dq_buf = empty(B * Tq, D, like=dout)
+            dqld, dqoff = D, 0
+            dkv = empty(B * Tk, 2 * D, like=dout)
+            dkvld, dkoff, dvoff = 2 * D, 0, D
+            kvb, kvld, koff, voff = c.kv, 2 * D, 0, D
+            qb, qld, qoff = c.qkv, D, 0
+        dS = empty(Z * Tq * Tk, like=dout)
+        K.gemm(Tq, Tk, dk, dctx, kvb, dS, mode_a=K.KC, lda=D, mode_b=K.KC, ldb=kvld, ldc=Tk, b_off=voff,
+               batch=Z, nb2=B, sa=(dk, Tq * D), sb=(dk, Tk * kvld), sc=(B * Tq * Tk, Tq * Tk))
+        K.gemm(Tk, dk, Tq, c.pv, dctx, dkv, mode_a=K.RC, lda=Tk, mode_b=K.RC, ldb=D, ldc=dkvld, c_off=dvoff,
+               batch=Z, nb2=B, sa=(B * Tq * Tk, Tq * Tk), sb=(dk, Tq * D), sc=(dk, Tk * dkvld))
+        K.attn_softmax_bwd(c.attn, dS, dS, c.pa, c.sa, math.sqrt(dk), Z * Tq, Tk)
+        K.gemm(Tq, dk, Tk, dS, kvb, dq_buf, mode_a=K.KC, lda=Tk, mode_b=K.RC, ldb=kvld, ldc=dqld, b_off=koff,
+               c_off=dqoff, batch=Z, nb2=B, sa=(B * Tq * Tk, Tq * Tk), sb=(dk, Tk * kvld), sc=(dk, Tq * dqld))
+        K.gemm(Tk, dk, Tq, dS, qb, dkv, mode_a=K.RC, lda=Tk, mode_b=K.RC, ldb=qld, ldc=dkvld, a_off=0, b_off=qoff,
+               c_off=dkoff, batch=Z, nb2=B, sa=(B * Tq * Tk, Tq * Tk), sb=(dk, Tq * qld), sc=(dk, Tk * dkvld))
+        if c.mem is None:
+            w, _ = self._w(("linear_q", "linear_k", "linear_v"))
+            gw, gb = self._w(("linear_q", "linear_k", "linear_v"), grad=True)
+            K.linear_bwd_weight(dq_buf, c.xq, gw, gb)
+            dx = empty(B * Tq, D, like=dout)
+            K.linear_bwd_data(dq_buf, w, dx)
+            return dx
+        dx = self.linear_q.bwd(dq_buf, c.xq)
+        w, _ = self._w(("linear_k", "linear_v"))
+        gw, gb = self._w(("linear_k", "linear_v"), grad=True)
+        K.linear_bwd_weight(dkv, c.mem, gw, gb)
+        K.linear_bwd_data(dkv, w, dmem, accumulate=True)
+        return dx
+
+
+class ConvolutionModule(nn.Module):
+    """conformer/convolution.py:13-79 (GLU, depthwise k, BatchNorm1d train stats, Swish)."""
+
+    def __init__(self, channels: int, kernel_size: int):
+        super().__init__()
+        assert (kernel_size - 1) % 2 == 0
+        self.pointwise_conv1 = nn.Conv1d(channels, 2 * channels, 1)
+        self.depthwise_conv = nn.Conv1d(channels, channels, kernel_size, padding=(kernel_size - 1) // 2,
+                                        groups=channels)
+        self.norm = nn.BatchNorm1d(channels)
+        self.pointwise_conv2 = nn.Conv1d(channels, channels, 1)
+        self.kernel_size = kernel_size
+
+    def fwd(self, x2d, resid, B, T, p_res, seeds: Seeds, training: bool):
+        M, D = x2d.shape
+        w1 = self.pointwise_conv1.weight.view(2 * D, D)
+        u = empty(M, 2 * D, like=x2d)
+        K.linear_fwd(x2d, w1, self.pointwise_conv1.bias, u)
+        g = empty(M, D, like=x2d)
+        K.glu_fwd(u, g)
+        y = empty(M, D, like=x2d)
+        K.dwconv1d(g, self.depthwise_conv.weight, self.depthwise_conv.bias, y, B, T, D, self.kernel_size)
+        s = empty(M, D, like=x2d)
+        mean = empty(D, like=x2d)
+        rstd = empty(D, like=x2d)
+        bn = self.norm
+        if training:
+            K.bn_swish_fwd(y, bn.weight, bn.bias, s, mean, rstd, bn.running_mean, bn.running_var,
+                           momentum=bn.momentum, eps=bn.eps)
+            bn.num_batches_tracked.add_(1)
+        else:
+            raise NotImplementedError("eval-mode BatchNorm (running statistics) is not on the training hot path")
+        out = empty(M, D, like=x2d)
+        pr = p_res if training else 0.0
+        so = seeds.next()
+        K.linear_fwd(s, self.pointwise_conv2.weight.view(D, D), self.pointwise_conv2.bias, out, drop_p=pr, seed=so,
+                     R=resid, beta=1.0)
+        return out, Ctx(x=x2d, u=u, g=g, y=y, s=s, mean=mean, rstd=rstd, pr=pr, so=so, B=B, T=T)
+
+    def bwd(self, c, dout):
+        M, D = dout.shape
+        dz = torch.empty_like(dout)
+        K.scale_dropout(dout, dz, drop_p=c.pr, seed=c.so)
+        w2 = self.pointwise_conv2.weight
+        K.linear_bwd_weight(dz, c.s, w2.grad.view(D, D), self.pointwise_conv2.bias.grad)
+        ds = empty(M, D, like=dout)
+        K.linear_bwd_data(dz, w2.view(D, D), ds)
+        dy = empty(M, D, like=dout)
+        sums = empty(2 * D, like=dout)
+        bn = self.norm
+        K.bn_swish_bwd(ds, c.y, c.mean, c.rstd, bn.weight, bn.bias, dy, bn.weight.grad, bn.bias.grad, sums)
+        dw = self.depthwise_conv
+        K.colsum(dy, dw.bias.grad, accumulate=True)
+        K.dwconv1d_wgrad(dy, c.g, dw.weight.grad, c.B, c.T, D, self.kernel_size)
+        dg = ds  # reuse
+        K.dwconv1d(dy, dw.weight, None, dg, c.B, c.T, D, self.kernel_size, flip=True)
+        du = empty(M, 2 * D, like=dout)
+        K.glu_bwd(c.u, dg, du)
+        w1 = self.pointwise_conv1.weight
+        K.linear_bwd_weight(du, c.x, w1.grad.view(2 * D, D), self.pointwise_conv1.bias.grad)
+        dx = empty(M, D, like=dout)
+        K.linear_bwd_data(du, w1.view(2 * D, D), dx)
+        return dx
+
+
+class Conv2dSubsampling(nn.Module):
+    """subsampling.py:42-87 in NHWC; returns x*sqrt(D) (+ dropout), before the rel-pos table."""
+
+    def __init__(self, idim: int, odim: int):
+        super().__init__()
+        self.conv = nn.Sequential(nn.Conv2d(1, odim, 3, 2), nn.ReLU(), nn.Conv2d(odim, odim, 3, 2), nn.ReLU())
+        self.f2 = ((idim - 1) // 2 - 1) // 2
+        self.out = nn.Sequential(Linear(odim * self.f2, odim))
+        self.odim = odim
+
+    def fwd(self, feats, xscale, p_drop, seeds: Seeds, training: bool):
+        B, T, F = feats.shape
+        D = self.odim
+        T1, F1 = (T - 3) // 2 + 1, (F - 3) // 2 + 1
+        T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
+        c0, c2 = self.conv[0], self.conv[2]
+        z1 = empty(B * T1 * F1 * D, like=feats)
+        K.conv1_fwd(feats, c0.weight, c0.bias, z1, B, T, F, D)
+        w2r = empty(D * 9 * D, like=feats)
+        K.permute3(c2.weight, w2r, D, D, 9)
+        z2 = empty(B * T2 * F2, D, like=feats)
+        ic = (T1, F1, D, T2, F2)
+        K.gemm(B * T2 * F2, D, 9 * D, z1, w2r, z2, mode_a=K.I2C_KC, lda=0, mode_b=K.KC, ldb=9 * D, ldc=D,
+               bias=c2.bias, act=K.ACT_RELU, ic_a=ic)
+        lin = self.out[0]
+        wor = empty(D * F2 * D, like=feats)
+        K.permute3(lin.weight, wor, D, D, F2)  # (n, c, f) -> (n, f, c)
+        x = empty(B * T2, D, like=feats)
+        pd = p_drop if training else 0.0
+        sd = seeds.next()
+        K.linear_fwd(z2.view(B * T2, F2 * D), wor.view(D, F2 * D), lin.bias, x, alpha=xscale, drop_p=pd, seed=sd)
+        return x, Ctx(feats=feats, z1=z1, w2r=w2r, z2=z2, wor=wor, pd=pd, sd=sd, xscale=xscale,
+                      B=B, T=T, F=F, T1=T1, F1=F1, T2=T2, F2=F2)
+
+    def bwd(self, c, dx):
+        D = self.odim
+        B, T2, F2, T1, F1 = c.B, c.T2, c.F2, c.T1, c.F1
+        c0, c2 = self.conv[0], self.conv[2]
+        lin = self.out[0]
+        dv = torch.empty_like(dx)
+        K.scale_dropout(dx, dv, alpha=c.xscale, drop_p=c.pd, seed=c.sd)
+        dwor = torch.zeros(D * F2 * D, dtype=torch.float32, device=dx.device)
+        z2f = c.z2.view(B * T2, F2 * D)
+        K.linear_bwd_weight(dv, z2f, dwor.view(D, F2 * D), lin.bias.grad)
+        K.permute3(dwor, lin.weight.grad, D, F2, D, accumulate=True)  # (n, f, c) -> (n, c, f)
+        dz2 = empty(B * T2, F2 * D, like=dx)
+        K.linear_bwd_data(dv, c.wor.view(D, F2 * D), dz2)
+        K.act_bwd(dz2, z2f, dz2, K.ACT_RELU)
+        npix2 = B * T2 * F2
+        dz2p = dz2.view(npix2, D)
+        ic = (T1, F1, D, T2, F2)
+        dw2r = empty(D, 9 * D, like=dx)
+        K.gemm(D, 9 * D, npix2, dz2p, c.z1, dw2r, mode_a=K.RC, lda=D, mode_b=K.I2C_RC, ldb=0, ldc=9 * D, ic_b=ic)
+        K.permute3(dw2r, c2.weight.grad, D, 9, D, accumulate=True)  # (o, kk, c) -> (o, c, kk)
+        K.colsum(dz2p, c2.bias.grad, accumulate=True)
+        dcol = empty(npix2, 9 * D, like=dx)
+        K.gemm(npix2, 9 * D, D, dz2p, c.w2r, dcol, mode_a=K.KC, lda=D, mode_b=K.RC, ldb=9 * D, ldc=9 * D)
+        dz1 = empty(B * T1 * F1 * D, like=dx)
+        K.col2im_relu(dcol, c.z1, dz1, B, T1, F1, D)
+        del dcol
+        K.conv1_wgrad(c.feats, dz1, c0.weight.grad.view(D, 9), c0.bias.grad, B, c.T, c.F, D)

@@ -1,0 +1,237 @@
+// Attention pieces around the MFMA GEMMs (attention.py:16-308):
+//   * heads_split: q + pos_bias_u / q + pos_bias_v into head-major (H,B,T,dk) layout
+//     (the layout the batch-summed linear_pos gradient GEMM needs, attention.py:290-293)
+//   * masked softmax with the rel-pos score assembly fused in:
+//       s[i,j] = (ac[i,j] + bd_shift[i,j]) / sqrt(dk), masked_fill(min) -> softmax ->
+//       masked_fill(0) -> (dropout copy)        (attention.py:64-96, 145-165, 240-263)
+//     latest : bd_shift[i,j] = bd[i, j+T-1-i]                  (bd: T x (2T-1))
+//     legacy : j<=i -> bd[i, j+T-1-i]; j==i+1 -> 0; j>i+1 -> bd[i+1, j-i-2]   (bd: T x T)
+//     mask   : key j valid iff j < klen[b] (and j <= i when causal, subsequent_mask)
+//   * softmax backward (+ attention-dropout backward) and the rel_shift adjoint (a
+//     gather, so no atomics: each bd element receives at most one score gradient).
+// One wave per score row; rows of <= 64*PER keys live in registers.
+#include "common.h"
+
+namespace {
+
+__global__ void heads_split_kernel(const float* __restrict__ src, long ld, int col0, int B, int T, int H, int dk,
+                                   const float* __restrict__ bias, float* __restrict__ dst) {
+  const long n = (long)H * B * T * dk;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int d = (int)(i % dk);
+    long r = i / dk;
+    const int t = (int)(r % T);
+    r /= T;
+    const int b = (int)(r % B);
+    const int h = (int)(r / B);
+    float v = src[((long)b * T + t) * ld + col0 + h * dk + d];
+    if (bias) v += bias[h * dk + d];
+    dst[i] = v;
+  }
+}
+
+// y[r*ldy + c] += x[r*ldx + c]
+__global__ void add2d_kernel(const float* __restrict__ x, long ldx, float* __restrict__ y, long ldy, int M, int N) {
+  const long n = (long)M * N;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / N;
+    const int c = (int)(i - r * N);
+    y[r * ldy + c] += x[r * ldx + c];
+  }
+}
+
+template <int PER>
+__global__ __launch_bounds__(256) void softmax_fwd_kernel(const float* ac, const float* __restrict__ bd, int relpos,
+                                                          int P, float sqrt_dk, const int* __restrict__ klen, int nb,
+                                                          int causal, float* attn, float* __restrict__ pdrop,
+                                                          uint32_t thr, float dscale, uint64_t seed, int Z, int Tq,
+                                                          int Tk) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (long)Z * Tq) return;
+  const int i = (int)(row % Tq);
+  const int z = (int)(row / Tq);
+  const int b = z % nb;  // z = h*nb + b
+  int kl = klen ? klen[b] : Tk;
+  if (kl > Tk) kl = Tk;
+  const float* acr = ac + row * Tk;
+  const float* bdz = bd ? bd + (long)z * Tq * P : nullptr;
+  float v[PER];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int j = lane + 64 * e;
+    float s = -INFINITY;
+    if (j < Tk && j < kl && !(causal && j > i)) {
+      float a = acr[j];
+      if (relpos == 1) {
+        a += bdz[(long)i * P + (j + Tq - 1 - i)];
+      } else if (relpos == 2) {
+        if (j <= i) a += bdz[(long)i * P + (j + Tq - 1 - i)];
+        else if (j > i + 1) a += bdz[(long)(i + 1) * P + (j - i - 2)];
+        else a += 0.f;
+      }
+      s = a / sqrt_dk;
+    }
+    v[e] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = esp::wave_max(mx);
+  float sum = 0.f;
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const float p = v[e] == -INFINITY ? 0.f : expf(v[e] - mx);
+    v[e] = p;
+    sum += p;
+  }
+  sum = esp::wave_sum(sum);
+  const float inv = sum > 0.f ? 1.0f / sum : 0.f;
+  float* ar = attn + row * Tk;
+  float* pr = pdrop ? pdrop + row * Tk : nullptr;
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int j = lane + 64 * e;
+    if (j < Tk) {
+      const float p = v[e] * inv;
+      ar[j] = p;
+      if (pr) pr[j] = esp::keep_elem(seed, (uint64_t)(row * Tk + j), thr) ? p * dscale : 0.f;
+    }
+  }
+}
+
+// dS = attn * (g - sum_j attn*g) / sqrt_dk,  g = dP * dropmask * dscale.  dS may alias dP.
+template <int PER>
+__global__ __launch_bounds__(256) void softmax_bwd_kernel(const float* __restrict__ attn, const float* dP, float* dS,
+                                                          uint32_t thr, float dscale, uint64_t seed, float sqrt_dk,
+                                                          long rows, int Tk) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* ar = attn + row * Tk;
+  const float* gr = dP + row * Tk;
+  float a[PER], g[PER];
+  float dot = 0.f;
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int j = lane + 64 * e;
+    a[e] = 0.f;
+    g[e] = 0.f;
+    if (j < Tk) {
+      a[e] = ar[j];
+      float gv = gr[j];
+      if (thr) gv = esp::keep_elem(seed, (uint64_t)(row * Tk + j), thr) ? gv * dscale : 0.f;
+      g[e] = gv;
+    }
+    dot += a[e] * g[e];
+  }
+  dot = esp::wave_sum(dot);
+  float* sr = dS + row * Tk;
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int j = lane + 64 * e;
+    if (j < Tk) sr[j] = a[e] * (g[e] - dot) / sqrt_dk;
+  }
+}
+
+// adjoint of the rel_shift gather: dbd (Z,T,P) from dS (Z,T,T)
+__global__ void relshift_bwd_kernel(const float* __restrict__ dS, float* __restrict__ dbd, int relpos, int Z, int T,
+                                    int P) {
+  const long n = (long)Z * T * P;
+  for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < n; idx += (long)gridDim.x * blockDim.x) {
+    const int k = (int)(idx % P);
+    const long r = idx / P;
+    const int i = (int)(r % T);
+    const long z = r / T;
+    const float* dz = dS + z * T * T;
+    float v = 0.f;
+    if (relpos == 1) {
+      const int j = k - (T - 1 - i);
+      if (j >= 0 && j < T) v = dz[(long)i * T + j];
+    } else {
+      if (k >= T - 1 - i) v = dz[(long)i * T + (k - T + 1 + i)];
+      else if (i >= 1 && k + i + 1 < T) v = dz[(long)(i - 1) * T + (k + i + 1)];
+    }
+    dbd[idx] = v;
+  }
+}
+
+inline int gridn(long n) {
+  long b = (n + 255) / 256;
+  return (int)(b > 65536 ? 65536 : (b < 1 ? 1 : b));
+}
+inline uint32_t drop_threshold(float p) {
+  if (p <= 0.f) return 0;
+  double t = (double)p * 4294967296.0;
+  uint32_t r = (uint32_t)(t >= 4294967295.0 ? 4294967295.0 : t);
+  return r ? r : 1;
+}
+
+}  // namespace
+
+ESP_API int esp_heads_split(const float* src, long ld, int col0, int B, int T, int H, int dk, const float* bias,
+                            float* dst, void* stream) {
+  hipLaunchKernelGGL(heads_split_kernel, dim3(gridn((long)H * B * T * dk)), dim3(256), 0, (hipStream_t)stream, src, ld,
+                     col0, B, T, H, dk, bias, dst);
+  ESP_CHECK_LAUNCH("esp_heads_split");
+  return 0;
+}
+
+ESP_API int esp_add2d(const float* x, long ldx, float* y, long ldy, int M, int N, void* stream) {
+  hipLaunchKernelGGL(add2d_kernel, dim3(gridn((long)M * N)), dim3(256), 0, (hipStream_t)stream, x, ldx, y, ldy, M, N);
+  ESP_CHECK_LAUNCH("esp_add2d");
+  return 0;
+}
+
+// relpos: 0 none, 1 latest (P=2T-1), 2 legacy (P=T). ac may alias attn (in-place).
+ESP_API int esp_attn_softmax_fwd(const float* ac, const float* bd, int relpos, int P, float sqrt_dk, const int* klen,
+                                 int nb, int causal, float* attn, float* pdrop, float drop_p, unsigned long long seed,
+                                 int Z, int Tq, int Tk, void* stream) {
+  ESP_ARG_CHECK(Tk <= 1024, "esp_attn_softmax_fwd: Tk=%d > 1024", Tk);
+  ESP_ARG_CHECK(relpos == 0 || (Tq == Tk && bd), "esp_attn_softmax_fwd: rel-pos needs Tq==Tk and bd");
+  ESP_ARG_CHECK(relpos != 1 || P == 2 * Tq - 1, "esp_attn_softmax_fwd: latest rel-pos needs P=2T-1");
+  ESP_ARG_CHECK(relpos != 2 || P == Tq, "esp_attn_softmax_fwd: legacy rel-pos needs P=T");
+  const uint32_t thr = drop_threshold(drop_p);
+  if (!thr) pdrop = nullptr;
+  const float ds = thr ? 1.f / (1.f - drop_p) : 1.f;
+  const long rows = (long)Z * Tq;
+  dim3 grid((unsigned)((rows + 3) / 4));
+  hipStream_t st = (hipStream_t)stream;
+#define ESP_SM(PER)                                                                                                 \
+  hipLaunchKernelGGL(softmax_fwd_kernel<PER>, grid, dim3(256), 0, st, ac, bd, relpos, P, sqrt_dk, klen, nb, causal, \
+                     attn, pdrop, thr, ds, (uint64_t)seed, Z, Tq, Tk)
+  if (Tk <= 64) ESP_SM(1);
+  else if (Tk <= 128) ESP_SM(2);
+  else if (Tk <= 256) ESP_SM(4);
+  else if (Tk <= 512) ESP_SM(8);
+  else ESP_SM(16);
+#undef ESP_SM
+  ESP_CHECK_LAUNCH("esp_attn_softmax_fwd");
+  return 0;
+}
+
+ESP_API int esp_attn_softmax_bwd(const float* attn, const float* dP, float* dS, float drop_p, unsigned long long seed,
+                                 float sqrt_dk, long rows, int Tk, void* stream) {
+  ESP_ARG_CHECK(Tk <= 1024, "esp_attn_softmax_bwd: Tk too large");
+  const uint32_t thr = drop_threshold(drop_p);
+  const float ds = thr ? 1.f / (1.f - drop_p) : 1.f;
+  dim3 grid((unsigned)((rows + 3) / 4));
+  hipStream_t st = (hipStream_t)stream;
+#define ESP_SB(PER) \
+  hipLaunchKernelGGL(softmax_bwd_kernel<PER>, grid, dim3(256), 0, st, attn, dP, dS, thr, ds, (uint64_t)seed, sqrt_dk, rows, Tk)
+  if (Tk <= 64) ESP_SB(1);
+  else if (Tk <= 128) ESP_SB(2);
+  else if (Tk <= 256) ESP_SB(4);
+  else if (Tk <= 512) ESP_SB(8);
+  else ESP_SB(16);
+#undef ESP_SB
+  ESP_CHECK_LAUNCH("esp_attn_softmax_bwd");
+  return 0;
+}
+
+ESP_API int esp_relshift_bwd(const float* dS, float* dbd, int relpos, int Z, int T, int P, void* stream) {
+  ESP_ARG_CHECK(relpos == 1 || relpos == 2, "esp_relshift_bwd: relpos must be 1 or 2");
+  hipLaunchKernelGGL(relshift_bwd_kernel, dim3(gridn((long)Z * T * P)), dim3(256), 0, (hipStream_t)stream, dS, dbd,
+                     relpos, Z, T, P);
+  ESP_CHECK_LAUNCH("esp_relshift_bwd");
+  return 0;
+}

@@ -1,0 +1,93 @@
+// Shared helpers for the gfx950 (MI355X / CDNA4) kernels of espnet_slurp_amd.
+// Wave = 64 lanes; all reductions are written for 64-wide wavefronts.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "espnet_mi355.h"  // the C ABI; definitions below must match it
+
+#define ESP_API extern "C" __attribute__((visibility("default")))
+
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+namespace esp {
+
+// last error string (host side), set by ESP_CHECK_LAUNCH / argument validation
+void set_error(const char* fmt, ...);
+
+// ---------------------------------------------------------------- counter RNG
+// splitmix64-style mixer: (seed, index) -> 32 random bits.  Stateless, so the
+// backward pass regenerates the forward dropout mask from the same (seed, index).
+__device__ __forceinline__ uint32_t rng_u32(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+// keep with probability (1-p): threshold = p * 2^32
+__device__ __forceinline__ bool keep_elem(uint64_t seed, uint64_t idx, uint32_t thresh) {
+  return rng_u32(seed, idx) >= thresh;
+}
+
+// ---------------------------------------------------------------- reductions (wave64)
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// block reduction, blockDim.x multiple of 64, up to 1024 threads; result broadcast
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* sh /* >= 16 */) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  if constexpr (sizeof(T) == 8) v = wave_sum_d(v); else v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  T r = 0;
+  for (int i = 0; i < nw; ++i) r += sh[i];
+  return r;
+}
+__device__ __forceinline__ float block_max(float v, float* sh) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  float r = -INFINITY;
+  for (int i = 0; i < nw; ++i) r = fmaxf(r, sh[i]);
+  return r;
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+}  // namespace esp
+
+#define ESP_CHECK_LAUNCH(name)                                              \
+  do {                                                                      \
+    hipError_t e__ = hipGetLastError();                                     \
+    if (e__ != hipSuccess) {                                                \
+      esp::set_error("%s: %s", name, hipGetErrorString(e__));               \
+      return (int)e__;                                                      \
+    }                                                                       \
+  } while (0)
+
+#define ESP_ARG_CHECK(cond, ...)          \
+  do {                                    \
+    if (!(cond)) {                        \
+      esp::set_error(__VA_ARGS__);        \
+      return -1;                          \
+    }                                     \
+  } while (0)

@@ -1,0 +1,197 @@
+// Conv2dSubsampling pieces (subsampling.py:42-87) in NHWC layout:
+//   conv1  Conv2d(1, D, 3, stride 2) + ReLU : direct kernel (K = 9, not GEMM-shaped)
+//   conv2  Conv2d(D, D, 3, stride 2) + ReLU : implicit-im2col MFMA GEMM (gemm.hip)
+//   adjoints: col2im gather (+ conv1 ReLU mask), conv1 weight gradient, and the weight
+//   re-layouts between the reference (o, c, kt, kf) / (n, c*F2+f) order and the NHWC
+//   order the GEMMs consume (forward copy; gradient scattered back, accumulated).
+#include "common.h"
+
+namespace {
+
+inline int gridn(long n) {
+  long b = (n + 255) / 256;
+  return (int)(b > 65536 ? 65536 : (b < 1 ? 1 : b));
+}
+
+// x (B,T,F) -> z (B,T1,F1,D), 4 channels per thread
+__global__ void conv1_fwd_kernel(const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
+                                 float* __restrict__ z, int B, int T, int F, int T1, int F1, int D) {
+  const int D4 = D / 4;
+  const long n = (long)B * T1 * F1 * D4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int o4 = (int)(i % D4);
+    long p = i / D4;
+    const int f1 = (int)(p % F1);
+    p /= F1;
+    const int t1 = (int)(p % T1);
+    const int b = (int)(p / T1);
+    const float* xp = x + ((long)b * T + 2 * t1) * F + 2 * f1;
+    float patch[9];
+#pragma unroll
+    for (int kt = 0; kt < 3; ++kt)
+#pragma unroll
+      for (int kf = 0; kf < 3; ++kf) patch[kt * 3 + kf] = xp[(long)kt * F + kf];
+    float out[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int o = o4 * 4 + q;
+      float a = bias[o];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) a += W[o * 9 + k] * patch[k];
+      out[q] = fmaxf(a, 0.f);
+    }
+    *reinterpret_cast<float4*>(z + (((long)b * T1 + t1) * F1 + f1) * D + o4 * 4) =
+        make_float4(out[0], out[1], out[2], out[3]);
+  }
+}
+
+// dz1pre[b,t1,f1,c] = (z1>0) * sum over valid taps of dcol[(b,t2,f2)][(kt*3+kf)*D + c]
+__global__ void col2im_relu_kernel(const float* __restrict__ dcol, const float* __restrict__ z1, float* __restrict__ dz1,
+                                   int B, int T1, int F1, int T2, int F2, int D) {
+  const int D4 = D / 4;
+  const long n = (long)B * T1 * F1 * D4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c4 = (int)(i % D4);
+    long p = i / D4;
+    const int f1 = (int)(p % F1);
+    p /= F1;
+    const int t1 = (int)(p % T1);
+    const int b = (int)(p / T1);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int kt = 0; kt < 3; ++kt) {
+      const int tt = t1 - kt;
+      if (tt < 0 || (tt & 1)) continue;
+      const int t2 = tt >> 1;
+      if (t2 >= T2) continue;
+#pragma unroll
+      for (int kf = 0; kf < 3; ++kf) {
+        const int ff = f1 - kf;
+        if (ff < 0 || (ff & 1)) continue;
+        const int f2 = ff >> 1;
+        if (f2 >= F2) continue;
+        const float4 v = *reinterpret_cast<const float4*>(
+            dcol + (((long)b * T2 + t2) * F2 + f2) * (9L * D) + (kt * 3 + kf) * D + c4 * 4);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+    }
+    const long o = (((long)b * T1 + t1) * F1 + f1) * D + c4 * 4;
+    const float4 zz = *reinterpret_cast<const float4*>(z1 + o);
+    acc.x = zz.x > 0.f ? acc.x : 0.f;
+    acc.y = zz.y > 0.f ? acc.y : 0.f;
+    acc.z = zz.z > 0.f ? acc.z : 0.f;
+    acc.w = zz.w > 0.f ? acc.w : 0.f;
+    *reinterpret_cast<float4*>(dz1 + o) = acc;
+  }
+}
+
+// conv1 weight/bias gradient partials: block = chunk of pixels, thread = channel.
+constexpr int C1_CHUNK = 2048, C1_SUB = 256;
+__global__ void conv1_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dz, float* __restrict__ part,
+                                   int B, int T, int F, int T1, int F1, int D) {
+  __shared__ float patch[C1_SUB][9];
+  const long npix = (long)B * T1 * F1;
+  const long p0 = (long)blockIdx.x * C1_CHUNK;
+  float acc[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) acc[k] = 0.f;
+  for (long s0 = p0; s0 < p0 + C1_CHUNK && s0 < npix; s0 += C1_SUB) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < C1_SUB * 9; e += blockDim.x) {
+      const int q = e / 9, k = e - q * 9;
+      const long p = s0 + q;
+      float v = 0.f;
+      if (p < npix) {
+        const int f1 = (int)(p % F1);
+        const long r = p / F1;
+        const int t1 = (int)(r % T1);
+        const int b = (int)(r / T1);
+        v = x[((long)b * T + 2 * t1 + k / 3) * F + 2 * f1 + k % 3];
+      }
+      patch[q][k] = v;
+    }
+    __syncthreads();
+    const int lim = (int)min((long)C1_SUB, npix - s0);
+    for (int o = threadIdx.x; o < D; o += blockDim.x) {
+      // one channel per thread (blockDim == D in practice)
+      for (int q = 0; q < lim; ++q) {
+        const float g = dz[(s0 + q) * D + o];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) acc[k] += g * patch[q][k];
+        acc[9] += g;
+      }
+    }
+  }
+  for (int o = threadIdx.x; o < D; o += blockDim.x) {
+    float* pr = part + ((long)blockIdx.x * D + o) * 10;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) pr[k] = acc[k];
+  }
+}
+
+__global__ void conv1_wgrad_finalize(const float* __restrict__ part, int nb, int D, float* __restrict__ dW,
+                                     float* __restrict__ db) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= D * 10) return;
+  float s = 0.f;
+  for (int p = 0; p < nb; ++p) s += part[(long)p * D * 10 + e];
+  const int o = e / 10, k = e - o * 10;
+  if (k < 9) dW[o * 9 + k] += s;
+  else db[o] += s;
+}
+
+// out[o][a][b] (+)= in[o][b][a], in = (O, Bd, Ad)
+__global__ void permute3_kernel(const float* __restrict__ in, float* __restrict__ out, int O, int Bd, int Ad,
+                                int accumulate) {
+  const long n = (long)O * Bd * Ad;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int bb = (int)(i % Bd);
+    long r = i / Bd;
+    const int a = (int)(r % Ad);
+    const int o = (int)(r / Ad);
+    const float v = in[((long)o * Bd + bb) * Ad + a];
+    out[i] = accumulate ? out[i] + v : v;
+  }
+}
+
+}  // namespace
+
+ESP_API int esp_conv1_fwd(const float* x, const float* W, const float* bias, float* z, int B, int T, int F, int D,
+                          void* stream) {
+  ESP_ARG_CHECK(D % 4 == 0, "esp_conv1_fwd: D %% 4 != 0");
+  const int T1 = (T - 3) / 2 + 1, F1 = (F - 3) / 2 + 1;
+  hipLaunchKernelGGL(conv1_fwd_kernel, dim3(gridn((long)B * T1 * F1 * (D / 4))), dim3(256), 0, (hipStream_t)stream, x,
+                     W, bias, z, B, T, F, T1, F1, D);
+  ESP_CHECK_LAUNCH("esp_conv1_fwd");
+  return 0;
+}
+
+ESP_API int esp_col2im_relu(const float* dcol, const float* z1, float* dz1, int B, int T1, int F1, int D, void* stream) {
+  ESP_ARG_CHECK(D % 4 == 0, "esp_col2im_relu: D %% 4 != 0");
+  const int T2 = (T1 - 3) / 2 + 1, F2 = (F1 - 3) / 2 + 1;
+  hipLaunchKernelGGL(col2im_relu_kernel, dim3(gridn((long)B * T1 * F1 * (D / 4))), dim3(256), 0, (hipStream_t)stream,
+                     dcol, z1, dz1, B, T1, F1, T2, F2, D);
+  ESP_CHECK_LAUNCH("esp_col2im_relu");
+  return 0;
+}
+
+// workspace: >= ceil(B*T1*F1/2048) * D * 10 floats.  dW (D,9) and db (D) accumulated.
+ESP_API int esp_conv1_wgrad(const float* x, const float* dz1, float* dW, float* db, int B, int T, int F, int D,
+                            float* work, void* stream) {
+  const int T1 = (T - 3) / 2 + 1, F1 = (F - 3) / 2 + 1;
+  const long npix = (long)B * T1 * F1;
+  const int nb = (int)((npix + C1_CHUNK - 1) / C1_CHUNK);
+  hipStream_t st = (hipStream_t)stream;
+  ESP_ARG_CHECK(D <= 1024, "esp_conv1_wgrad: D > 1024");
+  hipLaunchKernelGGL(conv1_wgrad_kernel, dim3(nb), dim3(D), 0, st, x, dz1, work, B, T, F, T1, F1, D);
+  hipLaunchKernelGGL(conv1_wgrad_finalize, dim3((D * 10 + 255) / 256), dim3(256), 0, st, work, nb, D, dW, db);
+  ESP_CHECK_LAUNCH("esp_conv1_wgrad");
+  return 0;
+}
+
+ESP_API int esp_permute3(const float* in, float* out, int O, int Bd, int Ad, int accumulate, void* stream) {
+  hipLaunchKernelGGL(permute3_kernel, dim3(gridn((long)O * Bd * Ad)), dim3(256), 0, (hipStream_t)stream, in, out, O, Bd,
+                     Ad, accumulate);
+  ESP_CHECK_LAUNCH("esp_permute3");
+  return 0;
+}

@@ -1,0 +1,329 @@
+// Memory-bound element-wise kernels: activation/dropout backward, residual scaling,
+// embedding, positional scaling, SpecAugment (time warp + masks), utterance MVN,
+// fused Adam over the flat parameter buffer, global grad-norm, and library errors.
+// All are HBM-bound: float4 loads/stores where the layout allows, grid-stride loops.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "common.h"
+
+namespace esp {
+static thread_local char g_err[512] = "";
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+}  // namespace esp
+
+ESP_API const char* esp_last_error(void) { return esp::g_err; }
+ESP_API int esp_abi_version(void) { return 1; }
+
+namespace {
+
+inline uint32_t drop_threshold(float p) {
+  if (p <= 0.f) return 0;
+  double t = (double)p * 4294967296.0;
+  uint32_t r = (uint32_t)(t >= 4294967295.0 ? 4294967295.0 : t);
+  return r ? r : 1;
+}
+
+inline int grid_for(long n, int per_thread = 1) {
+  long b = (n / per_thread + 255) / 256;
+  if (b > 65536) b = 65536;
+  return (int)(b < 1 ? 1 : b);
+}
+
+// dx = dy * keep*scale * act'(h)        (act: 0 none, 1 relu, 2 swish)
+__global__ void act_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ h,
+                               float* __restrict__ dx, long n, int act, uint32_t thr, float scale,
+                               uint64_t seed, long idx_off) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float g = dy[i];
+    if (thr) g = esp::keep_elem(seed, (uint64_t)(i + idx_off), thr) ? g * scale : 0.f;
+    const float x = h[i];
+    if (act == 1) g = x > 0.f ? g : 0.f;
+    else if (act == 2) {
+      const float s = 1.0f / (1.0f + expf(-x));
+      g = g * (s * (1.0f + x * (1.0f - s)));
+    }
+    dx[i] = g;
+  }
+}
+
+// y = alpha * keep*scale * x (+ beta * r)  — dropout forward/backward on residual branches
+__global__ void scale_drop_kernel(const float* __restrict__ x, float* __restrict__ y, long n, float alpha,
+                                  uint32_t thr, float scale, uint64_t seed, const float* r, float beta) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float v = x[i];
+    if (thr) v = esp::keep_elem(seed, (uint64_t)i, thr) ? v * scale : 0.f;
+    v *= alpha;
+    if (r) v += beta * r[i];
+    y[i] = v;
+  }
+}
+
+// encoder input of the blocks: x = drop(x * xscale); pos = drop(pos)  (embedding.py:228-244)
+// decoder: x = drop(E[tok] * xscale + pe[l])                            (embedding.py:81-94)
+__global__ void embed_fwd_kernel(const int64_t* __restrict__ tok, const float* __restrict__ E,
+                                 const float* __restrict__ pe, float* __restrict__ y, int L, int D,
+                                 float xscale, uint32_t thr, float scale, uint64_t seed, long n) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long row = i / D;
+    const int d = (int)(i - row * D);
+    const int l = (int)(row % L);
+    float v = E[tok[row] * (long)D + d] * xscale + pe[(long)l * D + d];
+    if (thr) v = esp::keep_elem(seed, (uint64_t)i, thr) ? v * scale : 0.f;
+    y[i] = v;
+  }
+}
+
+// dE[v, :] += sum over rows with tok==v of dy*mask*scale*xscale   (deterministic: one block
+// per vocab row scans the token list in order)
+__global__ void embed_bwd_kernel(const int64_t* __restrict__ tok, const float* __restrict__ dy,
+                                 float* __restrict__ dE, int nrows, int D, float xscale, uint32_t thr,
+                                 float scale, uint64_t seed) {
+  const int v = blockIdx.x;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float acc = 0.f;
+    bool any = false;
+    for (int r = 0; r < nrows; ++r) {
+      if (tok[r] != v) continue;
+      any = true;
+      const long i = (long)r * D + d;
+      float g = dy[i];
+      if (thr) g = esp::keep_elem(seed, (uint64_t)i, thr) ? g * scale : 0.f;
+      acc += g * xscale;
+    }
+    if (any) dE[(long)v * D + d] += acc;
+  }
+}
+
+__global__ void scale_by_dev_kernel(float* __restrict__ x, long n, const float* __restrict__ s) {
+  const float v = *s;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) x[i] *= v;
+}
+
+// ------------------------------------------------------------------------- SpecAugment
+// Bicubic (A=-0.75) resampling identical to torch upsample_bicubic2d with
+// align_corners=False along time only (the freq size is unchanged, so its weights are
+// the identity): time_warp.py:9-46.  One launch handles a whole batch; per utterance
+// (len, center, warped) describe the warp of x[b, :len] (len==T & shared params for the
+// equal-length branch of TimeWarp.forward, time_warp.py:73-86).
+__device__ __forceinline__ float cubic1(float x, float A) { return ((A + 2) * x - (A + 3)) * x * x + 1; }
+__device__ __forceinline__ float cubic2(float x, float A) { return ((A * x - 5 * A) * x + 8 * A) * x - 4 * A; }
+
+__device__ float bicubic_seg(const float* __restrict__ src, int F, int in_len, int out_len, int o, int f) {
+  // src points at the first row of the input segment (in_len rows of F)
+  const float sc = (float)in_len / (float)out_len;
+  const float real = sc * (o + 0.5f) - 0.5f;
+  const float fl = floorf(real);
+  const int i0 = (int)fl;
+  const float t = real - fl;
+  const float A = -0.75f;
+  const float w0 = cubic2(t + 1.0f, A), w1 = cubic1(t, A), w2 = cubic1(1.0f - t, A), w3 = cubic2(2.0f - t, A);
+  auto at = [&](int i) {
+    i = i < 0 ? 0 : (i > in_len - 1 ? in_len - 1 : i);
+    return src[(long)i * F + f];
+  };
+  return at(i0 - 1) * w0 + at(i0) * w1 + at(i0 + 1) * w2 + at(i0 + 2) * w3;
+}
+
+__global__ void specaug_kernel(const float* __restrict__ x, float* __restrict__ y, int B, int T, int F,
+                               const int* __restrict__ lens, const int* __restrict__ warp /*B x2*/,
+                               const int* __restrict__ fmask /*B x nf x2*/, int nf,
+                               const int* __restrict__ tmask /*B x nt x2*/, int nt) {
+  const long n = (long)B * T * F;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int f = (int)(i % F);
+    const long bt = i / F;
+    const int t = (int)(bt % T), b = (int)(bt / T);
+    const float* xb = x + (long)b * T * F;
+    const int len = lens[b];
+    float v;
+    if (warp && t >= len) {
+      v = 0.f;  // per-utterance warp pads with 0.0 (time_warp.py:86, pad_list)
+    } else if (warp && warp[2 * b] > 0) {
+      const int center = warp[2 * b], warped = warp[2 * b + 1];
+      if (t < warped) v = bicubic_seg(xb, F, center, warped, t, f);
+      else v = bicubic_seg(xb + (long)center * F, F, len - center, len - warped, t - warped, f);
+    } else {
+      v = xb[(long)t * F + f];
+    }
+    bool m = false;
+    for (int k = 0; k < nf; ++k) {
+      const int p = fmask[(b * nf + k) * 2], w = fmask[(b * nf + k) * 2 + 1];
+      m |= (f >= p && f < p + w);
+    }
+    for (int k = 0; k < nt; ++k) {
+      const int p = tmask[(b * nt + k) * 2], w = tmask[(b * nt + k) * 2 + 1];
+      m |= (t >= p && t < p + w);
+    }
+    y[i] = m ? 0.f : v;
+  }
+}
+
+// UtteranceMVN (norm_means=True, norm_vars=False): zero the pad, subtract the per-utterance
+// mean over valid frames from EVERY frame (pads become -mean), utterance_mvn.py:45-80.
+// One block per (b, feature-chunk of 64); threads stride over time.
+__global__ void mvn_kernel(float* __restrict__ x, int T, int F, const int* __restrict__ lens) {
+  const int b = blockIdx.x;
+  const int f = blockIdx.y * 64 + (threadIdx.x & 63);
+  const int tg = threadIdx.x >> 6, ntg = blockDim.x >> 6;
+  __shared__ double sh[16][64];
+  const int len = lens[b];
+  float* xb = x + (long)b * T * F;
+  double s = 0.0;
+  if (f < F)
+    for (int t = tg; t < len; t += ntg) s += xb[(long)t * F + f];
+  sh[tg][threadIdx.x & 63] = s;
+  __syncthreads();
+  double tot = 0.0;
+  for (int k = 0; k < ntg; ++k) tot += sh[k][threadIdx.x & 63];
+  const float mean = (float)(tot / (double)len);
+  if (f < F)
+    for (int t = tg; t < T; t += ntg) {
+      const long o = (long)t * F + f;
+      xb[o] = (t < len ? xb[o] : 0.f) - mean;
+    }
+}
+
+// ------------------------------------------------------------------------- optimizer
+// sum of squares of the flat gradient, stage 1 (per-block partial, fp64)
+__global__ void sumsq_kernel(const float* __restrict__ g, long n, double* __restrict__ part) {
+  __shared__ double sh[16];
+  double s = 0.0;
+  const long n4 = n / 4;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const float4 v = g4[i];
+    s += (double)v.x * v.x + (double)v.y * v.y + (double)v.z * v.z + (double)v.w * v.w;
+  }
+  for (long i = n4 * 4 + blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    s += (double)g[i] * g[i];
+  s = esp::block_sum<double>(s, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+// stage 2: norm, clip coefficient (torch clip_grad_norm_: coef = max_norm/(norm+1e-6),
+// clamped to 1) and finite flag. out[0]=norm, out[1]=coef, out[2]=finite(1/0)
+__global__ void norm_finalize_kernel(const double* __restrict__ part, int nb, float max_norm,
+                                     float* __restrict__ out) {
+  __shared__ double sh[16];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) s += part[i];
+  s = esp::block_sum<double>(s, sh);
+  if (threadIdx.x == 0) {
+    const float norm = (float)sqrt(s);
+    float coef = max_norm / (norm + 1e-6f);
+    coef = coef < 1.f ? coef : 1.f;
+    out[0] = norm;
+    out[1] = coef;
+    out[2] = isfinite(norm) ? 1.f : 0.f;
+  }
+}
+
+// torch.optim.Adam (non-amsgrad, L2 weight_decay added to the gradient), step `t`
+// (1-based), applied to the flat buffers; grad is first multiplied by the clip coefficient.
+// Skips entirely when the finite flag is 0 (trainer.py:651-667).
+__global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                            float* __restrict__ v, long n, const float* __restrict__ clip, float lr,
+                            float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt) {
+  if (clip[2] == 0.f) return;
+  const float coef = clip[1];
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float gi = g[i] * coef;
+    const float pi = p[i];
+    if (wd != 0.f) gi += wd * pi;
+    const float m0 = m[i];
+    const float mi = m0 + (1.f - b1) * (gi - m0);  // torch: exp_avg.lerp_(grad, 1-beta1)
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    p[i] = pi - (lr / bc1) * (mi / denom);
+  }
+}
+
+}  // namespace
+
+ESP_API int esp_act_bwd(const float* dy, const float* h, float* dx, long n, int act, float drop_p,
+                        unsigned long long seed, long idx_off, void* stream) {
+  const uint32_t thr = drop_threshold(drop_p);
+  hipLaunchKernelGGL(act_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, dy, h, dx, n, act,
+                     thr, thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed, idx_off);
+  ESP_CHECK_LAUNCH("esp_act_bwd");
+  return 0;
+}
+
+ESP_API int esp_scale_dropout(const float* x, float* y, long n, float alpha, float drop_p, unsigned long long seed,
+                              const float* r, float beta, void* stream) {
+  const uint32_t thr = drop_threshold(drop_p);
+  hipLaunchKernelGGL(scale_drop_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, y, n, alpha, thr,
+                     thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed, r, beta);
+  ESP_CHECK_LAUNCH("esp_scale_dropout");
+  return 0;
+}
+
+// x *= *s  (s on device: the autograd grad_output, no host sync)
+ESP_API int esp_scale_by_dev(float* x, long n, const float* s, void* stream) {
+  hipLaunchKernelGGL(scale_by_dev_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, n, s);
+  ESP_CHECK_LAUNCH("esp_scale_by_dev");
+  return 0;
+}
+
+ESP_API int esp_embed_fwd(const long long* tok, const float* E, const float* pe, float* y, int nrows, int L, int D,
+                          float xscale, float drop_p, unsigned long long seed, void* stream) {
+  const uint32_t thr = drop_threshold(drop_p);
+  const long n = (long)nrows * D;
+  hipLaunchKernelGGL(embed_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const int64_t*)tok, E,
+                     pe, y, L, D, xscale, thr, thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed, n);
+  ESP_CHECK_LAUNCH("esp_embed_fwd");
+  return 0;
+}
+
+ESP_API int esp_embed_bwd(const long long* tok, const float* dy, float* dE, int nrows, int V, int D, float xscale,
+                          float drop_p, unsigned long long seed, void* stream) {
+  const uint32_t thr = drop_threshold(drop_p);
+  hipLaunchKernelGGL(embed_bwd_kernel, dim3(V), dim3(256), 0, (hipStream_t)stream, (const int64_t*)tok, dy, dE, nrows,
+                     D, xscale, thr, thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed);
+  ESP_CHECK_LAUNCH("esp_embed_bwd");
+  return 0;
+}
+
+ESP_API int esp_specaug(const float* x, float* y, int B, int T, int F, const int* lens, const int* warp,
+                        const int* fmask, int nf, const int* tmask, int nt, void* stream) {
+  ESP_ARG_CHECK(x != y, "esp_specaug: in-place not supported");
+  const long n = (long)B * T * F;
+  hipLaunchKernelGGL(specaug_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, y, B, T, F, lens, warp,
+                     fmask, nf, tmask, nt);
+  ESP_CHECK_LAUNCH("esp_specaug");
+  return 0;
+}
+
+ESP_API int esp_utterance_mvn(float* x, int B, int T, int F, const int* lens, void* stream) {
+  hipLaunchKernelGGL(mvn_kernel, dim3(B, (F + 63) / 64), dim3(1024), 0, (hipStream_t)stream, x, T, F, lens);
+  ESP_CHECK_LAUNCH("esp_utterance_mvn");
+  return 0;
+}
+
+// workspace: >= 1024 doubles; out: 3 floats (norm, clip coef, finite flag) on device
+ESP_API int esp_grad_norm(const float* g, long n, float max_norm, double* work, float* out, void* stream) {
+  const int nb = 1024;
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, g, n, work);
+  hipLaunchKernelGGL(norm_finalize_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, work, nb, max_norm, out);
+  ESP_CHECK_LAUNCH("esp_grad_norm");
+  return 0;
+}
+
+ESP_API int esp_adam(float* p, const float* g, float* m, float* v, long n, const float* clip, float lr, float b1,
+                     float b2, float eps, float wd, int step, void* stream) {
+  ESP_ARG_CHECK(step >= 1, "esp_adam: step must be >= 1");
+  const float bc1 = (float)(1.0 - pow((double)b1, (double)step));  // python-float math, as torch
+  const float bc2 = (float)(1.0 - pow((double)b2, (double)step));
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, clip, lr,
+                     b1, b2, eps, wd, bc1, sqrtf(bc2));
+  ESP_CHECK_LAUNCH("esp_adam");
+  return 0;
+}

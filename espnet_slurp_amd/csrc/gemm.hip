@@ -1,0 +1,315 @@
+// FP32 MFMA GEMM for gfx950 (v_mfma_f32_32x32x2_f32: exact f32 fma chain, 64 FLOP/clk/SIMD).
+//
+//   C[z](m,n) = alpha * epi( sum_k A[z](m,k) * B[z](k,n) + bias[n] ) + beta * R[z](m,n)
+//
+// Operand access modes (template):
+//   KC     element (r,k) at p[r*ld + k]      (A row-major [M][K] / B as [N][K] = W of nn.Linear)
+//   RC     element (r,k) at p[k*ld + r]      (A as [K][M] / B row-major [K][N])
+//   I2C_KC im2col view of an NHWC map, (r = output pixel, k = (kt,kf,c))   [conv2 forward, A]
+//   I2C_RC same map with roles swapped (r = (kt,kf,c), k = output pixel)   [conv2 dW, B]
+// Batches: z = z1*nb2 + z2, operand offset = z1*s1 + z2*s2 (two-level strides cover the
+// (batch, head) layouts of attention without copies).
+//
+// Tiling: 128x128 block tile, BK=16, 256 threads = 4 waves (2x2), each wave 64x64 =
+// 2x2 MFMA 32x32 tiles. LDS holds both tiles as [row][BK+4] (row = m or n): a lane of
+// half h uses k = 8h+s for MFMA step s, so its 8 operands are 2 contiguous ds_read_b128,
+// conflict-free at the 20-float row stride. Global->LDS is register-staged and double
+// buffered (next slab's loads are issued before the current slab's MFMAs).
+// Epilogue (fused): bias, ReLU/Swish (pre-activation optionally stored to `aux`),
+// counter-RNG dropout, alpha scale and beta*R residual.
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 16, LDS_S = BK + 4, NT = 256;
+
+enum Mode { KC = 0, RC = 1, I2C_KC = 2, I2C_RC = 3 };
+enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_SWISH = 2 };
+
+struct Im2col {  // NHWC input map [Bn][H][W][C], 3x3 kernel, stride 2, no padding
+  int H, W, C, Ho, Wo;
+};
+
+struct Operand {
+  const float* p;
+  long ld;
+  long s1, s2;
+  int vec;  // float4 along the contiguous dim is legal
+  Im2col ic;
+};
+
+struct GemmArgs {
+  int M, N, K, nb2;
+  Operand a, b;
+  float* c;
+  long ldc, c1, c2;
+  const float* r;  // residual (same layout as C), may alias c
+  float* aux;      // pre-activation store (same layout as C)
+  const float* bias;
+  float alpha, beta;
+  int act;
+  uint32_t drop_thresh;  // 0 = no dropout
+  float drop_scale;
+  uint64_t seed;
+};
+
+// address of im2col element: pixel index `pix` of the output grid, column `col` = (kt,kf,c)
+__device__ __forceinline__ const float* i2c_ptr(const float* base, const Im2col& ic, long pix, int col) {
+  const int hw = ic.Ho * ic.Wo;
+  const long bi = pix / hw;
+  const int rem = (int)(pix - bi * hw);
+  const int ho = rem / ic.Wo, wo = rem - (rem / ic.Wo) * ic.Wo;
+  const int kk = col / ic.C, c = col - kk * ic.C;
+  const int kt = kk / 3, kf = kk - kt * 3;
+  return base + (((bi * ic.H + 2 * ho + kt) * (long)ic.W) + 2 * wo + kf) * ic.C + c;
+}
+
+// Load this thread's 2 float4 pieces of a (R rows x BK) operand slab into registers.
+// rows = M (A) or N (B); row0 = tile origin; k0 = slab origin.
+template <int MODE>
+__device__ __forceinline__ void load_slab(const Operand& op, const float* base, int rows, int K,
+                                          int row0, int k0, float4 (&reg)[2]) {
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int idx = threadIdx.x + it * NT;  // 0..511
+    if constexpr (MODE == KC || MODE == I2C_KC) {
+      // 128 rows x 4 quads along k
+      const int r = idx >> 2, kq = (idx & 3) * 4;
+      const int gr = row0 + r, gk = k0 + kq;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (gr < rows) {
+        if (MODE == KC) {
+          const float* p = base + (long)gr * op.ld + gk;
+          if (op.vec && gk + 3 < K) {
+            v = *reinterpret_cast<const float4*>(p);
+          } else {
+            if (gk + 0 < K) v.x = p[0];
+            if (gk + 1 < K) v.y = p[1];
+            if (gk + 2 < K) v.z = p[2];
+            if (gk + 3 < K) v.w = p[3];
+          }
+        } else {
+          if (gk + 3 < K) {  // C % 4 == 0 enforced on host: quad never straddles a tap
+            v = *reinterpret_cast<const float4*>(i2c_ptr(base, op.ic, gr, gk));
+          } else {
+            if (gk + 0 < K) v.x = *i2c_ptr(base, op.ic, gr, gk + 0);
+            if (gk + 1 < K) v.y = *i2c_ptr(base, op.ic, gr, gk + 1);
+            if (gk + 2 < K) v.z = *i2c_ptr(base, op.ic, gr, gk + 2);
+          }
+        }
+      }
+      reg[it] = v;
+    } else {
+      // BK k-rows x 32 quads along r
+      const int kr = idx >> 5, rq = (idx & 31) * 4;
+      const int gk = k0 + kr, gr = row0 + rq;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (gk < K) {
+        if (MODE == RC) {
+          const float* p = base + (long)gk * op.ld + gr;
+          if (op.vec && gr + 3 < rows) {
+            v = *reinterpret_cast<const float4*>(p);
+          } else {
+            if (gr + 0 < rows) v.x = p[0];
+            if (gr + 1 < rows) v.y = p[1];
+            if (gr + 2 < rows) v.z = p[2];
+            if (gr + 3 < rows) v.w = p[3];
+          }
+        } else {
+          if (gr + 3 < rows) {
+            v = *reinterpret_cast<const float4*>(i2c_ptr(base, op.ic, gk, gr));
+          } else {
+            if (gr + 0 < rows) v.x = *i2c_ptr(base, op.ic, gk, gr + 0);
+            if (gr + 1 < rows) v.y = *i2c_ptr(base, op.ic, gk, gr + 1);
+            if (gr + 2 < rows) v.z = *i2c_ptr(base, op.ic, gk, gr + 2);
+          }
+        }
+      }
+      reg[it] = v;
+    }
+  }
+}
+
+// LDS image: row r, k-quad q stored at quad (q ^ ((r >> 3) & 3)) of a 20-float row.
+// The XOR keeps the transposing scalar writes of RC operands at <=4-way bank conflicts
+// (a plain 20-float stride puts a wave's 32 writes on 2 banks) while every float4
+// stays contiguous for ds_read_b128 / ds_write_b128.
+__device__ __forceinline__ int lds_off(int r, int kq) { return r * LDS_S + ((kq ^ ((r >> 3) & 3)) << 2); }
+
+template <int MODE>
+__device__ __forceinline__ void store_slab(float* lds, const float4 (&reg)[2]) {
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int idx = threadIdx.x + it * NT;
+    if constexpr (MODE == KC || MODE == I2C_KC) {
+      const int r = idx >> 2, kq = idx & 3;
+      *reinterpret_cast<float4*>(lds + lds_off(r, kq)) = reg[it];
+    } else {
+      const int kr = idx >> 5, rq = (idx & 31) * 4;
+      const int q = kr >> 2, e = kr & 3;
+      lds[lds_off(rq + 0, q) + e] = reg[it].x;
+      lds[lds_off(rq + 1, q) + e] = reg[it].y;
+      lds[lds_off(rq + 2, q) + e] = reg[it].z;
+      lds[lds_off(rq + 3, q) + e] = reg[it].w;
+    }
+  }
+}
+
+template <int MA, int MB>
+__global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) float As[2][BM * LDS_S];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDS_S];
+
+  const int z = blockIdx.z;
+  const int z1 = z / g.nb2, z2 = z - z1 * g.nb2;
+  const float* Ab = g.a.p + z1 * g.a.s1 + z2 * g.a.s2;
+  const float* Bb = g.b.p + z1 * g.b.s1 + z2 * g.b.s2;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int h = lane >> 5, l32 = lane & 31;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  float4 ra[2], rb[2];
+  const int nk = (g.K + BK - 1) / BK;
+  load_slab<MA>(g.a, Ab, g.M, g.K, m0, 0, ra);
+  load_slab<MB>(g.b, Bb, g.N, g.K, n0, 0, rb);
+  store_slab<MA>(As[0], ra);
+  store_slab<MB>(Bs[0], rb);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      load_slab<MA>(g.a, Ab, g.M, g.K, m0, (kt + 1) * BK, ra);
+      load_slab<MB>(g.b, Bb, g.N, g.K, n0, (kt + 1) * BK, rb);
+    }
+    float af[2][8], bf[2][8];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int ra_ = wm * 64 + t * 32 + l32;
+      const float4 a0 = *reinterpret_cast<const float4*>(As[cur] + lds_off(ra_, 2 * h));
+      const float4 a1 = *reinterpret_cast<const float4*>(As[cur] + lds_off(ra_, 2 * h + 1));
+      af[t][0] = a0.x; af[t][1] = a0.y; af[t][2] = a0.z; af[t][3] = a0.w;
+      af[t][4] = a1.x; af[t][5] = a1.y; af[t][6] = a1.z; af[t][7] = a1.w;
+      const int rb_ = wn * 64 + t * 32 + l32;
+      const float4 b0 = *reinterpret_cast<const float4*>(Bs[cur] + lds_off(rb_, 2 * h));
+      const float4 b1 = *reinterpret_cast<const float4*>(Bs[cur] + lds_off(rb_, 2 * h + 1));
+      bf[t][0] = b0.x; bf[t][1] = b0.y; bf[t][2] = b0.z; bf[t][3] = b0.w;
+      bf[t][4] = b1.x; bf[t][5] = b1.y; bf[t][6] = b1.z; bf[t][7] = b1.w;
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+    if (kt + 1 < nk) {
+      store_slab<MA>(As[cur ^ 1], ra);
+      store_slab<MB>(Bs[cur ^ 1], rb);
+    }
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  float* Cb = g.c + z1 * g.c1 + z2 * g.c2;
+  const float* Rb = g.r ? g.r + z1 * g.c1 + z2 * g.c2 : nullptr;
+  float* Xb = g.aux ? g.aux + z1 * g.c1 + z2 * g.c2 : nullptr;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn * 64 + j * 32 + l32;
+      if (n >= g.N) continue;
+      const float bv = g.bias ? g.bias[n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m >= g.M) continue;
+        const long off = (long)m * g.ldc + n;
+        float v = acc[i][j][r] + bv;
+        if (Xb) Xb[off] = v;
+        if (g.act == ACT_RELU) v = fmaxf(v, 0.f);
+        else if (g.act == ACT_SWISH) v = v / (1.0f + expf(-v));
+        if (g.drop_thresh) {
+          const uint64_t idx = ((uint64_t)z * g.M + m) * (uint64_t)g.N + n;
+          v = esp::keep_elem(g.seed, idx, g.drop_thresh) ? v * g.drop_scale : 0.f;
+        }
+        v *= g.alpha;
+        if (Rb) v += g.beta * Rb[off];
+        Cb[off] = v;
+      }
+    }
+}
+
+template <int MA, int MB>
+int launch(const GemmArgs& g, int batch, hipStream_t st) {
+  dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, batch);
+  hipLaunchKernelGGL((gemm_f32_kernel<MA, MB>), grid, dim3(NT), 0, st, g);
+  ESP_CHECK_LAUNCH("gemm_f32");
+  return 0;
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+// C-ABI: see include/espnet_mi355.h for the contract.
+ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2,
+                         const float* A, long lda, long sa1, long sa2,
+                         const float* B, long ldb, long sb1, long sb2,
+                         float* C, long ldc, long sc1, long sc2,
+                         const float* bias, float alpha, float beta, const float* R,
+                         int act, float* aux, float drop_p, unsigned long long seed,
+                         const int* im2col_a, const int* im2col_b, void* stream) {
+  ESP_ARG_CHECK(M >= 0 && N >= 0 && K >= 0 && batch >= 1 && nb2 >= 1 && batch % nb2 == 0,
+                "esp_gemm_f32: bad sizes M=%d N=%d K=%d batch=%d nb2=%d", M, N, K, batch, nb2);
+  ESP_ARG_CHECK(mode_a >= 0 && mode_a <= 3 && mode_b >= 0 && mode_b <= 3, "esp_gemm_f32: bad mode");
+  ESP_ARG_CHECK(drop_p >= 0.f && drop_p < 1.f, "esp_gemm_f32: bad dropout p");
+  if (M == 0 || N == 0) return 0;
+  GemmArgs g{};
+  g.M = M; g.N = N; g.K = K; g.nb2 = nb2;
+  g.a = Operand{A, lda, sa1, sa2, 0, {}};
+  g.b = Operand{B, ldb, sb1, sb2, 0, {}};
+  g.a.vec = aligned16(A) && lda % 4 == 0 && sa1 % 4 == 0 && sa2 % 4 == 0;
+  g.b.vec = aligned16(B) && ldb % 4 == 0 && sb1 % 4 == 0 && sb2 % 4 == 0;
+  if (mode_a >= 2) {
+    ESP_ARG_CHECK(im2col_a && im2col_a[2] % 4 == 0 && aligned16(A), "esp_gemm_f32: im2col A needs C%%4==0");
+    g.a.ic = Im2col{im2col_a[0], im2col_a[1], im2col_a[2], im2col_a[3], im2col_a[4]};
+  }
+  if (mode_b >= 2) {
+    ESP_ARG_CHECK(im2col_b && im2col_b[2] % 4 == 0 && aligned16(B), "esp_gemm_f32: im2col B needs C%%4==0");
+    g.b.ic = Im2col{im2col_b[0], im2col_b[1], im2col_b[2], im2col_b[3], im2col_b[4]};
+  }
+  g.c = C; g.ldc = ldc; g.c1 = sc1; g.c2 = sc2;
+  g.r = R; g.aux = aux; g.bias = bias; g.alpha = alpha; g.beta = beta; g.act = act;
+  g.seed = seed;
+  if (drop_p > 0.f) {
+    double t = (double)drop_p * 4294967296.0;
+    g.drop_thresh = (uint32_t)(t >= 4294967295.0 ? 4294967295.0 : t);
+    if (g.drop_thresh == 0) g.drop_thresh = 1;
+    g.drop_scale = 1.0f / (1.0f - drop_p);
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const int key = mode_a * 4 + mode_b;
+  switch (key) {
+    case KC * 4 + KC: return launch<KC, KC>(g, batch, st);
+    case KC * 4 + RC: return launch<KC, RC>(g, batch, st);
+    case RC * 4 + KC: return launch<RC, KC>(g, batch, st);
+    case RC * 4 + RC: return launch<RC, RC>(g, batch, st);
+    case I2C_KC * 4 + KC: return launch<I2C_KC, KC>(g, batch, st);
+    case RC * 4 + I2C_RC: return launch<RC, I2C_RC>(g, batch, st);
+    default:
+      esp::set_error("esp_gemm_f32: unsupported mode pair %d,%d", mode_a, mode_b);
+      return -1;
+  }
+}

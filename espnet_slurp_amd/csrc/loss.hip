@@ -1,0 +1,407 @@
+// Loss kernels of the hybrid CTC/attention objective (espnet_model.py:169-297):
+//   * row log-softmax (CTC input, ctc.py:53)
+//   * CTC alpha/beta (one block per utterance and direction, the two recursions run
+//     concurrently) and the per-frame gradient w.r.t. the logits, following PyTorch's
+//     CPU ctc_loss (max-shifted 3-way log-sum-exp, zero_infinity, grad
+//     exp(lp) - exp(lcab + nll - lp), then log_softmax's adjoint)   [ctc.py:39-60]
+//   * label-smoothed KL (t*log t included) + gradient + th_accuracy counts
+//     [label_smoothing_loss.py:41-63, nets_utils.py:299-320]
+//   * deterministic final reduction to the reported scalars
+//   * CTC.argmax (ctc.py:119-127) and espnet1 CTC.forced_align Viterbi
+//     (espnet/nets/pytorch_backend/ctc.py:185-249) with its fp32-add and s=0 wrap quirks.
+#include "common.h"
+
+namespace {
+
+__device__ __forceinline__ float lse2(float a, float b) {
+  const float m = fmaxf(a, b);
+  if (m == -INFINITY) return -INFINITY;
+  return logf(expf(a - m) + expf(b - m)) + m;
+}
+
+// block-per-row log-softmax, any V
+__global__ void log_softmax_kernel(const float* __restrict__ x, float* __restrict__ y, int V) {
+  __shared__ float sh[16];
+  const long row = blockIdx.x;
+  const float* xr = x + row * V;
+  float m = -INFINITY;
+  for (int c = threadIdx.x; c < V; c += blockDim.x) m = fmaxf(m, xr[c]);
+  m = esp::block_max(m, sh);
+  float s = 0.f;
+  for (int c = threadIdx.x; c < V; c += blockDim.x) s += expf(xr[c] - m);
+  s = esp::block_sum<float>(s, sh);
+  const float lse = m + logf(s);
+  float* yr = y + row * V;
+  for (int c = threadIdx.x; c < V; c += blockDim.x) yr[c] = xr[c] - lse;
+}
+
+// blockIdx.x = utterance, blockIdx.y = 0 alpha / 1 beta.  lp: (B, T, V) log-probs.
+// labels (B, Umax) int64 (row b valid for tlen[b]); la/lb: (B, T, Smax) outputs.
+constexpr int CTC_NT = 256, CTC_SPT = 4;  // states per thread -> S <= 1024
+__global__ __launch_bounds__(CTC_NT) void ctc_alpha_beta_kernel(const float* __restrict__ lp, const int64_t* __restrict__ labels,
+                                                                int Umax, const int* __restrict__ ilen,
+                                                                const int* __restrict__ tlen, int T, int V, int Smax,
+                                                                int blank, float* __restrict__ la, float* __restrict__ lb,
+                                                                float* __restrict__ nll) {
+  const int b = blockIdx.x;
+  const int dir = blockIdx.y;
+  const int Tb = ilen[b], U = tlen[b], S = 2 * U + 1;
+  __shared__ float buf[2][CTC_NT * CTC_SPT + 2];
+  __shared__ int lab[CTC_NT * CTC_SPT + 2];
+  const float* lpb = lp + (long)b * T * V;
+  for (int s = threadIdx.x; s < S + 2; s += CTC_NT) {
+    int l = blank;
+    if (s < S && (s & 1)) l = (int)labels[(long)b * Umax + (s >> 1)];
+    lab[s] = l;
+  }
+  __syncthreads();
+  float* out = (dir == 0 ? la : lb) + (long)b * T * Smax;
+  if (Tb <= 0) {
+    if (dir == 0 && threadIdx.x == 0) nll[b] = INFINITY;
+    return;
+  }
+  int cur = 0;
+  if (dir == 0) {
+    for (int s = threadIdx.x; s < S; s += CTC_NT) {
+      float v = -INFINITY;
+      if (s == 0) v = lpb[blank];
+      else if (s == 1) v = lpb[lab[1]];
+      buf[0][s] = v;
+      out[s] = v;
+    }
+    __syncthreads();
+    for (int t = 1; t < Tb; ++t) {
+      const float* lpt = lpb + (long)t * V;
+      for (int s = threadIdx.x; s < S; s += CTC_NT) {
+        const float l1 = buf[cur][s];
+        const float l2 = s > 0 ? buf[cur][s - 1] : -INFINITY;
+        const float l3 = (s > 1 && lab[s] != lab[s - 2]) ? buf[cur][s - 2] : -INFINITY;
+        float m = fmaxf(l1, fmaxf(l2, l3));
+        if (m == -INFINITY) m = 0.f;
+        const float v = logf(expf(l1 - m) + expf(l2 - m) + expf(l3 - m)) + m + lpt[lab[s]];
+        buf[cur ^ 1][s] = v;
+        out[(long)t * Smax + s] = v;
+      }
+      cur ^= 1;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      const float l1 = buf[cur][S - 1];
+      const float l2 = S > 1 ? buf[cur][S - 2] : -INFINITY;
+      float m = fmaxf(l1, l2);
+      if (m == -INFINITY) m = 0.f;
+      nll[b] = -(logf(expf(l1 - m) + expf(l2 - m)) + m);
+    }
+  } else {
+    const float* lpt0 = lpb + (long)(Tb - 1) * V;
+    for (int s = threadIdx.x; s < S; s += CTC_NT) {
+      float v = -INFINITY;
+      if (s == S - 1) v = lpt0[blank];
+      else if (s == S - 2) v = lpt0[lab[S - 2]];
+      buf[0][s] = v;
+      out[(long)(Tb - 1) * Smax + s] = v;
+    }
+    __syncthreads();
+    for (int t = Tb - 2; t >= 0; --t) {
+      const float* lpt = lpb + (long)t * V;
+      for (int s = threadIdx.x; s < S; s += CTC_NT) {
+        const float l1 = buf[cur][s];
+        const float l2 = s < S - 1 ? buf[cur][s + 1] : -INFINITY;
+        const float l3 = (s < S - 2 && lab[s] != lab[s + 2]) ? buf[cur][s + 2] : -INFINITY;
+        float m = fmaxf(l1, fmaxf(l2, l3));
+        if (m == -INFINITY) m = 0.f;
+        const float v = logf(expf(l1 - m) + expf(l2 - m) + expf(l3 - m)) + m + lpt[lab[s]];
+        buf[cur ^ 1][s] = v;
+        out[(long)t * Smax + s] = v;
+      }
+      cur ^= 1;
+      __syncthreads();
+    }
+  }
+}
+
+// grid (T, B): gradient of gscale * nll_b w.r.t. the logits for frame t of utterance b
+constexpr int MAXV_LDS = 8192;
+__global__ __launch_bounds__(256) void ctc_grad_kernel(const float* __restrict__ lp, const int64_t* __restrict__ labels,
+                                                       int Umax, const int* __restrict__ ilen,
+                                                       const int* __restrict__ tlen, int T, int V, int Smax, int blank,
+                                                       const float* __restrict__ la, const float* __restrict__ lb,
+                                                       const float* __restrict__ nll, float gscale, int zero_infinity,
+                                                       float* __restrict__ grad) {
+  __shared__ float occ[MAXV_LDS];
+  __shared__ float sh[16];
+  const int t = blockIdx.x, b = blockIdx.y;
+  const int Tb = ilen[b], U = tlen[b], S = 2 * U + 1;
+  float* gr = grad + ((long)b * T + t) * V;
+  const float nl = nll[b];
+  if (t >= Tb || (zero_infinity && isinf(nl))) {
+    for (int c = threadIdx.x; c < V; c += blockDim.x) gr[c] = 0.f;
+    return;
+  }
+  for (int c = threadIdx.x; c < V; c += blockDim.x) occ[c] = 0.f;
+  const float* lat = la + ((long)b * T + t) * Smax;
+  const float* lbt = lb + ((long)b * T + t) * Smax;
+  float m = -INFINITY;
+  for (int s = threadIdx.x; s < S; s += blockDim.x) m = fmaxf(m, lat[s] + lbt[s]);
+  m = esp::block_max(m, sh);  // includes a barrier: occ is zeroed before the adds below
+  if (m != -INFINITY) {
+    for (int s = threadIdx.x; s < S; s += blockDim.x) {
+      const int l = (s & 1) ? (int)labels[(long)b * Umax + (s >> 1)] : blank;
+      const float v = lat[s] + lbt[s];
+      if (v != -INFINITY) atomicAdd(&occ[l], expf(v - m));
+    }
+  }
+  __syncthreads();
+  const float* lpt = lp + ((long)b * T + t) * V;
+  float gs = 0.f;
+  for (int c = threadIdx.x; c < V; c += blockDim.x) {
+    const float l = lpt[c];
+    const float o = occ[c];
+    const float lcab = o > 0.f ? m + logf(o) : -INFINITY;
+    const float g = expf(l) - expf(lcab + nl - l);
+    gs += g;
+  }
+  gs = esp::block_sum<float>(gs, sh);
+  for (int c = threadIdx.x; c < V; c += blockDim.x) {
+    const float l = lpt[c];
+    const float o = occ[c];
+    const float lcab = o > 0.f ? m + logf(o) : -INFINITY;
+    const float e = expf(l);
+    const float g = (e - expf(lcab + nl - l)) * gscale;
+    gr[c] = g - e * (gs * gscale);
+  }
+}
+
+// label smoothing: block per row.  rows with target == ignore get zero loss/grad.
+__global__ __launch_bounds__(256) void ls_kernel(const float* __restrict__ x, const int64_t* __restrict__ target,
+                                                 int V, int ignore, float smoothing, float gscale,
+                                                 float* __restrict__ grad, float* __restrict__ row_loss,
+                                                 int* __restrict__ row_stat) {
+  __shared__ float sh[16];
+  __shared__ int shi[16];
+  const long row = blockIdx.x;
+  const float* xr = x + row * V;
+  float* gr = grad ? grad + row * V : nullptr;
+  const int64_t tg = target[row];
+  if (tg == ignore) {
+    if (gr)
+      for (int c = threadIdx.x; c < V; c += blockDim.x) gr[c] = 0.f;
+    if (threadIdx.x == 0) {
+      row_loss[row] = 0.f;
+      row_stat[2 * row] = 0;
+      row_stat[2 * row + 1] = 0;
+    }
+    return;
+  }
+  // max + first argmax
+  float m = -INFINITY;
+  int am = 0x7fffffff;
+  for (int c = threadIdx.x; c < V; c += blockDim.x) {
+    const float v = xr[c];
+    if (v > m) { m = v; am = c; }
+  }
+  // wave/block argmax with first-index tie-break
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64);
+    const int oa = __shfl_xor(am, o, 64);
+    if (om > m || (om == m && oa < am)) { m = om; am = oa; }
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) { sh[w] = m; shi[w] = am; }
+  __syncthreads();
+  m = sh[0];
+  am = shi[0];
+  for (int i = 1; i < (int)(blockDim.x >> 6); ++i)
+    if (sh[i] > m || (sh[i] == m && shi[i] < am)) { m = sh[i]; am = shi[i]; }
+  __syncthreads();
+  float s = 0.f, slp = 0.f;
+  for (int c = threadIdx.x; c < V; c += blockDim.x) {
+    s += expf(xr[c] - m);
+    slp += xr[c];
+  }
+  s = esp::block_sum<float>(s, sh);
+  slp = esp::block_sum<float>(slp, sh);
+  const float lse = m + logf(s);
+  const float conf = 1.0f - smoothing;
+  const float sv = smoothing / (float)(V - 1);
+  const float lpt = xr[tg] - lse;
+  const float sum_lp = slp - (float)V * lse;
+  if (threadIdx.x == 0) {
+    float l = 0.f;
+    if (conf > 0.f) l += conf * (logf(conf) - lpt);
+    if (sv > 0.f) l += sv * ((float)(V - 1) * logf(sv) - (sum_lp - lpt));
+    row_loss[row] = l;
+    row_stat[2 * row] = (am == (int)tg) ? 1 : 0;
+    row_stat[2 * row + 1] = 1;
+  }
+  if (gr) {
+    const float tot = conf + sv * (float)(V - 1);
+    for (int c = threadIdx.x; c < V; c += blockDim.x) {
+      const float p = expf(xr[c] - lse);
+      const float td = (c == (int)tg) ? conf : sv;
+      gr[c] = (p * tot - td) * gscale;
+    }
+  }
+}
+
+// out[0] = ctc loss = sum_b nll_b' / B ;  out[1] = att loss = sum rows / denom ;
+// out[2] = acc ; out[3] = w*out[0] + (1-w)*out[1].  One block, fixed order.
+__global__ void reduce_losses_kernel(const float* __restrict__ nll, int B, int zero_inf, const float* __restrict__ row_loss,
+                                     const int* __restrict__ row_stat, int R, float denom, float ctc_w,
+                                     float* __restrict__ out) {
+  __shared__ double shd[16];
+  double a = 0.0;
+  for (int i = threadIdx.x; i < B && nll; i += blockDim.x) {
+    float v = nll[i];
+    if (zero_inf && isinf(v)) v = 0.f;
+    a += v;
+  }
+  a = esp::block_sum<double>(a, shd);
+  double l = 0.0, c = 0.0, n = 0.0;
+  for (int i = threadIdx.x; i < R && row_loss; i += blockDim.x) {
+    l += row_loss[i];
+    c += row_stat[2 * i];
+    n += row_stat[2 * i + 1];
+  }
+  l = esp::block_sum<double>(l, shd);
+  c = esp::block_sum<double>(c, shd);
+  n = esp::block_sum<double>(n, shd);
+  if (threadIdx.x == 0) {
+    const float lc = nll ? (float)(a / B) : 0.f;
+    const float lat = row_loss ? (float)(l / denom) : 0.f;
+    out[0] = lc;
+    out[1] = lat;
+    out[2] = (n > 0) ? (float)(c / n) : 0.f;
+    if (!nll) out[3] = lat;
+    else if (!row_loss) out[3] = lc;
+    else out[3] = ctc_w * lc + (1.0f - ctc_w) * lat;
+  }
+}
+
+__global__ void argmax_kernel(const float* __restrict__ x, int64_t* __restrict__ out, long rows, int V) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + row * V;
+  float m = -INFINITY;
+  int am = 0x7fffffff;
+  for (int c = lane; c < V; c += 64) {
+    const float v = xr[c];
+    if (v > m || (v != v && m == m)) { m = v; am = c; }  // NaN propagates like torch.argmax
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const float om = __shfl_xor(m, o, 64);
+    const int oa = __shfl_xor(am, o, 64);
+    if (om > m || (om == m && oa < am)) { m = om; am = oa; }
+  }
+  if (lane == 0) out[row] = am == 0x7fffffff ? 0 : am;
+}
+
+// espnet1 forced_align, one block per sequence. lpz (T,V) fp32; y (U); out (T) labels;
+// path: (T, S) int32 workspace
+__global__ __launch_bounds__(1024) void forced_align_kernel(const float* __restrict__ lpz, int T, int V,
+                                                            const int64_t* __restrict__ y, int U, int blank,
+                                                            int* __restrict__ path, int64_t* __restrict__ out) {
+  const int S = 2 * U + 1;
+  __shared__ double dl[2][1025];
+  __shared__ int lab[1025];
+  for (int s = threadIdx.x; s < S; s += blockDim.x) lab[s] = (s & 1) ? (int)y[s >> 1] : blank;
+  __syncthreads();
+  for (int s = threadIdx.x; s < S; s += blockDim.x) {
+    double v = -100000000000.0;
+    if (s == 0) v = (double)lpz[lab[0]];
+    else if (s == 1) v = (double)lpz[lab[1]];
+    dl[0][s] = v;
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int t = 1; t < T; ++t) {
+    for (int s = threadIdx.x; s < S; s += blockDim.x) {
+      const int sm1 = s - 1 < 0 ? S - 1 : s - 1;  // python index -1 -> last state
+      const double c0 = dl[cur][s], c1 = dl[cur][sm1];
+      double best = c0;
+      int prev = s;
+      if (c1 > best) { best = c1; prev = s - 1; }
+      if (!(lab[s] == blank || s < 2 || lab[s] == lab[s - 2])) {
+        const double c2 = dl[cur][s - 2];
+        if (c2 > best) { best = c2; prev = s - 2; }
+      }
+      const float add = (float)best + lpz[(long)t * V + lab[s]];  // fp32, as the reference
+      dl[cur ^ 1][s] = (double)add;
+      path[(long)t * S + s] = prev;
+    }
+    cur ^= 1;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    int st = dl[cur][S - 2] > dl[cur][S - 1] ? S - 2 : S - 1;
+    out[T - 1] = lab[st];
+    for (int t = T - 2; t >= 0; --t) {
+      int idx = st < 0 ? st + S : st;
+      st = path[(long)(t + 1) * S + idx];
+      out[t] = lab[st < 0 ? st + S : st];
+    }
+  }
+}
+
+}  // namespace
+
+ESP_API int esp_log_softmax(const float* x, float* y, long rows, int V, void* stream) {
+  hipLaunchKernelGGL(log_softmax_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, x, y, V);
+  ESP_CHECK_LAUNCH("esp_log_softmax");
+  return 0;
+}
+
+// lp (B,T,V) log-probs; labels (B,Umax) int64; ilen/tlen int32 device arrays.
+// Outputs: nll (B); grad (B,T,V) = gscale * d nll_b / d logits (zeroed where infinite
+// when zero_infinity).  work: >= 2*B*T*Smax floats, Smax = 2*Umax+1 <= 1024.
+ESP_API int esp_ctc_loss(const float* lp, const long long* labels, int Umax, const int* ilen, const int* tlen, int B,
+                         int T, int V, int blank, float gscale, int zero_infinity, float* nll, float* grad, float* work,
+                         void* stream) {
+  const int Smax = 2 * Umax + 1;
+  ESP_ARG_CHECK(Smax <= CTC_NT * CTC_SPT, "esp_ctc_loss: 2*Umax+1=%d > %d", Smax, CTC_NT * CTC_SPT);
+  ESP_ARG_CHECK(V <= MAXV_LDS, "esp_ctc_loss: V=%d > %d", V, MAXV_LDS);
+  float* la = work;
+  float* lb = work + (long)B * T * Smax;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(ctc_alpha_beta_kernel, dim3(B, 2), dim3(CTC_NT), 0, st, lp, (const int64_t*)labels, Umax, ilen, tlen,
+                     T, V, Smax, blank, la, lb, nll);
+  if (grad)
+    hipLaunchKernelGGL(ctc_grad_kernel, dim3(T, B), dim3(256), 0, st, lp, (const int64_t*)labels, Umax, ilen, tlen, T, V,
+                       Smax, blank, la, lb, nll, gscale, zero_infinity, grad);
+  ESP_CHECK_LAUNCH("esp_ctc_loss");
+  return 0;
+}
+
+ESP_API int esp_label_smoothing(const float* x, const long long* target, long rows, int V, int ignore, float smoothing,
+                                float gscale, float* grad, float* row_loss, int* row_stat, void* stream) {
+  hipLaunchKernelGGL(ls_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, x, (const int64_t*)target, V,
+                     ignore, smoothing, gscale, grad, row_loss, row_stat);
+  ESP_CHECK_LAUNCH("esp_label_smoothing");
+  return 0;
+}
+
+ESP_API int esp_reduce_losses(const float* nll, int B, int zero_inf, const float* row_loss, const int* row_stat, int R,
+                              float denom, float ctc_w, float* out, void* stream) {
+  hipLaunchKernelGGL(reduce_losses_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, nll, B, zero_inf, row_loss,
+                     row_stat, R, denom, ctc_w, out);
+  ESP_CHECK_LAUNCH("esp_reduce_losses");
+  return 0;
+}
+
+ESP_API int esp_argmax(const float* x, long long* out, long rows, int V, void* stream) {
+  hipLaunchKernelGGL(argmax_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x,
+                     (int64_t*)out, rows, V);
+  ESP_CHECK_LAUNCH("esp_argmax");
+  return 0;
+}
+
+ESP_API int esp_ctc_forced_align(const float* lpz, int T, int V, const long long* y, int U, int blank, int* path,
+                                 long long* out, void* stream) {
+  ESP_ARG_CHECK(2 * U + 1 <= 1024 && U >= 1 && T >= 1, "esp_ctc_forced_align: bad sizes T=%d U=%d", T, U);
+  hipLaunchKernelGGL(forced_align_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, lpz, T, V, (const int64_t*)y, U,
+                     blank, path, (int64_t*)out);
+  ESP_CHECK_LAUNCH("esp_ctc_forced_align");
+  return 0;
+}

@@ -1,0 +1,328 @@
+"""Typed wrappers over the C ABI (include/espnet_mi355.h) for device torch tensors.
+
+torch is used only as the device allocator / stream provider: every arithmetic op below
+is a HIP kernel of libespnet_mi355.so launched on torch's current HIP stream.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Sequence
+
+import torch
+
+from . import _native
+
+KC, RC, I2C_KC, I2C_RC = 0, 1, 2, 3
+ACT_NONE, ACT_RELU, ACT_SWISH = 0, 1, 2
+
+
+def _p(t: Optional[torch.Tensor], off: int = 0):
+    if t is None:
+        return None
+    return t.data_ptr() + off * t.element_size()
+
+
+def _st():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _f32(*ts):
+    for t in ts:
+        if t is not None:
+            assert t.dtype == torch.float32 and t.is_cuda, (t.dtype, t.device)
+
+
+class _Workspace:
+    """Grow-only scratch buffer per device (stream-ordered reuse is safe)."""
+
+    def __init__(self):
+        self.buf = {}
+
+    def get(self, nbytes: int, device) -> torch.Tensor:
+        key = (str(device),)
+        b = self.buf.get(key)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+            self.buf[key] = b
+        return b
+
+    def reserve(self, nbytes: int, device):
+        self.get(nbytes, device)
+
+
+WS = _Workspace()
+_WS2 = _Workspace()
+
+
+def _work(nbytes, device):
+    return WS.get(nbytes, device)
+
+
+# ----------------------------------------------------------------------------- GEMM
+_PROF = None  # when a list: (algorithmic flops, start event, end event) per GEMM launch
+
+
+def profile_gemm_start():
+    """Record a HIP event pair around every GEMM launch (on the launch stream) from now on."""
+    global _PROF
+    _PROF = []
+
+
+def profile_gemm_stop():
+    """-> (total algorithmic FLOPs, total kernel ms, launches) since profile_gemm_start()."""
+    global _PROF
+    prof, _PROF = _PROF or [], None
+    torch.cuda.synchronize()
+    flops = sum(f for f, _, _ in prof)
+    ms = sum(a.elapsed_time(b) for _, a, b in prof)
+    return flops, ms, len(prof)
+
+
+def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc,
+         a_off=0, b_off=0, c_off=0, batch=1, nb2=1, sa=(0, 0), sb=(0, 0), sc=(0, 0),
+         bias=None, alpha=1.0, beta=0.0, R=None, r_off=None, act=ACT_NONE, aux=None,
+         drop_p=0.0, seed=0, ic_a: Optional[Sequence[int]] = None, ic_b: Optional[Sequence[int]] = None):
+    """C[z](m,n) = alpha*epi(sum_k A(m,k)B(k,n) + bias) + beta*R (see gemm.hip)."""
+    if R is not None and r_off is None:
+        r_off = c_off
+    ica = (_native.I * 5)(*ic_a) if ic_a is not None else None
+    icb = (_native.I * 5)(*ic_b) if ic_b is not None else None
+    if _PROF is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    _native.call("esp_gemm_f32", mode_a, mode_b, M, N, K, batch, nb2,
+                 _p(A, a_off), lda, sa[0], sa[1], _p(B, b_off), ldb, sb[0], sb[1],
+                 _p(C, c_off), ldc, sc[0], sc[1], _p(bias), float(alpha), float(beta),
+                 _p(R, r_off or 0), act, _p(aux, c_off) if aux is not None else None,
+                 float(drop_p), seed & 0xFFFFFFFFFFFFFFFF,
+                 ctypes_ptr(ica), ctypes_ptr(icb), _st())
+    if _PROF is not None:
+        ev1.record()
+        _PROF.append((2.0 * M * N * K * batch, ev0, ev1))
+
+
+def ctypes_ptr(arr):
+    import ctypes
+    return ctypes.cast(arr, ctypes.c_void_p) if arr is not None else None
+
+
+def linear_fwd(x2d, W, b, out, *, act=ACT_NONE, aux=None, drop_p=0.0, seed=0, alpha=1.0, R=None, beta=1.0,
+               out_off=0, ldo=None):
+    """out = alpha*drop(act(x W^T + b)) (+ beta*R); x (M,K), W (N,K)."""
+    M, K = x2d.shape
+    N = W.shape[0]
+    gemm(M, N, K, x2d, W, out, mode_a=KC, lda=x2d.stride(0), mode_b=KC, ldb=W.stride(0),
+         ldc=ldo or N, c_off=out_off, bias=b, alpha=alpha, beta=beta if R is not None else 0.0, R=R,
+         act=act, aux=aux, drop_p=drop_p, seed=seed)
+    return out
+
+
+def linear_bwd_data(dy, W, dx, *, accumulate=False):
+    """dx (+)= dy W ; dy (M,N), W (N,K)."""
+    M, N = dy.shape
+    K = W.shape[1]
+    gemm(M, K, N, dy, W, dx, mode_a=KC, lda=dy.stride(0), mode_b=RC, ldb=W.stride(0), ldc=dx.stride(0),
+         R=dx if accumulate else None, beta=1.0)
+    return dx
+
+
+def linear_bwd_weight(dy, x, dW, db=None):
+    """dW += dy^T x ; db += colsum(dy)."""
+    M, N = dy.shape
+    K = x.shape[1]
+    gemm(N, K, M, dy, x, dW, mode_a=RC, lda=dy.stride(0), mode_b=RC, ldb=x.stride(0), ldc=dW.stride(0),
+         R=dW, beta=1.0)
+    if db is not None:
+        colsum(dy, db, accumulate=True)
+
+
+def colsum(x2d, out, accumulate=True, M=None, N=None, ld=None):
+    M = M if M is not None else x2d.shape[0]
+    N = N if N is not None else x2d.shape[1]
+    ld = ld if ld is not None else x2d.stride(0)
+    nb = (M + 63) // 64
+    w = _work(4 * N * max(nb, 1), x2d.device)
+    _native.call("esp_colsum", _p(x2d), M, N, ld, _p(out), int(accumulate), _p(w), _st())
+
+
+# ----------------------------------------------------------------------------- elementwise
+def act_bwd(dy, h, dx, act, drop_p=0.0, seed=0, idx_off=0):
+    _native.call("esp_act_bwd", _p(dy), _p(h), _p(dx), dy.numel(), act, float(drop_p), seed, idx_off, _st())
+    return dx
+
+
+def scale_dropout(x, y, alpha=1.0, drop_p=0.0, seed=0, r=None, beta=1.0):
+    _native.call("esp_scale_dropout", _p(x), _p(y), x.numel(), float(alpha), float(drop_p), seed, _p(r),
+                 float(beta), _st())
+    return y
+
+
+def scale_by_dev(x, s):
+    _native.call("esp_scale_by_dev", _p(x), x.numel(), _p(s), _st())
+
+
+def embed_fwd(tok, E, pe, y, L, xscale, drop_p, seed):
+    _native.call("esp_embed_fwd", _p(tok), _p(E), _p(pe), _p(y), tok.numel(), L, E.shape[1], float(xscale),
+                 float(drop_p), seed, _st())
+
+
+def embed_bwd(tok, dy, dE, xscale, drop_p, seed):
+    _native.call("esp_embed_bwd", _p(tok), _p(dy), _p(dE), tok.numel(), dE.shape[0], dE.shape[1],
+                 float(xscale), float(drop_p), seed, _st())
+
+
+def specaug(x, y, lens_i32, warp_i32, fmask_i32, tmask_i32):
+    B, T, F = x.shape
+    nf = 0 if fmask_i32 is None else fmask_i32.shape[1]
+    nt = 0 if tmask_i32 is None else tmask_i32.shape[1]
+    _native.call("esp_specaug", _p(x), _p(y), B, T, F, _p(lens_i32), _p(warp_i32), _p(fmask_i32), nf,
+                 _p(tmask_i32), nt, _st())
+
+
+def utterance_mvn(x, lens_i32):
+    B, T, F = x.shape
+    _native.call("esp_utterance_mvn", _p(x), B, T, F, _p(lens_i32), _st())
+
+
+def grad_norm(g, max_norm, out3):
+    w = _WS2.get(8 * 1024, g.device)
+    _native.call("esp_grad_norm", _p(g), g.numel(), float(max_norm), _p(w), _p(out3), _st())
+
+
+def adam(p, g, m, v, clip3, lr, b1, b2, eps, wd, step):
+    _native.call("esp_adam", _p(p), _p(g), _p(m), _p(v), p.numel(), _p(clip3), float(lr), float(b1), float(b2),
+                 float(eps), float(wd), int(step), _st())
+
+
+# ----------------------------------------------------------------------------- norms
+def layernorm_fwd(x2d, w, b, y, mean, rstd, eps=1e-12):
+    M, D = x2d.shape
+    _native.call("esp_layernorm_fwd", _p(x2d), _p(w), _p(b), _p(y), _p(mean), _p(rstd), M, D, float(eps), _st())
+
+
+def layernorm_bwd(dy, x, w, mean, rstd, dx, dw, db, accumulate=False):
+    M, D = x.shape
+    nb = (M + 63) // 64
+    ws = _work(4 * 2 * D * max(nb, 1), x.device)
+    _native.call("esp_layernorm_bwd", _p(dy), _p(x), _p(w), _p(mean), _p(rstd), _p(dx), int(accumulate), _p(dw),
+                 _p(db), M, D, _p(ws), _st())
+
+
+def glu_fwd(u, g):
+    rows, D = g.shape
+    _native.call("esp_glu_fwd", _p(u), _p(g), rows, D, _st())
+
+
+def glu_bwd(u, dg, du):
+    rows, D = dg.shape
+    _native.call("esp_glu_bwd", _p(u), _p(dg), _p(du), rows, D, _st())
+
+
+def dwconv1d(x, W, bias, y, Bn, T, D, K, flip=False):
+    _native.call("esp_dwconv1d", _p(x), _p(W), _p(bias), _p(y), Bn, T, D, K, int(flip), _st())
+
+
+def dwconv1d_wgrad(dy, x, dW, Bn, T, D, K):
+    nch = (T + 63) // 64
+    ws = _work(4 * Bn * nch * D * K, x.device)
+    _native.call("esp_dwconv1d_wgrad", _p(dy), _p(x), _p(dW), Bn, T, D, K, _p(ws), _st())
+
+
+def bn_swish_fwd(y, gamma, beta, s, mean, rstd, run_mean, run_var, momentum=0.1, eps=1e-5):
+    M, D = y.shape
+    nb = (M + 63) // 64
+    ws = _work(8 * D * max(nb, 1), y.device)
+    _native.call("esp_bn_swish_fwd", _p(y), _p(gamma), _p(beta), _p(s), _p(mean), _p(rstd), _p(run_mean),
+                 _p(run_var), float(momentum), float(eps), M, D, _p(ws), _st())
+
+
+def bn_swish_bwd(ds, y, mean, rstd, gamma, beta, dy, dgamma, dbeta, sums):
+    M, D = y.shape
+    nb = (M + 63) // 64
+    ws = _work(8 * 2 * D * max(nb, 1), y.device)
+    _native.call("esp_bn_swish_bwd", _p(ds), _p(y), _p(mean), _p(rstd), _p(gamma), _p(beta), _p(dy), _p(dgamma),
+                 _p(dbeta), M, D, _p(ws), _p(sums), _st())
+
+
+# ----------------------------------------------------------------------------- attention
+def heads_split(src, ld, col0, B, T, H, dk, bias, dst):
+    _native.call("esp_heads_split", _p(src), ld, col0, B, T, H, dk, _p(bias), _p(dst), _st())
+
+
+def add2d(x, ldx, y, ldy, M, N, x_off=0, y_off=0):
+    _native.call("esp_add2d", _p(x, x_off), ldx, _p(y, y_off), ldy, M, N, _st())
+
+
+def attn_softmax_fwd(ac, bd, relpos, P, sqrt_dk, klen_i32, nb, causal, attn, pdrop, drop_p, seed, Z, Tq, Tk):
+    _native.call("esp_attn_softmax_fwd", _p(ac), _p(bd), relpos, P, float(sqrt_dk), _p(klen_i32), nb, int(causal),
+                 _p(attn), _p(pdrop), float(drop_p), seed, Z, Tq, Tk, _st())
+
+
+def attn_softmax_bwd(attn, dP, dS, drop_p, seed, sqrt_dk, rows, Tk):
+    _native.call("esp_attn_softmax_bwd", _p(attn), _p(dP), _p(dS), float(drop_p), seed, float(sqrt_dk), rows, Tk,
+                 _st())
+
+
+def relshift_bwd(dS, dbd, relpos, Z, T, P):
+    _native.call("esp_relshift_bwd", _p(dS), _p(dbd), relpos, Z, T, P, _st())
+
+
+# ----------------------------------------------------------------------------- subsampling
+def conv1_fwd(x, W, b, z, B, T, F, D):
+    _native.call("esp_conv1_fwd", _p(x), _p(W), _p(b), _p(z), B, T, F, D, _st())
+
+
+def col2im_relu(dcol, z1, dz1, B, T1, F1, D):
+    _native.call("esp_col2im_relu", _p(dcol), _p(z1), _p(dz1), B, T1, F1, D, _st())
+
+
+def conv1_wgrad(x, dz1, dW, db, B, T, F, D):
+    T1, F1 = (T - 3) // 2 + 1, (F - 3) // 2 + 1
+    nb = (B * T1 * F1 + 2047) // 2048
+    ws = _work(4 * nb * D * 10, x.device)
+    _native.call("esp_conv1_wgrad", _p(x), _p(dz1), _p(dW), _p(db), B, T, F, D, _p(ws), _st())
+
+
+def permute3(inp, out, O, Bd, Ad, accumulate=False):
+    _native.call("esp_permute3", _p(inp), _p(out), O, Bd, Ad, int(accumulate), _st())
+
+
+# ----------------------------------------------------------------------------- losses
+def log_softmax(x, y, rows, V):
+    _native.call("esp_log_softmax", _p(x), _p(y), rows, V, _st())
+
+
+def ctc_loss(lp, labels, Umax, ilen_i32, tlen_i32, B, T, V, blank, gscale, zero_infinity, nll, grad):
+    S = 2 * Umax + 1
+    ws = _work(4 * 2 * B * T * S, lp.device)
+    _native.call("esp_ctc_loss", _p(lp), _p(labels), Umax, _p(ilen_i32), _p(tlen_i32), B, T, V, blank,
+                 float(gscale), int(zero_infinity), _p(nll), _p(grad), _p(ws), _st())
+
+
+def label_smoothing(x, target, V, ignore, smoothing, gscale, grad, row_loss, row_stat):
+    _native.call("esp_label_smoothing", _p(x), _p(target), target.numel(), V, ignore, float(smoothing),
+                 float(gscale), _p(grad), _p(row_loss), _p(row_stat), _st())
+
+
+def reduce_losses(nll, B, zero_inf, row_loss, row_stat, R, denom, ctc_w, out4):
+    _native.call("esp_reduce_losses", _p(nll), B, int(zero_inf), _p(row_loss), _p(row_stat), R, float(denom),
+                 float(ctc_w), _p(out4), _st())
+
+
+def argmax(x, out, rows, V):
+    _native.call("esp_argmax", _p(x), _p(out), rows, V, _st())
+
+
+def ctc_forced_align(lpz, y, blank=0):
+    """espnet1 CTC.forced_align on device: lpz (T,V) fp32 log-probs, y (U,) int64 -> (T,) int64."""
+    T, V = lpz.shape
+    U = y.numel()
+    path = torch.empty(T * (2 * U + 1), dtype=torch.int32, device=lpz.device)
+    out = torch.empty(T, dtype=torch.int64, device=lpz.device)
+    _native.call("esp_ctc_forced_align", _p(lpz), T, V, _p(y), U, blank, _p(path), _p(out), _st())
+    return out
+
+
+def reserve_workspace(nbytes, device):
+    WS.reserve(nbytes, device)

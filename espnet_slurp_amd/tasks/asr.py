@@ -1,0 +1,75 @@
+"""ASRTask subset: the espnet2 plugin registries and build_model (espnet2/tasks/asr.py:83-188,
+439-562) so egs2/slurp* YAML `encoder:`/`decoder:`/`specaug:`/`normalize:`/`model_conf:`
+sections drop in unchanged.  `ClassChoices.get_class` keeps the reference's error
+behaviour (ValueError on unknown names, espnet2/train/class_choices.py:63-77)."""
+from __future__ import annotations
+
+import argparse
+from typing import Dict, Optional, Type
+
+import torch
+
+from ..asr.ctc import CTC
+from ..asr.decoder.transformer_decoder import TransformerDecoder
+from ..asr.encoder.conformer_encoder import ConformerEncoder
+from ..asr.encoder.transformer_encoder import TransformerEncoder
+from ..asr.espnet_model import ESPnetASRModel
+from ..asr.specaug.specaug import SpecAug
+from ..layers.utterance_mvn import UtteranceMVN
+
+
+class ClassChoices:
+    def __init__(self, name: str, classes: Dict[str, Type], type_check=None, default: Optional[str] = None,
+                 optional: bool = False):
+        self.name = name
+        self.base_type = type_check
+        self.classes = {k.lower(): v for k, v in classes.items()}
+        if "none" in self.classes or "nil" in self.classes or "null" in self.classes:
+            raise ValueError('"none", "nil", and "null" are reserved.')
+        self.default = default
+        self.optional = optional
+
+    def choices(self):
+        return list(self.classes) + (["none"] if self.optional else [])
+
+    def get_class(self, name: Optional[str]) -> Optional[type]:
+        if name is None or (self.optional and name.lower() in ("none", "null", "nil")):
+            return None
+        if name.lower() in self.classes:
+            return self.classes[name.lower()]
+        raise ValueError(f"--{self.name} must be one of {self.choices()}: --{self.name} {name.lower()}")
+
+
+specaug_choices = ClassChoices("specaug", dict(specaug=SpecAug), default=None, optional=True)
+normalize_choices = ClassChoices("normalize", dict(utterance_mvn=UtteranceMVN), default="utterance_mvn",
+                                 optional=True)
+model_choices = ClassChoices("model", dict(espnet=ESPnetASRModel), default="espnet")
+encoder_choices = ClassChoices("encoder", dict(conformer=ConformerEncoder, transformer=TransformerEncoder),
+                               default="rnn")
+decoder_choices = ClassChoices("decoder", dict(transformer=TransformerDecoder), default="rnn", optional=True)
+
+
+def build_model(args: argparse.Namespace, device="cuda") -> ESPnetASRModel:
+    """ASRTask.build_model (asr.py:439-562) for the fbank (--input_size) path.
+
+    args needs: token_list, input_size, specaug/_conf, normalize/_conf, encoder/_conf,
+    decoder/_conf, ctc_conf, model_conf (the resolved config.yaml fields)."""
+    token_list = list(args.token_list)
+    vocab_size = len(token_list)
+    input_size = args.input_size
+    specaug_cls = specaug_choices.get_class(getattr(args, "specaug", None))
+    specaug = specaug_cls(**(getattr(args, "specaug_conf", None) or {})) if specaug_cls else None
+    norm_cls = normalize_choices.get_class(getattr(args, "normalize", "utterance_mvn"))
+    normalize = norm_cls(**(getattr(args, "normalize_conf", None) or {})) if norm_cls else None
+    encoder = encoder_choices.get_class(args.encoder)(input_size=input_size, **(args.encoder_conf or {}))
+    dec_cls = decoder_choices.get_class(getattr(args, "decoder", None))
+    decoder = dec_cls(vocab_size=vocab_size, encoder_output_size=encoder.output_size(),
+                      **(getattr(args, "decoder_conf", None) or {})) if dec_cls else None
+    ctc = CTC(odim=vocab_size, encoder_output_size=encoder.output_size(), **(getattr(args, "ctc_conf", None) or {}))
+    model_cls = model_choices.get_class(getattr(args, "model", "espnet"))
+    model = model_cls(vocab_size=vocab_size, frontend=None, specaug=specaug, normalize=normalize, preencoder=None,
+                      encoder=encoder, postencoder=None, decoder=decoder, ctc=ctc, joint_network=None,
+                      token_list=token_list, **(getattr(args, "model_conf", None) or {}))
+    model = model.to(device)
+    model.flatten()
+    return model

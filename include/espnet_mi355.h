@@ -1,0 +1,125 @@
+/* espnet_mi355.h — C ABI of libespnet_mi355.so, the MI355X (gfx950) kernels behind
+ * espnet_slurp_amd's drop-in ESPnet2 ASR training step.
+ *
+ * Conventions (every entry point):
+ *   - plain device pointers (fp32 unless stated; int64 token ids as `long long`), sizes as int/long;
+ *   - row-major, the layouts documented per function;
+ *   - `stream` is a hipStream_t passed as void*; work is enqueued asynchronously, nothing syncs;
+ *   - return 0 on success, non-zero on a launch/argument error; esp_last_error() describes it
+ *     (thread-local).  No allocation happens inside: callers pass workspaces.
+ *
+ * Which reference interface each entry point replaces (BriansIDP/espnet_slurp, file:line):
+ *   the reference has no native code on this path; these functions replace
+ *   the ATen ops its Python building blocks call.  The reference-side "binding" is the espnet2
+ *   plugin registry (espnet2/tasks/asr.py:133-188); see INTEGRATION.md.
+ */
+#ifndef ESPNET_MI355_H
+#define ESPNET_MI355_H
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+const char* esp_last_error(void);
+int esp_abi_version(void);
+
+/* ---- MFMA GEMM (nn.Linear fwd/bwd, Conv1d k=1, Conv2d via implicit im2col, attention
+ * matmuls; attention.py:55-58,112,200-205, positionwise_feed_forward.py:32,
+ * convolution.py:70-77, subsampling.py:84-85).
+ *   C[z](m,n) = alpha*epi(sum_k A(m,k) B(k,n) + bias[n]) + beta*R[z](m,n)
+ *   mode 0 (KC): elem(r,k)=p[r*ld+k]   mode 1 (RC): elem(r,k)=p[k*ld+r]
+ *   mode 2/3: im2col of an NHWC map (3x3, stride 2); im2col_x = {H, W, C, Ho, Wo}
+ *   z = z1*nb2+z2 ; operand offset = z1*s1 + z2*s2
+ *   act: 0 none, 1 ReLU, 2 Swish (pre-activation stored to aux if non-NULL); dropout with
+ *   probability drop_p keyed by (seed, (z*M+m)*N+n). */
+int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2,
+                 const float* A, long lda, long sa1, long sa2,
+                 const float* B, long ldb, long sb1, long sb2,
+                 float* C, long ldc, long sc1, long sc2,
+                 const float* bias, float alpha, float beta, const float* R,
+                 int act, float* aux, float drop_p, unsigned long long seed,
+                 const int* im2col_a, const int* im2col_b, void* stream);
+
+/* ---- element-wise (positionwise_feed_forward.py:32, conformer/swish.py:13-18, dropout) */
+int esp_act_bwd(const float* dy, const float* h, float* dx, long n, int act, float drop_p,
+                unsigned long long seed, long idx_off, void* stream);
+int esp_scale_dropout(const float* x, float* y, long n, float alpha, float drop_p,
+                      unsigned long long seed, const float* r, float beta, void* stream);
+int esp_scale_by_dev(float* x, long n, const float* s, void* stream);
+/* decoder embedding + abs positional encoding (transformer_decoder.py:68-71, embedding.py:81-94) */
+int esp_embed_fwd(const long long* tok, const float* E, const float* pe, float* y, int nrows, int L,
+                  int D, float xscale, float drop_p, unsigned long long seed, void* stream);
+int esp_embed_bwd(const long long* tok, const float* dy, float* dE, int nrows, int V, int D,
+                  float xscale, float drop_p, unsigned long long seed, void* stream);
+/* SpecAug with injected draws (specaug.py:89-96, time_warp.py:9-88, mask_along_axis.py:8-68):
+ * lens (B) int32; warp (B,2) {center, warped} or NULL (center<=0: no warp for that row);
+ * fmask (B,nf,2) / tmask (B,nt,2) {pos, width}. */
+int esp_specaug(const float* x, float* y, int B, int T, int F, const int* lens, const int* warp,
+                const int* fmask, int nf, const int* tmask, int nt, void* stream);
+/* UtteranceMVN(norm_means=True, norm_vars=False), in place (utterance_mvn.py:45-80) */
+int esp_utterance_mvn(float* x, int B, int T, int F, const int* lens, void* stream);
+/* clip_grad_norm_ + Adam over flat buffers (trainer.py:642-686, abs_task.py:78-79) */
+int esp_grad_norm(const float* g, long n, float max_norm, double* work, float* out3, void* stream);
+int esp_adam(float* p, const float* g, float* m, float* v, long n, const float* clip3, float lr,
+             float b1, float b2, float eps, float wd, int step, void* stream);
+
+/* ---- normalisation (layer_norm.py:12-38; convolution.py:56-79) */
+int esp_layernorm_fwd(const float* x, const float* w, const float* b, float* y, float* mean,
+                      float* rstd, int M, int D, float eps, void* stream);
+int esp_layernorm_bwd(const float* dy, const float* x, const float* w, const float* mean,
+                      const float* rstd, float* dx, int accumulate, float* dw, float* db, int M,
+                      int D, float* work, void* stream);
+int esp_colsum(const float* x, int M, int N, long ld, float* out, int accumulate, float* work,
+               void* stream);
+int esp_glu_fwd(const float* u, float* g, long rows, int D, void* stream);
+int esp_glu_bwd(const float* u, const float* dg, float* du, long rows, int D, void* stream);
+int esp_dwconv1d(const float* x, const float* W, const float* bias, float* y, int Bn, int T, int D,
+                 int K, int flip, void* stream);
+int esp_dwconv1d_wgrad(const float* dy, const float* x, float* dW, int Bn, int T, int D, int K,
+                       float* work, void* stream);
+int esp_bn_swish_fwd(const float* y, const float* gamma, const float* beta, float* s, float* mean,
+                     float* rstd, float* run_mean, float* run_var, float momentum, float eps, int M,
+                     int D, double* work, void* stream);
+int esp_bn_swish_bwd(const float* ds, const float* y, const float* mean, const float* rstd,
+                     const float* gamma, const float* beta, float* dy, float* dgamma, float* dbeta,
+                     int M, int D, double* work, float* sums, void* stream);
+
+/* ---- attention glue (attention.py:64-96,145-165,240-263) */
+int esp_heads_split(const float* src, long ld, int col0, int B, int T, int H, int dk,
+                    const float* bias, float* dst, void* stream);
+int esp_add2d(const float* x, long ldx, float* y, long ldy, int M, int N, void* stream);
+int esp_attn_softmax_fwd(const float* ac, const float* bd, int relpos, int P, float sqrt_dk,
+                         const int* klen, int nb, int causal, float* attn, float* pdrop,
+                         float drop_p, unsigned long long seed, int Z, int Tq, int Tk, void* stream);
+int esp_attn_softmax_bwd(const float* attn, const float* dP, float* dS, float drop_p,
+                         unsigned long long seed, float sqrt_dk, long rows, int Tk, void* stream);
+int esp_relshift_bwd(const float* dS, float* dbd, int relpos, int Z, int T, int P, void* stream);
+
+/* ---- Conv2dSubsampling (subsampling.py:53-87), NHWC */
+int esp_conv1_fwd(const float* x, const float* W, const float* bias, float* z, int B, int T,
+                  int F, int D, void* stream);
+int esp_col2im_relu(const float* dcol, const float* z1, float* dz1, int B, int T1, int F1, int D,
+                    void* stream);
+int esp_conv1_wgrad(const float* x, const float* dz1, float* dW, float* db, int B, int T, int F,
+                    int D, float* work, void* stream);
+int esp_permute3(const float* in, float* out, int O, int Bd, int Ad, int accumulate, void* stream);
+
+/* ---- losses (ctc.py:39-97, label_smoothing_loss.py:41-63, nets_utils.py:299-320,
+ *      espnet/nets/pytorch_backend/ctc.py:185-249) */
+int esp_log_softmax(const float* x, float* y, long rows, int V, void* stream);
+int esp_ctc_loss(const float* lp, const long long* labels, int Umax, const int* ilen,
+                 const int* tlen, int B, int T, int V, int blank, float gscale, int zero_infinity,
+                 float* nll, float* grad, float* work, void* stream);
+int esp_label_smoothing(const float* x, const long long* target, long rows, int V, int ignore,
+                        float smoothing, float gscale, float* grad, float* row_loss, int* row_stat,
+                        void* stream);
+int esp_reduce_losses(const float* nll, int B, int zero_inf, const float* row_loss,
+                      const int* row_stat, int R, float denom, float ctc_w, float* out4,
+                      void* stream);
+int esp_argmax(const float* x, long long* out, long rows, int V, void* stream);
+int esp_ctc_forced_align(const float* lpz, int T, int V, const long long* y, int U, int blank,
+                         int* path, long long* out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,317 @@
+"""Generate golden fixtures by running the REFERENCE implementation (this container only).
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+Imports BriansIDP/espnet_slurp from /root/reference through `refshim`,
+builds the reference modules, loads the seeded parameters of
+`oracle.espnet_cpu.deterministic_params`, runs them on seeded synthetic inputs and
+stores inputs + outputs (+ gradients) as small .npz files next to this script.  The
+fixtures are DATA; the reference's code never travels with them.  Each fixture is also
+checked against the oracle restatement here, so a drift is caught at generation time.
+"""
+import math
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, HERE)
+
+import refshim  # noqa: E402
+
+refshim.install()
+
+from espnet2.asr.ctc import CTC  # noqa: E402
+from espnet2.asr.decoder.transformer_decoder import TransformerDecoder  # noqa: E402
+from espnet2.asr.encoder.conformer_encoder import ConformerEncoder  # noqa: E402
+from espnet2.asr.encoder.transformer_encoder import TransformerEncoder  # noqa: E402
+from espnet2.asr.espnet_model import ESPnetASRModel  # noqa: E402
+from espnet2.asr.specaug.specaug import SpecAug  # noqa: E402
+from espnet2.layers.utterance_mvn import UtteranceMVN  # noqa: E402
+from espnet2.schedulers.warmup_lr import WarmupLR  # noqa: E402
+from espnet2.layers.mask_along_axis import mask_along_axis  # noqa: E402
+from espnet2.layers.time_warp import time_warp  # noqa: E402
+from espnet.nets.pytorch_backend.ctc import CTC as CTC1  # noqa: E402
+
+from oracle import espnet_cpu as O  # noqa: E402
+from oracle import ctc_np  # noqa: E402
+
+torch.set_num_threads(8)
+
+
+def token_list(V):
+    return ["<blank>", "<unk>"] + [f"t{i}" for i in range(V - 3)] + ["<sos/eos>"]
+
+
+def build_reference(cfg: O.ModelCfg):
+    e = cfg.enc
+    if e.kind == "conformer":
+        enc = ConformerEncoder(
+            input_size=e.input_size, output_size=e.output_size, attention_heads=e.attention_heads,
+            linear_units=e.linear_units, num_blocks=e.num_blocks, dropout_rate=e.dropout_rate,
+            positional_dropout_rate=e.positional_dropout_rate,
+            attention_dropout_rate=e.attention_dropout_rate, input_layer="conv2d",
+            normalize_before=True, macaron_style=e.macaron_style, rel_pos_type=e.rel_pos_type,
+            pos_enc_layer_type="rel_pos", selfattention_layer_type="rel_selfattn",
+            activation_type="swish", use_cnn_module=e.use_cnn_module,
+            cnn_module_kernel=e.cnn_module_kernel)
+    else:
+        enc = TransformerEncoder(
+            input_size=e.input_size, output_size=e.output_size, attention_heads=e.attention_heads,
+            linear_units=e.linear_units, num_blocks=e.num_blocks, dropout_rate=e.dropout_rate,
+            positional_dropout_rate=e.positional_dropout_rate,
+            attention_dropout_rate=e.attention_dropout_rate, input_layer="conv2d")
+    dec = None
+    if cfg.dec is not None and cfg.ctc_weight != 1.0:
+        d = cfg.dec
+        dec = TransformerDecoder(
+            vocab_size=cfg.vocab_size, encoder_output_size=e.output_size,
+            attention_heads=d.attention_heads, linear_units=d.linear_units, num_blocks=d.num_blocks,
+            dropout_rate=d.dropout_rate, positional_dropout_rate=d.positional_dropout_rate,
+            self_attention_dropout_rate=d.self_attention_dropout_rate,
+            src_attention_dropout_rate=d.src_attention_dropout_rate)
+    ctc = CTC(odim=cfg.vocab_size, encoder_output_size=e.output_size)
+    model = ESPnetASRModel(
+        vocab_size=cfg.vocab_size, token_list=token_list(cfg.vocab_size), frontend=None,
+        specaug=None, normalize=UtteranceMVN(), preencoder=None, encoder=enc, postencoder=None,
+        decoder=dec, ctc=ctc, joint_network=None, ctc_weight=cfg.ctc_weight,
+        lsm_weight=cfg.lsm_weight, length_normalized_loss=cfg.length_normalized_loss,
+        report_cer=False, report_wer=False)
+    return model
+
+
+def load_params(model, cfg, seed, dtype=torch.float32):
+    P = O.deterministic_params(cfg, seed, dtype)
+    sd = model.state_dict()
+    assert set(sd.keys()) == set(P.keys()), (set(sd) ^ set(P))
+    for k in sd:
+        assert tuple(sd[k].shape) == tuple(P[k].shape), (k, sd[k].shape, P[k].shape)
+    model.load_state_dict(P)
+    return P
+
+
+def small_cfg(rel_pos_type="latest", D=64, blocks=2, V=32):
+    return O.ModelCfg(
+        vocab_size=V,
+        enc=O.EncCfg(output_size=D, attention_heads=4, linear_units=128, num_blocks=blocks,
+                     rel_pos_type=rel_pos_type),
+        dec=O.DecCfg(attention_heads=4, linear_units=128, num_blocks=2),
+        ctc_weight=0.3, lsm_weight=0.1)
+
+
+def model_fixture(name, cfg, B, T, lens, ulens, seed, with_grads=True, dtype=torch.float32):
+    model = build_reference(cfg).to(dtype)
+    load_params(model, cfg, seed, dtype)
+    model.train()
+    speech, slen, text, tlen = O.synthetic_batch(B, T, cfg.enc.input_size, cfg.vocab_size, lens, ulens, seed + 1)
+    speech = speech.to(dtype)
+    loss, stats, weight = model(speech.clone(), slen.clone(), text.clone(), tlen.clone())
+    loss.backward()
+    out = dict(speech=speech.float().numpy(), speech_lengths=slen.numpy(), text=text.numpy(),
+               text_lengths=tlen.numpy(), seed=np.int64(seed), loss=np.float64(loss.item()))
+    for k in ("loss_ctc", "loss_att"):
+        if stats.get(k) is not None:
+            out[k] = np.float64(stats[k].item())
+    if stats.get("acc") is not None:
+        out["acc"] = np.float64(stats["acc"])
+    sd = model.state_dict()
+    if with_grads:
+        for n, p in model.named_parameters():
+            out["grad/" + n] = p.grad.float().numpy()
+        for n, b in sd.items():
+            if "running" in n:
+                out["buf/" + n] = b.float().numpy()
+    else:
+        for n, p in model.named_parameters():
+            out["gradnorm/" + n] = np.float64(p.grad.double().norm().item())
+    # cross-check the oracle restatement against the reference right here
+    P = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k)
+         for k, v in O.deterministic_params(cfg, seed, dtype).items()}
+    bn = {}
+    oloss, ostats, _ = O.asr_forward(P, speech, slen, text, tlen, cfg, bn_state=bn)
+    oloss.backward()
+    err = abs(oloss.item() - loss.item())
+    gerr = max(float((P[n].grad - p.grad).abs().max()) for n, p in model.named_parameters())
+    if with_grads:
+        berr = max(float((bn[n] - b).abs().max()) for n, b in sd.items() if "running" in n)
+        assert berr < 1e-5, berr
+    print(f"{name}: ref loss {loss.item():.6f} oracle {oloss.item():.6f} |dl|={err:.2e} max|dg|={gerr:.2e}")
+    assert err < 1e-5 * max(1.0, abs(loss.item())), err
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+
+
+def ctc_fixture():
+    rng = np.random.Generator(np.random.PCG64(7))
+    T, B, V = 40, 4, 12
+    logits = (2.0 * rng.standard_normal((T, B, V))).astype(np.float32)
+    ilens = np.array([40, 33, 20, 5], dtype=np.int64)
+    tlens = np.array([10, 7, 6, 9], dtype=np.int64)    # utt 3 infeasible -> inf -> zero_infinity
+    targets = rng.integers(1, V, size=(B, 10)).astype(np.int64)
+    targets[1, 2] = targets[1, 1]                        # repeated label
+    targets[2, :6] = [3, 3, 3, 4, 4, 5]
+    ref = CTC(odim=V, encoder_output_size=V)
+    th = torch.from_numpy(logits).requires_grad_(True)
+    ys_true = torch.cat([torch.from_numpy(targets[i, :l]) for i, l in enumerate(tlens)])
+    loss = ref.loss_fn(th, ys_true, torch.from_numpy(ilens), torch.from_numpy(tlens))
+    loss.backward()
+    per = torch.nn.functional.ctc_loss(torch.from_numpy(logits).log_softmax(2), ys_true,
+                                       torch.from_numpy(ilens), torch.from_numpy(tlens),
+                                       reduction="none", zero_infinity=True)
+    nll, g = ctc_np.ctc_loss_np(logits, ilens, targets, tlens)
+    print("ctc: ref", per.numpy(), "np", nll, "max|dgrad|", np.abs(g / B - th.grad.numpy()).max())
+    np.savez_compressed(os.path.join(HERE, "ctc.npz"), logits=logits, ilens=ilens, tlens=tlens,
+                        targets=targets, nll=per.double().numpy(), loss=np.float64(loss.item()),
+                        grad=th.grad.numpy())
+
+
+def align_fixture():
+    rng = np.random.Generator(np.random.PCG64(11))
+    V = 10
+    ctc1 = CTC1(odim=V, eprojs=V, dropout_rate=0.0)
+    with torch.no_grad():
+        ctc1.ctc_lo.weight.copy_(torch.eye(V))
+        ctc1.ctc_lo.bias.zero_()
+    cases = {}
+    for ci, (T, U, peaked) in enumerate([(30, 6, True), (25, 8, False), (12, 5, False), (40, 3, True)]):
+        y = rng.integers(1, V, size=U).astype(np.int64)
+        if ci == 2:
+            y[1] = y[0]
+        h = rng.standard_normal((T, V)).astype(np.float32)
+        if peaked:   # a plausible trained-model shape: a monotone path dominates
+            pos = np.sort(rng.choice(np.arange(1, T - 1), size=U, replace=False))
+            h[:, 0] += 3.0
+            for u, p in enumerate(pos):
+                h[p, y[u]] += 6.0
+        with torch.no_grad():
+            ali = ctc1.forced_align(torch.from_numpy(h)[None], torch.from_numpy(y), blank_id=0)
+            lpz = ctc1.log_softmax(torch.from_numpy(h)[None])[0].numpy()
+        ali = np.array([int(a) for a in ali], dtype=np.int64)
+        mine = np.array(ctc_np.forced_align_np(lpz, y), dtype=np.int64)
+        assert (mine == ali).all(), (ci, mine, ali)
+        cases[f"h{ci}"] = h
+        cases[f"lpz{ci}"] = lpz
+        cases[f"y{ci}"] = y
+        cases[f"ali{ci}"] = ali
+        cases[f"argmax{ci}"] = torch.argmax(torch.from_numpy(h), dim=-1).numpy()
+    print("align: ok", {k: v.tolist() for k, v in cases.items() if k.startswith("ali")})
+    np.savez_compressed(os.path.join(HERE, "align.npz"), **cases)
+
+
+def specaug_fixture():
+    B, T, F_ = 2, 100, 80
+    rng = np.random.Generator(np.random.PCG64(5))
+    x = rng.standard_normal((B, T, F_)).astype(np.float32)
+    out = dict(x=x)
+    # time warp (window 5, bicubic): replicate the reference's two torch.randint draws
+    for s in (3, 4):
+        torch.manual_seed(s)
+        y = time_warp(torch.from_numpy(x).clone(), window=5, mode="bicubic")
+        torch.manual_seed(s)
+        center = int(torch.randint(5, T - 5, (1,))[0])
+        warped = int(torch.randint(center - 5, center + 5, (1,))[0] + 1)
+        mine = O.time_warp_fixed(torch.from_numpy(x), center, warped)
+        assert torch.allclose(mine, y, atol=1e-6), float((mine - y).abs().max())
+        out[f"tw{s}_center"] = np.int64(center)
+        out[f"tw{s}_warped"] = np.int64(warped)
+        out[f"tw{s}_y"] = y.numpy()
+    for dim, rng_w, key in ((2, (0, 30), "freq"), (1, (0, 40), "time")):
+        torch.manual_seed(9)
+        y, _ = mask_along_axis(torch.from_numpy(x).clone(), None, rng_w, dim, 2)
+        torch.manual_seed(9)
+        ml = torch.randint(rng_w[0], rng_w[1], (B, 2))
+        mp = torch.randint(0, max(1, x.shape[dim] - int(ml.max())), (B, 2))
+        mine = O.mask_along_axis_fixed(torch.from_numpy(x), mp, ml, dim)
+        assert torch.equal(mine, y)
+        out[f"{key}_pos"] = mp.numpy()
+        out[f"{key}_len"] = ml.numpy()
+        out[f"{key}_y"] = y.numpy()
+    lens = torch.tensor([100, 71])
+    xm = torch.from_numpy(x).clone()
+    xm[1, 71:] = 0
+    y, _ = UtteranceMVN()(xm.clone(), lens)
+    assert torch.allclose(O.utterance_mvn(xm, lens), y)
+    out["mvn_x"] = xm.numpy()
+    out["mvn_lens"] = lens.numpy()
+    out["mvn_y"] = y.numpy()
+    # whole SpecAug module under a fixed seed, for the full-module shape contract
+    sa = SpecAug(apply_time_warp=True, time_warp_window=5, time_warp_mode="bicubic",
+                 freq_mask_width_range=(0, 30), num_freq_mask=2,
+                 time_mask_width_range=(0, 40), num_time_mask=2)
+    torch.manual_seed(21)
+    y, _ = sa(torch.from_numpy(x).clone(), torch.tensor([T, T]))
+    out["specaug_seed21_y"] = y.numpy()
+    print("specaug: ok")
+    np.savez_compressed(os.path.join(HERE, "specaug.npz"), **out)
+
+
+def train_step_fixture():
+    """Two reference optimizer steps: clip_grad_norm_(5) + Adam + WarmupLR (trainer.py:642-686)."""
+    cfg = small_cfg("latest", D=32, blocks=1, V=16)
+    model = build_reference(cfg)
+    load_params(model, cfg, 3)
+    model.train()
+    opt = torch.optim.Adam(model.parameters(), lr=0.002, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-6)
+    sch = WarmupLR(opt, warmup_steps=10)
+    out = {}
+    for step in range(2):
+        speech, slen, text, tlen = O.synthetic_batch(2, 64, 80, cfg.vocab_size, [64, 50], [5, 3], 100 + step)
+        loss, stats, weight = model(speech, slen, text, tlen)
+        loss.backward()
+        gn = torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=5.0, norm_type=2.0)
+        out[f"loss{step}"] = np.float64(loss.item())
+        out[f"gradnorm{step}"] = np.float64(gn.item())
+        out[f"lr{step}"] = np.float64(opt.param_groups[0]["lr"])
+        opt.step()
+        sch.step()
+        opt.zero_grad()
+    for n, p in model.named_parameters():
+        out["param/" + n] = p.detach().numpy()
+    print("train_step: losses", out["loss0"], out["loss1"], "gn", out["gradnorm0"], out["gradnorm1"])
+    np.savez_compressed(os.path.join(HERE, "train_step.npz"), **out)
+
+
+def fullsize_fixture():
+    """C2 shape (d=256, 12L, T=1500, B=2): fp32 vs fp64 reference loss (SURVEY.md §0.4 gate)."""
+    cfg = O.ModelCfg(vocab_size=600, enc=O.EncCfg(output_size=256, attention_heads=4, linear_units=1024,
+                                                   num_blocks=12, rel_pos_type="latest"),
+                     dec=O.DecCfg(attention_heads=4, linear_units=2048, num_blocks=6))
+    out = {}
+    for dt, tag in ((torch.float32, "f32"), (torch.float64, "f64")):
+        model = build_reference(cfg).to(dt)
+        load_params(model, cfg, 42, dt)
+        model.train()
+        speech, slen, text, tlen = O.synthetic_batch(2, 1500, 80, 600, [1500, 1337], [40, 27], 43)
+        with torch.no_grad():
+            loss, stats, _ = model(speech.to(dt), slen, text, tlen)
+        out[f"loss_{tag}"] = np.float64(loss.item())
+        out[f"loss_ctc_{tag}"] = np.float64(stats["loss_ctc"].item())
+        out[f"loss_att_{tag}"] = np.float64(stats["loss_att"].item())
+        print("fullsize", tag, loss.item())
+    out.update(lens=np.array([1500, 1337]), ulens=np.array([40, 27]), seed=np.int64(42))
+    np.savez_compressed(os.path.join(HERE, "fullsize_c2.npz"), **out)
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["ctc", "align", "specaug", "small", "c1", "train", "full"]
+    if "ctc" in which:
+        ctc_fixture()
+    if "align" in which:
+        align_fixture()
+    if "specaug" in which:
+        specaug_fixture()
+    if "small" in which:
+        model_fixture("model_small_latest", small_cfg("latest"), 3, 120, [120, 97, 64], [9, 5, 7], 1)
+        model_fixture("model_small_legacy", small_cfg("legacy"), 3, 120, [120, 97, 64], [9, 5, 7], 2)
+    if "c1" in which:
+        c1 = O.ModelCfg(vocab_size=30, enc=O.EncCfg(kind="transformer", output_size=256, attention_heads=4,
+                                                     linear_units=1024, num_blocks=4),
+                        dec=None, ctc_weight=1.0)
+        model_fixture("model_c1_transformer_ctc", c1, 2, 200, [200, 173], [10, 7], 5, with_grads=False)
+    if "train" in which:
+        train_step_fixture()
+    if "full" in which:
+        fullsize_fixture()

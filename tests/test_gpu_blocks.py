@@ -1,0 +1,108 @@
+"""Block-level parity (GPU vs the oracle restatement in fp64 with autograd): the relative-
+position MHA (latest and legacy), the convolution module and the subsampling stack, each
+forward + explicit backward, with padding masks."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from espnet_slurp_amd.blocks import ConvolutionModule, Conv2dSubsampling, RelPositionMultiHeadedAttention, Seeds
+from espnet_slurp_amd.asr.encoder.abs_encoder import pos_table
+from espnet_slurp_amd.flat import FlatParams
+from oracle import espnet_cpu as O
+from tests.helpers import rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _check_grads(mod, P, prefix, tol=2e-5):
+    """Per-tensor relative error; tensors whose exact gradient is 0 (softmax-invariant key
+    bias, BN-fed conv bias) are compared against the block's gradient scale instead."""
+    scale = max(float(P[prefix + "." + n].grad.abs().max()) for n, _ in mod.named_parameters())
+    errs = {}
+    for n, p in mod.named_parameters():
+        ref = P[prefix + "." + n].grad
+        if float(ref.abs().max()) < 1e-6 * scale:
+            assert float(p.grad.abs().max()) < 1e-5 * scale, n
+            continue
+        errs[n] = rel_err(p.grad.cpu(), ref)
+    print(sorted(errs.items(), key=lambda kv: kv[1])[-4:])
+    bad = {n: e for n, e in errs.items() if e >= tol}
+    assert not bad, bad
+
+
+def _params64(mod, prefix):
+    return {prefix + "." + k: v.detach().cpu().double().clone().requires_grad_(True) for k, v in mod.named_parameters()}
+
+
+@pytest.mark.parametrize("legacy", [False, True])
+def test_relpos_mha_block(dev, legacy):
+    torch.manual_seed(0)
+    B, T, D, H = 3, 29, 64, 4
+    klen = torch.tensor([29, 23, 15])
+    mod = RelPositionMultiHeadedAttention(H, D, 0.0, legacy).to(dev)
+    with torch.no_grad():
+        for p in mod.parameters():
+            p.normal_(0, 0.2)
+    flat = FlatParams(mod, dev)
+    mod.flat = flat
+    x = torch.randn(B * T, D)
+    res = torch.randn(B * T, D)
+    dout = torch.randn(B * T, D)
+    pos = pos_table("legacy" if legacy else "latest", T, D, dev)
+    out, c = mod.fwd(x.to(dev), res.to(dev), pos, klen.int().to(dev), B, T, 0.0, Seeds(1), True)
+    dx = mod.bwd(c, dout.to(dev))
+    P = _params64(mod, "a")
+    xt = x.double().view(B, T, D).requires_grad_(True)
+    mask = (~O.make_pad_mask(klen, T))[:, None, :]
+    ref = O.rel_mha(P, "a", xt, pos.cpu().double()[None], mask, H, legacy) + res.double().view(B, T, D)
+    ref.backward(dout.double().view(B, T, D))
+    assert rel_err(out.cpu(), ref.detach().view(B * T, D)) < 1e-5
+    assert rel_err(dx.cpu(), xt.grad.view(B * T, D)) < 1e-5
+    _check_grads(mod, P, "a")
+
+
+def test_conv_module_block(dev):
+    torch.manual_seed(1)
+    B, T, D = 3, 29, 64
+    mod = ConvolutionModule(D, 31).to(dev)
+    with torch.no_grad():
+        for p in mod.parameters():
+            p.normal_(0, 0.2)
+    flat = FlatParams(mod, dev)
+    x = torch.randn(B * T, D)
+    res = torch.randn(B * T, D)
+    dout = torch.randn(B * T, D)
+    out, c = mod.fwd(x.to(dev), res.to(dev), B, T, 0.0, Seeds(2), True)
+    dx = mod.bwd(c, dout.to(dev))
+    P = _params64(mod, "m")
+    P["m.norm.running_mean"] = torch.zeros(D, dtype=torch.double)
+    P["m.norm.running_var"] = torch.ones(D, dtype=torch.double)
+    xt = x.double().view(B, T, D).requires_grad_(True)
+    ref = O.conv_module(P, "m", xt, 31) + res.double().view(B, T, D)
+    ref.backward(dout.double().view(B, T, D))
+    assert rel_err(out.cpu(), ref.detach().view(B * T, D)) < 1e-5
+    assert rel_err(dx.cpu(), xt.grad.view(B * T, D)) < 1e-5
+    _check_grads(mod, P, "m")
+
+
+def test_subsampling_block(dev):
+    torch.manual_seed(2)
+    B, T, F, D = 2, 64, 80, 32
+    mod = Conv2dSubsampling(F, D).to(dev)
+    with torch.no_grad():
+        for p in mod.parameters():
+            p.normal_(0, 0.1)
+    flat = FlatParams(mod, dev)
+    x = torch.randn(B, T, F)
+    out, c = mod.fwd(x.to(dev), math.sqrt(D), 0.0, Seeds(3), True)
+    T2 = c.T2
+    dout = torch.randn(B * T2, D)
+    mod.bwd(c, dout.to(dev))
+    P = _params64(mod, "e")
+    y, _ = O.conv2d_subsampling(P, "e", x.double(), torch.ones(B, 1, T, dtype=torch.bool))
+    y = y * math.sqrt(D)
+    y.backward(dout.double().view(B, T2, D))
+    assert rel_err(out.cpu(), y.detach().reshape(B * T2, D)) < 1e-5
+    _check_grads(mod, P, "e")

@@ -1,0 +1,368 @@
+"""Kernel-level numerics on the MI355X: every HIP kernel against a plain PyTorch fp32/fp64 CPU
+reference of the same op (or the oracle / golden fixtures)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from espnet_slurp_amd import kernels as K
+from oracle import ctc_np
+from oracle import espnet_cpu as O
+from tests.helpers import golden, rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _r(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g) * scale
+
+
+def _gemm_ref(A, B, ma, mb):
+    A = A.double()
+    B = B.double()
+    a = A if ma == K.KC else A.t()
+    b = B.t() if mb == K.KC else B
+    return a @ b
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 1), (37, 53, 19), (128, 128, 16), (300, 260, 129), (1000, 96, 512),
+                                   (130, 7, 3)])
+@pytest.mark.parametrize("modes", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_gemm_modes(dev, shape, modes):
+    M, N, Kk = shape
+    ma, mb = modes
+    A = _r(M, Kk, seed=1) if ma == K.KC else _r(Kk, M, seed=1)
+    B = _r(N, Kk, seed=2) if mb == K.KC else _r(Kk, N, seed=2)
+    C = torch.empty(M, N, device=dev)
+    Ad, Bd = A.to(dev), B.to(dev)
+    K.gemm(M, N, Kk, Ad, Bd, C, mode_a=ma, lda=Ad.stride(0), mode_b=mb, ldb=Bd.stride(0), ldc=N)
+    ref = _gemm_ref(A, B, ma, mb)
+    torch.cuda.synchronize()
+    err = (C.cpu().double() - ref).abs().max().item()
+    assert err <= 1e-5 * max(1.0, math.sqrt(Kk)) * 4, err
+
+
+def test_gemm_epilogue(dev):
+    M, N, Kk = 257, 130, 64
+    X, W, b = _r(M, Kk, seed=3), _r(N, Kk, seed=4), _r(N, seed=5)
+    R = _r(M, N, seed=6)
+    Xd, Wd, bd, Rd = X.to(dev), W.to(dev), b.to(dev), R.to(dev)
+    out = torch.empty(M, N, device=dev)
+    aux = torch.empty(M, N, device=dev)
+    K.linear_fwd(Xd, Wd, bd, out, act=K.ACT_SWISH, aux=aux, alpha=0.5, R=Rd, beta=1.0)
+    pre = X.double() @ W.double().t() + b.double()
+    ref = 0.5 * pre * torch.sigmoid(pre) + R.double()
+    assert (aux.cpu().double() - pre).abs().max() < 1e-4
+    assert (out.cpu().double() - ref).abs().max() < 1e-4
+    # relu + dropout: deterministic in (seed, index), keep rate ~ 1-p, scale 1/(1-p)
+    o1 = torch.empty(M, N, device=dev)
+    o2 = torch.empty(M, N, device=dev)
+    K.linear_fwd(Xd, Wd, bd, o1, act=K.ACT_RELU, drop_p=0.25, seed=1234)
+    K.linear_fwd(Xd, Wd, bd, o2, act=K.ACT_RELU, drop_p=0.25, seed=1234)
+    assert torch.equal(o1, o2)
+    relu = torch.relu(pre).float()
+    o1c = o1.cpu()
+    kept = o1c != 0
+    pos = relu > 0
+    frac = (kept & pos).sum().item() / pos.sum().item()
+    assert abs(frac - 0.75) < 0.02, frac
+    assert torch.allclose(o1c[kept], relu[kept] / 0.75, atol=1e-4)
+    # the element-wise backward regenerates the same mask
+    g = torch.ones(M, N, device=dev)
+    dx = torch.empty(M, N, device=dev)
+    K.act_bwd(g, aux, dx, K.ACT_NONE, drop_p=0.25, seed=1234)
+    assert torch.equal((dx.cpu() != 0) & pos, o1c != 0)
+
+
+def test_gemm_batched_strided(dev):
+    # attention-style (head, batch) strides: q (B*T, 3D) read per (h,b)
+    B, T, H, dk = 3, 50, 4, 16
+    D = H * dk
+    qkv = _r(B * T, 3 * D, seed=7)
+    qd = qkv.to(dev)
+    S = torch.empty(H * B * T * T, device=dev)
+    K.gemm(T, T, dk, qd, qd, S, mode_a=K.KC, lda=3 * D, mode_b=K.KC, ldb=3 * D, ldc=T, b_off=D,
+           batch=H * B, nb2=B, sa=(dk, T * 3 * D), sb=(dk, T * 3 * D), sc=(B * T * T, T * T))
+    q = qkv[:, :D].view(B, T, H, dk).permute(2, 0, 1, 3).double()
+    k = qkv[:, D:2 * D].view(B, T, H, dk).permute(2, 0, 1, 3).double()
+    ref = q @ k.transpose(-1, -2)
+    assert (S.cpu().view(H, B, T, T).double() - ref).abs().max() < 1e-4
+
+
+def test_gemm_im2col_conv(dev):
+    Bn, T1, F1, C = 2, 21, 13, 8
+    x = _r(Bn, C, T1, F1, seed=8)
+    w = _r(C, C, 3, 3, seed=9)
+    b = _r(C, seed=10)
+    ref = F.relu(F.conv2d(x.double(), w.double(), b.double(), stride=2))  # (Bn, C, T2, F2)
+    T2, F2 = ref.shape[2], ref.shape[3]
+    z1 = x.permute(0, 2, 3, 1).contiguous().to(dev)  # NHWC
+    w2r = w.permute(0, 2, 3, 1).contiguous().to(dev)  # (o, kt, kf, c)
+    out = torch.empty(Bn * T2 * F2, C, device=dev)
+    K.gemm(Bn * T2 * F2, C, 9 * C, z1, w2r, out, mode_a=K.I2C_KC, lda=0, mode_b=K.KC, ldb=9 * C, ldc=C,
+           bias=b.to(dev), act=K.ACT_RELU, ic_a=(T1, F1, C, T2, F2))
+    got = out.cpu().view(Bn, T2, F2, C).permute(0, 3, 1, 2).double()
+    assert (got - ref).abs().max() < 1e-4
+    # weight-gradient form: dW[o, kk] = sum_pix g[pix, o] * col[pix, kk]
+    g = _r(Bn * T2 * F2, C, seed=11)
+    dw = torch.empty(C, 9 * C, device=dev)
+    K.gemm(C, 9 * C, Bn * T2 * F2, g.to(dev), z1, dw, mode_a=K.RC, lda=C, mode_b=K.I2C_RC, ldb=0, ldc=9 * C,
+           ic_b=(T1, F1, C, T2, F2))
+    cols = F.unfold(x.double(), 3, stride=2)  # (Bn, C*9, L) ordered (c, kt, kf)
+    cols = cols.view(Bn, C, 3, 3, -1).permute(0, 4, 2, 3, 1).reshape(Bn * T2 * F2, 9 * C)
+    ref_dw = g.double().t() @ cols
+    assert (dw.cpu().double() - ref_dw).abs().max() < 1e-3
+
+
+def test_layernorm(dev):
+    M, D = 333, 256
+    x = _r(M, D, seed=12, scale=3.0) + 1.5
+    w = _r(D, seed=13) * 0.1 + 1.0
+    b = _r(D, seed=14) * 0.1
+    dy = _r(M, D, seed=15)
+    xt = x.double().requires_grad_(True)
+    wt = w.double().requires_grad_(True)
+    bt = b.double().requires_grad_(True)
+    y = F.layer_norm(xt, (D,), wt, bt, 1e-12)
+    y.backward(dy.double())
+    xd, wd, bd = x.to(dev), w.to(dev), b.to(dev)
+    yd = torch.empty(M, D, device=dev)
+    mean = torch.empty(M, device=dev)
+    rstd = torch.empty(M, device=dev)
+    K.layernorm_fwd(xd, wd, bd, yd, mean, rstd)
+    dx = torch.zeros(M, D, device=dev)
+    dw = torch.zeros(D, device=dev)
+    db = torch.zeros(D, device=dev)
+    K.layernorm_bwd(dy.to(dev), xd, wd, mean, rstd, dx, dw, db)
+    assert rel_err(yd.cpu(), y.detach()) < 1e-5
+    assert rel_err(dx.cpu(), xt.grad) < 1e-5
+    assert rel_err(dw.cpu(), wt.grad) < 1e-5
+    assert rel_err(db.cpu(), bt.grad) < 1e-5
+
+
+def test_conv_module_pieces(dev):
+    Bn, T, D, Kk = 3, 57, 64, 31
+    u = _r(Bn * T, 2 * D, seed=16)
+    W = _r(D, 1, Kk, seed=17) * 0.2
+    bw = _r(D, seed=18)
+    gam = _r(D, seed=19) * 0.1 + 1
+    bet = _r(D, seed=20) * 0.1
+    ds = _r(Bn * T, D, seed=21)
+    ut = u.double().requires_grad_(True)
+    Wt = W.double().requires_grad_(True)
+    bwt = bw.double().requires_grad_(True)
+    gt = gam.double().requires_grad_(True)
+    bt = bet.double().requires_grad_(True)
+    g = F.glu(ut.view(Bn, T, 2 * D).transpose(1, 2), dim=1)
+    y = F.conv1d(g, Wt, bwt, padding=15, groups=D)
+    rm, rv = torch.zeros(D, dtype=torch.double), torch.ones(D, dtype=torch.double)
+    z = F.batch_norm(y, rm, rv, gt, bt, training=True, momentum=0.1, eps=1e-5)
+    s = z * torch.sigmoid(z)
+    s.backward(ds.double().view(Bn, T, D).transpose(1, 2))
+    ud = u.to(dev)
+    gd = torch.empty(Bn * T, D, device=dev)
+    K.glu_fwd(ud, gd)
+    yd = torch.empty(Bn * T, D, device=dev)
+    K.dwconv1d(gd, W.to(dev), bw.to(dev), yd, Bn, T, D, Kk)
+    sd = torch.empty(Bn * T, D, device=dev)
+    mean, rstd = torch.empty(D, device=dev), torch.empty(D, device=dev)
+    rmd, rvd = torch.zeros(D, device=dev), torch.ones(D, device=dev)
+    K.bn_swish_fwd(yd, gam.to(dev), bet.to(dev), sd, mean, rstd, rmd, rvd)
+    assert rel_err(sd.cpu(), s.detach().transpose(1, 2).reshape(Bn * T, D)) < 1e-5
+    assert rel_err(rmd.cpu(), rm) < 1e-5 and rel_err(rvd.cpu(), rv) < 1e-5
+    dy = torch.empty(Bn * T, D, device=dev)
+    dgam, dbet = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
+    sums = torch.empty(2 * D, device=dev)
+    K.bn_swish_bwd(ds.to(dev), yd, mean, rstd, gam.to(dev), bet.to(dev), dy, dgam, dbet, sums)
+    assert rel_err(dgam.cpu(), gt.grad) < 1e-5 and rel_err(dbet.cpu(), bt.grad) < 1e-5
+    dW = torch.zeros(D, 1, Kk, device=dev)
+    K.dwconv1d_wgrad(dy, gd, dW, Bn, T, D, Kk)
+    dbw = torch.zeros(D, device=dev)
+    K.colsum(dy, dbw)
+    assert rel_err(dW.cpu(), Wt.grad) < 1e-5
+    # the depthwise bias feeds a training-mode BatchNorm, so its true gradient is exactly 0:
+    # both sides are rounding noise; bound it absolutely (scale of the summed terms)
+    assert dbw.abs().max().item() < 1e-5 * dy.abs().sum(0).max().item() + 1e-6
+    dg = torch.empty(Bn * T, D, device=dev)
+    K.dwconv1d(dy, W.to(dev), None, dg, Bn, T, D, Kk, flip=True)
+    du = torch.empty(Bn * T, 2 * D, device=dev)
+    K.glu_bwd(ud, dg, du)
+    assert rel_err(du.cpu(), ut.grad) < 1e-5
+
+
+@pytest.mark.parametrize("legacy", [False, True])
+def test_relpos_softmax_and_adjoint(dev, legacy):
+    Z, T, dk, nb = 6, 45, 16, 3
+    P = T if legacy else 2 * T - 1
+    ac = _r(Z, T, T, seed=22)
+    bd = _r(Z, T, P, seed=23)
+    klen = torch.tensor([45, 30, 7], dtype=torch.int32)
+    act = ac.double().requires_grad_(True)
+    bdt = bd.double().requires_grad_(True)
+    sh = O.rel_shift_legacy(bdt.view(1, Z, T, P))[0] if legacy else O.rel_shift_latest(bdt.view(1, Z, T, P))[0]
+    sc = (act + sh) / math.sqrt(dk)
+    mask = (torch.arange(T)[None, :] < klen.long()[torch.arange(Z) % nb][:, None])[:, None, :]  # (Z,1,T)
+    minv = float(np.finfo(np.float64).min)
+    attn = torch.softmax(sc.masked_fill(~mask, minv), -1).masked_fill(~mask, 0.0)
+    dP = _r(Z, T, T, seed=24)
+    attn.backward(dP.double())
+    acd = ac.to(dev).contiguous()
+    att = torch.empty(Z * T * T, device=dev)
+    K.attn_softmax_fwd(acd, bd.to(dev), 2 if legacy else 1, P, math.sqrt(dk), klen.to(dev), nb, False, att, None,
+                       0.0, 0, Z, T, T)
+    assert rel_err(att.cpu().view(Z, T, T), attn.detach()) < 1e-5
+    dS = dP.to(dev).contiguous()
+    K.attn_softmax_bwd(att, dS, dS, 0.0, 0, math.sqrt(dk), Z * T, T)
+    assert rel_err(dS.cpu().view(Z, T, T), act.grad) < 1e-5
+    dbd = torch.empty(Z * T * P, device=dev)
+    K.relshift_bwd(dS, dbd, 2 if legacy else 1, Z, T, P)
+    assert rel_err(dbd.cpu().view(Z, T, P), bdt.grad) < 1e-5
+
+
+def test_causal_softmax_with_dropout(dev):
+    Z, Tq, Tk, nb = 4, 9, 9, 2
+    s = _r(Z, Tq, Tk, seed=25)
+    klen = torch.tensor([9, 5], dtype=torch.int32)
+    sd = s.to(dev).contiguous()
+    att = torch.empty(Z * Tq * Tk, device=dev)
+    pd = torch.empty(Z * Tq * Tk, device=dev)
+    K.attn_softmax_fwd(sd, None, 0, 0, 1.0, klen.to(dev), nb, True, att, pd, 0.5, 99, Z, Tq, Tk)
+    i = torch.arange(Tq)[:, None]
+    j = torch.arange(Tk)[None, :]
+    m = (j <= i)[None] & (j[None] < klen.long()[torch.arange(Z) % nb][:, None, None])
+    ref = torch.softmax(s.masked_fill(~m, float("-inf")), -1).masked_fill(~m, 0.0)
+    assert rel_err(att.cpu().view(Z, Tq, Tk), ref) < 1e-6
+    a, p = att.cpu(), pd.cpu()
+    kept = p != 0
+    assert torch.allclose(p[kept], a[kept] * 2.0, atol=1e-6)
+
+
+def test_ctc_against_golden_and_numpy(dev):
+    g = golden("ctc")
+    logits = torch.from_numpy(g["logits"])  # (T, B, V)
+    T, B, V = logits.shape
+    x = logits.permute(1, 0, 2).contiguous().to(dev)  # (B, T, V)
+    lp = torch.empty(B * T, V, device=dev)
+    K.log_softmax(x, lp, B * T, V)
+    nll = torch.empty(B, device=dev)
+    grad = torch.empty(B * T, V, device=dev)
+    ilen = torch.from_numpy(g["ilens"]).int().to(dev)
+    tlen = torch.from_numpy(g["tlens"]).int().to(dev)
+    tg = torch.from_numpy(g["targets"]).to(dev)
+    K.ctc_loss(lp, tg, tg.shape[1], ilen, tlen, B, T, V, 0, 1.0 / B, True, nll, grad)
+    nl = nll.cpu().numpy()
+    ref = g["nll"]
+    fin = np.isfinite(nl)
+    assert (~fin).sum() == 1 and not np.isfinite(nl[3])  # infeasible utterance -> inf (zeroed in the loss)
+    assert np.abs(nl[fin] - ref[fin]).max() < 1e-4
+    gr = grad.cpu().view(B, T, V).permute(1, 0, 2).numpy()
+    assert np.abs(gr - g["grad"]).max() < 1e-5
+    nll_np, g_np = ctc_np.ctc_loss_np(g["logits"], g["ilens"], g["targets"], g["tlens"])
+    assert np.abs(gr - g_np / B).max() < 1e-5
+    out4 = torch.empty(4, device=dev)
+    K.reduce_losses(nll, B, True, None, None, 0, 1.0, 1.0, out4)
+    assert abs(out4[0].item() - float(g["loss"])) < 1e-4
+
+
+def test_forced_align_and_argmax_bit_exact(dev):
+    g = golden("align")
+    for ci in range(4):
+        lpz = torch.from_numpy(g[f"lpz{ci}"]).to(dev).contiguous()
+        y = torch.from_numpy(g[f"y{ci}"]).to(dev)
+        ali = K.ctc_forced_align(lpz, y, 0).cpu().numpy()
+        assert (ali == g[f"ali{ci}"]).all(), (ci, ali, g[f"ali{ci}"])
+        h = torch.from_numpy(g[f"h{ci}"]).to(dev).contiguous()
+        am = torch.empty(h.shape[0], dtype=torch.int64, device=dev)
+        K.argmax(h, am, h.shape[0], h.shape[1])
+        assert (am.cpu().numpy() == g[f"argmax{ci}"]).all()
+
+
+def test_label_smoothing_and_accuracy(dev):
+    R, V = 37, 50
+    x = _r(R, V, seed=26, scale=3.0)
+    tgt = torch.randint(0, V, (R,), generator=torch.Generator().manual_seed(3))
+    tgt[::5] = -1
+    xt = x.double().requires_grad_(True)
+    ref = O.label_smoothing_loss(xt.view(1, R, V), tgt.view(1, R), V, -1, 0.1)
+    ref.backward()
+    acc = O.th_accuracy(x, tgt.view(1, R), -1)
+    xd = x.to(dev)
+    grad = torch.empty(R, V, device=dev)
+    rl = torch.empty(R, device=dev)
+    rs = torch.empty(2 * R, dtype=torch.int32, device=dev)
+    K.label_smoothing(xd, tgt.to(dev), V, -1, 0.1, 1.0, grad, rl, rs)
+    out4 = torch.empty(4, device=dev)
+    K.reduce_losses(None, 1, True, rl, rs, R, 1.0, 0.0, out4)
+    assert abs(out4[1].item() - ref.item()) < 1e-4 * max(1, abs(ref.item()))
+    assert abs(out4[2].item() - acc) < 1e-6
+    assert rel_err(grad.cpu(), xt.grad) < 1e-5
+
+
+def test_specaug_and_mvn_golden(dev):
+    g = golden("specaug")
+    x = torch.from_numpy(g["x"])
+    B, T, F_ = x.shape
+    lens = torch.full((B,), T, dtype=torch.int32).to(dev)
+    for s in (3, 4):
+        warp = torch.tensor([[int(g[f"tw{s}_center"]), int(g[f"tw{s}_warped"])]] * B, dtype=torch.int32)
+        y = torch.empty(B, T, F_, device=dev)
+        K.specaug(x.to(dev), y, lens, warp.to(dev), None, None)
+        assert np.abs(y.cpu().numpy() - g[f"tw{s}_y"]).max() < 1e-5
+    for key, dim in (("freq", 2), ("time", 1)):
+        m = torch.from_numpy(np.stack([g[f"{key}_pos"], g[f"{key}_len"]], -1)).int().to(dev)
+        y = torch.empty(B, T, F_, device=dev)
+        K.specaug(x.to(dev), y, lens, None, m if key == "freq" else None, m if key == "time" else None)
+        assert np.array_equal(y.cpu().numpy(), g[f"{key}_y"])
+    xm = torch.from_numpy(g["mvn_x"]).to(dev).contiguous()
+    K.utterance_mvn(xm, torch.from_numpy(g["mvn_lens"]).int().to(dev))
+    assert np.abs(xm.cpu().numpy() - g["mvn_y"]).max() < 1e-5
+
+
+def test_adam_and_clip(dev):
+    n = 1003
+    p0 = _r(n, seed=27)
+    gr = _r(n, seed=28) * 10
+    pt = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pt], lr=0.01, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-6)
+    pd, gd = p0.to(dev), gr.to(dev)
+    m, v = torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+    clip = torch.empty(3, device=dev)
+    for step in range(1, 4):
+        pt.grad = gr.clone()
+        norm = torch.nn.utils.clip_grad_norm_([pt], 5.0)
+        opt.step()
+        K.grad_norm(gd, 5.0, clip)
+        assert abs(clip[0].item() - norm.item()) < 1e-4 * norm.item()
+        K.adam(pd, gd, m, v, clip, 0.01, 0.9, 0.999, 1e-8, 1e-6, step)
+    assert rel_err(pd.cpu(), pt.detach()) < 1e-5
+    bad = gd.clone()
+    bad[7] = float("nan")
+    K.grad_norm(bad, 5.0, clip)
+    assert clip[2].item() == 0.0
+    before = pd.clone()
+    K.adam(pd, bad, m, v, clip, 0.01, 0.9, 0.999, 1e-8, 0.0, 4)
+    assert torch.equal(before, pd)  # non-finite grad norm -> step skipped (trainer.py:651)
+
+
+def test_subsampling_conv1_and_col2im(dev):
+    Bn, T, F_, D = 2, 31, 80, 8
+    x = _r(Bn, T, F_, seed=29)
+    w0 = _r(D, 1, 3, 3, seed=30)
+    b0 = _r(D, seed=31)
+    z = torch.empty(Bn * 15 * 39 * D, device=dev)
+    K.conv1_fwd(x.to(dev), w0.to(dev), b0.to(dev), z, Bn, T, F_, D)
+    xt = x.double().unsqueeze(1)
+    w0t = w0.double().requires_grad_(True)
+    b0t = b0.double().requires_grad_(True)
+    ref = F.relu(F.conv2d(xt, w0t, b0t, stride=2))
+    assert rel_err(z.cpu().view(Bn, 15, 39, D).permute(0, 3, 1, 2), ref.detach()) < 1e-6
+    dz = _r(Bn, 15, 39, D, seed=32)
+    ref.backward(dz.double().permute(0, 3, 1, 2))
+    dzm = dz.to(dev).contiguous() * (z.view(Bn, 15, 39, D) > 0)
+    dW, db = torch.zeros(D, 9, device=dev), torch.zeros(D, device=dev)
+    K.conv1_wgrad(x.to(dev), dzm.contiguous(), dW, db, Bn, T, F_, D)
+    assert rel_err(dW.cpu().view(D, 1, 3, 3), w0t.grad) < 1e-5
+    assert rel_err(db.cpu(), b0t.grad) < 1e-5
