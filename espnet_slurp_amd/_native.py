@@ -22,7 +22,7 @@ U64 = ctypes.c_ulonglong
 SIGNATURES = {
     "esp_last_error": [],
     "esp_abi_version": [],
-    "esp_gemm_f32": [I, I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, L, P, F, F, P, I, P, F, U64, P, P, P],
+    "esp_gemm_f32": [I, I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, L, P, F, F, P, I, P, F, U64, P, P, P, L, P],
     "esp_act_bwd": [P, P, P, L, I, F, U64, L, P],
     "esp_scale_dropout": [P, P, L, F, F, U64, P, F, P],
     "esp_scale_by_dev": [P, L, P, P],

@@ -51,7 +51,27 @@ struct GemmArgs {
   uint32_t drop_thresh;  // 0 = no dropout
   float drop_scale;
   uint64_t seed;
+  int batch;
+  int splits, kchunk;  // split-K: blockIdx.z = z*splits + split; partials -> work
+  float* work;
 };
+
+// fused epilogue for output element (z, m, n) with raw accumulator `acc`
+__device__ __forceinline__ void epi_store(const GemmArgs& g, int z, int m, int n, float acc) {
+  const int z1 = z / g.nb2, z2 = z - z1 * g.nb2;
+  const long off = (long)z1 * g.c1 + (long)z2 * g.c2 + (long)m * g.ldc + n;
+  float v = acc + (g.bias ? g.bias[n] : 0.f);
+  if (g.aux) g.aux[off] = v;
+  if (g.act == ACT_RELU) v = fmaxf(v, 0.f);
+  else if (g.act == ACT_SWISH) v = v / (1.0f + expf(-v));
+  if (g.drop_thresh) {
+    const uint64_t idx = ((uint64_t)z * g.M + m) * (uint64_t)g.N + n;
+    v = esp::keep_elem(g.seed, idx, g.drop_thresh) ? v * g.drop_scale : 0.f;
+  }
+  v *= g.alpha;
+  if (g.r) v += g.beta * g.r[off];
+  g.c[off] = v;
+}
 
 // address of im2col element: pixel index `pix` of the output grid, column `col` = (kt,kf,c)
 __device__ __forceinline__ const float* i2c_ptr(const float* base, const Im2col& ic, long pix, int col) {
@@ -160,8 +180,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) float As[2][BM * LDS_S];
   __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDS_S];
 
-  const int z = blockIdx.z;
+  const int split = blockIdx.z % g.splits;
+  const int z = blockIdx.z / g.splits;
   const int z1 = z / g.nb2, z2 = z - z1 * g.nb2;
+  const int kbeg = split * g.kchunk;
+  const int kend = min(g.K, kbeg + g.kchunk);
   const float* Ab = g.a.p + z1 * g.a.s1 + z2 * g.a.s2;
   const float* Bb = g.b.p + z1 * g.b.s1 + z2 * g.b.s2;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
@@ -179,9 +202,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmArgs g) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   float4 ra[2], rb[2];
-  const int nk = (g.K + BK - 1) / BK;
-  load_slab<MA>(g.a, Ab, g.M, g.K, m0, 0, ra);
-  load_slab<MB>(g.b, Bb, g.N, g.K, n0, 0, rb);
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  load_slab<MA>(g.a, Ab, g.M, kend, m0, kbeg, ra);
+  load_slab<MB>(g.b, Bb, g.N, kend, n0, kbeg, rb);
   store_slab<MA>(As[0], ra);
   store_slab<MB>(Bs[0], rb);
   __syncthreads();
@@ -189,8 +212,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmArgs g) {
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) {
-      load_slab<MA>(g.a, Ab, g.M, g.K, m0, (kt + 1) * BK, ra);
-      load_slab<MB>(g.b, Bb, g.N, g.K, n0, (kt + 1) * BK, rb);
+      load_slab<MA>(g.a, Ab, g.M, kend, m0, kbeg + (kt + 1) * BK, ra);
+      load_slab<MB>(g.b, Bb, g.N, kend, n0, kbeg + (kt + 1) * BK, rb);
     }
     float af[2][8], bf[2][8];
 #pragma unroll
@@ -221,40 +244,66 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmArgs g) {
   }
 
   // ---------------------------------------------------------------- epilogue
-  float* Cb = g.c + z1 * g.c1 + z2 * g.c2;
-  const float* Rb = g.r ? g.r + z1 * g.c1 + z2 * g.c2 : nullptr;
-  float* Xb = g.aux ? g.aux + z1 * g.c1 + z2 * g.c2 : nullptr;
+  float* W = g.splits > 1 ? g.work + ((long)split * g.batch + z) * (long)g.M * g.N : nullptr;  // [split][z][M][N]
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int n = n0 + wn * 64 + j * 32 + l32;
       if (n >= g.N) continue;
-      const float bv = g.bias ? g.bias[n] : 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (m >= g.M) continue;
-        const long off = (long)m * g.ldc + n;
-        float v = acc[i][j][r] + bv;
-        if (Xb) Xb[off] = v;
-        if (g.act == ACT_RELU) v = fmaxf(v, 0.f);
-        else if (g.act == ACT_SWISH) v = v / (1.0f + expf(-v));
-        if (g.drop_thresh) {
-          const uint64_t idx = ((uint64_t)z * g.M + m) * (uint64_t)g.N + n;
-          v = esp::keep_elem(g.seed, idx, g.drop_thresh) ? v * g.drop_scale : 0.f;
-        }
-        v *= g.alpha;
-        if (Rb) v += g.beta * Rb[off];
-        Cb[off] = v;
+        if (W) W[(long)m * g.N + n] = acc[i][j][r];
+        else epi_store(g, z, m, n, acc[i][j][r]);
       }
     }
 }
 
+// split-K reduction in fixed split order + the fused epilogue (4 outputs per thread when
+// N % 4 == 0: float4 partial loads)
+__global__ void splitk_reduce_kernel(GemmArgs g) {
+  const long MN = (long)g.M * g.N;
+  const long split_stride = MN * g.batch;
+  if ((g.N & 3) == 0) {
+    const long total4 = split_stride >> 2;
+    for (long e4 = blockIdx.x * (long)blockDim.x + threadIdx.x; e4 < total4; e4 += (long)gridDim.x * blockDim.x) {
+      const long e = e4 << 2;
+      float4 acc = *reinterpret_cast<const float4*>(g.work + e);
+      for (int s = 1; s < g.splits; ++s) {
+        const float4 v = *reinterpret_cast<const float4*>(g.work + s * split_stride + e);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+      const int z = (int)(e / MN);
+      const long r = e - (long)z * MN;
+      const int m = (int)(r / g.N), n = (int)(r - (long)m * g.N);
+      epi_store(g, z, m, n, acc.x);
+      epi_store(g, z, m, n + 1, acc.y);
+      epi_store(g, z, m, n + 2, acc.z);
+      epi_store(g, z, m, n + 3, acc.w);
+    }
+    return;
+  }
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < split_stride; e += (long)gridDim.x * blockDim.x) {
+    const int z = (int)(e / MN);
+    const long r = e - (long)z * MN;
+    const int m = (int)(r / g.N), n = (int)(r - (long)m * g.N);
+    float acc = 0.f;
+    for (int s = 0; s < g.splits; ++s) acc += g.work[s * split_stride + e];
+    epi_store(g, z, m, n, acc);
+  }
+}
+
 template <int MA, int MB>
 int launch(const GemmArgs& g, int batch, hipStream_t st) {
-  dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, batch);
+  dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, batch * g.splits);
   hipLaunchKernelGGL((gemm_f32_kernel<MA, MB>), grid, dim3(NT), 0, st, g);
+  if (g.splits > 1) {
+    long total = (long)g.M * g.N * batch;
+    long nb = (total + 255) / 256;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)(nb > 16384 ? 16384 : nb)), dim3(256), 0, st, g);
+  }
   ESP_CHECK_LAUNCH("gemm_f32");
   return 0;
 }
@@ -270,7 +319,8 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
                          float* C, long ldc, long sc1, long sc2,
                          const float* bias, float alpha, float beta, const float* R,
                          int act, float* aux, float drop_p, unsigned long long seed,
-                         const int* im2col_a, const int* im2col_b, void* stream) {
+                         const int* im2col_a, const int* im2col_b, float* work, long work_bytes,
+                         void* stream) {
   ESP_ARG_CHECK(M >= 0 && N >= 0 && K >= 0 && batch >= 1 && nb2 >= 1 && batch % nb2 == 0,
                 "esp_gemm_f32: bad sizes M=%d N=%d K=%d batch=%d nb2=%d", M, N, K, batch, nb2);
   ESP_ARG_CHECK(mode_a >= 0 && mode_a <= 3 && mode_b >= 0 && mode_b <= 3, "esp_gemm_f32: bad mode");
@@ -298,6 +348,29 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
     g.drop_thresh = (uint32_t)(t >= 4294967295.0 ? 4294967295.0 : t);
     if (g.drop_thresh == 0) g.drop_thresh = 1;
     g.drop_scale = 1.0f / (1.0f - drop_p);
+  }
+  // split-K when the tile grid cannot fill the 256 CUs (weight gradients: small M x N, huge K)
+  g.batch = batch;
+  g.splits = 1;
+  g.kchunk = K;
+  {
+    const long tiles = (long)((N + BN - 1) / BN) * ((M + BM - 1) / BM) * batch;
+    const long target = 2 * 256;
+    if (work && tiles < target && K >= 2 * 128) {
+      long sp = (target + tiles - 1) / tiles;
+      const long by_k = K / 128;  // keep >= 8 slabs of BK per split
+      if (sp > by_k) sp = by_k;
+      const long cap = work_bytes / (4L * M * N * batch);
+      if (sp > cap) sp = cap;
+      if (sp > 64) sp = 64;
+      if (sp >= 2) {
+        int chunk = (int)((K + sp - 1) / sp);
+        chunk = (chunk + BK - 1) / BK * BK;
+        g.splits = (int)((K + chunk - 1) / chunk);
+        g.kchunk = chunk;
+        g.work = work;
+      }
+    }
   }
   hipStream_t st = (hipStream_t)stream;
   const int key = mode_a * 4 + mode_b;

@@ -116,15 +116,26 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
   }
 }
 
-// out[c] (+)= sum_{p<nb} part[p*stride + c]   for c < N (fixed order)
+// out[c] (+)= sum_{p<nb} part[p*stride + c]   for c < N.  Block = 64 columns x 16 row
+// groups (1024 threads); each group sums rows g, g+16, ...; groups combined in fixed order.
 template <typename T>
-__global__ void finalize_cols_kernel(const T* __restrict__ part, int nb, long stride, int N,
-                                     float* __restrict__ out, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= N) return;
+__global__ __launch_bounds__(1024) void finalize_cols_kernel(const T* __restrict__ part, int nb, long stride, int N,
+                                                             float* __restrict__ out, int accumulate) {
+  __shared__ T sh[16][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   T s = 0;
-  for (int p = 0; p < nb; ++p) s += part[(long)p * stride + c];
-  out[c] = accumulate ? out[c] + (float)s : (float)s;
+  if (c < N) {
+#pragma unroll 4
+    for (int p = g; p < nb; p += 16) s += part[(long)p * stride + c];
+  }
+  sh[g][cl] = s;
+  __syncthreads();
+  if (g == 0 && c < N) {
+    T t = 0;
+    for (int k = 0; k < 16; ++k) t += sh[k][cl];
+    out[c] = accumulate ? out[c] + (float)t : (float)t;
+  }
 }
 
 // column partial sums of a [M][N] (ld) matrix: block = chunk of rows, thread = column
@@ -166,61 +177,90 @@ __global__ void glu_bwd_kernel(const float* __restrict__ u, const float* __restr
 
 // y[b,t,c] = bias[c] + sum_k W[c,k] * x[b, t + k - pad, c]   (flip=0, forward)
 // y[b,t,c] = sum_k W[c,k] * x[b, t - k + pad, c]             (flip=1, input grad)
-constexpr int DW_TT = 8;  // time steps per thread
-__global__ void dwconv_kernel(const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
-                              float* __restrict__ y, int Bn, int T, int D, int K, int flip) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  const int t0 = blockIdx.y * DW_TT;
-  const int b = blockIdx.z;
-  if (c >= D) return;
+// Block = 64 channels x DW_TT time steps; the input window (DW_TT + K - 1 rows) and the
+// 64 filters are staged in LDS; a thread owns one channel and DW_TT/4 consecutive steps.
+constexpr int DW_TT = 32, DW_KMAX = 64;
+__global__ __launch_bounds__(256) void dwconv_kernel(const float* __restrict__ x, const float* __restrict__ W,
+                                                     const float* __restrict__ bias, float* __restrict__ y, int Bn,
+                                                     int T, int D, int K, int flip) {
+  __shared__ float xs[DW_TT + DW_KMAX][64];
+  __shared__ float ws[64][DW_KMAX + 1];
+  const int c0 = blockIdx.x * 64, t0 = blockIdx.y * DW_TT, b = blockIdx.z;
   const int pad = (K - 1) / 2;
-  float acc[DW_TT];
+  const int cl = threadIdx.x & 63, tg = threadIdx.x >> 6;
+  const int c = c0 + cl;
+  const float* xb = x + (long)b * T * D;
+  const int rows = DW_TT + K - 1;
+  for (int r = tg; r < rows; r += 4) {
+    const int t = t0 - pad + r;
+    xs[r][cl] = (c < D && t >= 0 && t < T) ? xb[(long)t * D + c] : 0.f;
+  }
+  for (int e = threadIdx.x; e < 64 * K; e += 256) {
+    const int cc = e / K, k = e - cc * K;
+    ws[cc][k] = (c0 + cc < D) ? W[(long)(c0 + cc) * K + (flip ? (K - 1 - k) : k)] : 0.f;
+  }
+  __syncthreads();
+  if (c >= D) return;
+  constexpr int PT = DW_TT / 4;
+  float acc[PT];
   const float bv = bias ? bias[c] : 0.f;
 #pragma unroll
-  for (int j = 0; j < DW_TT; ++j) acc[j] = bv;
-  const float* xb = x + (long)b * T * D + c;
-  // window of inputs: forward needs t0-pad .. t0+DW_TT-1+pad
+  for (int j = 0; j < PT; ++j) acc[j] = bv;
+  const int base = tg * PT;
   for (int k = 0; k < K; ++k) {
-    const float wk = W[c * K + (flip ? (K - 1 - k) : k)];
+    const float wk = ws[cl][k];
 #pragma unroll
-    for (int j = 0; j < DW_TT; ++j) {
-      const int ti = t0 + j + k - pad;
-      if (ti >= 0 && ti < T) acc[j] += wk * xb[(long)ti * D];
-    }
+    for (int j = 0; j < PT; ++j) acc[j] += wk * xs[base + j + k][cl];
   }
 #pragma unroll
-  for (int j = 0; j < DW_TT; ++j)
-    if (t0 + j < T) y[((long)b * T + t0 + j) * D + c] = acc[j];
+  for (int j = 0; j < PT; ++j) {
+    const int t = t0 + base + j;
+    if (t < T) y[((long)b * T + t) * D + c] = acc[j];
+  }
 }
 
-// dW[c,k] partials: sum_{t in chunk} dy[b,t,c] * x[b,t+k-pad,c]; part[(b*nch+ch)][c][k]
+// dW[c,k] partials over a DWW_TCH-step time chunk: sum_t dy[b,t,c] * x[b,t+k-pad,c].
+// Block = 64 channels; 4 tap groups (k = kg, kg+4, ...); dy and x windows in LDS.
 constexpr int DWW_TCH = 64;
-template <int KT>  // KT>0: compile-time kernel size (registers); KT==0: runtime K (scratch)
-__global__ void dwconv_wgrad_kernel(const float* __restrict__ dy, const float* __restrict__ x, float* __restrict__ part,
-                                    int T, int D, int Kr) {
-  const int K = KT > 0 ? KT : Kr;
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  const int ch = blockIdx.y, b = blockIdx.z, nch = gridDim.y;
-  if (c >= D) return;
+__global__ __launch_bounds__(256) void dwconv_wgrad_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                           float* __restrict__ part, int T, int D, int K) {
+  __shared__ float xs[DWW_TCH + DW_KMAX][64];
+  __shared__ float gs[DWW_TCH][64];
+  const int c0 = blockIdx.x * 64, ch = blockIdx.y, b = blockIdx.z, nch = gridDim.y;
+  const int t0 = ch * DWW_TCH;
   const int pad = (K - 1) / 2;
-  float acc[KT > 0 ? KT : 64];
+  const int cl = threadIdx.x & 63, kg = threadIdx.x >> 6;
+  const int c = c0 + cl;
+  const float* xb = x + (long)b * T * D;
+  const float* db = dy + (long)b * T * D;
+  for (int r = kg; r < DWW_TCH + K - 1; r += 4) {
+    const int t = t0 - pad + r;
+    xs[r][cl] = (c < D && t >= 0 && t < T) ? xb[(long)t * D + c] : 0.f;
+  }
+  for (int r = kg; r < DWW_TCH; r += 4) {
+    const int t = t0 + r;
+    gs[r][cl] = (c < D && t < T) ? db[(long)t * D + c] : 0.f;
+  }
+  __syncthreads();
+  if (c >= D) return;
+  constexpr int KPT = DW_KMAX / 4;  // taps per thread (k = kg + 4i)
+  float acc[KPT];
 #pragma unroll
-  for (int k = 0; k < (KT > 0 ? KT : 64); ++k) acc[k] = 0.f;
-  const int t0 = ch * DWW_TCH, t1 = min(T, t0 + DWW_TCH);
-  const float* xb = x + (long)b * T * D + c;
-  const float* db = dy + (long)b * T * D + c;
-  for (int t = t0; t < t1; ++t) {
-    const float g = db[(long)t * D];
+  for (int i = 0; i < KPT; ++i) acc[i] = 0.f;
+  for (int t = 0; t < DWW_TCH; ++t) {
+    const float g = gs[t][cl];
 #pragma unroll
-    for (int k = 0; k < (KT > 0 ? KT : 64); ++k) {
-      const int ti = t + k - pad;
-      if (k < K && ti >= 0 && ti < T) acc[k] += g * xb[(long)ti * D];
+    for (int i = 0; i < KPT; ++i) {
+      const int k = kg + 4 * i;
+      if (k < K) acc[i] += g * xs[t + k][cl];
     }
   }
   float* pr = part + ((long)(b * nch + ch) * D + c) * K;
 #pragma unroll
-  for (int k = 0; k < (KT > 0 ? KT : 64); ++k)
-    if (k < K) pr[k] = acc[k];
+  for (int i = 0; i < KPT; ++i) {
+    const int k = kg + 4 * i;
+    if (k < K) pr[k] = acc[i];
+  }
 }
 
 // BatchNorm statistics, stage 1: per row-chunk partial sums (double) of x and, given a
@@ -244,14 +284,29 @@ __global__ void bn_part_kernel(const float* __restrict__ x, int M, int D, int ro
   part[(long)blockIdx.x * D + c] = s;
 }
 
-// finalize: mode 0 -> mean[c] = S/M ; mode 1 -> rstd[c], running stats update
-__global__ void bn_finalize_kernel(const double* __restrict__ part, int nb, int D, int M, int mode,
-                                   float* __restrict__ mean, float* __restrict__ rstd, float* __restrict__ run_mean,
-                                   float* __restrict__ run_var, float momentum, float eps) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= D) return;
+// fixed-order sum of nb partial rows for 64 columns: 16 groups of 64 lanes
+__device__ __forceinline__ double sum_parts16(const double* __restrict__ part, int nb, long stride, int c, bool ok,
+                                              double (*sh)[64]) {
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
   double s = 0.0;
-  for (int p = 0; p < nb; ++p) s += part[(long)p * D + c];
+  if (ok)
+    for (int p = g; p < nb; p += 16) s += part[(long)p * stride + c];
+  sh[g][cl] = s;
+  __syncthreads();
+  double t = 0.0;
+  for (int k = 0; k < 16; ++k) t += sh[k][cl];
+  return t;
+}
+
+// finalize: mode 0 -> mean[c] = S/M ; mode 1 -> rstd[c], running stats update
+__global__ __launch_bounds__(1024) void bn_finalize_kernel(const double* __restrict__ part, int nb, int D, int M, int mode,
+                                                           float* __restrict__ mean, float* __restrict__ rstd,
+                                                           float* __restrict__ run_mean, float* __restrict__ run_var,
+                                                           float momentum, float eps) {
+  __shared__ double sh[16][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const double s = sum_parts16(part, nb, D, c, c < D, sh);
+  if ((threadIdx.x >> 6) != 0 || c >= D) return;
   if (mode == 0) {
     mean[c] = (float)(s / M);
   } else {
@@ -298,18 +353,18 @@ __global__ void bn_swish_bwd_part_kernel(const float* __restrict__ ds, const flo
     s2 += (double)d * xh;
   }
   part[((long)blockIdx.x * 2) * D + c] = s1;
-  part[((long)blockIdx.x * 2 + 1) * D + c] = s2;
+  part[((long)blockIdx.x * 2) * D + D + c] = s2;
 }
 
-__global__ void bn_bwd_finalize_kernel(const double* __restrict__ part, int nb, int D, float* __restrict__ sums,
-                                       float* __restrict__ dgamma, float* __restrict__ dbeta) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= D) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int p = 0; p < nb; ++p) {
-    s1 += part[((long)p * 2) * D + c];
-    s2 += part[((long)p * 2 + 1) * D + c];
-  }
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const double* __restrict__ part, int nb, int D,
+                                                               float* __restrict__ sums, float* __restrict__ dgamma,
+                                                               float* __restrict__ dbeta) {
+  __shared__ double sh[16][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const double s1 = sum_parts16(part, nb, 2L * D, c, c < D, sh);
+  __syncthreads();
+  const double s2 = sum_parts16(part + D, nb, 2L * D, c, c < D, sh);
+  if ((threadIdx.x >> 6) != 0 || c >= D) return;
   sums[c] = (float)s1;
   sums[D + c] = (float)s2;
   dbeta[c] += (float)s1;
@@ -332,6 +387,12 @@ inline int gridn(long n) {
   return (int)(b > 65536 ? 65536 : (b < 1 ? 1 : b));
 }
 inline int nchunks(int M, int target_rows) { return (M + target_rows - 1) / target_rows; }
+// rows per block so that about 384 blocks share the rows (fills 256 CUs, bounded partials)
+inline int rows_per_block(int M) {
+  int r = (M + 383) / 384;
+  return r < 8 ? 8 : r;
+}
+inline dim3 fin_grid(int N) { return dim3((N + 63) / 64); }
 
 }  // namespace
 
@@ -354,7 +415,7 @@ ESP_API int esp_layernorm_bwd(const float* dy, const float* x, const float* w, c
                               float* dx, int accumulate, float* dw, float* db, int M, int D, float* work,
                               void* stream) {
   ESP_ARG_CHECK(D <= MAXD, "esp_layernorm_bwd: D too large");
-  const int rpb = 64;
+  const int rpb = rows_per_block(M);
   const int nb = nchunks(M, rpb);
   hipStream_t st = (hipStream_t)stream;
   const int per = (D + 63) / 64;
@@ -364,16 +425,15 @@ ESP_API int esp_layernorm_bwd(const float* dy, const float* x, const float* w, c
     hipLaunchKernelGGL(ln_bwd_kernel<8>, dim3(nb), dim3(256), 0, st, dy, x, w, mean, rstd, dx, accumulate, work, M, D, rpb);
   else
     hipLaunchKernelGGL(ln_bwd_kernel<32>, dim3(nb), dim3(256), 0, st, dy, x, w, mean, rstd, dx, accumulate, work, M, D, rpb);
-  hipLaunchKernelGGL(finalize_cols_kernel<float>, dim3((D + 255) / 256), dim3(256), 0, st, work, nb, (long)2 * D, D, dw, 1);
-  hipLaunchKernelGGL(finalize_cols_kernel<float>, dim3((D + 255) / 256), dim3(256), 0, st, work + D, nb, (long)2 * D, D,
-                     db, 1);
+  hipLaunchKernelGGL(finalize_cols_kernel<float>, fin_grid(D), dim3(1024), 0, st, work, nb, (long)2 * D, D, dw, 1);
+  hipLaunchKernelGGL(finalize_cols_kernel<float>, fin_grid(D), dim3(1024), 0, st, work + D, nb, (long)2 * D, D, db, 1);
   ESP_CHECK_LAUNCH("esp_layernorm_bwd");
   return 0;
 }
 
 // out[c] (+)= sum_r x[r*ld + c].  workspace: >= N*ceil(M/64) floats
 ESP_API int esp_colsum(const float* x, int M, int N, long ld, float* out, int accumulate, float* work, void* stream) {
-  const int rpb = 64;
+  const int rpb = rows_per_block(M);
   const int nb = nchunks(M, rpb);
   hipStream_t st = (hipStream_t)stream;
   if (M == 0) {
@@ -382,8 +442,7 @@ ESP_API int esp_colsum(const float* x, int M, int N, long ld, float* out, int ac
   }
   const int ty = (N + 255) / 256;
   hipLaunchKernelGGL(colsum_part_kernel, dim3(nb, ty), dim3(256), 0, st, x, M, N, ld, rpb, work);
-  hipLaunchKernelGGL(finalize_cols_kernel<float>, dim3((N + 255) / 256), dim3(256), 0, st, work, nb, (long)N, N, out,
-                     accumulate);
+  hipLaunchKernelGGL(finalize_cols_kernel<float>, fin_grid(N), dim3(1024), 0, st, work, nb, (long)N, N, out, accumulate);
   ESP_CHECK_LAUNCH("esp_colsum");
   return 0;
 }
@@ -405,7 +464,7 @@ ESP_API int esp_dwconv1d(const float* x, const float* W, const float* bias, floa
                          int flip, void* stream) {
   ESP_ARG_CHECK(K % 2 == 1 && K <= 64, "esp_dwconv1d: K must be odd and <= 64");
   dim3 grid((D + 63) / 64, (T + DW_TT - 1) / DW_TT, Bn);
-  hipLaunchKernelGGL(dwconv_kernel, grid, dim3(64), 0, (hipStream_t)stream, x, W, flip ? nullptr : bias, y, Bn, T, D, K,
+  hipLaunchKernelGGL(dwconv_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, W, flip ? nullptr : bias, y, Bn, T, D, K,
                      flip);
   ESP_CHECK_LAUNCH("esp_dwconv1d");
   return 0;
@@ -417,12 +476,9 @@ ESP_API int esp_dwconv1d_wgrad(const float* dy, const float* x, float* dW, int B
   ESP_ARG_CHECK(K % 2 == 1 && K <= 64, "esp_dwconv1d_wgrad: K must be odd and <= 64");
   const int nch = (T + DWW_TCH - 1) / DWW_TCH;
   hipStream_t st = (hipStream_t)stream;
-  if (K == 31)
-    hipLaunchKernelGGL(dwconv_wgrad_kernel<31>, dim3((D + 63) / 64, nch, Bn), dim3(64), 0, st, dy, x, work, T, D, K);
-  else
-    hipLaunchKernelGGL(dwconv_wgrad_kernel<0>, dim3((D + 63) / 64, nch, Bn), dim3(64), 0, st, dy, x, work, T, D, K);
-  hipLaunchKernelGGL(finalize_cols_kernel<float>, dim3((D * K + 255) / 256), dim3(256), 0, st, work, Bn * nch,
-                     (long)D * K, D * K, dW, 1);
+  hipLaunchKernelGGL(dwconv_wgrad_kernel, dim3((D + 63) / 64, nch, Bn), dim3(256), 0, st, dy, x, work, T, D, K);
+  hipLaunchKernelGGL(finalize_cols_kernel<float>, fin_grid(D * K), dim3(1024), 0, st, work, Bn * nch, (long)D * K,
+                     D * K, dW, 1);
   ESP_CHECK_LAUNCH("esp_dwconv1d_wgrad");
   return 0;
 }
@@ -432,15 +488,15 @@ ESP_API int esp_dwconv1d_wgrad(const float* dy, const float* x, float* dW, int B
 ESP_API int esp_bn_swish_fwd(const float* y, const float* gamma, const float* beta, float* s, float* mean, float* rstd,
                              float* run_mean, float* run_var, float momentum, float eps, int M, int D, double* work,
                              void* stream) {
-  const int rpb = 64, nb = nchunks(M, rpb);
+  const int rpb = rows_per_block(M), nb = nchunks(M, rpb);
   hipStream_t st = (hipStream_t)stream;
   dim3 g1(nb, (D + 255) / 256), gf((D + 255) / 256);
   hipLaunchKernelGGL(bn_part_kernel, g1, dim3(256), 0, st, y, M, D, rpb, nullptr, 0, work);
-  hipLaunchKernelGGL(bn_finalize_kernel, gf, dim3(256), 0, st, work, nb, D, M, 0, mean, rstd, nullptr, nullptr,
-                     momentum, eps);
+  hipLaunchKernelGGL(bn_finalize_kernel, fin_grid(D), dim3(1024), 0, st, work, nb, D, M, 0, mean, rstd, nullptr,
+                     nullptr, momentum, eps);
   hipLaunchKernelGGL(bn_part_kernel, g1, dim3(256), 0, st, y, M, D, rpb, mean, 1, work);
-  hipLaunchKernelGGL(bn_finalize_kernel, gf, dim3(256), 0, st, work, nb, D, M, 1, mean, rstd, run_mean, run_var,
-                     momentum, eps);
+  hipLaunchKernelGGL(bn_finalize_kernel, fin_grid(D), dim3(1024), 0, st, work, nb, D, M, 1, mean, rstd, run_mean,
+                     run_var, momentum, eps);
   hipLaunchKernelGGL(bn_swish_fwd_kernel, dim3(gridn((long)M * D)), dim3(256), 0, st, y, mean, rstd, gamma, beta, s,
                      (long)M * D, D);
   ESP_CHECK_LAUNCH("esp_bn_swish_fwd");
@@ -452,11 +508,11 @@ ESP_API int esp_bn_swish_fwd(const float* y, const float* gamma, const float* be
 ESP_API int esp_bn_swish_bwd(const float* ds, const float* y, const float* mean, const float* rstd, const float* gamma,
                              const float* beta, float* dy, float* dgamma, float* dbeta, int M, int D, double* work,
                              float* sums, void* stream) {
-  const int rpb = 64, nb = nchunks(M, rpb);
+  const int rpb = rows_per_block(M), nb = nchunks(M, rpb);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(bn_swish_bwd_part_kernel, dim3(nb, (D + 255) / 256), dim3(256), 0, st, ds, y, mean, rstd, gamma,
                      beta, dy, M, D, rpb, work);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((D + 255) / 256), dim3(256), 0, st, work, nb, D, sums, dgamma, dbeta);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, fin_grid(D), dim3(1024), 0, st, work, nb, D, sums, dgamma, dbeta);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(gridn((long)M * D)), dim3(256), 0, st, dy, y, mean, rstd, gamma, sums,
                      (long)M * D, D, M);
   ESP_CHECK_LAUNCH("esp_bn_swish_bwd");

@@ -52,6 +52,8 @@ class _Workspace:
 
 WS = _Workspace()
 _WS2 = _Workspace()
+_GEMM_WS = _Workspace()          # split-K partials (stream-ordered reuse)
+_GEMM_WS_BYTES = 64 << 20
 
 
 def _work(nbytes, device):
@@ -68,13 +70,24 @@ def profile_gemm_start():
     _PROF = []
 
 
-def profile_gemm_stop():
-    """-> (total algorithmic FLOPs, total kernel ms, launches) since profile_gemm_start()."""
+def profile_gemm_stop(by_shape: bool = False):
+    """-> (total algorithmic FLOPs, total kernel ms, launches) since profile_gemm_start();
+    with by_shape, also {(modes, M, N, K, batch): [launches, ms, flops]}."""
     global _PROF
     prof, _PROF = _PROF or [], None
     torch.cuda.synchronize()
-    flops = sum(f for f, _, _ in prof)
-    ms = sum(a.elapsed_time(b) for _, a, b in prof)
+    flops = sum(p[0] for p in prof)
+    ms = 0.0
+    shapes = {}
+    for f, a, b, key in prof:
+        t = a.elapsed_time(b)
+        ms += t
+        s = shapes.setdefault(key, [0, 0.0, 0.0])
+        s[0] += 1
+        s[1] += t
+        s[2] += f
+    if by_shape:
+        return flops, ms, len(prof), shapes
     return flops, ms, len(prof)
 
 
@@ -85,6 +98,7 @@ def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc
     """C[z](m,n) = alpha*epi(sum_k A(m,k)B(k,n) + bias) + beta*R (see gemm.hip)."""
     if R is not None and r_off is None:
         r_off = c_off
+    ws = _GEMM_WS.get(_GEMM_WS_BYTES, C.device)
     ica = (_native.I * 5)(*ic_a) if ic_a is not None else None
     icb = (_native.I * 5)(*ic_b) if ic_b is not None else None
     if _PROF is not None:
@@ -96,10 +110,10 @@ def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc
                  _p(C, c_off), ldc, sc[0], sc[1], _p(bias), float(alpha), float(beta),
                  _p(R, r_off or 0), act, _p(aux, c_off) if aux is not None else None,
                  float(drop_p), seed & 0xFFFFFFFFFFFFFFFF,
-                 ctypes_ptr(ica), ctypes_ptr(icb), _st())
+                 ctypes_ptr(ica), ctypes_ptr(icb), _p(ws), ws.numel(), _st())
     if _PROF is not None:
         ev1.record()
-        _PROF.append((2.0 * M * N * K * batch, ev0, ev1))
+        _PROF.append((2.0 * M * N * K * batch, ev0, ev1, (mode_a, mode_b, M, N, K, batch)))
 
 
 def ctypes_ptr(arr):

@@ -30,14 +30,17 @@ int esp_abi_version(void);
  *   mode 2/3: im2col of an NHWC map (3x3, stride 2); im2col_x = {H, W, C, Ho, Wo}
  *   z = z1*nb2+z2 ; operand offset = z1*s1 + z2*s2
  *   act: 0 none, 1 ReLU, 2 Swish (pre-activation stored to aux if non-NULL); dropout with
- *   probability drop_p keyed by (seed, (z*M+m)*N+n). */
+ *   probability drop_p keyed by (seed, (z*M+m)*N+n).
+ *   work/work_bytes: optional scratch; when the tile grid is too small to fill the chip the
+ *   K range is split over blocks and reduced (fixed order, deterministic) before the epilogue. */
 int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2,
                  const float* A, long lda, long sa1, long sa2,
                  const float* B, long ldb, long sb1, long sb2,
                  float* C, long ldc, long sc1, long sc2,
                  const float* bias, float alpha, float beta, const float* R,
                  int act, float* aux, float drop_p, unsigned long long seed,
-                 const int* im2col_a, const int* im2col_b, void* stream);
+                 const int* im2col_a, const int* im2col_b, float* work, long work_bytes,
+                 void* stream);
 
 /* ---- element-wise (positionwise_feed_forward.py:32, conformer/swish.py:13-18, dropout) */
 int esp_act_bwd(const float* dy, const float* h, float* dx, long n, int act, float drop_p,

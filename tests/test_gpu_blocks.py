@@ -58,8 +58,8 @@ def test_relpos_mha_block(dev, legacy):
     mask = (~O.make_pad_mask(klen, T))[:, None, :]
     ref = O.rel_mha(P, "a", xt, pos.cpu().double()[None], mask, H, legacy) + res.double().view(B, T, D)
     ref.backward(dout.double().view(B, T, D))
-    assert rel_err(out.cpu(), ref.detach().view(B * T, D)) < 1e-5
-    assert rel_err(dx.cpu(), xt.grad.view(B * T, D)) < 1e-5
+    assert rel_err(out.cpu(), ref.detach().reshape(B * T, D)) < 1e-5
+    assert rel_err(dx.cpu(), xt.grad.reshape(B * T, D)) < 1e-5
     _check_grads(mod, P, "a")
 
 
@@ -82,8 +82,8 @@ def test_conv_module_block(dev):
     xt = x.double().view(B, T, D).requires_grad_(True)
     ref = O.conv_module(P, "m", xt, 31) + res.double().view(B, T, D)
     ref.backward(dout.double().view(B, T, D))
-    assert rel_err(out.cpu(), ref.detach().view(B * T, D)) < 1e-5
-    assert rel_err(dx.cpu(), xt.grad.view(B * T, D)) < 1e-5
+    assert rel_err(out.cpu(), ref.detach().reshape(B * T, D)) < 1e-5
+    assert rel_err(dx.cpu(), xt.grad.reshape(B * T, D)) < 1e-5
     _check_grads(mod, P, "m")
 
 
@@ -103,6 +103,6 @@ def test_subsampling_block(dev):
     P = _params64(mod, "e")
     y, _ = O.conv2d_subsampling(P, "e", x.double(), torch.ones(B, 1, T, dtype=torch.bool))
     y = y * math.sqrt(D)
-    y.backward(dout.double().view(B, T2, D))
+    y.backward(dout.double().reshape(B, T2, D))
     assert rel_err(out.cpu(), y.detach().reshape(B * T2, D)) < 1e-5
     _check_grads(mod, P, "e")
