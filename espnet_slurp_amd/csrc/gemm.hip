@@ -11,17 +11,18 @@
 // (batch, head) layouts of attention without copies).
 //
 // Tiling: 128x128 block tile, BK=16, 256 threads = 4 waves (2x2), each wave 64x64 =
-// 2x2 MFMA 32x32 tiles. LDS holds both tiles as [row][BK+4] (row = m or n): a lane of
-// half h uses k = 8h+s for MFMA step s, so its 8 operands are 2 contiguous ds_read_b128,
-// conflict-free at the 20-float row stride. Global->LDS is register-staged and double
+// 2x2 MFMA 32x32 tiles. A lane of half h uses k = 8h+s for MFMA step s (both operands agree);
+// see store_slab/load_frag for the two LDS images. Global->LDS is register-staged and double
 // buffered (next slab's loads are issued before the current slab's MFMAs).
 // Epilogue (fused): bias, ReLU/Swish (pre-activation optionally stored to `aux`),
 // counter-RNG dropout, alpha scale and beta*R residual.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 16, LDS_S = BK + 4, NT = 256;
+constexpr int BM = 128, BN = 128, BK = 32, NT = 256;  // BK: split-K granularity
 
 enum Mode { KC = 0, RC = 1, I2C_KC = 2, I2C_RC = 3 };
 enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_SWISH = 2 };
@@ -84,17 +85,17 @@ __device__ __forceinline__ const float* i2c_ptr(const float* base, const Im2col&
   return base + (((bi * ic.H + 2 * ho + kt) * (long)ic.W) + 2 * wo + kf) * ic.C + c;
 }
 
-// Load this thread's 2 float4 pieces of a (R rows x BK) operand slab into registers.
-// rows = M (A) or N (B); row0 = tile origin; k0 = slab origin.
-template <int MODE>
+// Load this thread's NL float4 pieces of a (128 rows x BKT) operand slab into registers.
+// rows = M (A) or N (B); row0 = tile origin; k0 = slab origin; K = end of this split's range.
+template <int MODE, int BKT>
 __device__ __forceinline__ void load_slab(const Operand& op, const float* base, int rows, int K,
-                                          int row0, int k0, float4 (&reg)[2]) {
+                                          int row0, int k0, float4 (&reg)[BKT / 8]) {
+  constexpr int QPR = BKT / 4;  // quads per row (KC)
 #pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int idx = threadIdx.x + it * NT;  // 0..511
+  for (int it = 0; it < BKT / 8; ++it) {
+    const int idx = threadIdx.x + it * NT;
     if constexpr (MODE == KC || MODE == I2C_KC) {
-      // 128 rows x 4 quads along k
-      const int r = idx >> 2, kq = (idx & 3) * 4;
+      const int r = idx / QPR, kq = (idx % QPR) * 4;
       const int gr = row0 + r, gk = k0 + kq;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (gr < rows) {
@@ -120,7 +121,7 @@ __device__ __forceinline__ void load_slab(const Operand& op, const float* base, 
       }
       reg[it] = v;
     } else {
-      // BK k-rows x 32 quads along r
+      // BKT k-rows x 32 quads along r
       const int kr = idx >> 5, rq = (idx & 31) * 4;
       const int gk = k0 + kr, gr = row0 + rq;
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -150,35 +151,93 @@ __device__ __forceinline__ void load_slab(const Operand& op, const float* base, 
   }
 }
 
-// LDS image: row r, k-quad q stored at quad (q ^ ((r >> 3) & 3)) of a 20-float row.
-// The XOR keeps the transposing scalar writes of RC operands at <=4-way bank conflicts
-// (a plain 20-float stride puts a wave's 32 writes on 2 banks) while every float4
-// stays contiguous for ds_read_b128 / ds_write_b128.
-__device__ __forceinline__ int lds_off(int r, int kq) { return r * LDS_S + ((kq ^ ((r >> 3) & 3)) << 2); }
+// LDS images (no transposition on either side):
+//   KC operands  [row][BKT+4] : float4 along k written as loaded; a lane's BKT/2 k-values are
+//                               BKT/8 ds_read_b128 (stride (BKT+4) floats = odd # of quads:
+//                               16 distinct rows hit 16 distinct 16-B slots, conflict-free)
+//   RC operands  [BKT][128+4] : float4 along rows written as loaded; a lane reads its row's
+//                               value per k with ds_read_b32 (32 consecutive floats per half)
+constexpr int LDS_RC = BM + 4;
+template <int BKT>
+struct Lds {
+  static constexpr int KC_S = BKT + 4;
+  static constexpr int TILE = (BM * KC_S > BKT * LDS_RC) ? BM * KC_S : BKT * LDS_RC;
+};
 
-template <int MODE>
-__device__ __forceinline__ void store_slab(float* lds, const float4 (&reg)[2]) {
+template <int MODE, int BKT>
+__device__ __forceinline__ void store_slab(float* lds, const float4 (&reg)[BKT / 8]) {
+  constexpr int QPR = BKT / 4;
 #pragma unroll
-  for (int it = 0; it < 2; ++it) {
+  for (int it = 0; it < BKT / 8; ++it) {
     const int idx = threadIdx.x + it * NT;
     if constexpr (MODE == KC || MODE == I2C_KC) {
-      const int r = idx >> 2, kq = idx & 3;
-      *reinterpret_cast<float4*>(lds + lds_off(r, kq)) = reg[it];
+      const int r = idx / QPR, kq = idx % QPR;
+      *reinterpret_cast<float4*>(lds + r * Lds<BKT>::KC_S + kq * 4) = reg[it];
     } else {
       const int kr = idx >> 5, rq = (idx & 31) * 4;
-      const int q = kr >> 2, e = kr & 3;
-      lds[lds_off(rq + 0, q) + e] = reg[it].x;
-      lds[lds_off(rq + 1, q) + e] = reg[it].y;
-      lds[lds_off(rq + 2, q) + e] = reg[it].z;
-      lds[lds_off(rq + 3, q) + e] = reg[it].w;
+      *reinterpret_cast<float4*>(lds + kr * LDS_RC + rq) = reg[it];
     }
   }
 }
 
-template <int MA, int MB>
-__global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) float As[2][BM * LDS_S];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDS_S];
+// the KH = BKT/2 k-values (k = KH*h + s) of row `r` of the current slab
+template <int MODE, int BKT>
+__device__ __forceinline__ void load_frag(const float* lds, int r, int h, float (&f)[BKT / 2]) {
+  constexpr int KH = BKT / 2;
+  if constexpr (MODE == KC || MODE == I2C_KC) {
+#pragma unroll
+    for (int q = 0; q < KH / 4; ++q) {
+      const float4 v = *reinterpret_cast<const float4*>(lds + r * Lds<BKT>::KC_S + KH * h + 4 * q);
+      f[4 * q + 0] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < KH; ++q) f[q] = lds[(KH * h + q) * LDS_RC + r];
+  }
+}
+
+// half hs (0/1) of the BK=32 fragment: k = 16h + 8hs + q, q = 0..7
+template <int MODE>
+__device__ __forceinline__ void load_frag_half(const float* lds, int r, int h, int hs, float (&f)[8]) {
+  if constexpr (MODE == KC || MODE == I2C_KC) {
+    const float* p = lds + r * Lds<32>::KC_S + 16 * h + 8 * hs;
+    const float4 v0 = *reinterpret_cast<const float4*>(p);
+    const float4 v1 = *reinterpret_cast<const float4*>(p + 4);
+    f[0] = v0.x; f[1] = v0.y; f[2] = v0.z; f[3] = v0.w;
+    f[4] = v1.x; f[5] = v1.y; f[6] = v1.z; f[7] = v1.w;
+  } else {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) f[q] = lds[(16 * h + 8 * hs + q) * LDS_RC + r];
+  }
+}
+
+// one slab of MFMAs on the fragments in registers
+template <int KH>
+__device__ __forceinline__ void mfma_slab(f32x16 (&acc)[2][2], const float (&af)[2][KH], const float (&bf)[2][KH]) {
+#pragma unroll
+  for (int s = 0; s < KH; ++s)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+}
+
+// VARIANT 0: BK=16, register-staged double-buffered LDS (next slab's global loads in flight
+//            during this slab's MFMAs), one barrier per slab.
+// VARIANT 1: BK=32, single LDS buffer, no software pipelining (two barriers per slab); the
+//            overlap comes from 4 resident blocks per CU (36 KB LDS, ~110 VGPRs each).
+// VARIANT 2: BK=32, register-staged prefetch of slab k+1 during slab k's MFMAs into a
+//            single LDS buffer (two barriers per slab; 2 waves/SIMD by VGPRs).
+// VARIANT 3: VARIANT 1 with the slab's MFMAs in two halves (fragments for 8 k-steps live at a
+//            time) so the kernel fits 128 VGPRs: 4 waves/SIMD.
+template <int MA, int MB, int VARIANT>
+__global__ __launch_bounds__(NT, VARIANT == 3 ? 4 : 2) void gemm_f32_kernel(GemmArgs g) {
+  constexpr int BKT = VARIANT == 0 ? 16 : 32;
+  constexpr int KH = BKT / 2;
+  constexpr int NBUF = VARIANT == 0 ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) float As[NBUF][Lds<BKT>::TILE];
+  __shared__ __attribute__((aligned(16))) float Bs[NBUF][Lds<BKT>::TILE];
 
   const int split = blockIdx.z % g.splits;
   const int z = blockIdx.z / g.splits;
@@ -201,49 +260,91 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  float4 ra[2], rb[2];
-  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-  load_slab<MA>(g.a, Ab, g.M, kend, m0, kbeg, ra);
-  load_slab<MB>(g.b, Bb, g.N, kend, n0, kbeg, rb);
-  store_slab<MA>(As[0], ra);
-  store_slab<MB>(Bs[0], rb);
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      load_slab<MA>(g.a, Ab, g.M, kend, m0, kbeg + (kt + 1) * BK, ra);
-      load_slab<MB>(g.b, Bb, g.N, kend, n0, kbeg + (kt + 1) * BK, rb);
-    }
-    float af[2][8], bf[2][8];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int ra_ = wm * 64 + t * 32 + l32;
-      const float4 a0 = *reinterpret_cast<const float4*>(As[cur] + lds_off(ra_, 2 * h));
-      const float4 a1 = *reinterpret_cast<const float4*>(As[cur] + lds_off(ra_, 2 * h + 1));
-      af[t][0] = a0.x; af[t][1] = a0.y; af[t][2] = a0.z; af[t][3] = a0.w;
-      af[t][4] = a1.x; af[t][5] = a1.y; af[t][6] = a1.z; af[t][7] = a1.w;
-      const int rb_ = wn * 64 + t * 32 + l32;
-      const float4 b0 = *reinterpret_cast<const float4*>(Bs[cur] + lds_off(rb_, 2 * h));
-      const float4 b1 = *reinterpret_cast<const float4*>(Bs[cur] + lds_off(rb_, 2 * h + 1));
-      bf[t][0] = b0.x; bf[t][1] = b0.y; bf[t][2] = b0.z; bf[t][3] = b0.w;
-      bf[t][4] = b1.x; bf[t][5] = b1.y; bf[t][6] = b1.z; bf[t][7] = b1.w;
-    }
-#pragma unroll
-    for (int s = 0; s < 8; ++s)
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
-    if (kt + 1 < nk) {
-      store_slab<MA>(As[cur ^ 1], ra);
-      store_slab<MB>(Bs[cur ^ 1], rb);
-    }
+  float4 ra[BKT / 8], rb[BKT / 8];
+  const int nk = kend > kbeg ? (kend - kbeg + BKT - 1) / BKT : 0;
+  if constexpr (VARIANT == 0) {
+    load_slab<MA, BKT>(g.a, Ab, g.M, kend, m0, kbeg, ra);
+    load_slab<MB, BKT>(g.b, Bb, g.N, kend, n0, kbeg, rb);
+    store_slab<MA, BKT>(As[0], ra);
+    store_slab<MB, BKT>(Bs[0], rb);
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) {
+        load_slab<MA, BKT>(g.a, Ab, g.M, kend, m0, kbeg + (kt + 1) * BKT, ra);
+        load_slab<MB, BKT>(g.b, Bb, g.N, kend, n0, kbeg + (kt + 1) * BKT, rb);
+      }
+      float af[2][KH], bf[2][KH];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        load_frag<MA, BKT>(As[cur], wm * 64 + t * 32 + l32, h, af[t]);
+        load_frag<MB, BKT>(Bs[cur], wn * 64 + t * 32 + l32, h, bf[t]);
+      }
+      mfma_slab<KH>(acc, af, bf);
+      if (kt + 1 < nk) {
+        store_slab<MA, BKT>(As[cur ^ 1], ra);
+        store_slab<MB, BKT>(Bs[cur ^ 1], rb);
+      }
+      __syncthreads();
+    }
+  } else if constexpr (VARIANT == 2) {  // NOLINT
+    if (nk > 0) {
+      load_slab<MA, BKT>(g.a, Ab, g.M, kend, m0, kbeg, ra);
+      load_slab<MB, BKT>(g.b, Bb, g.N, kend, n0, kbeg, rb);
+    }
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt > 0) __syncthreads();  // previous slab fully read
+      store_slab<MA, BKT>(As[0], ra);
+      store_slab<MB, BKT>(Bs[0], rb);
+      __syncthreads();
+      if (kt + 1 < nk) {  // next slab's global loads fly during this slab's MFMAs
+        load_slab<MA, BKT>(g.a, Ab, g.M, kend, m0, kbeg + (kt + 1) * BKT, ra);
+        load_slab<MB, BKT>(g.b, Bb, g.N, kend, n0, kbeg + (kt + 1) * BKT, rb);
+      }
+      float af[2][KH], bf[2][KH];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        load_frag<MA, BKT>(As[0], wm * 64 + t * 32 + l32, h, af[t]);
+        load_frag<MB, BKT>(Bs[0], wn * 64 + t * 32 + l32, h, bf[t]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_slab<KH>(acc, af, bf);
+    }
+  } else {
+    for (int kt = 0; kt < nk; ++kt) {
+      load_slab<MA, BKT>(g.a, Ab, g.M, kend, m0, kbeg + kt * BKT, ra);
+      load_slab<MB, BKT>(g.b, Bb, g.N, kend, n0, kbeg + kt * BKT, rb);
+      if (kt > 0) __syncthreads();  // everyone finished reading the previous slab
+      store_slab<MA, BKT>(As[0], ra);
+      store_slab<MB, BKT>(Bs[0], rb);
+      __syncthreads();
+      if constexpr (VARIANT == 3) {
+#pragma unroll
+        for (int hs = 0; hs < 2; ++hs) {
+          float af[2][8], bf[2][8];
+#pragma unroll
+          for (int t = 0; t < 2; ++t) {
+            load_frag_half<MA>(As[0], wm * 64 + t * 32 + l32, h, hs, af[t]);
+            load_frag_half<MB>(Bs[0], wn * 64 + t * 32 + l32, h, hs, bf[t]);
+          }
+          mfma_slab<8>(acc, af, bf);
+        }
+      } else {
+        float af[2][KH], bf[2][KH];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          load_frag<MA, BKT>(As[0], wm * 64 + t * 32 + l32, h, af[t]);
+          load_frag<MB, BKT>(Bs[0], wn * 64 + t * 32 + l32, h, bf[t]);
+        }
+        // issue every LDS read of the slab before the first MFMA (one latency per slab
+        // instead of one per MFMA group); the MFMA chain then runs back to back
+        __builtin_amdgcn_sched_barrier(0);
+        mfma_slab<KH>(acc, af, bf);
+      }
+    }
   }
 
-  // ---------------------------------------------------------------- epilogue
+// ---------------------------------------------------------------- epilogue
   float* W = g.splits > 1 ? g.work + ((long)split * g.batch + z) * (long)g.M * g.N : nullptr;  // [split][z][M][N]
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -295,10 +396,22 @@ __global__ void splitk_reduce_kernel(GemmArgs g) {
   }
 }
 
+int g_variant = -1;
+int variant() {
+  if (g_variant < 0) {
+    const char* e = getenv("ESP_GEMM_VARIANT");
+    g_variant = e ? atoi(e) : 1;
+  }
+  return g_variant;
+}
+
 template <int MA, int MB>
 int launch(const GemmArgs& g, int batch, hipStream_t st) {
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, batch * g.splits);
-  hipLaunchKernelGGL((gemm_f32_kernel<MA, MB>), grid, dim3(NT), 0, st, g);
+  if (variant() == 0) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 0>), grid, dim3(NT), 0, st, g);
+  else if (variant() == 2) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 2>), grid, dim3(NT), 0, st, g);
+  else if (variant() == 3) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 3>), grid, dim3(NT), 0, st, g);
+  else hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 1>), grid, dim3(NT), 0, st, g);
   if (g.splits > 1) {
     long total = (long)g.M * g.N * batch;
     long nb = (total + 255) / 256;
@@ -355,6 +468,9 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
   g.kchunk = K;
   {
     const long tiles = (long)((N + BN - 1) / BN) * ((M + BM - 1) / BM) * batch;
+    // target two blocks per CU.  Measured (tools/gemm_bench.py, B=64 FFN w2 M=23936 N=256
+    // K=1024): split 2 + reduce 153 us vs no split 191 us, although the reduce pass alone is
+    // ~20% of the GEMM's GRBM_GUI_ACTIVE cycles
     const long target = 2 * 256;
     if (work && tiles < target && K >= 2 * 128) {
       long sp = (target + tiles - 1) / tiles;

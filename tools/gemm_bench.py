@@ -1,0 +1,56 @@
+"""Microbenchmark of the MFMA GEMM on the shapes of the C2 training step (B=64)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from espnet_slurp_amd import kernels as K  # noqa: E402
+
+M = 64 * 374
+SHAPES = [  # (mode_a, mode_b, M, N, K, batch, label)
+    (0, 1, M, 1024, 256, 1, "ffn w1 fwd"),
+    (0, 1, M, 256, 1024, 1, "ffn w2 fwd"),
+    (0, 0, M, 256, 1024, 1, "ffn dX w2"),
+    (0, 0, M, 1024, 256, 1, "ffn dX w1"),
+    (1, 1, 256, 1024, M, 1, "ffn dW w2"),
+    (1, 1, 1024, 256, M, 1, "ffn dW w1"),
+    (1, 1, 256, 256, M, 1, "dW 256x256"),
+    (0, 1, M, 768, 256, 1, "qkv fwd"),
+    (0, 0, 374, 374, 64, 256, "scores ac"),
+    (0, 1, 374, 64, 374, 256, "ctx = P V"),
+    (1, 1, 374, 64, 374, 256, "dV / dk"),
+    (0, 1, 64 * 41, 256, 256, 1, "decoder q"),
+    (0, 1, 64 * 41, 256, 2048, 1, "decoder ffn w2"),
+]
+
+
+def run(ma, mb, m, n, k, batch, reps=20):
+    dev = torch.device("cuda:0")
+    A = torch.randn(batch * m * k, device=dev)
+    B = torch.randn(batch * n * k, device=dev)
+    C = torch.empty(batch * m * n, device=dev)
+    lda = k if ma == 0 else m
+    ldb = k if mb == 0 else n
+    kw = dict(mode_a=ma, lda=lda, mode_b=mb, ldb=ldb, ldc=n, batch=batch, nb2=1, sa=(m * k, 0), sb=(n * k, 0),
+              sc=(m * n, 0))
+    for _ in range(3):
+        K.gemm(m, n, k, A, B, C, **kw)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        K.gemm(m, n, k, A, B, C, **kw)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    return ms, 2.0 * m * n * k * batch / (ms * 1e-3) / 1e12
+
+
+if __name__ == "__main__":
+    only = [int(a) for a in sys.argv[1:]]
+    for i, (ma, mb, m, n, k, b, lab) in enumerate(SHAPES):
+        if only and i not in only:
+            continue
+        ms, tf = run(ma, mb, m, n, k, b)
+        print(f"{lab:16s} ({ma},{mb}) M={m:6d} N={n:5d} K={k:6d} b={b:3d}  {ms * 1e3:8.1f} us  {tf:6.1f} TF/s")
