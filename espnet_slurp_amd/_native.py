@@ -58,6 +58,7 @@ SIGNATURES = {
     "esp_ctc_forced_align": [P, I, I, P, I, I, P, P, P],
 }
 _RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I}
+ABI_VERSION = 2  # bumped whenever a signature in include/espnet_mi355.h changes
 
 _lib = None
 
@@ -76,6 +77,9 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = _RESTYPES.get(name, I)
+    if lib.esp_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"espnet_slurp_amd: {LIB_PATH} has ABI {lib.esp_abi_version()}, expected "
+                           f"{ABI_VERSION}; rebuild with `make -C espnet_slurp_amd/csrc`")
     _lib = lib
     return lib
 

@@ -39,7 +39,7 @@ class CTC(nn.Module):
         logits = self.logits(hs2d)
         lp = empty(B * T, V, like=hs2d)
         K.log_softmax(logits, lp, B * T, V)
-        nll = empty(B, like=hs2d)
+        nll = torch.empty(B, dtype=torch.float64, device=hs2d.device)  # fp64 per-utterance nll
         grad = empty(B * T, V, like=hs2d) if want_grad else None
         K.ctc_loss(lp, ys_pad, Umax, hlens_i32, ys_lens_i32, B, T, V, 0, gscale, self.zero_infinity, nll, grad)
         return nll, grad, lp
@@ -58,7 +58,7 @@ class CTC(nn.Module):
                                            ys.shape[1], 1.0, want_grad=False)
             if self.zero_infinity:
                 nll = torch.where(torch.isinf(nll), torch.zeros_like(nll), nll)
-        return nll.sum() / B if self.reduce else nll / B
+        return (nll.sum() / B).float() if self.reduce else (nll / B).float()
 
     def log_softmax(self, hs_pad):
         B, T, D = hs_pad.shape

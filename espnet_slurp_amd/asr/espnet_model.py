@@ -147,7 +147,7 @@ class ESPnetASRModel(AbsESPnetModel):
                                                       seeds, self.training)
             V = self.vocab_size
             grad_att = empty(R, V, like=hs) if want_grad else None
-            row_loss = empty(R, like=hs)
+            row_loss = torch.empty(R, dtype=torch.float64, device=dev)
             row_stat = torch.empty(2 * R, dtype=torch.int32, device=dev)
             K.label_smoothing(logits, ys_out_d, V, self.ignore_id, self.lsm_weight,
                               (1.0 - self.ctc_weight) / denom, grad_att, row_loss, row_stat)

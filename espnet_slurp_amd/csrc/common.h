@@ -60,14 +60,16 @@ __device__ __forceinline__ T block_sum(T v, T* sh /* >= 16 */) {
   for (int i = 0; i < nw; ++i) r += sh[i];
   return r;
 }
-__device__ __forceinline__ float block_max(float v, float* sh) {
+template <typename T = float>
+__device__ __forceinline__ T block_max(T v, T* sh) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-  v = wave_max(v);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
   __syncthreads();
   if (lane == 0) sh[w] = v;
   __syncthreads();
-  float r = -INFINITY;
-  for (int i = 0; i < nw; ++i) r = fmaxf(r, sh[i]);
+  T r = -INFINITY;
+  for (int i = 0; i < nw; ++i) r = fmax(r, sh[i]);
   return r;
 }
 

@@ -35,8 +35,9 @@ struct Operand {
   const float* p;
   long ld;
   long s1, s2;
-  int vec;  // float4 along the contiguous dim is legal
+  int vec;   // float4 along the contiguous dim is legal
   Im2col ic;
+  int glds;  // 16-B LDS-DMA of any in-range quad stays inside the operand (see glds_ok)
 };
 
 struct GemmArgs {
@@ -362,6 +363,262 @@ __global__ __launch_bounds__(NT, VARIANT == 3 ? 4 : 2) void gemm_f32_kernel(Gemm
     }
 }
 
+// ============================================================================ glds kernel
+// The production path.  Global->LDS staging with global_load_lds_dwordx4 (LDS-DMA: no VGPR
+// round trip, asynchronous until its vmcnt), two LDS buffers, raw s_barrier with explicit
+// waits, so slab k+1 streams in while slab k's MFMAs run.  All LDS in ONE __shared__ array
+// (a second object makes hipcc drain vmcnt before every ds_read).  Requires 16-B aligned
+// operands with ld % 4 == 0 (the host falls back to the register-staged kernel otherwise).
+//
+// LDS images are lane-linear per wave instruction (1 KB = 64 lanes x 16 B); the swizzle is
+// applied to the per-lane GLOBAL source address:
+//   KC [rows][32]: quad q of row r at slot r*8 + (q ^ (r&7))   -> ds_read_b128 conflict-free
+//   RC [32][rows]: element (k,r) at k*rows + (r ^ ((k>>4)<<5)) -> the two lane halves
+//                  (k and k+16) land on opposite 32-bank halves, ds_read_b32 conflict-free
+// Out-of-range rows / k are clamped to in-bounds addresses (their products only reach
+// discarded outputs); the K tail of the last slab is zeroed in LDS before use.
+// Block ids are remapped so that consecutive tiles (same A row panel) share an XCD's L2.
+
+struct FastDiv {  // n / d for n < 2^31: (n * m) >> s, m = ceil(2^s / d), s = 31 + ceil(log2 d)
+  uint64_t m;
+  uint32_t s, d;
+};
+static FastDiv make_fastdiv(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  FastDiv f;
+  f.s = 31 + l;
+  f.m = ((1ull << f.s) + d - 1) / d;
+  f.d = d;
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (uint32_t)(((uint64_t)n * f.m) >> f.s);
+}
+
+struct GldsArgs {
+  FastDiv c_a, c_b;    // im2col channel count C
+  FastDiv hw_b, wo_b;  // I2C_RC: output pixels per map (Ho*Wo), Wo
+  FastDiv hw_a, wo_a;  // I2C_KC
+  int ntx, nty;        // tile grid (N tiles, M tiles)
+};
+
+constexpr int GL_BK = 32;
+
+// One global_load_lds_dwordx4: lane l's 16 B at gptr land at lds_wave_base + 16*l.  Issued from
+// inline asm so that hipcc does not see an LDS-DMA store: with the builtin it cannot prove
+// the DMA target (the other buffer) disjoint from this slab's ds_reads and drains vmcnt(0)
+// before every slab's first ds_read, serialising the pipeline.  The ordering the compiler
+// no longer sees is made explicit: wait_vm0() + raw_barrier() before a slab is read, and the
+// "memory" clobber keeps LDS accesses on their side of the asm.  M0 is set per instruction.
+__device__ __forceinline__ void lds_dma16(const float* gptr, float* lds_wave_base) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds_wave_base);
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr), "s"(m0) : "memory", "m0");
+}
+
+// element offset of im2col column `col` (= (kt,kf,c)) relative to the receptive field origin
+__device__ __forceinline__ long i2c_col_off(const Im2col& ic, const FastDiv& fc, int col) {
+  const int kk = (int)fdiv((uint32_t)col, fc), c = col - kk * ic.C;
+  const int kt = kk / 3, kf = kk - kt * 3;
+  return ((long)kt * ic.W + kf) * ic.C + c;
+}
+// element offset of output pixel `pix`'s receptive field origin
+__device__ __forceinline__ long i2c_pix_off(const Im2col& ic, const FastDiv& fhw, const FastDiv& fwo, int pix) {
+  const int bi = (int)fdiv((uint32_t)pix, fhw);
+  const int rem = pix - bi * (int)fhw.d;
+  const int ho = (int)fdiv((uint32_t)rem, fwo), wo = rem - ho * (int)fwo.d;
+  return (((long)bi * ic.H + 2 * ho) * ic.W + 2 * wo) * ic.C;
+}
+
+// Per-lane source bookkeeping for one operand: NI wave-instructions per slab.
+template <int MODE, int ROWS, int NI>
+struct Stage {
+  const float* p[NI];  // per instruction: base incl. the slab-invariant part
+  int q[NI];           // KC: k offset inside the slab (4*quad) ; RC: k-row inside the slab
+  __device__ __forceinline__ void init(const Operand& op, const float* base, int rows, int K, int row0,
+                                       const FastDiv& fc, const FastDiv& fhw, const FastDiv& fwo, int wave,
+                                       int lane) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int slot = (i * 4 + wave) * 64 + lane;
+      if constexpr (MODE == KC || MODE == I2C_KC) {
+        const int r = slot >> 3, qs = slot & 7;
+        const int qq = qs ^ (r & 7);
+        const int gr = min(row0 + r, rows - 1);
+        q[i] = 4 * qq;
+        if constexpr (MODE == KC) p[i] = base + (long)gr * op.ld;
+        else p[i] = base + i2c_pix_off(op.ic, fhw, fwo, gr);
+      } else {
+        constexpr int QPR = ROWS / 4;  // quads per k-row
+        const int kr = slot / QPR, rs = slot % QPR;
+        const int rq = rs ^ (((kr >> 4) & 1) << 3);
+        const int gr = min(row0 + 4 * rq, (rows - 1) & ~3);
+        q[i] = kr;
+        if constexpr (MODE == RC) p[i] = base + gr;
+        else p[i] = base + i2c_col_off(op.ic, fc, gr);
+      }
+    }
+  }
+  // issue this lane's NI LDS-DMA loads of the slab starting at k0 into `dst`
+  __device__ __forceinline__ void issue(const Operand& op, int K, int k0, float* dst, int wave, const FastDiv& fc,
+                                        const FastDiv& fhw, const FastDiv& fwo) const {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      float* ldsw = dst + (i * 4 + wave) * 256;
+      if constexpr (MODE == KC || MODE == I2C_KC) {
+        const int k = min(k0 + q[i], (K - 1) & ~3);
+        if constexpr (MODE == KC) lds_dma16(p[i] + k, ldsw);
+        else lds_dma16(p[i] + i2c_col_off(op.ic, fc, k), ldsw);
+      } else {
+        const int k = min(k0 + q[i], K - 1);
+        if constexpr (MODE == RC) lds_dma16(p[i] + (long)k * op.ld, ldsw);
+        else lds_dma16(p[i] + i2c_pix_off(op.ic, fhw, fwo, k), ldsw);
+      }
+    }
+  }
+};
+
+// zero k >= kv of a staged slab (last slab of a K range that is not a multiple of 32)
+template <int MODE, int ROWS>
+__device__ __forceinline__ void zero_tail(float* slab, int kv) {
+  for (int idx = threadIdx.x; idx < ROWS * GL_BK; idx += NT) {
+    if constexpr (MODE == KC || MODE == I2C_KC) {
+      const int r = idx >> 5, k = idx & 31;
+      if (k >= kv) slab[(r * 8 + ((k >> 2) ^ (r & 7))) * 4 + (k & 3)] = 0.f;
+    } else {
+      const int k = idx / ROWS;
+      if (k >= kv) slab[idx] = 0.f;
+    }
+  }
+}
+
+// the 16 k-values (k = 16h + s) of tile row r
+template <int MODE, int ROWS>
+__device__ __forceinline__ void frag16(const float* slab, int r, int h, float (&f)[16]) {
+  if constexpr (MODE == KC || MODE == I2C_KC) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 v = *reinterpret_cast<const float4*>(slab + (r * 8 + ((4 * h + j) ^ (r & 7))) * 4);
+      f[4 * j + 0] = v.x; f[4 * j + 1] = v.y; f[4 * j + 2] = v.z; f[4 * j + 3] = v.w;
+    }
+  } else {
+    const int rr = r ^ (h << 5);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) f[s] = slab[(16 * h + s) * ROWS + rr];
+  }
+}
+
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// s_barrier without __syncthreads()'s fence (which would drain vmcnt); the empty asm keeps
+// the compiler from moving LDS accesses across it
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int MA, int MB, int BNT>
+__global__ __launch_bounds__(NT, 2) void gemm_glds_kernel(GemmArgs g, GldsArgs x) {
+  constexpr int WN = BNT / 64, WM = 4 / WN, TM = BM / (WM * 32), TN = 2;
+  constexpr int A_SZ = BM * GL_BK, B_SZ = BNT * GL_BK, BUF = A_SZ + B_SZ;
+  constexpr int NIA = A_SZ / 4 / NT, NIB = B_SZ / 4 / NT;
+  __shared__ __attribute__((aligned(16))) float smem[2 * BUF];
+
+  // XCD-aware remap of the linear block id (bijective for any grid size)
+  const int nbl = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, per = nbl >> 3, rem = nbl & 7;
+  const int wg = (xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per) + (orig >> 3);
+  const int tn = wg % x.ntx;
+  const int t2 = wg / x.ntx;
+  const int tm = t2 % x.nty;
+  const int zz = t2 / x.nty;
+  const int split = zz % g.splits;
+  const int z = zz / g.splits;
+  const int z1 = z / g.nb2, z2 = z - z1 * g.nb2;
+  const int kbeg = split * g.kchunk;
+  const int kend = min(g.K, kbeg + g.kchunk);
+  const float* Ab = g.a.p + z1 * g.a.s1 + z2 * g.a.s2;
+  const float* Bb = g.b.p + z1 * g.b.s1 + z2 * g.b.s2;
+  const int m0 = tm * BM, n0 = tn * BNT;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int h = lane >> 5, l32 = lane & 31;
+
+  Stage<MA, BM, NIA> sa;
+  Stage<MB, BNT, NIB> sb;
+  sa.init(g.a, Ab, g.M, g.K, m0, x.c_a, x.hw_a, x.wo_a, wave, lane);
+  sb.init(g.b, Bb, g.N, g.K, n0, x.c_b, x.hw_b, x.wo_b, wave, lane);
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nk = kend > kbeg ? (kend - kbeg + GL_BK - 1) / GL_BK : 0;
+  if (nk > 0) {
+    sa.issue(g.a, g.K, kbeg, smem, wave, x.c_a, x.hw_a, x.wo_a);
+    sb.issue(g.b, g.K, kbeg, smem + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
+    wait_vm0();
+    raw_barrier();
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    float* cur = smem + (kt & 1) * BUF;
+    if (kt + 1 < nk) {  // slab kt+1 streams into the other buffer (last read before the previous barrier)
+      float* nxt = smem + ((kt + 1) & 1) * BUF;
+      const int k1 = kbeg + (kt + 1) * GL_BK;
+      sa.issue(g.a, g.K, k1, nxt, wave, x.c_a, x.hw_a, x.wo_a);
+      sb.issue(g.b, g.K, k1, nxt + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
+    } else {
+      const int kv = kend - (kbeg + kt * GL_BK);
+      if (kv < GL_BK) {
+        zero_tail<MA, BM>(cur, kv);
+        zero_tail<MB, BNT>(cur + A_SZ, kv);
+        wait_lgkm0();
+        raw_barrier();
+      }
+    }
+    float af[TM][16], bf[TN][16];
+#pragma unroll
+    for (int t = 0; t < TM; ++t) frag16<MA, BM>(cur, wm * TM * 32 + t * 32 + l32, h, af[t]);
+#pragma unroll
+    for (int t = 0; t < TN; ++t) frag16<MB, BNT>(cur + A_SZ, wn * 64 + t * 32 + l32, h, bf[t]);
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+    wait_vm0();    // this wave's DMA of slab kt+1 has landed
+    wait_lgkm0();  // this wave's reads of slab kt are done
+    raw_barrier(); // -> everyone's: slab kt+1 readable, buffer kt free for slab kt+2
+  }
+
+  float* W = g.splits > 1 ? g.work + ((long)split * g.batch + z) * (long)g.M * g.N : nullptr;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * 64 + j * 32 + l32;
+      if (n >= g.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m >= g.M) continue;
+        if (W) W[(long)m * g.N + n] = acc[i][j][r];
+        else epi_store(g, z, m, n, acc[i][j][r]);
+      }
+    }
+}
+
 // split-K reduction in fixed split order + the fused epilogue (4 outputs per thread when
 // N % 4 == 0: float4 partial loads)
 __global__ void splitk_reduce_kernel(GemmArgs g) {
@@ -400,15 +657,37 @@ int g_variant = -1;
 int variant() {
   if (g_variant < 0) {
     const char* e = getenv("ESP_GEMM_VARIANT");
-    g_variant = e ? atoi(e) : 1;
+    g_variant = e ? atoi(e) : 4;
   }
   return g_variant;
+}
+
+template <int MA, int MB, int BNT>
+void launch_glds(const GemmArgs& g, int batch, hipStream_t st) {
+  GldsArgs x{};
+  x.ntx = (g.N + BNT - 1) / BNT;
+  x.nty = (g.M + BM - 1) / BM;
+  if (MA == I2C_KC) {
+    x.c_a = make_fastdiv(g.a.ic.C);
+    x.hw_a = make_fastdiv(g.a.ic.Ho * g.a.ic.Wo);
+    x.wo_a = make_fastdiv(g.a.ic.Wo);
+  }
+  if (MB == I2C_RC) {
+    x.c_b = make_fastdiv(g.b.ic.C);
+    x.hw_b = make_fastdiv(g.b.ic.Ho * g.b.ic.Wo);
+    x.wo_b = make_fastdiv(g.b.ic.Wo);
+  }
+  const long nbl = (long)x.ntx * x.nty * batch * g.splits;
+  hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT>), dim3((unsigned)nbl), dim3(NT), 0, st, g, x);
 }
 
 template <int MA, int MB>
 int launch(const GemmArgs& g, int batch, hipStream_t st) {
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, batch * g.splits);
-  if (variant() == 0) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 0>), grid, dim3(NT), 0, st, g);
+  if (variant() == 4 && g.a.glds && g.b.glds) {
+    if (g.N <= 64) launch_glds<MA, MB, 64>(g, batch, st);
+    else launch_glds<MA, MB, 128>(g, batch, st);
+  } else if (variant() == 0) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 0>), grid, dim3(NT), 0, st, g);
   else if (variant() == 2) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 2>), grid, dim3(NT), 0, st, g);
   else if (variant() == 3) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 3>), grid, dim3(NT), 0, st, g);
   else hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 1>), grid, dim3(NT), 0, st, g);
@@ -422,6 +701,17 @@ int launch(const GemmArgs& g, int batch, hipStream_t st) {
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// LDS-DMA staging reads whole 16-B quads along the contiguous dim `cont` (K for KC, the row
+// count for RC) at clamped indices: legal when quads are aligned and the row pitch covers the
+// rounded-up run (or there is a single line whose run is a multiple of 4).
+bool glds_ok(int mode, const void* p, long ld, long s1, long s2, int rows, int K) {
+  if (!aligned16(p) || s1 % 4 || s2 % 4) return false;
+  if (mode >= 2) return true;  // im2col: C % 4 == 0 checked by the caller
+  const long cont = mode == 0 ? K : rows, lines = mode == 0 ? rows : K;
+  if (lines == 1) return cont % 4 == 0;
+  return ld % 4 == 0 && ld >= cont;
+}
 
 }  // namespace
 
@@ -445,6 +735,8 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
   g.b = Operand{B, ldb, sb1, sb2, 0, {}};
   g.a.vec = aligned16(A) && lda % 4 == 0 && sa1 % 4 == 0 && sa2 % 4 == 0;
   g.b.vec = aligned16(B) && ldb % 4 == 0 && sb1 % 4 == 0 && sb2 % 4 == 0;
+  g.a.glds = glds_ok(mode_a, A, lda, sa1, sa2, M, K);
+  g.b.glds = glds_ok(mode_b, B, ldb, sb1, sb2, N, K);
   if (mode_a >= 2) {
     ESP_ARG_CHECK(im2col_a && im2col_a[2] % 4 == 0 && aligned16(A), "esp_gemm_f32: im2col A needs C%%4==0");
     g.a.ic = Im2col{im2col_a[0], im2col_a[1], im2col_a[2], im2col_a[3], im2col_a[4]};

@@ -13,10 +13,13 @@
 
 namespace {
 
-__device__ __forceinline__ float lse2(float a, float b) {
-  const float m = fmaxf(a, b);
+// log(e^a + e^b + e^c) with the max shift; the recursion values stay fp64 (alpha/beta reach
+// -O(10^3): an fp32 running value would round by ~1e-4 per frame), the O(1) shifted
+// exponentials are evaluated in fp32 (relative 1e-7, i.e. 1e-7 absolute after the log)
+__device__ __forceinline__ double lse3(double a, double b, double c) {
+  const double m = fmax(a, fmax(b, c));
   if (m == -INFINITY) return -INFINITY;
-  return logf(expf(a - m) + expf(b - m)) + m;
+  return (double)logf(expf((float)(a - m)) + expf((float)(b - m)) + expf((float)(c - m))) + m;
 }
 
 // block-per-row log-softmax, any V
@@ -27,12 +30,13 @@ __global__ void log_softmax_kernel(const float* __restrict__ x, float* __restric
   float m = -INFINITY;
   for (int c = threadIdx.x; c < V; c += blockDim.x) m = fmaxf(m, xr[c]);
   m = esp::block_max(m, sh);
-  float s = 0.f;
-  for (int c = threadIdx.x; c < V; c += blockDim.x) s += expf(xr[c] - m);
-  s = esp::block_sum<float>(s, sh);
-  const float lse = m + logf(s);
+  __shared__ double shd[16];
+  double s = 0.0;
+  for (int c = threadIdx.x; c < V; c += blockDim.x) s += (double)expf(xr[c] - m);
+  s = esp::block_sum<double>(s, shd);
+  const double lse = (double)m + log(s);
   float* yr = y + row * V;
-  for (int c = threadIdx.x; c < V; c += blockDim.x) yr[c] = xr[c] - lse;
+  for (int c = threadIdx.x; c < V; c += blockDim.x) yr[c] = (float)((double)xr[c] - lse);
 }
 
 // blockIdx.x = utterance, blockIdx.y = 0 alpha / 1 beta.  lp: (B, T, V) log-probs.
@@ -41,12 +45,12 @@ constexpr int CTC_NT = 256, CTC_SPT = 4;  // states per thread -> S <= 1024
 __global__ __launch_bounds__(CTC_NT) void ctc_alpha_beta_kernel(const float* __restrict__ lp, const int64_t* __restrict__ labels,
                                                                 int Umax, const int* __restrict__ ilen,
                                                                 const int* __restrict__ tlen, int T, int V, int Smax,
-                                                                int blank, float* __restrict__ la, float* __restrict__ lb,
-                                                                float* __restrict__ nll) {
+                                                                int blank, double* __restrict__ la, double* __restrict__ lb,
+                                                                double* __restrict__ nll) {
   const int b = blockIdx.x;
   const int dir = blockIdx.y;
   const int Tb = ilen[b], U = tlen[b], S = 2 * U + 1;
-  __shared__ float buf[2][CTC_NT * CTC_SPT + 2];
+  __shared__ double buf[2][CTC_NT * CTC_SPT + 2];
   __shared__ int lab[CTC_NT * CTC_SPT + 2];
   const float* lpb = lp + (long)b * T * V;
   for (int s = threadIdx.x; s < S + 2; s += CTC_NT) {
@@ -55,7 +59,7 @@ __global__ __launch_bounds__(CTC_NT) void ctc_alpha_beta_kernel(const float* __r
     lab[s] = l;
   }
   __syncthreads();
-  float* out = (dir == 0 ? la : lb) + (long)b * T * Smax;
+  double* out = (dir == 0 ? la : lb) + (long)b * T * Smax;
   if (Tb <= 0) {
     if (dir == 0 && threadIdx.x == 0) nll[b] = INFINITY;
     return;
@@ -63,7 +67,7 @@ __global__ __launch_bounds__(CTC_NT) void ctc_alpha_beta_kernel(const float* __r
   int cur = 0;
   if (dir == 0) {
     for (int s = threadIdx.x; s < S; s += CTC_NT) {
-      float v = -INFINITY;
+      double v = -INFINITY;
       if (s == 0) v = lpb[blank];
       else if (s == 1) v = lpb[lab[1]];
       buf[0][s] = v;
@@ -73,12 +77,9 @@ __global__ __launch_bounds__(CTC_NT) void ctc_alpha_beta_kernel(const float* __r
     for (int t = 1; t < Tb; ++t) {
       const float* lpt = lpb + (long)t * V;
       for (int s = threadIdx.x; s < S; s += CTC_NT) {
-        const float l1 = buf[cur][s];
-        const float l2 = s > 0 ? buf[cur][s - 1] : -INFINITY;
-        const float l3 = (s > 1 && lab[s] != lab[s - 2]) ? buf[cur][s - 2] : -INFINITY;
-        float m = fmaxf(l1, fmaxf(l2, l3));
-        if (m == -INFINITY) m = 0.f;
-        const float v = logf(expf(l1 - m) + expf(l2 - m) + expf(l3 - m)) + m + lpt[lab[s]];
+        const double v = lse3(buf[cur][s], s > 0 ? buf[cur][s - 1] : -INFINITY,
+                              (s > 1 && lab[s] != lab[s - 2]) ? buf[cur][s - 2] : -INFINITY) +
+                         (double)lpt[lab[s]];
         buf[cur ^ 1][s] = v;
         out[(long)t * Smax + s] = v;
       }
@@ -86,16 +87,12 @@ __global__ __launch_bounds__(CTC_NT) void ctc_alpha_beta_kernel(const float* __r
       __syncthreads();
     }
     if (threadIdx.x == 0) {
-      const float l1 = buf[cur][S - 1];
-      const float l2 = S > 1 ? buf[cur][S - 2] : -INFINITY;
-      float m = fmaxf(l1, l2);
-      if (m == -INFINITY) m = 0.f;
-      nll[b] = -(logf(expf(l1 - m) + expf(l2 - m)) + m);
+      nll[b] = -lse3(buf[cur][S - 1], S > 1 ? buf[cur][S - 2] : -INFINITY, -INFINITY);
     }
   } else {
     const float* lpt0 = lpb + (long)(Tb - 1) * V;
     for (int s = threadIdx.x; s < S; s += CTC_NT) {
-      float v = -INFINITY;
+      double v = -INFINITY;
       if (s == S - 1) v = lpt0[blank];
       else if (s == S - 2) v = lpt0[lab[S - 2]];
       buf[0][s] = v;
@@ -105,12 +102,9 @@ __global__ __launch_bounds__(CTC_NT) void ctc_alpha_beta_kernel(const float* __r
     for (int t = Tb - 2; t >= 0; --t) {
       const float* lpt = lpb + (long)t * V;
       for (int s = threadIdx.x; s < S; s += CTC_NT) {
-        const float l1 = buf[cur][s];
-        const float l2 = s < S - 1 ? buf[cur][s + 1] : -INFINITY;
-        const float l3 = (s < S - 2 && lab[s] != lab[s + 2]) ? buf[cur][s + 2] : -INFINITY;
-        float m = fmaxf(l1, fmaxf(l2, l3));
-        if (m == -INFINITY) m = 0.f;
-        const float v = logf(expf(l1 - m) + expf(l2 - m) + expf(l3 - m)) + m + lpt[lab[s]];
+        const double v = lse3(buf[cur][s], s < S - 1 ? buf[cur][s + 1] : -INFINITY,
+                              (s < S - 2 && lab[s] != lab[s + 2]) ? buf[cur][s + 2] : -INFINITY) +
+                         (double)lpt[lab[s]];
         buf[cur ^ 1][s] = v;
         out[(long)t * Smax + s] = v;
       }
@@ -125,57 +119,57 @@ constexpr int MAXV_LDS = 8192;
 __global__ __launch_bounds__(256) void ctc_grad_kernel(const float* __restrict__ lp, const int64_t* __restrict__ labels,
                                                        int Umax, const int* __restrict__ ilen,
                                                        const int* __restrict__ tlen, int T, int V, int Smax, int blank,
-                                                       const float* __restrict__ la, const float* __restrict__ lb,
-                                                       const float* __restrict__ nll, float gscale, int zero_infinity,
+                                                       const double* __restrict__ la, const double* __restrict__ lb,
+                                                       const double* __restrict__ nll, float gscale, int zero_infinity,
                                                        float* __restrict__ grad) {
   __shared__ float occ[MAXV_LDS];
   __shared__ float sh[16];
+  __shared__ double shd[16];
   const int t = blockIdx.x, b = blockIdx.y;
   const int Tb = ilen[b], U = tlen[b], S = 2 * U + 1;
   float* gr = grad + ((long)b * T + t) * V;
-  const float nl = nll[b];
+  const double nl = nll[b];
   if (t >= Tb || (zero_infinity && isinf(nl))) {
     for (int c = threadIdx.x; c < V; c += blockDim.x) gr[c] = 0.f;
     return;
   }
   for (int c = threadIdx.x; c < V; c += blockDim.x) occ[c] = 0.f;
-  const float* lat = la + ((long)b * T + t) * Smax;
-  const float* lbt = lb + ((long)b * T + t) * Smax;
-  float m = -INFINITY;
-  for (int s = threadIdx.x; s < S; s += blockDim.x) m = fmaxf(m, lat[s] + lbt[s]);
-  m = esp::block_max(m, sh);  // includes a barrier: occ is zeroed before the adds below
+  const double* lat = la + ((long)b * T + t) * Smax;
+  const double* lbt = lb + ((long)b * T + t) * Smax;
+  double m = -INFINITY;
+  for (int s = threadIdx.x; s < S; s += blockDim.x) m = fmax(m, lat[s] + lbt[s]);
+  m = esp::block_max<double>(m, shd);  // includes a barrier: occ is zeroed before the adds below
   if (m != -INFINITY) {
     for (int s = threadIdx.x; s < S; s += blockDim.x) {
       const int l = (s & 1) ? (int)labels[(long)b * Umax + (s >> 1)] : blank;
-      const float v = lat[s] + lbt[s];
-      if (v != -INFINITY) atomicAdd(&occ[l], expf(v - m));
+      const double v = lat[s] + lbt[s];
+      if (v != -INFINITY) atomicAdd(&occ[l], expf((float)(v - m)));
     }
   }
   __syncthreads();
   const float* lpt = lp + ((long)b * T + t) * V;
+  const double mn = m + nl;  // log occupancy offset: exp(lcab + nll - lp) = occ * exp(m + nll - lp)
   float gs = 0.f;
   for (int c = threadIdx.x; c < V; c += blockDim.x) {
     const float l = lpt[c];
     const float o = occ[c];
-    const float lcab = o > 0.f ? m + logf(o) : -INFINITY;
-    const float g = expf(l) - expf(lcab + nl - l);
-    gs += g;
+    const float q = o > 0.f ? o * expf((float)(mn - (double)l)) : 0.f;
+    gs += expf(l) - q;
   }
   gs = esp::block_sum<float>(gs, sh);
   for (int c = threadIdx.x; c < V; c += blockDim.x) {
     const float l = lpt[c];
     const float o = occ[c];
-    const float lcab = o > 0.f ? m + logf(o) : -INFINITY;
+    const float q = o > 0.f ? o * expf((float)(mn - (double)l)) : 0.f;
     const float e = expf(l);
-    const float g = (e - expf(lcab + nl - l)) * gscale;
-    gr[c] = g - e * (gs * gscale);
+    gr[c] = (e - q) * gscale - e * (gs * gscale);
   }
 }
 
 // label smoothing: block per row.  rows with target == ignore get zero loss/grad.
 __global__ __launch_bounds__(256) void ls_kernel(const float* __restrict__ x, const int64_t* __restrict__ target,
                                                  int V, int ignore, float smoothing, float gscale,
-                                                 float* __restrict__ grad, float* __restrict__ row_loss,
+                                                 float* __restrict__ grad, double* __restrict__ row_loss,
                                                  int* __restrict__ row_stat) {
   __shared__ float sh[16];
   __shared__ int shi[16];
@@ -187,7 +181,7 @@ __global__ __launch_bounds__(256) void ls_kernel(const float* __restrict__ x, co
     if (gr)
       for (int c = threadIdx.x; c < V; c += blockDim.x) gr[c] = 0.f;
     if (threadIdx.x == 0) {
-      row_loss[row] = 0.f;
+      row_loss[row] = 0.0;
       row_stat[2 * row] = 0;
       row_stat[2 * row + 1] = 0;
     }
@@ -215,22 +209,25 @@ __global__ __launch_bounds__(256) void ls_kernel(const float* __restrict__ x, co
   for (int i = 1; i < (int)(blockDim.x >> 6); ++i)
     if (sh[i] > m || (sh[i] == m && shi[i] < am)) { m = sh[i]; am = shi[i]; }
   __syncthreads();
-  float s = 0.f, slp = 0.f;
+  __shared__ double shd[16];
+  double s = 0.0, slp = 0.0;
   for (int c = threadIdx.x; c < V; c += blockDim.x) {
-    s += expf(xr[c] - m);
-    slp += xr[c];
+    s += (double)expf(xr[c] - m);
+    slp += (double)xr[c];
   }
-  s = esp::block_sum<float>(s, sh);
-  slp = esp::block_sum<float>(slp, sh);
-  const float lse = m + logf(s);
+  s = esp::block_sum<double>(s, shd);
+  slp = esp::block_sum<double>(slp, shd);
+  const double lse_d = (double)m + log(s);
+  const float lse = (float)lse_d;
   const float conf = 1.0f - smoothing;
   const float sv = smoothing / (float)(V - 1);
-  const float lpt = xr[tg] - lse;
-  const float sum_lp = slp - (float)V * lse;
-  if (threadIdx.x == 0) {
-    float l = 0.f;
-    if (conf > 0.f) l += conf * (logf(conf) - lpt);
-    if (sv > 0.f) l += sv * ((float)(V - 1) * logf(sv) - (sum_lp - lpt));
+  if (threadIdx.x == 0) {  // KL(true_dist || p) in fp64 from the fp32 logits
+    const double lpt = (double)xr[tg] - lse_d;
+    const double sum_lp = slp - (double)V * lse_d;
+    const double cd = 1.0 - (double)smoothing, svd = (double)smoothing / (double)(V - 1);
+    double l = 0.0;
+    if (conf > 0.f) l += cd * (log(cd) - lpt);
+    if (sv > 0.f) l += svd * ((double)(V - 1) * log(svd) - (sum_lp - lpt));
     row_loss[row] = l;
     row_stat[2 * row] = (am == (int)tg) ? 1 : 0;
     row_stat[2 * row + 1] = 1;
@@ -247,14 +244,14 @@ __global__ __launch_bounds__(256) void ls_kernel(const float* __restrict__ x, co
 
 // out[0] = ctc loss = sum_b nll_b' / B ;  out[1] = att loss = sum rows / denom ;
 // out[2] = acc ; out[3] = w*out[0] + (1-w)*out[1].  One block, fixed order.
-__global__ void reduce_losses_kernel(const float* __restrict__ nll, int B, int zero_inf, const float* __restrict__ row_loss,
+__global__ void reduce_losses_kernel(const double* __restrict__ nll, int B, int zero_inf, const double* __restrict__ row_loss,
                                      const int* __restrict__ row_stat, int R, float denom, float ctc_w,
                                      float* __restrict__ out) {
   __shared__ double shd[16];
   double a = 0.0;
   for (int i = threadIdx.x; i < B && nll; i += blockDim.x) {
-    float v = nll[i];
-    if (zero_inf && isinf(v)) v = 0.f;
+    double v = nll[i];
+    if (zero_inf && isinf(v)) v = 0.0;
     a += v;
   }
   a = esp::block_sum<double>(a, shd);
@@ -268,14 +265,14 @@ __global__ void reduce_losses_kernel(const float* __restrict__ nll, int B, int z
   c = esp::block_sum<double>(c, shd);
   n = esp::block_sum<double>(n, shd);
   if (threadIdx.x == 0) {
-    const float lc = nll ? (float)(a / B) : 0.f;
-    const float lat = row_loss ? (float)(l / denom) : 0.f;
-    out[0] = lc;
-    out[1] = lat;
+    const double lc = nll ? a / B : 0.0;
+    const double lat = row_loss ? l / denom : 0.0;
+    out[0] = (float)lc;
+    out[1] = (float)lat;
     out[2] = (n > 0) ? (float)(c / n) : 0.f;
-    if (!nll) out[3] = lat;
-    else if (!row_loss) out[3] = lc;
-    else out[3] = ctc_w * lc + (1.0f - ctc_w) * lat;
+    if (!nll) out[3] = (float)lat;
+    else if (!row_loss) out[3] = (float)lc;
+    else out[3] = (float)((double)ctc_w * lc + (1.0 - (double)ctc_w) * lat);
   }
 }
 
@@ -355,15 +352,15 @@ ESP_API int esp_log_softmax(const float* x, float* y, long rows, int V, void* st
 
 // lp (B,T,V) log-probs; labels (B,Umax) int64; ilen/tlen int32 device arrays.
 // Outputs: nll (B); grad (B,T,V) = gscale * d nll_b / d logits (zeroed where infinite
-// when zero_infinity).  work: >= 2*B*T*Smax floats, Smax = 2*Umax+1 <= 1024.
+// when zero_infinity).  work: >= 2*B*T*Smax doubles, Smax = 2*Umax+1 <= 1024.
 ESP_API int esp_ctc_loss(const float* lp, const long long* labels, int Umax, const int* ilen, const int* tlen, int B,
-                         int T, int V, int blank, float gscale, int zero_infinity, float* nll, float* grad, float* work,
-                         void* stream) {
+                         int T, int V, int blank, float gscale, int zero_infinity, double* nll, float* grad,
+                         double* work, void* stream) {
   const int Smax = 2 * Umax + 1;
   ESP_ARG_CHECK(Smax <= CTC_NT * CTC_SPT, "esp_ctc_loss: 2*Umax+1=%d > %d", Smax, CTC_NT * CTC_SPT);
   ESP_ARG_CHECK(V <= MAXV_LDS, "esp_ctc_loss: V=%d > %d", V, MAXV_LDS);
-  float* la = work;
-  float* lb = work + (long)B * T * Smax;
+  double* la = work;
+  double* lb = work + (long)B * T * Smax;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(ctc_alpha_beta_kernel, dim3(B, 2), dim3(CTC_NT), 0, st, lp, (const int64_t*)labels, Umax, ilen, tlen,
                      T, V, Smax, blank, la, lb, nll);
@@ -375,14 +372,14 @@ ESP_API int esp_ctc_loss(const float* lp, const long long* labels, int Umax, con
 }
 
 ESP_API int esp_label_smoothing(const float* x, const long long* target, long rows, int V, int ignore, float smoothing,
-                                float gscale, float* grad, float* row_loss, int* row_stat, void* stream) {
+                                float gscale, float* grad, double* row_loss, int* row_stat, void* stream) {
   hipLaunchKernelGGL(ls_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, x, (const int64_t*)target, V,
                      ignore, smoothing, gscale, grad, row_loss, row_stat);
   ESP_CHECK_LAUNCH("esp_label_smoothing");
   return 0;
 }
 
-ESP_API int esp_reduce_losses(const float* nll, int B, int zero_inf, const float* row_loss, const int* row_stat, int R,
+ESP_API int esp_reduce_losses(const double* nll, int B, int zero_inf, const double* row_loss, const int* row_stat, int R,
                               float denom, float ctc_w, float* out, void* stream) {
   hipLaunchKernelGGL(reduce_losses_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, nll, B, zero_inf, row_loss,
                      row_stat, R, denom, ctc_w, out);

@@ -307,19 +307,28 @@ def log_softmax(x, y, rows, V):
     _native.call("esp_log_softmax", _p(x), _p(y), rows, V, _st())
 
 
+def _need_f64(*ts):
+    for t in ts:
+        if t is not None and t.dtype != torch.float64:
+            raise TypeError(f"espnet_slurp_amd: expected a float64 buffer, got {t.dtype}")
+
+
 def ctc_loss(lp, labels, Umax, ilen_i32, tlen_i32, B, T, V, blank, gscale, zero_infinity, nll, grad):
+    _need_f64(nll)
     S = 2 * Umax + 1
-    ws = _work(4 * 2 * B * T * S, lp.device)
+    ws = _work(8 * 2 * B * T * S, lp.device)  # fp64 alpha / beta
     _native.call("esp_ctc_loss", _p(lp), _p(labels), Umax, _p(ilen_i32), _p(tlen_i32), B, T, V, blank,
                  float(gscale), int(zero_infinity), _p(nll), _p(grad), _p(ws), _st())
 
 
 def label_smoothing(x, target, V, ignore, smoothing, gscale, grad, row_loss, row_stat):
+    _need_f64(row_loss)
     _native.call("esp_label_smoothing", _p(x), _p(target), target.numel(), V, ignore, float(smoothing),
                  float(gscale), _p(grad), _p(row_loss), _p(row_stat), _st())
 
 
 def reduce_losses(nll, B, zero_inf, row_loss, row_stat, R, denom, ctc_w, out4):
+    _need_f64(nll, row_loss)
     _native.call("esp_reduce_losses", _p(nll), B, int(zero_inf), _p(row_loss), _p(row_stat), R, float(denom),
                  float(ctc_w), _p(out4), _st())
 

@@ -109,13 +109,16 @@ int esp_permute3(const float* in, float* out, int O, int Bd, int Ad, int accumul
 /* ---- losses (ctc.py:39-97, label_smoothing_loss.py:41-63, nets_utils.py:299-320,
  *      espnet/nets/pytorch_backend/ctc.py:185-249) */
 int esp_log_softmax(const float* x, float* y, long rows, int V, void* stream);
+/* Loss internals run in fp64 where fp32 rounding would exceed the 1e-4 loss gate: the CTC
+ * alpha/beta recursions (values ~ -10^3), per-utterance nll, per-row label-smoothing KL and
+ * the final reductions.  nll (B) and row_loss (R) are fp64; work >= 2*B*T*(2*Umax+1) doubles. */
 int esp_ctc_loss(const float* lp, const long long* labels, int Umax, const int* ilen,
                  const int* tlen, int B, int T, int V, int blank, float gscale, int zero_infinity,
-                 float* nll, float* grad, float* work, void* stream);
+                 double* nll, float* grad, double* work, void* stream);
 int esp_label_smoothing(const float* x, const long long* target, long rows, int V, int ignore,
-                        float smoothing, float gscale, float* grad, float* row_loss, int* row_stat,
+                        float smoothing, float gscale, float* grad, double* row_loss, int* row_stat,
                         void* stream);
-int esp_reduce_losses(const float* nll, int B, int zero_inf, const float* row_loss,
+int esp_reduce_losses(const double* nll, int B, int zero_inf, const double* row_loss,
                       const int* row_stat, int R, float denom, float ctc_w, float* out4,
                       void* stream);
 int esp_argmax(const float* x, long long* out, long rows, int V, void* stream);

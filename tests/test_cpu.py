@@ -144,7 +144,7 @@ def test_library_exports_every_header_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(_native.SIGNATURES), set(names) ^ set(_native.SIGNATURES)
-    assert lib.esp_abi_version() == 1
+    assert lib.esp_abi_version() == _native.ABI_VERSION
 
 
 def test_product_never_imports_oracle():

@@ -45,6 +45,38 @@ def test_gemm_modes(dev, shape, modes):
     assert err <= 1e-5 * max(1.0, math.sqrt(Kk)) * 4, err
 
 
+def _padded(rows, cols, pad, seed):
+    """(rows, cols) values inside a (rows, cols+pad) buffer: a 16-B aligned pitch > extent."""
+    buf = _r(rows, cols + pad, seed=seed)
+    return buf, buf[:, :cols]
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 4), (130, 64, 36), (257, 200, 100), (64, 33, 1000), (384, 256, 2048),
+                                   (5, 700, 64), (129, 60, 19), (300, 128, 77)])
+@pytest.mark.parametrize("modes", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_gemm_lds_dma_paths(dev, shape, modes):
+    """Aligned pitches select the LDS-DMA kernel: M/N/K tails, K % 4 != 0 inside a padded pitch,
+    the 128x64 tile (N <= 64) and split-K (small M x N, long K)."""
+    M, N, Kk = shape
+    ma, mb = modes
+    pad = (-Kk) % 4 + 4
+    if ma == K.KC:
+        Abuf, A = _padded(M, Kk, (-Kk) % 4 + 4, 21)
+    else:
+        Abuf, A = _padded(Kk, M, (-M) % 4 + 4, 21)
+    if mb == K.KC:
+        Bbuf, B = _padded(N, Kk, pad, 22)
+    else:
+        Bbuf, B = _padded(Kk, N, (-N) % 4 + 4, 22)
+    Ad, Bd = Abuf.to(dev), Bbuf.to(dev)
+    C = torch.empty(M, N, device=dev)
+    K.gemm(M, N, Kk, Ad, Bd, C, mode_a=ma, lda=Ad.stride(0), mode_b=mb, ldb=Bd.stride(0), ldc=N)
+    ref = _gemm_ref(A, B, ma, mb)
+    torch.cuda.synchronize()
+    err = (C.cpu().double() - ref).abs().max().item()
+    assert err <= 1e-5 * max(1.0, math.sqrt(Kk)) * 4, err
+
+
 def test_gemm_epilogue(dev):
     M, N, Kk = 257, 130, 64
     X, W, b = _r(M, Kk, seed=3), _r(N, Kk, seed=4), _r(N, seed=5)
@@ -115,6 +147,31 @@ def test_gemm_im2col_conv(dev):
     cols = cols.view(Bn, C, 3, 3, -1).permute(0, 4, 2, 3, 1).reshape(Bn * T2 * F2, 9 * C)
     ref_dw = g.double().t() @ cols
     assert (dw.cpu().double() - ref_dw).abs().max() < 1e-3
+
+
+@pytest.mark.parametrize("C", [32, 12])
+def test_gemm_im2col_lds_dma(dev, C):
+    """conv2-shaped implicit im2col through the LDS-DMA kernel (C % 32 == 0 keeps a slab inside
+    one tap; C = 12 crosses taps inside a slab)."""
+    Bn, T1, F1 = 3, 23, 15
+    x = _r(Bn, C, T1, F1, seed=31)
+    w = _r(C, C, 3, 3, seed=32)
+    ref = F.conv2d(x.double(), w.double(), None, stride=2)
+    T2, F2 = ref.shape[2], ref.shape[3]
+    z1 = x.permute(0, 2, 3, 1).contiguous().to(dev)
+    w2r = w.permute(0, 2, 3, 1).contiguous().to(dev)
+    out = torch.empty(Bn * T2 * F2, C, device=dev)
+    K.gemm(Bn * T2 * F2, C, 9 * C, z1, w2r, out, mode_a=K.I2C_KC, lda=0, mode_b=K.KC, ldb=9 * C, ldc=C,
+           ic_a=(T1, F1, C, T2, F2))
+    got = out.cpu().view(Bn, T2, F2, C).permute(0, 3, 1, 2).double()
+    assert (got - ref).abs().max() < 1e-4
+    g = _r(Bn * T2 * F2, C, seed=33)
+    dw = torch.empty(C, 9 * C, device=dev)
+    K.gemm(C, 9 * C, Bn * T2 * F2, g.to(dev), z1, dw, mode_a=K.RC, lda=C, mode_b=K.I2C_RC, ldb=0, ldc=9 * C,
+           ic_b=(T1, F1, C, T2, F2))
+    cols = F.unfold(x.double(), 3, stride=2)
+    cols = cols.view(Bn, C, 3, 3, -1).permute(0, 4, 2, 3, 1).reshape(Bn * T2 * F2, 9 * C)
+    assert (dw.cpu().double() - g.double().t() @ cols).abs().max() < 1e-3
 
 
 def test_layernorm(dev):
@@ -247,7 +304,7 @@ def test_ctc_against_golden_and_numpy(dev):
     x = logits.permute(1, 0, 2).contiguous().to(dev)  # (B, T, V)
     lp = torch.empty(B * T, V, device=dev)
     K.log_softmax(x, lp, B * T, V)
-    nll = torch.empty(B, device=dev)
+    nll = torch.empty(B, dtype=torch.float64, device=dev)
     grad = torch.empty(B * T, V, device=dev)
     ilen = torch.from_numpy(g["ilens"]).int().to(dev)
     tlen = torch.from_numpy(g["tlens"]).int().to(dev)
@@ -291,7 +348,7 @@ def test_label_smoothing_and_accuracy(dev):
     acc = O.th_accuracy(x, tgt.view(1, R), -1)
     xd = x.to(dev)
     grad = torch.empty(R, V, device=dev)
-    rl = torch.empty(R, device=dev)
+    rl = torch.empty(R, dtype=torch.float64, device=dev)
     rs = torch.empty(2 * R, dtype=torch.int32, device=dev)
     K.label_smoothing(xd, tgt.to(dev), V, -1, 0.1, 1.0, grad, rl, rs)
     out4 = torch.empty(4, device=dev)

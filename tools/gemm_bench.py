@@ -47,10 +47,35 @@ def run(ma, mb, m, n, k, batch, reps=20):
     return ms, 2.0 * m * n * k * batch / (ms * 1e-3) / 1e12
 
 
+def run_torch(ma, mb, m, n, k, batch, reps=20):
+    """The same product through torch.matmul (rocBLAS / hipBLASLt fp32) for comparison."""
+    dev = torch.device("cuda:0")
+    A = torch.randn(batch, m, k, device=dev) if ma == 0 else torch.randn(batch, k, m, device=dev).transpose(1, 2)
+    B = torch.randn(batch, n, k, device=dev).transpose(1, 2) if mb == 0 else torch.randn(batch, k, n, device=dev)
+    if batch == 1:
+        A, B = A[0], B[0]
+    for _ in range(3):
+        C = torch.matmul(A, B)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        C = torch.matmul(A, B)
+    e1.record()
+    torch.cuda.synchronize()
+    del C
+    ms = e0.elapsed_time(e1) / reps
+    return ms, 2.0 * m * n * k * batch / (ms * 1e-3) / 1e12
+
+
 if __name__ == "__main__":
     only = [int(a) for a in sys.argv[1:]]
     for i, (ma, mb, m, n, k, b, lab) in enumerate(SHAPES):
         if only and i not in only:
             continue
         ms, tf = run(ma, mb, m, n, k, b)
-        print(f"{lab:16s} ({ma},{mb}) M={m:6d} N={n:5d} K={k:6d} b={b:3d}  {ms * 1e3:8.1f} us  {tf:6.1f} TF/s")
+        line = f"{lab:16s} ({ma},{mb}) M={m:6d} N={n:5d} K={k:6d} b={b:3d}  {ms * 1e3:8.1f} us  {tf:6.1f} TF/s"
+        if os.environ.get("GEMM_BENCH_TORCH"):
+            tms, ttf = run_torch(ma, mb, m, n, k, b)
+            line += f"   | torch.matmul {tms * 1e3:8.1f} us  {ttf:6.1f} TF/s"
+        print(line, flush=True)
