@@ -181,23 +181,25 @@ class RelPositionMultiHeadedAttention(nn.Module):
         q_v = empty(Z * T * dk, like=x2d)
         K.heads_split(qkv, 3 * D, 0, B, T, H, dk, self.pos_bias_u, q_u)
         K.heads_split(qkv, 3 * D, 0, B, T, H, dk, self.pos_bias_v, q_v)
-        ac = empty(Z * T * T, like=x2d)
+        Tp, Pp = K.pitch(T), K.pitch(P)  # 16-B aligned score rows
+        ac = empty(Z * T * Tp, like=x2d)
         # ac[z] = q_u[z] k[b,h]^T
-        K.gemm(T, T, dk, q_u, qkv, ac, mode_a=K.KC, lda=dk, mode_b=K.KC, ldb=3 * D, ldc=T, b_off=D,
-               batch=Z, nb2=B, sa=(B * T * dk, T * dk), sb=(dk, T * 3 * D), sc=(B * T * T, T * T))
-        bd = empty(Z * T * P, like=x2d)
-        K.gemm(T, P, dk, q_v, p, bd, mode_a=K.KC, lda=dk, mode_b=K.KC, ldb=D, ldc=P,
-               batch=Z, nb2=B, sa=(B * T * dk, T * dk), sb=(dk, 0), sc=(B * T * P, T * P))
+        K.gemm(T, T, dk, q_u, qkv, ac, mode_a=K.KC, lda=dk, mode_b=K.KC, ldb=3 * D, ldc=Tp, b_off=D,
+               batch=Z, nb2=B, sa=(B * T * dk, T * dk), sb=(dk, T * 3 * D), sc=(B * T * Tp, T * Tp))
+        bd = empty(Z * T * Pp, like=x2d)
+        K.gemm(T, P, dk, q_v, p, bd, mode_a=K.KC, lda=dk, mode_b=K.KC, ldb=D, ldc=Pp,
+               batch=Z, nb2=B, sa=(B * T * dk, T * dk), sb=(dk, 0), sc=(B * T * Pp, T * Pp))
         pa = self.p if training else 0.0
         sa = seeds.next()
-        pdrop = empty(Z * T * T, like=x2d) if pa > 0 else None
-        K.attn_softmax_fwd(ac, bd, relpos, P, math.sqrt(dk), klen, B, False, ac, pdrop, pa, sa, Z, T, T)
+        pdrop = empty(Z * T * Tp, like=x2d) if pa > 0 else None
+        K.attn_softmax_fwd(ac, bd, relpos, P, math.sqrt(dk), klen, B, False, ac, pdrop, pa, sa, Z, T, T,
+                           lds=Tp, ldp=Pp)
         del bd
         attn = ac
         pv = pdrop if pdrop is not None else attn
         ctx_ = empty(M, D, like=x2d)
-        K.gemm(T, dk, T, pv, qkv, ctx_, mode_a=K.KC, lda=T, mode_b=K.RC, ldb=3 * D, ldc=D, b_off=2 * D,
-               batch=Z, nb2=B, sa=(B * T * T, T * T), sb=(dk, T * 3 * D), sc=(dk, T * D))
+        K.gemm(T, dk, T, pv, qkv, ctx_, mode_a=K.KC, lda=Tp, mode_b=K.RC, ldb=3 * D, ldc=D, b_off=2 * D,
+               batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * 3 * D), sc=(dk, T * D))
         out = empty(M, D, like=x2d)
         pr = p_res if training else 0.0
         so = seeds.next()
@@ -215,33 +217,34 @@ class RelPositionMultiHeadedAttention(nn.Module):
         K.scale_dropout(dout, dz, drop_p=c.pr, seed=c.so)
         dctx = self.linear_out.bwd(dz, c.ctx)
         dqkv = empty(M, 3 * D, like=dout)
+        Tp, Pp = K.pitch(T), K.pitch(P)
         # dP = dctx v^T  (into a (Z,T,T) buffer)
-        dS = empty(Z * T * T, like=dout)
-        K.gemm(T, T, dk, dctx, c.qkv, dS, mode_a=K.KC, lda=D, mode_b=K.KC, ldb=3 * D, ldc=T, b_off=2 * D,
-               batch=Z, nb2=B, sa=(dk, T * D), sb=(dk, T * 3 * D), sc=(B * T * T, T * T))
+        dS = empty(Z * T * Tp, like=dout)
+        K.gemm(T, T, dk, dctx, c.qkv, dS, mode_a=K.KC, lda=D, mode_b=K.KC, ldb=3 * D, ldc=Tp, b_off=2 * D,
+               batch=Z, nb2=B, sa=(dk, T * D), sb=(dk, T * 3 * D), sc=(B * T * Tp, T * Tp))
         # dV = pv^T dctx -> dqkv[:, 2D:3D]
-        K.gemm(T, dk, T, c.pv, dctx, dqkv, mode_a=K.RC, lda=T, mode_b=K.RC, ldb=D, ldc=3 * D, c_off=2 * D,
-               batch=Z, nb2=B, sa=(B * T * T, T * T), sb=(dk, T * D), sc=(dk, T * 3 * D))
-        K.attn_softmax_bwd(c.attn, dS, dS, c.pa, c.sa, math.sqrt(dk), Z * T, T)
-        dbd = empty(Z * T * P, like=dout)
-        K.relshift_bwd(dS, dbd, relpos, Z, T, P)
+        K.gemm(T, dk, T, c.pv, dctx, dqkv, mode_a=K.RC, lda=Tp, mode_b=K.RC, ldb=D, ldc=3 * D, c_off=2 * D,
+               batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * D), sc=(dk, T * 3 * D))
+        K.attn_softmax_bwd(c.attn, dS, dS, c.pa, c.sa, math.sqrt(dk), Z * T, T, lds=Tp)
+        dbd = empty(Z * T * Pp, like=dout)
+        K.relshift_bwd(dS, dbd, relpos, Z, T, P, lds=Tp, ldp=Pp)
         # dq_u = dS k -> dqkv[:, 0:D]
-        K.gemm(T, dk, T, dS, c.qkv, dqkv, mode_a=K.KC, lda=T, mode_b=K.RC, ldb=3 * D, ldc=3 * D, b_off=D,
-               batch=Z, nb2=B, sa=(B * T * T, T * T), sb=(dk, T * 3 * D), sc=(dk, T * 3 * D))
+        K.gemm(T, dk, T, dS, c.qkv, dqkv, mode_a=K.KC, lda=Tp, mode_b=K.RC, ldb=3 * D, ldc=3 * D, b_off=D,
+               batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * 3 * D), sc=(dk, T * 3 * D))
         # dk = dS^T q_u -> dqkv[:, D:2D]
-        K.gemm(T, dk, T, dS, c.q_u, dqkv, mode_a=K.RC, lda=T, mode_b=K.RC, ldb=dk, ldc=3 * D, c_off=D,
-               batch=Z, nb2=B, sa=(B * T * T, T * T), sb=(B * T * dk, T * dk), sc=(dk, T * 3 * D))
+        K.gemm(T, dk, T, dS, c.q_u, dqkv, mode_a=K.RC, lda=Tp, mode_b=K.RC, ldb=dk, ldc=3 * D, c_off=D,
+               batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(B * T * dk, T * dk), sc=(dk, T * 3 * D))
         K.colsum(dqkv, self.pos_bias_u.grad.view(-1), accumulate=True, M=M, N=D, ld=3 * D)
         # dq_v = dbd p -> tmp
         tmp = empty(M, D, like=dout)
-        K.gemm(T, dk, P, dbd, c.p, tmp, mode_a=K.KC, lda=P, mode_b=K.RC, ldb=D, ldc=D,
-               batch=Z, nb2=B, sa=(B * T * P, T * P), sb=(dk, 0), sc=(dk, T * D))
+        K.gemm(T, dk, P, dbd, c.p, tmp, mode_a=K.KC, lda=Pp, mode_b=K.RC, ldb=D, ldc=D,
+               batch=Z, nb2=B, sa=(B * T * Pp, T * Pp), sb=(dk, 0), sc=(dk, T * D))
         K.colsum(tmp, self.pos_bias_v.grad.view(-1), accumulate=True)
         K.add2d(tmp, D, dqkv, 3 * D, M, D)
         # dp[:, h] = sum_b dbd[h,b]^T q_v[h,b]   (K = B*T)
         dp = empty(P, D, like=dout)
-        K.gemm(P, dk, B * T, dbd, c.q_v, dp, mode_a=K.RC, lda=P, mode_b=K.RC, ldb=dk, ldc=D,
-               batch=H, nb2=1, sa=(B * T * P, 0), sb=(B * T * dk, 0), sc=(dk, 0))
+        K.gemm(P, dk, B * T, dbd, c.q_v, dp, mode_a=K.RC, lda=Pp, mode_b=K.RC, ldb=dk, ldc=D,
+               batch=H, nb2=1, sa=(B * T * Pp, 0), sb=(B * T * dk, 0), sc=(dk, 0))
         # linear_pos weight grad only (pos_emb is a constant table)
         K.gemm(D, D, P, dp, c.pos, self.linear_pos.weight.grad, mode_a=K.RC, lda=D, mode_b=K.RC, ldb=D, ldc=D,
                R=self.linear_pos.weight.grad, beta=1.0)
@@ -295,17 +298,18 @@ class MultiHeadedAttention(nn.Module):
             K.linear_fwd(mem, w, b, kv)
             qb, qld, qoff = qkv, D, 0
             kvb, kvld, koff, voff = kv, 2 * D, 0, D
-        sc = empty(Z * Tq * Tk, like=xq)
-        K.gemm(Tq, Tk, dk, qb, kvb, sc, mode_a=K.KC, lda=qld, mode_b=K.KC, ldb=kvld, ldc=Tk, a_off=qoff, b_off=koff,
-               batch=Z, nb2=B, sa=(dk, Tq * qld), sb=(dk, Tk * kvld), sc=(B * Tq * Tk, Tq * Tk))
+        Tkp = K.pitch(Tk)
+        sc = empty(Z * Tq * Tkp, like=xq)
+        K.gemm(Tq, Tk, dk, qb, kvb, sc, mode_a=K.KC, lda=qld, mode_b=K.KC, ldb=kvld, ldc=Tkp, a_off=qoff, b_off=koff,
+               batch=Z, nb2=B, sa=(dk, Tq * qld), sb=(dk, Tk * kvld), sc=(B * Tq * Tkp, Tq * Tkp))
         pa = self.p if training else 0.0
         sa = seeds.next()
-        pdrop = empty(Z * Tq * Tk, like=xq) if pa > 0 else None
-        K.attn_softmax_fwd(sc, None, 0, 0, math.sqrt(dk), klen, B, causal, sc, pdrop, pa, sa, Z, Tq, Tk)
+        pdrop = empty(Z * Tq * Tkp, like=xq) if pa > 0 else None
+        K.attn_softmax_fwd(sc, None, 0, 0, math.sqrt(dk), klen, B, causal, sc, pdrop, pa, sa, Z, Tq, Tk, lds=Tkp)
         pv = pdrop if pdrop is not None else sc
         ctx_ = empty(B * Tq, D, like=xq)
-        K.gemm(Tq, dk, Tk, pv, kvb, ctx_, mode_a=K.KC, lda=Tk, mode_b=K.RC, ldb=kvld, ldc=D, b_off=voff,
-               batch=Z, nb2=B, sa=(B * Tq * Tk, Tq * Tk), sb=(dk, Tk * kvld), sc=(dk, Tq * D))
+        K.gemm(Tq, dk, Tk, pv, kvb, ctx_, mode_a=K.KC, lda=Tkp, mode_b=K.RC, ldb=kvld, ldc=D, b_off=voff,
+               batch=Z, nb2=B, sa=(B * Tq * Tkp, Tq * Tkp), sb=(dk, Tk * kvld), sc=(dk, Tq * D))
         out = empty(B * Tq, D, like=xq)
         pr = p_res if training else 0.0
         so = seeds.next()
@@ -335,16 +339,17 @@ class MultiHeadedAttention(nn.Module):
             dkvld, dkoff, dvoff = 2 * D, 0, D
             kvb, kvld, koff, voff = c.kv, 2 * D, 0, D
             qb, qld, qoff = c.qkv, D, 0
-        dS = empty(Z * Tq * Tk, like=dout)
-        K.gemm(Tq, Tk, dk, dctx, kvb, dS, mode_a=K.KC, lda=D, mode_b=K.KC, ldb=kvld, ldc=Tk, b_off=voff,
-               batch=Z, nb2=B, sa=(dk, Tq * D), sb=(dk, Tk * kvld), sc=(B * Tq * Tk, Tq * Tk))
-        K.gemm(Tk, dk, Tq, c.pv, dctx, dkv, mode_a=K.RC, lda=Tk, mode_b=K.RC, ldb=D, ldc=dkvld, c_off=dvoff,
-               batch=Z, nb2=B, sa=(B * Tq * Tk, Tq * Tk), sb=(dk, Tq * D), sc=(dk, Tk * dkvld))
-        K.attn_softmax_bwd(c.attn, dS, dS, c.pa, c.sa, math.sqrt(dk), Z * Tq, Tk)
-        K.gemm(Tq, dk, Tk, dS, kvb, dq_buf, mode_a=K.KC, lda=Tk, mode_b=K.RC, ldb=kvld, ldc=dqld, b_off=koff,
-               c_off=dqoff, batch=Z, nb2=B, sa=(B * Tq * Tk, Tq * Tk), sb=(dk, Tk * kvld), sc=(dk, Tq * dqld))
-        K.gemm(Tk, dk, Tq, dS, qb, dkv, mode_a=K.RC, lda=Tk, mode_b=K.RC, ldb=qld, ldc=dkvld, a_off=0, b_off=qoff,
-               c_off=dkoff, batch=Z, nb2=B, sa=(B * Tq * Tk, Tq * Tk), sb=(dk, Tq * qld), sc=(dk, Tk * dkvld))
+        Tkp = K.pitch(Tk)
+        dS = empty(Z * Tq * Tkp, like=dout)
+        K.gemm(Tq, Tk, dk, dctx, kvb, dS, mode_a=K.KC, lda=D, mode_b=K.KC, ldb=kvld, ldc=Tkp, b_off=voff,
+               batch=Z, nb2=B, sa=(dk, Tq * D), sb=(dk, Tk * kvld), sc=(B * Tq * Tkp, Tq * Tkp))
+        K.gemm(Tk, dk, Tq, c.pv, dctx, dkv, mode_a=K.RC, lda=Tkp, mode_b=K.RC, ldb=D, ldc=dkvld, c_off=dvoff,
+               batch=Z, nb2=B, sa=(B * Tq * Tkp, Tq * Tkp), sb=(dk, Tq * D), sc=(dk, Tk * dkvld))
+        K.attn_softmax_bwd(c.attn, dS, dS, c.pa, c.sa, math.sqrt(dk), Z * Tq, Tk, lds=Tkp)
+        K.gemm(Tq, dk, Tk, dS, kvb, dq_buf, mode_a=K.KC, lda=Tkp, mode_b=K.RC, ldb=kvld, ldc=dqld, b_off=koff,
+               c_off=dqoff, batch=Z, nb2=B, sa=(B * Tq * Tkp, Tq * Tkp), sb=(dk, Tk * kvld), sc=(dk, Tq * dqld))
+        K.gemm(Tk, dk, Tq, dS, qb, dkv, mode_a=K.RC, lda=Tkp, mode_b=K.RC, ldb=qld, ldc=dkvld, a_off=0, b_off=qoff,
+               c_off=dkoff, batch=Z, nb2=B, sa=(B * Tq * Tkp, Tq * Tkp), sb=(dk, Tq * qld), sc=(dk, Tk * dkvld))
         if c.mem is None:
             w, _ = self._w(("linear_q", "linear_k", "linear_v"))
             gw, gb = self._w(("linear_q", "linear_k", "linear_v"), grad=True)

@@ -45,7 +45,7 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(const float* ac, const
                                                           int P, float sqrt_dk, const int* __restrict__ klen, int nb,
                                                           int causal, float* attn, float* __restrict__ pdrop,
                                                           uint32_t thr, float dscale, uint64_t seed, int Z, int Tq,
-                                                          int Tk) {
+                                                          int Tk, long lds, long ldp) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= (long)Z * Tq) return;
@@ -54,8 +54,8 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(const float* ac, const
   const int b = z % nb;  // z = h*nb + b
   int kl = klen ? klen[b] : Tk;
   if (kl > Tk) kl = Tk;
-  const float* acr = ac + row * Tk;
-  const float* bdz = bd ? bd + (long)z * Tq * P : nullptr;
+  const float* acr = ac + row * lds;
+  const float* bdz = bd ? bd + (long)z * Tq * ldp : nullptr;
   float v[PER];
   float mx = -INFINITY;
 #pragma unroll
@@ -65,10 +65,10 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(const float* ac, const
     if (j < Tk && j < kl && !(causal && j > i)) {
       float a = acr[j];
       if (relpos == 1) {
-        a += bdz[(long)i * P + (j + Tq - 1 - i)];
+        a += bdz[(long)i * ldp + (j + Tq - 1 - i)];
       } else if (relpos == 2) {
-        if (j <= i) a += bdz[(long)i * P + (j + Tq - 1 - i)];
-        else if (j > i + 1) a += bdz[(long)(i + 1) * P + (j - i - 2)];
+        if (j <= i) a += bdz[(long)i * ldp + (j + Tq - 1 - i)];
+        else if (j > i + 1) a += bdz[(long)(i + 1) * ldp + (j - i - 2)];
         else a += 0.f;
       }
       s = a / sqrt_dk;
@@ -86,8 +86,8 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(const float* ac, const
   }
   sum = esp::wave_sum(sum);
   const float inv = sum > 0.f ? 1.0f / sum : 0.f;
-  float* ar = attn + row * Tk;
-  float* pr = pdrop ? pdrop + row * Tk : nullptr;
+  float* ar = attn + row * lds;
+  float* pr = pdrop ? pdrop + row * lds : nullptr;
 #pragma unroll
   for (int e = 0; e < PER; ++e) {
     const int j = lane + 64 * e;
@@ -103,12 +103,12 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(const float* ac, const
 template <int PER>
 __global__ __launch_bounds__(256) void softmax_bwd_kernel(const float* __restrict__ attn, const float* dP, float* dS,
                                                           uint32_t thr, float dscale, uint64_t seed, float sqrt_dk,
-                                                          long rows, int Tk) {
+                                                          long rows, int Tk, long lds) {
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
-  const float* ar = attn + row * Tk;
-  const float* gr = dP + row * Tk;
+  const float* ar = attn + row * lds;
+  const float* gr = dP + row * lds;
   float a[PER], g[PER];
   float dot = 0.f;
 #pragma unroll
@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(const float* __restric
     dot += a[e] * g[e];
   }
   dot = esp::wave_sum(dot);
-  float* sr = dS + row * Tk;
+  float* sr = dS + row * lds;
 #pragma unroll
   for (int e = 0; e < PER; ++e) {
     const int j = lane + 64 * e;
@@ -133,25 +133,25 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(const float* __restric
   }
 }
 
-// adjoint of the rel_shift gather: dbd (Z,T,P) from dS (Z,T,T)
-__global__ void relshift_bwd_kernel(const float* __restrict__ dS, float* __restrict__ dbd, int relpos, int Z, int T,
-                                    int P) {
+// adjoint of the rel_shift gather: dbd (Z,T,P) [pitch ldp] from dS (Z,T,T) [pitch lds]
+__global__ void relshift_bwd_kernel(const float* __restrict__ dS, long lds, float* __restrict__ dbd, long ldp,
+                                    int relpos, int Z, int T, int P) {
   const long n = (long)Z * T * P;
   for (long idx = blockIdx.x * (long)blockDim.x + threadIdx.x; idx < n; idx += (long)gridDim.x * blockDim.x) {
     const int k = (int)(idx % P);
     const long r = idx / P;
     const int i = (int)(r % T);
     const long z = r / T;
-    const float* dz = dS + z * T * T;
+    const float* dz = dS + z * T * lds;
     float v = 0.f;
     if (relpos == 1) {
       const int j = k - (T - 1 - i);
-      if (j >= 0 && j < T) v = dz[(long)i * T + j];
+      if (j >= 0 && j < T) v = dz[(long)i * lds + j];
     } else {
-      if (k >= T - 1 - i) v = dz[(long)i * T + (k - T + 1 + i)];
-      else if (i >= 1 && k + i + 1 < T) v = dz[(long)(i - 1) * T + (k + i + 1)];
+      if (k >= T - 1 - i) v = dz[(long)i * lds + (k - T + 1 + i)];
+      else if (i >= 1 && k + i + 1 < T) v = dz[(long)(i - 1) * lds + (k + i + 1)];
     }
-    dbd[idx] = v;
+    dbd[r * ldp + k] = v;
   }
 }
 
@@ -183,13 +183,15 @@ ESP_API int esp_add2d(const float* x, long ldx, float* y, long ldy, int M, int N
 }
 
 // relpos: 0 none, 1 latest (P=2T-1), 2 legacy (P=T). ac may alias attn (in-place).
+// lds: row pitch of ac/attn/pdrop (>= Tk), ldp: row pitch of bd (>= P).
 ESP_API int esp_attn_softmax_fwd(const float* ac, const float* bd, int relpos, int P, float sqrt_dk, const int* klen,
                                  int nb, int causal, float* attn, float* pdrop, float drop_p, unsigned long long seed,
-                                 int Z, int Tq, int Tk, void* stream) {
+                                 int Z, int Tq, int Tk, long lds, long ldp, void* stream) {
   ESP_ARG_CHECK(Tk <= 1024, "esp_attn_softmax_fwd: Tk=%d > 1024", Tk);
   ESP_ARG_CHECK(relpos == 0 || (Tq == Tk && bd), "esp_attn_softmax_fwd: rel-pos needs Tq==Tk and bd");
   ESP_ARG_CHECK(relpos != 1 || P == 2 * Tq - 1, "esp_attn_softmax_fwd: latest rel-pos needs P=2T-1");
   ESP_ARG_CHECK(relpos != 2 || P == Tq, "esp_attn_softmax_fwd: legacy rel-pos needs P=T");
+  ESP_ARG_CHECK(lds >= Tk && (relpos == 0 || ldp >= P), "esp_attn_softmax_fwd: pitch < row length");
   const uint32_t thr = drop_threshold(drop_p);
   if (!thr) pdrop = nullptr;
   const float ds = thr ? 1.f / (1.f - drop_p) : 1.f;
@@ -198,7 +200,7 @@ ESP_API int esp_attn_softmax_fwd(const float* ac, const float* bd, int relpos, i
   hipStream_t st = (hipStream_t)stream;
 #define ESP_SM(PER)                                                                                                 \
   hipLaunchKernelGGL(softmax_fwd_kernel<PER>, grid, dim3(256), 0, st, ac, bd, relpos, P, sqrt_dk, klen, nb, causal, \
-                     attn, pdrop, thr, ds, (uint64_t)seed, Z, Tq, Tk)
+                     attn, pdrop, thr, ds, (uint64_t)seed, Z, Tq, Tk, lds, ldp)
   if (Tk <= 64) ESP_SM(1);
   else if (Tk <= 128) ESP_SM(2);
   else if (Tk <= 256) ESP_SM(4);
@@ -210,14 +212,15 @@ ESP_API int esp_attn_softmax_fwd(const float* ac, const float* bd, int relpos, i
 }
 
 ESP_API int esp_attn_softmax_bwd(const float* attn, const float* dP, float* dS, float drop_p, unsigned long long seed,
-                                 float sqrt_dk, long rows, int Tk, void* stream) {
+                                 float sqrt_dk, long rows, int Tk, long lds, void* stream) {
   ESP_ARG_CHECK(Tk <= 1024, "esp_attn_softmax_bwd: Tk too large");
+  ESP_ARG_CHECK(lds >= Tk, "esp_attn_softmax_bwd: pitch < Tk");
   const uint32_t thr = drop_threshold(drop_p);
   const float ds = thr ? 1.f / (1.f - drop_p) : 1.f;
   dim3 grid((unsigned)((rows + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
 #define ESP_SB(PER) \
-  hipLaunchKernelGGL(softmax_bwd_kernel<PER>, grid, dim3(256), 0, st, attn, dP, dS, thr, ds, (uint64_t)seed, sqrt_dk, rows, Tk)
+  hipLaunchKernelGGL(softmax_bwd_kernel<PER>, grid, dim3(256), 0, st, attn, dP, dS, thr, ds, (uint64_t)seed, sqrt_dk, rows, Tk, lds)
   if (Tk <= 64) ESP_SB(1);
   else if (Tk <= 128) ESP_SB(2);
   else if (Tk <= 256) ESP_SB(4);
@@ -228,10 +231,12 @@ ESP_API int esp_attn_softmax_bwd(const float* attn, const float* dP, float* dS, 
   return 0;
 }
 
-ESP_API int esp_relshift_bwd(const float* dS, float* dbd, int relpos, int Z, int T, int P, void* stream) {
+ESP_API int esp_relshift_bwd(const float* dS, long lds, float* dbd, long ldp, int relpos, int Z, int T, int P,
+                             void* stream) {
   ESP_ARG_CHECK(relpos == 1 || relpos == 2, "esp_relshift_bwd: relpos must be 1 or 2");
-  hipLaunchKernelGGL(relshift_bwd_kernel, dim3(gridn((long)Z * T * P)), dim3(256), 0, (hipStream_t)stream, dS, dbd,
-                     relpos, Z, T, P);
+  ESP_ARG_CHECK(lds >= T && ldp >= P, "esp_relshift_bwd: pitch < row length");
+  hipLaunchKernelGGL(relshift_bwd_kernel, dim3(gridn((long)Z * T * P)), dim3(256), 0, (hipStream_t)stream, dS, lds,
+                     dbd, ldp, relpos, Z, T, P);
   ESP_CHECK_LAUNCH("esp_relshift_bwd");
   return 0;
 }

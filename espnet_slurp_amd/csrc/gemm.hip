@@ -56,6 +56,7 @@ struct GemmArgs {
   int batch;
   int splits, kchunk;  // split-K: blockIdx.z = z*splits + split; partials -> work
   float* work;
+  int bnt;  // LDS-DMA kernel tile width (128, or 64 for narrow / mid-size grids); 0 = fallback kernel
 };
 
 // fused epilogue for output element (z, m, n) with raw accumulator `acc`
@@ -684,9 +685,10 @@ void launch_glds(const GemmArgs& g, int batch, hipStream_t st) {
 template <int MA, int MB>
 int launch(const GemmArgs& g, int batch, hipStream_t st) {
   dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, batch * g.splits);
-  if (variant() == 4 && g.a.glds && g.b.glds) {
-    if (g.N <= 64) launch_glds<MA, MB, 64>(g, batch, st);
-    else launch_glds<MA, MB, 128>(g, batch, st);
+  if (g.bnt == 64) {
+    launch_glds<MA, MB, 64>(g, batch, st);
+  } else if (g.bnt == 128) {
+    launch_glds<MA, MB, 128>(g, batch, st);
   } else if (variant() == 0) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 0>), grid, dim3(NT), 0, st, g);
   else if (variant() == 2) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 2>), grid, dim3(NT), 0, st, g);
   else if (variant() == 3) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 3>), grid, dim3(NT), 0, st, g);
@@ -754,16 +756,23 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
     if (g.drop_thresh == 0) g.drop_thresh = 1;
     g.drop_scale = 1.0f / (1.0f - drop_p);
   }
-  // split-K when the tile grid cannot fill the 256 CUs (weight gradients: small M x N, huge K)
+  // Tile choice: the LDS-DMA kernel when both operands allow it, 128x64 tiles when N <= 64
+  // or when 128x128 tiles leave the grid under two blocks per CU but 128x64 tiles do not
+  // (e.g. N = 256 over 23936 rows: 374 -> 748 tiles, no split-K reduction pass needed).
+  // Then split-K when the grid still cannot fill the 256 CUs (weight gradients: small
+  // M x N, huge K).
   g.batch = batch;
   g.splits = 1;
   g.kchunk = K;
+  const long target = 2 * 256;
+  auto ntiles = [&](int bn) { return (long)((N + bn - 1) / bn) * ((M + BM - 1) / BM) * batch; };
+  g.bnt = 0;
+  if (variant() == 4 && g.a.glds && g.b.glds) {
+    g.bnt = N <= 64 ? 64 : 128;
+    if (g.bnt == 128 && ntiles(128) < target && ntiles(64) >= target) g.bnt = 64;
+  }
   {
-    const long tiles = (long)((N + BN - 1) / BN) * ((M + BM - 1) / BM) * batch;
-    // target two blocks per CU.  Measured (tools/gemm_bench.py, B=64 FFN w2 M=23936 N=256
-    // K=1024): split 2 + reduce 153 us vs no split 191 us, although the reduce pass alone is
-    // ~20% of the GEMM's GRBM_GUI_ACTIVE cycles
-    const long target = 2 * 256;
+    const long tiles = ntiles(g.bnt ? g.bnt : BN);
     if (work && tiles < target && K >= 2 * 128) {
       long sp = (target + tiles - 1) / tiles;
       const long by_k = K / 128;  // keep >= 8 slabs of BK per split

@@ -268,18 +268,25 @@ def add2d(x, ldx, y, ldy, M, N, x_off=0, y_off=0):
     _native.call("esp_add2d", _p(x, x_off), ldx, _p(y, y_off), ldy, M, N, _st())
 
 
-def attn_softmax_fwd(ac, bd, relpos, P, sqrt_dk, klen_i32, nb, causal, attn, pdrop, drop_p, seed, Z, Tq, Tk):
+def pitch(n: int) -> int:
+    """Row pitch of score-like buffers: a multiple of 4 floats, so every row is 16-B aligned
+    and the GEMMs reading them take the LDS-DMA path."""
+    return (n + 3) & ~3
+
+
+def attn_softmax_fwd(ac, bd, relpos, P, sqrt_dk, klen_i32, nb, causal, attn, pdrop, drop_p, seed, Z, Tq, Tk,
+                     lds=None, ldp=None):
     _native.call("esp_attn_softmax_fwd", _p(ac), _p(bd), relpos, P, float(sqrt_dk), _p(klen_i32), nb, int(causal),
-                 _p(attn), _p(pdrop), float(drop_p), seed, Z, Tq, Tk, _st())
+                 _p(attn), _p(pdrop), float(drop_p), seed, Z, Tq, Tk, lds or Tk, ldp or max(P, 1), _st())
 
 
-def attn_softmax_bwd(attn, dP, dS, drop_p, seed, sqrt_dk, rows, Tk):
+def attn_softmax_bwd(attn, dP, dS, drop_p, seed, sqrt_dk, rows, Tk, lds=None):
     _native.call("esp_attn_softmax_bwd", _p(attn), _p(dP), _p(dS), float(drop_p), seed, float(sqrt_dk), rows, Tk,
-                 _st())
+                 lds or Tk, _st())
 
 
-def relshift_bwd(dS, dbd, relpos, Z, T, P):
-    _native.call("esp_relshift_bwd", _p(dS), _p(dbd), relpos, Z, T, P, _st())
+def relshift_bwd(dS, dbd, relpos, Z, T, P, lds=None, ldp=None):
+    _native.call("esp_relshift_bwd", _p(dS), lds or T, _p(dbd), ldp or P, relpos, Z, T, P, _st())
 
 
 # ----------------------------------------------------------------------------- subsampling

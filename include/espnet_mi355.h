@@ -90,12 +90,18 @@ int esp_bn_swish_bwd(const float* ds, const float* y, const float* mean, const f
 int esp_heads_split(const float* src, long ld, int col0, int B, int T, int H, int dk,
                     const float* bias, float* dst, void* stream);
 int esp_add2d(const float* x, long ldx, float* y, long ldy, int M, int N, void* stream);
+/* score rows (ac / attn / pdrop / dP / dS) have pitch lds >= Tk, bd / dbd rows pitch ldp >= P
+ * (multiples of 4 keep every row 16-B aligned for the GEMMs' LDS-DMA staging); dropout
+ * masks are keyed by the logical index row*Tk + j, independent of the pitch. */
 int esp_attn_softmax_fwd(const float* ac, const float* bd, int relpos, int P, float sqrt_dk,
                          const int* klen, int nb, int causal, float* attn, float* pdrop,
-                         float drop_p, unsigned long long seed, int Z, int Tq, int Tk, void* stream);
+                         float drop_p, unsigned long long seed, int Z, int Tq, int Tk, long lds,
+                         long ldp, void* stream);
 int esp_attn_softmax_bwd(const float* attn, const float* dP, float* dS, float drop_p,
-                         unsigned long long seed, float sqrt_dk, long rows, int Tk, void* stream);
-int esp_relshift_bwd(const float* dS, float* dbd, int relpos, int Z, int T, int P, void* stream);
+                         unsigned long long seed, float sqrt_dk, long rows, int Tk, long lds,
+                         void* stream);
+int esp_relshift_bwd(const float* dS, long lds, float* dbd, long ldp, int relpos, int Z, int T, int P,
+                     void* stream);
 
 /* ---- Conv2dSubsampling (subsampling.py:53-87), NHWC */
 int esp_conv1_fwd(const float* x, const float* W, const float* bias, float* z, int B, int T,

@@ -250,8 +250,9 @@ def test_conv_module_pieces(dev):
     assert rel_err(du.cpu(), ut.grad) < 1e-5
 
 
+@pytest.mark.parametrize("padded", [False, True])
 @pytest.mark.parametrize("legacy", [False, True])
-def test_relpos_softmax_and_adjoint(dev, legacy):
+def test_relpos_softmax_and_adjoint(dev, legacy, padded):
     Z, T, dk, nb = 6, 45, 16, 3
     P = T if legacy else 2 * T - 1
     ac = _r(Z, T, T, seed=22)
@@ -266,17 +267,25 @@ def test_relpos_softmax_and_adjoint(dev, legacy):
     attn = torch.softmax(sc.masked_fill(~mask, minv), -1).masked_fill(~mask, 0.0)
     dP = _r(Z, T, T, seed=24)
     attn.backward(dP.double())
-    acd = ac.to(dev).contiguous()
-    att = torch.empty(Z * T * T, device=dev)
-    K.attn_softmax_fwd(acd, bd.to(dev), 2 if legacy else 1, P, math.sqrt(dk), klen.to(dev), nb, False, att, None,
-                       0.0, 0, Z, T, T)
-    assert rel_err(att.cpu().view(Z, T, T), attn.detach()) < 1e-5
-    dS = dP.to(dev).contiguous()
-    K.attn_softmax_bwd(att, dS, dS, 0.0, 0, math.sqrt(dk), Z * T, T)
-    assert rel_err(dS.cpu().view(Z, T, T), act.grad) < 1e-5
-    dbd = torch.empty(Z * T * P, device=dev)
-    K.relshift_bwd(dS, dbd, 2 if legacy else 1, Z, T, P)
-    assert rel_err(dbd.cpu().view(Z, T, P), bdt.grad) < 1e-5
+    # padded: rows live at a pitch > length (the layout the model uses, K.pitch + 4 here)
+    Tp, Pp = (K.pitch(T) + 4, K.pitch(P) + 4) if padded else (T, P)
+
+    def put(x, n, pitch):
+        buf = torch.full((x.shape[0], x.shape[1], pitch), float("nan"))
+        buf[:, :, :n] = x
+        return buf.to(dev).contiguous()
+
+    acd = put(ac, T, Tp)
+    att = torch.full((Z * T * Tp,), float("nan"), device=dev)
+    K.attn_softmax_fwd(acd, put(bd, P, Pp), 2 if legacy else 1, P, math.sqrt(dk), klen.to(dev), nb, False, att, None,
+                       0.0, 0, Z, T, T, lds=Tp, ldp=Pp)
+    assert rel_err(att.cpu().view(Z, T, Tp)[:, :, :T], attn.detach()) < 1e-5
+    dS = put(dP, T, Tp)
+    K.attn_softmax_bwd(att, dS, dS, 0.0, 0, math.sqrt(dk), Z * T, T, lds=Tp)
+    assert rel_err(dS.cpu().view(Z, T, Tp)[:, :, :T], act.grad) < 1e-5
+    dbd = torch.empty(Z * T * Pp, device=dev)
+    K.relshift_bwd(dS, dbd, 2 if legacy else 1, Z, T, P, lds=Tp, ldp=Pp)
+    assert rel_err(dbd.cpu().view(Z, T, Pp)[:, :, :P], bdt.grad) < 1e-5
 
 
 def test_causal_softmax_with_dropout(dev):

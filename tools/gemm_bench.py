@@ -20,20 +20,44 @@ SHAPES = [  # (mode_a, mode_b, M, N, K, batch, label)
     (0, 0, 374, 374, 64, 256, "scores ac"),
     (0, 1, 374, 64, 374, 256, "ctx = P V"),
     (1, 1, 374, 64, 374, 256, "dV / dk"),
+    (0, 1, 374, 64, 374, 256, "ctx pad376", 376),
+    (1, 1, 374, 64, 374, 256, "dV pad376", 376),
+    (0, 0, 374, 374, 64, 256, "scores ldc376", 376),
+    (1, 3, 256, 2304, 64 * 374 * 19, 1, "conv2 dW"),
+    (2, 0, 64 * 374 * 19, 256, 2304, 1, "conv2 fwd"),
+    (0, 1, 64 * 374 * 19, 2304, 256, 1, "conv2 dcol"),
     (0, 1, 64 * 41, 256, 256, 1, "decoder q"),
     (0, 1, 64 * 41, 256, 2048, 1, "decoder ffn w2"),
 ]
 
 
-def run(ma, mb, m, n, k, batch, reps=20):
+def run(ma, mb, m, n, k, batch, pad=None, reps=20):
     dev = torch.device("cuda:0")
-    A = torch.randn(batch * m * k, device=dev)
-    B = torch.randn(batch * n * k, device=dev)
-    C = torch.empty(batch * m * n, device=dev)
     lda = k if ma == 0 else m
     ldb = k if mb == 0 else n
-    kw = dict(mode_a=ma, lda=lda, mode_b=mb, ldb=ldb, ldc=n, batch=batch, nb2=1, sa=(m * k, 0), sb=(n * k, 0),
-              sc=(m * n, 0))
+    ldc = n
+    if pad:  # padded pitch on the T-long dims (attention score layouts)
+        if ma == 0 and k == 374:
+            lda = pad
+        if ma == 1 and m == 374:
+            lda = pad
+        if n == 374:
+            ldc = pad
+    ic_a = ic_b = None
+    if ma == 2:  # conv2 forward: NHWC map (B, 749, 39, 256) -> pixels (B*374*19)
+        ic_a = (749, 39, 256, 374, 19)
+        A = torch.randn(64 * 749 * 39 * 256, device=dev)
+    else:
+        A = torch.randn(batch * max(m, lda) * max(k, lda), device=dev) if pad else torch.randn(batch * m * k, device=dev)
+    if mb == 3:
+        ic_b = (749, 39, 256, 374, 19)
+        B = torch.randn(64 * 749 * 39 * 256, device=dev)
+    else:
+        B = torch.randn(batch * n * k, device=dev)
+    C = torch.empty(batch * m * ldc, device=dev)
+    sa = (m * k, 0) if not pad else (A.numel() // batch, 0)
+    kw = dict(mode_a=ma, lda=lda, mode_b=mb, ldb=ldb, ldc=ldc, batch=batch, nb2=1, sa=sa, sb=(n * k, 0),
+              sc=(m * ldc, 0), ic_a=ic_a, ic_b=ic_b)
     for _ in range(3):
         K.gemm(m, n, k, A, B, C, **kw)
     torch.cuda.synchronize()
@@ -70,12 +94,14 @@ def run_torch(ma, mb, m, n, k, batch, reps=20):
 
 if __name__ == "__main__":
     only = [int(a) for a in sys.argv[1:]]
-    for i, (ma, mb, m, n, k, b, lab) in enumerate(SHAPES):
+    for i, sh in enumerate(SHAPES):
+        ma, mb, m, n, k, b, lab = sh[:7]
+        pad = sh[7] if len(sh) > 7 else None
         if only and i not in only:
             continue
-        ms, tf = run(ma, mb, m, n, k, b)
+        ms, tf = run(ma, mb, m, n, k, b, pad)
         line = f"{lab:16s} ({ma},{mb}) M={m:6d} N={n:5d} K={k:6d} b={b:3d}  {ms * 1e3:8.1f} us  {tf:6.1f} TF/s"
-        if os.environ.get("GEMM_BENCH_TORCH"):
+        if os.environ.get("GEMM_BENCH_TORCH") and ma < 2 and mb < 2 and not pad:
             tms, ttf = run_torch(ma, mb, m, n, k, b)
             line += f"   | torch.matmul {tms * 1e3:8.1f} us  {ttf:6.1f} TF/s"
         print(line, flush=True)
