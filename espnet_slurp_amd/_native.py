@@ -22,7 +22,8 @@ U64 = ctypes.c_ulonglong
 SIGNATURES = {
     "esp_last_error": [],
     "esp_abi_version": [],
-    "esp_gemm_f32": [I, I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, L, P, F, F, P, I, P, F, U64, P, P, P, L, P],
+    "esp_gemm_f32": [I, I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, L, P, F, F, P, I, P, F, U64, I, P, P,
+                     P, P, P, L, P],
     "esp_act_bwd": [P, P, P, L, I, F, U64, L, P],
     "esp_scale_dropout": [P, P, L, F, F, U64, P, F, P],
     "esp_scale_by_dev": [P, L, P, P],
@@ -58,7 +59,7 @@ SIGNATURES = {
     "esp_ctc_forced_align": [P, I, I, P, I, I, P, P, P],
 }
 _RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I}
-ABI_VERSION = 3  # bumped whenever a signature in include/espnet_mi355.h changes
+ABI_VERSION = 4  # bumped whenever a signature in include/espnet_mi355.h changes
 
 _lib = None
 

@@ -95,7 +95,7 @@ def draw_seed() -> int:
 
 
 def lengths_to_device(lens: torch.Tensor, device) -> torch.Tensor:
-    return lens.to(torch.int32).to(device, non_blocking=True)
+    return K.h2d(lens.to(torch.int32), device)
 
 
 class EncoderFn(torch.autograd.Function):

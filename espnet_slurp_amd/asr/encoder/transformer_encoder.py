@@ -127,4 +127,8 @@ class TransformerEncoder(AbsEncoder):
             olens = subsampled_lengths(ilens_cpu, feats.shape[1])
         else:
             hs, olens, _ = self.run_forward(feats, ilens_cpu, Seeds(seed), self.training)
-        return hs, olens.to(xs_pad.device), None
+        return hs, K.h2d(olens, xs_pad.device), None
+
+    def output_lengths(self, ilens_cpu: torch.Tensor, T: int) -> torch.Tensor:
+        """Valid output frames per utterance (host, no device round trip)."""
+        return subsampled_lengths(ilens_cpu, T)

@@ -121,13 +121,13 @@ class ESPnetASRModel(AbsESPnetModel):
         B, T, D = hs.shape
         dev = hs.device
         hs2d = hs.reshape(B * T, D)
-        hlens_i32 = hlens_cpu.to(torch.int32).to(dev, non_blocking=True)
+        hlens_i32 = K.h2d(hlens_cpu.to(torch.int32), dev)
         state = {"hs2d": hs2d, "B": B, "T": T}
         nll = grad_ctc = None
         if self.ctc is not None:
             Umax = text_cpu.shape[1]
-            ys = text_cpu.to(dev, non_blocking=True)
-            tl = text_lengths_cpu.to(torch.int32).to(dev, non_blocking=True)
+            ys = K.h2d(text_cpu, dev)
+            tl = K.h2d(text_lengths_cpu.to(torch.int32), dev)
             nll, grad_ctc, _ = self.ctc.loss_and_grad(hs2d, B, T, hlens_i32, ys, tl, Umax,
                                                       self.ctc_weight / B, want_grad=want_grad)
             state["grad_ctc"] = grad_ctc
@@ -140,10 +140,10 @@ class ESPnetASRModel(AbsESPnetModel):
             R = B * L
             if self.length_normalized_loss:
                 denom = float(int((ys_out != self.ignore_id).sum()))
-            ys_in_d = ys_in.to(dev, non_blocking=True)
-            ys_out_d = ys_out.to(dev, non_blocking=True)
+            ys_in_d = K.h2d(ys_in, dev)
+            ys_out_d = K.h2d(ys_out, dev)
             logits, dsaved = self.decoder.run_forward(hs, hlens_i32, ys_in_d,
-                                                      ys_in_lens.to(torch.int32).to(dev, non_blocking=True),
+                                                      K.h2d(ys_in_lens.to(torch.int32), dev),
                                                       seeds, self.training)
             V = self.vocab_size
             grad_att = empty(R, V, like=hs) if want_grad else None
@@ -187,7 +187,10 @@ class ESPnetASRModel(AbsESPnetModel):
         tl_cpu = text_lengths.detach().cpu()
         text_cpu = text.detach().cpu()[:, : int(tl_cpu.max())]
         encoder_out, encoder_out_lens = self.encode(speech, speech_lengths, sl_cpu, specaug_draws)
-        hlens_cpu = encoder_out_lens.detach().cpu()
+        if hasattr(self.encoder, "output_lengths"):  # host-side lengths: no device round trip
+            hlens_cpu = self.encoder.output_lengths(sl_cpu, int(sl_cpu.max()))
+        else:
+            hlens_cpu = encoder_out_lens.detach().cpu()
         seed = draw_seed()
         anchor = next(p for p in (self.ctc or self.decoder).parameters())
         if torch.is_grad_enabled() and anchor.requires_grad:
@@ -203,7 +206,7 @@ class ESPnetASRModel(AbsESPnetModel):
             cer=None, wer=None,
             loss=loss.detach(),
         )
-        weight = torch.tensor([B], dtype=torch.long, device=loss.device)
+        weight = K.h2d(torch.tensor([B], dtype=torch.long), loss.device)
         return loss, stats, weight
 
     def encode(self, speech: torch.Tensor, speech_lengths: torch.Tensor, sl_cpu: Optional[torch.Tensor] = None,

@@ -107,8 +107,8 @@ class SpecAug(AbsSpecAug):
             draws = self.draw(B, T, F, lens.tolist())
         dev = x.device
         y = torch.empty_like(x)
-        K.specaug(x.contiguous(), y, lens.to(torch.int32).to(dev),
-                  draws["warp"].to(dev) if "warp" in draws else None,
-                  draws["fmask"].to(dev) if "fmask" in draws else None,
-                  draws["tmask"].to(dev) if "tmask" in draws else None)
+        K.specaug(x.contiguous(), y, K.h2d(lens.to(torch.int32), dev),
+                  K.h2d(draws["warp"], dev) if "warp" in draws else None,
+                  K.h2d(draws["fmask"], dev) if "fmask" in draws else None,
+                  K.h2d(draws["tmask"], dev) if "tmask" in draws else None)
         return y, x_lengths

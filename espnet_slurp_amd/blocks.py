@@ -131,8 +131,9 @@ class PositionwiseFeedForward(nn.Module):
         """dout: grad w.r.t. the residual output; returns grad w.r.t. x2d (new buffer)."""
         dz = torch.empty_like(dout)
         K.scale_dropout(dout, dz, alpha=c.alpha, drop_p=c.pr, seed=c.s2)
-        dh = self.w_2.bwd(dz, c.h)
-        K.act_bwd(dh, c.pre, dh, self.act, drop_p=c.p_in, seed=c.s1)
+        K.linear_bwd_weight(dz, c.h, self.w_2.weight.grad, self.w_2.bias.grad)
+        dh = torch.empty_like(c.pre)
+        K.linear_bwd_data_act(dz, self.w_2.weight, dh, c.pre, self.act, drop_p=c.p_in, seed=c.s1)
         return self.w_1.bwd(dh, c.x)
 
 
@@ -476,15 +477,14 @@ class Conv2dSubsampling(nn.Module):
         K.linear_bwd_weight(dv, z2f, dwor.view(D, F2 * D), lin.bias.grad)
         K.permute3(dwor, lin.weight.grad, D, F2, D, accumulate=True)  # (n, f, c) -> (n, c, f)
         dz2 = empty(B * T2, F2 * D, like=dx)
-        K.linear_bwd_data(dv, c.wor.view(D, F2 * D), dz2)
-        K.act_bwd(dz2, z2f, dz2, K.ACT_RELU)
+        K.linear_bwd_data_act(dv, c.wor.view(D, F2 * D), dz2, z2f, K.ACT_RELU)  # ReLU' from its output
         npix2 = B * T2 * F2
         dz2p = dz2.view(npix2, D)
         ic = (T1, F1, D, T2, F2)
         dw2r = empty(D, 9 * D, like=dx)
-        K.gemm(D, 9 * D, npix2, dz2p, c.z1, dw2r, mode_a=K.RC, lda=D, mode_b=K.I2C_RC, ldb=0, ldc=9 * D, ic_b=ic)
+        K.gemm(D, 9 * D, npix2, dz2p, c.z1, dw2r, mode_a=K.RC, lda=D, mode_b=K.I2C_RC, ldb=0, ldc=9 * D, ic_b=ic,
+               rowsum=c2.bias.grad)
         K.permute3(dw2r, c2.weight.grad, D, 9, D, accumulate=True)  # (o, kk, c) -> (o, c, kk)
-        K.colsum(dz2p, c2.bias.grad, accumulate=True)
         dcol = empty(npix2, 9 * D, like=dx)
         K.gemm(npix2, 9 * D, D, dz2p, c.w2r, dcol, mode_a=K.KC, lda=D, mode_b=K.RC, ldb=9 * D, ldc=9 * D)
         dz1 = empty(B * T1 * F1 * D, like=dx)

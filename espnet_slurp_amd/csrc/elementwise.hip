@@ -18,7 +18,7 @@ void set_error(const char* fmt, ...) {
 }  // namespace esp
 
 ESP_API const char* esp_last_error(void) { return esp::g_err; }
-ESP_API int esp_abi_version(void) { return 3; }
+ESP_API int esp_abi_version(void) { return 4; }
 
 namespace {
 

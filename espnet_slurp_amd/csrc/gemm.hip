@@ -57,23 +57,140 @@ struct GemmArgs {
   int splits, kchunk;  // split-K: blockIdx.z = z*splits + split; partials -> work
   float* work;
   int bnt;  // LDS-DMA kernel tile width (128, or 64 for narrow / mid-size grids); 0 = fallback kernel
+  int bwd_act;       // != 0: backward epilogue  v = drop'(acc) * act'(pre)  (act code, dropout regenerated)
+  const float* pre;  // pre-activation (same layout as C) for bwd_act
+  float* rowsum;     // != NULL: rowsum[m] += sum_k A(m,k)  (bias gradient of a weight-gradient GEMM)
+  float* rs_work;    // split-K partial row sums [split][M]
 };
 
-// fused epilogue for output element (z, m, n) with raw accumulator `acc`
-__device__ __forceinline__ void epi_store(const GemmArgs& g, int z, int m, int n, float acc) {
-  const int z1 = z / g.nb2, z2 = z - z1 * g.nb2;
-  const long off = (long)z1 * g.c1 + (long)z2 * g.c2 + (long)m * g.ldc + n;
-  float v = acc + (g.bias ? g.bias[n] : 0.f);
-  if (g.aux) g.aux[off] = v;
-  if (g.act == ACT_RELU) v = fmaxf(v, 0.f);
-  else if (g.act == ACT_SWISH) v = v / (1.0f + expf(-v));
-  if (g.drop_thresh) {
-    const uint64_t idx = ((uint64_t)z * g.M + m) * (uint64_t)g.N + n;
-    v = esp::keep_elem(g.seed, idx, g.drop_thresh) ? v * g.drop_scale : 0.f;
+// Fused epilogue for output element (m, n) of batch z with raw accumulator `acc`.  The kind is
+// chosen once per launch (a template argument), so the per-element path is straight-line:
+//   EPI 0: alpha*acc (+ beta*R)
+//   EPI 1: forward  alpha*drop(act(acc + bias)) (+ beta*R), pre-activation to aux
+//   EPI 2: backward  drop'(acc + bias) * act'(pre)  (dropout mask regenerated), alpha, R
+// cbase = offset of batch z in C/R/aux/pre, dbase = z*M*N (dropout index base).
+enum { EPI_PLAIN = 0, EPI_FWD = 1, EPI_BWD = 2 };
+__host__ __device__ inline int epi_kind(const GemmArgs& g) {
+  return g.bwd_act ? EPI_BWD : ((g.bias || g.aux || g.act || g.drop_thresh) ? EPI_FWD : EPI_PLAIN);
+}
+template <int EPI>
+__device__ __forceinline__ void epi_store(const GemmArgs& g, long cbase, uint64_t dbase, int m, int n, float acc) {
+  const long off = cbase + (long)m * g.ldc + n;
+  float v = acc;
+  if constexpr (EPI == EPI_FWD) {
+    if (g.bias) v += g.bias[n];
+    if (g.aux) g.aux[off] = v;
+    if (g.act == ACT_RELU) v = fmaxf(v, 0.f);
+    else if (g.act == ACT_SWISH) v = v / (1.0f + expf(-v));
+    if (g.drop_thresh) {
+      const uint64_t idx = dbase + (uint64_t)m * (uint64_t)g.N + n;
+      v = esp::keep_elem(g.seed, idx, g.drop_thresh) ? v * g.drop_scale : 0.f;
+    }
+  } else if constexpr (EPI == EPI_BWD) {
+    // gradient w.r.t. the pre-activation of  h = drop(act(pre))  given dL/dh = v
+    if (g.bias) v += g.bias[n];
+    if (g.drop_thresh) {
+      const uint64_t idx = dbase + (uint64_t)m * (uint64_t)g.N + n;
+      v = esp::keep_elem(g.seed, idx, g.drop_thresh) ? v * g.drop_scale : 0.f;
+    }
+    const float x = g.pre[off];
+    if (g.bwd_act == ACT_RELU) v = x > 0.f ? v : 0.f;
+    else {
+      const float sg = 1.0f / (1.0f + expf(-x));
+      v = v * (sg * (1.0f + x * (1.0f - sg)));
+    }
   }
   v *= g.alpha;
   if (g.r) v += g.beta * g.r[off];
   g.c[off] = v;
+}
+__device__ __forceinline__ long c_base(const GemmArgs& g, int z) {
+  const int z1 = z / g.nb2, z2 = z - z1 * g.nb2;
+  return (long)z1 * g.c1 + (long)z2 * g.c2;
+}
+
+// store a wave's TM x TN 32x32 accumulator tiles (rows mrow0 + 32i + ..., cols ncol0 + 32j + l32).
+// Per 32x32 tile, every load the epilogue needs (residual R, pre-activation) is issued, in
+// program order, before the tile's first store: R / pre may alias C, so a load placed after a
+// store cannot be hoisted by the compiler and each element would pay a memory round trip.
+template <int EPI, int TM, int TN>
+__device__ __forceinline__ void store_tiles(const GemmArgs& g, int z, int mrow0, int ncol0, int h, int l32,
+                                            const f32x16 (&acc)[TM][TN]) {
+  const long cbase = c_base(g, z);
+  const uint64_t dbase = (uint64_t)z * (uint64_t)g.M * (uint64_t)g.N;
+  const bool has_r = g.r != nullptr;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = ncol0 + j * 32 + l32;
+    if (n >= g.N) continue;
+    const float bn = (EPI != EPI_PLAIN && g.bias) ? g.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      float rr[16], pp[EPI == EPI_BWD ? 16 : 1];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const long off = cbase + (long)m * g.ldc + n;
+        rr[r] = (has_r && m < g.M) ? g.r[off] : 0.f;
+        if constexpr (EPI == EPI_BWD) pp[r] = m < g.M ? g.pre[off] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m >= g.M) continue;
+        const long off = cbase + (long)m * g.ldc + n;
+        float v = acc[i][j][r] + bn;
+        if constexpr (EPI == EPI_FWD) {
+          if (g.aux) g.aux[off] = v;
+          if (g.act == ACT_RELU) v = fmaxf(v, 0.f);
+          else if (g.act == ACT_SWISH) v = v / (1.0f + expf(-v));
+          if (g.drop_thresh) {
+            const uint64_t idx = dbase + (uint64_t)m * (uint64_t)g.N + n;
+            v = esp::keep_elem(g.seed, idx, g.drop_thresh) ? v * g.drop_scale : 0.f;
+          }
+        } else if constexpr (EPI == EPI_BWD) {
+          if (g.drop_thresh) {
+            const uint64_t idx = dbase + (uint64_t)m * (uint64_t)g.N + n;
+            v = esp::keep_elem(g.seed, idx, g.drop_thresh) ? v * g.drop_scale : 0.f;
+          }
+          const float x = pp[r];
+          if (g.bwd_act == ACT_RELU) v = x > 0.f ? v : 0.f;
+          else {
+            const float sg = 1.0f / (1.0f + expf(-x));
+            v = v * (sg * (1.0f + x * (1.0f - sg)));
+          }
+        }
+        v *= g.alpha;
+        if (has_r) v += g.beta * rr[r];
+        g.c[off] = v;
+      }
+    }
+  }
+}
+// split-K partial stores: W[split][z][M][N]
+template <int TM, int TN>
+__device__ __forceinline__ void store_partials(const GemmArgs& g, float* W, int mrow0, int ncol0, int h, int l32,
+                                               const f32x16 (&acc)[TM][TN]) {
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = ncol0 + j * 32 + l32;
+      if (n >= g.N) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (m < g.M) W[(long)m * g.N + n] = acc[i][j][r];
+      }
+    }
+}
+template <int TM, int TN>
+__device__ __forceinline__ void epilogue(const GemmArgs& g, float* W, int z, int mrow0, int ncol0, int h, int l32,
+                                         const f32x16 (&acc)[TM][TN]) {
+  if (W) store_partials<TM, TN>(g, W, mrow0, ncol0, h, l32, acc);
+  else if (g.bwd_act) store_tiles<EPI_BWD, TM, TN>(g, z, mrow0, ncol0, h, l32, acc);
+  else if (g.bias || g.aux || g.act || g.drop_thresh) store_tiles<EPI_FWD, TM, TN>(g, z, mrow0, ncol0, h, l32, acc);
+  else store_tiles<EPI_PLAIN, TM, TN>(g, z, mrow0, ncol0, h, l32, acc);
 }
 
 // address of im2col element: pixel index `pix` of the output grid, column `col` = (kt,kf,c)
@@ -348,20 +465,7 @@ __global__ __launch_bounds__(NT, VARIANT == 3 ? 4 : 2) void gemm_f32_kernel(Gemm
 
 // ---------------------------------------------------------------- epilogue
   float* W = g.splits > 1 ? g.work + ((long)split * g.batch + z) * (long)g.M * g.N : nullptr;  // [split][z][M][N]
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wn * 64 + j * 32 + l32;
-      if (n >= g.N) continue;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (m >= g.M) continue;
-        if (W) W[(long)m * g.N + n] = acc[i][j][r];
-        else epi_store(g, z, m, n, acc[i][j][r]);
-      }
-    }
+  epilogue<2, 2>(g, W, z, m0 + wm * 64, n0 + wn * 64, h, l32, acc);
 }
 
 // ============================================================================ glds kernel
@@ -520,7 +624,7 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int MA, int MB, int BNT>
+template <int MA, int MB, int BNT, bool RS, int EPI>
 __global__ __launch_bounds__(NT, 2) void gemm_glds_kernel(GemmArgs g, GldsArgs x) {
   constexpr int WN = BNT / 64, WM = 4 / WN, TM = BM / (WM * 32), TN = 2;
   constexpr int A_SZ = BM * GL_BK, B_SZ = BNT * GL_BK, BUF = A_SZ + B_SZ;
@@ -563,6 +667,12 @@ __global__ __launch_bounds__(NT, 2) void gemm_glds_kernel(GemmArgs g, GldsArgs x
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  // fused bias gradient (A = dy in RC mode): the first column tile's wn==0 waves sum their A
+  // fragments over k; halves combined and splits reduced in fixed order (deterministic)
+  const bool do_rs = RS && tn == 0 && wn == 0;
+  float rs[TM];
+#pragma unroll
+  for (int t = 0; t < TM; ++t) rs[t] = 0.f;
   const int nk = kend > kbeg ? (kend - kbeg + GL_BK - 1) / GL_BK : 0;
   if (nk > 0) {
     sa.issue(g.a, g.K, kbeg, smem, wave, x.c_a, x.hw_a, x.wo_a);
@@ -598,31 +708,58 @@ __global__ __launch_bounds__(NT, 2) void gemm_glds_kernel(GemmArgs g, GldsArgs x
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+    if constexpr (RS) {
+      if (do_rs) {  // after the MFMAs were issued: the adds ride in their shadow
+#pragma unroll
+        for (int t = 0; t < TM; ++t) {
+          float a0 = 0.f;
+#pragma unroll
+          for (int s = 0; s < 16; ++s) a0 += af[t][s];
+          rs[t] += a0;
+        }
+      }
+    }
     wait_vm0();    // this wave's DMA of slab kt+1 has landed
     wait_lgkm0();  // this wave's reads of slab kt are done
     raw_barrier(); // -> everyone's: slab kt+1 readable, buffer kt free for slab kt+2
   }
 
-  float* W = g.splits > 1 ? g.work + ((long)split * g.batch + z) * (long)g.M * g.N : nullptr;
+  if (RS && do_rs) {
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * 64 + j * 32 + l32;
-      if (n >= g.N) continue;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (m >= g.M) continue;
-        if (W) W[(long)m * g.N + n] = acc[i][j][r];
-        else epi_store(g, z, m, n, acc[i][j][r]);
+    for (int t = 0; t < TM; ++t) {
+      const float v = rs[t] + __shfl_xor(rs[t], 32, 64);  // k halves 0-15 / 16-31 of every slab
+      const int m = m0 + wm * TM * 32 + t * 32 + l32;
+      if (h == 0 && m < g.M) {
+        if (g.splits > 1) g.rs_work[(long)split * g.M + m] = v;
+        else g.rowsum[m] += v;
       }
     }
+  }
+  float* W = g.splits > 1 ? g.work + ((long)split * g.batch + z) * (long)g.M * g.N : nullptr;
+  if (W) store_partials<TM, TN>(g, W, m0 + wm * TM * 32, n0 + wn * 64, h, l32, acc);
+  else store_tiles<EPI, TM, TN>(g, z, m0 + wm * TM * 32, n0 + wn * 64, h, l32, acc);
 }
 
 // split-K reduction in fixed split order + the fused epilogue (4 outputs per thread when
 // N % 4 == 0: float4 partial loads)
+__device__ __forceinline__ void reduce_store(const GemmArgs& g, int z, int m, int n, float acc) {
+  const long cb = c_base(g, z);
+  const uint64_t db = (uint64_t)z * (uint64_t)g.M * (uint64_t)g.N;
+  switch (epi_kind(g)) {
+    case EPI_BWD: epi_store<EPI_BWD>(g, cb, db, m, n, acc); break;
+    case EPI_FWD: epi_store<EPI_FWD>(g, cb, db, m, n, acc); break;
+    default: epi_store<EPI_PLAIN>(g, cb, db, m, n, acc);
+  }
+}
+
 __global__ void splitk_reduce_kernel(GemmArgs g) {
+  if (g.rowsum && g.rs_work) {
+    for (long m = blockIdx.x * (long)blockDim.x + threadIdx.x; m < g.M; m += (long)gridDim.x * blockDim.x) {
+      float acc = 0.f;
+      for (int s = 0; s < g.splits; ++s) acc += g.rs_work[(long)s * g.M + m];
+      g.rowsum[m] += acc;
+    }
+  }
   const long MN = (long)g.M * g.N;
   const long split_stride = MN * g.batch;
   if ((g.N & 3) == 0) {
@@ -637,10 +774,10 @@ __global__ void splitk_reduce_kernel(GemmArgs g) {
       const int z = (int)(e / MN);
       const long r = e - (long)z * MN;
       const int m = (int)(r / g.N), n = (int)(r - (long)m * g.N);
-      epi_store(g, z, m, n, acc.x);
-      epi_store(g, z, m, n + 1, acc.y);
-      epi_store(g, z, m, n + 2, acc.z);
-      epi_store(g, z, m, n + 3, acc.w);
+      reduce_store(g, z, m, n, acc.x);
+      reduce_store(g, z, m, n + 1, acc.y);
+      reduce_store(g, z, m, n + 2, acc.z);
+      reduce_store(g, z, m, n + 3, acc.w);
     }
     return;
   }
@@ -650,8 +787,18 @@ __global__ void splitk_reduce_kernel(GemmArgs g) {
     const int m = (int)(r / g.N), n = (int)(r - (long)m * g.N);
     float acc = 0.f;
     for (int s = 0; s < g.splits; ++s) acc += g.work[s * split_stride + e];
-    epi_store(g, z, m, n, acc);
+    reduce_store(g, z, m, n, acc);
   }
+}
+
+// rowsum[r] += sum_k A(r,k) for an RC-mode A (element (r,k) at p[k*ld + r]) — used only when
+// the LDS-DMA kernel (which fuses it) is not eligible; fixed k order per row
+__global__ void rowsum_rc_kernel(const float* __restrict__ p, long ld, int M, int K, float* __restrict__ out) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= M) return;
+  float s = 0.f;
+  for (int k = 0; k < K; ++k) s += p[(long)k * ld + r];
+  out[r] += s;
 }
 
 int g_variant = -1;
@@ -663,8 +810,16 @@ int variant() {
   return g_variant;
 }
 
+// Launch the LDS-DMA kernel with the epilogue kind compiled in (each kind is its own kernel,
+// so the plain GEMMs carry none of the fused epilogues' registers).  Returns false when the
+// mode pair has no instantiation of the needed kind (the caller falls back).
 template <int MA, int MB, int BNT>
-void launch_glds(const GemmArgs& g, int batch, hipStream_t st) {
+bool launch_glds(const GemmArgs& g, int batch, hipStream_t st) {
+  constexpr bool can_rs = MA == RC;
+  constexpr bool can_fwd = (MA == KC && (MB == KC || MB == RC)) || (MA == I2C_KC && MB == KC);
+  constexpr bool can_bwd = MA == KC && MB == RC;
+  const int kind = g.splits > 1 ? EPI_PLAIN : epi_kind(g);
+  if ((kind == EPI_FWD && !can_fwd) || (kind == EPI_BWD && !can_bwd)) return false;
   GldsArgs x{};
   x.ntx = (g.N + BNT - 1) / BNT;
   x.nty = (g.M + BM - 1) / BM;
@@ -678,21 +833,37 @@ void launch_glds(const GemmArgs& g, int batch, hipStream_t st) {
     x.hw_b = make_fastdiv(g.b.ic.Ho * g.b.ic.Wo);
     x.wo_b = make_fastdiv(g.b.ic.Wo);
   }
-  const long nbl = (long)x.ntx * x.nty * batch * g.splits;
-  hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT>), dim3((unsigned)nbl), dim3(NT), 0, st, g, x);
+  const dim3 grid((unsigned)((long)x.ntx * x.nty * batch * g.splits));
+  if (can_rs && g.rowsum)
+    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, can_rs, EPI_PLAIN>), grid, dim3(NT), 0, st, g, x);
+  else if (kind == EPI_PLAIN)
+    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_PLAIN>), grid, dim3(NT), 0, st, g, x);
+  else if constexpr (can_fwd) {
+    if (kind == EPI_FWD)
+      hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_FWD>), grid, dim3(NT), 0, st, g, x);
+    else if constexpr (can_bwd)
+      hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_BWD>), grid, dim3(NT), 0, st, g, x);
+  }
+  return true;
 }
 
 template <int MA, int MB>
-int launch(const GemmArgs& g, int batch, hipStream_t st) {
-  dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, batch * g.splits);
-  if (g.bnt == 64) {
-    launch_glds<MA, MB, 64>(g, batch, st);
-  } else if (g.bnt == 128) {
-    launch_glds<MA, MB, 128>(g, batch, st);
-  } else if (variant() == 0) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 0>), grid, dim3(NT), 0, st, g);
-  else if (variant() == 2) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 2>), grid, dim3(NT), 0, st, g);
-  else if (variant() == 3) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 3>), grid, dim3(NT), 0, st, g);
-  else hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 1>), grid, dim3(NT), 0, st, g);
+int launch(const GemmArgs& g0, int batch, hipStream_t st) {
+  bool done = false;
+  if (g0.bnt == 64) done = launch_glds<MA, MB, 64>(g0, batch, st);
+  else if (g0.bnt == 128) done = launch_glds<MA, MB, 128>(g0, batch, st);
+  GemmArgs g = g0;
+  if (!done) {
+    g.rs_work = nullptr;
+    if (g.rowsum && MA == RC)  // the register-staged kernel does not fuse the row sums
+      hipLaunchKernelGGL(rowsum_rc_kernel, dim3((g.M + 255) / 256), dim3(256), 0, st, g.a.p, g.a.ld, g.M, g.K,
+                         g.rowsum);
+    dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, batch * g.splits);
+    if (variant() == 0) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 0>), grid, dim3(NT), 0, st, g);
+    else if (variant() == 2) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 2>), grid, dim3(NT), 0, st, g);
+    else if (variant() == 3) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 3>), grid, dim3(NT), 0, st, g);
+    else hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 1>), grid, dim3(NT), 0, st, g);
+  }
   if (g.splits > 1) {
     long total = (long)g.M * g.N * batch;
     long nb = (total + 255) / 256;
@@ -724,12 +895,15 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
                          float* C, long ldc, long sc1, long sc2,
                          const float* bias, float alpha, float beta, const float* R,
                          int act, float* aux, float drop_p, unsigned long long seed,
+                         int bwd_act, const float* pre, float* rowsum,
                          const int* im2col_a, const int* im2col_b, float* work, long work_bytes,
                          void* stream) {
   ESP_ARG_CHECK(M >= 0 && N >= 0 && K >= 0 && batch >= 1 && nb2 >= 1 && batch % nb2 == 0,
                 "esp_gemm_f32: bad sizes M=%d N=%d K=%d batch=%d nb2=%d", M, N, K, batch, nb2);
   ESP_ARG_CHECK(mode_a >= 0 && mode_a <= 3 && mode_b >= 0 && mode_b <= 3, "esp_gemm_f32: bad mode");
   ESP_ARG_CHECK(drop_p >= 0.f && drop_p < 1.f, "esp_gemm_f32: bad dropout p");
+  ESP_ARG_CHECK(!bwd_act || (pre && !aux && act == 0), "esp_gemm_f32: bwd_act needs pre and no forward activation");
+  ESP_ARG_CHECK(!rowsum || (mode_a == 1 && batch == 1), "esp_gemm_f32: rowsum needs an RC-mode A and batch 1");
   if (M == 0 || N == 0) return 0;
   GemmArgs g{};
   g.M = M; g.N = N; g.K = K; g.nb2 = nb2;
@@ -749,6 +923,7 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
   }
   g.c = C; g.ldc = ldc; g.c1 = sc1; g.c2 = sc2;
   g.r = R; g.aux = aux; g.bias = bias; g.alpha = alpha; g.beta = beta; g.act = act;
+  g.bwd_act = bwd_act; g.pre = pre; g.rowsum = rowsum;
   g.seed = seed;
   if (drop_p > 0.f) {
     double t = (double)drop_p * 4294967296.0;
@@ -777,7 +952,7 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
       long sp = (target + tiles - 1) / tiles;
       const long by_k = K / 128;  // keep >= 8 slabs of BK per split
       if (sp > by_k) sp = by_k;
-      const long cap = work_bytes / (4L * M * N * batch);
+      const long cap = work_bytes / (4L * ((long)M * N * batch + (rowsum ? M : 0)));
       if (sp > cap) sp = cap;
       if (sp > 64) sp = 64;
       if (sp >= 2) {
@@ -786,6 +961,7 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
         g.splits = (int)((K + chunk - 1) / chunk);
         g.kchunk = chunk;
         g.work = work;
+        if (rowsum && g.bnt) g.rs_work = work + (long)g.splits * batch * M * N;
       }
     }
   }

@@ -52,66 +52,103 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
 }
 
 // dx (+)= rstd * (g - mean(g) - xhat*mean(g*xhat)), g = dy*w; partial dw/db per block.
-template <int PER>
+// A wave owns LN_RB consecutive rows per pass (their loads are all in flight before the first
+// reduction: row-level ILP), float4 along the row (D % 4 == 0); a block covers
+// LN_BWD_ROWS rows so that ~M/32 blocks keep every CU busy (the HBM roofline needs many
+// rows in flight, a wave walking 16 rows one by one is latency-bound).
+constexpr int LN_RB = 4, LN_BWD_ROWS = 32;
+template <int PQ>  // float4 quads per lane: D <= 256 * PQ
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                      const float* __restrict__ w, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, float* __restrict__ dx,
-                                                     int accumulate, float* __restrict__ part, int M, int D,
-                                                     int rows_per_block) {
+                                                     int accumulate, float* __restrict__ part, int M, int D) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  __shared__ float sh[4][2][64];
-  float pw[PER], pb[PER];
+  const int nq = D >> 2;
+  __shared__ float4 sh[4][64];
+  float4 pw[PQ], pb[PQ], wq[PQ];
 #pragma unroll
-  for (int i = 0; i < PER; ++i) pw[i] = pb[i] = 0.f;
-  const int r0 = blockIdx.x * rows_per_block;
-  const int r1 = min(M, r0 + rows_per_block);
-  for (int row = r0 + wv; row < r1; row += 4) {
-    const float* xr = x + (long)row * D;
-    const float* dyr = dy + (long)row * D;
-    const float mu = mean_in[row], rs = rstd_in[row];
-    float xh[PER], g[PER];
-    float s1 = 0.f, s2 = 0.f;
+  for (int i = 0; i < PQ; ++i) {
+    pw[i] = pb[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int q = lane + 64 * i;
+    wq[i] = q < nq ? reinterpret_cast<const float4*>(w)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const int r0 = blockIdx.x * LN_BWD_ROWS;
+  const int r1 = min(M, r0 + LN_BWD_ROWS);
+  const float invD = 1.0f / (float)D;
+  for (int base = r0 + wv * LN_RB; base < r1; base += 4 * LN_RB) {
+    float4 xh[LN_RB][PQ], g[LN_RB][PQ];
+    float s1[LN_RB], s2[LN_RB], rs[LN_RB];
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int c = lane + 64 * i;
-      if (c < D) {
-        xh[i] = (xr[c] - mu) * rs;
-        const float d = dyr[c];
-        g[i] = d * w[c];
-        pw[i] += d * xh[i];
-        pb[i] += d;
-      } else {
-        xh[i] = g[i] = 0.f;
+    for (int j = 0; j < LN_RB; ++j) {
+      const int row = base + j;
+      const bool ok = row < r1;
+      const float mu = ok ? mean_in[row] : 0.f;
+      rs[j] = ok ? rstd_in[row] : 0.f;
+      s1[j] = s2[j] = 0.f;
+#pragma unroll
+      for (int i = 0; i < PQ; ++i) {
+        const int q = lane + 64 * i;
+        float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), d = xv;
+        if (ok && q < nq) {
+          xv = reinterpret_cast<const float4*>(x + (long)row * D)[q];
+          d = reinterpret_cast<const float4*>(dy + (long)row * D)[q];
+        }
+        float4 h;
+        h.x = (xv.x - mu) * rs[j]; h.y = (xv.y - mu) * rs[j]; h.z = (xv.z - mu) * rs[j]; h.w = (xv.w - mu) * rs[j];
+        float4 gg;
+        gg.x = d.x * wq[i].x; gg.y = d.y * wq[i].y; gg.z = d.z * wq[i].z; gg.w = d.w * wq[i].w;
+        pw[i].x += d.x * h.x; pw[i].y += d.y * h.y; pw[i].z += d.z * h.z; pw[i].w += d.w * h.w;
+        pb[i].x += d.x; pb[i].y += d.y; pb[i].z += d.z; pb[i].w += d.w;
+        s1[j] += (gg.x + gg.y) + (gg.z + gg.w);
+        s2[j] += (gg.x * h.x + gg.y * h.y) + (gg.z * h.z + gg.w * h.w);
+        xh[j][i] = h;
+        g[j][i] = gg;
       }
-      s1 += g[i];
-      s2 += g[i] * xh[i];
     }
-    s1 = esp::wave_sum(s1) / (float)D;
-    s2 = esp::wave_sum(s2) / (float)D;
-    float* dxr = dx + (long)row * D;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int c = lane + 64 * i;
-      if (c < D) {
-        const float v = rs * (g[i] - s1 - xh[i] * s2);
-        dxr[c] = accumulate ? dxr[c] + v : v;
+    for (int j = 0; j < LN_RB; ++j) {
+      s1[j] = esp::wave_sum(s1[j]) * invD;
+      s2[j] = esp::wave_sum(s2[j]) * invD;
+    }
+#pragma unroll
+    for (int j = 0; j < LN_RB; ++j) {
+      const int row = base + j;
+      if (row >= r1) continue;
+      float4* dxr = reinterpret_cast<float4*>(dx + (long)row * D);
+#pragma unroll
+      for (int i = 0; i < PQ; ++i) {
+        const int q = lane + 64 * i;
+        if (q >= nq) continue;
+        float4 v;
+        v.x = rs[j] * (g[j][i].x - s1[j] - xh[j][i].x * s2[j]);
+        v.y = rs[j] * (g[j][i].y - s1[j] - xh[j][i].y * s2[j]);
+        v.z = rs[j] * (g[j][i].z - s1[j] - xh[j][i].z * s2[j]);
+        v.w = rs[j] * (g[j][i].w - s1[j] - xh[j][i].w * s2[j]);
+        if (accumulate) {
+          const float4 o = dxr[q];
+          v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+        }
+        dxr[q] = v;
       }
     }
   }
-  // combine the 4 waves' column partials in fixed order
+  // combine the 4 waves' column partials in fixed order: part[blk][0:D] = dw, [D:2D] = db
   float* pr = part + (long)blockIdx.x * 2 * D;
 #pragma unroll
-  for (int i = 0; i < PER; ++i) {
-    const int c = lane + 64 * i;
-    __syncthreads();
-    if (c < D) {
-      sh[wv][0][lane] = pw[i];
-      sh[wv][1][lane] = pb[i];
-    }
-    __syncthreads();
-    if (wv == 0 && c < D) {
-      pr[c] = sh[0][0][lane] + sh[1][0][lane] + sh[2][0][lane] + sh[3][0][lane];
-      pr[D + c] = sh[0][1][lane] + sh[1][1][lane] + sh[2][1][lane] + sh[3][1][lane];
+  for (int i = 0; i < PQ; ++i) {
+    const int q = lane + 64 * i;
+#pragma unroll
+    for (int which = 0; which < 2; ++which) {
+      __syncthreads();
+      sh[wv][lane] = which ? pb[i] : pw[i];
+      __syncthreads();
+      if (wv == 0 && q < nq) {
+        const float4 a = sh[0][lane], b = sh[1][lane], c = sh[2][lane], e = sh[3][lane];
+        float4 t;
+        t.x = ((a.x + b.x) + c.x) + e.x; t.y = ((a.y + b.y) + c.y) + e.y;
+        t.z = ((a.z + b.z) + c.z) + e.z; t.w = ((a.w + b.w) + c.w) + e.w;
+        reinterpret_cast<float4*>(pr + which * D)[q] = t;
+      }
     }
   }
 }
@@ -138,14 +175,63 @@ __global__ __launch_bounds__(1024) void finalize_cols_kernel(const T* __restrict
   }
 }
 
-// column partial sums of a [M][N] (ld) matrix: block = chunk of rows, thread = column
-__global__ void colsum_part_kernel(const float* __restrict__ x, int M, int N, long ld, int rows_per_block,
-                                   float* __restrict__ part) {
-  const int r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
-  for (int c = blockIdx.y * blockDim.x + threadIdx.x; c < N; c += gridDim.y * blockDim.x) {
-    float s = 0.f;
-    for (int r = r0; r < r1; ++r) s += x[(long)r * ld + c];
-    part[(long)blockIdx.x * N + c] = s;
+// the same over 2*D columns of [nb][2D] partials, accumulated into out0 (c < D) / out1 (c >= D)
+__global__ __launch_bounds__(1024) void finalize_cols2_kernel(const float* __restrict__ part, int nb, long stride, int D,
+                                                              float* __restrict__ out0, float* __restrict__ out1) {
+  __shared__ float sh[16][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float s = 0.f;
+  if (c < 2 * D) {
+#pragma unroll 4
+    for (int p = g; p < nb; p += 16) s += part[(long)p * stride + c];
+  }
+  sh[g][cl] = s;
+  __syncthreads();
+  if (g == 0 && c < 2 * D) {
+    float t = 0.f;
+    for (int k = 0; k < 16; ++k) t += sh[k][cl];
+    if (c < D) out0[c] += t;
+    else out1[c - D] += t;
+  }
+}
+
+// column partial sums of a [M][N] (ld) matrix: block = CS_ROWS rows x 256 columns; lane =
+// column quad (float4 when vec), 4 waves interleave the rows, combined in fixed order.
+constexpr int CS_ROWS = 32;
+__global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restrict__ x, int M, int N, long ld, int vec,
+                                                          float* __restrict__ part) {
+  __shared__ float4 sh[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = (blockIdx.y * 64 + lane) * 4;
+  const int r0 = blockIdx.x * CS_ROWS, r1 = min(M, r0 + CS_ROWS);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < N) {
+    if (vec) {
+#pragma unroll 4
+      for (int r = r0 + wv; r < r1; r += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(x + (long)r * ld + c);
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+    } else {
+      for (int r = r0 + wv; r < r1; r += 4) {
+        const float* xr = x + (long)r * ld + c;
+        s.x += xr[0];
+        if (c + 1 < N) s.y += xr[1];
+        if (c + 2 < N) s.z += xr[2];
+        if (c + 3 < N) s.w += xr[3];
+      }
+    }
+  }
+  sh[wv][lane] = s;
+  __syncthreads();
+  if (wv == 0 && c < N) {
+    const float4 a = sh[0][lane], b = sh[1][lane], d = sh[2][lane], e = sh[3][lane];
+    float* pr = part + (long)blockIdx.x * N + c;
+    pr[0] = ((a.x + b.x) + d.x) + e.x;
+    if (c + 1 < N) pr[1] = ((a.y + b.y) + d.y) + e.y;
+    if (c + 2 < N) pr[2] = ((a.z + b.z) + d.z) + e.z;
+    if (c + 3 < N) pr[3] = ((a.w + b.w) + d.w) + e.w;
   }
 }
 
@@ -410,38 +496,36 @@ ESP_API int esp_layernorm_fwd(const float* x, const float* w, const float* b, fl
   return 0;
 }
 
-// workspace: >= 2*D*ceil(M/64) floats.  dw/db are accumulated (+=).
+// workspace: >= 2*D*ceil(M/32) floats.  dw/db are accumulated (+=).
 ESP_API int esp_layernorm_bwd(const float* dy, const float* x, const float* w, const float* mean, const float* rstd,
                               float* dx, int accumulate, float* dw, float* db, int M, int D, float* work,
                               void* stream) {
-  ESP_ARG_CHECK(D <= MAXD, "esp_layernorm_bwd: D too large");
-  const int rpb = rows_per_block(M);
-  const int nb = nchunks(M, rpb);
+  ESP_ARG_CHECK(D <= MAXD && D % 4 == 0, "esp_layernorm_bwd: D=%d must be a multiple of 4 and <= %d", D, MAXD);
+  if (M <= 0) return 0;
+  const int nb = (M + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
   hipStream_t st = (hipStream_t)stream;
-  const int per = (D + 63) / 64;
-  if (per <= 4)
-    hipLaunchKernelGGL(ln_bwd_kernel<4>, dim3(nb), dim3(256), 0, st, dy, x, w, mean, rstd, dx, accumulate, work, M, D, rpb);
-  else if (per <= 8)
-    hipLaunchKernelGGL(ln_bwd_kernel<8>, dim3(nb), dim3(256), 0, st, dy, x, w, mean, rstd, dx, accumulate, work, M, D, rpb);
+  const int pq = (D / 4 + 63) / 64;
+  if (pq <= 1)
+    hipLaunchKernelGGL(ln_bwd_kernel<1>, dim3(nb), dim3(256), 0, st, dy, x, w, mean, rstd, dx, accumulate, work, M, D);
+  else if (pq <= 2)
+    hipLaunchKernelGGL(ln_bwd_kernel<2>, dim3(nb), dim3(256), 0, st, dy, x, w, mean, rstd, dx, accumulate, work, M, D);
   else
-    hipLaunchKernelGGL(ln_bwd_kernel<32>, dim3(nb), dim3(256), 0, st, dy, x, w, mean, rstd, dx, accumulate, work, M, D, rpb);
-  hipLaunchKernelGGL(finalize_cols_kernel<float>, fin_grid(D), dim3(1024), 0, st, work, nb, (long)2 * D, D, dw, 1);
-  hipLaunchKernelGGL(finalize_cols_kernel<float>, fin_grid(D), dim3(1024), 0, st, work + D, nb, (long)2 * D, D, db, 1);
+    hipLaunchKernelGGL(ln_bwd_kernel<8>, dim3(nb), dim3(256), 0, st, dy, x, w, mean, rstd, dx, accumulate, work, M, D);
+  hipLaunchKernelGGL(finalize_cols2_kernel, fin_grid(2 * D), dim3(1024), 0, st, work, nb, (long)2 * D, D, dw, db);
   ESP_CHECK_LAUNCH("esp_layernorm_bwd");
   return 0;
 }
 
-// out[c] (+)= sum_r x[r*ld + c].  workspace: >= N*ceil(M/64) floats
+// out[c] (+)= sum_r x[r*ld + c].  workspace: >= N*ceil(M/32) floats
 ESP_API int esp_colsum(const float* x, int M, int N, long ld, float* out, int accumulate, float* work, void* stream) {
-  const int rpb = rows_per_block(M);
-  const int nb = nchunks(M, rpb);
   hipStream_t st = (hipStream_t)stream;
   if (M == 0) {
     if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float) * N, st);
     return 0;
   }
-  const int ty = (N + 255) / 256;
-  hipLaunchKernelGGL(colsum_part_kernel, dim3(nb, ty), dim3(256), 0, st, x, M, N, ld, rpb, work);
+  const int nb = (M + CS_ROWS - 1) / CS_ROWS;
+  const int vec = ((uintptr_t)x % 16 == 0) && ld % 4 == 0 && N % 4 == 0;
+  hipLaunchKernelGGL(colsum_part_kernel, dim3(nb, (N + 255) / 256), dim3(256), 0, st, x, M, N, ld, vec, work);
   hipLaunchKernelGGL(finalize_cols_kernel<float>, fin_grid(N), dim3(1024), 0, st, work, nb, (long)N, N, out, accumulate);
   ESP_CHECK_LAUNCH("esp_colsum");
   return 0;

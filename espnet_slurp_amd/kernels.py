@@ -60,6 +60,15 @@ def _work(nbytes, device):
     return WS.get(nbytes, device)
 
 
+def h2d(t: torch.Tensor, device) -> torch.Tensor:
+    """Host tensor -> device through pinned memory, non-blocking: a pageable H2D copy would
+    make the host wait for the stream to drain (a hidden synchronisation per call)."""
+    device = torch.device(device)
+    if device.type != "cuda" or t.is_cuda:
+        return t.to(device)
+    return t.pin_memory().to(device, non_blocking=True)
+
+
 # ----------------------------------------------------------------------------- GEMM
 _PROF = None  # when a list: (algorithmic flops, start event, end event) per GEMM launch
 
@@ -94,8 +103,10 @@ def profile_gemm_stop(by_shape: bool = False):
 def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc,
          a_off=0, b_off=0, c_off=0, batch=1, nb2=1, sa=(0, 0), sb=(0, 0), sc=(0, 0),
          bias=None, alpha=1.0, beta=0.0, R=None, r_off=None, act=ACT_NONE, aux=None,
-         drop_p=0.0, seed=0, ic_a: Optional[Sequence[int]] = None, ic_b: Optional[Sequence[int]] = None):
-    """C[z](m,n) = alpha*epi(sum_k A(m,k)B(k,n) + bias) + beta*R (see gemm.hip)."""
+         drop_p=0.0, seed=0, ic_a: Optional[Sequence[int]] = None, ic_b: Optional[Sequence[int]] = None,
+         bwd_act=ACT_NONE, pre=None, rowsum=None):
+    """C[z](m,n) = alpha*epi(sum_k A(m,k)B(k,n) + bias) + beta*R (see gemm.hip).
+    bwd_act/pre: epilogue drop'(.)*act'(pre) (FFN backward); rowsum: += sum_k A(m,k) (bias grad)."""
     if R is not None and r_off is None:
         r_off = c_off
     ws = _GEMM_WS.get(_GEMM_WS_BYTES, C.device)
@@ -110,6 +121,7 @@ def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc
                  _p(C, c_off), ldc, sc[0], sc[1], _p(bias), float(alpha), float(beta),
                  _p(R, r_off or 0), act, _p(aux, c_off) if aux is not None else None,
                  float(drop_p), seed & 0xFFFFFFFFFFFFFFFF,
+                 int(bwd_act), _p(pre, c_off) if pre is not None else None, _p(rowsum),
                  ctypes_ptr(ica), ctypes_ptr(icb), _p(ws), ws.numel(), _st())
     if _PROF is not None:
         ev1.record()
@@ -141,21 +153,29 @@ def linear_bwd_data(dy, W, dx, *, accumulate=False):
     return dx
 
 
+def linear_bwd_data_act(dy, W, dx, pre, act, drop_p=0.0, seed=0):
+    """dx = drop'(dy W) * act'(pre): the input gradient of w_2 fused with the backward of
+    h = drop(act(pre)) (positionwise_feed_forward.py:32)."""
+    M, N = dy.shape
+    K = W.shape[1]
+    gemm(M, K, N, dy, W, dx, mode_a=KC, lda=dy.stride(0), mode_b=RC, ldb=W.stride(0), ldc=dx.stride(0),
+         bwd_act=act, pre=pre, drop_p=drop_p, seed=seed)
+    return dx
+
+
 def linear_bwd_weight(dy, x, dW, db=None):
-    """dW += dy^T x ; db += colsum(dy)."""
+    """dW += dy^T x ; db += colsum(dy) (fused into the same GEMM pass over dy)."""
     M, N = dy.shape
     K = x.shape[1]
     gemm(N, K, M, dy, x, dW, mode_a=RC, lda=dy.stride(0), mode_b=RC, ldb=x.stride(0), ldc=dW.stride(0),
-         R=dW, beta=1.0)
-    if db is not None:
-        colsum(dy, db, accumulate=True)
+         R=dW, beta=1.0, rowsum=db)
 
 
 def colsum(x2d, out, accumulate=True, M=None, N=None, ld=None):
     M = M if M is not None else x2d.shape[0]
     N = N if N is not None else x2d.shape[1]
     ld = ld if ld is not None else x2d.stride(0)
-    nb = (M + 63) // 64
+    nb = (M + 31) // 32
     w = _work(4 * N * max(nb, 1), x2d.device)
     _native.call("esp_colsum", _p(x2d), M, N, ld, _p(out), int(accumulate), _p(w), _st())
 
@@ -217,7 +237,7 @@ def layernorm_fwd(x2d, w, b, y, mean, rstd, eps=1e-12):
 
 def layernorm_bwd(dy, x, w, mean, rstd, dx, dw, db, accumulate=False):
     M, D = x.shape
-    nb = (M + 63) // 64
+    nb = (M + 31) // 32
     ws = _work(4 * 2 * D * max(nb, 1), x.device)
     _native.call("esp_layernorm_bwd", _p(dy), _p(x), _p(w), _p(mean), _p(rstd), _p(dx), int(accumulate), _p(dw),
                  _p(db), M, D, _p(ws), _st())

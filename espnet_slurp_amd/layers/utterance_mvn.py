@@ -29,5 +29,5 @@ class UtteranceMVN(AbsNormalize):
         if ilens is None:
             ilens = torch.full((B,), T, dtype=torch.long)
         y = x.contiguous().clone() if x.requires_grad else x.contiguous()
-        K.utterance_mvn(y, ilens.to(torch.int32).to(x.device))
+        K.utterance_mvn(y, K.h2d(ilens.to(torch.int32), x.device))
         return y, ilens

@@ -42,6 +42,12 @@ class Trainer:
         self.iiter = 0
         self.n_skipped = 0
         self._clip = torch.empty(3, dtype=torch.float32, device=model.flat.flat.device)
+        # finite flag of the last optimizer step, read back asynchronously (pinned buffer + event)
+        # and acted on just before the NEXT optimizer step: the host never drains the queue
+        cuda = self._clip.is_cuda
+        self._flag_host = torch.empty(1, dtype=torch.float32, pin_memory=cuda)
+        self._flag_event = torch.cuda.Event() if cuda else None
+        self._pending = False
 
     def train_one_step(self, batch: Dict[str, torch.Tensor], check_finite: bool = True) -> Dict[str, torch.Tensor]:
         """One iteration of train_one_epoch's loop body; returns device-side stats."""
@@ -62,28 +68,44 @@ class Trainer:
         if self.iiter % opts.accum_grad == 0:
             if self.reducer is not None:
                 self.reducer.finish()
+            self.resolve_pending()  # scheduler step of the previous update (if it was finite)
             clip_grad_norm_(model.flat, opts.grad_clip, self._clip)
+            # the Adam kernel itself skips a non-finite update on device (trainer.py:651-667)
             self.optimizer.step(clip=self._clip)
-            finite = True
             if check_finite:
-                finite = bool(self._clip[2].item() != 0.0)
-            if finite:
-                if isinstance(self.scheduler, AbsBatchStepScheduler):
-                    self.scheduler.step()
-            else:
-                self.n_skipped += 1
+                self._flag_host.copy_(self._clip[2:3], non_blocking=True)
+                if self._flag_event is not None:
+                    self._flag_event.record()
+                self._pending = True
+            elif isinstance(self.scheduler, AbsBatchStepScheduler):
+                self.scheduler.step()
             self.optimizer.zero_grad()
         stats["grad_norm"] = self._clip[0:1]
         return stats
+
+    def resolve_pending(self):
+        """Apply the bookkeeping of the last optimizer step once its finite flag is on the host:
+        WarmupLR batch step if the gradient norm was finite, else count a skipped step
+        (trainer.py:651-686).  Called before the next optimizer step and at epoch end."""
+        if not self._pending:
+            return
+        if self._flag_event is not None:
+            self._flag_event.synchronize()
+        self._pending = False
+        if float(self._flag_host[0]) != 0.0:
+            if isinstance(self.scheduler, AbsBatchStepScheduler):
+                self.scheduler.step()
+        else:
+            self.n_skipped += 1
 
     def train_one_epoch(self, iterator: Iterable, reporter=None) -> bool:
         """Loop over (utt_id, batch) like trainer.py:502-714; returns True if every step was
         skipped (all_steps_are_invalid)."""
         self.model.train()
-        all_invalid = True
+        it0, sk0 = self.iiter, self.n_skipped
         for _, batch in iterator:
             stats = self.train_one_step(batch)
             if reporter is not None:
                 reporter(stats)
-            all_invalid = all_invalid and (self.n_skipped == self.iiter)
-        return all_invalid
+        self.resolve_pending()
+        return (self.n_skipped - sk0) == (self.iiter - it0)

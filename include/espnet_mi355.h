@@ -31,6 +31,11 @@ int esp_abi_version(void);
  *   z = z1*nb2+z2 ; operand offset = z1*s1 + z2*s2
  *   act: 0 none, 1 ReLU, 2 Swish (pre-activation stored to aux if non-NULL); dropout with
  *   probability drop_p keyed by (seed, (z*M+m)*N+n).
+ *   bwd_act != 0 (backward of h = drop(act(pre)), positionwise_feed_forward.py:32): the
+ *   epilogue is  v = drop'(acc + bias) * act'(pre)  with the dropout mask regenerated from
+ *   (drop_p, seed); act must be 0 and aux NULL.
+ *   rowsum != NULL (mode_a RC, batch 1): rowsum[m] += sum_k A(m,k) — the bias gradient of a
+ *   weight-gradient GEMM (dW = dy^T x, db = colsum dy) in the same pass over dy.
  *   work/work_bytes: optional scratch; when the tile grid is too small to fill the chip the
  *   K range is split over blocks and reduced (fixed order, deterministic) before the epilogue. */
 int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2,
@@ -39,6 +44,7 @@ int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2
                  float* C, long ldc, long sc1, long sc2,
                  const float* bias, float alpha, float beta, const float* R,
                  int act, float* aux, float drop_p, unsigned long long seed,
+                 int bwd_act, const float* pre, float* rowsum,
                  const int* im2col_a, const int* im2col_b, float* work, long work_bytes,
                  void* stream);
 

@@ -109,6 +109,57 @@ def test_gemm_epilogue(dev):
     assert torch.equal((dx.cpu() != 0) & pos, o1c != 0)
 
 
+@pytest.mark.parametrize("act", [K.ACT_RELU, K.ACT_SWISH])
+def test_gemm_backward_activation_epilogue(dev, act):
+    """dx = drop'(dy W) * act'(pre) in the GEMM epilogue == the separate act_bwd kernel path
+    (positionwise_feed_forward.py:32 backward), dropout mask regenerated from the seed."""
+    M, N, Kk = 300, 96, 160
+    dy, W, pre = _r(M, N, seed=11), _r(N, Kk, seed=12), _r(M, Kk, seed=13)
+    dyd, Wd, pred = dy.to(dev), W.to(dev), pre.to(dev)
+    out = torch.empty(M, Kk, device=dev)
+    K.linear_bwd_data_act(dyd, Wd, out, pred, act, drop_p=0.2, seed=77)
+    ref = torch.empty(M, Kk, device=dev)
+    K.linear_bwd_data(dyd, Wd, ref)
+    K.act_bwd(ref, pred, ref, act, drop_p=0.2, seed=77)
+    torch.cuda.synchronize()
+    assert torch.equal(out == 0, ref == 0)
+    assert (out - ref).abs().max().item() <= 1e-5 * max(1.0, ref.abs().max().item())
+    x = pre.double()
+    g = (dy.double() @ W.double())
+    mask = (ref.cpu() != 0).double() / 0.8
+    d = torch.where(x > 0, 1.0, 0.0) if act == K.ACT_RELU else torch.sigmoid(x) * (1 + x * (1 - torch.sigmoid(x)))
+    assert (out.cpu().double() - g * mask * d).abs().max().item() < 1e-4
+
+
+@pytest.mark.parametrize("M,N,Kk,pad", [(64, 48, 40, 0), (23936 // 8, 256, 64, 0), (5000, 100, 36, 0),
+                                        (777, 33, 20, 3)])
+def test_gemm_weight_grad_fused_bias(dev, M, N, Kk, pad):
+    """dW = dy^T x with db = colsum(dy) fused in the same GEMM (split-K and not; pad != 0 makes
+    the pitch unaligned and selects the register-staged kernel + the separate row-sum kernel)."""
+    dyb = _r(M, N + pad, seed=14)
+    dy = dyb[:, :N]
+    x = _r(M, Kk, seed=15)
+    dyd, xd = dyb.to(dev), x.to(dev)
+    dW = torch.full((N, Kk), 0.5, device=dev)
+    db = torch.full((N,), 0.25, device=dev)
+    K.gemm(N, Kk, M, dyd, xd, dW, mode_a=K.RC, lda=N + pad, mode_b=K.RC, ldb=Kk, ldc=Kk, R=dW, beta=1.0, rowsum=db)
+    torch.cuda.synchronize()
+    refW = dy.double().t() @ x.double() + 0.5
+    refb = dy.double().sum(0) + 0.25
+    assert (dW.cpu().double() - refW).abs().max().item() <= 1e-5 * math.sqrt(M) * 4
+    assert (db.cpu().double() - refb).abs().max().item() <= 1e-5 * math.sqrt(M) * 4
+
+
+def test_colsum_and_layernorm_bwd_shapes(dev):
+    for (M, N, ld) in [(23936 // 4, 256, 256), (1001, 1024, 1024), (37, 30, 33), (3, 5, 8)]:
+        x = _r(M, ld, seed=16)
+        out = torch.full((N,), 1.0, device=dev)
+        K.colsum(x.to(dev), out, accumulate=True, M=M, N=N, ld=ld)
+        torch.cuda.synchronize()
+        ref = x[:, :N].double().sum(0) + 1.0
+        assert (out.cpu().double() - ref).abs().max().item() < 1e-4 * math.sqrt(M)
+
+
 def test_gemm_batched_strided(dev):
     # attention-style (head, batch) strides: q (B*T, 3D) read per (h,b)
     B, T, H, dk = 3, 50, 4, 16
