@@ -136,6 +136,7 @@ def main():
     ap.add_argument("--vocab", type=int, default=600)
     ap.add_argument("--rel-pos", default="latest", choices=["latest", "legacy"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="launch kernel by kernel instead of replaying a HIP graph")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -156,14 +157,16 @@ def main():
     model.train()
     opt = FusedAdam(model.parameters(), model.flat, lr=2e-4)
     sched = WarmupLR(opt, warmup_steps=25000)
-    trainer = Trainer(model, opt, sched, TrainerOptions(grad_clip=5.0), distributed=world > 1)
+    trainer = Trainer(model, opt, sched, TrainerOptions(grad_clip=5.0), distributed=world > 1,
+                      cuda_graph=not args.eager)
     batch = synthetic_batch(args.batch, args.vocab, rank, device)
 
     for _ in range(args.warmup):
         trainer.train_one_step(batch)
     torch.cuda.synchronize()
 
-    K.profile_gemm_start()
+    if args.eager:
+        K.profile_gemm_start()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -174,6 +177,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if not args.eager:
+        # the graph's kernels cannot be bracketed one by one: time the same GEMM launches (same
+        # kernels, shapes and inputs) in one eager step right after the timed region
+        eager = Trainer(model, opt, sched, TrainerOptions(grad_clip=5.0), distributed=world > 1)
+        K.profile_gemm_start()
+        eager.train_one_step(batch)
+        eager.resolve_pending()
     gemm_flops, gemm_ms, gemm_launches = K.profile_gemm_stop()
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=device)
@@ -201,13 +211,15 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (N(0,1) fbank, random tokens U[20,40], random-init weights)",
+            "launch": "eager" if args.eager else "hip_graph",
             "config": {"workload": f"C2 SLURP Conformer-medium d={args.d} H={args.heads} FF={args.ff} "
                                    f"{args.layers}L enc / 6L dec, V={args.vocab}, rel_pos={args.rel_pos}, "
                                    "ctc 0.3, lsm 0.1, dropout 0.1, SpecAug on",
                        "global_batch": world * args.batch, "seq_len": 1500, "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-                         "kernel": "gemm_f32_kernel (all MFMA GEMM launches in the timed region)",
+                         "kernel": "gemm_glds_kernel family (all MFMA GEMM launches of one step, HIP events"
+                                   + (" in the timed region)" if args.eager else " on an eager replay of the step)"),
                          "launches": gemm_launches,
                          "avg_launch_us": round(1e3 * gemm_ms / max(1, gemm_launches), 2)},
             "step_roofline": {"train_gflop_per_utt": round(train / 1e9, 2),

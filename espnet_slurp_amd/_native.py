@@ -33,6 +33,11 @@ SIGNATURES = {
     "esp_utterance_mvn": [P, I, I, I, P, P],
     "esp_grad_norm": [P, L, F, P, P, P],
     "esp_adam": [P, P, P, P, L, P, F, F, F, F, F, I, P],
+    "esp_opt_hyper": [P, ctypes.c_double, ctypes.c_double, F, F, P, P],
+    "esp_adam_dev": [P, P, P, P, L, P, P, F, F, F, F, P],
+    "esp_opt_advance": [P, P, P],
+    "esp_set_rng_key": [P],
+    "esp_rng_advance": [P, P],
     "esp_layernorm_fwd": [P, P, P, P, P, P, I, I, F, P],
     "esp_layernorm_bwd": [P, P, P, P, P, P, I, P, P, I, I, P, P],
     "esp_colsum": [P, I, I, L, P, I, P, P],
@@ -59,7 +64,7 @@ SIGNATURES = {
     "esp_ctc_forced_align": [P, I, I, P, I, I, P, P, P],
 }
 _RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I}
-ABI_VERSION = 4  # bumped whenever a signature in include/espnet_mi355.h changes
+ABI_VERSION = 5  # bumped whenever a signature in include/espnet_mi355.h changes
 
 _lib = None
 

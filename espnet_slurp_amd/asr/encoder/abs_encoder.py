@@ -103,8 +103,8 @@ class EncoderFn(torch.autograd.Function):
     flat gradient buffer (flat.py) and returns no input gradient (fbank needs none)."""
 
     @staticmethod
-    def forward(ctx, feats, anchor, enc, ilens_cpu, seed, grad_hook):
-        hs, olens, saved = enc.run_forward(feats, ilens_cpu, Seeds(seed), enc.training)
+    def forward(ctx, feats, anchor, enc, ilens_cpu, seed, grad_hook, klen=None):
+        hs, olens, saved = enc.run_forward(feats, ilens_cpu, Seeds(seed), enc.training, klen=klen)
         ctx.enc = enc
         ctx.saved = saved
         ctx.grad_hook = grad_hook
@@ -115,4 +115,4 @@ class EncoderFn(torch.autograd.Function):
     def backward(ctx, dhs):
         ctx.enc.run_backward(ctx.saved, dhs.contiguous(), ctx.grad_hook)
         ctx.saved = None
-        return None, None, None, None, None, None
+        return None, None, None, None, None, None, None

@@ -167,7 +167,7 @@ class ConformerEncoder(AbsEncoder):
             l.self_attn.flat = flat
 
     # ---------------------------------------------------------------- explicit passes
-    def run_forward(self, feats, ilens_cpu, seeds: Seeds, training: bool):
+    def run_forward(self, feats, ilens_cpu, seeds: Seeds, training: bool, klen=None):
         B, T, _ = feats.shape
         if T < 7:
             raise TooShortUttError(
@@ -175,7 +175,8 @@ class ConformerEncoder(AbsEncoder):
                 T, 7)
         D = self._output_size
         olens = subsampled_lengths(ilens_cpu, T)
-        klen = lengths_to_device(olens, feats.device)
+        if klen is None:
+            klen = lengths_to_device(olens, feats.device)
         x, c_emb = self.embed.fwd(feats, math.sqrt(D), self.positional_dropout_rate, seeds, training)
         T2 = c_emb.T2
         tab = pos_table("legacy" if self.legacy else "latest", T2, D, feats.device, self.max_pos_emb_len)
@@ -212,15 +213,18 @@ class ConformerEncoder(AbsEncoder):
         assert self.flat is not None, "call espnet_slurp_amd.flatten_model(model) before running"
         ilens_cpu = ilens.detach().cpu()
         feats = xs_pad.contiguous().float()
-        seed = draw_seed()
+        olens = subsampled_lengths(ilens_cpu, feats.shape[1])
+        hs = self.forward_prepared(feats, ilens_cpu, lengths_to_device(olens, feats.device), draw_seed())
+        return hs, K.h2d(olens, xs_pad.device), None
+
+    def forward_prepared(self, feats: torch.Tensor, ilens_cpu: torch.Tensor, klen: torch.Tensor, seed: int):
+        """Encoder output hs (B, T', D) from device-resident inputs only (klen: int32 output
+        lengths on device): no host->device traffic, so it can be captured in a HIP graph."""
         anchor = self.after_norm.weight
         hook = getattr(self, "_grad_hook", None)
         if torch.is_grad_enabled() and anchor.requires_grad:
-            hs = EncoderFn.apply(feats, anchor, self, ilens_cpu, seed, hook)
-            olens = subsampled_lengths(ilens_cpu, feats.shape[1])
-        else:
-            hs, olens, _ = self.run_forward(feats, ilens_cpu, Seeds(seed), self.training)
-        return hs, K.h2d(olens, xs_pad.device), None
+            return EncoderFn.apply(feats, anchor, self, ilens_cpu, seed, hook, klen)
+        return self.run_forward(feats, ilens_cpu, Seeds(seed), self.training, klen=klen)[0]
 
     def output_lengths(self, ilens_cpu: torch.Tensor, T: int) -> torch.Tensor:
         """Valid output frames per utterance (host, no device round trip)."""

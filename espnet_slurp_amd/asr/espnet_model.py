@@ -52,8 +52,8 @@ class HeadsFn(torch.autograd.Function):
     """CTC + attention-decoder losses of one batch; backward returns d loss / d hs."""
 
     @staticmethod
-    def forward(ctx, hs, anchor, model, hlens_cpu, text_cpu, text_lengths_cpu, seed):
-        out4, state = model._heads_forward(hs, hlens_cpu, text_cpu, text_lengths_cpu, Seeds(seed), True)
+    def forward(ctx, hs, anchor, model, prep, seed):
+        out4, state = model._heads_forward(hs, prep, Seeds(seed), True)
         ctx.model = model
         ctx.state = state
         loss = out4[3:4].clone()
@@ -65,7 +65,26 @@ class HeadsFn(torch.autograd.Function):
     def backward(ctx, g_loss, g_others):
         dhs = ctx.model._heads_backward(ctx.state, g_loss.contiguous())
         ctx.state = None
-        return dhs, None, None, None, None, None, None
+        return dhs, None, None, None, None
+
+
+class Prepared(dict):
+    """Host-side bookkeeping of one batch (lengths, sos/eos targets, SpecAug draws, dropout
+    seeds) and its device-resident copies.  Everything the kernels read per step lives in
+    `dev` (device tensors), so a captured HIP graph is re-targeted at a new batch of the same
+    shapes by copying the new host values into the same device tensors (`copy_into`)."""
+    __getattr__ = dict.__getitem__
+
+    def to_device(self, device):
+        self["dev"] = {k: K.h2d(v, device) for k, v in self["host"].items()}
+        return self
+
+    def copy_into(self, other: "Prepared"):
+        """Write this batch's host values into another Prepared's device tensors (same shapes)."""
+        for k, v in self["host"].items():
+            d = other["dev"][k]
+            assert d.shape == v.shape, (k, d.shape, v.shape)
+            d.copy_(v.pin_memory(), non_blocking=True)
 
 
 class ESPnetASRModel(AbsESPnetModel):
@@ -117,39 +136,29 @@ class ESPnetASRModel(AbsESPnetModel):
         return self.flat
 
     # ------------------------------------------------------------------ heads
-    def _heads_forward(self, hs, hlens_cpu, text_cpu, text_lengths_cpu, seeds: Seeds, want_grad: bool):
+    def _heads_forward(self, hs, prep: "Prepared", seeds: Seeds, want_grad: bool):
         B, T, D = hs.shape
         dev = hs.device
         hs2d = hs.reshape(B * T, D)
-        hlens_i32 = K.h2d(hlens_cpu.to(torch.int32), dev)
+        d = prep.dev
+        hlens_i32 = d["hlens"]
         state = {"hs2d": hs2d, "B": B, "T": T}
         nll = grad_ctc = None
         if self.ctc is not None:
-            Umax = text_cpu.shape[1]
-            ys = K.h2d(text_cpu, dev)
-            tl = K.h2d(text_lengths_cpu.to(torch.int32), dev)
-            nll, grad_ctc, _ = self.ctc.loss_and_grad(hs2d, B, T, hlens_i32, ys, tl, Umax,
+            nll, grad_ctc, _ = self.ctc.loss_and_grad(hs2d, B, T, hlens_i32, d["ys"], d["tlens"], prep.Umax,
                                                       self.ctc_weight / B, want_grad=want_grad)
             state["grad_ctc"] = grad_ctc
         row_loss = row_stat = None
         R = 0
-        denom = float(B)
+        denom = prep.denom
         if self.decoder is not None:
-            ys_in, ys_out, ys_in_lens = add_sos_eos(text_cpu, text_lengths_cpu, self.sos, self.eos, self.ignore_id)
-            L = ys_in.shape[1]
-            R = B * L
-            if self.length_normalized_loss:
-                denom = float(int((ys_out != self.ignore_id).sum()))
-            ys_in_d = K.h2d(ys_in, dev)
-            ys_out_d = K.h2d(ys_out, dev)
-            logits, dsaved = self.decoder.run_forward(hs, hlens_i32, ys_in_d,
-                                                      K.h2d(ys_in_lens.to(torch.int32), dev),
-                                                      seeds, self.training)
+            R = B * prep.L
+            logits, dsaved = self.decoder.run_forward(hs, hlens_i32, d["ys_in"], d["ys_in_lens"], seeds, self.training)
             V = self.vocab_size
             grad_att = empty(R, V, like=hs) if want_grad else None
             row_loss = torch.empty(R, dtype=torch.float64, device=dev)
             row_stat = torch.empty(2 * R, dtype=torch.int32, device=dev)
-            K.label_smoothing(logits, ys_out_d, V, self.ignore_id, self.lsm_weight,
+            K.label_smoothing(logits, d["ys_out"], V, self.ignore_id, self.lsm_weight,
                               (1.0 - self.ctc_weight) / denom, grad_att, row_loss, row_stat)
             state["grad_att"] = grad_att
             state["dec"] = dsaved
@@ -175,28 +184,55 @@ class ESPnetASRModel(AbsESPnetModel):
         return dhs.view(state["B"], state["T"], -1)
 
     # ------------------------------------------------------------------ forward
-    def forward(self, speech: torch.Tensor, speech_lengths: torch.Tensor, text: torch.Tensor,
-                text_lengths: torch.Tensor, specaug_draws: Optional[dict] = None, **kwargs):
+    def prepare(self, speech_lengths: torch.Tensor, text: torch.Tensor, text_lengths: torch.Tensor, T_in: int,
+                F_in: int, specaug_draws: Optional[dict] = None) -> Prepared:
+        """All host-side work of a step (espnet_model.py:169-297 before any kernel): lengths,
+        the target slice, add_sos_eos, SpecAug draws (CPU generator, as time_warp.py), the
+        dropout seeds.  Returns host tensors; `.to_device()` moves them (pinned, async)."""
         assert text_lengths.dim() == 1, text_lengths.shape
-        assert speech.shape[0] == speech_lengths.shape[0] == text.shape[0] == text_lengths.shape[0], (
-            speech.shape, speech_lengths.shape, text.shape, text_lengths.shape)
-        assert self.flat is not None, "call model.flatten() after moving the model to the GPU"
-        B = speech.shape[0]
+        B = int(speech_lengths.shape[0])
+        text = text.detach().cpu().clone()
         text[text == -1] = self.ignore_id
         sl_cpu = speech_lengths.detach().cpu()
         tl_cpu = text_lengths.detach().cpu()
-        text_cpu = text.detach().cpu()[:, : int(tl_cpu.max())]
-        encoder_out, encoder_out_lens = self.encode(speech, speech_lengths, sl_cpu, specaug_draws)
-        if hasattr(self.encoder, "output_lengths"):  # host-side lengths: no device round trip
-            hlens_cpu = self.encoder.output_lengths(sl_cpu, int(sl_cpu.max()))
-        else:
-            hlens_cpu = encoder_out_lens.detach().cpu()
-        seed = draw_seed()
+        text_cpu = text[:, : int(tl_cpu.max())].contiguous()
+        T = min(T_in, int(sl_cpu.max()))
+        host = {"lens": sl_cpu.to(torch.int32), "weight": torch.tensor([B], dtype=torch.long)}
+        if self.specaug is not None and self.training:
+            draws = specaug_draws if specaug_draws is not None else self.specaug.draw(B, T, F_in, sl_cpu.tolist())
+            for k, v in draws.items():
+                host["sa_" + k] = v.to(torch.int32)
+        host["hlens"] = self.encoder.output_lengths(sl_cpu, T).to(torch.int32)
+        prep = Prepared(B=B, T=T, Umax=int(text_cpu.shape[1]), denom=float(B), L=0, host=host,
+                        enc_seed=draw_seed(), heads_seed=draw_seed(), sl_cpu=sl_cpu)
+        if self.ctc is not None:
+            host["ys"] = text_cpu
+            host["tlens"] = tl_cpu.to(torch.int32)
+        if self.decoder is not None:
+            ys_in, ys_out, ys_in_lens = add_sos_eos(text_cpu, tl_cpu, self.sos, self.eos, self.ignore_id)
+            prep["L"] = int(ys_in.shape[1])
+            if self.length_normalized_loss:
+                prep["denom"] = float(int((ys_out != self.ignore_id).sum()))
+            host["ys_in"], host["ys_out"] = ys_in, ys_out
+            host["ys_in_lens"] = ys_in_lens.to(torch.int32)
+        return prep
+
+    def forward_prepared(self, speech: torch.Tensor, prep: Prepared):
+        """The step's device work from a prepared batch: no host->device traffic and no host
+        synchronisation, so the forward + backward can be captured as one HIP graph."""
+        d = prep.dev
+        feats = speech[:, : prep.T].contiguous().float()
+        if self.specaug is not None and self.training:
+            draws = {k[3:]: v for k, v in d.items() if k.startswith("sa_")}
+            feats = self.specaug.apply_prepared(feats, d["lens"], draws)
+        if self.normalize is not None:
+            feats = self.normalize.apply_prepared(feats, d["lens"])
+        encoder_out = self.encoder.forward_prepared(feats, prep.sl_cpu, d["hlens"], prep.enc_seed)
         anchor = next(p for p in (self.ctc or self.decoder).parameters())
         if torch.is_grad_enabled() and anchor.requires_grad:
-            loss, others = HeadsFn.apply(encoder_out, anchor, self, hlens_cpu, text_cpu, tl_cpu, seed)
+            loss, others = HeadsFn.apply(encoder_out, anchor, self, prep, prep.heads_seed)
         else:
-            out4, _ = self._heads_forward(encoder_out, hlens_cpu, text_cpu, tl_cpu, Seeds(seed), False)
+            out4, _ = self._heads_forward(encoder_out, prep, Seeds(prep.heads_seed), False)
             loss, others = out4[3:4], out4[0:3]
         stats = dict(
             loss_ctc=others[0:1].detach() if self.ctc is not None else None,
@@ -206,8 +242,18 @@ class ESPnetASRModel(AbsESPnetModel):
             cer=None, wer=None,
             loss=loss.detach(),
         )
-        weight = K.h2d(torch.tensor([B], dtype=torch.long), loss.device)
-        return loss, stats, weight
+        return loss, stats, d["weight"]
+
+    def forward(self, speech: torch.Tensor, speech_lengths: torch.Tensor, text: torch.Tensor,
+                text_lengths: torch.Tensor, specaug_draws: Optional[dict] = None, **kwargs):
+        assert text_lengths.dim() == 1, text_lengths.shape
+        assert speech.shape[0] == speech_lengths.shape[0] == text.shape[0] == text_lengths.shape[0], (
+            speech.shape, speech_lengths.shape, text.shape, text_lengths.shape)
+        assert self.flat is not None, "call model.flatten() after moving the model to the GPU"
+        text[text == -1] = self.ignore_id  # the reference mutates the batch (espnet_model.py:196)
+        prep = self.prepare(speech_lengths, text, text_lengths, speech.shape[1], speech.shape[2], specaug_draws)
+        prep.to_device(speech.device)
+        return self.forward_prepared(speech, prep)
 
     def encode(self, speech: torch.Tensor, speech_lengths: torch.Tensor, sl_cpu: Optional[torch.Tensor] = None,
                specaug_draws: Optional[dict] = None):

@@ -106,9 +106,12 @@ class SpecAug(AbsSpecAug):
         if draws is None:
             draws = self.draw(B, T, F, lens.tolist())
         dev = x.device
+        ddev = {k: K.h2d(v, dev) for k, v in draws.items()}
+        return self.apply_prepared(x, K.h2d(lens.to(torch.int32), dev), ddev), x_lengths
+
+    @staticmethod
+    def apply_prepared(x: torch.Tensor, lens_i32: torch.Tensor, draws_dev: dict) -> torch.Tensor:
+        """Warp + masks from device-resident lengths and draws (one kernel, graph-capturable)."""
         y = torch.empty_like(x)
-        K.specaug(x.contiguous(), y, K.h2d(lens.to(torch.int32), dev),
-                  K.h2d(draws["warp"], dev) if "warp" in draws else None,
-                  K.h2d(draws["fmask"], dev) if "fmask" in draws else None,
-                  K.h2d(draws["tmask"], dev) if "tmask" in draws else None)
-        return y, x_lengths
+        K.specaug(x.contiguous(), y, lens_i32, draws_dev.get("warp"), draws_dev.get("fmask"), draws_dev.get("tmask"))
+        return y

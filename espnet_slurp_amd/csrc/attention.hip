@@ -45,7 +45,8 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(const float* ac, const
                                                           int P, float sqrt_dk, const int* __restrict__ klen, int nb,
                                                           int causal, float* attn, float* __restrict__ pdrop,
                                                           uint32_t thr, float dscale, uint64_t seed, int Z, int Tq,
-                                                          int Tk, long lds, long ldp) {
+                                                          int Tk, long lds, long ldp, const uint64_t* __restrict__ key) {
+  seed = esp::keyed(seed, key);
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= (long)Z * Tq) return;
@@ -103,7 +104,8 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(const float* ac, const
 template <int PER>
 __global__ __launch_bounds__(256) void softmax_bwd_kernel(const float* __restrict__ attn, const float* dP, float* dS,
                                                           uint32_t thr, float dscale, uint64_t seed, float sqrt_dk,
-                                                          long rows, int Tk, long lds) {
+                                                          long rows, int Tk, long lds, const uint64_t* __restrict__ key) {
+  seed = esp::keyed(seed, key);
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -200,7 +202,7 @@ ESP_API int esp_attn_softmax_fwd(const float* ac, const float* bd, int relpos, i
   hipStream_t st = (hipStream_t)stream;
 #define ESP_SM(PER)                                                                                                 \
   hipLaunchKernelGGL(softmax_fwd_kernel<PER>, grid, dim3(256), 0, st, ac, bd, relpos, P, sqrt_dk, klen, nb, causal, \
-                     attn, pdrop, thr, ds, (uint64_t)seed, Z, Tq, Tk, lds, ldp)
+                     attn, pdrop, thr, ds, (uint64_t)seed, Z, Tq, Tk, lds, ldp, esp::rng_key_ptr())
   if (Tk <= 64) ESP_SM(1);
   else if (Tk <= 128) ESP_SM(2);
   else if (Tk <= 256) ESP_SM(4);
@@ -220,7 +222,7 @@ ESP_API int esp_attn_softmax_bwd(const float* attn, const float* dP, float* dS, 
   dim3 grid((unsigned)((rows + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
 #define ESP_SB(PER) \
-  hipLaunchKernelGGL(softmax_bwd_kernel<PER>, grid, dim3(256), 0, st, attn, dP, dS, thr, ds, (uint64_t)seed, sqrt_dk, rows, Tk, lds)
+  hipLaunchKernelGGL(softmax_bwd_kernel<PER>, grid, dim3(256), 0, st, attn, dP, dS, thr, ds, (uint64_t)seed, sqrt_dk, rows, Tk, lds, esp::rng_key_ptr())
   if (Tk <= 64) ESP_SB(1);
   else if (Tk <= 128) ESP_SB(2);
   else if (Tk <= 256) ESP_SB(4);

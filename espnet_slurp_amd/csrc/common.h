@@ -26,6 +26,11 @@ __device__ __forceinline__ uint32_t rng_u32(uint64_t seed, uint64_t idx) {
   z ^= z >> 31;
   return (uint32_t)(z >> 32);
 }
+// Optional device-resident dropout key (esp_set_rng_key): every dropout kernel XORs its seed
+// with *key, so a captured HIP graph draws fresh masks on every replay (the key is advanced
+// on device by esp_rng_advance) while the host-side seeds stay baked into the graph.
+const uint64_t* rng_key_ptr();
+__device__ __forceinline__ uint64_t keyed(uint64_t seed, const uint64_t* key) { return key ? seed ^ *key : seed; }
 // keep with probability (1-p): threshold = p * 2^32
 __device__ __forceinline__ bool keep_elem(uint64_t seed, uint64_t idx, uint32_t thresh) {
   return rng_u32(seed, idx) >= thresh;

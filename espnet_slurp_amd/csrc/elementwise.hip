@@ -9,6 +9,8 @@
 
 namespace esp {
 static thread_local char g_err[512] = "";
+static const uint64_t* g_rng_key = nullptr;
+const uint64_t* rng_key_ptr() { return g_rng_key; }
 void set_error(const char* fmt, ...) {
   va_list ap;
   va_start(ap, fmt);
@@ -18,7 +20,11 @@ void set_error(const char* fmt, ...) {
 }  // namespace esp
 
 ESP_API const char* esp_last_error(void) { return esp::g_err; }
-ESP_API int esp_abi_version(void) { return 4; }
+ESP_API int esp_abi_version(void) { return 5; }
+ESP_API int esp_set_rng_key(const unsigned long long* key) {
+  esp::g_rng_key = (const uint64_t*)key;
+  return 0;
+}
 
 namespace {
 
@@ -38,7 +44,8 @@ inline int grid_for(long n, int per_thread = 1) {
 // dx = dy * keep*scale * act'(h)        (act: 0 none, 1 relu, 2 swish)
 __global__ void act_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ h,
                                float* __restrict__ dx, long n, int act, uint32_t thr, float scale,
-                               uint64_t seed, long idx_off) {
+                               uint64_t seed, long idx_off, const uint64_t* __restrict__ key) {
+  seed = esp::keyed(seed, key);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     float g = dy[i];
     if (thr) g = esp::keep_elem(seed, (uint64_t)(i + idx_off), thr) ? g * scale : 0.f;
@@ -54,7 +61,9 @@ __global__ void act_bwd_kernel(const float* __restrict__ dy, const float* __rest
 
 // y = alpha * keep*scale * x (+ beta * r)  — dropout forward/backward on residual branches
 __global__ void scale_drop_kernel(const float* __restrict__ x, float* __restrict__ y, long n, float alpha,
-                                  uint32_t thr, float scale, uint64_t seed, const float* r, float beta) {
+                                  uint32_t thr, float scale, uint64_t seed, const float* r, float beta,
+                                  const uint64_t* __restrict__ key) {
+  seed = esp::keyed(seed, key);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     float v = x[i];
     if (thr) v = esp::keep_elem(seed, (uint64_t)i, thr) ? v * scale : 0.f;
@@ -68,7 +77,9 @@ __global__ void scale_drop_kernel(const float* __restrict__ x, float* __restrict
 // decoder: x = drop(E[tok] * xscale + pe[l])                            (embedding.py:81-94)
 __global__ void embed_fwd_kernel(const int64_t* __restrict__ tok, const float* __restrict__ E,
                                  const float* __restrict__ pe, float* __restrict__ y, int L, int D,
-                                 float xscale, uint32_t thr, float scale, uint64_t seed, long n) {
+                                 float xscale, uint32_t thr, float scale, uint64_t seed, long n,
+                                 const uint64_t* __restrict__ key) {
+  seed = esp::keyed(seed, key);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const long row = i / D;
     const int d = (int)(i - row * D);
@@ -83,7 +94,8 @@ __global__ void embed_fwd_kernel(const int64_t* __restrict__ tok, const float* _
 // per vocab row scans the token list in order)
 __global__ void embed_bwd_kernel(const int64_t* __restrict__ tok, const float* __restrict__ dy,
                                  float* __restrict__ dE, int nrows, int D, float xscale, uint32_t thr,
-                                 float scale, uint64_t seed) {
+                                 float scale, uint64_t seed, const uint64_t* __restrict__ key) {
+  seed = esp::keyed(seed, key);
   const int v = blockIdx.x;
   for (int d = threadIdx.x; d < D; d += blockDim.x) {
     float acc = 0.f;
@@ -229,8 +241,14 @@ __global__ void norm_finalize_kernel(const double* __restrict__ part, int nb, fl
 // Skips entirely when the finite flag is 0 (trainer.py:651-667).
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                             float* __restrict__ v, long n, const float* __restrict__ clip, float lr,
-                            float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt) {
+                            float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt,
+                            const float* __restrict__ hyper) {
   if (clip[2] == 0.f) return;
+  if (hyper) {  // device-resident step hyper-parameters (HIP-graph replay): {lr, bc1, sqrt(bc2)}
+    lr = hyper[0];
+    bc1 = hyper[1];
+    bc2_sqrt = hyper[2];
+  }
   const float coef = clip[1];
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     float gi = g[i] * coef;
@@ -252,7 +270,7 @@ ESP_API int esp_act_bwd(const float* dy, const float* h, float* dx, long n, int 
                         unsigned long long seed, long idx_off, void* stream) {
   const uint32_t thr = drop_threshold(drop_p);
   hipLaunchKernelGGL(act_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, dy, h, dx, n, act,
-                     thr, thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed, idx_off);
+                     thr, thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed, idx_off, esp::rng_key_ptr());
   ESP_CHECK_LAUNCH("esp_act_bwd");
   return 0;
 }
@@ -261,7 +279,7 @@ ESP_API int esp_scale_dropout(const float* x, float* y, long n, float alpha, flo
                               const float* r, float beta, void* stream) {
   const uint32_t thr = drop_threshold(drop_p);
   hipLaunchKernelGGL(scale_drop_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, y, n, alpha, thr,
-                     thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed, r, beta);
+                     thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed, r, beta, esp::rng_key_ptr());
   ESP_CHECK_LAUNCH("esp_scale_dropout");
   return 0;
 }
@@ -278,7 +296,7 @@ ESP_API int esp_embed_fwd(const long long* tok, const float* E, const float* pe,
   const uint32_t thr = drop_threshold(drop_p);
   const long n = (long)nrows * D;
   hipLaunchKernelGGL(embed_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const int64_t*)tok, E,
-                     pe, y, L, D, xscale, thr, thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed, n);
+                     pe, y, L, D, xscale, thr, thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed, n, esp::rng_key_ptr());
   ESP_CHECK_LAUNCH("esp_embed_fwd");
   return 0;
 }
@@ -287,7 +305,7 @@ ESP_API int esp_embed_bwd(const long long* tok, const float* dy, float* dE, int 
                           float drop_p, unsigned long long seed, void* stream) {
   const uint32_t thr = drop_threshold(drop_p);
   hipLaunchKernelGGL(embed_bwd_kernel, dim3(V), dim3(256), 0, (hipStream_t)stream, (const int64_t*)tok, dy, dE, nrows,
-                     D, xscale, thr, thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed);
+                     D, xscale, thr, thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed, esp::rng_key_ptr());
   ESP_CHECK_LAUNCH("esp_embed_bwd");
   return 0;
 }
@@ -323,7 +341,60 @@ ESP_API int esp_adam(float* p, const float* g, float* m, float* v, long n, const
   const float bc1 = (float)(1.0 - pow((double)b1, (double)step));  // python-float math, as torch
   const float bc2 = (float)(1.0 - pow((double)b2, (double)step));
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, clip, lr,
-                     b1, b2, eps, wd, bc1, sqrtf(bc2));
+                     b1, b2, eps, wd, bc1, sqrtf(bc2), nullptr);
   ESP_CHECK_LAUNCH("esp_adam");
+  return 0;
+}
+
+// ---- device-resident optimizer bookkeeping, so a whole training step can be one HIP graph.
+// state[0] = Adam steps applied so far, state[1] = WarmupLR steps taken (scheduler.last_epoch).
+namespace {
+__global__ void opt_hyper_kernel(const double* __restrict__ state, double base_lr, double warmup, float b1, float b2,
+                                 float* __restrict__ hyper) {
+  const double t = state[0] + 1.0, s = state[1] + 1.0;
+  double lr = base_lr;
+  if (warmup > 0.0) lr = base_lr * sqrt(warmup) * fmin(1.0 / sqrt(s), s * pow(warmup, -1.5));
+  hyper[0] = (float)lr;
+  hyper[1] = (float)(1.0 - pow((double)b1, t));
+  hyper[2] = sqrtf((float)(1.0 - pow((double)b2, t)));
+}
+__global__ void opt_advance_kernel(double* __restrict__ state, const float* __restrict__ clip) {
+  if (clip[2] != 0.f) {
+    state[0] += 1.0;
+    state[1] += 1.0;
+  }
+}
+__global__ void rng_advance_kernel(unsigned long long* __restrict__ key) {
+  uint64_t z = *key + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  *key = z ^ (z >> 31);
+}
+}  // namespace
+
+ESP_API int esp_opt_hyper(const double* state, double base_lr, double warmup, float b1, float b2, float* hyper,
+                          void* stream) {
+  hipLaunchKernelGGL(opt_hyper_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, state, base_lr, warmup, b1, b2, hyper);
+  ESP_CHECK_LAUNCH("esp_opt_hyper");
+  return 0;
+}
+
+ESP_API int esp_adam_dev(float* p, const float* g, float* m, float* v, long n, const float* clip, const float* hyper,
+                         float b1, float b2, float eps, float wd, void* stream) {
+  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, clip, 0.f, b1,
+                     b2, eps, wd, 1.f, 1.f, hyper);
+  ESP_CHECK_LAUNCH("esp_adam_dev");
+  return 0;
+}
+
+ESP_API int esp_opt_advance(double* state, const float* clip, void* stream) {
+  hipLaunchKernelGGL(opt_advance_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, state, clip);
+  ESP_CHECK_LAUNCH("esp_opt_advance");
+  return 0;
+}
+
+ESP_API int esp_rng_advance(unsigned long long* key, void* stream) {
+  hipLaunchKernelGGL(rng_advance_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, key);
+  ESP_CHECK_LAUNCH("esp_rng_advance");
   return 0;
 }

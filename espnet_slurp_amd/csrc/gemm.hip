@@ -53,6 +53,7 @@ struct GemmArgs {
   uint32_t drop_thresh;  // 0 = no dropout
   float drop_scale;
   uint64_t seed;
+  const uint64_t* key;  // device dropout key (esp_set_rng_key) or NULL
   int batch;
   int splits, kchunk;  // split-K: blockIdx.z = z*splits + split; partials -> work
   float* work;
@@ -76,6 +77,7 @@ __host__ __device__ inline int epi_kind(const GemmArgs& g) {
 template <int EPI>
 __device__ __forceinline__ void epi_store(const GemmArgs& g, long cbase, uint64_t dbase, int m, int n, float acc) {
   const long off = cbase + (long)m * g.ldc + n;
+  const uint64_t seed = g.drop_thresh ? esp::keyed(g.seed, g.key) : 0;
   float v = acc;
   if constexpr (EPI == EPI_FWD) {
     if (g.bias) v += g.bias[n];
@@ -84,14 +86,14 @@ __device__ __forceinline__ void epi_store(const GemmArgs& g, long cbase, uint64_
     else if (g.act == ACT_SWISH) v = v / (1.0f + expf(-v));
     if (g.drop_thresh) {
       const uint64_t idx = dbase + (uint64_t)m * (uint64_t)g.N + n;
-      v = esp::keep_elem(g.seed, idx, g.drop_thresh) ? v * g.drop_scale : 0.f;
+      v = esp::keep_elem(seed, idx, g.drop_thresh) ? v * g.drop_scale : 0.f;
     }
   } else if constexpr (EPI == EPI_BWD) {
     // gradient w.r.t. the pre-activation of  h = drop(act(pre))  given dL/dh = v
     if (g.bias) v += g.bias[n];
     if (g.drop_thresh) {
       const uint64_t idx = dbase + (uint64_t)m * (uint64_t)g.N + n;
-      v = esp::keep_elem(g.seed, idx, g.drop_thresh) ? v * g.drop_scale : 0.f;
+      v = esp::keep_elem(seed, idx, g.drop_thresh) ? v * g.drop_scale : 0.f;
     }
     const float x = g.pre[off];
     if (g.bwd_act == ACT_RELU) v = x > 0.f ? v : 0.f;
@@ -119,6 +121,7 @@ __device__ __forceinline__ void store_tiles(const GemmArgs& g, int z, int mrow0,
   const long cbase = c_base(g, z);
   const uint64_t dbase = (uint64_t)z * (uint64_t)g.M * (uint64_t)g.N;
   const bool has_r = g.r != nullptr;
+  const uint64_t seed = (EPI != EPI_PLAIN && g.drop_thresh) ? esp::keyed(g.seed, g.key) : 0;  // before any store
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = ncol0 + j * 32 + l32;
@@ -146,12 +149,12 @@ __device__ __forceinline__ void store_tiles(const GemmArgs& g, int z, int mrow0,
           else if (g.act == ACT_SWISH) v = v / (1.0f + expf(-v));
           if (g.drop_thresh) {
             const uint64_t idx = dbase + (uint64_t)m * (uint64_t)g.N + n;
-            v = esp::keep_elem(g.seed, idx, g.drop_thresh) ? v * g.drop_scale : 0.f;
+            v = esp::keep_elem(seed, idx, g.drop_thresh) ? v * g.drop_scale : 0.f;
           }
         } else if constexpr (EPI == EPI_BWD) {
           if (g.drop_thresh) {
             const uint64_t idx = dbase + (uint64_t)m * (uint64_t)g.N + n;
-            v = esp::keep_elem(g.seed, idx, g.drop_thresh) ? v * g.drop_scale : 0.f;
+            v = esp::keep_elem(seed, idx, g.drop_thresh) ? v * g.drop_scale : 0.f;
           }
           const float x = pp[r];
           if (g.bwd_act == ACT_RELU) v = x > 0.f ? v : 0.f;
@@ -925,6 +928,7 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
   g.r = R; g.aux = aux; g.bias = bias; g.alpha = alpha; g.beta = beta; g.act = act;
   g.bwd_act = bwd_act; g.pre = pre; g.rowsum = rowsum;
   g.seed = seed;
+  g.key = esp::rng_key_ptr();
   if (drop_p > 0.f) {
     double t = (double)drop_p * 4294967296.0;
     g.drop_thresh = (uint32_t)(t >= 4294967295.0 ? 4294967295.0 : t);

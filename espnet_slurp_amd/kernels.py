@@ -229,6 +229,29 @@ def adam(p, g, m, v, clip3, lr, b1, b2, eps, wd, step):
                  float(eps), float(wd), int(step), _st())
 
 
+def opt_hyper(state_f64, base_lr, warmup, b1, b2, hyper3):
+    _native.call("esp_opt_hyper", _p(state_f64), float(base_lr), float(warmup), float(b1), float(b2), _p(hyper3),
+                 _st())
+
+
+def adam_dev(p, g, m, v, clip3, hyper3, b1, b2, eps, wd):
+    _native.call("esp_adam_dev", _p(p), _p(g), _p(m), _p(v), p.numel(), _p(clip3), _p(hyper3), float(b1), float(b2),
+                 float(eps), float(wd), _st())
+
+
+def opt_advance(state_f64, clip3):
+    _native.call("esp_opt_advance", _p(state_f64), _p(clip3), _st())
+
+
+def set_rng_key(key_u64: Optional[torch.Tensor]):
+    """Route every dropout kernel's seed through *key (device int64 tensor) or switch it off."""
+    _native.call("esp_set_rng_key", _p(key_u64))
+
+
+def rng_advance(key_u64):
+    _native.call("esp_rng_advance", _p(key_u64), _st())
+
+
 # ----------------------------------------------------------------------------- norms
 def layernorm_fwd(x2d, w, b, y, mean, rstd, eps=1e-12):
     M, D = x2d.shape

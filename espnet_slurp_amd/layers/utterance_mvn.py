@@ -28,6 +28,10 @@ class UtteranceMVN(AbsNormalize):
         B, T, F = x.shape
         if ilens is None:
             ilens = torch.full((B,), T, dtype=torch.long)
+        return self.apply_prepared(x, K.h2d(ilens.to(torch.int32), x.device)), ilens
+
+    @staticmethod
+    def apply_prepared(x: torch.Tensor, lens_i32: torch.Tensor) -> torch.Tensor:
         y = x.contiguous().clone() if x.requires_grad else x.contiguous()
-        K.utterance_mvn(y, K.h2d(ilens.to(torch.int32), x.device))
-        return y, ilens
+        K.utterance_mvn(y, lens_i32)
+        return y

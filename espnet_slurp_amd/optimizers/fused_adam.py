@@ -44,6 +44,42 @@ class FusedAdam(torch.optim.Optimizer):
                g["lr"], b1, b2, g["eps"], g["weight_decay"], self.n_steps)
         return None
 
+    # ---------------------------------------------------------- device-resident bookkeeping
+    def device_state(self, scheduler=None) -> torch.Tensor:
+        """{Adam steps applied, scheduler steps taken} as a device float64 pair, initialised from
+        the host counters (graph mode keeps counting on device, esp_opt_advance)."""
+        if getattr(self, "_dstate", None) is None:
+            dev = self.flat.flat.device
+            last = float(scheduler.last_epoch) if scheduler is not None else 0.0
+            self._dstate = torch.tensor([float(self.n_steps), last], dtype=torch.float64, device=dev)
+            self._hyper = torch.empty(3, dtype=torch.float32, device=dev)
+        return self._dstate
+
+    def step_device(self, clip: torch.Tensor, scheduler=None):
+        """Adam step whose lr / bias corrections come from the device state (WarmupLR formula
+        on device): capturable in a HIP graph.  Counts the step (and the scheduler step) on
+        device only when the gradient norm was finite."""
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        st = self.device_state(scheduler)
+        warmup = float(getattr(scheduler, "warmup_steps", 0.0) or 0.0)
+        base = scheduler.base_lrs[0] if scheduler is not None else g["lr"]
+        K.opt_hyper(st, base, warmup, b1, b2, self._hyper)
+        K.adam_dev(self.flat.flat, self.flat.grad, self.exp_avg, self.exp_avg_sq, clip, self._hyper, b1, b2, g["eps"],
+                   g["weight_decay"])
+        K.opt_advance(st, clip)
+
+    def sync_from_device(self, scheduler=None):
+        """Copy the device counters back to the host objects (after graph replays)."""
+        if getattr(self, "_dstate", None) is None:
+            return
+        n, s = (int(x) for x in self._dstate.tolist())
+        self.n_steps = n
+        if scheduler is not None and s != scheduler.last_epoch:
+            scheduler.last_epoch = s
+            for grp, lr in zip(self.param_groups, scheduler.get_lr()):
+                grp["lr"] = lr
+
     def zero_grad(self, set_to_none: bool = False):
         self.flat.zero_grad()
 

@@ -22,7 +22,7 @@ from ..flat import FlatParams
 
 
 class FlatGradReducer:
-    def __init__(self, model, flat: FlatParams, bucket_mb: float = 25.0, group=None):
+    def __init__(self, model, flat: FlatParams, bucket_mb: float = 25.0, group=None, hooks: bool = True):
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group)
@@ -51,10 +51,11 @@ class FlatGradReducer:
                     self.bucket_count[bi] += 1
                     break
         self._reset()
-        model._grad_hook = self.module_done
-        for m in (getattr(model, "encoder", None), getattr(model, "decoder", None)):
-            if m is not None:
-                m._grad_hook = self.module_done
+        if hooks:  # eager mode: launch buckets as the explicit backward completes modules
+            model._grad_hook = self.module_done
+            for m in (getattr(model, "encoder", None), getattr(model, "decoder", None)):
+                if m is not None:
+                    m._grad_hook = self.module_done
 
     def _reset(self):
         self.ready = [0] * len(self.buckets)
@@ -92,6 +93,14 @@ class FlatGradReducer:
             else:  # gloo on host tensors (the CPU multi-process tests)
                 self.flat.grad.mul_(1.0 / self.world)
         self._reset()
+
+    def allreduce_sum(self):
+        """SUM all-reduce of the whole flat gradient in the same buckets (HIP-graph mode: the
+        caller pre-scaled each replica's gradient by w_r / sum w)."""
+        hs = [dist.all_reduce(self.flat.grad[s:e], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+              for s, e in self.buckets]
+        for h in hs:
+            h.wait()
 
     def broadcast_buffers(self, model):
         for b in model.buffers():

@@ -17,6 +17,7 @@ import torch.distributed as dist
 
 from ..optimizers.fused_adam import FusedAdam, clip_grad_norm_
 from ..schedulers.warmup_lr import AbsBatchStepScheduler
+from .. import kernels as K
 from .distributed import FlatGradReducer, fused_stats_allreduce
 
 
@@ -29,16 +30,28 @@ class TrainerOptions:
     log_interval: Optional[int] = None
 
 
+class _GraphEntry:
+    """One captured training step for a batch signature (shapes): static inputs + outputs."""
+    __slots__ = ("graph", "speech", "prep", "stats", "weight")
+
+
 class Trainer:
     def __init__(self, model, optimizer: FusedAdam, scheduler=None, options: TrainerOptions = None,
-                 distributed: bool = False, bucket_mb: float = 25.0):
+                 distributed: bool = False, bucket_mb: float = 25.0, cuda_graph: bool = False):
         self.model = model
         self.optimizer = optimizer
         self.scheduler = scheduler
         self.options = options or TrainerOptions()
         self.distributed = distributed and dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size() if self.distributed else 1
-        self.reducer = FlatGradReducer(model, model.flat, bucket_mb) if self.distributed else None
+        # HIP-graph mode: the whole step (forward, backward, clip, Adam, zero_grad; with DDP the
+        # forward + backward, then the gradient exchange and the update eagerly) is captured once
+        # per batch signature and replayed: ~1500 launches per step cost one graph launch
+        self.cuda_graph = bool(cuda_graph) and model.flat.flat.is_cuda
+        self._graphs = {}
+        self._key = None
+        self.reducer = (FlatGradReducer(model, model.flat, bucket_mb, hooks=not self.cuda_graph)
+                        if self.distributed else None)
         self.iiter = 0
         self.n_skipped = 0
         self._clip = torch.empty(3, dtype=torch.float32, device=model.flat.flat.device)
@@ -51,6 +64,8 @@ class Trainer:
 
     def train_one_step(self, batch: Dict[str, torch.Tensor], check_finite: bool = True) -> Dict[str, torch.Tensor]:
         """One iteration of train_one_epoch's loop body; returns device-side stats."""
+        if self.cuda_graph and self.options.accum_grad == 1:
+            return self._graph_step(batch)
         opts = self.options
         self.iiter += 1
         model = self.model
@@ -83,6 +98,89 @@ class Trainer:
         stats["grad_norm"] = self._clip[0:1]
         return stats
 
+    # ---------------------------------------------------------------- HIP-graph path
+    def _graph_step(self, batch):
+        model = self.model
+        speech = batch["speech"]
+        self.iiter += 1
+        self.resolve_pending()
+        prep = model.prepare(batch["speech_lengths"], batch["text"], batch["text_lengths"], speech.shape[1],
+                             speech.shape[2])
+        sig = (tuple(speech.shape), prep.T, prep.Umax, prep.L,
+               tuple((k, tuple(v.shape)) for k, v in sorted(prep.host.items())))
+        e = self._graphs.get(sig)
+        if e is None:  # the capture call's eager warm-up IS this iteration's step
+            e = self._capture(speech, prep)
+            self._graphs[sig] = e
+        else:
+            e.speech.copy_(speech, non_blocking=True)
+            prep.copy_into(e.prep)
+            e.graph.replay()
+            if self.distributed:
+                self._dp_tail(e.stats, e.weight)
+        return e.stats
+
+    def _device_body(self, speech, prep, with_opt: bool):
+        """Device-only work of one step (nothing here talks to the host)."""
+        K.rng_advance(self._key)
+        loss, stats, weight = self.model.forward_prepared(speech, prep)
+        loss.backward()
+        stats = {k: v for k, v in stats.items() if v is not None}
+        stats["grad_norm"] = self._clip[0:1]
+        if with_opt:
+            self._opt_tail()
+        return stats, weight
+
+    def _opt_tail(self):
+        clip_grad_norm_(self.model.flat, self.options.grad_clip, self._clip)
+        self.optimizer.step_device(self._clip, self.scheduler)  # counts itself only if finite
+        self.model.flat.grad.zero_()
+
+    def _dp_tail(self, stats, weight):
+        """DDP semantics after a replayed forward+backward (trainer.py:594-608 + DDP average):
+        grad = sum_r (w_r / sum w) grad_r, stats weighted-averaged, then clip + Adam."""
+        avg, wsum = fused_stats_allreduce({k: v for k, v in stats.items() if k != "grad_norm"}, weight)
+        for k, v in avg.items():
+            stats[k].copy_(v)
+        scale = weight.to(torch.float32).view(1) / wsum
+        K.scale_by_dev(self.model.flat.grad, scale)
+        self.reducer.allreduce_sum()
+        self._opt_tail()
+
+    def _capture(self, speech, prep):
+        dev = self.model.flat.flat.device
+        if self._key is None:  # dropout key from the CPU generator; advanced on device per step
+            self._key = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).to(dev)
+        e = _GraphEntry()
+        e.speech = speech.to(dev).clone()
+        e.prep = prep.to_device(dev)
+        with_opt = not self.distributed
+        K.set_rng_key(self._key)
+        try:
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):  # warm-up = this iteration's step (allocates workspaces)
+                stats, w = self._device_body(e.speech, e.prep, with_opt)
+                if not with_opt:
+                    self._dp_tail(stats, w)
+            torch.cuda.current_stream(dev).wait_stream(side)
+            torch.cuda.synchronize(dev)
+            g = torch.cuda.CUDAGraph()
+            # thread_local: the RCCL watchdog thread keeps querying its events during the capture
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                e.stats, e.weight = self._device_body(e.speech, e.prep, with_opt)
+            e.graph = g
+        finally:
+            K.set_rng_key(None)  # eager calls keep their host seeds; the graph baked the key pointer
+        for k, v in stats.items():  # the warm-up step's values are this call's results
+            e.stats[k].copy_(v)
+        return e
+
+    def sync_host_state(self):
+        """Bring the host-side optimizer / scheduler counters up to date after graph replays."""
+        if self.cuda_graph:
+            self.optimizer.sync_from_device(self.scheduler)
+
     def resolve_pending(self):
         """Apply the bookkeeping of the last optimizer step once its finite flag is on the host:
         WarmupLR batch step if the gradient norm was finite, else count a skipped step
@@ -95,8 +193,9 @@ class Trainer:
         if float(self._flag_host[0]) != 0.0:
             if isinstance(self.scheduler, AbsBatchStepScheduler):
                 self.scheduler.step()
-        else:
+        else:  # torch Adam would not have counted this step (the kernel skipped it on device)
             self.n_skipped += 1
+            self.optimizer.n_steps -= 1
 
     def train_one_epoch(self, iterator: Iterable, reporter=None) -> bool:
         """Loop over (utt_id, batch) like trainer.py:502-714; returns True if every step was
@@ -108,4 +207,5 @@ class Trainer:
             if reporter is not None:
                 reporter(stats)
         self.resolve_pending()
+        self.sync_host_state()
         return (self.n_skipped - sk0) == (self.iiter - it0)

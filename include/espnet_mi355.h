@@ -70,6 +70,21 @@ int esp_utterance_mvn(float* x, int B, int T, int F, const int* lens, void* stre
 int esp_grad_norm(const float* g, long n, float max_norm, double* work, float* out3, void* stream);
 int esp_adam(float* p, const float* g, float* m, float* v, long n, const float* clip3, float lr,
              float b1, float b2, float eps, float wd, int step, void* stream);
+/* Device-resident optimizer bookkeeping (a whole training step as one HIP graph):
+ * state (2 doubles) = {Adam steps applied, WarmupLR steps taken}.  esp_opt_hyper writes the
+ * next step's {lr, 1-b1^t, sqrt(1-b2^t)} (warmuplr.py:43-50, torch Adam) to hyper (3 floats);
+ * esp_adam_dev reads them; esp_opt_advance counts the step only if clip3[2] (finite) != 0,
+ * which is exactly when trainer.py:651-686 steps the optimizer and the scheduler. */
+int esp_opt_hyper(const double* state, double base_lr, double warmup, float b1, float b2, float* hyper,
+                  void* stream);
+int esp_adam_dev(float* p, const float* g, float* m, float* v, long n, const float* clip3,
+                 const float* hyper, float b1, float b2, float eps, float wd, void* stream);
+int esp_opt_advance(double* state, const float* clip3, void* stream);
+/* Dropout key: every dropout kernel XORs its seed with *key when set (NULL: off).  The key
+ * lives in device memory so a replayed HIP graph draws fresh masks; esp_rng_advance mixes it
+ * (splitmix64) on device. */
+int esp_set_rng_key(const unsigned long long* key);
+int esp_rng_advance(unsigned long long* key, void* stream);
 
 /* ---- normalisation (layer_norm.py:12-38; convolution.py:56-79) */
 int esp_layernorm_fwd(const float* x, const float* w, const float* b, float* y, float* mean,
