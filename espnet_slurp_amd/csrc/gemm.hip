@@ -18,6 +18,8 @@
 // counter-RNG dropout, alpha scale and beta*R residual.
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -62,6 +64,7 @@ struct GemmArgs {
   const float* pre;  // pre-activation (same layout as C) for bwd_act
   float* rowsum;     // != NULL: rowsum[m] += sum_k A(m,k)  (bias gradient of a weight-gradient GEMM)
   float* rs_work;    // split-K partial row sums [split][M]
+  int wide;          // float4 epilogue legal (N, ldc, batch strides % 4 == 0, 16-B aligned C/R/aux/pre/bias/work)
 };
 
 // Fused epilogue for output element (m, n) of batch z with raw accumulator `acc`.  The kind is
@@ -170,6 +173,126 @@ __device__ __forceinline__ void store_tiles(const GemmArgs& g, int z, int mrow0,
     }
   }
 }
+// ---------------------------------------------------------------- widened epilogue
+// A 32x32 f32 MFMA accumulator holds one COLUMN per lane (16 rows), so a direct store is 16
+// dword stores per tile.  Two DPP butterfly stages transpose 4x4 blocks inside each lane quad:
+// afterwards lane (h, l32 = 4q + j) holds in registers 4g..4g+3 the row 8g + 4h + j, columns
+// 4q..4q+3 — one float4 per group, 4 dwordx4 stores per tile (the store tail is issue-bound:
+// 4x fewer instructions for the same bytes).  Residual / pre-activation loads widen alike.
+__device__ __forceinline__ float dpp_xor1(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
+}
+__device__ __forceinline__ float dpp_xor2(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
+}
+__device__ __forceinline__ void quad_transpose(f32x16& v, int lane) {
+  const bool odd = lane & 1, hi = lane & 2;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float a0 = v[4 * g], a1 = v[4 * g + 1], a2 = v[4 * g + 2], a3 = v[4 * g + 3];
+    // stage 1: reg k of lane j takes reg k^1 of lane j^1 where the parities of j and k differ
+    const float s0 = dpp_xor1(a1), s1 = dpp_xor1(a0), s2 = dpp_xor1(a3), s3 = dpp_xor1(a2);
+    const float b0 = odd ? s0 : a0, b1 = odd ? a1 : s1, b2 = odd ? s2 : a2, b3 = odd ? a3 : s3;
+    // stage 2: the same with bit 1
+    const float t0 = dpp_xor2(b2), t1 = dpp_xor2(b3), t2 = dpp_xor2(b0), t3 = dpp_xor2(b1);
+    v[4 * g] = hi ? t0 : b0;
+    v[4 * g + 1] = hi ? t1 : b1;
+    v[4 * g + 2] = hi ? b2 : t2;
+    v[4 * g + 3] = hi ? b3 : t3;
+  }
+}
+
+// needs N % 4 == 0, ldc % 4 == 0 and 16-B aligned C / R / aux / pre / bias (host: g.wide)
+template <int EPI, int TM, int TN>
+__device__ __forceinline__ void store_tiles_wide(const GemmArgs& g, int z, int mrow0, int ncol0, int lane,
+                                                 f32x16 (&acc)[TM][TN]) {
+  const int h = lane >> 5, l32 = lane & 31;
+  const long cbase = c_base(g, z);
+  const uint64_t dbase = (uint64_t)z * (uint64_t)g.M * (uint64_t)g.N;
+  const bool has_r = g.r != nullptr;
+  const uint64_t seed = (EPI != EPI_PLAIN && g.drop_thresh) ? esp::keyed(g.seed, g.key) : 0;  // before any store
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = ncol0 + j * 32 + 4 * (l32 >> 2);
+    const bool nok = n < g.N;
+    float4 bn = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (EPI != EPI_PLAIN && g.bias && nok) bn = *reinterpret_cast<const float4*>(g.bias + n);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      quad_transpose(acc[i][j], lane);
+      float4 rr[4], pp[EPI == EPI_BWD ? 4 : 1];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int m = mrow0 + i * 32 + 8 * q + 4 * h + (l32 & 3);
+        const long off = cbase + (long)m * g.ldc + n;
+        const bool ok = nok && m < g.M;
+        rr[q] = (has_r && ok) ? *reinterpret_cast<const float4*>(g.r + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if constexpr (EPI == EPI_BWD)
+          pp[q] = ok ? *reinterpret_cast<const float4*>(g.pre + off) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int m = mrow0 + i * 32 + 8 * q + 4 * h + (l32 & 3);
+        if (!nok || m >= g.M) continue;
+        const long off = cbase + (long)m * g.ldc + n;
+        float v[4] = {acc[i][j][4 * q] + bn.x, acc[i][j][4 * q + 1] + bn.y, acc[i][j][4 * q + 2] + bn.z,
+                      acc[i][j][4 * q + 3] + bn.w};
+        const float r4[4] = {rr[q].x, rr[q].y, rr[q].z, rr[q].w};
+        if constexpr (EPI == EPI_FWD) {
+          if (g.aux) *reinterpret_cast<float4*>(g.aux + off) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float w = v[e];
+          if constexpr (EPI == EPI_FWD) {
+            if (g.act == ACT_RELU) w = fmaxf(w, 0.f);
+            else if (g.act == ACT_SWISH) w = w / (1.0f + expf(-w));
+            if (g.drop_thresh) {
+              const uint64_t idx = dbase + (uint64_t)m * (uint64_t)g.N + n + e;
+              w = esp::keep_elem(seed, idx, g.drop_thresh) ? w * g.drop_scale : 0.f;
+            }
+          } else if constexpr (EPI == EPI_BWD) {
+            if (g.drop_thresh) {
+              const uint64_t idx = dbase + (uint64_t)m * (uint64_t)g.N + n + e;
+              w = esp::keep_elem(seed, idx, g.drop_thresh) ? w * g.drop_scale : 0.f;
+            }
+            const float xp = e == 0 ? pp[q].x : e == 1 ? pp[q].y : e == 2 ? pp[q].z : pp[q].w;
+            if (g.bwd_act == ACT_RELU) w = xp > 0.f ? w : 0.f;
+            else {
+              const float sg = 1.0f / (1.0f + expf(-xp));
+              w = w * (sg * (1.0f + xp * (1.0f - sg)));
+            }
+          }
+          w *= g.alpha;
+          if (has_r) w += g.beta * r4[e];
+          v[e] = w;
+        }
+        *reinterpret_cast<float4*>(g.c + off) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+}
+template <int TM, int TN>
+__device__ __forceinline__ void store_partials_wide(const GemmArgs& g, float* W, int mrow0, int ncol0, int lane,
+                                                    f32x16 (&acc)[TM][TN]) {
+  const int h = lane >> 5, l32 = lane & 31;
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      quad_transpose(acc[i][j], lane);
+      const int n = ncol0 + j * 32 + 4 * (l32 >> 2);
+      if (n >= g.N) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int m = mrow0 + i * 32 + 8 * q + 4 * h + (l32 & 3);
+        if (m < g.M)
+          *reinterpret_cast<float4*>(W + (long)m * g.N + n) =
+              make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]);
+      }
+    }
+}
+
 // split-K partial stores: W[split][z][M][N]
 template <int TM, int TN>
 __device__ __forceinline__ void store_partials(const GemmArgs& g, float* W, int mrow0, int ncol0, int h, int l32,
@@ -509,6 +632,10 @@ struct GldsArgs {
   FastDiv hw_b, wo_b;  // I2C_RC: output pixels per map (Ho*Wo), Wo
   FastDiv hw_a, wo_a;  // I2C_KC
   int ntx, nty;        // tile grid (N tiles, M tiles)
+  int ntiles;          // ntx * nty * batch * splits
+  int abl;             // diagnostic ablation bits (ESP_GEMM_ABL, timing only): 1 no DMA after the
+                       // first slab, 2 no epilogue stores, 4 no k-loop barrier / waits, 16 dword
+                       // (not float4) epilogue stores
 };
 
 constexpr int GL_BK = 32;
@@ -627,6 +754,38 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// Tile t of the launch -> coordinates.  Tiles are processed in rounds of G (the grid): tile t
+// runs on block t % G, which the hardware placed on XCD (t % G) & 7; inside a round the tile
+// order is remapped (bijectively, also for a partial last round) so that the tiles resident on
+// one XCD at the same time are consecutive: they share A row panels in that XCD's L2.
+struct TileCoord {
+  int m0, n0, tn, z, split, kbeg, kend, nk;
+};
+template <int BNT>
+__device__ __forceinline__ TileCoord tile_coord(const GemmArgs& g, const GldsArgs& x, int t, int G) {
+  const int round = t / G, b = t - round * G;
+  const int nr = min(G, x.ntiles - round * G);
+  const int xcd = b & 7, per = nr >> 3, rem = nr & 7;
+  const int wg = round * G + (xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per) + (b >> 3);
+  TileCoord c;
+  c.tn = wg % x.ntx;
+  const int t2 = wg / x.ntx;
+  const int tm = t2 % x.nty;
+  const int zz = t2 / x.nty;
+  c.split = zz % g.splits;
+  c.z = zz / g.splits;
+  c.kbeg = c.split * g.kchunk;
+  c.kend = min(g.K, c.kbeg + g.kchunk);
+  c.nk = (c.kend - c.kbeg + GL_BK - 1) / GL_BK;  // >= 1: the host routes K == 0 elsewhere
+  c.m0 = tm * BM;
+  c.n0 = c.tn * BNT;
+  return c;
+}
+
+// Persistent: block b processes tiles b, b+G, b+2G, ... as ONE continuous slab pipeline — the
+// first slab of the next tile streams in during the last slab of the current one, and the
+// current tile's epilogue stores drain while the next tile's MFMAs run (on this and the other
+// resident block's waves).  With G = #tiles every block runs one tile (the classic launch).
 template <int MA, int MB, int BNT, bool RS, int EPI>
 __global__ __launch_bounds__(NT, 2) void gemm_glds_kernel(GemmArgs g, GldsArgs x) {
   constexpr int WN = BNT / 64, WM = 4 / WN, TM = BM / (WM * 32), TN = 2;
@@ -634,113 +793,144 @@ __global__ __launch_bounds__(NT, 2) void gemm_glds_kernel(GemmArgs g, GldsArgs x
   constexpr int NIA = A_SZ / 4 / NT, NIB = B_SZ / 4 / NT;
   __shared__ __attribute__((aligned(16))) float smem[2 * BUF];
 
-  // XCD-aware remap of the linear block id (bijective for any grid size)
-  const int nbl = gridDim.x;
-  const int orig = blockIdx.x;
-  const int xcd = orig & 7, per = nbl >> 3, rem = nbl & 7;
-  const int wg = (xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per) + (orig >> 3);
-  const int tn = wg % x.ntx;
-  const int t2 = wg / x.ntx;
-  const int tm = t2 % x.nty;
-  const int zz = t2 / x.nty;
-  const int split = zz % g.splits;
-  const int z = zz / g.splits;
-  const int z1 = z / g.nb2, z2 = z - z1 * g.nb2;
-  const int kbeg = split * g.kchunk;
-  const int kend = min(g.K, kbeg + g.kchunk);
-  const float* Ab = g.a.p + z1 * g.a.s1 + z2 * g.a.s2;
-  const float* Bb = g.b.p + z1 * g.b.s1 + z2 * g.b.s2;
-  const int m0 = tm * BM, n0 = tn * BNT;
+  const int G = gridDim.x;
+  int t = blockIdx.x;
+  if (t >= x.ntiles) return;
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int h = lane >> 5, l32 = lane & 31;
 
+  auto a_base = [&](const TileCoord& c) {
+    const int z1 = c.z / g.nb2, z2 = c.z - z1 * g.nb2;
+    return g.a.p + z1 * g.a.s1 + z2 * g.a.s2;
+  };
+  auto b_base = [&](const TileCoord& c) {
+    const int z1 = c.z / g.nb2, z2 = c.z - z1 * g.nb2;
+    return g.b.p + z1 * g.b.s1 + z2 * g.b.s2;
+  };
+
+  TileCoord c = tile_coord<BNT>(g, x, t, G);
   Stage<MA, BM, NIA> sa;
   Stage<MB, BNT, NIB> sb;
-  sa.init(g.a, Ab, g.M, g.K, m0, x.c_a, x.hw_a, x.wo_a, wave, lane);
-  sb.init(g.b, Bb, g.N, g.K, n0, x.c_b, x.hw_b, x.wo_b, wave, lane);
+  sa.init(g.a, a_base(c), g.M, g.K, c.m0, x.c_a, x.hw_a, x.wo_a, wave, lane);
+  sb.init(g.b, b_base(c), g.N, g.K, c.n0, x.c_b, x.hw_b, x.wo_b, wave, lane);
+  sa.issue(g.a, g.K, c.kbeg, smem, wave, x.c_a, x.hw_a, x.wo_a);
+  sb.issue(g.b, g.K, c.kbeg, smem + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
+  wait_vm0();
+  raw_barrier();
+  int buf = 0;
 
-  f32x16 acc[TM][TN];
+  for (;;) {
+    f32x16 acc[TM][TN];
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    // fused bias gradient (A = dy in RC mode): the first column tile's wn==0 waves sum their A
+    // fragments over k; halves combined and splits reduced in fixed order (deterministic)
+    const bool do_rs = RS && c.tn == 0 && wn == 0;
+    float rs[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) rs[i] = 0.f;
+    const int tnext = t + G;
+    const bool has_next = tnext < x.ntiles;
+    TileCoord cn = c;
 
-  // fused bias gradient (A = dy in RC mode): the first column tile's wn==0 waves sum their A
-  // fragments over k; halves combined and splits reduced in fixed order (deterministic)
-  const bool do_rs = RS && tn == 0 && wn == 0;
-  float rs[TM];
+    // frags + MFMAs of one staged slab (and the fused row sums)
+    auto compute = [&](const float* cur) {
+      float af[TM][16], bf[TN][16];
 #pragma unroll
-  for (int t = 0; t < TM; ++t) rs[t] = 0.f;
-  const int nk = kend > kbeg ? (kend - kbeg + GL_BK - 1) / GL_BK : 0;
-  if (nk > 0) {
-    sa.issue(g.a, g.K, kbeg, smem, wave, x.c_a, x.hw_a, x.wo_a);
-    sb.issue(g.b, g.K, kbeg, smem + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
-    wait_vm0();
-    raw_barrier();
-  }
-  for (int kt = 0; kt < nk; ++kt) {
-    float* cur = smem + (kt & 1) * BUF;
-    if (kt + 1 < nk) {  // slab kt+1 streams into the other buffer (last read before the previous barrier)
-      float* nxt = smem + ((kt + 1) & 1) * BUF;
-      const int k1 = kbeg + (kt + 1) * GL_BK;
-      sa.issue(g.a, g.K, k1, nxt, wave, x.c_a, x.hw_a, x.wo_a);
-      sb.issue(g.b, g.K, k1, nxt + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
-    } else {
-      const int kv = kend - (kbeg + kt * GL_BK);
+      for (int i = 0; i < TM; ++i) frag16<MA, BM>(cur, wm * TM * 32 + i * 32 + l32, h, af[i]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) frag16<MB, BNT>(cur + A_SZ, wn * 64 + j * 32 + l32, h, bf[j]);
+#pragma unroll
+      for (int s = 0; s < 16; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+      if constexpr (RS) {
+        if (do_rs) {  // after the MFMAs were issued: the adds ride in their shadow
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            float a0 = 0.f;
+#pragma unroll
+            for (int s = 0; s < 16; ++s) a0 += af[i][s];
+            rs[i] += a0;
+          }
+        }
+      }
+    };
+    auto finish_slab = [&]() {
+      if (!(x.abl & 4)) {
+        wait_vm0();     // this wave's DMA of the next slab has landed
+        wait_lgkm0();   // this wave's reads of this slab are done
+        raw_barrier();  // -> everyone's: next slab readable, this buffer free for the one after
+      }
+      buf ^= 1;
+    };
+
+    for (int kt = 0; kt + 1 < c.nk; ++kt) {  // all but the last slab: slab kt+1 streams in
+      const int k1 = c.kbeg + (kt + 1) * GL_BK;
+      float* nxt = smem + (buf ^ 1) * BUF;  // last read before the previous barrier
+      if (!(x.abl & 1)) {
+        sa.issue(g.a, g.K, k1, nxt, wave, x.c_a, x.hw_a, x.wo_a);
+        sb.issue(g.b, g.K, k1, nxt + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
+      }
+      compute(smem + buf * BUF);
+      finish_slab();
+    }
+    {  // last slab: the next tile's first slab streams in (this tile's stages are done)
+      float* cur = smem + buf * BUF;
+      float* nxt = smem + (buf ^ 1) * BUF;
+      if (has_next) {
+        cn = tile_coord<BNT>(g, x, tnext, G);
+        sa.init(g.a, a_base(cn), g.M, g.K, cn.m0, x.c_a, x.hw_a, x.wo_a, wave, lane);
+        sb.init(g.b, b_base(cn), g.N, g.K, cn.n0, x.c_b, x.hw_b, x.wo_b, wave, lane);
+        sa.issue(g.a, g.K, cn.kbeg, nxt, wave, x.c_a, x.hw_a, x.wo_a);
+        sb.issue(g.b, g.K, cn.kbeg, nxt + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
+      }
+      const int kv = c.kend - (c.kbeg + (c.nk - 1) * GL_BK);
       if (kv < GL_BK) {
         zero_tail<MA, BM>(cur, kv);
         zero_tail<MB, BNT>(cur + A_SZ, kv);
         wait_lgkm0();
         raw_barrier();
       }
+      compute(cur);
+      finish_slab();
     }
-    float af[TM][16], bf[TN][16];
+    // epilogue: fire-and-forget stores that drain under the next tile's first slab
+    if (RS && do_rs) {
 #pragma unroll
-    for (int t = 0; t < TM; ++t) frag16<MA, BM>(cur, wm * TM * 32 + t * 32 + l32, h, af[t]);
-#pragma unroll
-    for (int t = 0; t < TN; ++t) frag16<MB, BNT>(cur + A_SZ, wn * 64 + t * 32 + l32, h, bf[t]);
-#pragma unroll
-    for (int s = 0; s < 16; ++s)
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
-    if constexpr (RS) {
-      if (do_rs) {  // after the MFMAs were issued: the adds ride in their shadow
-#pragma unroll
-        for (int t = 0; t < TM; ++t) {
-          float a0 = 0.f;
-#pragma unroll
-          for (int s = 0; s < 16; ++s) a0 += af[t][s];
-          rs[t] += a0;
+      for (int i = 0; i < TM; ++i) {
+        const float v = rs[i] + __shfl_xor(rs[i], 32, 64);  // k halves 0-15 / 16-31 of every slab
+        const int m = c.m0 + wm * TM * 32 + i * 32 + l32;
+        if (h == 0 && m < g.M) {
+          if (g.splits > 1) g.rs_work[(long)c.split * g.M + m] = v;
+          else g.rowsum[m] += v;
         }
       }
     }
-    wait_vm0();    // this wave's DMA of slab kt+1 has landed
-    wait_lgkm0();  // this wave's reads of slab kt are done
-    raw_barrier(); // -> everyone's: slab kt+1 readable, buffer kt free for slab kt+2
-  }
-
-  if (RS && do_rs) {
-#pragma unroll
-    for (int t = 0; t < TM; ++t) {
-      const float v = rs[t] + __shfl_xor(rs[t], 32, 64);  // k halves 0-15 / 16-31 of every slab
-      const int m = m0 + wm * TM * 32 + t * 32 + l32;
-      if (h == 0 && m < g.M) {
-        if (g.splits > 1) g.rs_work[(long)split * g.M + m] = v;
-        else g.rowsum[m] += v;
+    if (!(x.abl & 2)) {
+      float* W = g.splits > 1 ? g.work + ((long)c.split * g.batch + c.z) * (long)g.M * g.N : nullptr;
+      if (g.wide) {
+        if (W) store_partials_wide<TM, TN>(g, W, c.m0 + wm * TM * 32, c.n0 + wn * 64, lane, acc);
+        else store_tiles_wide<EPI, TM, TN>(g, c.z, c.m0 + wm * TM * 32, c.n0 + wn * 64, lane, acc);
+      } else {
+        if (W) store_partials<TM, TN>(g, W, c.m0 + wm * TM * 32, c.n0 + wn * 64, h, l32, acc);
+        else store_tiles<EPI, TM, TN>(g, c.z, c.m0 + wm * TM * 32, c.n0 + wn * 64, h, l32, acc);
       }
     }
+    if (!has_next) break;
+    t = tnext;
+    c = cn;
   }
-  float* W = g.splits > 1 ? g.work + ((long)split * g.batch + z) * (long)g.M * g.N : nullptr;
-  if (W) store_partials<TM, TN>(g, W, m0 + wm * TM * 32, n0 + wn * 64, h, l32, acc);
-  else store_tiles<EPI, TM, TN>(g, z, m0 + wm * TM * 32, n0 + wn * 64, h, l32, acc);
 }
 
 // split-K reduction in fixed split order + the fused epilogue (4 outputs per thread when
@@ -804,6 +994,20 @@ __global__ void rowsum_rc_kernel(const float* __restrict__ p, long ld, int M, in
   out[r] += s;
 }
 
+// resident blocks of the persistent LDS-DMA kernel: 2 per CU (64 KB LDS each);
+// ESP_GEMM_PERSIST=0 launches one block per tile instead
+long g_persist = -1;
+long persist_blocks() {
+  if (g_persist < 0) {
+    const char* e = getenv("ESP_GEMM_PERSIST");
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+    g_persist = (e && atoi(e) == 0) ? (1L << 40) : 2L * cus;
+  }
+  return g_persist;
+}
+
 int g_variant = -1;
 int variant() {
   if (g_variant < 0) {
@@ -836,7 +1040,13 @@ bool launch_glds(const GemmArgs& g, int batch, hipStream_t st) {
     x.hw_b = make_fastdiv(g.b.ic.Ho * g.b.ic.Wo);
     x.wo_b = make_fastdiv(g.b.ic.Wo);
   }
-  const dim3 grid((unsigned)((long)x.ntx * x.nty * batch * g.splits));
+  x.ntiles = (int)((long)x.ntx * x.nty * batch * g.splits);
+  {
+    static int abl = -1;
+    if (abl < 0) abl = getenv("ESP_GEMM_ABL") ? atoi(getenv("ESP_GEMM_ABL")) : 0;
+    x.abl = abl;
+  }
+  const dim3 grid((unsigned)std::min<long>(x.ntiles, persist_blocks()));
   if (can_rs && g.rowsum)
     hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, can_rs, EPI_PLAIN>), grid, dim3(NT), 0, st, g, x);
   else if (kind == EPI_PLAIN)
@@ -929,6 +1139,13 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
   g.bwd_act = bwd_act; g.pre = pre; g.rowsum = rowsum;
   g.seed = seed;
   g.key = esp::rng_key_ptr();
+  g.wide = N % 4 == 0 && ldc % 4 == 0 && sc1 % 4 == 0 && sc2 % 4 == 0 && aligned16(C) && (!R || aligned16(R)) &&
+           (!aux || aligned16(aux)) && (!pre || aligned16(pre)) && (!bias || aligned16(bias)) &&
+           (!work || aligned16(work));
+  {
+    const char* e = getenv("ESP_GEMM_ABL");
+    if (e && (atoi(e) & 16)) g.wide = 0;
+  }
   if (drop_p > 0.f) {
     double t = (double)drop_p * 4294967296.0;
     g.drop_thresh = (uint32_t)(t >= 4294967295.0 ? 4294967295.0 : t);
@@ -946,7 +1163,7 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
   const long target = 2 * 256;
   auto ntiles = [&](int bn) { return (long)((N + bn - 1) / bn) * ((M + BM - 1) / BM) * batch; };
   g.bnt = 0;
-  if (variant() == 4 && g.a.glds && g.b.glds) {
+  if (variant() == 4 && g.a.glds && g.b.glds && K > 0) {
     g.bnt = N <= 64 ? 64 : 128;
     if (g.bnt == 128 && ntiles(128) < target && ntiles(64) >= target) g.bnt = 64;
   }
