@@ -945,6 +945,73 @@ __device__ __forceinline__ void reduce_store(const GemmArgs& g, int z, int m, in
   }
 }
 
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// Split-K reduction + the fused epilogue.  Block = 64 float4 slots x 4 split groups: thread
+// (slot, grp) sums splits grp, grp+4, ... of its float4 (independent 16-B loads, fixed order),
+// the 4 group partials are combined in fixed order through LDS, and each of the 4 threads of a
+// slot then finishes one element (deterministic).  The fused row sums (bias gradient) are
+// reduced by the first blocks.  Requires N % 4 == 0 (else the scalar kernel below).
+constexpr int RED_SLOTS = 64, RED_GROUPS = 4;
+__global__ __launch_bounds__(256) void splitk_reduce4_kernel(GemmArgs g) {
+  __shared__ float4 part[RED_GROUPS][RED_SLOTS];
+  const long MN = (long)g.M * g.N;
+  const long split_stride = MN * g.batch;
+  if (g.rowsum && g.rs_work) {
+    const long m = blockIdx.x * (long)blockDim.x + threadIdx.x;
+    if (m < g.M) {
+      float acc = 0.f;
+      int s = 0;
+      for (; s + 8 <= g.splits; s += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = g.rs_work[(long)(s + u) * g.M + m];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += v[u];
+      }
+      for (; s < g.splits; ++s) acc += g.rs_work[(long)s * g.M + m];
+      g.rowsum[m] += acc;
+    }
+  }
+  const int slot = threadIdx.x & (RED_SLOTS - 1), grp = threadIdx.x / RED_SLOTS;
+  const long total4 = split_stride >> 2;
+  const long e4 = blockIdx.x * (long)RED_SLOTS + slot;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e4 < total4) {
+    const float4* w = reinterpret_cast<const float4*>(g.work) + e4;
+    const long st4 = split_stride >> 2;
+    int s = grp;
+    for (; s + 3 * RED_GROUPS < g.splits; s += 4 * RED_GROUPS) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = w[(long)(s + u * RED_GROUPS) * st4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
+      }
+    }
+    for (; s < g.splits; s += RED_GROUPS) {
+      const float4 v = w[(long)s * st4];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  part[grp][slot] = acc;
+  __syncthreads();
+  if (e4 >= total4) return;
+  float r = 0.f;
+#pragma unroll
+  for (int q = 0; q < RED_GROUPS; ++q) {
+    const float4 v = part[q][slot];
+    r += grp == 0 ? v.x : grp == 1 ? v.y : grp == 2 ? v.z : v.w;
+  }
+  const long e = (e4 << 2) + grp;
+  const int z = (int)(e / MN);
+  const long rr = e - (long)z * MN;
+  const int m = (int)(rr / g.N), n = (int)(rr - (long)m * g.N);
+  reduce_store(g, z, m, n, r);
+}
+
+// scalar fallback (N % 4 != 0)
 __global__ void splitk_reduce_kernel(GemmArgs g) {
   if (g.rowsum && g.rs_work) {
     for (long m = blockIdx.x * (long)blockDim.x + threadIdx.x; m < g.M; m += (long)gridDim.x * blockDim.x) {
@@ -955,25 +1022,6 @@ __global__ void splitk_reduce_kernel(GemmArgs g) {
   }
   const long MN = (long)g.M * g.N;
   const long split_stride = MN * g.batch;
-  if ((g.N & 3) == 0) {
-    const long total4 = split_stride >> 2;
-    for (long e4 = blockIdx.x * (long)blockDim.x + threadIdx.x; e4 < total4; e4 += (long)gridDim.x * blockDim.x) {
-      const long e = e4 << 2;
-      float4 acc = *reinterpret_cast<const float4*>(g.work + e);
-      for (int s = 1; s < g.splits; ++s) {
-        const float4 v = *reinterpret_cast<const float4*>(g.work + s * split_stride + e);
-        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-      }
-      const int z = (int)(e / MN);
-      const long r = e - (long)z * MN;
-      const int m = (int)(r / g.N), n = (int)(r - (long)m * g.N);
-      reduce_store(g, z, m, n, acc.x);
-      reduce_store(g, z, m, n + 1, acc.y);
-      reduce_store(g, z, m, n + 2, acc.z);
-      reduce_store(g, z, m, n + 3, acc.w);
-    }
-    return;
-  }
   for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < split_stride; e += (long)gridDim.x * blockDim.x) {
     const int z = (int)(e / MN);
     const long r = e - (long)z * MN;
@@ -1078,15 +1126,20 @@ int launch(const GemmArgs& g0, int batch, hipStream_t st) {
     else hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 1>), grid, dim3(NT), 0, st, g);
   }
   if (g.splits > 1) {
-    long total = (long)g.M * g.N * batch;
-    long nb = (total + 255) / 256;
-    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)(nb > 16384 ? 16384 : nb)), dim3(256), 0, st, g);
+    const long total = (long)g.M * g.N * batch;
+    if ((g.N & 3) == 0 && aligned16(g.work)) {
+      long nb = (total / 4 + RED_SLOTS - 1) / RED_SLOTS;
+      if (g.rowsum && g.rs_work && nb < (g.M + 255) / 256) nb = (g.M + 255) / 256;
+      hipLaunchKernelGGL(splitk_reduce4_kernel, dim3((unsigned)nb), dim3(256), 0, st, g);
+    } else {
+      const long nb = (total + 255) / 256;
+      hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)(nb > 16384 ? 16384 : nb)), dim3(256), 0, st, g);
+    }
   }
   ESP_CHECK_LAUNCH("gemm_f32");
   return 0;
 }
 
-bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // LDS-DMA staging reads whole 16-B quads along the contiguous dim `cont` (K for KC, the row
 // count for RC) at clamped indices: legal when quads are aligned and the row pitch covers the
