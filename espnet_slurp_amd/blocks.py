@@ -187,15 +187,19 @@ class RelPositionMultiHeadedAttention(nn.Module):
         # ac[z] = q_u[z] k[b,h]^T
         K.gemm(T, T, dk, q_u, qkv, ac, mode_a=K.KC, lda=dk, mode_b=K.KC, ldb=3 * D, ldc=Tp, b_off=D,
                batch=Z, nb2=B, sa=(B * T * dk, T * dk), sb=(dk, T * 3 * D), sc=(B * T * Tp, T * Tp))
-        bd = empty(Z * T * Pp, like=x2d)
-        K.gemm(T, P, dk, q_v, p, bd, mode_a=K.KC, lda=dk, mode_b=K.KC, ldb=D, ldc=Pp,
-               batch=Z, nb2=B, sa=(B * T * dk, T * dk), sb=(dk, 0), sc=(B * T * Pp, T * Pp))
         pa = self.p if training else 0.0
         sa = seeds.next()
         pdrop = empty(Z * T * Tp, like=x2d) if pa > 0 else None
-        K.attn_softmax_fwd(ac, bd, relpos, P, math.sqrt(dk), klen, B, False, ac, pdrop, pa, sa, Z, T, T,
-                           lds=Tp, ldp=Pp)
-        del bd
+        if not self.legacy and K.relpos_fused_ok(T, dk):
+            # bd band on the MFMA inside the softmax kernel: no (Z, T, 2T-1) bd tensor
+            K.relpos_softmax_fwd(q_v, p, D, B, H, ac, math.sqrt(dk), klen, ac, pdrop, pa, sa, T, Tp)
+        else:
+            bd = empty(Z * T * Pp, like=x2d)
+            K.gemm(T, P, dk, q_v, p, bd, mode_a=K.KC, lda=dk, mode_b=K.KC, ldb=D, ldc=Pp,
+                   batch=Z, nb2=B, sa=(B * T * dk, T * dk), sb=(dk, 0), sc=(B * T * Pp, T * Pp))
+            K.attn_softmax_fwd(ac, bd, relpos, P, math.sqrt(dk), klen, B, False, ac, pdrop, pa, sa, Z, T, T,
+                               lds=Tp, ldp=Pp)
+            del bd
         attn = ac
         pv = pdrop if pdrop is not None else attn
         ctx_ = empty(M, D, like=x2d)

@@ -157,6 +157,109 @@ __global__ void relshift_bwd_kernel(const float* __restrict__ dS, long lds, floa
   }
 }
 
+// ---------------------------------------------------------------- fused latest rel-pos softmax
+// One block per (32 query rows, z): the bd window of the block is computed on the MFMA
+//   Sbd[r][c] = q_v[z][i0 + r] . p[kmin + c],   kmin = T - 32 - i0,  c in [0, T + 31)
+// (the 32 x (T+31) band of (q+v) p^T that rel_shift reads: bd_shift[i][j] = Sbd[i-i0][j-(i-i0)+31])
+// into LDS, then each wave finishes 8 score rows: s = (ac + bd_shift) / sqrt(dk), key mask,
+// softmax (wave shuffles), attention-dropout copy.  Replaces the (Z,T,2T-1) bd GEMM + its HBM
+// round trip + the separate softmax pass.  d_k = 64; LDS = 32 x WP floats (WP = 32*ceil((T+31)/32)+4).
+// MFMA operand k-order: lane half hf supplies d = 32c + 16hf + s at step (c, s) for both operands.
+constexpr int RP_ROWS = 32, RP_DK = 64;
+template <int PER>
+__global__ __launch_bounds__(256) void relpos_softmax_fwd_kernel(
+    const float* __restrict__ qv, const float* __restrict__ pm, long ldpm, int nb, int H, const float* ac,
+    float sqrt_dk, const int* __restrict__ klen, float* attn, float* __restrict__ pdrop, uint32_t thr, float dscale,
+    uint64_t seed, int T, long lds, int WP, const uint64_t* __restrict__ key) {
+  extern __shared__ __attribute__((aligned(16))) float sbd[];  // [32][WP]
+  seed = esp::keyed(seed, key);
+  const int z = blockIdx.y;
+  const int i0 = blockIdx.x * RP_ROWS;
+  const int head = z / nb, b = z - head * nb;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int hf = lane >> 5, l32 = lane & 31;
+  const int P = 2 * T - 1;
+  const int kmin = T - RP_ROWS - i0;
+  const int ntile = (T + RP_ROWS - 1 + 31) / 32;
+
+  // A fragments: row i0 + l32 of q_v[z] (rows past T clamped: their scores are never used)
+  float af[2][16];
+  {
+    const float* q = qv + ((long)z * T + min(i0 + l32, T - 1)) * RP_DK;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 v = *reinterpret_cast<const float4*>(q + 32 * c + 16 * hf + 4 * u);
+        af[c][4 * u] = v.x; af[c][4 * u + 1] = v.y; af[c][4 * u + 2] = v.z; af[c][4 * u + 3] = v.w;
+      }
+  }
+  for (int ct = wave; ct < ntile; ct += 4) {
+    const int k = min(max(kmin + ct * 32 + l32, 0), P - 1);
+    const float* pr = pm + (long)k * ldpm + head * RP_DK;
+    float bfr[2][16];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 v = *reinterpret_cast<const float4*>(pr + 32 * c + 16 * hf + 4 * u);
+        bfr[c][4 * u] = v.x; bfr[c][4 * u + 1] = v.y; bfr[c][4 * u + 2] = v.z; bfr[c][4 * u + 3] = v.w;
+      }
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int st = 0; st < 16; ++st) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[c][st], bfr[c][st], acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sbd[((r & 3) + 8 * (r >> 2) + 4 * hf) * WP + ct * 32 + l32] = acc[r];
+  }
+  __syncthreads();
+
+  const int* klp = klen;
+  int kl = klp ? klp[b] : T;
+  if (kl > T) kl = T;
+  for (int rr = wave; rr < RP_ROWS; rr += 4) {
+    const int i = i0 + rr;
+    if (i >= T) break;
+    const long row = (long)z * T + i;
+    const float* acr = ac + row * lds;
+    const float* sb = sbd + rr * WP + (RP_ROWS - 1 - rr);
+    float v[PER];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int j = lane + 64 * e;
+      float sc = -INFINITY;
+      if (j < T && j < kl) sc = (acr[j] + sb[j]) / sqrt_dk;
+      v[e] = sc;
+      mx = fmaxf(mx, sc);
+    }
+    mx = esp::wave_max(mx);
+    float sum = 0.f;
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const float pe = v[e] == -INFINITY ? 0.f : expf(v[e] - mx);
+      v[e] = pe;
+      sum += pe;
+    }
+    sum = esp::wave_sum(sum);
+    const float inv = sum > 0.f ? 1.0f / sum : 0.f;
+    float* ar = attn + row * lds;
+    float* pd = pdrop ? pdrop + row * lds : nullptr;
+#pragma unroll
+    for (int e = 0; e < PER; ++e) {
+      const int j = lane + 64 * e;
+      if (j < T) {
+        const float pe = v[e] * inv;
+        ar[j] = pe;
+        if (pd) pd[j] = esp::keep_elem(seed, (uint64_t)(row * T + j), thr) ? pe * dscale : 0.f;
+      }
+    }
+  }
+}
+
 inline int gridn(long n) {
   long b = (n + 255) / 256;
   return (int)(b > 65536 ? 65536 : (b < 1 ? 1 : b));
@@ -240,5 +343,36 @@ ESP_API int esp_relshift_bwd(const float* dS, long lds, float* dbd, long ldp, in
   hipLaunchKernelGGL(relshift_bwd_kernel, dim3(gridn((long)Z * T * P)), dim3(256), 0, (hipStream_t)stream, dS, lds,
                      dbd, ldp, relpos, Z, T, P);
   ESP_CHECK_LAUNCH("esp_relshift_bwd");
+  return 0;
+}
+
+// Fused latest rel-pos scores + softmax: q_v (Z,T,64) head-major (z = h*nb + b), p rows of
+// length ldpm with head h at column 64h (P = 2T-1 rows), ac (Z,T) pitch lds -> attn (may
+// alias ac) [+ dropout copy pdrop].
+ESP_API int esp_relpos_softmax_fwd(const float* qv, const float* p, long ldp_row, int nb, int H, const float* ac,
+                                   float sqrt_dk, const int* klen, float* attn, float* pdrop, float drop_p,
+                                   unsigned long long seed, int T, long lds, void* stream) {
+  ESP_ARG_CHECK(T >= 1 && T <= 1024 && lds >= T && nb >= 1 && H >= 1, "esp_relpos_softmax_fwd: bad sizes T=%d", T);
+  ESP_ARG_CHECK(ldp_row % 4 == 0 && ((uintptr_t)p & 15) == 0 && ((uintptr_t)qv & 15) == 0,
+                "esp_relpos_softmax_fwd: q_v / p must be 16-B aligned with ld %% 4 == 0");
+  const uint32_t thr = drop_threshold(drop_p);
+  if (!thr) pdrop = nullptr;
+  const float ds = thr ? 1.f / (1.f - drop_p) : 1.f;
+  const int ntile = (T + RP_ROWS - 1 + 31) / 32;
+  const int WP = ntile * 32 + 4;
+  const size_t shm = (size_t)RP_ROWS * WP * sizeof(float);
+  ESP_ARG_CHECK(shm <= 65536, "esp_relpos_softmax_fwd: T=%d needs %zu B of LDS (> 64 KB)", T, shm);
+  dim3 grid((unsigned)((T + RP_ROWS - 1) / RP_ROWS), (unsigned)(nb * H));
+  hipStream_t st = (hipStream_t)stream;
+#define ESP_RP(PER)                                                                                              \
+  hipLaunchKernelGGL(relpos_softmax_fwd_kernel<PER>, grid, dim3(256), shm, st, qv, p, ldp_row, nb, H, ac, sqrt_dk, \
+                     klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, WP, esp::rng_key_ptr())
+  if (T <= 64) ESP_RP(1);
+  else if (T <= 128) ESP_RP(2);
+  else if (T <= 256) ESP_RP(4);
+  else if (T <= 512) ESP_RP(8);
+  else ESP_RP(16);
+#undef ESP_RP
+  ESP_CHECK_LAUNCH("esp_relpos_softmax_fwd");
   return 0;
 }

@@ -323,6 +323,18 @@ def attn_softmax_fwd(ac, bd, relpos, P, sqrt_dk, klen_i32, nb, causal, attn, pdr
                  _p(attn), _p(pdrop), float(drop_p), seed, Z, Tq, Tk, lds or Tk, ldp or max(P, 1), _st())
 
 
+def relpos_softmax_fwd(q_v, p, ldp_row, nb, H, ac, sqrt_dk, klen_i32, attn, pdrop, drop_p, seed, T, lds):
+    """Fused latest rel-pos bd window (MFMA) + rel_shift + masked softmax + dropout copy."""
+    _f32(q_v, p, ac, attn, pdrop)
+    _native.call("esp_relpos_softmax_fwd", _p(q_v), _p(p), ldp_row, nb, H, _p(ac), float(sqrt_dk), _p(klen_i32),
+                 _p(attn), _p(pdrop), float(drop_p), int(seed) & (2 ** 64 - 1), T, lds, _st())
+
+
+def relpos_fused_ok(T: int, dk: int) -> bool:
+    """Whether esp_relpos_softmax_fwd covers this shape (d_k 64, 32-row window in 64 KB LDS)."""
+    return dk == 64 and 32 * (32 * ((T + 62) // 32) + 4) * 4 <= 65536
+
+
 def attn_softmax_bwd(attn, dP, dS, drop_p, seed, sqrt_dk, rows, Tk, lds=None):
     _native.call("esp_attn_softmax_bwd", _p(attn), _p(dP), _p(dS), float(drop_p), seed, float(sqrt_dk), rows, Tk,
                  lds or Tk, _st())

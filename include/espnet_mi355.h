@@ -123,6 +123,15 @@ int esp_attn_softmax_bwd(const float* attn, const float* dP, float* dS, float dr
                          void* stream);
 int esp_relshift_bwd(const float* dS, long lds, float* dbd, long ldp, int relpos, int Z, int T, int P,
                      void* stream);
+/* Fused latest rel-pos scores + softmax (attention.py:240-263 with the latest rel_shift,
+ * embedding.py:173-244): bd_shift[i][j] = q_v[i] . p[j + T-1-i] is computed on the MFMA per
+ * 32-row block inside the kernel (no (Z,T,2T-1) bd tensor), then s = (ac + bd_shift)/sqrt(dk),
+ * key mask j < klen[b], softmax, dropout copy.  q_v (Z,T,64) head-major z = h*nb + b;
+ * p: P = 2T-1 rows of pitch ldp_row, head h at column 64h.  d_k must be 64; T such that the
+ * 32 x (32*ceil((T+31)/32)+4) float window fits 64 KB (T <= 449).  attn may alias ac. */
+int esp_relpos_softmax_fwd(const float* qv, const float* p, long ldp_row, int nb, int H, const float* ac,
+                           float sqrt_dk, const int* klen, float* attn, float* pdrop, float drop_p,
+                           unsigned long long seed, int T, long lds, void* stream);
 
 /* ---- Conv2dSubsampling (subsampling.py:53-87), NHWC */
 int esp_conv1_fwd(const float* x, const float* W, const float* bias, float* z, int B, int T,

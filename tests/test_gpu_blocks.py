@@ -63,6 +63,56 @@ def test_relpos_mha_block(dev, legacy):
     _check_grads(mod, P, "a")
 
 
+@pytest.mark.parametrize("T,klens", [(29, [29, 23, 15]), (77, [77, 40, 9]), (130, [130, 129, 64])])
+def test_relpos_mha_fused_dk64(dev, T, klens):
+    """d_k = 64 latest rel-pos: the fused bd-window + softmax kernel (esp_relpos_softmax_fwd),
+    several 32-row blocks incl. a partial last block, against the fp64 oracle."""
+    from espnet_slurp_amd import kernels as K
+    torch.manual_seed(3)
+    B, D, H = 3, 256, 4
+    assert K.relpos_fused_ok(T, D // H)
+    klen = torch.tensor(klens)
+    mod = RelPositionMultiHeadedAttention(H, D, 0.0, False).to(dev)
+    with torch.no_grad():
+        for p in mod.parameters():
+            p.normal_(0, 0.1)
+    mod.flat = FlatParams(mod, dev)
+    x = torch.randn(B * T, D)
+    res = torch.randn(B * T, D)
+    dout = torch.randn(B * T, D)
+    pos = pos_table("latest", T, D, dev)
+    out, c = mod.fwd(x.to(dev), res.to(dev), pos, klen.int().to(dev), B, T, 0.0, Seeds(1), True)
+    dx = mod.bwd(c, dout.to(dev))
+    P = _params64(mod, "a")
+    xt = x.double().view(B, T, D).requires_grad_(True)
+    mask = (~O.make_pad_mask(klen, T))[:, None, :]
+    ref = O.rel_mha(P, "a", xt, pos.cpu().double()[None], mask, H, False) + res.double().view(B, T, D)
+    ref.backward(dout.double().view(B, T, D))
+    assert rel_err(out.cpu(), ref.detach().reshape(B * T, D)) < 1e-5
+    assert rel_err(dx.cpu(), xt.grad.reshape(B * T, D)) < 1e-5
+    _check_grads(mod, P, "a")
+
+
+def test_relpos_fused_matches_unfused_with_dropout(dev, monkeypatch):
+    """Same seeds -> the fused kernel reproduces the unfused path's attention probabilities and
+    dropout masks (mask index row*T + j) and therefore the same block output."""
+    from espnet_slurp_amd import kernels as K
+    torch.manual_seed(4)
+    B, T, D, H = 2, 100, 256, 4
+    klen = torch.tensor([100, 61]).int().to(dev)
+    mod = RelPositionMultiHeadedAttention(H, D, 0.1, False).to(dev)
+    mod.flat = FlatParams(mod, dev)
+    x = torch.randn(B * T, D, device=dev)
+    res = torch.randn(B * T, D, device=dev)
+    pos = pos_table("latest", T, D, dev)
+    out_f, c_f = mod.fwd(x, res, pos, klen, B, T, 0.0, Seeds(7), True)
+    monkeypatch.setattr(K, "relpos_fused_ok", lambda T, dk: False)
+    out_u, c_u = mod.fwd(x, res, pos, klen, B, T, 0.0, Seeds(7), True)
+    assert float((c_f.attn - c_u.attn).abs().max()) < 1e-6
+    assert bool(((c_f.pv == 0) == (c_u.pv == 0)).all())
+    assert float((out_f - out_u).abs().max()) < 1e-4
+
+
 def test_conv_module_block(dev):
     torch.manual_seed(1)
     B, T, D = 3, 29, 64
