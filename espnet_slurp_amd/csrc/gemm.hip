@@ -782,12 +782,17 @@ __device__ __forceinline__ TileCoord tile_coord(const GemmArgs& g, const GldsArg
   return c;
 }
 
+// resident blocks per CU: 128x64 tiles (48 KB LDS) fit three, 128x128 tiles (64 KB) two; the
+// fused epilogues need the registers of two
+template <int BNT, int EPI>
+constexpr int glds_occupancy() { return (BNT == 64 && EPI == 0) ? 3 : 2; }
+
 // Persistent: block b processes tiles b, b+G, b+2G, ... as ONE continuous slab pipeline — the
 // first slab of the next tile streams in during the last slab of the current one, and the
 // current tile's epilogue stores drain while the next tile's MFMAs run (on this and the other
-// resident block's waves).  With G = #tiles every block runs one tile (the classic launch).
+// resident blocks' waves).  With G = #tiles every block runs one tile (the classic launch).
 template <int MA, int MB, int BNT, bool RS, int EPI>
-__global__ __launch_bounds__(NT, 2) void gemm_glds_kernel(GemmArgs g, GldsArgs x) {
+__global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_kernel(GemmArgs g, GldsArgs x) {
   constexpr int WN = BNT / 64, WM = 4 / WN, TM = BM / (WM * 32), TN = 2;
   constexpr int A_SZ = BM * GL_BK, B_SZ = BNT * GL_BK, BUF = A_SZ + B_SZ;
   constexpr int NIA = A_SZ / 4 / NT, NIB = B_SZ / 4 / NT;
@@ -1045,15 +1050,15 @@ __global__ void rowsum_rc_kernel(const float* __restrict__ p, long ld, int M, in
 // resident blocks of the persistent LDS-DMA kernel: 2 per CU (64 KB LDS each);
 // ESP_GEMM_PERSIST=0 launches one block per tile instead
 long g_persist = -1;
-long persist_blocks() {
+long persist_blocks(int per_cu) {
   if (g_persist < 0) {
     const char* e = getenv("ESP_GEMM_PERSIST");
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess)
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-    g_persist = (e && atoi(e) == 0) ? (1L << 40) : 2L * cus;
+    g_persist = (e && atoi(e) == 0) ? 0 : cus;
   }
-  return g_persist;
+  return g_persist ? (long)per_cu * g_persist : (1L << 40);
 }
 
 int g_variant = -1;
@@ -1094,16 +1099,20 @@ bool launch_glds(const GemmArgs& g, int batch, hipStream_t st) {
     if (abl < 0) abl = getenv("ESP_GEMM_ABL") ? atoi(getenv("ESP_GEMM_ABL")) : 0;
     x.abl = abl;
   }
-  const dim3 grid((unsigned)std::min<long>(x.ntiles, persist_blocks()));
+  auto grid = [&](int per_cu) { return dim3((unsigned)std::min<long>(x.ntiles, persist_blocks(per_cu))); };
   if (can_rs && g.rowsum)
-    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, can_rs, EPI_PLAIN>), grid, dim3(NT), 0, st, g, x);
+    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, can_rs, EPI_PLAIN>), grid(glds_occupancy<BNT, EPI_PLAIN>()),
+                       dim3(NT), 0, st, g, x);
   else if (kind == EPI_PLAIN)
-    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_PLAIN>), grid, dim3(NT), 0, st, g, x);
+    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_PLAIN>), grid(glds_occupancy<BNT, EPI_PLAIN>()),
+                       dim3(NT), 0, st, g, x);
   else if constexpr (can_fwd) {
     if (kind == EPI_FWD)
-      hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_FWD>), grid, dim3(NT), 0, st, g, x);
+      hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_FWD>), grid(glds_occupancy<BNT, EPI_FWD>()),
+                         dim3(NT), 0, st, g, x);
     else if constexpr (can_bwd)
-      hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_BWD>), grid, dim3(NT), 0, st, g, x);
+      hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_BWD>), grid(glds_occupancy<BNT, EPI_BWD>()),
+                         dim3(NT), 0, st, g, x);
   }
   return true;
 }
@@ -1217,8 +1226,15 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
   auto ntiles = [&](int bn) { return (long)((N + bn - 1) / bn) * ((M + BM - 1) / BM) * batch; };
   g.bnt = 0;
   if (variant() == 4 && g.a.glds && g.b.glds && K > 0) {
-    g.bnt = N <= 64 ? 64 : 128;
-    if (g.bnt == 128 && ntiles(128) < target && ntiles(64) >= target) g.bnt = 64;
+    // per-CU time model: ceil(tiles / CUs) tiles of bn/64 units each, x1.3 when the grid
+    // leaves CUs with a single resident block (one wave per SIMD); ties keep 128 (intensity)
+    auto cost = [&](int bn) {
+      const long t = ntiles(bn);
+      double c = (double)((t + 255) / 256) * (bn / 64);
+      if (t < 2 * 256) c *= 1.3;
+      return c;
+    };
+    g.bnt = (N <= 64 || cost(64) < cost(128)) ? 64 : 128;
   }
   {
     const long tiles = ntiles(g.bnt ? g.bnt : BN);
