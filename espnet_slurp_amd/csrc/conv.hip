@@ -13,18 +13,29 @@ inline int gridn(long n) {
   return (int)(b > 65536 ? 65536 : (b < 1 ? 1 : b));
 }
 
-// x (B,T,F) -> z (B,T1,F1,D), 4 channels per thread
-__global__ void conv1_fwd_kernel(const float* __restrict__ x, const float* __restrict__ W, const float* __restrict__ bias,
-                                 float* __restrict__ z, int B, int T, int F, int T1, int F1, int D) {
+// x (B,T,F) -> z (B,T1,F1,D).  A thread owns 4 output channels (weights + bias in registers,
+// loaded once) and strides over pixels; a wave covers 64 channel quads of one pixel, so the
+// 9-tap patch load is a broadcast and the store is 1 KB contiguous per wave.
+__global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict__ x, const float* __restrict__ W,
+                                                        const float* __restrict__ bias, float* __restrict__ z, int B,
+                                                        int T, int F, int T1, int F1, int D) {
   const int D4 = D / 4;
-  const long n = (long)B * T1 * F1 * D4;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const int o4 = (int)(i % D4);
-    long p = i / D4;
+  const long tid = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  const long nthr = (long)gridDim.x * blockDim.x;  // multiple of D4 (host)
+  const int o4 = (int)(tid % D4);
+  float w[4][9], bb[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    bb[q] = bias[o4 * 4 + q];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) w[q][k] = W[(o4 * 4 + q) * 9 + k];
+  }
+  const long npix = (long)B * T1 * F1;
+  for (long p = tid / D4; p < npix; p += nthr / D4) {
     const int f1 = (int)(p % F1);
-    p /= F1;
-    const int t1 = (int)(p % T1);
-    const int b = (int)(p / T1);
+    const long r = p / F1;
+    const int t1 = (int)(r % T1);
+    const int b = (int)(r / T1);
     const float* xp = x + ((long)b * T + 2 * t1) * F + 2 * f1;
     float patch[9];
 #pragma unroll
@@ -34,14 +45,12 @@ __global__ void conv1_fwd_kernel(const float* __restrict__ x, const float* __res
     float out[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int o = o4 * 4 + q;
-      float a = bias[o];
+      float a = bb[q];
 #pragma unroll
-      for (int k = 0; k < 9; ++k) a += W[o * 9 + k] * patch[k];
+      for (int k = 0; k < 9; ++k) a += w[q][k] * patch[k];
       out[q] = fmaxf(a, 0.f);
     }
-    *reinterpret_cast<float4*>(z + (((long)b * T1 + t1) * F1 + f1) * D + o4 * 4) =
-        make_float4(out[0], out[1], out[2], out[3]);
+    *reinterpret_cast<float4*>(z + p * D + o4 * 4) = make_float4(out[0], out[1], out[2], out[3]);
   }
 }
 
@@ -85,59 +94,79 @@ __global__ void col2im_relu_kernel(const float* __restrict__ dcol, const float* 
   }
 }
 
-// conv1 weight/bias gradient partials: block = chunk of pixels, thread = channel.
+// conv1 weight/bias gradient partials: block = chunk of pixels, thread = channel; the 9-tap
+// patches of a sub-chunk are staged in LDS (3 x float4 per pixel, broadcast reads), the dz rows
+// are read 4 pixels ahead.  Partials are stored output-major part[(o*10+k)*nb + block] so the
+// finalize pass reads each output's partials contiguously.
 constexpr int C1_CHUNK = 2048, C1_SUB = 256;
-__global__ void conv1_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dz, float* __restrict__ part,
-                                   int B, int T, int F, int T1, int F1, int D) {
-  __shared__ float patch[C1_SUB][9];
+__global__ __launch_bounds__(1024) void conv1_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dz,
+                                                          float* __restrict__ part, int B, int T, int F, int T1, int F1,
+                                                          int D, int nb) {
+  __shared__ float4 patch[C1_SUB][3];
   const long npix = (long)B * T1 * F1;
   const long p0 = (long)blockIdx.x * C1_CHUNK;
+  const int o = threadIdx.x;  // blockDim == D rounded up to a wave
+  const bool own = o < D;
   float acc[10];
 #pragma unroll
   for (int k = 0; k < 10; ++k) acc[k] = 0.f;
   for (long s0 = p0; s0 < p0 + C1_CHUNK && s0 < npix; s0 += C1_SUB) {
     __syncthreads();
-    for (int e = threadIdx.x; e < C1_SUB * 9; e += blockDim.x) {
-      const int q = e / 9, k = e - q * 9;
+    for (int e = threadIdx.x; e < C1_SUB * 12; e += blockDim.x) {
+      const int q = e / 12, k = e - q * 12;
       const long p = s0 + q;
       float v = 0.f;
-      if (p < npix) {
+      if (p < npix && k < 9) {
         const int f1 = (int)(p % F1);
         const long r = p / F1;
         const int t1 = (int)(r % T1);
         const int b = (int)(r / T1);
         v = x[((long)b * T + 2 * t1 + k / 3) * F + 2 * f1 + k % 3];
       }
-      patch[q][k] = v;
+      reinterpret_cast<float*>(&patch[q][0])[k] = v;
     }
     __syncthreads();
-    const int lim = (int)min((long)C1_SUB, npix - s0);
-    for (int o = threadIdx.x; o < D; o += blockDim.x) {
-      // one channel per thread (blockDim == D in practice)
-      for (int q = 0; q < lim; ++q) {
-        const float g = dz[(s0 + q) * D + o];
+    const int lim = own ? (int)min((long)C1_SUB, npix - s0) : 0;
+    const float* dzp = dz + s0 * D + o;
+    int q = 0;
+    for (; q + 4 <= lim; q += 4) {
+      float g[4];
 #pragma unroll
-        for (int k = 0; k < 9; ++k) acc[k] += g * patch[q][k];
-        acc[9] += g;
+      for (int u = 0; u < 4; ++u) g[u] = dzp[(long)(q + u) * D];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 a = patch[q + u][0], bq = patch[q + u][1], c = patch[q + u][2];
+        acc[0] += g[u] * a.x; acc[1] += g[u] * a.y; acc[2] += g[u] * a.z; acc[3] += g[u] * a.w;
+        acc[4] += g[u] * bq.x; acc[5] += g[u] * bq.y; acc[6] += g[u] * bq.z; acc[7] += g[u] * bq.w;
+        acc[8] += g[u] * c.x; acc[9] += g[u];
       }
     }
+    for (; q < lim; ++q) {
+      const float gg = dzp[(long)q * D];
+      const float4 a = patch[q][0], bq = patch[q][1], c = patch[q][2];
+      acc[0] += gg * a.x; acc[1] += gg * a.y; acc[2] += gg * a.z; acc[3] += gg * a.w;
+      acc[4] += gg * bq.x; acc[5] += gg * bq.y; acc[6] += gg * bq.z; acc[7] += gg * bq.w;
+      acc[8] += gg * c.x; acc[9] += gg;
+    }
   }
-  for (int o = threadIdx.x; o < D; o += blockDim.x) {
-    float* pr = part + ((long)blockIdx.x * D + o) * 10;
+  if (own)
 #pragma unroll
-    for (int k = 0; k < 10; ++k) pr[k] = acc[k];
-  }
+    for (int k = 0; k < 10; ++k) part[((long)o * 10 + k) * nb + blockIdx.x] = acc[k];
 }
 
-__global__ void conv1_wgrad_finalize(const float* __restrict__ part, int nb, int D, float* __restrict__ dW,
-                                     float* __restrict__ db) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= D * 10) return;
+// one block per (o, k) output: fixed-order strided sum + LDS tree (deterministic)
+__global__ __launch_bounds__(256) void conv1_wgrad_finalize(const float* __restrict__ part, int nb, int D,
+                                                            float* __restrict__ dW, float* __restrict__ db) {
+  __shared__ float sh[16];
+  const int e = blockIdx.x;
   float s = 0.f;
-  for (int p = 0; p < nb; ++p) s += part[(long)p * D * 10 + e];
-  const int o = e / 10, k = e - o * 10;
-  if (k < 9) dW[o * 9 + k] += s;
-  else db[o] += s;
+  for (int p = threadIdx.x; p < nb; p += blockDim.x) s += part[(long)e * nb + p];
+  s = esp::block_sum(s, sh);
+  if (threadIdx.x == 0) {
+    const int o = e / 10, k = e - o * 10;
+    if (k < 9) dW[o * 9 + k] += s;
+    else db[o] += s;
+  }
 }
 
 // out[o][a][b] (+)= in[o][b][a], in = (O, Bd, Ad)
@@ -160,8 +189,12 @@ ESP_API int esp_conv1_fwd(const float* x, const float* W, const float* bias, flo
                           void* stream) {
   ESP_ARG_CHECK(D % 4 == 0, "esp_conv1_fwd: D %% 4 != 0");
   const int T1 = (T - 3) / 2 + 1, F1 = (F - 3) / 2 + 1;
-  hipLaunchKernelGGL(conv1_fwd_kernel, dim3(gridn((long)B * T1 * F1 * (D / 4))), dim3(256), 0, (hipStream_t)stream, x,
-                     W, bias, z, B, T, F, T1, F1, D);
+  ESP_ARG_CHECK(256 % (D / 4) == 0, "esp_conv1_fwd: D/4 must divide 256");
+  const long npix = (long)B * T1 * F1;
+  long nblk = (npix * (D / 4) + 255) / 256;
+  if (nblk > 8192) nblk = 8192;  // ~16 pixels per thread at the C2 sizes: weights amortised
+  hipLaunchKernelGGL(conv1_fwd_kernel, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, x, W, bias, z, B, T,
+                     F, T1, F1, D);
   ESP_CHECK_LAUNCH("esp_conv1_fwd");
   return 0;
 }
@@ -183,8 +216,8 @@ ESP_API int esp_conv1_wgrad(const float* x, const float* dz1, float* dW, float* 
   const int nb = (int)((npix + C1_CHUNK - 1) / C1_CHUNK);
   hipStream_t st = (hipStream_t)stream;
   ESP_ARG_CHECK(D <= 1024, "esp_conv1_wgrad: D > 1024");
-  hipLaunchKernelGGL(conv1_wgrad_kernel, dim3(nb), dim3(D), 0, st, x, dz1, work, B, T, F, T1, F1, D);
-  hipLaunchKernelGGL(conv1_wgrad_finalize, dim3((D * 10 + 255) / 256), dim3(256), 0, st, work, nb, D, dW, db);
+  hipLaunchKernelGGL(conv1_wgrad_kernel, dim3(nb), dim3((D + 63) / 64 * 64), 0, st, x, dz1, work, B, T, F, T1, F1, D, nb);
+  hipLaunchKernelGGL(conv1_wgrad_finalize, dim3(D * 10), dim3(256), 0, st, work, nb, D, dW, db);
   ESP_CHECK_LAUNCH("esp_conv1_wgrad");
   return 0;
 }
