@@ -184,16 +184,17 @@ class RelPositionMultiHeadedAttention(nn.Module):
         K.heads_split(qkv, 3 * D, 0, B, T, H, dk, self.pos_bias_v, q_v)
         Tp, Pp = K.pitch(T), K.pitch(P)  # 16-B aligned score rows
         ac = empty(Z * T * Tp, like=x2d)
-        # ac[z] = q_u[z] k[b,h]^T
-        K.gemm(T, T, dk, q_u, qkv, ac, mode_a=K.KC, lda=dk, mode_b=K.KC, ldb=3 * D, ldc=Tp, b_off=D,
-               batch=Z, nb2=B, sa=(B * T * dk, T * dk), sb=(dk, T * 3 * D), sc=(B * T * Tp, T * Tp))
         pa = self.p if training else 0.0
         sa = seeds.next()
         pdrop = empty(Z * T * Tp, like=x2d) if pa > 0 else None
         if not self.legacy and K.relpos_fused_ok(T, dk):
-            # bd band on the MFMA inside the softmax kernel: no (Z, T, 2T-1) bd tensor
-            K.relpos_softmax_fwd(q_v, p, D, B, H, ac, math.sqrt(dk), klen, ac, pdrop, pa, sa, T, Tp)
+            # ac and the bd band on the MFMA inside the softmax kernel: only attn reaches HBM
+            K.relpos_attn_fwd(q_u, q_v, qkv, 3 * D, p, D, B, H, math.sqrt(dk), klen, ac, pdrop, pa, sa, T, Tp,
+                              k_off=D)
         else:
+            # ac[z] = q_u[z] k[b,h]^T
+            K.gemm(T, T, dk, q_u, qkv, ac, mode_a=K.KC, lda=dk, mode_b=K.KC, ldb=3 * D, ldc=Tp, b_off=D,
+                   batch=Z, nb2=B, sa=(B * T * dk, T * dk), sb=(dk, T * 3 * D), sc=(B * T * Tp, T * Tp))
             bd = empty(Z * T * Pp, like=x2d)
             K.gemm(T, P, dk, q_v, p, bd, mode_a=K.KC, lda=dk, mode_b=K.KC, ldb=D, ldc=Pp,
                    batch=Z, nb2=B, sa=(B * T * dk, T * dk), sb=(dk, 0), sc=(B * T * Pp, T * Pp))

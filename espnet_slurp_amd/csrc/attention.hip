@@ -10,6 +10,8 @@
 //   * softmax backward (+ attention-dropout backward) and the rel_shift adjoint (a
 //     gather, so no atomics: each bd element receives at most one score gradient).
 // One wave per score row; rows of <= 64*PER keys live in registers.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace {
@@ -260,6 +262,163 @@ __global__ __launch_bounds__(256) void relpos_softmax_fwd_kernel(
   }
 }
 
+// ---------------------------------------------------------------- fused latest rel-pos attention scores
+// The whole score path of one (32 query rows, z) block in one kernel — no (Z,T,T) ac and no
+// (Z,T,2T-1) bd tensor in HBM:
+//   1. bd band window  Sbd[r][c] = q_v[i0+r] . p[kmin+c]     (MFMA, LDS)          as above
+//   2. ac tiles        ac[r][j]  = q_u[i0+r] . k[j]          (MFMA, registers; wave w owns
+//                                                            key tiles w, w+4, ...)
+//   3. s = (ac + Sbd[r][j-r+31]) / sqrt(dk), key mask, row max / sum by xor-shuffles inside the
+//      32-lane halves + a 4-wave LDS exchange, p = e/sum -> attn (+ dropout copy pdrop).
+// k rows are read from the fused qkv projection: k[z][j] = kmat[(b*T + j)*ldk + 64*head].
+template <int NTA>  // key tiles per wave: ceil(ceil(T/32)/4) <= 4
+__global__ __launch_bounds__(256) void relpos_attn_fwd_kernel(
+    const float* __restrict__ qu, const float* __restrict__ qv, const float* __restrict__ kmat, long ldk,
+    const float* __restrict__ pm, long ldpm, int nb, float sqrt_dk, const int* __restrict__ klen,
+    float* __restrict__ attn, float* __restrict__ pdrop, uint32_t thr, float dscale, uint64_t seed, int T, long lds,
+    int WP, const uint64_t* __restrict__ key) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sbd = smem;                  // [32][WP]
+  float* rmax = smem + RP_ROWS * WP;  // [4 waves][32 rows]
+  float* rsum = rmax + 4 * RP_ROWS;
+  seed = esp::keyed(seed, key);
+  const int z = blockIdx.y;
+  const int i0 = blockIdx.x * RP_ROWS;
+  const int head = z / nb, b = z - head * nb;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int hf = lane >> 5, l32 = lane & 31;
+  const int P = 2 * T - 1;
+  const int kmin = T - RP_ROWS - i0;
+  const int nbd = (T + RP_ROWS - 1 + 31) / 32;
+  const int nac = (T + 31) / 32;
+
+  auto load_row32 = [&](const float* row, float (&f)[2][16]) {  // d = 32c + 16hf + s
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 v = *reinterpret_cast<const float4*>(row + 32 * c + 16 * hf + 4 * u);
+        f[c][4 * u] = v.x; f[c][4 * u + 1] = v.y; f[c][4 * u + 2] = v.z; f[c][4 * u + 3] = v.w;
+      }
+  };
+  auto mfma_tile = [&](const float (&a)[2][16], const float (&bb)[2][16]) {
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int st = 0; st < 16; ++st) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[c][st], bb[c][st], acc, 0, 0, 0);
+    return acc;
+  };
+
+  // Every B fragment of a phase is requested before its first MFMA (one exposed latency per
+  // phase, not per tile); phase 2's key rows are requested as phase 1's tiles retire.
+  float aq[2][16], au[2][16], bq[4][2][16];
+  auto p_row = [&](int ct) { return pm + (long)min(max(kmin + ct * 32 + l32, 0), P - 1) * ldpm + head * RP_DK; };
+  auto k_row = [&](int ct) { return kmat + ((long)b * T + min(ct * 32 + l32, T - 1)) * ldk + head * RP_DK; };
+  // 1. bd band window -> LDS  (nbd <= 15: at most 4 tiles per wave)
+  load_row32(qv + ((long)z * T + min(i0 + l32, T - 1)) * RP_DK, aq);
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+    if (wave + 4 * t < nbd) load_row32(p_row(wave + 4 * t), bq[t]);
+  load_row32(qu + ((long)z * T + min(i0 + l32, T - 1)) * RP_DK, au);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int ct = wave + 4 * t;
+    if (ct < nbd) {
+      const f32x16 acc = mfma_tile(aq, bq[t]);
+      if (t < NTA && ct < nac) load_row32(k_row(ct), bq[t]);  // phase-2 key rows of the same slot
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sbd[((r & 3) + 8 * (r >> 2) + 4 * hf) * WP + ct * 32 + l32] = acc[r];
+    } else if (t < NTA && ct < nac) {
+      load_row32(k_row(ct), bq[t]);
+    }
+  }
+  int kl = klen ? klen[b] : T;
+  if (kl > T) kl = T;
+  __syncthreads();
+
+  // 2. ac tiles + score assembly in registers
+  f32x16 sc[NTA];
+#pragma unroll
+  for (int t = 0; t < NTA; ++t) {
+    const int ct = wave + 4 * t;
+    const int j = ct * 32 + l32;
+    if (ct < nac) {
+      const f32x16 acc = mfma_tile(au, bq[t]);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int il = (r & 3) + 8 * (r >> 2) + 4 * hf;
+        sc[t][r] = (j < kl) ? (acc[r] + sbd[il * WP + j - il + RP_ROWS - 1]) / sqrt_dk : -INFINITY;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sc[t][r] = -INFINITY;
+    }
+  }
+  // 3. row max (rows of register r: il(r)); lanes of a half share rows, differ in key
+  float m[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float v = sc[0][r];
+#pragma unroll
+    for (int t = 1; t < NTA; ++t) v = fmaxf(v, sc[t][r]);
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    m[r] = v;
+  }
+  if (l32 == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rmax[wave * RP_ROWS + (r & 3) + 8 * (r >> 2) + 4 * hf] = m[r];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int il = (r & 3) + 8 * (r >> 2) + 4 * hf;
+    m[r] = fmaxf(fmaxf(rmax[il], rmax[RP_ROWS + il]), fmaxf(rmax[2 * RP_ROWS + il], rmax[3 * RP_ROWS + il]));
+  }
+  float sm[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float v = 0.f;
+#pragma unroll
+    for (int t = 0; t < NTA; ++t) {
+      const float e = sc[t][r] == -INFINITY ? 0.f : expf(sc[t][r] - m[r]);
+      sc[t][r] = e;
+      v += e;
+    }
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);
+    sm[r] = v;
+  }
+  if (l32 == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rsum[wave * RP_ROWS + (r & 3) + 8 * (r >> 2) + 4 * hf] = sm[r];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int il = (r & 3) + 8 * (r >> 2) + 4 * hf;
+    const float tot = (rsum[il] + rsum[RP_ROWS + il]) + (rsum[2 * RP_ROWS + il] + rsum[3 * RP_ROWS + il]);
+    sm[r] = tot > 0.f ? 1.0f / tot : 0.f;
+  }
+#pragma unroll
+  for (int t = 0; t < NTA; ++t) {
+    const int j = (wave + 4 * t) * 32 + l32;
+    if (j >= T) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = i0 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+      if (i >= T) continue;
+      const long row = (long)z * T + i;
+      const float pe = sc[t][r] * sm[r];
+      attn[row * lds + j] = pe;
+      if (pdrop) pdrop[row * lds + j] = esp::keep_elem(seed, (uint64_t)(row * T + j), thr) ? pe * dscale : 0.f;
+    }
+  }
+}
+
 inline int gridn(long n) {
   long b = (n + 255) / 256;
   return (int)(b > 65536 ? 65536 : (b < 1 ? 1 : b));
@@ -374,5 +533,37 @@ ESP_API int esp_relpos_softmax_fwd(const float* qv, const float* p, long ldp_row
   else ESP_RP(16);
 #undef ESP_RP
   ESP_CHECK_LAUNCH("esp_relpos_softmax_fwd");
+  return 0;
+}
+
+// Fully fused latest rel-pos attention probabilities: ac = q_u k^T and the bd band both on the
+// MFMA inside the kernel, softmax + dropout copy -> attn / pdrop (pitch lds).  q_u, q_v (Z,T,64)
+// head-major; k rows at kmat + (b*T + j)*ldk + 64*head; p as in esp_relpos_softmax_fwd.
+ESP_API int esp_relpos_attn_fwd(const float* qu, const float* qv, const float* kmat, long ldk, const float* p,
+                                long ldp_row, int nb, int H, float sqrt_dk, const int* klen, float* attn, float* pdrop,
+                                float drop_p, unsigned long long seed, int T, long lds, void* stream) {
+  ESP_ARG_CHECK(T >= 1 && lds >= T && nb >= 1 && H >= 1, "esp_relpos_attn_fwd: bad sizes T=%d", T);
+  ESP_ARG_CHECK(ldp_row % 4 == 0 && ldk % 4 == 0 && ((uintptr_t)p & 15) == 0 && ((uintptr_t)qv & 15) == 0 &&
+                    ((uintptr_t)qu & 15) == 0 && ((uintptr_t)kmat & 15) == 0,
+                "esp_relpos_attn_fwd: operands must be 16-B aligned with ld %% 4 == 0");
+  const uint32_t thr = drop_threshold(drop_p);
+  if (!thr) pdrop = nullptr;
+  const float ds = thr ? 1.f / (1.f - drop_p) : 1.f;
+  const int nbd = (T + RP_ROWS - 1 + 31) / 32;
+  const int WP = nbd * 32 + 4;
+  const size_t shm = ((size_t)RP_ROWS * WP + 8 * RP_ROWS) * sizeof(float);
+  ESP_ARG_CHECK(shm <= 65536, "esp_relpos_attn_fwd: T=%d needs %zu B of LDS (> 64 KB)", T, shm);
+  const int nta = ((T + 31) / 32 + 3) / 4;
+  dim3 grid((unsigned)((T + RP_ROWS - 1) / RP_ROWS), (unsigned)(nb * H));
+  hipStream_t st = (hipStream_t)stream;
+#define ESP_RA(N)                                                                                                    \
+  hipLaunchKernelGGL(relpos_attn_fwd_kernel<N>, grid, dim3(256), shm, st, qu, qv, kmat, ldk, p, ldp_row, nb, sqrt_dk, \
+                     klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, WP, esp::rng_key_ptr())
+  if (nta <= 1) ESP_RA(1);
+  else if (nta == 2) ESP_RA(2);
+  else if (nta == 3) ESP_RA(3);
+  else ESP_RA(4);
+#undef ESP_RA
+  ESP_CHECK_LAUNCH("esp_relpos_attn_fwd");
   return 0;
 }

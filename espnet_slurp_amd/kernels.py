@@ -330,9 +330,18 @@ def relpos_softmax_fwd(q_v, p, ldp_row, nb, H, ac, sqrt_dk, klen_i32, attn, pdro
                  _p(attn), _p(pdrop), float(drop_p), int(seed) & (2 ** 64 - 1), T, lds, _st())
 
 
+def relpos_attn_fwd(q_u, q_v, kmat, ldk, p, ldp_row, nb, H, sqrt_dk, klen_i32, attn, pdrop, drop_p, seed, T, lds,
+                    k_off=0):
+    """Fused latest rel-pos attention probabilities (ac and the bd band on the MFMA in-kernel)."""
+    _f32(q_u, q_v, kmat, p, attn, pdrop)
+    _native.call("esp_relpos_attn_fwd", _p(q_u), _p(q_v), _p(kmat, k_off), ldk, _p(p), ldp_row, nb, H,
+                 float(sqrt_dk), _p(klen_i32), _p(attn), _p(pdrop), float(drop_p), int(seed) & (2 ** 64 - 1), T, lds,
+                 _st())
+
+
 def relpos_fused_ok(T: int, dk: int) -> bool:
     """Whether esp_relpos_softmax_fwd covers this shape (d_k 64, 32-row window in 64 KB LDS)."""
-    return dk == 64 and 32 * (32 * ((T + 62) // 32) + 4) * 4 <= 65536
+    return dk == 64 and (32 * (32 * ((T + 62) // 32) + 4) + 256) * 4 <= 65536
 
 
 def attn_softmax_bwd(attn, dP, dS, drop_p, seed, sqrt_dk, rows, Tk, lds=None):

@@ -132,6 +132,15 @@ int esp_relshift_bwd(const float* dS, long lds, float* dbd, long ldp, int relpos
 int esp_relpos_softmax_fwd(const float* qv, const float* p, long ldp_row, int nb, int H, const float* ac,
                            float sqrt_dk, const int* klen, float* attn, float* pdrop, float drop_p,
                            unsigned long long seed, int T, long lds, void* stream);
+/* Fully fused latest rel-pos attention probabilities: ac = (q+u) k^T AND the bd band on the
+ * MFMA per 32-row block, softmax, dropout copy (attention.py:240-263, 64-96): no score
+ * tensor other than attn / pdrop reaches HBM.  q_u, q_v (Z,T,64) head-major z = h*nb + b;
+ * k row j of utterance b, head h at kmat + (b*T + j)*ldk + 64h (the fused qkv projection);
+ * p as above.  Same limits as esp_relpos_softmax_fwd. */
+int esp_relpos_attn_fwd(const float* qu, const float* qv, const float* kmat, long ldk, const float* p,
+                        long ldp_row, int nb, int H, float sqrt_dk, const int* klen, float* attn,
+                        float* pdrop, float drop_p, unsigned long long seed, int T, long lds,
+                        void* stream);
 
 /* ---- Conv2dSubsampling (subsampling.py:53-87), NHWC */
 int esp_conv1_fwd(const float* x, const float* W, const float* bias, float* z, int B, int T,
