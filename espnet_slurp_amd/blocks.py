@@ -231,9 +231,12 @@ class RelPositionMultiHeadedAttention(nn.Module):
         # dV = pv^T dctx -> dqkv[:, 2D:3D]
         K.gemm(T, dk, T, c.pv, dctx, dqkv, mode_a=K.RC, lda=Tp, mode_b=K.RC, ldb=D, ldc=3 * D, c_off=2 * D,
                batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * D), sc=(dk, T * 3 * D))
-        K.attn_softmax_bwd(c.attn, dS, dS, c.pa, c.sa, math.sqrt(dk), Z * T, T, lds=Tp)
         dbd = empty(Z * T * Pp, like=dout)
-        K.relshift_bwd(dS, dbd, relpos, Z, T, P, lds=Tp, ldp=Pp)
+        if not self.legacy:
+            K.attn_softmax_bwd_relpos(c.attn, dS, dS, dbd, Pp, c.pa, c.sa, math.sqrt(dk), Z * T, T, Tp)
+        else:
+            K.attn_softmax_bwd(c.attn, dS, dS, c.pa, c.sa, math.sqrt(dk), Z * T, T, lds=Tp)
+            K.relshift_bwd(dS, dbd, relpos, Z, T, P, lds=Tp, ldp=Pp)
         # dq_u = dS k -> dqkv[:, 0:D]
         K.gemm(T, dk, T, dS, c.qkv, dqkv, mode_a=K.KC, lda=Tp, mode_b=K.RC, ldb=3 * D, ldc=3 * D, b_off=D,
                batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * 3 * D), sc=(dk, T * 3 * D))

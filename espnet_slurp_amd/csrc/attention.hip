@@ -137,6 +137,54 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(const float* __restric
   }
 }
 
+// softmax backward fused with the latest rel_shift adjoint: the wave that owns score row
+// (z, i) writes dS[i][j] and the whole dbd row  dbd[i][k] = dS[i][k - (T-1-i)]  (0 outside the
+// band), so dS is not re-read by a separate relshift pass.  dS may alias dP.
+template <int PER>
+__global__ __launch_bounds__(256) void softmax_bwd_relpos_kernel(const float* __restrict__ attn, const float* dP,
+                                                                 float* dS, float* __restrict__ dbd, long ldp,
+                                                                 uint32_t thr, float dscale, uint64_t seed,
+                                                                 float sqrt_dk, long rows, int T, long lds,
+                                                                 const uint64_t* __restrict__ key) {
+  seed = esp::keyed(seed, key);
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int i = (int)(row % T);
+  const float* ar = attn + row * lds;
+  const float* gr = dP + row * lds;
+  float a[PER], g[PER];
+  float dot = 0.f;
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int j = lane + 64 * e;
+    a[e] = 0.f;
+    g[e] = 0.f;
+    if (j < T) {
+      a[e] = ar[j];
+      float gv = gr[j];
+      if (thr) gv = esp::keep_elem(seed, (uint64_t)(row * T + j), thr) ? gv * dscale : 0.f;
+      g[e] = gv;
+    }
+    dot += a[e] * g[e];
+  }
+  dot = esp::wave_sum(dot);
+  float* sr = dS + row * lds;
+  float* br = dbd + row * ldp;
+  const int sh = T - 1 - i;
+#pragma unroll
+  for (int e = 0; e < PER; ++e) {
+    const int j = lane + 64 * e;
+    if (j < T) {
+      const float v = a[e] * (g[e] - dot) / sqrt_dk;
+      sr[j] = v;
+      br[j + sh] = v;
+    }
+  }
+  for (int k = lane; k < sh; k += 64) br[k] = 0.f;
+  for (int k = sh + T + lane; k < 2 * T - 1; k += 64) br[k] = 0.f;
+}
+
 // adjoint of the rel_shift gather: dbd (Z,T,P) [pitch ldp] from dS (Z,T,T) [pitch lds]
 __global__ void relshift_bwd_kernel(const float* __restrict__ dS, long lds, float* __restrict__ dbd, long ldp,
                                     int relpos, int Z, int T, int P) {
@@ -565,5 +613,27 @@ ESP_API int esp_relpos_attn_fwd(const float* qu, const float* qv, const float* k
   else ESP_RA(4);
 #undef ESP_RA
   ESP_CHECK_LAUNCH("esp_relpos_attn_fwd");
+  return 0;
+}
+
+// softmax backward + latest rel_shift adjoint in one pass (see softmax_bwd_relpos_kernel)
+ESP_API int esp_attn_softmax_bwd_relpos(const float* attn, const float* dP, float* dS, float* dbd, long ldp,
+                                        float drop_p, unsigned long long seed, float sqrt_dk, long rows, int T,
+                                        long lds, void* stream) {
+  ESP_ARG_CHECK(T >= 1 && T <= 1024 && lds >= T && ldp >= 2 * T - 1, "esp_attn_softmax_bwd_relpos: bad sizes");
+  const uint32_t thr = drop_threshold(drop_p);
+  const float ds = thr ? 1.f / (1.f - drop_p) : 1.f;
+  dim3 grid((unsigned)((rows + 3) / 4));
+  hipStream_t st = (hipStream_t)stream;
+#define ESP_SBR(PER)                                                                                          \
+  hipLaunchKernelGGL(softmax_bwd_relpos_kernel<PER>, grid, dim3(256), 0, st, attn, dP, dS, dbd, ldp, thr, ds, \
+                     (uint64_t)seed, sqrt_dk, rows, T, lds, esp::rng_key_ptr())
+  if (T <= 64) ESP_SBR(1);
+  else if (T <= 128) ESP_SBR(2);
+  else if (T <= 256) ESP_SBR(4);
+  else if (T <= 512) ESP_SBR(8);
+  else ESP_SBR(16);
+#undef ESP_SBR
+  ESP_CHECK_LAUNCH("esp_attn_softmax_bwd_relpos");
   return 0;
 }

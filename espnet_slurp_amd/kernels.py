@@ -349,6 +349,12 @@ def attn_softmax_bwd(attn, dP, dS, drop_p, seed, sqrt_dk, rows, Tk, lds=None):
                  lds or Tk, _st())
 
 
+def attn_softmax_bwd_relpos(attn, dP, dS, dbd, ldp, drop_p, seed, sqrt_dk, rows, T, lds):
+    """Softmax backward fused with the latest rel_shift adjoint (writes dS and dbd)."""
+    _native.call("esp_attn_softmax_bwd_relpos", _p(attn), _p(dP), _p(dS), _p(dbd), ldp, float(drop_p), seed,
+                 float(sqrt_dk), rows, T, lds, _st())
+
+
 def relshift_bwd(dS, dbd, relpos, Z, T, P, lds=None, ldp=None):
     _native.call("esp_relshift_bwd", _p(dS), lds or T, _p(dbd), ldp or P, relpos, Z, T, P, _st())
 

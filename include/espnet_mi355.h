@@ -123,6 +123,11 @@ int esp_attn_softmax_bwd(const float* attn, const float* dP, float* dS, float dr
                          void* stream);
 int esp_relshift_bwd(const float* dS, long lds, float* dbd, long ldp, int relpos, int Z, int T, int P,
                      void* stream);
+/* esp_attn_softmax_bwd fused with the latest (relpos 1) esp_relshift_bwd: writes dS and the
+ * full dbd rows (P = 2T-1 columns, pitch ldp) in one pass. */
+int esp_attn_softmax_bwd_relpos(const float* attn, const float* dP, float* dS, float* dbd, long ldp,
+                                float drop_p, unsigned long long seed, float sqrt_dk, long rows,
+                                int T, long lds, void* stream);
 /* Fused latest rel-pos scores + softmax (attention.py:240-263 with the latest rel_shift,
  * embedding.py:173-244): bd_shift[i][j] = q_v[i] . p[j + T-1-i] is computed on the MFMA per
  * 32-row block inside the kernel (no (Z,T,2T-1) bd tensor), then s = (ac + bd_shift)/sqrt(dk),
