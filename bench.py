@@ -123,6 +123,32 @@ def cpu_baseline(args):
                       f"1 warmup + 3 timed steps, {t:.2f} s/step on {n} threads"}
 
 
+def gemm_algorithmic_bytes(shapes) -> float:
+    """Sum over the profiled GEMM launches of the bytes each must move at least once: A, B read,
+    C written (fp32).  An implicit-im2col operand counts its NHWC source map (~ 4/9 of the
+    virtual M x K matrix for the 3x3 / stride-2 convolution)."""
+    tot = 0.0
+    for (ma, mb, M, N, Kd, batch), (n, _ms, _f) in shapes.items():
+        a = M * Kd * (4 / 9 if ma >= 2 else 1.0)
+        b = N * Kd * (4 / 9 if mb >= 2 else 1.0)
+        tot += n * 4.0 * batch * (a + b + M * N)
+    return tot
+
+
+def measured_gemm_traffic() -> dict:
+    """HBM bytes per launch of the GEMM family from the newest committed PMC measurement
+    (profiles/*_gemm_traffic.json, written by tools/pmc_traffic.py from two rocprofv3 --pmc
+    passes of this bench); {} when none is present."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                          "*_gemm_traffic.json")))
+    if not files:
+        return {}
+    d = json.load(open(files[-1]))
+    d["source"] = os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))
+    return d
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -184,7 +210,7 @@ def main():
         K.profile_gemm_start()
         eager.train_one_step(batch)
         eager.resolve_pending()
-    gemm_flops, gemm_ms, gemm_launches = K.profile_gemm_stop()
+    gemm_flops, gemm_ms, gemm_launches, gemm_shapes = K.profile_gemm_stop(by_shape=True)
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
@@ -192,6 +218,7 @@ def main():
     elapsed = float(el.item())
 
     if rank == 0:
+        traffic = measured_gemm_traffic()
         fwd, train = conformer_flops_per_utt(args.d, args.heads, args.ff, args.layers, 2048, 6, args.vocab)
         value = world * args.batch * args.steps / elapsed
         achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
@@ -217,7 +244,10 @@ def main():
                                    "ctc 0.3, lsm 0.1, dropout 0.1, SpecAug on",
                        "global_batch": world * args.batch, "seq_len": 1500, "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                         "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                         "traffic": traffic.get("hbm_bytes_per_launch"),
+                         "traffic_source": traffic.get("source"),
+                         "algorithmic_bytes_per_launch": round(gemm_algorithmic_bytes(gemm_shapes) / max(1, gemm_launches)),
                          "kernel": "gemm_glds_kernel family (all MFMA GEMM launches of one step, HIP events"
                                    + (" in the timed region)" if args.eager else " on an eager replay of the step)"),
                          "launches": gemm_launches,

@@ -45,6 +45,13 @@ def main():
     print(f"{'ms/step':>9} {'%':>6} {'calls/step':>10} {'avg us':>9}  kernel")
     for k, (n, t) in sorted(tot.items(), key=lambda kv: -kv[1][1]):
         print(f"{t / steps / 1e6:9.3f} {100 * t / total:6.2f} {n / steps:10.1f} {t / n / 1e3:9.1f}  {k}")
+    # the bench's roofline kernel: every instantiation of the MFMA GEMM family together
+    fam = [(n, t) for k, (n, t) in tot.items() if k.startswith("gemm_glds_kernel")]
+    if fam:
+        n = sum(f[0] for f in fam)
+        t = sum(f[1] for f in fam)
+        print(f"# family gemm_glds_kernel<*>: {n / steps:.1f} launches/step, {t / steps / 1e6:.3f} ms/step, "
+              f"avg {t / n / 1e3:.1f} us per launch")
     if "--gemm" in sys.argv:
         g = collections.defaultdict(lambda: [0, 0])
         for name, dur, grid in rows:
