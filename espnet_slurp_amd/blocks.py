@@ -224,15 +224,23 @@ class RelPositionMultiHeadedAttention(nn.Module):
         dctx = self.linear_out.bwd(dz, c.ctx)
         dqkv = empty(M, 3 * D, like=dout)
         Tp, Pp = K.pitch(T), K.pitch(P)
-        # dP = dctx v^T  (into a (Z,T,T) buffer)
         dS = empty(Z * T * Tp, like=dout)
-        K.gemm(T, T, dk, dctx, c.qkv, dS, mode_a=K.KC, lda=D, mode_b=K.KC, ldb=3 * D, ldc=Tp, b_off=2 * D,
-               batch=Z, nb2=B, sa=(dk, T * D), sb=(dk, T * 3 * D), sc=(B * T * Tp, T * Tp))
+        dbd = empty(Z * T * Pp, like=dout)
+        # the fused dP + softmax/rel_shift adjoint kernel measures slower than the K=64 GEMM + the
+        # row-wise adjoint pass at C2 (198 vs 157 us per layer): opt-in until it is reworked
+        fused = not self.legacy and K.relpos_fused_ok(T, dk) and K.FUSED_ATTN_BWD
+        if fused:  # dP = dctx v^T on the MFMA inside the softmax / rel_shift adjoint kernel
+            K.relpos_attn_bwd(dctx, D, c.qkv, 3 * D, c.attn, dS, dbd, Pp, B, H, math.sqrt(dk), c.pa, c.sa, T, Tp,
+                              v_off=2 * D)
+        else:  # dP = dctx v^T  (into a (Z,T,T) buffer)
+            K.gemm(T, T, dk, dctx, c.qkv, dS, mode_a=K.KC, lda=D, mode_b=K.KC, ldb=3 * D, ldc=Tp, b_off=2 * D,
+                   batch=Z, nb2=B, sa=(dk, T * D), sb=(dk, T * 3 * D), sc=(B * T * Tp, T * Tp))
         # dV = pv^T dctx -> dqkv[:, 2D:3D]
         K.gemm(T, dk, T, c.pv, dctx, dqkv, mode_a=K.RC, lda=Tp, mode_b=K.RC, ldb=D, ldc=3 * D, c_off=2 * D,
                batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * D), sc=(dk, T * 3 * D))
-        dbd = empty(Z * T * Pp, like=dout)
-        if not self.legacy:
+        if fused:
+            pass
+        elif not self.legacy:
             K.attn_softmax_bwd_relpos(c.attn, dS, dS, dbd, Pp, c.pa, c.sa, math.sqrt(dk), Z * T, T, Tp)
         else:
             K.attn_softmax_bwd(c.attn, dS, dS, c.pa, c.sa, math.sqrt(dk), Z * T, T, lds=Tp)

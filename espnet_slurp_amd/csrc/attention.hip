@@ -16,6 +16,8 @@
 
 namespace {
 
+constexpr int RP_ROWS = 32, RP_DK = 64;  // fused rel-pos kernels: query rows per block, d_k
+
 __global__ void heads_split_kernel(const float* __restrict__ src, long ld, int col0, int B, int T, int H, int dk,
                                    const float* __restrict__ bias, float* __restrict__ dst) {
   const long n = (long)H * B * T * dk;
@@ -185,6 +187,112 @@ __global__ __launch_bounds__(256) void softmax_bwd_relpos_kernel(const float* __
   for (int k = sh + T + lane; k < 2 * T - 1; k += 64) br[k] = 0.f;
 }
 
+// Fused latest rel-pos attention backward, one block per (32 query rows, z):
+//   dP = dctx V^T on the MFMA (key tiles w, w+4, ... per wave; V rows from the fused qkv),
+//   g  = dropout'(dP) (mask regenerated), dot_i = sum_j attn*g (xor shuffles + LDS exchange),
+//   dS = attn*(g - dot)/sqrt(dk)  -> dS (pitch lds) and dbd[i][j + T-1-i] (pitch ldp, zero
+//   outside the band).  Replaces the dctx.V^T GEMM (K = 64) + the softmax/rel_shift adjoint.
+template <int NTA>
+__global__ __launch_bounds__(256) void relpos_attn_bwd_kernel(
+    const float* __restrict__ dctx, long ldd, const float* __restrict__ vmat, long ldv, const float* __restrict__ attn,
+    float* __restrict__ dS, float* __restrict__ dbd, long ldp, int nb, float sqrt_dk, uint32_t thr, float dscale,
+    uint64_t seed, int T, long lds, const uint64_t* __restrict__ key) {
+  __shared__ float rdot[4][RP_ROWS];
+  seed = esp::keyed(seed, key);
+  const int z = blockIdx.y;
+  const int i0 = blockIdx.x * RP_ROWS;
+  const int head = z / nb, b = z - head * nb;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int hf = lane >> 5, l32 = lane & 31;
+  const int nac = (T + 31) / 32;
+
+  auto load_row32 = [&](const float* row, float (&f)[2][16]) {  // d = 32c + 16hf + s
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 v = *reinterpret_cast<const float4*>(row + 32 * c + 16 * hf + 4 * u);
+        f[c][4 * u] = v.x; f[c][4 * u + 1] = v.y; f[c][4 * u + 2] = v.z; f[c][4 * u + 3] = v.w;
+      }
+  };
+  float ad[2][16], bq[NTA][2][16];
+  load_row32(dctx + ((long)b * T + min(i0 + l32, T - 1)) * ldd + head * RP_DK, ad);
+#pragma unroll
+  for (int t = 0; t < NTA; ++t)
+    if (wave + 4 * t < nac)
+      load_row32(vmat + ((long)b * T + min((wave + 4 * t) * 32 + l32, T - 1)) * ldv + head * RP_DK, bq[t]);
+
+  f32x16 g[NTA], a[NTA];
+  float dot[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) dot[r] = 0.f;
+#pragma unroll
+  for (int t = 0; t < NTA; ++t) {
+    const int j = (wave + 4 * t) * 32 + l32;
+    const bool jok = j < T && wave + 4 * t < nac;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {  // attn loads first: they fly during the MFMAs
+      const int i = min(i0 + (r & 3) + 8 * (r >> 2) + 4 * hf, T - 1);
+      a[t][r] = jok ? attn[((long)z * T + i) * lds + j] : 0.f;
+    }
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    if (wave + 4 * t < nac) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int st = 0; st < 16; ++st) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ad[c][st], bq[t][c][st], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const long row = (long)z * T + min(i0 + (r & 3) + 8 * (r >> 2) + 4 * hf, T - 1);
+      float gv = jok ? acc[r] : 0.f;
+      if (thr && jok) gv = esp::keep_elem(seed, (uint64_t)(row * T + j), thr) ? gv * dscale : 0.f;
+      g[t][r] = gv;
+      dot[r] += a[t][r] * gv;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) dot[r] += __shfl_xor(dot[r], o, 64);
+  }
+  if (l32 == 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rdot[wave][(r & 3) + 8 * (r >> 2) + 4 * hf] = dot[r];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int il = (r & 3) + 8 * (r >> 2) + 4 * hf;
+    dot[r] = (rdot[0][il] + rdot[1][il]) + (rdot[2][il] + rdot[3][il]);
+  }
+#pragma unroll
+  for (int t = 0; t < NTA; ++t) {
+    const int j = (wave + 4 * t) * 32 + l32;
+    if (j >= T || wave + 4 * t >= nac) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int i = i0 + (r & 3) + 8 * (r >> 2) + 4 * hf;
+      if (i >= T) continue;
+      const long row = (long)z * T + i;
+      const float v = a[t][r] * (g[t][r] - dot[r]) / sqrt_dk;
+      dS[row * lds + j] = v;
+      dbd[row * ldp + j + (T - 1 - i)] = v;
+    }
+  }
+  // zero the dbd entries outside each row's band (k < T-1-i and k > 2T-2-i)
+  for (int rr = wave; rr < RP_ROWS; rr += 4) {
+    const int i = i0 + rr;
+    if (i >= T) break;
+    float* br = dbd + ((long)z * T + i) * ldp;
+    const int sh = T - 1 - i;
+    for (int k = lane; k < sh; k += 64) br[k] = 0.f;
+    for (int k = sh + T + lane; k < 2 * T - 1; k += 64) br[k] = 0.f;
+  }
+}
+
 // adjoint of the rel_shift gather: dbd (Z,T,P) [pitch ldp] from dS (Z,T,T) [pitch lds]
 __global__ void relshift_bwd_kernel(const float* __restrict__ dS, long lds, float* __restrict__ dbd, long ldp,
                                     int relpos, int Z, int T, int P) {
@@ -215,7 +323,6 @@ __global__ void relshift_bwd_kernel(const float* __restrict__ dS, long lds, floa
 // softmax (wave shuffles), attention-dropout copy.  Replaces the (Z,T,2T-1) bd GEMM + its HBM
 // round trip + the separate softmax pass.  d_k = 64; LDS = 32 x WP floats (WP = 32*ceil((T+31)/32)+4).
 // MFMA operand k-order: lane half hf supplies d = 32c + 16hf + s at step (c, s) for both operands.
-constexpr int RP_ROWS = 32, RP_DK = 64;
 template <int PER>
 __global__ __launch_bounds__(256) void relpos_softmax_fwd_kernel(
     const float* __restrict__ qv, const float* __restrict__ pm, long ldpm, int nb, int H, const float* ac,
@@ -635,5 +742,31 @@ ESP_API int esp_attn_softmax_bwd_relpos(const float* attn, const float* dP, floa
   else ESP_SBR(16);
 #undef ESP_SBR
   ESP_CHECK_LAUNCH("esp_attn_softmax_bwd_relpos");
+  return 0;
+}
+
+// Fused latest rel-pos attention backward (see relpos_attn_bwd_kernel): dctx rows at
+// dctx + (b*T + i)*ldd + 64h, V rows at vmat + (b*T + j)*ldv + 64h; attn/dS pitch lds, dbd pitch ldp.
+ESP_API int esp_relpos_attn_bwd(const float* dctx, long ldd, const float* vmat, long ldv, const float* attn,
+                                float* dS, float* dbd, long ldp, int nb, int H, float sqrt_dk, float drop_p,
+                                unsigned long long seed, int T, long lds, void* stream) {
+  ESP_ARG_CHECK(T >= 1 && T <= 512 && lds >= T && ldp >= 2 * T - 1 && nb >= 1 && H >= 1,
+                "esp_relpos_attn_bwd: bad sizes T=%d", T);
+  ESP_ARG_CHECK(ldd % 4 == 0 && ldv % 4 == 0 && ((uintptr_t)dctx & 15) == 0 && ((uintptr_t)vmat & 15) == 0,
+                "esp_relpos_attn_bwd: dctx / v must be 16-B aligned with ld %% 4 == 0");
+  const uint32_t thr = drop_threshold(drop_p);
+  const float ds = thr ? 1.f / (1.f - drop_p) : 1.f;
+  const int nta = ((T + 31) / 32 + 3) / 4;
+  dim3 grid((unsigned)((T + RP_ROWS - 1) / RP_ROWS), (unsigned)(nb * H));
+  hipStream_t st = (hipStream_t)stream;
+#define ESP_RB(N)                                                                                                  \
+  hipLaunchKernelGGL(relpos_attn_bwd_kernel<N>, grid, dim3(256), 0, st, dctx, ldd, vmat, ldv, attn, dS, dbd, ldp, nb, \
+                     sqrt_dk, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr())
+  if (nta <= 1) ESP_RB(1);
+  else if (nta == 2) ESP_RB(2);
+  else if (nta == 3) ESP_RB(3);
+  else ESP_RB(4);
+#undef ESP_RB
+  ESP_CHECK_LAUNCH("esp_relpos_attn_bwd");
   return 0;
 }

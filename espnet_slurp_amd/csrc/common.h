@@ -17,14 +17,23 @@ namespace esp {
 void set_error(const char* fmt, ...);
 
 // ---------------------------------------------------------------- counter RNG
-// splitmix64-style mixer: (seed, index) -> 32 random bits.  Stateless, so the
+// Counter hash (seed, index) -> 32 random bits, 32-bit arithmetic only (4 v_mul_lo_u32 per
+// element instead of splitmix64's 64-bit multiplies: dropout masks are generated inside MFMA
+// epilogues and softmax passes, where the hash is the dominant VALU cost).  Two rounds of
+// Wellons' lowbias32 finaliser, the seed's halves injected before each.  Stateless, so the
 // backward pass regenerates the forward dropout mask from the same (seed, index).
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
 __device__ __forceinline__ uint32_t rng_u32(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (uint32_t)(z >> 32);
+  uint32_t x = (uint32_t)idx + 0x9E3779B9u * (uint32_t)(idx >> 32);
+  x = mix32(x ^ (uint32_t)seed);
+  return mix32(x + (uint32_t)(seed >> 32));
 }
 // Optional device-resident dropout key (esp_set_rng_key): every dropout kernel XORs its seed
 // with *key, so a captured HIP graph draws fresh masks on every replay (the key is advanced

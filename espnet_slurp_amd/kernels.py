@@ -6,6 +6,7 @@ is a HIP kernel of libespnet_mi355.so launched on torch's current HIP stream.
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional, Sequence
 
 import torch
@@ -353,6 +354,16 @@ def attn_softmax_bwd_relpos(attn, dP, dS, dbd, ldp, drop_p, seed, sqrt_dk, rows,
     """Softmax backward fused with the latest rel_shift adjoint (writes dS and dbd)."""
     _native.call("esp_attn_softmax_bwd_relpos", _p(attn), _p(dP), _p(dS), _p(dbd), ldp, float(drop_p), seed,
                  float(sqrt_dk), rows, T, lds, _st())
+
+
+FUSED_ATTN_BWD = os.environ.get("ESP_FUSED_ATTN_BWD", "0") == "1"
+
+
+def relpos_attn_bwd(dctx, ldd, vmat, ldv, attn, dS, dbd, ldp, nb, H, sqrt_dk, drop_p, seed, T, lds, v_off=0):
+    """Fused latest rel-pos attention backward: dP = dctx V^T (MFMA), dropout/softmax/rel_shift adjoints."""
+    _f32(dctx, vmat, attn, dS, dbd)
+    _native.call("esp_relpos_attn_bwd", _p(dctx), ldd, _p(vmat, v_off), ldv, _p(attn), _p(dS), _p(dbd), ldp, nb, H,
+                 float(sqrt_dk), float(drop_p), int(seed) & (2 ** 64 - 1), T, lds, _st())
 
 
 def relshift_bwd(dS, dbd, relpos, Z, T, P, lds=None, ldp=None):

@@ -128,6 +128,12 @@ int esp_relshift_bwd(const float* dS, long lds, float* dbd, long ldp, int relpos
 int esp_attn_softmax_bwd_relpos(const float* attn, const float* dP, float* dS, float* dbd, long ldp,
                                 float drop_p, unsigned long long seed, float sqrt_dk, long rows,
                                 int T, long lds, void* stream);
+/* Fused latest rel-pos attention backward: dP = dctx V^T on the MFMA per 32-row block, attention
+ * dropout adjoint, softmax adjoint, rel_shift adjoint -> dS (pitch lds) and dbd (pitch ldp).
+ * dctx rows at dctx + (b*T+i)*ldd + 64h, V rows at vmat + (b*T+j)*ldv + 64h; d_k = 64, T <= 512. */
+int esp_relpos_attn_bwd(const float* dctx, long ldd, const float* vmat, long ldv, const float* attn,
+                        float* dS, float* dbd, long ldp, int nb, int H, float sqrt_dk, float drop_p,
+                        unsigned long long seed, int T, long lds, void* stream);
 /* Fused latest rel-pos scores + softmax (attention.py:240-263 with the latest rel_shift,
  * embedding.py:173-244): bd_shift[i][j] = q_v[i] . p[j + T-1-i] is computed on the MFMA per
  * 32-row block inside the kernel (no (Z,T,2T-1) bd tensor), then s = (ac + bd_shift)/sqrt(dk),

@@ -63,11 +63,13 @@ def test_relpos_mha_block(dev, legacy):
     _check_grads(mod, P, "a")
 
 
+@pytest.mark.parametrize("fused_bwd", [False, True])
 @pytest.mark.parametrize("T,klens", [(29, [29, 23, 15]), (77, [77, 40, 9]), (130, [130, 129, 64])])
-def test_relpos_mha_fused_dk64(dev, T, klens):
+def test_relpos_mha_fused_dk64(dev, T, klens, fused_bwd, monkeypatch):
     """d_k = 64 latest rel-pos: the fused bd-window + softmax kernel (esp_relpos_softmax_fwd),
     several 32-row blocks incl. a partial last block, against the fp64 oracle."""
     from espnet_slurp_amd import kernels as K
+    monkeypatch.setattr(K, "FUSED_ATTN_BWD", fused_bwd)
     torch.manual_seed(3)
     B, D, H = 3, 256, 4
     assert K.relpos_fused_ok(T, D // H)
@@ -105,12 +107,21 @@ def test_relpos_fused_matches_unfused_with_dropout(dev, monkeypatch):
     x = torch.randn(B * T, D, device=dev)
     res = torch.randn(B * T, D, device=dev)
     pos = pos_table("latest", T, D, dev)
+    dout = torch.randn(B * T, D, device=dev)
+    monkeypatch.setattr(K, "FUSED_ATTN_BWD", True)
     out_f, c_f = mod.fwd(x, res, pos, klen, B, T, 0.0, Seeds(7), True)
+    dx_f = mod.bwd(c_f, dout)
+    g_f = mod.flat.grad.clone()
+    mod.flat.grad.zero_()
     monkeypatch.setattr(K, "relpos_fused_ok", lambda T, dk: False)
     out_u, c_u = mod.fwd(x, res, pos, klen, B, T, 0.0, Seeds(7), True)
+    dx_u = mod.bwd(c_u, dout)
     assert float((c_f.attn - c_u.attn).abs().max()) < 1e-6
     assert bool(((c_f.pv == 0) == (c_u.pv == 0)).all())
     assert float((out_f - out_u).abs().max()) < 1e-4
+    # backward: the fused dP / dropout / softmax / rel_shift adjoint kernel regenerates the same masks
+    assert rel_err(dx_f.cpu(), dx_u.cpu()) < 1e-5
+    assert rel_err(g_f.cpu(), mod.flat.grad.cpu()) < 1e-5
 
 
 def test_conv_module_block(dev):
