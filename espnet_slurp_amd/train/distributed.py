@@ -103,8 +103,19 @@ class FlatGradReducer:
             h.wait()
 
     def broadcast_buffers(self, model):
-        for b in model.buffers():
-            dist.broadcast(b, 0, group=self.group)
+        """DDP's broadcast_buffers (X7): rank 0's floating buffers (BatchNorm running stats) to
+        every replica before the forward, coalesced into ONE broadcast.  Training-mode outputs
+        do not read them, so this only keeps the replicas' eval-mode state equal to rank 0's."""
+        bufs = [b for b in model.buffers() if b.is_floating_point()]
+        if not bufs:
+            return
+        flat = torch.cat([b.detach().reshape(-1).float() for b in bufs])
+        dist.broadcast(flat, 0, group=self.group)
+        o = 0
+        for b in bufs:
+            n = b.numel()
+            b.copy_(flat[o:o + n].view_as(b))
+            o += n
 
 
 def fused_stats_allreduce(stats: Dict[str, torch.Tensor], weight: torch.Tensor, group=None):

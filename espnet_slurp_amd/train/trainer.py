@@ -70,7 +70,7 @@ class Trainer:
         self.iiter += 1
         model = self.model
         if self.distributed and self.reducer is not None:
-            pass
+            self.reducer.broadcast_buffers(model)
         loss, stats, weight = model(**batch)
         stats = {k: v for k, v in stats.items() if v is not None}
         if self.distributed:
@@ -109,6 +109,8 @@ class Trainer:
         sig = (tuple(speech.shape), prep.T, prep.Umax, prep.L,
                tuple((k, tuple(v.shape)) for k, v in sorted(prep.host.items())))
         e = self._graphs.get(sig)
+        if self.distributed:  # DDP broadcast_buffers (X7), outside the graph (a collective)
+            self.reducer.broadcast_buffers(model)
         if e is None:  # the capture call's eager warm-up IS this iteration's step
             e = self._capture(speech, prep)
             self._graphs[sig] = e
