@@ -56,6 +56,8 @@ SIGNATURES = {
     "esp_relpos_attn_fwd": [P, P, P, L, P, L, I, I, F, P, P, P, F, U64, I, L, P],
     "esp_attn_softmax_bwd_relpos": [P, P, P, P, L, F, U64, F, L, I, L, P],
     "esp_relpos_attn_bwd": [P, L, P, L, P, P, P, L, I, I, F, F, U64, I, L, P],
+    "esp_fbank_fwd": [P, L, P, I, I, I, I, P, P, P, P, P, I, P, I, P],
+    "esp_global_mvn": [P, P, I, I, I, P, P, I, I, P],
     "esp_conv1_fwd": [P, P, P, P, I, I, I, I, P],
     "esp_col2im_relu": [P, P, P, I, I, I, I, P],
     "esp_conv1_wgrad": [P, P, P, P, I, I, I, I, P, P],
@@ -68,7 +70,7 @@ SIGNATURES = {
     "esp_ctc_forced_align": [P, I, I, P, I, I, P, P, P],
 }
 _RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I}
-ABI_VERSION = 9  # bumped whenever a signature in include/espnet_mi355.h changes
+ABI_VERSION = 10  # bumped whenever a signature in include/espnet_mi355.h changes
 
 _lib = None
 

@@ -97,8 +97,10 @@ class ESPnetASRModel(AbsESPnetModel):
                  lang_token_id: int = -1):
         assert 0.0 <= ctc_weight <= 1.0, ctc_weight
         super().__init__()
-        if frontend is not None or preencoder is not None or postencoder is not None or joint_network is not None:
-            raise NotImplementedError("frontend/pre-/post-encoder/transducer are not on the fbank hot path")
+        if preencoder is not None or postencoder is not None or joint_network is not None:
+            raise NotImplementedError("pre-/post-encoder/transducer are not on the hot path")
+        if frontend is not None and not hasattr(frontend, "apply_prepared"):
+            raise NotImplementedError("frontend: only the native DefaultFrontend (frontend: default)")
         if interctc_weight != 0.0 or lang_token_id != -1:
             raise NotImplementedError("interctc / lang_token_id")
         self.blank_id = token_list.index(sym_blank)
@@ -196,15 +198,24 @@ class ESPnetASRModel(AbsESPnetModel):
         sl_cpu = speech_lengths.detach().cpu()
         tl_cpu = text_lengths.detach().cpu()
         text_cpu = text[:, : int(tl_cpu.max())].contiguous()
-        T = min(T_in, int(sl_cpu.max()))
-        host = {"lens": sl_cpu.to(torch.int32), "weight": torch.tensor([B], dtype=torch.long)}
+        host = {}
+        n_samples = 0
+        if self.frontend is not None:  # _extract_feats: speech[:, :max(len)] -> frames (host-side lengths)
+            n_samples = min(T_in, int(sl_cpu.max()))
+            host["wav_lens"] = sl_cpu.to(torch.int32)
+            T = self.frontend.num_frames(n_samples)
+            sl_cpu = self.frontend.output_lengths(sl_cpu)
+            F_in = self.frontend.output_size()
+        else:
+            T = min(T_in, int(sl_cpu.max()))
+        host.update({"lens": sl_cpu.to(torch.int32), "weight": torch.tensor([B], dtype=torch.long)})
         if self.specaug is not None and self.training:
             draws = specaug_draws if specaug_draws is not None else self.specaug.draw(B, T, F_in, sl_cpu.tolist())
             for k, v in draws.items():
                 host["sa_" + k] = v.to(torch.int32)
         host["hlens"] = self.encoder.output_lengths(sl_cpu, T).to(torch.int32)
         prep = Prepared(B=B, T=T, Umax=int(text_cpu.shape[1]), denom=float(B), L=0, host=host,
-                        enc_seed=draw_seed(), heads_seed=draw_seed(), sl_cpu=sl_cpu)
+                        enc_seed=draw_seed(), heads_seed=draw_seed(), sl_cpu=sl_cpu, n_samples=n_samples)
         if self.ctc is not None:
             host["ys"] = text_cpu
             host["tlens"] = tl_cpu.to(torch.int32)
@@ -221,7 +232,10 @@ class ESPnetASRModel(AbsESPnetModel):
         """The step's device work from a prepared batch: no host->device traffic and no host
         synchronisation, so the forward + backward can be captured as one HIP graph."""
         d = prep.dev
-        feats = speech[:, : prep.T].contiguous().float()
+        if self.frontend is not None:  # raw samples -> log-mel on device (one kernel)
+            feats = self.frontend.apply_prepared(speech, d["wav_lens"], prep.n_samples)
+        else:
+            feats = speech[:, : prep.T].contiguous().float()
         if self.specaug is not None and self.training:
             draws = {k[3:]: v for k, v in d.items() if k.startswith("sa_")}
             feats = self.specaug.apply_prepared(feats, d["lens"], draws)
@@ -251,7 +265,8 @@ class ESPnetASRModel(AbsESPnetModel):
             speech.shape, speech_lengths.shape, text.shape, text_lengths.shape)
         assert self.flat is not None, "call model.flatten() after moving the model to the GPU"
         text[text == -1] = self.ignore_id  # the reference mutates the batch (espnet_model.py:196)
-        prep = self.prepare(speech_lengths, text, text_lengths, speech.shape[1], speech.shape[2], specaug_draws)
+        F_in = speech.shape[2] if speech.dim() == 3 else 0
+        prep = self.prepare(speech_lengths, text, text_lengths, speech.shape[1], F_in, specaug_draws)
         prep.to_device(speech.device)
         return self.forward_prepared(speech, prep)
 
@@ -260,8 +275,11 @@ class ESPnetASRModel(AbsESPnetModel):
         """espnet_model.py:319-377 (frontend=None: feats = speech[:, :max_len])."""
         if sl_cpu is None:
             sl_cpu = speech_lengths.detach().cpu()
-        feats = speech[:, : int(sl_cpu.max())].contiguous().float()
-        feats_lengths = sl_cpu
+        if self.frontend is not None:
+            feats, feats_lengths = self.frontend(speech, sl_cpu)
+        else:
+            feats = speech[:, : int(sl_cpu.max())].contiguous().float()
+            feats_lengths = sl_cpu
         if self.specaug is not None and self.training:
             feats, _ = self.specaug(feats, feats_lengths, draws=specaug_draws)
         if self.normalize is not None:
@@ -269,4 +287,7 @@ class ESPnetASRModel(AbsESPnetModel):
         return self.encoder(feats, feats_lengths)[:2]
 
     def collect_feats(self, speech, speech_lengths, text, text_lengths, **kwargs) -> Dict[str, torch.Tensor]:
+        if self.frontend is not None and self.extract_feats_in_collect_stats:
+            feats, flens = self.frontend(speech, speech_lengths)
+            return {"feats": feats, "feats_lengths": flens}
         return {"feats": speech[:, : int(speech_lengths.max())], "feats_lengths": speech_lengths}

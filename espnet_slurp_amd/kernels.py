@@ -437,3 +437,19 @@ def ctc_forced_align(lpz, y, blank=0):
 
 def reserve_workspace(nbytes, device):
     WS.reserve(nbytes, device)
+
+
+# ----------------------------------------------------------------------------- front end
+def fbank_fwd(wave, lens_i32, B, N, n_fft, hop, window, twiddle, melw, mel_lo, mel_hi, n_mels, out, T):
+    """STFT -> power -> log-mel in one kernel (esp_fbank_fwd); wave (B, ldw) fp32 on device."""
+    _f32(wave, window, twiddle, melw, out)
+    _native.call("esp_fbank_fwd", _p(wave), wave.stride(0), _p(lens_i32), B, N, n_fft, hop, _p(window), _p(twiddle),
+                 _p(melw), _p(mel_lo), _p(mel_hi), n_mels, _p(out), T, _st())
+
+
+def global_mvn(x, lens_i32, mean, std, norm_means=True, norm_vars=True):
+    """In place: ((x - mean), padded frames zeroed) / std."""
+    _f32(x, mean, std)
+    B, T, F = x.shape
+    _native.call("esp_global_mvn", _p(x), _p(lens_i32), B, T, F, _p(mean), _p(std), int(norm_means),
+                 int(norm_vars), _st())

@@ -15,6 +15,8 @@ from ..asr.encoder.conformer_encoder import ConformerEncoder
 from ..asr.encoder.transformer_encoder import TransformerEncoder
 from ..asr.espnet_model import ESPnetASRModel
 from ..asr.specaug.specaug import SpecAug
+from ..asr.frontend.default import DefaultFrontend
+from ..layers.global_mvn import GlobalMVN
 from ..layers.utterance_mvn import UtteranceMVN
 
 
@@ -40,9 +42,10 @@ class ClassChoices:
         raise ValueError(f"--{self.name} must be one of {self.choices()}: --{self.name} {name.lower()}")
 
 
+frontend_choices = ClassChoices("frontend", dict(default=DefaultFrontend), default="default")
 specaug_choices = ClassChoices("specaug", dict(specaug=SpecAug), default=None, optional=True)
-normalize_choices = ClassChoices("normalize", dict(utterance_mvn=UtteranceMVN), default="utterance_mvn",
-                                 optional=True)
+normalize_choices = ClassChoices("normalize", dict(global_mvn=GlobalMVN, utterance_mvn=UtteranceMVN),
+                                 default="utterance_mvn", optional=True)
 model_choices = ClassChoices("model", dict(espnet=ESPnetASRModel), default="espnet")
 encoder_choices = ClassChoices("encoder", dict(conformer=ConformerEncoder, transformer=TransformerEncoder),
                                default="rnn")
@@ -56,7 +59,13 @@ def build_model(args: argparse.Namespace, device="cuda") -> ESPnetASRModel:
     decoder/_conf, ctc_conf, model_conf (the resolved config.yaml fields)."""
     token_list = list(args.token_list)
     vocab_size = len(token_list)
-    input_size = args.input_size
+    if getattr(args, "input_size", None) is None:  # extract features in the model (asr.py:459-468)
+        frontend = frontend_choices.get_class(getattr(args, "frontend", "default"))(
+            **(getattr(args, "frontend_conf", None) or {}))
+        input_size = frontend.output_size()
+    else:  # features from the data loader
+        frontend = None
+        input_size = args.input_size
     specaug_cls = specaug_choices.get_class(getattr(args, "specaug", None))
     specaug = specaug_cls(**(getattr(args, "specaug_conf", None) or {})) if specaug_cls else None
     norm_cls = normalize_choices.get_class(getattr(args, "normalize", "utterance_mvn"))
@@ -67,7 +76,7 @@ def build_model(args: argparse.Namespace, device="cuda") -> ESPnetASRModel:
                       **(getattr(args, "decoder_conf", None) or {})) if dec_cls else None
     ctc = CTC(odim=vocab_size, encoder_output_size=encoder.output_size(), **(getattr(args, "ctc_conf", None) or {}))
     model_cls = model_choices.get_class(getattr(args, "model", "espnet"))
-    model = model_cls(vocab_size=vocab_size, frontend=None, specaug=specaug, normalize=normalize, preencoder=None,
+    model = model_cls(vocab_size=vocab_size, frontend=frontend, specaug=specaug, normalize=normalize, preencoder=None,
                       encoder=encoder, postencoder=None, decoder=decoder, ctc=ctc, joint_network=None,
                       token_list=token_list, **(getattr(args, "model_conf", None) or {}))
     model = model.to(device)

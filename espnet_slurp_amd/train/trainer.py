@@ -105,8 +105,8 @@ class Trainer:
         self.iiter += 1
         self.resolve_pending()
         prep = model.prepare(batch["speech_lengths"], batch["text"], batch["text_lengths"], speech.shape[1],
-                             speech.shape[2])
-        sig = (tuple(speech.shape), prep.T, prep.Umax, prep.L,
+                             speech.shape[2] if speech.dim() == 3 else 0)
+        sig = (tuple(speech.shape), prep.T, prep.Umax, prep.L, prep.get("n_samples", 0),
                tuple((k, tuple(v.shape)) for k, v in sorted(prep.host.items())))
         e = self._graphs.get(sig)
         if self.distributed:  # DDP broadcast_buffers (X7), outside the graph (a collective)

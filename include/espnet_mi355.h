@@ -153,6 +153,21 @@ int esp_relpos_attn_fwd(const float* qu, const float* qv, const float* kmat, lon
                         float* pdrop, float drop_p, unsigned long long seed, int T, long lds,
                         void* stream);
 
+/* ---- feature front end: DefaultFrontend + GlobalMVN
+ * esp_fbank_fwd: STFT (center, reflect, window of length n_fft, onesided) -> power -> mel
+ * (dense (n_fft/2+1, n_mels) matrix, band [mel_lo[m], mel_hi[m]) nonzero) -> clamp 1e-10 ->
+ * log; frames t >= lens[b]/hop + 1 written as 0 (default.py:82-131, stft.py:63-160,
+ * log_mel.py:57-81).  wave (B, N) row pitch ldw; lens (device int32, samples); twiddle
+ * n_fft (cos, -sin) pairs of exp(-2 pi i j / n_fft); out (B, T, n_mels), T = N/hop + 1.
+ * n_fft even in [16, 2048]: radix-2 FFT when a power of two, direct DFT otherwise. */
+int esp_fbank_fwd(const float* wave, long ldw, const int* lens, int B, int N, int n_fft, int hop,
+                  const float* window, const float* twiddle, const float* melw, const int* mel_lo,
+                  const int* mel_hi, int n_mels, float* out, int T, void* stream);
+/* GlobalMVN in place: x (B,T,F) -> ((x - mean), frames t >= lens[b] zeroed) / std
+ * (global_mvn.py:67-90). */
+int esp_global_mvn(float* x, const int* lens, int B, int T, int F, const float* mean,
+                   const float* stdv, int norm_means, int norm_vars, void* stream);
+
 /* ---- Conv2dSubsampling (subsampling.py:53-87), NHWC */
 int esp_conv1_fwd(const float* x, const float* W, const float* bias, float* z, int B, int T,
                   int F, int D, void* stream);

@@ -295,8 +295,54 @@ def fullsize_fixture():
     np.savez_compressed(os.path.join(HERE, "fullsize_c2.npz"), **out)
 
 
+def frontend_fixture():
+    """Front end: the reference Stft, the LogMel forward (with the
+    oracle's restated mel matrix injected: librosa is absent) and GlobalMVN on seeded audio."""
+    import tempfile
+
+    from espnet2.layers.global_mvn import GlobalMVN
+    from espnet2.layers.log_mel import LogMel
+    from espnet2.layers.stft import Stft
+
+    from oracle import frontend_cpu as FE
+    g = torch.Generator().manual_seed(77)
+    lens = torch.tensor([3000, 2571, 1234])
+    x = torch.randn(3, 3000, generator=g) * 0.3
+    for b, n in enumerate(lens.tolist()):
+        x[b, n:] = 0.0
+    st = Stft(n_fft=512, hop_length=128)
+    spec, olens = st(x, lens)
+    ospec, oolens = FE.stft(x, lens, 512, 128)
+    assert torch.equal(olens, oolens) and torch.allclose(spec, ospec, rtol=0, atol=1e-5)
+    power = spec[..., 0] ** 2 + spec[..., 1] ** 2
+    melmat = torch.from_numpy(FE.mel_filters(16000, 512, 80, 0.0, 8000.0).T).float()
+    lm = LogMel.__new__(LogMel)
+    torch.nn.Module.__init__(lm)
+    lm.register_buffer("melmat", melmat)
+    lm.log_base = None
+    lm.mel_options = {}
+    feats, flens = lm(power, olens)
+    assert torch.allclose(feats, FE.log_mel(power, olens, melmat), rtol=0, atol=1e-5)
+    stats = {"count": np.float64(1234.0), "sum": np.random.RandomState(3).randn(80) * 50.0,
+             "sum_square": np.random.RandomState(4).rand(80) * 9e4 + 2e4}
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "feats_stats.npz")
+        np.savez(path, **stats)
+        gm = GlobalMVN(path)
+        normed, _ = gm(feats.clone(), flens)
+    mean, std = FE.global_mvn_stats(stats)
+    assert torch.allclose(normed, FE.global_mvn(feats, flens, mean, std), rtol=0, atol=1e-5)
+    np.savez_compressed(os.path.join(HERE, "frontend.npz"), x=x.numpy(), lens=lens.numpy(),
+                        spec=spec.numpy(), olens=olens.numpy(), melmat=melmat.numpy(), feats=feats.numpy(),
+                        stat_count=stats["count"], stat_sum=stats["sum"], stat_sum_square=stats["sum_square"],
+                        normed=normed.numpy())
+    print("frontend", tuple(spec.shape), tuple(feats.shape))
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["ctc", "align", "specaug", "small", "c1", "train", "full"]
+    which = sys.argv[1:] or ["ctc", "align", "specaug", "small", "c1", "train", "full", "frontend"]
+    if "frontend" in which:
+        frontend_fixture()
     if "ctc" in which:
         ctc_fixture()
     if "align" in which:

@@ -36,7 +36,7 @@ def c2_cfg(rel_pos_type="latest", blocks=12):
                       dec=O.DecCfg(attention_heads=4, linear_units=2048, num_blocks=6))
 
 
-def build_model(cfg: O.ModelCfg, device, specaug=None, dropout=None):
+def build_model(cfg: O.ModelCfg, device, specaug=None, dropout=None, frontend=None):
     from espnet_slurp_amd.asr.ctc import CTC
     from espnet_slurp_amd.asr.decoder.transformer_decoder import TransformerDecoder
     from espnet_slurp_amd.asr.encoder.conformer_encoder import ConformerEncoder
@@ -63,7 +63,7 @@ def build_model(cfg: O.ModelCfg, device, specaug=None, dropout=None):
                                  num_blocks=d.num_blocks, dropout_rate=p, positional_dropout_rate=p,
                                  self_attention_dropout_rate=p, src_attention_dropout_rate=p)
     ctc = CTC(odim=cfg.vocab_size, encoder_output_size=e.output_size)
-    m = ESPnetASRModel(vocab_size=cfg.vocab_size, token_list=token_list(cfg.vocab_size), frontend=None,
+    m = ESPnetASRModel(vocab_size=cfg.vocab_size, token_list=token_list(cfg.vocab_size), frontend=frontend,
                        specaug=specaug, normalize=UtteranceMVN(), preencoder=None, encoder=enc, postencoder=None,
                        decoder=dec, ctc=ctc, joint_network=None, ctc_weight=cfg.ctc_weight,
                        lsm_weight=cfg.lsm_weight, length_normalized_loss=cfg.length_normalized_loss,

@@ -293,3 +293,54 @@ def test_flat_grad_reducer_gloo_world2():
         p.join(timeout=60)
     assert sorted(r[0] for r in res) == [0, 1]
     assert all(r[1] and r[2] for r in res), res
+
+
+# ----------------------------------------------------------------------------- front end (§8(f) rank 1)
+def _frontend_golden():
+    return np.load(os.path.join(os.path.dirname(__file__), "golden", "frontend.npz"))
+
+
+def test_frontend_oracle_vs_reference_golden():
+    """oracle/frontend_cpu.py restates Stft / LogMel.forward / GlobalMVN; the fixture was produced
+    by the reference modules themselves (tests/golden/make_golden.py frontend)."""
+    from oracle import frontend_cpu as FE
+    g = _frontend_golden()
+    x, lens = torch.from_numpy(g["x"]), torch.from_numpy(g["lens"])
+    spec, olens = FE.stft(x, lens, 512, 128)
+    assert torch.equal(olens, torch.from_numpy(g["olens"]))
+    assert float((spec - torch.from_numpy(g["spec"])).abs().max()) < 1e-5
+    power = spec[..., 0] ** 2 + spec[..., 1] ** 2
+    feats = FE.log_mel(power, olens, torch.from_numpy(g["melmat"]))
+    assert float((feats - torch.from_numpy(g["feats"])).abs().max()) < 1e-5
+    stats = {"count": g["stat_count"], "sum": g["stat_sum"], "sum_square": g["stat_sum_square"]}
+    mean, std = FE.global_mvn_stats(stats)
+    normed = FE.global_mvn(torch.from_numpy(g["feats"]), olens, mean, std)
+    assert float((normed - torch.from_numpy(g["normed"])).abs().max()) < 1e-5
+    # the fixture's mel matrix is the oracle's restated librosa Slaney filterbank (parity unpinned:
+    # librosa is absent and the reference holds no mel fixture)
+    assert np.array_equal(FE.mel_filters(16000, 512, 80, 0.0, 8000.0).T, g["melmat"])
+
+
+def test_frontend_mel_restatements_agree():
+    """The product's filterbank (asr/frontend/default.py) and the oracle's, written separately
+    from librosa's published algorithm, agree (Slaney and HTK scales, band edges)."""
+    from espnet_slurp_amd.asr.frontend.default import mel_filters
+    from oracle import frontend_cpu as FE
+    for args in ((16000, 512, 80, 0.0, 8000.0, False), (16000, 400, 40, 20.0, 7600.0, False),
+                 (8000, 256, 23, 0.0, 4000.0, True)):
+        a, b = mel_filters(*args), FE.mel_filters(*args)
+        assert a.dtype == b.dtype == np.float32 and a.shape == b.shape
+        assert np.allclose(a, b, rtol=1e-6, atol=1e-9), args
+
+
+def test_frontend_and_global_mvn_state_dict_keys(tmp_path):
+    from espnet_slurp_amd.asr.frontend.default import DefaultFrontend
+    from espnet_slurp_amd.layers.global_mvn import GlobalMVN
+    fe = DefaultFrontend()
+    assert list(fe.state_dict()) == ["logmel.melmat"] and fe.state_dict()["logmel.melmat"].shape == (257, 80)
+    assert fe.output_size() == 80 and fe.num_frames(3000) == 24
+    p = tmp_path / "feats_stats.npz"
+    np.savez(p, count=np.float64(10.0), sum=np.ones(80), sum_square=np.full(80, 2.0))
+    gm = GlobalMVN(p)
+    assert sorted(gm.state_dict()) == ["mean", "std"]
+    assert np.allclose(gm.mean.numpy(), 0.1) and np.allclose(gm.std.numpy(), np.sqrt(0.2 - 0.01))
