@@ -58,6 +58,7 @@ SIGNATURES = {
     "esp_relpos_attn_bwd": [P, L, P, L, P, P, P, L, I, I, F, F, U64, I, L, P],
     "esp_fbank_fwd": [P, L, P, I, I, I, I, P, P, P, P, P, I, P, I, P],
     "esp_global_mvn": [P, P, I, I, I, P, P, I, I, P],
+    "esp_conv2_dgrad": [P, P, P, P, I, I, I, I, P, P, P],
     "esp_conv1_fwd": [P, P, P, P, I, I, I, I, P],
     "esp_col2im_relu": [P, P, P, I, I, I, I, P],
     "esp_conv1_wgrad": [P, P, P, P, I, I, I, I, P, P],
@@ -70,7 +71,7 @@ SIGNATURES = {
     "esp_ctc_forced_align": [P, I, I, P, I, I, P, P, P],
 }
 _RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I}
-ABI_VERSION = 10  # bumped whenever a signature in include/espnet_mi355.h changes
+ABI_VERSION = 11  # bumped whenever a signature in include/espnet_mi355.h changes
 
 _lib = None
 

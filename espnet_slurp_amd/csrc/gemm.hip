@@ -26,8 +26,25 @@ namespace {
 
 constexpr int BM = 128, BN = 128, BK = 32, NT = 256;  // BK: split-K granularity
 
-enum Mode { KC = 0, RC = 1, I2C_KC = 2, I2C_RC = 3 };
+enum Mode { KC = 0, RC = 1, I2C_KC = 2, I2C_RC = 3, I2CT_KC = 4 };
 enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_SWISH = 2 };
+
+struct FastDiv {  // n / d for n < 2^31: (n * m) >> s, m = ceil(2^s / d), s = 31 + ceil(log2 d)
+  uint64_t m;
+  uint32_t s, d;
+};
+static FastDiv make_fastdiv(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  FastDiv f;
+  f.s = 31 + l;
+  f.m = ((1ull << f.s) + d - 1) / d;
+  f.d = d;
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (uint32_t)(((uint64_t)n * f.m) >> f.s);
+}
 
 struct Im2col {  // NHWC input map [Bn][H][W][C], 3x3 kernel, stride 2, no padding
   int H, W, C, Ho, Wo;
@@ -65,7 +82,20 @@ struct GemmArgs {
   float* rowsum;     // != NULL: rowsum[m] += sum_k A(m,k)  (bias gradient of a weight-gradient GEMM)
   float* rs_work;    // split-K partial row sums [split][M]
   int wide;          // float4 epilogue legal (N, ldc, batch strides % 4 == 0, 16-B aligned C/R/aux/pre/bias/work)
+  // output row map (conv2 input gradient, one parity class (ph, pw) of the conv1 output grid):
+  // row m = (b, a, e) of the class grid (Ha x We) -> pixel (b, 2a+ph, 2e+pw) of the T1 x F1 map
+  int cmap;
+  FastDiv cm_hw, cm_w;
+  int cm_T1, cm_F1, cm_ph, cm_pw;
 };
+
+__device__ __forceinline__ long row_off(const GemmArgs& g, int m) {
+  if (!g.cmap) return (long)m * g.ldc;
+  const int b = (int)fdiv((uint32_t)m, g.cm_hw);
+  const int rem = m - b * (int)g.cm_hw.d;
+  const int a = (int)fdiv((uint32_t)rem, g.cm_w), e = rem - a * (int)g.cm_w.d;
+  return (((long)b * g.cm_T1 + 2 * a + g.cm_ph) * g.cm_F1 + 2 * e + g.cm_pw) * g.ldc;
+}
 
 // Fused epilogue for output element (m, n) of batch z with raw accumulator `acc`.  The kind is
 // chosen once per launch (a template argument), so the per-element path is straight-line:
@@ -79,7 +109,7 @@ __host__ __device__ inline int epi_kind(const GemmArgs& g) {
 }
 template <int EPI>
 __device__ __forceinline__ void epi_store(const GemmArgs& g, long cbase, uint64_t dbase, int m, int n, float acc) {
-  const long off = cbase + (long)m * g.ldc + n;
+  const long off = cbase + row_off(g, m) + n;
   const uint64_t seed = g.drop_thresh ? esp::keyed(g.seed, g.key) : 0;
   float v = acc;
   if constexpr (EPI == EPI_FWD) {
@@ -136,7 +166,7 @@ __device__ __forceinline__ void store_tiles(const GemmArgs& g, int z, int mrow0,
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = mrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const long off = cbase + (long)m * g.ldc + n;
+        const long off = cbase + row_off(g, m) + n;
         rr[r] = (has_r && m < g.M) ? g.r[off] : 0.f;
         if constexpr (EPI == EPI_BWD) pp[r] = m < g.M ? g.pre[off] : 0.f;
       }
@@ -144,7 +174,7 @@ __device__ __forceinline__ void store_tiles(const GemmArgs& g, int z, int mrow0,
       for (int r = 0; r < 16; ++r) {
         const int m = mrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (m >= g.M) continue;
-        const long off = cbase + (long)m * g.ldc + n;
+        const long off = cbase + row_off(g, m) + n;
         float v = acc[i][j][r] + bn;
         if constexpr (EPI == EPI_FWD) {
           if (g.aux) g.aux[off] = v;
@@ -224,7 +254,7 @@ __device__ __forceinline__ void store_tiles_wide(const GemmArgs& g, int z, int m
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int m = mrow0 + i * 32 + 8 * q + 4 * h + (l32 & 3);
-        const long off = cbase + (long)m * g.ldc + n;
+        const long off = cbase + row_off(g, m) + n;
         const bool ok = nok && m < g.M;
         rr[q] = (has_r && ok) ? *reinterpret_cast<const float4*>(g.r + off) : make_float4(0.f, 0.f, 0.f, 0.f);
         if constexpr (EPI == EPI_BWD)
@@ -234,7 +264,7 @@ __device__ __forceinline__ void store_tiles_wide(const GemmArgs& g, int z, int m
       for (int q = 0; q < 4; ++q) {
         const int m = mrow0 + i * 32 + 8 * q + 4 * h + (l32 & 3);
         if (!nok || m >= g.M) continue;
-        const long off = cbase + (long)m * g.ldc + n;
+        const long off = cbase + row_off(g, m) + n;
         float v[4] = {acc[i][j][4 * q] + bn.x, acc[i][j][4 * q + 1] + bn.y, acc[i][j][4 * q + 2] + bn.z,
                       acc[i][j][4 * q + 3] + bn.w};
         const float r4[4] = {rr[q].x, rr[q].y, rr[q].z, rr[q].w};
@@ -610,22 +640,6 @@ __global__ __launch_bounds__(NT, VARIANT == 3 ? 4 : 2) void gemm_f32_kernel(Gemm
 // discarded outputs); the K tail of the last slab is zeroed in LDS before use.
 // Block ids are remapped so that consecutive tiles (same A row panel) share an XCD's L2.
 
-struct FastDiv {  // n / d for n < 2^31: (n * m) >> s, m = ceil(2^s / d), s = 31 + ceil(log2 d)
-  uint64_t m;
-  uint32_t s, d;
-};
-static FastDiv make_fastdiv(uint32_t d) {
-  uint32_t l = 0;
-  while ((1ull << l) < d) ++l;
-  FastDiv f;
-  f.s = 31 + l;
-  f.m = ((1ull << f.s) + d - 1) / d;
-  f.d = d;
-  return f;
-}
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
-  return (uint32_t)(((uint64_t)n * f.m) >> f.s);
-}
 
 struct GldsArgs {
   FastDiv c_a, c_b;    // im2col channel count C
@@ -633,6 +647,13 @@ struct GldsArgs {
   FastDiv hw_a, wo_a;  // I2C_KC
   int ntx, nty;        // tile grid (N tiles, M tiles)
   int ntiles;          // ntx * nty * batch * splits
+  // I2CT_KC (conv2 input gradient as an implicit GEMM per parity class): A(r, k) =
+  // dY[b, a - dt[t], e - df[t], o] (0 outside the T2 x F2 grid), r = (b, a, e) over Ha x We,
+  // k = t*C + o (tap t of the class, channel o); C % 32 == 0 so a slab never straddles taps
+  FastDiv t_hw, t_w;
+  int t_T2, t_F2, t_C;
+  int t_dt[4], t_df[4];
+  const float* t_zeros;  // >= 16 zero bytes: the DMA source of lanes outside the grid
   int abl;             // diagnostic ablation bits (ESP_GEMM_ABL, timing only): 1 no DMA after the
                        // first slab, 2 no epilogue stores, 4 no k-loop barrier / waits, 16 dword
                        // (not float4) epilogue stores
@@ -669,21 +690,31 @@ __device__ __forceinline__ long i2c_pix_off(const Im2col& ic, const FastDiv& fhw
 // Per-lane source bookkeeping for one operand: NI wave-instructions per slab.
 template <int MODE, int ROWS, int NI>
 struct Stage {
+  static constexpr bool kKC = MODE == KC || MODE == I2C_KC || MODE == I2CT_KC;
   const float* p[NI];  // per instruction: base incl. the slab-invariant part
   int q[NI];           // KC: k offset inside the slab (4*quad) ; RC: k-row inside the slab
+  int ga[MODE == I2CT_KC ? NI : 1], ge[MODE == I2CT_KC ? NI : 1];  // I2CT: class-grid row / column
   __device__ __forceinline__ void init(const Operand& op, const float* base, int rows, int K, int row0,
                                        const FastDiv& fc, const FastDiv& fhw, const FastDiv& fwo, int wave,
-                                       int lane) {
+                                       int lane, const GldsArgs* x = nullptr) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int slot = (i * 4 + wave) * 64 + lane;
-      if constexpr (MODE == KC || MODE == I2C_KC) {
+      if constexpr (kKC) {
         const int r = slot >> 3, qs = slot & 7;
         const int qq = qs ^ (r & 7);
         const int gr = min(row0 + r, rows - 1);
         q[i] = 4 * qq;
         if constexpr (MODE == KC) p[i] = base + (long)gr * op.ld;
-        else p[i] = base + i2c_pix_off(op.ic, fhw, fwo, gr);
+        else if constexpr (MODE == I2C_KC) p[i] = base + i2c_pix_off(op.ic, fhw, fwo, gr);
+        else {
+          const int bb = (int)fdiv((uint32_t)gr, x->t_hw);
+          const int rem = gr - bb * (int)x->t_hw.d;
+          const int a = (int)fdiv((uint32_t)rem, x->t_w), e = rem - a * (int)x->t_w.d;
+          ga[i] = a;
+          ge[i] = e;
+          p[i] = base + (((long)bb * x->t_T2 + a) * x->t_F2 + e) * x->t_C;
+        }
       } else {
         constexpr int QPR = ROWS / 4;  // quads per k-row
         const int kr = slot / QPR, rs = slot % QPR;
@@ -697,14 +728,26 @@ struct Stage {
   }
   // issue this lane's NI LDS-DMA loads of the slab starting at k0 into `dst`
   __device__ __forceinline__ void issue(const Operand& op, int K, int k0, float* dst, int wave, const FastDiv& fc,
-                                        const FastDiv& fhw, const FastDiv& fwo) const {
+                                        const FastDiv& fhw, const FastDiv& fwo, const GldsArgs* x = nullptr) const {
+    int dt = 0, df = 0, o0 = 0;
+    if constexpr (MODE == I2CT_KC) {  // the slab's tap (uniform: C % 32 == 0)
+      const int t = k0 / x->t_C;
+      o0 = k0 - t * x->t_C;
+      dt = x->t_dt[t];
+      df = x->t_df[t];
+    }
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       float* ldsw = dst + (i * 4 + wave) * 256;
-      if constexpr (MODE == KC || MODE == I2C_KC) {
+      if constexpr (kKC) {
         const int k = min(k0 + q[i], (K - 1) & ~3);
         if constexpr (MODE == KC) lds_dma16(p[i] + k, ldsw);
-        else lds_dma16(p[i] + i2c_col_off(op.ic, fc, k), ldsw);
+        else if constexpr (MODE == I2C_KC) lds_dma16(p[i] + i2c_col_off(op.ic, fc, k), ldsw);
+        else {
+          const int a = ga[i] - dt, e = ge[i] - df;
+          const bool in = a >= 0 && a < x->t_T2 && e >= 0 && e < x->t_F2;
+          lds_dma16(in ? p[i] - ((long)dt * x->t_F2 + df) * x->t_C + o0 + q[i] : x->t_zeros, ldsw);
+        }
       } else {
         const int k = min(k0 + q[i], K - 1);
         if constexpr (MODE == RC) lds_dma16(p[i] + (long)k * op.ld, ldsw);
@@ -718,7 +761,7 @@ struct Stage {
 template <int MODE, int ROWS>
 __device__ __forceinline__ void zero_tail(float* slab, int kv) {
   for (int idx = threadIdx.x; idx < ROWS * GL_BK; idx += NT) {
-    if constexpr (MODE == KC || MODE == I2C_KC) {
+    if constexpr (MODE == KC || MODE == I2C_KC || MODE == I2CT_KC) {
       const int r = idx >> 5, k = idx & 31;
       if (k >= kv) slab[(r * 8 + ((k >> 2) ^ (r & 7))) * 4 + (k & 3)] = 0.f;
     } else {
@@ -731,7 +774,7 @@ __device__ __forceinline__ void zero_tail(float* slab, int kv) {
 // the 16 k-values (k = 16h + s) of tile row r
 template <int MODE, int ROWS>
 __device__ __forceinline__ void frag16(const float* slab, int r, int h, float (&f)[16]) {
-  if constexpr (MODE == KC || MODE == I2C_KC) {
+  if constexpr (MODE == KC || MODE == I2C_KC || MODE == I2CT_KC) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const float4 v = *reinterpret_cast<const float4*>(slab + (r * 8 + ((4 * h + j) ^ (r & 7))) * 4);
@@ -819,9 +862,9 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_ke
   TileCoord c = tile_coord<BNT>(g, x, t, G);
   Stage<MA, BM, NIA> sa;
   Stage<MB, BNT, NIB> sb;
-  sa.init(g.a, a_base(c), g.M, g.K, c.m0, x.c_a, x.hw_a, x.wo_a, wave, lane);
+  sa.init(g.a, a_base(c), g.M, g.K, c.m0, x.c_a, x.hw_a, x.wo_a, wave, lane, &x);
   sb.init(g.b, b_base(c), g.N, g.K, c.n0, x.c_b, x.hw_b, x.wo_b, wave, lane);
-  sa.issue(g.a, g.K, c.kbeg, smem, wave, x.c_a, x.hw_a, x.wo_a);
+  sa.issue(g.a, g.K, c.kbeg, smem, wave, x.c_a, x.hw_a, x.wo_a, &x);
   sb.issue(g.b, g.K, c.kbeg, smem + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
   wait_vm0();
   raw_barrier();
@@ -884,7 +927,7 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_ke
       const int k1 = c.kbeg + (kt + 1) * GL_BK;
       float* nxt = smem + (buf ^ 1) * BUF;  // last read before the previous barrier
       if (!(x.abl & 1)) {
-        sa.issue(g.a, g.K, k1, nxt, wave, x.c_a, x.hw_a, x.wo_a);
+        sa.issue(g.a, g.K, k1, nxt, wave, x.c_a, x.hw_a, x.wo_a, &x);
         sb.issue(g.b, g.K, k1, nxt + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
       }
       compute(smem + buf * BUF);
@@ -895,9 +938,9 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_ke
       float* nxt = smem + (buf ^ 1) * BUF;
       if (has_next) {
         cn = tile_coord<BNT>(g, x, tnext, G);
-        sa.init(g.a, a_base(cn), g.M, g.K, cn.m0, x.c_a, x.hw_a, x.wo_a, wave, lane);
+        sa.init(g.a, a_base(cn), g.M, g.K, cn.m0, x.c_a, x.hw_a, x.wo_a, wave, lane, &x);
         sb.init(g.b, b_base(cn), g.N, g.K, cn.n0, x.c_b, x.hw_b, x.wo_b, wave, lane);
-        sa.issue(g.a, g.K, cn.kbeg, nxt, wave, x.c_a, x.hw_a, x.wo_a);
+        sa.issue(g.a, g.K, cn.kbeg, nxt, wave, x.c_a, x.hw_a, x.wo_a, &x);
         sb.issue(g.b, g.K, cn.kbeg, nxt + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
       }
       const int kv = c.kend - (c.kbeg + (c.nk - 1) * GL_BK);
@@ -1074,13 +1117,14 @@ int variant() {
 // so the plain GEMMs carry none of the fused epilogues' registers).  Returns false when the
 // mode pair has no instantiation of the needed kind (the caller falls back).
 template <int MA, int MB, int BNT>
-bool launch_glds(const GemmArgs& g, int batch, hipStream_t st) {
+bool launch_glds(const GemmArgs& g, int batch, hipStream_t st, const GldsArgs* tconv = nullptr) {
   constexpr bool can_rs = MA == RC;
   constexpr bool can_fwd = (MA == KC && (MB == KC || MB == RC)) || (MA == I2C_KC && MB == KC);
-  constexpr bool can_bwd = MA == KC && MB == RC;
+  constexpr bool can_bwd = (MA == KC || MA == I2CT_KC) && MB == RC;
   const int kind = g.splits > 1 ? EPI_PLAIN : epi_kind(g);
   if ((kind == EPI_FWD && !can_fwd) || (kind == EPI_BWD && !can_bwd)) return false;
   GldsArgs x{};
+  if (MA == I2CT_KC) x = *tconv;  // the transposed-conv gather parameters
   x.ntx = (g.N + BNT - 1) / BNT;
   x.nty = (g.M + BM - 1) / BM;
   if (MA == I2C_KC) {
@@ -1106,13 +1150,13 @@ bool launch_glds(const GemmArgs& g, int batch, hipStream_t st) {
   else if (kind == EPI_PLAIN)
     hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_PLAIN>), grid(glds_occupancy<BNT, EPI_PLAIN>()),
                        dim3(NT), 0, st, g, x);
-  else if constexpr (can_fwd) {
-    if (kind == EPI_FWD)
+  else if (kind == EPI_FWD) {
+    if constexpr (can_fwd)
       hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_FWD>), grid(glds_occupancy<BNT, EPI_FWD>()),
                          dim3(NT), 0, st, g, x);
-    else if constexpr (can_bwd)
-      hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_BWD>), grid(glds_occupancy<BNT, EPI_BWD>()),
-                         dim3(NT), 0, st, g, x);
+  } else if constexpr (can_bwd) {
+    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_BWD>), grid(glds_occupancy<BNT, EPI_BWD>()),
+                       dim3(NT), 0, st, g, x);
   }
   return true;
 }
@@ -1268,4 +1312,78 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
       esp::set_error("esp_gemm_f32: unsupported mode pair %d,%d", mode_a, mode_b);
       return -1;
   }
+}
+
+
+// ============================================================================ conv2 input gradient
+// Conv2d(D, D, 3, stride 2) input gradient as 4 implicit GEMMs, one per parity class (ph, pw)
+// of the conv1 output grid (the sub-pixel decomposition of a strided transposed convolution):
+//   dz1[b, 2a+ph, 2e+pw, c] = relu'(z1) * sum_{taps (kt,kf) of the class, o} dz2[b, a-dt, e-df, o] W[o,c,kt,kf]
+// with kt in {0,2} (ph = 0) or {1} (ph = 1), dt = (kt-ph)/2 (same for f).  A = the dz2 gather
+// (I2CT_KC: LDS-DMA from dz2, lanes outside the T2 x F2 grid read a zero page), B = the class's
+// taps of W re-laid [(t*D + o)][c], epilogue = the conv1 ReLU mask (EPI_BWD, act' from z1) with
+// the output row map to the class's pixels.  Replaces the (B*T2*F2, 9D) column GEMM + col2im:
+// no 9x column buffer.  (subsampling.py:53-87 backward)
+namespace {
+__global__ void conv2_class_weights_kernel(const float* __restrict__ W, float* __restrict__ Wc, int D) {
+  // global tap slots: class (0,0) taps 0-3, (0,1) 4-5, (1,0) 6-7, (1,1) 8
+  const long n = 9L * D * D;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % D);
+    const long r = i / D;
+    const int o = (int)(r % D);
+    const int slot = (int)(r / D);
+    int kt, kf;
+    if (slot < 4) { kt = 2 * (slot >> 1); kf = 2 * (slot & 1); }
+    else if (slot < 6) { kt = 2 * (slot - 4); kf = 1; }
+    else if (slot < 8) { kt = 1; kf = 2 * (slot - 6); }
+    else { kt = 1; kf = 1; }
+    Wc[i] = W[(((long)o * D + c) * 3 + kt) * 3 + kf];
+  }
+}
+}  // namespace
+
+ESP_API int esp_conv2_dgrad(const float* dz2, const float* W, const float* z1, float* dz1, int B, int T1, int F1,
+                            int D, const float* zeros16, float* wc_work, void* stream) {
+  const int T2 = (T1 - 3) / 2 + 1, F2 = (F1 - 3) / 2 + 1;
+  ESP_ARG_CHECK(B >= 1 && T2 >= 1 && F2 >= 1 && D % 32 == 0, "esp_conv2_dgrad: bad sizes (D %% 32 == 0 needed)");
+  ESP_ARG_CHECK(aligned16(dz2) && aligned16(z1) && aligned16(dz1) && aligned16(zeros16) && aligned16(wc_work),
+                "esp_conv2_dgrad: operands must be 16-B aligned");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(conv2_class_weights_kernel, dim3(1024), dim3(256), 0, st, W, wc_work, D);
+  ESP_CHECK_LAUNCH("esp_conv2_dgrad (weights)");
+  const int slot0[4] = {0, 4, 6, 8};
+  for (int cls = 0; cls < 4; ++cls) {
+    const int ph = cls >> 1, pw = cls & 1;
+    const int Ha = (T1 - ph + 1) / 2, We = (F1 - pw + 1) / 2;
+    const int nkt = ph ? 1 : 2, nkf = pw ? 1 : 2, ntap = nkt * nkf;
+    GldsArgs t{};
+    t.t_hw = make_fastdiv((uint32_t)(Ha * We));
+    t.t_w = make_fastdiv((uint32_t)We);
+    t.t_T2 = T2; t.t_F2 = F2; t.t_C = D;
+    for (int ti = 0; ti < ntap; ++ti) {
+      const int kt = ph ? 1 : 2 * (ti / nkf), kf = pw ? 1 : 2 * (ti % nkf);
+      t.t_dt[ti] = (kt - ph) / 2;
+      t.t_df[ti] = (kf - pw) / 2;
+    }
+    t.t_zeros = zeros16;
+    GemmArgs g{};
+    g.M = B * Ha * We; g.N = D; g.K = ntap * D; g.nb2 = 1;
+    g.a = Operand{dz2, 0, 0, 0, 1, {}, 1};
+    g.b = Operand{wc_work + (long)slot0[cls] * D * D, D, 0, 0, 1, {}, 1};
+    g.c = dz1; g.ldc = D; g.alpha = 1.f; g.beta = 0.f;
+    g.bwd_act = ACT_RELU; g.pre = z1;
+    g.key = esp::rng_key_ptr();
+    g.wide = 1;
+    g.batch = 1; g.splits = 1; g.kchunk = g.K; g.bnt = 64;
+    g.cmap = 1;
+    g.cm_hw = t.t_hw; g.cm_w = t.t_w;
+    g.cm_T1 = T1; g.cm_F1 = F1; g.cm_ph = ph; g.cm_pw = pw;
+    if (!launch_glds<I2CT_KC, RC, 64>(g, 1, st, &t)) {
+      esp::set_error("esp_conv2_dgrad: no kernel for the class GEMM");
+      return -1;
+    }
+    ESP_CHECK_LAUNCH("esp_conv2_dgrad");
+  }
+  return 0;
 }

@@ -453,3 +453,17 @@ def global_mvn(x, lens_i32, mean, std, norm_means=True, norm_vars=True):
     B, T, F = x.shape
     _native.call("esp_global_mvn", _p(x), _p(lens_i32), B, T, F, _p(mean), _p(std), int(norm_means),
                  int(norm_vars), _st())
+
+
+_ZEROS = {}
+CONV2_IMPLICIT_DGRAD = os.environ.get("ESP_CONV2_IMPLICIT_DGRAD", "0") == "1"
+
+
+def conv2_dgrad(dz2, W, z1, dz1, B, T1, F1, D):
+    """Conv2d(D, D, 3, 2) input gradient x conv1 ReLU mask as 4 implicit parity-class GEMMs."""
+    _f32(dz2, W, z1, dz1)
+    key = str(dz2.device)
+    if key not in _ZEROS:
+        _ZEROS[key] = torch.zeros(64, dtype=torch.float32, device=dz2.device)
+    wc = _WS2.get(9 * D * D * 4, dz2.device)
+    _native.call("esp_conv2_dgrad", _p(dz2), _p(W), _p(z1), _p(dz1), B, T1, F1, D, _p(_ZEROS[key]), _p(wc), _st())

@@ -171,6 +171,12 @@ int esp_global_mvn(float* x, const int* lens, int B, int T, int F, const float* 
 /* ---- Conv2dSubsampling (subsampling.py:53-87), NHWC */
 int esp_conv1_fwd(const float* x, const float* W, const float* bias, float* z, int B, int T,
                   int F, int D, void* stream);
+/* conv2 input gradient as 4 implicit GEMMs (one per parity class of the conv1 output grid):
+ * dz1 = relu'(z1) * conv_transpose(dz2, W), W = Conv2d(D,D,3,2).weight (o,c,kt,kf) as the
+ * reference stores it; no 9x column buffer.  zeros16: >= 16 B of zeros (device); wc_work:
+ * 9*D*D floats (the per-class weight re-layout).  D % 32 == 0. */
+int esp_conv2_dgrad(const float* dz2, const float* W, const float* z1, float* dz1, int B, int T1, int F1,
+                    int D, const float* zeros16, float* wc_work, void* stream);
 int esp_col2im_relu(const float* dcol, const float* z1, float* dz1, int B, int T1, int F1, int D,
                     void* stream);
 int esp_conv1_wgrad(const float* x, const float* dz1, float* dW, float* db, int B, int T, int F,

@@ -148,9 +148,13 @@ def test_conv_module_block(dev):
     _check_grads(mod, P, "m")
 
 
-def test_subsampling_block(dev):
+@pytest.mark.parametrize("implicit", [False, True])
+@pytest.mark.parametrize("T,F,D", [(64, 80, 32), (65, 81, 64)])  # odd / even conv1 grid (parity classes)
+def test_subsampling_block(dev, T, F, D, implicit, monkeypatch):
+    from espnet_slurp_amd import kernels as K
+    monkeypatch.setattr(K, "CONV2_IMPLICIT_DGRAD", implicit)
     torch.manual_seed(2)
-    B, T, F, D = 2, 64, 80, 32
+    B = 2
     mod = Conv2dSubsampling(F, D).to(dev)
     with torch.no_grad():
         for p in mod.parameters():

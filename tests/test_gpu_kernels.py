@@ -489,3 +489,26 @@ def test_subsampling_conv1_and_col2im(dev):
     K.conv1_wgrad(x.to(dev), dzm.contiguous(), dW, db, Bn, T, F_, D)
     assert rel_err(dW.cpu().view(D, 1, 3, 3), w0t.grad) < 1e-5
     assert rel_err(db.cpu(), b0t.grad) < 1e-5
+
+
+@pytest.mark.parametrize("T1,F1", [(31, 39), (32, 40), (9, 7)])
+def test_conv2_dgrad_parity_classes_vs_column_path(dev, T1, F1):
+    """esp_conv2_dgrad (4 implicit parity-class GEMMs, zero-page gather at the grid edges, ReLU
+    mask + pixel row map in the epilogue) == the column GEMM + col2im it replaces."""
+    B, D = 3, 64
+    T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
+    g = torch.Generator().manual_seed(31)
+    dz2 = torch.randn(B * T2 * F2, D, generator=g).to(dev)
+    W = (torch.randn(D, D, 3, 3, generator=g) * 0.1).to(dev)
+    z1 = torch.relu(torch.randn(B * T1 * F1 * D, generator=g)).to(dev)
+    w2r = torch.empty(D * 9 * D, device=dev)
+    K.permute3(W, w2r, D, D, 9)
+    dcol = torch.empty(B * T2 * F2, 9 * D, device=dev)
+    K.gemm(B * T2 * F2, 9 * D, D, dz2, w2r, dcol, mode_a=K.KC, lda=D, mode_b=K.RC, ldb=9 * D, ldc=9 * D)
+    ref = torch.empty(B * T1 * F1 * D, device=dev)
+    K.col2im_relu(dcol, z1, ref, B, T1, F1, D)
+    got = torch.full((B * T1 * F1 * D,), float("nan"), device=dev)
+    K.conv2_dgrad(dz2, W, z1, got, B, T1, F1, D)
+    torch.cuda.synchronize()
+    assert not torch.isnan(got).any()
+    assert rel_err(got.cpu(), ref.cpu()) < 1e-5
