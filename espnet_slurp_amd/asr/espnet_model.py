@@ -64,6 +64,7 @@ class HeadsFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_loss, g_others):
         dhs = ctx.model._heads_backward(ctx.state, g_loss.contiguous())
+        K.join_side(dhs.device)
         ctx.state = None
         return dhs, None, None, None, None
 
