@@ -123,6 +123,17 @@ def cpu_baseline(args):
                       f"1 warmup + 3 timed steps, {t:.2f} s/step on {n} threads"}
 
 
+def workload_name(args) -> str:
+    """BASELINE.json config name of the shape being run (C2 is the default / headline)."""
+    if (args.d, args.heads, args.ff, args.layers) == (256, 4, 1024, 12):
+        return "C2 SLURP Conformer-medium"
+    if (args.d, args.heads, args.ff, args.layers) == (512, 8, 2048, 17):
+        return "C4-shape LibriSpeech Conformer-large (fp32)"
+    if (args.d, args.heads, args.ff, args.layers) == (512, 8, 2048, 12):
+        return "C5-shape SLURP-entity Conformer (fp32)"
+    return "custom Conformer"
+
+
 def gemm_algorithmic_bytes(shapes) -> float:
     """Sum over the profiled GEMM launches of the bytes each must move at least once: A, B read,
     C written (fp32).  An implicit-im2col operand counts its NHWC source map (~ 4/9 of the
@@ -239,7 +250,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic (N(0,1) fbank, random tokens U[20,40], random-init weights)",
             "launch": "eager" if args.eager else "hip_graph",
-            "config": {"workload": f"C2 SLURP Conformer-medium d={args.d} H={args.heads} FF={args.ff} "
+            "config": {"workload": f"{workload_name(args)} d={args.d} H={args.heads} FF={args.ff} "
                                    f"{args.layers}L enc / 6L dec, V={args.vocab}, rel_pos={args.rel_pos}, "
                                    "ctc 0.3, lsm 0.1, dropout 0.1, SpecAug on",
                        "global_batch": world * args.batch, "seq_len": 1500, "parallelism": f"dp{world}"},
