@@ -349,6 +349,118 @@ __global__ __launch_bounds__(256) void dwconv_wgrad_kernel(const float* __restri
   }
 }
 
+// Register-blocked variants for the common kernel sizes (cnn_module_kernel 31 / 15): a thread's
+// PT outputs need PT + K - 1 inputs, read ONCE from LDS into a register window (the LDS-tiled
+// kernels above read K*PT values per thread), filters in registers.
+constexpr int DWR_PT = 16, DWR_TT = 4 * DWR_PT;  // outputs per thread, time steps per block
+// rows t_lo .. t_lo + DWR_TT + KT - 2 of channels c0 .. c0+63 into LDS (zero outside [0,T) x [0,D)),
+// float4 per lane: 16 lanes per row, 16 rows per pass of the 256-thread block
+template <int KT>
+__device__ __forceinline__ void dw_stage(float (*xs)[64], const float* __restrict__ xb, int t_lo, int T, int D,
+                                         int c0) {
+  const int q = threadIdx.x & 15, r0 = threadIdx.x >> 4;
+  const int c = c0 + 4 * q;
+  const bool vec = (D & 3) == 0 && c + 4 <= D;
+  for (int r = r0; r < DWR_TT + KT - 1; r += 16) {
+    const int t = t_lo + r;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (t >= 0 && t < T) {
+      const float* src = xb + (long)t * D + c;
+      if (vec) {
+        v = *reinterpret_cast<const float4*>(src);
+      } else {
+        if (c < D) v.x = src[0];
+        if (c + 1 < D) v.y = src[1];
+        if (c + 2 < D) v.z = src[2];
+        if (c + 3 < D) v.w = src[3];
+      }
+    }
+    *reinterpret_cast<float4*>(&xs[r][4 * q]) = v;
+  }
+}
+template <int KT>
+__global__ __launch_bounds__(256) void dwconv_rb_kernel(const float* __restrict__ x, const float* __restrict__ W,
+                                                        const float* __restrict__ bias, float* __restrict__ y, int T,
+                                                        int D, int flip) {
+  __shared__ __attribute__((aligned(16))) float xs[DWR_TT + KT - 1][64];
+  __shared__ float ws[KT][64];
+  constexpr int pad = (KT - 1) / 2;
+  const int c0 = blockIdx.x * 64, t0 = blockIdx.y * DWR_TT, b = blockIdx.z;
+  const int cl = threadIdx.x & 63, tg = threadIdx.x >> 6;
+  const int c = c0 + cl;
+  const float* xb = x + (long)b * T * D;
+  // the block's 64 x KT weights are contiguous in W: coalesced load, transposed into LDS
+  const int nw = min(64, D - c0) * KT;
+  for (int i = threadIdx.x; i < nw; i += 256) {
+    const int cc = i / KT, kk = i - cc * KT;
+    ws[flip ? (KT - 1 - kk) : kk][cc] = W[(long)c0 * KT + i];
+  }
+  dw_stage<KT>(xs, xb, t0 - pad, T, D, c0);
+  __syncthreads();
+  if (c >= D) return;
+  float w[KT];
+#pragma unroll
+  for (int k = 0; k < KT; ++k) w[k] = ws[k][cl];
+  float win[DWR_PT + KT - 1];
+#pragma unroll
+  for (int i = 0; i < DWR_PT + KT - 1; ++i) win[i] = xs[tg * DWR_PT + i][cl];
+  const float bv = bias ? bias[c] : 0.f;
+#pragma unroll
+  for (int j = 0; j < DWR_PT; ++j) {
+    float a = bv;
+#pragma unroll
+    for (int k = 0; k < KT; ++k) a += w[k] * win[j + k];
+    const int t = t0 + tg * DWR_PT + j;
+    if (t < T) y[((long)b * T + t) * D + c] = a;
+  }
+}
+
+// dW[c,k] partials over a DWR_TT-step chunk: thread (channel, time group) accumulates all K taps
+// over its 16 steps from a register window, the 4 time groups are summed in LDS (fixed order).
+template <int KT>
+__global__ __launch_bounds__(256) void dwconv_wgrad_rb_kernel(const float* __restrict__ dy,
+                                                              const float* __restrict__ x,
+                                                              float* __restrict__ part, int T, int D) {
+  __shared__ __attribute__((aligned(16))) float xs[DWR_TT + KT - 1][64];
+  __shared__ float red[3][KT][64];
+  constexpr int pad = (KT - 1) / 2;
+  const int c0 = blockIdx.x * 64, ch = blockIdx.y, b = blockIdx.z, nch = gridDim.y;
+  const int t0 = ch * DWR_TT;
+  const int cl = threadIdx.x & 63, tg = threadIdx.x >> 6;
+  const int c = c0 + cl;
+  const float* xb = x + (long)b * T * D;
+  const float* db = dy + (long)b * T * D;
+  dw_stage<KT>(xs, xb, t0 - pad, T, D, c0);
+  float g[DWR_PT];
+#pragma unroll
+  for (int j = 0; j < DWR_PT; ++j) {
+    const int t = t0 + tg * DWR_PT + j;
+    g[j] = (c < D && t < T) ? db[(long)t * D + c] : 0.f;
+  }
+  __syncthreads();
+  float win[DWR_PT + KT - 1];
+#pragma unroll
+  for (int i = 0; i < DWR_PT + KT - 1; ++i) win[i] = xs[tg * DWR_PT + i][cl];
+  float acc[KT];
+#pragma unroll
+  for (int k = 0; k < KT; ++k) {
+    float a = 0.f;
+#pragma unroll
+    for (int j = 0; j < DWR_PT; ++j) a += g[j] * win[j + k];
+    acc[k] = a;
+  }
+  if (tg > 0) {
+#pragma unroll
+    for (int k = 0; k < KT; ++k) red[tg - 1][k][cl] = acc[k];
+  }
+  __syncthreads();
+  if (tg == 0 && c < D) {
+    float* pr = part + ((long)(b * nch + ch) * D + c) * KT;
+#pragma unroll
+    for (int k = 0; k < KT; ++k) pr[k] = ((acc[k] + red[0][k][cl]) + red[1][k][cl]) + red[2][k][cl];
+  }
+}
+
 // BatchNorm statistics, stage 1: per row-chunk partial sums (double) of x and, given a
 // mean, of (x-mean)^2.  mode 0: sum x ; mode 1: sum (x-mean)^2
 __global__ void bn_part_kernel(const float* __restrict__ x, int M, int D, int rows_per_block,
@@ -547,6 +659,17 @@ ESP_API int esp_glu_bwd(const float* u, const float* dg, float* du, long rows, i
 ESP_API int esp_dwconv1d(const float* x, const float* W, const float* bias, float* y, int Bn, int T, int D, int K,
                          int flip, void* stream) {
   ESP_ARG_CHECK(K % 2 == 1 && K <= 64, "esp_dwconv1d: K must be odd and <= 64");
+  if (K == 31 || K == 15) {
+    dim3 g2((D + 63) / 64, (T + DWR_TT - 1) / DWR_TT, Bn);
+    if (K == 31)
+      hipLaunchKernelGGL(dwconv_rb_kernel<31>, g2, dim3(256), 0, (hipStream_t)stream, x, W, flip ? nullptr : bias, y, T,
+                         D, flip);
+    else
+      hipLaunchKernelGGL(dwconv_rb_kernel<15>, g2, dim3(256), 0, (hipStream_t)stream, x, W, flip ? nullptr : bias, y, T,
+                         D, flip);
+    ESP_CHECK_LAUNCH("esp_dwconv1d");
+    return 0;
+  }
   dim3 grid((D + 63) / 64, (T + DW_TT - 1) / DW_TT, Bn);
   hipLaunchKernelGGL(dwconv_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, W, flip ? nullptr : bias, y, Bn, T, D, K,
                      flip);
@@ -558,9 +681,15 @@ ESP_API int esp_dwconv1d(const float* x, const float* W, const float* bias, floa
 ESP_API int esp_dwconv1d_wgrad(const float* dy, const float* x, float* dW, int Bn, int T, int D, int K, float* work,
                                void* stream) {
   ESP_ARG_CHECK(K % 2 == 1 && K <= 64, "esp_dwconv1d_wgrad: K must be odd and <= 64");
-  const int nch = (T + DWW_TCH - 1) / DWW_TCH;
+  const bool rb = K == 31 || K == 15;
+  const int nch = rb ? (T + DWR_TT - 1) / DWR_TT : (T + DWW_TCH - 1) / DWW_TCH;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(dwconv_wgrad_kernel, dim3((D + 63) / 64, nch, Bn), dim3(256), 0, st, dy, x, work, T, D, K);
+  if (K == 31)
+    hipLaunchKernelGGL(dwconv_wgrad_rb_kernel<31>, dim3((D + 63) / 64, nch, Bn), dim3(256), 0, st, dy, x, work, T, D);
+  else if (K == 15)
+    hipLaunchKernelGGL(dwconv_wgrad_rb_kernel<15>, dim3((D + 63) / 64, nch, Bn), dim3(256), 0, st, dy, x, work, T, D);
+  else
+    hipLaunchKernelGGL(dwconv_wgrad_kernel, dim3((D + 63) / 64, nch, Bn), dim3(256), 0, st, dy, x, work, T, D, K);
   hipLaunchKernelGGL(finalize_cols_kernel<float>, fin_grid(D * K), dim3(1024), 0, st, work, Bn * nch, (long)D * K,
                      D * K, dW, 1);
   ESP_CHECK_LAUNCH("esp_dwconv1d_wgrad");

@@ -251,8 +251,9 @@ def test_layernorm(dev):
     assert rel_err(db.cpu(), bt.grad) < 1e-5
 
 
-def test_conv_module_pieces(dev):
-    Bn, T, D, Kk = 3, 57, 64, 31
+@pytest.mark.parametrize("Kk,T,D", [(31, 57, 64), (15, 130, 96), (9, 40, 64)])  # register-blocked 31/15, generic 9
+def test_conv_module_pieces(dev, Kk, T, D):
+    Bn = 3
     u = _r(Bn * T, 2 * D, seed=16)
     W = _r(D, 1, Kk, seed=17) * 0.2
     bw = _r(D, seed=18)
@@ -265,7 +266,7 @@ def test_conv_module_pieces(dev):
     gt = gam.double().requires_grad_(True)
     bt = bet.double().requires_grad_(True)
     g = F.glu(ut.view(Bn, T, 2 * D).transpose(1, 2), dim=1)
-    y = F.conv1d(g, Wt, bwt, padding=15, groups=D)
+    y = F.conv1d(g, Wt, bwt, padding=(Kk - 1) // 2, groups=D)
     rm, rv = torch.zeros(D, dtype=torch.double), torch.ones(D, dtype=torch.double)
     z = F.batch_norm(y, rm, rv, gt, bt, training=True, momentum=0.1, eps=1e-5)
     s = z * torch.sigmoid(z)
