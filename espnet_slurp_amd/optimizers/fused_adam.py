@@ -85,7 +85,76 @@ class FusedAdam(torch.optim.Optimizer):
     def zero_grad(self, set_to_none: bool = False):
         self.flat.zero_grad()
 
+    # ---------------------------------------------------------- checkpoint interop
+    def _adam_group(self) -> dict:
+        """param_groups[0] as torch.optim.Adam would hold it (every Adam default key of this
+        torch version, with this optimizer's hyper-parameters)."""
+        g = self.param_groups[0]
+        ref = torch.optim.Adam([torch.nn.Parameter(torch.zeros(1))], lr=g["lr"], betas=g["betas"], eps=g["eps"],
+                               weight_decay=g["weight_decay"])
+        return dict(ref.param_groups[0])
+
     def state_dict(self):
-        sd = super().state_dict()
-        sd["flat_state"] = {"exp_avg": self.exp_avg, "exp_avg_sq": self.exp_avg_sq, "step": self.n_steps}
-        return sd
+        """torch.optim.Adam.state_dict() format — what the reference's checkpoint.pth holds under
+        "optimizers" (trainer.py:340-352, abs_task.py:78-79): per parameter (keyed by its index
+        in param_groups[0]["params"]) {"step": float32 scalar, "exp_avg", "exp_avg_sq"} with the
+        parameter's shape, copied out of the flat moment buffers.  Graph mode keeps the step
+        count on device: it is read from there.  The group's lr is the host value — call
+        Trainer.sync_host_state() first (train_one_epoch does)."""
+        g = self.param_groups[0]
+        n = int(self._dstate[0].item()) if getattr(self, "_dstate", None) is not None else self.n_steps
+        state = {}
+        if n > 0:
+            for i, p in enumerate(g["params"]):
+                o, k = self.flat.slots[id(p)]
+                state[i] = {"step": torch.tensor(float(n), dtype=torch.float32),
+                            "exp_avg": self.exp_avg[o:o + k].view(p.shape).clone(),
+                            "exp_avg_sq": self.exp_avg_sq[o:o + k].view(p.shape).clone()}
+        group = self._adam_group()
+        group["params"] = list(range(len(g["params"])))
+        if "initial_lr" in g:  # added by the LR scheduler (torch _LRScheduler.__init__)
+            group["initial_lr"] = g["initial_lr"]
+        return {"state": state, "param_groups": [group]}
+
+    @torch.no_grad()
+    def load_state_dict(self, state_dict):
+        """Load a torch.optim.Adam state_dict (the reference's checkpoint, or ours): the moments
+        are copied into the flat buffers in place (a captured HIP graph keeps pointing at them),
+        the step count into the host and device counters.  FusedAdam keeps ONE step count: a
+        checkpoint whose parameters have different Adam step counts is refused."""
+        saved_groups = state_dict["param_groups"]
+        g = self.param_groups[0]
+        if len(saved_groups) != 1 or len(saved_groups[0]["params"]) != len(g["params"]):
+            raise ValueError("loaded state dict has a different number of parameter groups / parameters")
+        sg = saved_groups[0]
+        if sg.get("amsgrad", False):
+            raise NotImplementedError("amsgrad")
+        for key in ("lr", "betas", "eps", "weight_decay"):
+            g[key] = tuple(sg[key]) if key == "betas" else sg[key]
+        if "initial_lr" in sg:  # set by the LR scheduler at construction
+            g["initial_lr"] = sg["initial_lr"]
+        index = dict(zip(sg["params"], g["params"]))
+        self.exp_avg.zero_()
+        self.exp_avg_sq.zero_()
+        steps = set()
+        for i, st in state_dict["state"].items():
+            p = index[int(i)]
+            o, k = self.flat.slots[id(p)]
+            if st["exp_avg"].numel() != k:
+                raise ValueError(f"state of parameter {i}: {tuple(st['exp_avg'].shape)} != {tuple(p.shape)}")
+            self.exp_avg[o:o + k].copy_(st["exp_avg"].reshape(-1))
+            self.exp_avg_sq[o:o + k].copy_(st["exp_avg_sq"].reshape(-1))
+            steps.add(int(float(st["step"])))
+        if len(steps) > 1:
+            raise ValueError(f"parameters have different Adam step counts {sorted(steps)}")
+        self.n_steps = steps.pop() if steps else 0
+        if getattr(self, "_dstate", None) is not None:
+            self._dstate[0].fill_(float(self.n_steps))
+
+    def refresh_device_state(self, scheduler=None):
+        """After loading optimizer / scheduler state: write the host counters into the device
+        state in place (graph mode reads the lr schedule position from there)."""
+        if getattr(self, "_dstate", None) is None:
+            return
+        last = float(scheduler.last_epoch) if scheduler is not None else 0.0
+        self._dstate.copy_(torch.tensor([float(self.n_steps), last], dtype=torch.float64))

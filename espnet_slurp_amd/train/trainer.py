@@ -62,6 +62,12 @@ class Trainer:
         self._flag_event = torch.cuda.Event() if cuda else None
         self._pending = False
 
+    @staticmethod
+    def resume(checkpoint, model, reporter, optimizers, schedulers, scaler=None, ngpu: int = 0):
+        """Trainer.resume (trainer.py:124-151): see train/checkpoint.resume."""
+        from .checkpoint import resume
+        resume(checkpoint, model, reporter, optimizers, schedulers, scaler, ngpu)
+
     def train_one_step(self, batch: Dict[str, torch.Tensor], check_finite: bool = True) -> Dict[str, torch.Tensor]:
         """One iteration of train_one_epoch's loop body; returns device-side stats."""
         if self.cuda_graph and self.options.accum_grad == 1:

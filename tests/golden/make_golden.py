@@ -339,10 +339,95 @@ def frontend_fixture():
     print("frontend", tuple(spec.shape), tuple(feats.shape))
 
 
+def checkpoint_fixture():
+    """Checkpoint interop.  checkpoint_ref.pth is what the reference's
+    Trainer writes after an epoch (trainer.py:340-352): a tiny Conformer after two steps of the
+    reference's own clip + Adam + WarmupLR, and a Reporter holding one epoch of train / valid
+    stats.  checkpoint_ref_meta.json: the parameter names in optimizer order and the values
+    the tests check.  The reverse direction is checked here (the reference cannot be imported
+    by the tests): our resume() of that file followed by our save_checkpoint() is loaded back
+    by the reference's own Trainer.resume into fresh reference objects, and every tensor,
+    the optimizer / scheduler state and the reporter must come back identical."""
+    import json
+    import tempfile
+
+    from espnet2.train.reporter import Reporter
+    from espnet2.train.trainer import Trainer as RefTrainer
+
+    cfg = small_cfg("latest", D=16, blocks=1, V=12)
+    model = build_reference(cfg)
+    load_params(model, cfg, 7)
+    model.train()
+    opt = torch.optim.Adam(model.parameters(), lr=0.002, betas=(0.9, 0.98), eps=1e-9, weight_decay=1e-6)
+    sch = WarmupLR(opt, warmup_steps=10)
+    rep = Reporter()
+    rep.set_epoch(1)
+    with rep.observe("train") as sub:
+        for step in range(2):
+            speech, slen, text, tlen = O.synthetic_batch(2, 48, 80, cfg.vocab_size, [48, 40], [4, 3], 200 + step)
+            loss, stats, weight = model(speech, slen, text, tlen)
+            loss.backward()
+            torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=5.0)
+            opt.step()
+            sch.step()
+            opt.zero_grad()
+            sub.register({k: v for k, v in stats.items() if v is not None}, weight)
+            sub.next()
+    with rep.observe("valid") as sub:
+        sub.register({"acc": 0.25, "loss": 3.5})
+        sub.next()
+    ckpt = {"model": model.state_dict(), "reporter": rep.state_dict(), "optimizers": [opt.state_dict()],
+            "schedulers": [sch.state_dict()], "scaler": None}
+    path = os.path.join(HERE, "checkpoint_ref.pth")
+    torch.save(ckpt, path)
+    names = [n for n, _ in model.named_parameters()]
+    meta = {"param_names": names, "cfg": {"D": 16, "blocks": 1, "V": 12}, "lr": opt.param_groups[0]["lr"],
+            "last_epoch": sch.last_epoch, "adam_step": float(opt.state_dict()["state"][0]["step"]),
+            "train_loss": float(rep.get_value("train", "loss")), "valid_acc": float(rep.get_value("valid", "acc"))}
+    with open(os.path.join(HERE, "checkpoint_ref_meta.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+
+    # reverse direction: ours -> reference
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from tests.helpers import build_model
+    from espnet_slurp_amd.optimizers.fused_adam import FusedAdam
+    from espnet_slurp_amd.schedulers.warmup_lr import WarmupLR as OurWarmupLR
+    from espnet_slurp_amd.train import checkpoint as CK
+    from espnet_slurp_amd.train.reporter import Reporter as OurReporter
+    ours = build_model(cfg, torch.device("cpu"))
+    oopt = FusedAdam(ours.parameters(), ours.flat, lr=0.002, betas=(0.9, 0.98), eps=1e-9, weight_decay=1e-6)
+    osch = OurWarmupLR(oopt, warmup_steps=10)
+    orep = OurReporter()
+    CK.resume(path, ours, orep, [oopt], [osch], None, ngpu=0)
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "checkpoint.pth")
+        CK.save_checkpoint(out, ours, orep, [oopt], [osch])
+        m2 = build_reference(cfg)
+        o2 = torch.optim.Adam(m2.parameters(), lr=0.1)
+        s2 = WarmupLR(o2, warmup_steps=99)
+        r2 = Reporter()
+        # torch >= 2.6 loads weights_only by default: the reference's own resume needs the
+        # reporter's timedelta / numpy stat types allow-listed even for its own checkpoints
+        with torch.serialization.safe_globals(CK._safe_globals()):
+            RefTrainer.resume(out, m2, r2, [o2], [s2], None, ngpu=0)
+    for k, v in model.state_dict().items():
+        assert torch.equal(v, m2.state_dict()[k]), k
+    a, b = opt.state_dict(), o2.state_dict()
+    assert a["param_groups"] == b["param_groups"], (a["param_groups"], b["param_groups"])
+    for i in a["state"]:
+        for k in ("step", "exp_avg", "exp_avg_sq"):
+            assert torch.equal(a["state"][i][k], b["state"][i][k]), (i, k)
+    assert sch.state_dict() == s2.state_dict(), (sch.state_dict(), s2.state_dict())
+    assert rep.state_dict() == r2.state_dict()
+    print("checkpoint: ref -> ours -> ref round trip identical;", os.path.getsize(path), "bytes")
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["ctc", "align", "specaug", "small", "c1", "train", "full", "frontend"]
+    which = sys.argv[1:] or ["ctc", "align", "specaug", "small", "c1", "train", "full", "frontend", "checkpoint"]
     if "frontend" in which:
         frontend_fixture()
+    if "checkpoint" in which:
+        checkpoint_fixture()
     if "ctc" in which:
         ctc_fixture()
     if "align" in which:
