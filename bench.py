@@ -28,6 +28,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: bf16 dense MFMA (no sparsity)
+# BASELINE.json configs by name: (d, heads, ff, encoder blocks, bf16 GEMMs)
+PRESETS = {"c2": (256, 4, 1024, 12, False), "c4": (512, 8, 2048, 17, False), "c5": (512, 8, 2048, 12, True)}
 HBM_PEAK_GBS = 8000.0
 
 
@@ -119,7 +122,8 @@ def cpu_baseline(args):
         times.append(time.perf_counter() - t0)
     t = sum(times[1:]) / len(times[1:])
     return {"value": round(B / t, 4), "unit": "utt/s", "cores": n, "kind": "port",
-            "sample": f"oracle/espnet_cpu.py C2 step (fwd+bwd+clip+Adam), B=4 x 1500 frames, fp32, "
+            "sample": f"oracle/espnet_cpu.py {workload_name(args).split()[0]}-shape step (fwd+bwd+clip+Adam), "
+                      f"d={args.d} {args.layers}L, B=4 x 1500 frames, fp32, "
                       f"1 warmup + 3 timed steps, {t:.2f} s/step on {n} threads"}
 
 
@@ -130,7 +134,8 @@ def workload_name(args) -> str:
     if (args.d, args.heads, args.ff, args.layers) == (512, 8, 2048, 17):
         return "C4-shape LibriSpeech Conformer-large (fp32)"
     if (args.d, args.heads, args.ff, args.layers) == (512, 8, 2048, 12):
-        return "C5-shape SLURP-entity Conformer (fp32)"
+        return ("C5 SLURP-entity Conformer + SpecAug, bf16 MFMA (fp32 master weights)" if args.amp
+                else "C5-shape SLURP-entity Conformer (fp32)")
     return "custom Conformer"
 
 
@@ -174,7 +179,13 @@ def main():
     ap.add_argument("--rel-pos", default="latest", choices=["latest", "legacy"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch kernel by kernel instead of replaying a HIP graph")
+    ap.add_argument("--amp", action="store_true", help="bf16 GEMM operands, fp32 accumulate (TrainerOptions.use_amp)")
+    ap.add_argument("--config", choices=sorted(PRESETS), default=None,
+                    help="BASELINE.json config preset (overrides --d/--heads/--ff/--layers; c5 implies --amp)")
     args = ap.parse_args()
+    if args.config:
+        args.d, args.heads, args.ff, args.layers, amp = PRESETS[args.config]
+        args.amp = args.amp or amp
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -194,7 +205,7 @@ def main():
     model.train()
     opt = FusedAdam(model.parameters(), model.flat, lr=2e-4)
     sched = WarmupLR(opt, warmup_steps=25000)
-    trainer = Trainer(model, opt, sched, TrainerOptions(grad_clip=5.0), distributed=world > 1,
+    trainer = Trainer(model, opt, sched, TrainerOptions(grad_clip=5.0, use_amp=args.amp), distributed=world > 1,
                       cuda_graph=not args.eager)
     batch = synthetic_batch(args.batch, args.vocab, rank, device)
 
@@ -217,7 +228,7 @@ def main():
     if not args.eager:
         # the graph's kernels cannot be bracketed one by one: time the same GEMM launches (same
         # kernels, shapes and inputs) in one eager step right after the timed region
-        eager = Trainer(model, opt, sched, TrainerOptions(grad_clip=5.0), distributed=world > 1)
+        eager = Trainer(model, opt, sched, TrainerOptions(grad_clip=5.0, use_amp=args.amp), distributed=world > 1)
         K.profile_gemm_start()
         eager.train_one_step(batch)
         eager.resolve_pending()
@@ -233,6 +244,7 @@ def main():
         fwd, train = conformer_flops_per_utt(args.d, args.heads, args.ff, args.layers, 2048, 6, args.vocab)
         value = world * args.batch * args.steps / elapsed
         achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
+        peak = BF16_MFMA_PEAK_TFLOPS if args.amp else FP32_MFMA_PEAK_TFLOPS
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args)
@@ -247,25 +259,26 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "bf16-mfma/f32-accumulate" if args.amp else "f32",
             "data": "synthetic (N(0,1) fbank, random tokens U[20,40], random-init weights)",
             "launch": "eager" if args.eager else "hip_graph",
             "config": {"workload": f"{workload_name(args)} d={args.d} H={args.heads} FF={args.ff} "
                                    f"{args.layers}L enc / 6L dec, V={args.vocab}, rel_pos={args.rel_pos}, "
                                    "ctc 0.3, lsm 0.1, dropout 0.1, SpecAug on",
                        "global_batch": world * args.batch, "seq_len": 1500, "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-                         "traffic": traffic.get("hbm_bytes_per_launch"),
-                         "traffic_source": traffic.get("source"),
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
+                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                         "traffic": None if args.amp else traffic.get("hbm_bytes_per_launch"),
+                         "traffic_source": None if args.amp else traffic.get("source"),
                          "algorithmic_bytes_per_launch": round(gemm_algorithmic_bytes(gemm_shapes) / max(1, gemm_launches)),
-                         "kernel": "gemm_glds_kernel family (all MFMA GEMM launches of one step, HIP events"
+                         "kernel": ("gemm_glds_kernel<BF16> (bf16 MFMA)" if args.amp else "gemm_glds_kernel")
+                                   + " family (all MFMA GEMM launches of one step, HIP events"
                                    + (" in the timed region)" if args.eager else " on an eager replay of the step)"),
                          "launches": gemm_launches,
                          "avg_launch_us": round(1e3 * gemm_ms / max(1, gemm_launches), 2)},
             "step_roofline": {"train_gflop_per_utt": round(train / 1e9, 2),
                               "achieved_tflops": round(value / world * train / 1e12, 2),
-                              "frac_of_fp32_mfma_peak": round(value / world * train / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)},
+                              "frac_of_mfma_peak": round(value / world * train / 1e12 / peak, 4)},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

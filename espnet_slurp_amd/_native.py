@@ -24,6 +24,8 @@ SIGNATURES = {
     "esp_abi_version": [],
     "esp_gemm_f32": [I, I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, L, P, F, F, P, I, P, F, U64, I, P, P,
                      P, P, P, L, P],
+    "esp_set_gemm_compute": [I],
+    "esp_get_gemm_compute": [],
     "esp_act_bwd": [P, P, P, L, I, F, U64, L, P],
     "esp_scale_dropout": [P, P, L, F, F, U64, P, F, P],
     "esp_scale_by_dev": [P, L, P, P],
@@ -70,8 +72,9 @@ SIGNATURES = {
     "esp_argmax": [P, P, L, I, P],
     "esp_ctc_forced_align": [P, I, I, P, I, I, P, P, P],
 }
-_RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I}
-ABI_VERSION = 11  # bumped whenever a signature in include/espnet_mi355.h changes
+_RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I, "esp_set_gemm_compute": I,
+             "esp_get_gemm_compute": I}
+ABI_VERSION = 12  # bumped whenever a signature in include/espnet_mi355.h changes
 
 _lib = None
 

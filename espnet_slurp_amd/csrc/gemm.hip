@@ -76,6 +76,7 @@ struct GemmArgs {
   int batch;
   int splits, kchunk;  // split-K: blockIdx.z = z*splits + split; partials -> work
   float* work;
+  int bf16;  // bf16-input MFMA kernel (esp_set_gemm_compute(1)); fp32 operands rounded in LDS staging
   int bnt;  // LDS-DMA kernel tile width (128, or 64 for narrow / mid-size grids); 0 = fallback kernel
   int bwd_act;       // != 0: backward epilogue  v = drop'(acc) * act'(pre)  (act code, dropout regenerated)
   const float* pre;  // pre-activation (same layout as C) for bwd_act
@@ -624,6 +625,153 @@ __global__ __launch_bounds__(NT, VARIANT == 3 ? 4 : 2) void gemm_f32_kernel(Gemm
   epilogue<2, 2>(g, W, z, m0 + wm * 64, n0 + wn * 64, h, l32, acc);
 }
 
+// ============================================================================ bf16 kernel
+// bf16-input MFMA GEMM (v_mfma_f32_32x32x16_bf16, fp32 accumulate) for the reduced-precision
+// training mode (bf16 GEMM inputs, fp32 master weights / activations in HBM).
+// Register-staged FALLBACK for operands the LDS-DMA kernel cannot take (unaligned pitches);
+// the production bf16 path is gemm_glds_kernel<..., BF16 = true> below.
+// Operands stay fp32 in HBM; each 128 x 32 slab is loaded as float4, rounded to bf16 (RNE,
+// v_cvt_pk_bf16_f32) and written to LDS as [row][k] with a 40-element (80 B) row pitch, so the
+// per-lane fragment of a 32x32x16 step (8 consecutive k of one row, k = 16s + 8h + j) is one
+// conflict-free ds_read_b128 (row pitch 20 dwords: 16 rows cover the 64 banks once).
+//   KC operands: the thread's float4 is 4 consecutive k of one row -> one ds_write_b64.
+//   RC operands: the thread loads 4 float4 (k .. k+3) x (rows r .. r+3) and transposes in
+//                registers -> four ds_write_b64 (row r+i, k .. k+3).
+// The next slab's global loads fly during this slab's MFMAs (single LDS buffer, two barriers
+// per slab).  Epilogues, split-K partials and the row-sum side pass are those of the fp32 path.
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+constexpr int BF_KS = 32 + 8;  // LDS row pitch in bf16 elements
+
+template <int MODE>
+__device__ __forceinline__ float4 ld4_rc(const Operand& op, const float* base, int rows, int K, int gk, int gr) {
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (gk >= K) return v;
+  if constexpr (MODE == RC) {
+    const float* p = base + (long)gk * op.ld + gr;
+    if (op.vec && gr + 3 < rows) return *reinterpret_cast<const float4*>(p);
+    if (gr + 0 < rows) v.x = p[0];
+    if (gr + 1 < rows) v.y = p[1];
+    if (gr + 2 < rows) v.z = p[2];
+    if (gr + 3 < rows) v.w = p[3];
+  } else {  // I2C_RC
+    if (gr + 3 < rows) return *reinterpret_cast<const float4*>(i2c_ptr(base, op.ic, gk, gr));
+    if (gr + 0 < rows) v.x = *i2c_ptr(base, op.ic, gk, gr + 0);
+    if (gr + 1 < rows) v.y = *i2c_ptr(base, op.ic, gk, gr + 1);
+    if (gr + 2 < rows) v.z = *i2c_ptr(base, op.ic, gk, gr + 2);
+  }
+  return v;
+}
+
+// this thread's 16 elements of a (128 rows x 32 k) slab
+template <int MODE>
+__device__ __forceinline__ void load_slab_bf(const Operand& op, const float* base, int rows, int K, int row0,
+                                             int k0, float4 (&reg)[4]) {
+  if constexpr (MODE == KC || MODE == I2C_KC) {
+    load_slab<MODE, 32>(op, base, rows, K, row0, k0, reg);  // reg[it]: row (t + 256 it) / 8, k 4 * (t % 8)
+  } else {
+    const int rq = (threadIdx.x & 31) * 4, kq = (threadIdx.x >> 5) * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) reg[j] = ld4_rc<MODE>(op, base, rows, K, k0 + kq + j, row0 + rq);
+  }
+}
+
+__device__ __forceinline__ bf16x4 to_bf4(float a, float b, float c, float d) {
+  bf16x4 r;
+  r[0] = (__bf16)a; r[1] = (__bf16)b; r[2] = (__bf16)c; r[3] = (__bf16)d;
+  return r;
+}
+
+template <int MODE>
+__device__ __forceinline__ void store_slab_bf(__bf16* lds, const float4 (&reg)[4]) {
+  if constexpr (MODE == KC || MODE == I2C_KC) {
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int idx = threadIdx.x + it * NT;
+      const int r = idx >> 3, kq = (idx & 7) * 4;
+      *reinterpret_cast<bf16x4*>(lds + r * BF_KS + kq) = to_bf4(reg[it].x, reg[it].y, reg[it].z, reg[it].w);
+    }
+  } else {
+    const int rq = (threadIdx.x & 31) * 4, kq = (threadIdx.x >> 5) * 4;
+    *reinterpret_cast<bf16x4*>(lds + (rq + 0) * BF_KS + kq) = to_bf4(reg[0].x, reg[1].x, reg[2].x, reg[3].x);
+    *reinterpret_cast<bf16x4*>(lds + (rq + 1) * BF_KS + kq) = to_bf4(reg[0].y, reg[1].y, reg[2].y, reg[3].y);
+    *reinterpret_cast<bf16x4*>(lds + (rq + 2) * BF_KS + kq) = to_bf4(reg[0].z, reg[1].z, reg[2].z, reg[3].z);
+    *reinterpret_cast<bf16x4*>(lds + (rq + 3) * BF_KS + kq) = to_bf4(reg[0].w, reg[1].w, reg[2].w, reg[3].w);
+  }
+}
+
+template <int MA, int MB>
+__global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) __bf16 lds[(BM + BN) * BF_KS];
+  __bf16* As = lds;
+  __bf16* Bs = lds + BM * BF_KS;
+
+  const int split = blockIdx.z % g.splits;
+  const int z = blockIdx.z / g.splits;
+  const int z1 = z / g.nb2, z2 = z - z1 * g.nb2;
+  const int kbeg = split * g.kchunk;
+  const int kend = min(g.K, kbeg + g.kchunk);
+  const float* Ab = g.a.p + z1 * g.a.s1 + z2 * g.a.s2;
+  const float* Bb = g.b.p + z1 * g.b.s1 + z2 * g.b.s2;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int h = lane >> 5, l32 = lane & 31;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  float4 ra[4], rb[4];
+  const int nk = kend > kbeg ? (kend - kbeg + 31) / 32 : 0;
+  if (nk > 0) {
+    load_slab_bf<MA>(g.a, Ab, g.M, kend, m0, kbeg, ra);
+    load_slab_bf<MB>(g.b, Bb, g.N, kend, n0, kbeg, rb);
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt > 0) __syncthreads();  // previous slab fully read
+    store_slab_bf<MA>(As, ra);
+    store_slab_bf<MB>(Bs, rb);
+    __syncthreads();
+    if (kt + 1 < nk) {
+      load_slab_bf<MA>(g.a, Ab, g.M, kend, m0, kbeg + (kt + 1) * 32, ra);
+      load_slab_bf<MB>(g.b, Bb, g.N, kend, n0, kbeg + (kt + 1) * 32, rb);
+    }
+    bf16x8 af[2][2], bf[2][2];  // [tile][k-step]
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        af[t][s] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + t * 32 + l32) * BF_KS + 16 * s + 8 * h);
+        bf[t][s] = *reinterpret_cast<const bf16x8*>(Bs + (wn * 64 + t * 32 + l32) * BF_KS + 16 * s + 8 * h);
+      }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+  }
+
+  float* W = g.splits > 1 ? g.work + ((long)split * g.batch + z) * (long)g.M * g.N : nullptr;
+  if (g.wide) {
+    if (W) store_partials_wide<2, 2>(g, W, m0 + wm * 64, n0 + wn * 64, lane, acc);
+    else if (g.bwd_act) store_tiles_wide<EPI_BWD, 2, 2>(g, z, m0 + wm * 64, n0 + wn * 64, lane, acc);
+    else if (g.bias || g.aux || g.act || g.drop_thresh)
+      store_tiles_wide<EPI_FWD, 2, 2>(g, z, m0 + wm * 64, n0 + wn * 64, lane, acc);
+    else store_tiles_wide<EPI_PLAIN, 2, 2>(g, z, m0 + wm * 64, n0 + wn * 64, lane, acc);
+  } else {
+    epilogue<2, 2>(g, W, z, m0 + wm * 64, n0 + wn * 64, h, l32, acc);
+  }
+}
+
 // ============================================================================ glds kernel
 // The production path.  Global->LDS staging with global_load_lds_dwordx4 (LDS-DMA: no VGPR
 // round trip, asynchronous until its vmcnt), two LDS buffers, raw s_barrier with explicit
@@ -834,7 +982,13 @@ constexpr int glds_occupancy() { return (BNT == 64 && EPI == 0) ? 3 : 2; }
 // first slab of the next tile streams in during the last slab of the current one, and the
 // current tile's epilogue stores drain while the next tile's MFMAs run (on this and the other
 // resident blocks' waves).  With G = #tiles every block runs one tile (the classic launch).
-template <int MA, int MB, int BNT, bool RS, int EPI>
+//
+// BF16 = true (esp_set_gemm_compute(1)): the same fp32 LDS-DMA pipeline, but each lane's 16
+// staged k-values per tile row are rounded to bf16 in registers (v_cvt_pk_bf16_f32) and fed to
+// two v_mfma_f32_32x32x16_bf16 per (i, j) tile pair instead of sixteen 32x32x2 f32 MFMAs: k-step
+// 0 takes the lane's values s = 0..7 (k = 16h + s), step 1 s = 8..15, identically for A and B,
+// so the two steps cover the slab's 32 k once.  The fused row sums stay fp32.
+template <int MA, int MB, int BNT, bool RS, int EPI, bool BF16 = false>
 __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_kernel(GemmArgs g, GldsArgs x) {
   constexpr int WN = BNT / 64, WM = 4 / WN, TM = BM / (WM * 32), TN = 2;
   constexpr int A_SZ = BM * GL_BK, B_SZ = BNT * GL_BK, BUF = A_SZ + B_SZ;
@@ -895,13 +1049,35 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_ke
       for (int i = 0; i < TM; ++i) frag16<MA, BM>(cur, wm * TM * 32 + i * 32 + l32, h, af[i]);
 #pragma unroll
       for (int j = 0; j < TN; ++j) frag16<MB, BNT>(cur + A_SZ, wn * 64 + j * 32 + l32, h, bf[j]);
+      if constexpr (BF16) {
+        bf16x8 ah[TM][2], bh[TN][2];
 #pragma unroll
-      for (int s = 0; s < 16; ++s)
+        for (int hs = 0; hs < 2; ++hs) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) ah[i][hs][e] = (__bf16)af[i][8 * hs + e];
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bh[j][hs][e] = (__bf16)bf[j][8 * hs + e];
+        }
+#pragma unroll
+        for (int hs = 0; hs < 2; ++hs)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][hs], bh[j][hs], acc[i][j], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
+      }
       if constexpr (RS) {
         if (do_rs) {  // after the MFMAs were issued: the adds ride in their shadow
 #pragma unroll
@@ -1104,6 +1280,8 @@ long persist_blocks(int per_cu) {
   return g_persist ? (long)per_cu * g_persist : (1L << 40);
 }
 
+int g_compute = 0;  // 0: fp32 MFMA (exact f32 fma chain), 1: bf16-input MFMA with fp32 accumulate
+
 int g_variant = -1;
 int variant() {
   if (g_variant < 0) {
@@ -1116,8 +1294,8 @@ int variant() {
 // Launch the LDS-DMA kernel with the epilogue kind compiled in (each kind is its own kernel,
 // so the plain GEMMs carry none of the fused epilogues' registers).  Returns false when the
 // mode pair has no instantiation of the needed kind (the caller falls back).
-template <int MA, int MB, int BNT>
-bool launch_glds(const GemmArgs& g, int batch, hipStream_t st, const GldsArgs* tconv = nullptr) {
+template <int MA, int MB, int BNT, bool BF>
+bool launch_glds_t(const GemmArgs& g, int batch, hipStream_t st, const GldsArgs* tconv) {
   constexpr bool can_rs = MA == RC;
   constexpr bool can_fwd = (MA == KC && (MB == KC || MB == RC)) || (MA == I2C_KC && MB == KC);
   constexpr bool can_bwd = (MA == KC || MA == I2CT_KC) && MB == RC;
@@ -1145,20 +1323,25 @@ bool launch_glds(const GemmArgs& g, int batch, hipStream_t st, const GldsArgs* t
   }
   auto grid = [&](int per_cu) { return dim3((unsigned)std::min<long>(x.ntiles, persist_blocks(per_cu))); };
   if (can_rs && g.rowsum)
-    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, can_rs, EPI_PLAIN>), grid(glds_occupancy<BNT, EPI_PLAIN>()),
+    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, can_rs, EPI_PLAIN, BF>), grid(glds_occupancy<BNT, EPI_PLAIN>()),
                        dim3(NT), 0, st, g, x);
   else if (kind == EPI_PLAIN)
-    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_PLAIN>), grid(glds_occupancy<BNT, EPI_PLAIN>()),
+    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_PLAIN, BF>), grid(glds_occupancy<BNT, EPI_PLAIN>()),
                        dim3(NT), 0, st, g, x);
   else if (kind == EPI_FWD) {
     if constexpr (can_fwd)
-      hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_FWD>), grid(glds_occupancy<BNT, EPI_FWD>()),
+      hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_FWD, BF>), grid(glds_occupancy<BNT, EPI_FWD>()),
                          dim3(NT), 0, st, g, x);
   } else if constexpr (can_bwd) {
-    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_BWD>), grid(glds_occupancy<BNT, EPI_BWD>()),
+    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_BWD, BF>), grid(glds_occupancy<BNT, EPI_BWD>()),
                        dim3(NT), 0, st, g, x);
   }
   return true;
+}
+template <int MA, int MB, int BNT>
+bool launch_glds(const GemmArgs& g, int batch, hipStream_t st, const GldsArgs* tconv = nullptr) {
+  if (g.bf16) return launch_glds_t<MA, MB, BNT, true>(g, batch, st, tconv);
+  return launch_glds_t<MA, MB, BNT, false>(g, batch, st, tconv);
 }
 
 template <int MA, int MB>
@@ -1173,7 +1356,8 @@ int launch(const GemmArgs& g0, int batch, hipStream_t st) {
       hipLaunchKernelGGL(rowsum_rc_kernel, dim3((g.M + 255) / 256), dim3(256), 0, st, g.a.p, g.a.ld, g.M, g.K,
                          g.rowsum);
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, batch * g.splits);
-    if (variant() == 0) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 0>), grid, dim3(NT), 0, st, g);
+    if (g.bf16) hipLaunchKernelGGL((gemm_bf16_kernel<MA, MB>), grid, dim3(NT), 0, st, g);
+    else if (variant() == 0) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 0>), grid, dim3(NT), 0, st, g);
     else if (variant() == 2) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 2>), grid, dim3(NT), 0, st, g);
     else if (variant() == 3) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 3>), grid, dim3(NT), 0, st, g);
     else hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 1>), grid, dim3(NT), 0, st, g);
@@ -1208,6 +1392,14 @@ bool glds_ok(int mode, const void* p, long ld, long s1, long s2, int rows, int K
 }  // namespace
 
 // C-ABI: see include/espnet_mi355.h for the contract.
+ESP_API int esp_set_gemm_compute(int dtype) {
+  ESP_ARG_CHECK(dtype == 0 || dtype == 1, "esp_set_gemm_compute: dtype must be 0 (fp32) or 1 (bf16), got %d", dtype);
+  const int prev = g_compute;
+  g_compute = dtype;
+  return prev;
+}
+ESP_API int esp_get_gemm_compute(void) { return g_compute; }
+
 ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2,
                          const float* A, long lda, long sa1, long sa2,
                          const float* B, long ldb, long sb1, long sb2,
@@ -1269,6 +1461,7 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
   const long target = 2 * 256;
   auto ntiles = [&](int bn) { return (long)((N + bn - 1) / bn) * ((M + BM - 1) / BM) * batch; };
   g.bnt = 0;
+  g.bf16 = g_compute == 1;
   if (variant() == 4 && g.a.glds && g.b.glds && K > 0) {
     // per-CU time model: ceil(tiles / CUs) tiles of bn/64 units each, x1.3 when the grid
     // leaves CUs with a single resident block (one wave per SIMD); ties keep 128 (intensity)

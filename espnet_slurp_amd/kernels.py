@@ -282,6 +282,39 @@ def opt_advance(state_f64, clip3):
     _native.call("esp_opt_advance", _p(state_f64), _p(clip3), _st())
 
 
+GEMM_FP32, GEMM_BF16 = 0, 1
+
+
+def set_gemm_compute(dtype) -> int:
+    """Select the MFMA input type of every later GEMM launch: "fp32"/0 (default, exact f32
+    fma chain) or "bf16"/1 (operands rounded to bf16 in LDS staging, fp32 accumulate and
+    outputs).  Process-wide; returns the previous setting (esp_set_gemm_compute)."""
+    code = {"fp32": GEMM_FP32, "float32": GEMM_FP32, "bf16": GEMM_BF16, "bfloat16": GEMM_BF16}.get(dtype, dtype)
+    lib = _native.load()
+    prev = lib.esp_set_gemm_compute(int(code))
+    if prev < 0:
+        raise _native.NativeError(f"esp_set_gemm_compute failed: {lib.esp_last_error().decode()}")
+    return prev
+
+
+def get_gemm_compute() -> int:
+    return _native.load().esp_get_gemm_compute()
+
+
+class gemm_compute:
+    """Context manager: GEMMs inside the block run with the given input type."""
+
+    def __init__(self, dtype):
+        self.dtype = dtype
+
+    def __enter__(self):
+        self.prev = set_gemm_compute(self.dtype)
+        return self
+
+    def __exit__(self, *exc):
+        set_gemm_compute(self.prev)
+
+
 def set_rng_key(key_u64: Optional[torch.Tensor]):
     """Route every dropout kernel's seed through *key (device int64 tensor) or switch it off."""
     _native.call("esp_set_rng_key", _p(key_u64))

@@ -28,6 +28,11 @@ class TrainerOptions:
     accum_grad: int = 1
     no_forward_run: bool = False
     log_interval: Optional[int] = None
+    # reduced-precision training (trainer.py:181-195,554 offer fp16 autocast + GradScaler under
+    # `use_amp`): here every GEMM takes bf16 operands with fp32 accumulate (esp_set_gemm_compute);
+    # parameters, gradients, optimizer state and all non-GEMM kernels stay fp32.  bf16 has the
+    # fp32 exponent range, so no loss scaler is needed.  SURVEY §8(d) C5.
+    use_amp: bool = False
 
 
 class _GraphEntry:
@@ -70,6 +75,10 @@ class Trainer:
 
     def train_one_step(self, batch: Dict[str, torch.Tensor], check_finite: bool = True) -> Dict[str, torch.Tensor]:
         """One iteration of train_one_epoch's loop body; returns device-side stats."""
+        with K.gemm_compute("bf16" if self.options.use_amp else "fp32"):
+            return self._train_one_step(batch, check_finite)
+
+    def _train_one_step(self, batch, check_finite):
         if self.cuda_graph and self.options.accum_grad == 1:
             return self._graph_step(batch)
         opts = self.options

@@ -47,6 +47,14 @@ int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2
                  int bwd_act, const float* pre, float* rowsum,
                  const int* im2col_a, const int* im2col_b, float* work, long work_bytes,
                  void* stream);
+/* GEMM compute type for every later esp_gemm_f32 launch (process-wide host state, read at
+ * launch time, so a captured HIP graph keeps the kernels of its capture): 0 = fp32 MFMA
+ * (default; the reference's train_dtype float32), 1 = bf16 operands (fp32 values rounded to
+ * nearest-even while staged into LDS) with fp32 accumulate and fp32 epilogue / outputs.
+ * Mode 1 is the reduced-precision training path of SURVEY §8(d) C5; the reference's nearest
+ * knob is `use_amp` (fp16 autocast, trainer.py:181-195,554).  Returns the previous value. */
+int esp_set_gemm_compute(int dtype);
+int esp_get_gemm_compute(void);
 
 /* ---- element-wise (positionwise_feed_forward.py:32, conformer/swish.py:13-18, dropout) */
 int esp_act_bwd(const float* dy, const float* h, float* dx, long n, int act, float drop_p,

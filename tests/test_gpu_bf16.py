@@ -1,0 +1,145 @@
+"""bf16-input MFMA GEMM path (esp_set_gemm_compute(1); TrainerOptions.use_amp).
+
+Kernel level: with operands rounded to bf16 (round-to-nearest-even, as the kernel's LDS staging
+does) every product is exact in fp32, so the kernel must match an fp64 GEMM of the ROUNDED
+operands up to fp32 accumulation order: |err| <= 4e-6 * sqrt(K) * max|a||b| scale.  Against the
+unrounded fp32 GEMM the error is the bf16 input rounding (relative 2^-8 per operand).
+Model level: the reference offers only fp16 autocast here (trainer.py:181-195), so parity of the
+bf16 step is statistical: the bf16 loss within 1 % of the fp32 loss of the same weights and
+batch, and the gradient direction (cosine) within 1e-3 of the fp32 gradient.
+"""
+import math
+
+import pytest
+import torch
+
+from espnet_slurp_amd import kernels as K
+from oracle import espnet_cpu as O
+from tests.helpers import build_model, load_seeded, small_cfg
+
+pytestmark = pytest.mark.gpu
+
+
+def _r(*shape, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g)
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).double()
+
+
+def _ref(A, B, ma, mb):
+    a = _bf(A) if ma == K.KC else _bf(A).t()
+    b = _bf(B).t() if mb == K.KC else _bf(B)
+    return a @ b
+
+
+@pytest.fixture
+def bf16_mode():
+    prev = K.set_gemm_compute("bf16")
+    yield
+    K.set_gemm_compute(prev)
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 1), (37, 53, 19), (128, 128, 32), (300, 260, 129), (1000, 96, 512),
+                                   (130, 7, 3), (64, 33, 3000), (384, 256, 2048)])
+@pytest.mark.parametrize("modes", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_bf16_gemm_modes(dev, bf16_mode, shape, modes):
+    M, N, Kk = shape
+    ma, mb = modes
+    A = _r(M, Kk, seed=1) if ma == K.KC else _r(Kk, M, seed=1)
+    B = _r(N, Kk, seed=2) if mb == K.KC else _r(Kk, N, seed=2)
+    Ad, Bd = A.to(dev), B.to(dev)
+    C = torch.empty(M, N, device=dev)
+    K.gemm(M, N, Kk, Ad, Bd, C, mode_a=ma, lda=Ad.stride(0), mode_b=mb, ldb=Bd.stride(0), ldc=N)
+    torch.cuda.synchronize()
+    ref = _ref(A, B, ma, mb)
+    err = (C.cpu().double() - ref).abs().max().item()
+    assert err <= 4e-6 * max(1.0, math.sqrt(Kk)) * 4, err
+    # and it is NOT the fp32 GEMM (the mode switch took effect)
+    if Kk >= 19:
+        a = A.double() if ma == K.KC else A.double().t()
+        b = B.double().t() if mb == K.KC else B.double()
+        assert (C.cpu().double() - a @ b).abs().max().item() > 1e-4
+
+
+def test_bf16_gemm_epilogue_and_batched(dev, bf16_mode):
+    M, N, Kk = 257, 132, 96
+    X, W, b, R = _r(M, Kk, seed=3), _r(N, Kk, seed=4), _r(N, seed=5), _r(M, N, seed=6)
+    out = torch.empty(M, N, device=dev)
+    aux = torch.empty(M, N, device=dev)
+    K.linear_fwd(X.to(dev), W.to(dev), b.to(dev), out, act=K.ACT_SWISH, aux=aux, alpha=0.5, R=R.to(dev), beta=1.0)
+    pre = _bf(X) @ _bf(W).t() + b.double()
+    ref = 0.5 * pre * torch.sigmoid(pre) + R.double()
+    torch.cuda.synchronize()
+    assert (aux.cpu().double() - pre).abs().max() < 1e-4
+    assert (out.cpu().double() - ref).abs().max() < 1e-4
+    # batched (z = z1*nb2 + z2) attention-style product: (H*B) x (T x dk) @ (T x dk)^T
+    Z, T, dk = 6, 75, 64
+    q, k = _r(Z, T, dk, seed=7), _r(Z, T, dk, seed=8)
+    s = torch.empty(Z, T, T, device=dev)
+    qd, kd = q.to(dev), k.to(dev)
+    K.gemm(T, T, dk, qd, kd, s, mode_a=K.KC, lda=dk, mode_b=K.KC, ldb=dk, ldc=T, batch=Z, nb2=1,
+           sa=(T * dk, 0), sb=(T * dk, 0), sc=(T * T, 0))
+    torch.cuda.synchronize()
+    ref = torch.bmm(_bf(q), _bf(k).transpose(1, 2))
+    assert (s.cpu().double() - ref).abs().max() < 4e-6 * 8 * 4
+
+
+def test_gemm_compute_setter(dev):
+    prev = K.set_gemm_compute("fp32")
+    assert K.get_gemm_compute() == 0
+    with K.gemm_compute("bf16"):
+        assert K.get_gemm_compute() == 1
+    assert K.get_gemm_compute() == 0
+    with pytest.raises(RuntimeError):
+        K.set_gemm_compute(7)
+    K.set_gemm_compute(prev)
+
+
+def _loss_and_grad(dev, use_amp):
+    cfg = small_cfg("latest", D=128, blocks=2, V=64)
+    model = build_model(cfg, dev, dropout=0.0)
+    load_seeded(model, cfg, 5)
+    model.train()
+    speech, slen, text, tlen = O.synthetic_batch(3, 160, 80, 64, [160, 140, 120], [9, 7, 5], 3)
+    with K.gemm_compute("bf16" if use_amp else "fp32"):
+        loss, stats, _ = model(speech=speech.to(dev), speech_lengths=slen, text=text, text_lengths=tlen)
+        loss.backward()
+    torch.cuda.synchronize()
+    return loss.item(), model.flat.grad.detach().double().cpu().clone()
+
+
+def test_bf16_model_step_close_to_fp32(dev):
+    l32, g32 = _loss_and_grad(dev, False)
+    l16, g16 = _loss_and_grad(dev, True)
+    assert abs(l16 - l32) <= 1e-2 * abs(l32), (l16, l32)
+    cos = float((g16 @ g32) / (g16.norm() * g32.norm()))
+    assert cos > 0.999, cos
+    assert g16.norm() > 0 and torch.isfinite(g16).all()
+
+
+def test_bf16_trainer_graph_matches_eager(dev):
+    from espnet_slurp_amd.optimizers.fused_adam import FusedAdam
+    from espnet_slurp_amd.train.trainer import Trainer, TrainerOptions
+
+    def make(graph):
+        cfg = small_cfg("latest")
+        model = build_model(cfg, dev, dropout=0.0)
+        load_seeded(model, cfg, 11)
+        model.train()
+        opt = FusedAdam(model.parameters(), model.flat, lr=1e-3)
+        return Trainer(model, opt, None, TrainerOptions(grad_clip=5.0, use_amp=True), cuda_graph=graph), model
+
+    te, me = make(False)
+    tg, mg = make(True)
+    for _ in range(3):
+        speech, slen, text, tlen = O.synthetic_batch(3, 96, 80, 32, [96, 80, 71], [6, 5, 4], 12)
+        b = dict(speech=speech.to(dev), speech_lengths=slen, text=text, text_lengths=tlen)
+        le = te.train_one_step(dict(b, speech=b["speech"].clone(), text=b["text"].clone()))["loss"].item()
+        lg = tg.train_one_step(dict(b, speech=b["speech"].clone(), text=b["text"].clone()))["loss"].item()
+        assert abs(le - lg) <= 1e-6 * max(1.0, abs(le)), (le, lg)
+    assert K.get_gemm_compute() == 0  # the trainer restores the process-wide setting
+    torch.cuda.synchronize()
+    assert torch.allclose(me.flat.flat, mg.flat.flat, rtol=0, atol=1e-6)
