@@ -48,6 +48,7 @@ SIGNATURES = {
     "esp_dwconv1d": [P, P, P, P, I, I, I, I, I, P],
     "esp_dwconv1d_wgrad": [P, P, P, I, I, I, I, P, P],
     "esp_bn_swish_fwd": [P, P, P, P, P, P, P, P, F, F, I, I, P, P],
+    "esp_bn_swish_eval": [P, P, P, P, P, P, F, I, I, P, P, P],
     "esp_bn_swish_bwd": [P, P, P, P, P, P, P, P, P, I, I, P, P, P],
     "esp_heads_split": [P, L, I, I, I, I, I, P, P, P],
     "esp_add2d": [P, L, P, L, I, I, P],
@@ -71,10 +72,12 @@ SIGNATURES = {
     "esp_reduce_losses": [P, I, I, P, P, I, F, F, P, P],
     "esp_argmax": [P, P, L, I, P],
     "esp_ctc_forced_align": [P, I, I, P, I, I, P, P, P],
+    "esp_ctc_prefix_init": [P, I, I, I, P, P],
+    "esp_ctc_prefix_score": [P, I, I, P, P, I, P, I, I, I, I, P, P, P],
 }
 _RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I, "esp_set_gemm_compute": I,
              "esp_get_gemm_compute": I}
-ABI_VERSION = 12  # bumped whenever a signature in include/espnet_mi355.h changes
+ABI_VERSION = 13  # bumped whenever a signature in include/espnet_mi355.h changes
 
 _lib = None
 

@@ -412,8 +412,8 @@ class ConvolutionModule(nn.Module):
             K.bn_swish_fwd(y, bn.weight, bn.bias, s, mean, rstd, bn.running_mean, bn.running_var,
                            momentum=bn.momentum, eps=bn.eps)
             bn.num_batches_tracked.add_(1)
-        else:
-            raise NotImplementedError("eval-mode BatchNorm (running statistics) is not on the training hot path")
+        else:  # inference: running statistics (no backward is taken in eval mode)
+            K.bn_swish_eval(y, bn.weight, bn.bias, s, bn.running_mean, bn.running_var, mean, rstd, eps=bn.eps)
         out = empty(M, D, like=x2d)
         pr = p_res if training else 0.0
         so = seeds.next()

@@ -402,3 +402,84 @@ ESP_API int esp_ctc_forced_align(const float* lpz, int T, int V, const long long
   ESP_CHECK_LAUNCH("esp_ctc_forced_align");
   return 0;
 }
+
+// ============================================================================ CTC prefix scoring
+// Beam-search CTC prefix scorer (espnet/nets/ctc_prefix_score.py:279-359, CTCPrefixScore,
+// used through espnet/nets/scorers/ctc.py CTCPrefixScorer): for every running hypothesis g
+// (states r_prev = log r_t^n(g), log r_t^b(g), t < T) and each candidate label c, the forward
+// variables of h = g + c and the prefix probability log psi(h).  fp32 like the reference's
+// numpy path; logaddexp in numpy's form; logzero = -1e10.
+// One thread per (hypothesis, candidate): the recursion over t is serial, the (hyp, cand)
+// pairs are independent.  lp is one utterance's (T, V) log-softmax.
+namespace {
+constexpr float kLogZero = -10000000000.0f;
+__device__ __forceinline__ float logaddexpf_np(float x, float y) {
+  if (x == y) return x + 0.693147180559945309f;
+  const float d = x - y;
+  return d > 0.f ? x + log1pf(expf(-d)) : y + log1pf(expf(d));
+}
+__global__ void ctc_prefix_init_kernel(const float* __restrict__ lp, int T, int V, int blank, float* __restrict__ r) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  float acc = lp[blank];
+  r[0] = kLogZero;
+  r[1] = acc;
+  for (int t = 1; t < T; ++t) {
+    acc = acc + lp[(long)t * V + blank];
+    r[2 * t] = kLogZero;
+    r[2 * t + 1] = acc;
+  }
+}
+__global__ void ctc_prefix_score_kernel(const float* __restrict__ lp, int T, int V, const float* __restrict__ r_prev,
+                                        const long long* __restrict__ last, int out_len, const long long* __restrict__ cands,
+                                        int NH, int C, int blank, int eos, float* __restrict__ r_new,
+                                        float* __restrict__ log_psi) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= NH * C) return;
+  const int hy = idx / C;
+  const int c = (int)cands[idx];
+  const float* rp = r_prev + (long)hy * T * 2;
+  float* rn = r_new + (long)idx * T * 2;
+  const bool same_as_last = out_len > 0 && c == (int)last[hy];
+  for (int t = 0; t < T; ++t) {  // rows before the recursion start are never read downstream
+    rn[2 * t] = kLogZero;
+    rn[2 * t + 1] = kLogZero;
+  }
+  if (out_len == 0) rn[0] = lp[c];
+  const int start = out_len > 1 ? out_len : 1;
+  float rn0 = rn[2 * (start - 1)], rb0 = rn[2 * (start - 1) + 1];
+  float psi = rn0;
+  for (int t = start; t < T; ++t) {
+    const float phi = same_as_last ? rp[2 * (t - 1) + 1] : logaddexpf_np(rp[2 * (t - 1)], rp[2 * (t - 1) + 1]);
+    const float xc = lp[(long)t * V + c];
+    const float n1 = logaddexpf_np(rn0, phi) + xc;
+    const float b1 = logaddexpf_np(rn0, rb0) + lp[(long)t * V + blank];
+    psi = logaddexpf_np(psi, phi + xc);
+    rn[2 * t] = n1;
+    rn[2 * t + 1] = b1;
+    rn0 = n1;
+    rb0 = b1;
+  }
+  if (c == eos) psi = logaddexpf_np(rp[2 * (T - 1)], rp[2 * (T - 1) + 1]);
+  if (c == blank) psi = kLogZero;
+  log_psi[idx] = psi;
+}
+}  // namespace
+
+ESP_API int esp_ctc_prefix_init(const float* lp, int T, int V, int blank, float* r0, void* stream) {
+  ESP_ARG_CHECK(T >= 1 && V >= 1 && blank >= 0 && blank < V, "esp_ctc_prefix_init: bad sizes T=%d V=%d", T, V);
+  hipLaunchKernelGGL(ctc_prefix_init_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, lp, T, V, blank, r0);
+  ESP_CHECK_LAUNCH("esp_ctc_prefix_init");
+  return 0;
+}
+
+ESP_API int esp_ctc_prefix_score(const float* lp, int T, int V, const float* r_prev, const long long* last,
+                                 int out_len, const long long* cands, int NH, int C, int blank, int eos,
+                                 float* r_new, float* log_psi, void* stream) {
+  ESP_ARG_CHECK(T >= 1 && V >= 1 && NH >= 1 && C >= 1 && out_len >= 0 && out_len <= T,
+                "esp_ctc_prefix_score: bad sizes T=%d V=%d NH=%d C=%d out_len=%d", T, V, NH, C, out_len);
+  const int n = NH * C;
+  hipLaunchKernelGGL(ctc_prefix_score_kernel, dim3((n + 63) / 64), dim3(64), 0, (hipStream_t)stream, lp, T, V, r_prev,
+                     last, out_len, cands, NH, C, blank, eos, r_new, log_psi);
+  ESP_CHECK_LAUNCH("esp_ctc_prefix_score");
+  return 0;
+}

@@ -716,6 +716,28 @@ ESP_API int esp_bn_swish_fwd(const float* y, const float* gamma, const float* be
   return 0;
 }
 
+// eval mode (BatchNorm1d with track_running_stats, convolution.py:56-79 under model.eval()):
+// mean / rstd from the running statistics, then the same fused BN + Swish
+__global__ void bn_running_kernel(const float* __restrict__ rm, const float* __restrict__ rv, float eps, int D,
+                                  float* __restrict__ mean, float* __restrict__ rstd) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < D) {
+    mean[c] = rm[c];
+    rstd[c] = 1.0f / sqrtf(rv[c] + eps);
+  }
+}
+ESP_API int esp_bn_swish_eval(const float* y, const float* gamma, const float* beta, float* s, const float* run_mean,
+                              const float* run_var, float eps, int M, int D, float* mean, float* rstd, void* stream) {
+  ESP_ARG_CHECK(M >= 0 && D >= 1, "esp_bn_swish_eval: bad sizes M=%d D=%d", M, D);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(bn_running_kernel, dim3((D + 255) / 256), dim3(256), 0, st, run_mean, run_var, eps, D, mean, rstd);
+  if ((long)M * D > 0)
+    hipLaunchKernelGGL(bn_swish_fwd_kernel, dim3(gridn((long)M * D)), dim3(256), 0, st, y, mean, rstd, gamma, beta, s,
+                       (long)M * D, D);
+  ESP_CHECK_LAUNCH("esp_bn_swish_eval");
+  return 0;
+}
+
 // given ds = dL/ds, writes dy (grad wrt BN input) into `dy`; dgamma/dbeta accumulated.
 // workspace: >= 2*D*ceil(M/64) doubles + 2*D floats (sums) passed separately
 ESP_API int esp_bn_swish_bwd(const float* ds, const float* y, const float* mean, const float* rstd, const float* gamma,

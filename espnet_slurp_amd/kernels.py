@@ -366,6 +366,13 @@ def bn_swish_fwd(y, gamma, beta, s, mean, rstd, run_mean, run_var, momentum=0.1,
                  _p(run_var), float(momentum), float(eps), M, D, _p(ws), _st())
 
 
+def bn_swish_eval(y, gamma, beta, s, run_mean, run_var, mean, rstd, eps=1e-5):
+    """Eval-mode BatchNorm (running statistics) fused with Swish."""
+    M, D = y.shape
+    _native.call("esp_bn_swish_eval", _p(y), _p(gamma), _p(beta), _p(s), _p(run_mean), _p(run_var), float(eps), M, D,
+                 _p(mean), _p(rstd), _st())
+
+
 def bn_swish_bwd(ds, y, mean, rstd, gamma, beta, dy, dgamma, dbeta, sums):
     M, D = y.shape
     nb = (M + 63) // 64
@@ -504,6 +511,28 @@ def ctc_forced_align(lpz, y, blank=0):
     out = torch.empty(T, dtype=torch.int64, device=lpz.device)
     _native.call("esp_ctc_forced_align", _p(lpz), T, V, _p(y), U, blank, _p(path), _p(out), _st())
     return out
+
+
+def ctc_prefix_init(lp, blank=0):
+    """Initial CTC prefix state (T, 2) of the <sos> prefix for one utterance's log-probs lp (T, V)."""
+    T, V = lp.shape
+    r0 = torch.empty(T, 2, dtype=torch.float32, device=lp.device)
+    _native.call("esp_ctc_prefix_init", _p(lp), T, V, blank, _p(r0), _st())
+    return r0
+
+
+def ctc_prefix_score(lp, r_prev, last, out_len, cands, blank, eos):
+    """CTCPrefixScore for NH hypotheses x C candidates: r_prev (NH, T, 2), last (NH,) int64,
+    cands (NH, C) int64 -> (log_psi (NH, C), r_new (NH, C, T, 2))."""
+    T, V = lp.shape
+    NH, C = cands.shape
+    assert r_prev.shape == (NH, T, 2) and last.shape == (NH,)
+    assert int(cands.min()) >= 0 and int(cands.max()) < V
+    r_new = torch.empty(NH, C, T, 2, dtype=torch.float32, device=lp.device)
+    psi = torch.empty(NH, C, dtype=torch.float32, device=lp.device)
+    _native.call("esp_ctc_prefix_score", _p(lp), T, V, _p(r_prev), _p(last), int(out_len), _p(cands), NH, C,
+                 int(blank), int(eos), _p(r_new), _p(psi), _st())
+    return psi, r_new
 
 
 def reserve_workspace(nbytes, device):

@@ -111,6 +111,9 @@ int esp_dwconv1d_wgrad(const float* dy, const float* x, float* dW, int Bn, int T
 int esp_bn_swish_fwd(const float* y, const float* gamma, const float* beta, float* s, float* mean,
                      float* rstd, float* run_mean, float* run_var, float momentum, float eps, int M,
                      int D, double* work, void* stream);
+/* eval mode: statistics from run_mean / run_var (mean / rstd written for inspection) */
+int esp_bn_swish_eval(const float* y, const float* gamma, const float* beta, float* s, const float* run_mean,
+                      const float* run_var, float eps, int M, int D, float* mean, float* rstd, void* stream);
 int esp_bn_swish_bwd(const float* ds, const float* y, const float* mean, const float* rstd,
                      const float* gamma, const float* beta, float* dy, float* dgamma, float* dbeta,
                      int M, int D, double* work, float* sums, void* stream);
@@ -209,6 +212,18 @@ int esp_reduce_losses(const double* nll, int B, int zero_inf, const double* row_
 int esp_argmax(const float* x, long long* out, long rows, int V, void* stream);
 int esp_ctc_forced_align(const float* lpz, int T, int V, const long long* y, int U, int blank,
                          int* path, long long* out, void* stream);
+
+/* ---- beam-search CTC prefix scoring (espnet/nets/ctc_prefix_score.py:279-359 CTCPrefixScore,
+ *      espnet/nets/scorers/ctc.py CTCPrefixScorer; inference)
+ * lp: one utterance's (T, V) CTC log-softmax.  States are (T, 2) fp32 rows (log r^n, log r^b).
+ * init: r0 = initial state of the <sos> prefix.  score: for NH hypotheses (states r_prev
+ * (NH, T, 2), last label last[NH], common output length out_len = len(prefix) - 1) and C
+ * candidate labels each (cands (NH, C)), writes r_new (NH, C, T, 2) and log_psi (NH, C);
+ * log_psi = log r^n+r^b at T-1 for c == eos, -1e10 for c == blank. */
+int esp_ctc_prefix_init(const float* lp, int T, int V, int blank, float* r0, void* stream);
+int esp_ctc_prefix_score(const float* lp, int T, int V, const float* r_prev, const long long* last,
+                         int out_len, const long long* cands, int NH, int C, int blank, int eos,
+                         float* r_new, float* log_psi, void* stream);
 
 #ifdef __cplusplus
 }

@@ -11,6 +11,9 @@ Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import 
   (SURVEY.md §0.5): state s=0 also reads state -1 (Python wrap to the last state), and
   every `max + lpz` is computed in fp32 then stored in a float64 table.
 * `ctc_argmax_np` restates `CTC.argmax` (espnet2/asr/ctc.py:119-127): first max wins.
+* `ctc_prefix_init_np` / `ctc_prefix_score_np` restate the beam-search CTC prefix scorer
+  (espnet/nets/ctc_prefix_score.py:279-359, CTCPrefixScore.initial_state / __call__) in fp32
+  with numpy's logaddexp, pinned by tests/golden/inference.npz.
 """
 from __future__ import annotations
 
@@ -120,3 +123,44 @@ def forced_align_np(lpz, y, blank_id=0):
     for t in range(T - 2, -1, -1):
         seq[t] = state_path[t + 1, seq[t + 1]]
     return [int(lab[s]) for s in seq]
+
+
+LOGZERO = np.float32(-10000000000.0)
+
+
+def ctc_prefix_init_np(lp, blank=0):
+    """initial_state (ctc_prefix_score.py:290-302): r^n = logzero, r^b = cumulative blank."""
+    T = lp.shape[0]
+    r = np.full((T, 2), LOGZERO, dtype=np.float32)
+    r[0, 1] = lp[0, blank]
+    for t in range(1, T):
+        r[t, 1] = r[t - 1, 1] + lp[t, blank]
+    return r
+
+
+def ctc_prefix_score_np(lp, y, cs, r_prev, blank, eos):
+    """__call__ (ctc_prefix_score.py:304-359) for prefix y (with <sos>), candidates cs:
+    returns (log_psi (C,), r (C, T, 2)); rows before the recursion start are logzero."""
+    lp = np.asarray(lp, dtype=np.float32)
+    T = lp.shape[0]
+    n_out = len(y) - 1
+    C = len(cs)
+    xs = lp[:, cs]
+    r = np.full((T, 2, C), LOGZERO, dtype=np.float32)
+    if n_out == 0:
+        r[0, 0] = xs[0]
+    r_sum = np.logaddexp(r_prev[:, 0], r_prev[:, 1])
+    phi = np.repeat(r_sum[:, None], C, axis=1)
+    if n_out > 0:
+        for i, c in enumerate(cs):
+            if c == y[-1]:
+                phi[:, i] = r_prev[:, 1]
+    start = max(n_out, 1)
+    psi = r[start - 1, 0].copy()
+    for t in range(start, T):
+        r[t, 0] = np.logaddexp(r[t - 1, 0], phi[t - 1]) + xs[t]
+        r[t, 1] = np.logaddexp(r[t - 1, 0], r[t - 1, 1]) + lp[t, blank]
+        psi = np.logaddexp(psi, phi[t - 1] + xs[t])
+    psi[np.asarray(cs) == eos] = r_sum[-1]
+    psi[np.asarray(cs) == blank] = LOGZERO
+    return psi, np.moveaxis(r, 2, 0)
