@@ -151,18 +151,19 @@ def gemm_algorithmic_bytes(shapes) -> float:
     return tot
 
 
-def measured_gemm_traffic() -> dict:
+def measured_gemm_traffic(args) -> dict:
     """HBM bytes per launch of the GEMM family from the newest committed PMC measurement
     (profiles/*_gemm_traffic.json, written by tools/pmc_traffic.py from two rocprofv3 --pmc
     passes of this bench); {} when none is present."""
     import glob
     files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
                                           "*_gemm_traffic.json")))
-    if not files:
-        return {}
-    d = json.load(open(files[-1]))
-    d["source"] = os.path.relpath(files[-1], os.path.dirname(os.path.abspath(__file__)))
-    return d
+    for f in reversed(files):  # newest measurement of THIS workload (batch and model shape)
+        d = json.load(open(f))
+        if d.get("batch") == args.batch and (args.d, args.layers) == (256, 12) and not args.amp:
+            d["source"] = os.path.relpath(f, os.path.dirname(os.path.abspath(__file__)))
+            return d
+    return {}
 
 
 def main():
@@ -170,7 +171,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=64, help="utterances per GPU")
+    # B per GPU ("tune; report B"): measured at C2 64 -> 848, 96 -> 875, 128 -> 906,
+    # 192 -> 917, 256 -> 932 utt/s (profiles/r01g_batch_sweep.txt); 128 keeps the 8-GPU global batch at 1024
+    ap.add_argument("--batch", type=int, default=128, help="utterances per GPU")
     ap.add_argument("--d", type=int, default=256)
     ap.add_argument("--heads", type=int, default=4)
     ap.add_argument("--ff", type=int, default=1024)
@@ -240,7 +243,7 @@ def main():
     elapsed = float(el.item())
 
     if rank == 0:
-        traffic = measured_gemm_traffic()
+        traffic = measured_gemm_traffic(args)
         fwd, train = conformer_flops_per_utt(args.d, args.heads, args.ff, args.layers, 2048, 6, args.vocab)
         value = world * args.batch * args.steps / elapsed
         achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
