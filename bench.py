@@ -79,10 +79,15 @@ def build(args, device):
     return model
 
 
-def synthetic_batch(B, V, rank, device):
+def synthetic_batch(B, V, rank, device, variable=False):
+    """SURVEY §8(d) synthetic inputs: N(0,1) fbank, lengths 1500 (or U[1000,1500] sorted
+    descending with variable=True), tokens U[2, V-2], label lengths U[20,40] padded -1."""
     g = torch.Generator().manual_seed(1234 + rank)
     speech = torch.randn(B, 1500, 80, generator=g).to(device)
     speech_lengths = torch.full((B,), 1500, dtype=torch.long)
+    if variable:
+        speech_lengths = torch.sort(torch.randint(1000, 1501, (B,), generator=g), descending=True)[0]
+        speech_lengths[0] = 1500  # the padded width stays T = 1500
     tl = torch.randint(20, 41, (B,), generator=g)
     text = torch.full((B, int(tl.max())), -1, dtype=torch.long)
     for i in range(B):
@@ -182,6 +187,8 @@ def main():
     ap.add_argument("--rel-pos", default="latest", choices=["latest", "legacy"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch kernel by kernel instead of replaying a HIP graph")
+    ap.add_argument("--variable-lengths", action="store_true",
+                    help="speech lengths U[1000,1500] sorted descending (SURVEY 8(d) variable variant)")
     ap.add_argument("--amp", action="store_true", help="bf16 GEMM operands, fp32 accumulate (TrainerOptions.use_amp)")
     ap.add_argument("--config", choices=sorted(PRESETS), default=None,
                     help="BASELINE.json config preset (overrides --d/--heads/--ff/--layers; c5 implies --amp)")
@@ -194,6 +201,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        # enough RCCL channels that a ring uses all 7 xGMI links of each GPU
+        os.environ.setdefault("NCCL_MIN_NCHANNELS", "8")
         dist.init_process_group("nccl")
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
@@ -210,7 +219,7 @@ def main():
     sched = WarmupLR(opt, warmup_steps=25000)
     trainer = Trainer(model, opt, sched, TrainerOptions(grad_clip=5.0, use_amp=args.amp), distributed=world > 1,
                       cuda_graph=not args.eager)
-    batch = synthetic_batch(args.batch, args.vocab, rank, device)
+    batch = synthetic_batch(args.batch, args.vocab, rank, device, args.variable_lengths)
 
     for _ in range(args.warmup):
         trainer.train_one_step(batch)
@@ -267,7 +276,8 @@ def main():
             "launch": "eager" if args.eager else "hip_graph",
             "config": {"workload": f"{workload_name(args)} d={args.d} H={args.heads} FF={args.ff} "
                                    f"{args.layers}L enc / 6L dec, V={args.vocab}, rel_pos={args.rel_pos}, "
-                                   "ctc 0.3, lsm 0.1, dropout 0.1, SpecAug on",
+                                   "ctc 0.3, lsm 0.1, dropout 0.1, SpecAug on"
+                                   + (", lengths U[1000,1500]" if args.variable_lengths else ""),
                        "global_batch": world * args.batch, "seq_len": 1500, "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 4),

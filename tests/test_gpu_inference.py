@@ -98,3 +98,24 @@ def test_beam_search_matches_reference(dev, tag):
         wi = want_y[i][want_y[i] >= 0]
         assert res[i][3].yseq.tolist() == wi.tolist(), i
         assert abs(res[i][3].score - want_s[i]) <= 1e-3 * abs(want_s[i]), i
+
+
+def test_slu_model_loss_equals_asr(dev):
+    """Same weights and batch: the SLU model's training loss is the ASR model's (transcript ignored)."""
+    from oracle import espnet_cpu as O
+    from espnet_slurp_amd.slu.espnet_model import ESPnetSLUModel
+    from tests.helpers import token_list
+    cfg = small_cfg("latest")
+    asr = build_model(cfg, dev, dropout=0.0)
+    load_seeded(asr, cfg, 9)
+    from tests.test_slu import _parts
+    slu = ESPnetSLUModel(vocab_size=cfg.vocab_size, token_list=token_list(cfg.vocab_size), ctc_weight=cfg.ctc_weight,
+                         lsm_weight=cfg.lsm_weight, **_parts(cfg)).to(dev)
+    slu.flatten()
+    load_seeded(slu, cfg, 9)
+    speech, slen, text, tlen = O.synthetic_batch(2, 96, 80, cfg.vocab_size, [96, 70], [6, 4], 3)
+    asr.train()
+    slu.train()
+    la = asr(speech.to(dev), slen, text.clone(), tlen)[0].item()
+    ls = slu(speech.to(dev), slen, text.clone(), tlen, transcript=text.clone(), transcript_lengths=tlen)[0].item()
+    assert abs(la - ls) <= 1e-6 * max(1.0, abs(la)), (la, ls)
