@@ -233,10 +233,18 @@ __device__ __forceinline__ void quad_transpose(f32x16& v, int lane) {
   }
 }
 
+// 16-B output store; nt = streaming (non-temporal) hint, so the write does not displace the
+// operand panels the co-resident tiles still read from L2 (ESP_GEMM_ABL bit 32, measured)
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st4(float* p, const float (&v)[4], bool nt) {
+  const f32x4v w = {v[0], v[1], v[2], v[3]};
+  if (nt) __builtin_nontemporal_store(w, reinterpret_cast<f32x4v*>(p));
+  else *reinterpret_cast<f32x4v*>(p) = w;
+}
 // needs N % 4 == 0, ldc % 4 == 0 and 16-B aligned C / R / aux / pre / bias (host: g.wide)
 template <int EPI, int TM, int TN>
 __device__ __forceinline__ void store_tiles_wide(const GemmArgs& g, int z, int mrow0, int ncol0, int lane,
-                                                 f32x16 (&acc)[TM][TN]) {
+                                                 f32x16 (&acc)[TM][TN], bool nt = false) {
   const int h = lane >> 5, l32 = lane & 31;
   const long cbase = c_base(g, z);
   const uint64_t dbase = (uint64_t)z * (uint64_t)g.M * (uint64_t)g.N;
@@ -270,7 +278,7 @@ __device__ __forceinline__ void store_tiles_wide(const GemmArgs& g, int z, int m
                       acc[i][j][4 * q + 3] + bn.w};
         const float r4[4] = {rr[q].x, rr[q].y, rr[q].z, rr[q].w};
         if constexpr (EPI == EPI_FWD) {
-          if (g.aux) *reinterpret_cast<float4*>(g.aux + off) = make_float4(v[0], v[1], v[2], v[3]);
+          if (g.aux) st4(g.aux + off, v, nt);
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -298,7 +306,7 @@ __device__ __forceinline__ void store_tiles_wide(const GemmArgs& g, int z, int m
           if (has_r) w += g.beta * r4[e];
           v[e] = w;
         }
-        *reinterpret_cast<float4*>(g.c + off) = make_float4(v[0], v[1], v[2], v[3]);
+        st4(g.c + off, v, nt);
       }
     }
   }
@@ -804,7 +812,7 @@ struct GldsArgs {
   const float* t_zeros;  // >= 16 zero bytes: the DMA source of lanes outside the grid
   int abl;             // diagnostic ablation bits (ESP_GEMM_ABL, timing only): 1 no DMA after the
                        // first slab, 2 no epilogue stores, 4 no k-loop barrier / waits, 16 dword
-                       // (not float4) epilogue stores
+                       // (not float4) epilogue stores, 32 non-temporal epilogue stores
 };
 
 constexpr int GL_BK = 32;
@@ -1145,7 +1153,7 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_ke
       float* W = g.splits > 1 ? g.work + ((long)c.split * g.batch + c.z) * (long)g.M * g.N : nullptr;
       if (g.wide) {
         if (W) store_partials_wide<TM, TN>(g, W, c.m0 + wm * TM * 32, c.n0 + wn * 64, lane, acc);
-        else store_tiles_wide<EPI, TM, TN>(g, c.z, c.m0 + wm * TM * 32, c.n0 + wn * 64, lane, acc);
+        else store_tiles_wide<EPI, TM, TN>(g, c.z, c.m0 + wm * TM * 32, c.n0 + wn * 64, lane, acc, (x.abl & 32) != 0);
       } else {
         if (W) store_partials<TM, TN>(g, W, c.m0 + wm * TM * 32, c.n0 + wn * 64, h, l32, acc);
         else store_tiles<EPI, TM, TN>(g, c.z, c.m0 + wm * TM * 32, c.n0 + wn * 64, h, l32, acc);

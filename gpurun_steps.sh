@@ -1,14 +1,9 @@
-#!/bin/bash
-# Run GPU steps in sequence; continue past ordinary test failures (exit 1) but stop at
-# anything that looks like a fault / abort / timeout (exit >= 2).
+set -o pipefail
 mkdir -p gpurun_out
-i=0
-for cmd in "$@"; do
-  i=$((i+1))
-  echo "=== step $i: $cmd" >> gpurun_out/steps.log
-  bash -c "$cmd"
-  rc=$?
-  echo "=== step $i rc=$rc" >> gpurun_out/steps.log
-  if [ $rc -ge 2 ]; then echo "stopping after rc=$rc"; exit $rc; fi
-done
-exit 0
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+ESP_GEMM_ABL=32 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/nt2_bench_nt_a.log 2>&1 &&
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/nt2_bench_default_a.log 2>&1 &&
+ESP_GEMM_ABL=32 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/nt2_bench_nt_b.log 2>&1 &&
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/nt2_bench_default_b.log 2>&1 &&
+ESP_GEMM_ABL=32 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_nt -o run -- python3 bench.py --steps 5 --warmup 3 > gpurun_out/nt2_prof_nt.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_def -o run -- python3 bench.py --steps 5 --warmup 3 > gpurun_out/nt2_prof_def.log 2>&1
