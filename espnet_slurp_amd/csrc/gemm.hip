@@ -1490,6 +1490,19 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
       const long cap = work_bytes / (4L * ((long)M * N * batch + (rowsum ? M : 0)));
       if (sp > cap) sp = cap;
       if (sp > 64) sp = 64;
+      // CU balance: with ceil(tiles*sp / 256) tile-rounds on the busiest CU, 72 tiles x 8 splits
+      // (conv2 weight gradient) leave a third of the chip idle in the last round; take the
+      // smallest sp up to 4x the target-derived one whose last round is >= 95 % full.
+      if (sp >= 2 && !getenv("ESP_SPLITK_NOBALANCE")) {
+        auto imb = [&](long s) { const long t = tiles * s; return (double)((t + 255) / 256 * 256) / (double)t; };
+        const long hi = std::min(std::min(by_k, cap), std::min<long>(64, 4 * sp));
+        long best = sp;
+        for (long s = sp; s <= hi; ++s) {
+          if (imb(s) < imb(best) - 1e-9) best = s;
+          if (imb(best) <= 1.05) break;
+        }
+        sp = best;
+      }
       if (sp >= 2) {
         int chunk = (int)((K + sp - 1) / sp);
         chunk = (chunk + BK - 1) / BK * BK;
