@@ -19,6 +19,7 @@ from .. import kernels as K
 from ..blocks import Seeds, empty
 from ..flat import FlatParams
 from .encoder.abs_encoder import draw_seed
+from .error_calculator import ErrorCalculator
 
 
 class AbsESPnetModel(nn.Module):
@@ -122,7 +123,9 @@ class ESPnetASRModel(AbsESPnetModel):
         self.ctc = None if ctc_weight == 0.0 else ctc
         self.lsm_weight = lsm_weight
         self.length_normalized_loss = length_normalized_loss
-        self.error_calculator = None
+        # eval-mode cer_ctc / cer / wer (espnet_model.py:152-154, 515-540)
+        self.error_calculator = (ErrorCalculator(token_list, sym_space, sym_blank, report_cer, report_wer)
+                                 if report_cer or report_wer else None)
         self.extract_feats_in_collect_stats = extract_feats_in_collect_stats
         self.flat: Optional[FlatParams] = None
         if self.blank_id != 0:
@@ -165,6 +168,8 @@ class ESPnetASRModel(AbsESPnetModel):
                               (1.0 - self.ctc_weight) / denom, grad_att, row_loss, row_stat)
             state["grad_att"] = grad_att
             state["dec"] = dsaved
+            if not self.training:  # eval-mode cer / wer read the decoder argmax (_error_rates)
+                prep["eval_logits"] = logits
         out4 = empty(4, like=hs)
         K.reduce_losses(nll, B, self.ctc.zero_infinity if self.ctc is not None else True, row_loss, row_stat, R,
                         denom, self.ctc_weight, out4)
@@ -216,7 +221,8 @@ class ESPnetASRModel(AbsESPnetModel):
                 host["sa_" + k] = v.to(torch.int32)
         host["hlens"] = self.encoder.output_lengths(sl_cpu, T).to(torch.int32)
         prep = Prepared(B=B, T=T, Umax=int(text_cpu.shape[1]), denom=float(B), L=0, host=host,
-                        enc_seed=draw_seed(), heads_seed=draw_seed(), sl_cpu=sl_cpu, n_samples=n_samples)
+                        enc_seed=draw_seed(), heads_seed=draw_seed(), sl_cpu=sl_cpu, n_samples=n_samples,
+                        ys_pad_cpu=text_cpu)
         if self.ctc is not None:
             host["ys"] = text_cpu
             host["tlens"] = tl_cpu.to(torch.int32)
@@ -257,7 +263,27 @@ class ESPnetASRModel(AbsESPnetModel):
             cer=None, wer=None,
             loss=loss.detach(),
         )
+        if not self.training and self.error_calculator is not None:
+            stats.update(self._error_rates(encoder_out, prep))
         return loss, stats, d["weight"]
+
+    def _error_rates(self, encoder_out, prep) -> Dict[str, Optional[torch.Tensor]]:
+        """Eval-mode error rates (espnet_model.py:515-521, 536-539): greedy CTC and decoder
+        argmaxes on device, then the reference's host-side string edit distances."""
+        dev = encoder_out.device
+        as_t = lambda v: None if v is None else torch.tensor([v], dtype=torch.float32, device=dev)
+        out = {}
+        ys_pad = prep.ys_pad_cpu
+        if self.ctc is not None:
+            ys_hat = self.ctc.argmax(encoder_out).cpu()
+            out["cer_ctc"] = as_t(self.error_calculator(ys_hat, ys_pad, is_ctc=True))
+        if self.decoder is not None:
+            R = prep.B * prep.L
+            am = torch.empty(R, dtype=torch.int64, device=dev)
+            K.argmax(prep.pop("eval_logits"), am, R, self.vocab_size)
+            cer, wer = self.error_calculator(am.view(prep.B, prep.L).cpu(), ys_pad)
+            out["cer"], out["wer"] = as_t(cer), as_t(wer)
+        return out
 
     def forward(self, speech: torch.Tensor, speech_lengths: torch.Tensor, text: torch.Tensor,
                 text_lengths: torch.Tensor, specaug_draws: Optional[dict] = None, **kwargs):

@@ -18,6 +18,7 @@ from ..asr.specaug.specaug import SpecAug
 from ..asr.frontend.default import DefaultFrontend
 from ..layers.global_mvn import GlobalMVN
 from ..layers.utterance_mvn import UtteranceMVN
+from ..torch_utils.initialize import initialize
 
 
 class ClassChoices:
@@ -55,15 +56,29 @@ decoder_choices = ClassChoices("decoder", dict(transformer=TransformerDecoder), 
 def build_model(args: argparse.Namespace, device="cuda") -> ESPnetASRModel:
     """ASRTask.build_model (asr.py:439-562) for the fbank (--input_size) path.
 
-    args needs: token_list, input_size, specaug/_conf, normalize/_conf, encoder/_conf,
-    decoder/_conf, ctc_conf, model_conf (the resolved config.yaml fields)."""
-    token_list = list(args.token_list)
+    args needs: token_list (a list or a token file path, as asr.py:441-450), input_size,
+    specaug/_conf, normalize/_conf, encoder/_conf, decoder/_conf, ctc_conf, model_conf, init
+    (the resolved config.yaml fields)."""
+    if isinstance(args.token_list, str):
+        with open(args.token_list, encoding="utf-8") as f:
+            token_list = [line.rstrip() for line in f]
+        args.token_list = list(token_list)  # "portable", as the reference does
+    elif isinstance(args.token_list, (tuple, list)):
+        token_list = list(args.token_list)
+    else:
+        raise RuntimeError("token_list must be str or list")
+    for opt in ("preencoder", "postencoder"):
+        if getattr(args, opt, None) is not None:
+            raise NotImplementedError(f"--{opt}: not on the Conformer CTC/attention hot path")
+    if getattr(args, "decoder", None) == "transducer":
+        raise NotImplementedError("--decoder transducer: not on the CTC/attention hot path")
     vocab_size = len(token_list)
     if getattr(args, "input_size", None) is None:  # extract features in the model (asr.py:459-468)
         frontend = frontend_choices.get_class(getattr(args, "frontend", "default"))(
             **(getattr(args, "frontend_conf", None) or {}))
         input_size = frontend.output_size()
     else:  # features from the data loader
+        args.frontend, args.frontend_conf = None, {}
         frontend = None
         input_size = args.input_size
     specaug_cls = specaug_choices.get_class(getattr(args, "specaug", None))
@@ -79,6 +94,8 @@ def build_model(args: argparse.Namespace, device="cuda") -> ESPnetASRModel:
     model = model_cls(vocab_size=vocab_size, frontend=frontend, specaug=specaug, normalize=normalize, preencoder=None,
                       encoder=encoder, postencoder=None, decoder=decoder, ctc=ctc, joint_network=None,
                       token_list=token_list, **(getattr(args, "model_conf", None) or {}))
+    if getattr(args, "init", None) is not None:  # asr.py:556-557
+        initialize(model, args.init)
     model = model.to(device)
     model.flatten()
     return model

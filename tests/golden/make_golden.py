@@ -295,6 +295,167 @@ def fullsize_fixture():
     np.savez_compressed(os.path.join(HERE, "fullsize_c2.npz"), **out)
 
 
+N_SLICE = 16
+
+
+def slice_indices(name: str, numel: int) -> np.ndarray:
+    """Fixed element indices per tensor (first 4, last 4, 8 seeded by the name)."""
+    import zlib
+    rng = np.random.Generator(np.random.PCG64(zlib.crc32(name.encode())))
+    k = min(numel, N_SLICE)
+    if numel <= N_SLICE:
+        return np.arange(numel, dtype=np.int64)
+    idx = np.concatenate([np.arange(4), np.arange(numel - 4, numel), rng.integers(4, numel - 4, size=k - 8)])
+    return idx.astype(np.int64)
+
+
+def grad_summary(model, tag: str, out: dict):
+    """Per-tensor gradient L2 norm (fp64), max |g| and a fixed slice of elements."""
+    for n, p in model.named_parameters():
+        g = p.grad.detach().double().reshape(-1)
+        idx = slice_indices(n, g.numel())
+        out[f"gn_{tag}/{n}"] = np.float64(g.norm().item())
+        out[f"gmax_{tag}/{n}"] = np.float64(g.abs().max().item())
+        out[f"gidx/{n}"] = idx
+        out[f"gs_{tag}/{n}"] = g[torch.from_numpy(idx)].numpy()
+
+
+def fullsize_train_fixture(name: str, cfg, B=2, T=1500, lens=(1500, 1337), ulens=(40, 27), seed=42,
+                           with_grads=True, build=None, train=True):
+    """Full-size fp32 AND fp64 reference step (SURVEY.md §8(d) gate judged against fp64): loss,
+    loss_ctc / loss_att / acc and, with_grads, every parameter's gradient norm and a fixed
+    slice of its elements.  train=False runs the reference in eval mode (validation step:
+    no dropout, no SpecAug, BatchNorm from its running statistics)."""
+    import time as _t
+    build = build or (lambda: build_reference(cfg))
+    out = {}
+    F_ = cfg.enc.input_size
+    for dt, tag in ((torch.float32, "f32"), (torch.float64, "f64")):
+        t0 = _t.time()
+        model = build().to(dt)
+        load_params(model, cfg, seed, dt)
+        model.train(train)
+        speech, slen, text, tlen = O.synthetic_batch(B, T, F_, cfg.vocab_size, list(lens), list(ulens), seed + 1)
+        if with_grads:
+            loss, stats, _ = model(speech.to(dt), slen, text, tlen)
+            loss.backward()
+            grad_summary(model, tag, out)
+        else:
+            with torch.no_grad():
+                loss, stats, _ = model(speech.to(dt), slen, text, tlen)
+        out[f"loss_{tag}"] = np.float64(loss.item())
+        for k in ("loss_ctc", "loss_att", "acc", "cer_ctc", "cer", "wer"):
+            if stats.get(k) is not None:
+                out[f"{k}_{tag}"] = np.float64(float(stats[k]))
+        if not train:  # the greedy sequences the eval-mode error calculator scored
+            with torch.no_grad():
+                hs, hl = model.encode(speech.to(dt), slen)
+                out[f"ctc_argmax_{tag}"] = model.ctc.argmax(hs).numpy()
+        print(f"{name} {tag}: loss {loss.item():.6f} ({_t.time() - t0:.1f} s)", flush=True)
+        del model
+    out.update(lens=np.array(lens), ulens=np.array(ulens), seed=np.int64(seed), B=np.int64(B), T=np.int64(T))
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+
+
+def c2_cfg(rel_pos_type):
+    return O.ModelCfg(vocab_size=600, enc=O.EncCfg(output_size=256, attention_heads=4, linear_units=1024,
+                                                   num_blocks=12, rel_pos_type=rel_pos_type),
+                      dec=O.DecCfg(attention_heads=4, linear_units=2048, num_blocks=6))
+
+
+SLURP_YAML = "egs2/slurp/asr1/conf/tuning/train_asr_conformer.yaml"
+
+
+def slurp_config():
+    """The SLURP recipe's training config as the reference resolves it (config.yaml fields).
+
+    egs2/slurp/asr1/run.sh:14-31 trains with --feats_type fbank_pitch (83-dim Kaldi fbank +
+    pitch, so asr.sh passes --input_size=83, asr.sh:1034-1042) and --feats_normalize
+    utterance_mvn (the default normalize, asr.sh:1046-1049); the YAML has no rel_pos_type, so
+    ConformerEncoder's default "legacy" applies (conformer_encoder.py:98,116-120)."""
+    import yaml
+    with open(os.path.join(refshim.REF, SLURP_YAML)) as f:
+        conf = yaml.safe_load(f)
+    keys = ("encoder", "encoder_conf", "decoder", "decoder_conf", "model_conf", "specaug", "specaug_conf",
+            "optim", "optim_conf", "scheduler", "scheduler_conf", "max_epoch", "best_model_criterion",
+            "keep_nbest_models")
+    resolved = {k: conf[k] for k in keys if k in conf}
+    resolved.update(input_size=83, normalize="utterance_mvn", normalize_conf={}, ctc_conf={}, frontend=None,
+                    token_list_size=600, source=SLURP_YAML + " + egs2/slurp/asr1/run.sh (fbank_pitch, utterance_mvn)")
+    return resolved
+
+
+def build_reference_from_config(conf, V):
+    """ASRTask.build_model (espnet2/tasks/asr.py:439-562) steps 1-7 replayed on the reference's
+    own classes: espnet2.tasks.asr itself does not import in this fork (asr.py:27 imports
+    espnet/nets/pytorch_backend/conformer/contextual_block_encoder_layer.py, which is absent)."""
+    enc_cls = {"conformer": ConformerEncoder, "transformer": TransformerEncoder}[conf["encoder"]]
+    spec = SpecAug(**conf["specaug_conf"]) if conf.get("specaug") == "specaug" else None
+    norm = UtteranceMVN(**conf["normalize_conf"]) if conf.get("normalize") == "utterance_mvn" else None
+    enc = enc_cls(input_size=conf["input_size"], **conf["encoder_conf"])
+    dec = TransformerDecoder(vocab_size=V, encoder_output_size=enc.output_size(), **conf["decoder_conf"])
+    ctc = CTC(odim=V, encoder_output_size=enc.output_size(), **conf["ctc_conf"])
+    return ESPnetASRModel(vocab_size=V, frontend=None, specaug=spec, normalize=norm, preencoder=None, encoder=enc,
+                          postencoder=None, decoder=dec, ctc=ctc, joint_network=None, token_list=token_list(V),
+                          **conf["model_conf"])
+
+
+def slurp_cfg_from_config(conf, V, dropout_zero=False):
+    e, d = conf["encoder_conf"], conf["decoder_conf"]
+    z = (lambda x: 0.0) if dropout_zero else (lambda x: x)
+    return O.ModelCfg(
+        vocab_size=V,
+        enc=O.EncCfg(input_size=conf["input_size"], output_size=e["output_size"], attention_heads=e["attention_heads"],
+                     linear_units=e["linear_units"], num_blocks=e["num_blocks"], dropout_rate=z(e["dropout_rate"]),
+                     positional_dropout_rate=z(e["positional_dropout_rate"]),
+                     attention_dropout_rate=z(e["attention_dropout_rate"]),
+                     rel_pos_type=e.get("rel_pos_type", "legacy"), macaron_style=e["macaron_style"],
+                     use_cnn_module=e["use_cnn_module"], cnn_module_kernel=e["cnn_module_kernel"]),
+        dec=O.DecCfg(attention_heads=d["attention_heads"], linear_units=d["linear_units"], num_blocks=d["num_blocks"],
+                     dropout_rate=z(d["dropout_rate"]), positional_dropout_rate=z(d["positional_dropout_rate"]),
+                     self_attention_dropout_rate=z(d["self_attention_dropout_rate"]),
+                     src_attention_dropout_rate=z(d["src_attention_dropout_rate"])),
+        ctc_weight=conf["model_conf"]["ctc_weight"], lsm_weight=conf["model_conf"]["lsm_weight"],
+        length_normalized_loss=conf["model_conf"]["length_normalized_loss"])
+
+
+def slurp_yaml_fixture():
+    """The SLURP recipe config end to end (VERDICT r1 'missing' 1): the resolved config as JSON
+    (data: the GPU box has no /root/reference), the reference model's state_dict key/shape
+    list, and full-size (B=2, T=1500, 83-dim) fp32/fp64 reference results for
+      * the YAML model exactly as configured, in eval mode (validate_one_epoch: dropout and
+        SpecAug off, BatchNorm running statistics);
+      * the same architecture with every dropout rate 0 and SpecAug off, in train mode
+        (BatchNorm batch statistics), with every parameter gradient summarised."""
+    import json
+    V = 600
+    conf = slurp_config()
+    ref = build_reference_from_config(conf, V)
+    sd = ref.state_dict()
+    cfg = slurp_cfg_from_config(conf, V)
+    P = O.deterministic_params(cfg, 0)
+    assert set(P) == set(sd), set(P) ^ set(sd)
+    conf["reference_state_dict"] = [[k, list(v.shape)] for k, v in sd.items()]
+    conf["reference_num_params"] = int(sum(p.numel() for p in ref.parameters()))
+    conf["reference_modules"] = {"encoder.encoders.0.self_attn": type(ref.encoder.encoders[0].self_attn).__name__,
+                                 "encoder.embed.1": type(ref.encoder.embed.out[1]).__name__
+                                 if hasattr(ref.encoder.embed, "out") else ""}
+    with open(os.path.join(HERE, "slurp_asr_conformer_config.json"), "w") as f:
+        json.dump(conf, f, indent=1)
+    print("slurp config:", conf["reference_num_params"], "params", conf["reference_modules"])
+    del ref
+    fullsize_train_fixture("slurp_yaml_eval", cfg, seed=61, with_grads=False, train=False,
+                           build=lambda: build_reference_from_config(conf, V))
+    conf0 = json.loads(json.dumps(conf))
+    for sec in ("encoder_conf", "decoder_conf"):
+        for k in list(conf0[sec]):
+            if k.endswith("dropout_rate"):
+                conf0[sec][k] = 0.0
+    conf0["specaug"] = None
+    fullsize_train_fixture("slurp_yaml_train", slurp_cfg_from_config(conf, V, dropout_zero=True), seed=62,
+                           build=lambda: build_reference_from_config(conf0, V))
+
+
 def frontend_fixture():
     """Front end: the reference Stft, the LogMel forward (with the
     oracle's restated mel matrix injected: librosa is absent) and GlobalMVN on seeded audio."""
@@ -446,3 +607,13 @@ if __name__ == "__main__":
         train_step_fixture()
     if "full" in which:
         fullsize_fixture()
+    if "fullgrad" in which:  # full-size C2 gradients, latest and legacy (round 2)
+        fullsize_train_fixture("fullsize_c2_grad_latest", c2_cfg("latest"), seed=42)
+        fullsize_train_fixture("fullsize_c2_grad_legacy", c2_cfg("legacy"), seed=44)
+    if "c4" in which:  # C4 shape: d=512, H=8, FF=2048, 17 blocks, latest; forward loss
+        c4 = O.ModelCfg(vocab_size=600, enc=O.EncCfg(output_size=512, attention_heads=8, linear_units=2048,
+                                                     num_blocks=17, rel_pos_type="latest"),
+                        dec=O.DecCfg(attention_heads=8, linear_units=2048, num_blocks=6))
+        fullsize_train_fixture("fullsize_c4_loss", c4, seed=51, with_grads=False)
+    if "slurp" in which:
+        slurp_yaml_fixture()

@@ -34,7 +34,17 @@ def install():
     _stub("typeguard", check_argument_types=lambda *a, **k: True,
           check_return_type=lambda *a, **k: True, check_type=lambda *a, **k: None)
     _stub("humanfriendly", format_timespan=str, format_size=str)
-    _stub("editdistance", eval=lambda *a, **k: (_ for _ in ()).throw(ImportError("editdistance")))
+    def _levenshtein(a, b):  # editdistance.eval: unit-cost edit distance over two sequences
+        a, b = list(a), list(b)
+        prev = list(range(len(b) + 1))
+        for i, x in enumerate(a, 1):
+            cur = [i] + [0] * len(b)
+            for j, y in enumerate(b, 1):
+                cur[j] = min(prev[j] + 1, cur[j - 1] + 1, prev[j - 1] + (x != y))
+            prev = cur
+        return prev[-1]
+
+    _stub("editdistance", eval=_levenshtein)
     lib = _stub("librosa")
     lib.filters = _Raiser()
     lib.util = _Raiser()

@@ -83,3 +83,80 @@ def rel_err(a, b):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
     return float(np.abs(a - b).max() / (np.abs(b).max() + 1e-12))
+
+
+def slurp_config():
+    """egs2/slurp/asr1 training config as resolved by the reference (fixture written by
+    tests/golden/make_golden.py slurp from the recipe YAML; the GPU box has no reference)."""
+    import json
+    with open(os.path.join(GOLDEN, "slurp_asr_conformer_config.json")) as f:
+        return json.load(f)
+
+
+def slurp_args(conf, dropout_zero=False, specaug=True):
+    """argparse.Namespace with the fields ASRTask.build_model reads (asr.py:439-562)."""
+    import argparse
+    import copy
+    conf = copy.deepcopy(conf)
+    if dropout_zero:
+        for sec in ("encoder_conf", "decoder_conf"):
+            for k in conf[sec]:
+                if k.endswith("dropout_rate"):
+                    conf[sec][k] = 0.0
+    return argparse.Namespace(
+        token_list=token_list(conf["token_list_size"]), input_size=conf["input_size"],
+        frontend=None, frontend_conf={}, specaug=conf["specaug"] if specaug else None,
+        specaug_conf=conf["specaug_conf"], normalize=conf["normalize"], normalize_conf=conf["normalize_conf"],
+        preencoder=None, encoder=conf["encoder"], encoder_conf=conf["encoder_conf"], postencoder=None,
+        decoder=conf["decoder"], decoder_conf=conf["decoder_conf"], ctc_conf=conf["ctc_conf"],
+        model="espnet", model_conf=conf["model_conf"], init=None)
+
+
+def cfg_from_config(conf, dropout_zero=False):
+    """The oracle ModelCfg of a resolved config (parameter shapes / seeded values)."""
+    e, d = conf["encoder_conf"], conf["decoder_conf"]
+    z = (lambda x: 0.0) if dropout_zero else (lambda x: x)
+    return O.ModelCfg(
+        vocab_size=conf["token_list_size"],
+        enc=O.EncCfg(input_size=conf["input_size"], output_size=e["output_size"], attention_heads=e["attention_heads"],
+                     linear_units=e["linear_units"], num_blocks=e["num_blocks"], dropout_rate=z(e["dropout_rate"]),
+                     positional_dropout_rate=z(e["positional_dropout_rate"]),
+                     attention_dropout_rate=z(e["attention_dropout_rate"]),
+                     rel_pos_type=e.get("rel_pos_type", "legacy"), macaron_style=e["macaron_style"],
+                     use_cnn_module=e["use_cnn_module"], cnn_module_kernel=e["cnn_module_kernel"]),
+        dec=O.DecCfg(attention_heads=d["attention_heads"], linear_units=d["linear_units"], num_blocks=d["num_blocks"]),
+        ctc_weight=conf["model_conf"]["ctc_weight"], lsm_weight=conf["model_conf"]["lsm_weight"],
+        length_normalized_loss=conf["model_conf"]["length_normalized_loss"])
+
+
+def grad_gate(model, g, skip_rel=1e-6):
+    """Per-tensor gradient gate of a full-size fixture (make_golden.fullsize_train_fixture):
+    the L2 norm and a fixed element slice must be as close to the fp64 reference as the
+    reference's own fp32 result is (x2), or within 1e-4 relative.  Returns the failures."""
+    scale = max(float(g["gmax_f64/" + n]) for n, _ in model.named_parameters())
+    bad = []
+    for n, p in model.named_parameters():
+        got = p.grad.detach().double().reshape(-1).cpu()
+        gm = float(g["gmax_f64/" + n])
+        if gm < skip_rel * scale:  # exactly-zero gradients: fp32 noise on both sides
+            if float(got.abs().max()) > 1e-5 * scale:
+                bad.append((n, "nonzero", float(got.abs().max())))
+            continue
+        gn64, gn32 = float(g["gn_f64/" + n]), float(g["gn_f32/" + n])
+        e_gpu = abs(float(got.norm()) - gn64) / gn64
+        e_ref = abs(gn32 - gn64) / gn64
+        if e_gpu > max(1e-4, 2 * e_ref):
+            bad.append((n, "norm", e_gpu, e_ref))
+        s = got[torch.from_numpy(g["gidx/" + n])].numpy()
+        es = float(np.abs(s - g["gs_f64/" + n]).max()) / gm
+        er = float(np.abs(g["gs_f32/" + n] - g["gs_f64/" + n]).max()) / gm
+        if es > max(1e-4, 2 * er):
+            bad.append((n, "slice", es, er))
+    return bad
+
+
+def loss_gate(got, g, key="loss", slack=0.0):
+    """|build - ref64| <= max(1e-4, 2 |ref32 - ref64|) (+ slack)."""
+    l64, l32 = float(g[f"{key}_f64"]), float(g[f"{key}_f32"])
+    tol = max(1e-4, 2 * abs(l32 - l64)) + slack
+    return abs(got - l64) <= tol, (key, got, l64, tol)
