@@ -156,7 +156,10 @@ class ESPnetASRModel(AbsESPnetModel):
             state["grad_ctc"] = grad_ctc
         row_loss = row_stat = None
         R = 0
-        denom = prep.denom
+        # length_normalized_loss: the denominator is this batch's target count, taken on device
+        # by esp_reduce_losses (denom 0) and applied to the decoder gradient in the backward
+        ln = self.length_normalized_loss
+        denom = 0.0 if ln else prep.denom
         if self.decoder is not None:
             R = B * prep.L
             logits, dsaved = self.decoder.run_forward(hs, hlens_i32, d["ys_in"], d["ys_in_lens"], seeds, self.training)
@@ -165,14 +168,16 @@ class ESPnetASRModel(AbsESPnetModel):
             row_loss = torch.empty(R, dtype=torch.float64, device=dev)
             row_stat = torch.empty(2 * R, dtype=torch.int32, device=dev)
             K.label_smoothing(logits, d["ys_out"], V, self.ignore_id, self.lsm_weight,
-                              (1.0 - self.ctc_weight) / denom, grad_att, row_loss, row_stat)
+                              (1.0 - self.ctc_weight) / (1.0 if ln else denom), grad_att, row_loss, row_stat)
             state["grad_att"] = grad_att
             state["dec"] = dsaved
             if not self.training:  # eval-mode cer / wer read the decoder argmax (_error_rates)
                 prep["eval_logits"] = logits
-        out4 = empty(4, like=hs)
+        out4 = empty(5, like=hs)
         K.reduce_losses(nll, B, self.ctc.zero_infinity if self.ctc is not None else True, row_loss, row_stat, R,
                         denom, self.ctc_weight, out4)
+        if ln and self.decoder is not None:
+            state["inv_denom"] = out4[4:5]
         return out4, state
 
     def _heads_backward(self, state, g_loss):
@@ -187,6 +192,8 @@ class ESPnetASRModel(AbsESPnetModel):
                 hook(self.ctc)
         if self.decoder is not None:
             g = state["grad_att"]
+            if state.get("inv_denom") is not None:
+                K.scale_by_dev(g, state["inv_denom"])
             K.scale_by_dev(g, g_loss)
             self.decoder.run_backward(state["dec"], g, dhs, hook)
         return dhs.view(state["B"], state["T"], -1)
@@ -229,8 +236,6 @@ class ESPnetASRModel(AbsESPnetModel):
         if self.decoder is not None:
             ys_in, ys_out, ys_in_lens = add_sos_eos(text_cpu, tl_cpu, self.sos, self.eos, self.ignore_id)
             prep["L"] = int(ys_in.shape[1])
-            if self.length_normalized_loss:
-                prep["denom"] = float(int((ys_out != self.ignore_id).sum()))
             host["ys_in"], host["ys_out"] = ys_in, ys_out
             host["ys_in_lens"] = ys_in_lens.to(torch.int32)
         return prep
@@ -291,6 +296,8 @@ class ESPnetASRModel(AbsESPnetModel):
         assert speech.shape[0] == speech_lengths.shape[0] == text.shape[0] == text_lengths.shape[0], (
             speech.shape, speech_lengths.shape, text.shape, text_lengths.shape)
         assert self.flat is not None, "call model.flatten() after moving the model to the GPU"
+        if torch.is_grad_enabled():
+            self.flat.ensure_grads()  # after a torch optimizer's zero_grad(set_to_none=True)
         text[text == -1] = self.ignore_id  # the reference mutates the batch (espnet_model.py:196)
         F_in = speech.shape[2] if speech.dim() == 3 else 0
         prep = self.prepare(speech_lengths, text, text_lengths, speech.shape[1], F_in, specaug_draws)

@@ -266,7 +266,12 @@ __global__ void reduce_losses_kernel(const double* __restrict__ nll, int B, int 
   n = esp::block_sum<double>(n, shd);
   if (threadIdx.x == 0) {
     const double lc = nll ? a / B : 0.0;
-    const double lat = row_loss ? l / denom : 0.0;
+    // denom <= 0: length-normalised loss (label_smoothing_loss.py:56-60 normalize_length):
+    // the count of non-ignored targets of THIS batch, taken on device (a captured graph
+    // must not bake a host value); its reciprocal goes to out[4] for the gradient scale
+    const double dn = denom > 0.f ? (double)denom : n;
+    const double lat = row_loss ? l / dn : 0.0;
+    if (denom <= 0.f) out[4] = (float)(1.0 / dn);
     out[0] = (float)lc;
     out[1] = (float)lat;
     out[2] = (n > 0) ? (float)(c / n) : 0.f;

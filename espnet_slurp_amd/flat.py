@@ -60,6 +60,19 @@ class FlatParams:
                 o, n = self.slots[id(p)]
                 self.flat[o:o + n].copy_(p.detach().reshape(-1).to(device=device, dtype=torch.float32))
                 p.data = self.flat[o:o + n].view(p.shape)
+        # floating buffers (BatchNorm running statistics) as views into one more flat buffer:
+        # DDP's per-forward buffer broadcast (X7) is then ONE collective with no packing
+        self.buffers = [b for _, b in model.named_buffers() if b.dtype == torch.float32]
+        self.other_buffers = [b for _, b in model.named_buffers() if b.is_floating_point() and b.dtype != torch.float32]
+        nb = sum(_align4(b.numel()) for b in self.buffers)
+        self.buf_flat = torch.zeros(max(nb, 4), dtype=torch.float32, device=device)
+        off = 0
+        with torch.no_grad():
+            for b in self.buffers:
+                n = b.numel()
+                self.buf_flat[off:off + n].copy_(b.detach().reshape(-1).to(device=device, dtype=torch.float32))
+                b.data = self.buf_flat[off:off + n].view(b.shape)
+                off += _align4(n)
         self.link_grads(zero=True)
 
     def view(self, p: nn.Parameter) -> torch.Tensor:
@@ -103,6 +116,14 @@ class FlatParams:
                     with torch.no_grad():
                         g.copy_(p.grad)
                 p.grad = g
+
+    def ensure_grads(self):
+        """Cheap per-step check: a caller's optimizer.zero_grad() (set_to_none=True, the torch
+        default) leaves p.grad None; re-attach the flat views (zeroed) before the backward."""
+        for _, p in self.params:
+            if p.grad is None:
+                self.link_grads()
+                return
 
     def zero_grad(self):
         self.grad.zero_()

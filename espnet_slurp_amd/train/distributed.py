@@ -57,6 +57,8 @@ class FlatGradReducer:
                 if m is not None:
                     m._grad_hook = self.module_done
 
+    sync = True  # False between the micro-batches of one optimizer step (DDP.no_sync)
+
     def _reset(self):
         self.ready = [0] * len(self.buckets)
         self.seen = set()
@@ -75,6 +77,8 @@ class FlatGradReducer:
             self.next_launch += 1
 
     def module_done(self, module):
+        if not self.sync:  # an earlier micro-batch of accum_grad: accumulate locally
+            return
         for p in module.parameters():
             if id(p) in self.seen or id(p) not in self.param_bucket:
                 continue
@@ -108,18 +112,13 @@ class FlatGradReducer:
 
     def broadcast_buffers(self, model):
         """DDP's broadcast_buffers (X7): rank 0's floating buffers (BatchNorm running stats) to
-        every replica before the forward, coalesced into ONE broadcast.  Training-mode outputs
-        do not read them, so this only keeps the replicas' eval-mode state equal to rank 0's."""
-        bufs = [b for b in model.buffers() if b.is_floating_point()]
-        if not bufs:
-            return
-        flat = torch.cat([b.detach().reshape(-1).float() for b in bufs])
-        dist.broadcast(flat, 0, group=self.group)
-        o = 0
-        for b in bufs:
-            n = b.numel()
-            b.copy_(flat[o:o + n].view_as(b))
-            o += n
+        every replica before the forward, as ONE broadcast of the flat buffer they are views
+        of (flat.py).  Training-mode outputs do not read them, so this only keeps the
+        replicas' eval-mode state equal to rank 0's."""
+        if self.flat.buffers:
+            dist.broadcast(self.flat.buf_flat, 0, group=self.group)
+        for b in self.flat.other_buffers:
+            dist.broadcast(b, 0, group=self.group)
 
 
 def fused_stats_allreduce(stats: Dict[str, torch.Tensor], weight: torch.Tensor, group=None):

@@ -54,11 +54,15 @@ class Trainer:
         # per batch signature and replayed: ~1500 launches per step cost one graph launch
         self.cuda_graph = bool(cuda_graph) and model.flat.flat.is_cuda
         self._graphs = {}
+        self.max_graphs = 32  # LRU bound on captured step graphs (each pins its workspace)
         self._key = None
+        self._acc = None      # DDP + graph + accum_grad > 1: prescaled gradient of earlier micro-batches
         self.reducer = (FlatGradReducer(model, model.flat, bucket_mb, hooks=not self.cuda_graph)
                         if self.distributed else None)
-        self.iiter = 0
-        self.n_skipped = 0
+        self.iiter = 0          # micro-batches (trainer.py:502 iiter)
+        self.n_updates = 0      # optimizer steps attempted (every accum_grad micro-batches)
+        self.n_skipped = 0      # ... of which skipped for a non-finite gradient norm
+        self._synced_updates = 0  # n_updates at the last device->host counter sync (graph mode)
         self._clip = torch.empty(3, dtype=torch.float32, device=model.flat.flat.device)
         # finite flag of the last optimizer step, read back asynchronously (pinned buffer + event)
         # and acted on just before the NEXT optimizer step: the host never drains the queue
@@ -79,12 +83,17 @@ class Trainer:
             return self._train_one_step(batch, check_finite)
 
     def _train_one_step(self, batch, check_finite):
-        if self.cuda_graph and self.options.accum_grad == 1:
+        if self.cuda_graph:
             return self._graph_step(batch)
         opts = self.options
         self.iiter += 1
+        last = self.iiter % opts.accum_grad == 0
         model = self.model
-        if self.distributed and self.reducer is not None:
+        if self.reducer is not None:
+            # gradient exchange once per optimizer step: the earlier micro-batches accumulate
+            # locally (DDP.no_sync); averaging the accumulated sum equals the reference's
+            # per-micro-batch DDP average (the all-reduce is linear)
+            self.reducer.sync = last
             self.reducer.broadcast_buffers(model)
         loss, stats, weight = model(**batch)
         stats = {k: v for k, v in stats.items() if v is not None}
@@ -95,10 +104,11 @@ class Trainer:
             loss = (loss * w).sum() / wsum * self.world
         loss = loss / opts.accum_grad
         loss.backward()
-        if self.iiter % opts.accum_grad == 0:
+        if last:
             if self.reducer is not None:
                 self.reducer.finish()
             self.resolve_pending()  # scheduler step of the previous update (if it was finite)
+            self.n_updates += 1
             clip_grad_norm_(model.flat, opts.grad_clip, self._clip)
             # the Adam kernel itself skips a non-finite update on device (trainer.py:651-667)
             self.optimizer.step(clip=self._clip)
@@ -116,32 +126,43 @@ class Trainer:
     # ---------------------------------------------------------------- HIP-graph path
     def _graph_step(self, batch):
         model = self.model
+        opts = self.options
         speech = batch["speech"]
         self.iiter += 1
-        self.resolve_pending()
+        last = self.iiter % opts.accum_grad == 0
         prep = model.prepare(batch["speech_lengths"], batch["text"], batch["text_lengths"], speech.shape[1],
                              speech.shape[2] if speech.dim() == 3 else 0)
-        sig = (tuple(speech.shape), prep.T, prep.Umax, prep.L, prep.get("n_samples", 0),
+        sig = (tuple(speech.shape), prep.T, prep.Umax, prep.L, prep.get("n_samples", 0), last,
                tuple((k, tuple(v.shape)) for k, v in sorted(prep.host.items())))
-        e = self._graphs.get(sig)
+        e = self._graphs.pop(sig, None)
         if self.distributed:  # DDP broadcast_buffers (X7), outside the graph (a collective)
             self.reducer.broadcast_buffers(model)
+        dp_accum = self.distributed and opts.accum_grad > 1
+        if dp_accum:  # this micro-batch's gradient is computed alone, then prescaled and added
+            if self._acc is None:
+                self._acc = torch.zeros_like(model.flat.grad)
+            self._acc.copy_(model.flat.grad)
+            model.flat.grad.zero_()
+        if last:
+            self.n_updates += 1
         if e is None:  # the capture call's eager warm-up IS this iteration's step
-            e = self._capture(speech, prep)
-            self._graphs[sig] = e
+            e = self._capture(speech, prep, last)
         else:
             e.speech.copy_(speech, non_blocking=True)
             prep.copy_into(e.prep)
             e.graph.replay()
             if self.distributed:
-                self._dp_tail(e.stats, e.weight)
+                self._dp_tail(e.stats, e.weight, last)
+        self._graphs[sig] = e  # most recently used last
+        while len(self._graphs) > self.max_graphs:
+            self._graphs.pop(next(iter(self._graphs)))
         return e.stats
 
     def _device_body(self, speech, prep, with_opt: bool):
         """Device-only work of one step (nothing here talks to the host)."""
         K.rng_advance(self._key)
         loss, stats, weight = self.model.forward_prepared(speech, prep)
-        loss.backward()
+        (loss / self.options.accum_grad if self.options.accum_grad > 1 else loss).backward()
         stats = {k: v for k, v in stats.items() if v is not None}
         stats["grad_norm"] = self._clip[0:1]
         if with_opt:
@@ -153,7 +174,7 @@ class Trainer:
         self.optimizer.step_device(self._clip, self.scheduler)  # counts itself only if finite
         self.model.flat.grad.zero_()
 
-    def _dp_tail(self, stats, weight):
+    def _dp_tail(self, stats, weight, last: bool = True):
         """DDP semantics after a replayed forward+backward (trainer.py:594-608 + DDP average):
         grad = sum_r (w_r / sum w) grad_r, stats weighted-averaged, then clip + Adam."""
         avg, wsum = fused_stats_allreduce({k: v for k, v in stats.items() if k != "grad_norm"}, weight)
@@ -161,25 +182,32 @@ class Trainer:
             stats[k].copy_(v)
         scale = weight.to(torch.float32).view(1) / wsum
         K.scale_by_dev(self.model.flat.grad, scale)
-        self.reducer.allreduce_sum()
-        self._opt_tail()
+        if self._acc is not None and self.options.accum_grad > 1:
+            K.scale_dropout(self.model.flat.grad, self.model.flat.grad, alpha=1.0, r=self._acc, beta=1.0)
+        if last:
+            self.reducer.allreduce_sum()
+            self._opt_tail()
 
-    def _capture(self, speech, prep):
+    def _capture(self, speech, prep, last: bool = True):
         dev = self.model.flat.flat.device
         if self._key is None:  # dropout key from the CPU generator; advanced on device per step
             self._key = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).to(dev)
         e = _GraphEntry()
         e.speech = speech.to(dev).clone()
         e.prep = prep.to_device(dev)
-        with_opt = not self.distributed
+        with_opt = last and not self.distributed
         K.set_rng_key(self._key)
+        grad_save = None
         try:
             side = torch.cuda.Stream(device=dev)
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):  # warm-up = this iteration's step (allocates workspaces)
                 stats, w = self._device_body(e.speech, e.prep, with_opt)
-                if not with_opt:
-                    self._dp_tail(stats, w)
+                if self.distributed:
+                    self._dp_tail(stats, w, last)
+                if not with_opt:  # the capture below must start from the same gradient state
+                    grad_save = self.model.flat.grad.clone()
+                    self.model.flat.grad.zero_()
             torch.cuda.current_stream(dev).wait_stream(side)
             torch.cuda.synchronize(dev)
             g = torch.cuda.CUDAGraph()
@@ -189,14 +217,21 @@ class Trainer:
             e.graph = g
         finally:
             K.set_rng_key(None)  # eager calls keep their host seeds; the graph baked the key pointer
+        if grad_save is not None:  # capturing ran nothing: restore the warm-up's gradient
+            self.model.flat.grad.copy_(grad_save)
         for k, v in stats.items():  # the warm-up step's values are this call's results
             e.stats[k].copy_(v)
         return e
 
     def sync_host_state(self):
-        """Bring the host-side optimizer / scheduler counters up to date after graph replays."""
-        if self.cuda_graph:
+        """Bring the host-side optimizer / scheduler counters up to date after graph replays,
+        and count the optimizer steps the device skipped (non-finite gradient norm)."""
+        if self.cuda_graph and getattr(self.optimizer, "_dstate", None) is not None:
+            before = self.optimizer.n_steps
             self.optimizer.sync_from_device(self.scheduler)
+            taken = self.optimizer.n_steps - before
+            self.n_skipped += (self.n_updates - self._synced_updates) - taken
+        self._synced_updates = self.n_updates
 
     def resolve_pending(self):
         """Apply the bookkeeping of the last optimizer step once its finite flag is on the host:
@@ -218,11 +253,42 @@ class Trainer:
         """Loop over (utt_id, batch) like trainer.py:502-714; returns True if every step was
         skipped (all_steps_are_invalid)."""
         self.model.train()
-        it0, sk0 = self.iiter, self.n_skipped
-        for _, batch in iterator:
+        self.sync_host_state()
+        up0, sk0 = self.n_updates, self.n_skipped
+        for _, batch in self._stop_aligned(iterator):
             stats = self.train_one_step(batch)
             if reporter is not None:
                 reporter(stats)
         self.resolve_pending()
         self.sync_host_state()
-        return (self.n_skipped - sk0) == (self.iiter - it0)
+        # trainer.py:436-440: True when no optimizer step of the epoch was applied
+        return (self.n_skipped - sk0) == (self.n_updates - up0)
+
+    def _stop_aligned(self, iterator):
+        """iterator_stop (X1, trainer.py:505-510, 716-719): every rank stops when the first one
+        runs out of batches.  The reference all-reduces a flag before EVERY batch (a host sync
+        per step); here the ranks agree once on the shortest shard length up front, which
+        gives the same batches when the iterator knows its length (the sharded sampler
+        iterators do); an iterator without len() falls back to the per-step flag."""
+        if not self.distributed:
+            yield from iterator
+            return
+        dev = self.model.flat.flat.device
+        n = len(iterator) if hasattr(iterator, "__len__") else -1
+        t = torch.tensor([n if n >= 0 else 2 ** 62], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        n_min = int(t.item())
+        if n >= 0 or n_min < 2 ** 62:
+            for i, item in enumerate(iterator):
+                if i >= n_min:
+                    break
+                yield item
+            return
+        stop = torch.zeros(1, dtype=torch.int64, device=dev)
+        for item in iterator:
+            dist.all_reduce(stop)
+            if int(stop.item()) > 0:
+                return
+            yield item
+        stop.fill_(1)
+        dist.all_reduce(stop)

@@ -206,6 +206,9 @@ int esp_ctc_loss(const float* lp, const long long* labels, int Umax, const int* 
 int esp_label_smoothing(const float* x, const long long* target, long rows, int V, int ignore,
                         float smoothing, float gscale, float* grad, double* row_loss, int* row_stat,
                         void* stream);
+/* out4 = {loss_ctc, loss_att, acc, loss}; denom <= 0 selects the length-normalised
+ * attention loss (denominator = non-ignored targets, counted on device) and then also
+ * writes out4[4] = 1 / that count (out4 must hold 5 floats). */
 int esp_reduce_losses(const double* nll, int B, int zero_inf, const double* row_loss,
                       const int* row_stat, int R, float denom, float ctc_w, float* out4,
                       void* stream);

@@ -1,0 +1,68 @@
+"""One data-parallel rank of tests/test_gpu_distributed.py (run as a child process).
+
+    python tests/dist_worker.py <out.pt> <eager|graph> <accum_grad>   (RANK / WORLD_SIZE /
+    MASTER_ADDR / MASTER_PORT from the environment)
+
+Every rank shares cuda:0 and talks over gloo (RCCL refuses two ranks on one GPU); the
+trainer code path is the multi-GPU one (bucket hooks / prescale + SUM, fused stats)."""
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from oracle import espnet_cpu as O  # noqa: E402
+from tests.helpers import build_model, load_seeded, small_cfg  # noqa: E402
+
+# global batch per micro-step: utterance lengths / label lengths, split batch[rank::world]
+# (abs_task.py:1542) -> unequal shard sizes 3 / 2, so the w_r / sum w weighting matters
+# (each rank's padded label length stays 6 / 5 across steps, so graph mode replays)
+GLOBAL = [([96, 90, 84, 80, 71], [6, 5, 5, 4, 3]), ([96, 93, 77, 70, 66], [6, 5, 2, 5, 3]),
+          ([96, 95, 90, 85, 60], [5, 5, 6, 2, 4]), ([96, 81, 80, 79, 78], [6, 4, 5, 5, 6])]
+
+
+def shard(step, rank, world):
+    lens, ulens = GLOBAL[step]
+    speech, slen, text, tlen = O.synthetic_batch(len(lens), 96, 80, 32, lens, ulens, 500 + step)
+    idx = list(range(rank, len(lens), world))
+    t = text[idx][:, : int(tlen[idx].max())]
+    return speech[idx], slen[idx], t, tlen[idx]
+
+
+def main():
+    out, mode, accum = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from espnet_slurp_amd.optimizers.fused_adam import FusedAdam
+    from espnet_slurp_amd.schedulers.warmup_lr import WarmupLR
+    from espnet_slurp_amd.train.trainer import Trainer, TrainerOptions
+    dev = torch.device("cuda:0")
+    cfg = small_cfg("latest")
+    model = build_model(cfg, dev)
+    load_seeded(model, cfg, 11)
+    model.train()
+    opt = FusedAdam(model.parameters(), model.flat, lr=2e-3, weight_decay=1e-6)
+    sch = WarmupLR(opt, warmup_steps=10)
+    tr = Trainer(model, opt, sch, TrainerOptions(grad_clip=5.0, accum_grad=accum), distributed=True,
+                 cuda_graph=(mode == "graph"))
+    stats = []
+    for step in range(len(GLOBAL)):
+        speech, slen, text, tlen = shard(step, rank, world)
+        st = tr.train_one_step(dict(speech=speech.to(dev), speech_lengths=slen, text=text, text_lengths=tlen))
+        stats.append({k: float(v) for k, v in st.items() if k != "grad_norm"})
+    tr.resolve_pending()
+    tr.sync_host_state()
+    torch.cuda.synchronize()
+    torch.save({"params": {n: p.detach().cpu() for n, p in model.named_parameters()},
+                "bufs": {n: b.detach().cpu() for n, b in model.named_buffers()},
+                "stats": stats, "n_steps": opt.n_steps, "n_updates": tr.n_updates,
+                "graphs": len(tr._graphs)}, out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

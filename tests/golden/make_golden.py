@@ -598,6 +598,10 @@ if __name__ == "__main__":
     if "small" in which:
         model_fixture("model_small_latest", small_cfg("latest"), 3, 120, [120, 97, 64], [9, 5, 7], 1)
         model_fixture("model_small_legacy", small_cfg("legacy"), 3, 120, [120, 97, 64], [9, 5, 7], 2)
+    if "lnorm" in which:  # length_normalized_loss=True (LabelSmoothingLoss normalize_length)
+        cfg = small_cfg("latest")
+        cfg.length_normalized_loss = True
+        model_fixture("model_small_lnorm", cfg, 3, 120, [120, 97, 64], [9, 5, 7], 4)
     if "c1" in which:
         c1 = O.ModelCfg(vocab_size=30, enc=O.EncCfg(kind="transformer", output_size=256, attention_heads=4,
                                                      linear_units=1024, num_blocks=4),

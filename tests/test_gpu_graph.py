@@ -12,17 +12,19 @@ from tests.helpers import build_model, load_seeded, small_cfg
 pytestmark = pytest.mark.gpu
 
 
-def _trainer(dev, graph, dropout=0.0, seed=11):
+def _trainer(dev, graph, dropout=0.0, seed=11, accum=1, lnorm=False):
     from espnet_slurp_amd.optimizers.fused_adam import FusedAdam
     from espnet_slurp_amd.schedulers.warmup_lr import WarmupLR
     from espnet_slurp_amd.train.trainer import Trainer, TrainerOptions
     cfg = small_cfg("latest")
+    cfg.length_normalized_loss = lnorm
     model = build_model(cfg, dev, dropout=dropout)
     load_seeded(model, cfg, seed)
     model.train()
     opt = FusedAdam(model.parameters(), model.flat, lr=1e-3)
     sched = WarmupLR(opt, warmup_steps=10)
-    return Trainer(model, opt, sched, TrainerOptions(grad_clip=5.0), cuda_graph=graph), model, opt, sched
+    return (Trainer(model, opt, sched, TrainerOptions(grad_clip=5.0, accum_grad=accum), cuda_graph=graph),
+            model, opt, sched)
 
 
 def _batch(dev):
@@ -115,3 +117,65 @@ def test_graph_and_eager_with_weight_gradient_stream(dev, monkeypatch):
     for losses, flat in ref[1:]:
         assert all(abs(a - b) <= 1e-6 * max(1.0, abs(a)) for a, b in zip(ref[0][0], losses))
         assert torch.allclose(ref[0][1], flat, rtol=0, atol=1e-6)
+
+
+def _batches_same_shapes(dev):
+    """Two batches with identical padded shapes but different lengths / target counts."""
+    out = []
+    for lens, ulens, seed in (([96, 80, 71], [6, 5, 4], 12), ([90, 96, 60], [6, 2, 1], 13)):
+        speech, slen, text, tlen = O.synthetic_batch(3, 96, 80, 32, lens, ulens, seed)
+        out.append(dict(speech=speech.to(dev), speech_lengths=slen, text=text, text_lengths=tlen))
+    return out
+
+
+def _copy(b):
+    return dict(b, speech=b["speech"].clone(), text=b["text"].clone())
+
+
+def test_graph_length_normalized_loss_not_baked(dev):
+    """length_normalized_loss: the denominator (non-ignored targets) differs between two
+    batches of the same shapes; the replayed graph must use the new batch's count."""
+    te, me, _, _ = _trainer(dev, False, lnorm=True)
+    tg, mg, _, _ = _trainer(dev, True, lnorm=True)
+    b1, b2 = _batches_same_shapes(dev)
+    for b in (b1, b2, b1, b2):
+        le = te.train_one_step(_copy(b))["loss"].item()
+        lg = tg.train_one_step(_copy(b))["loss"].item()
+        assert abs(le - lg) <= 1e-6 * max(1.0, abs(le)), (le, lg)
+    te.resolve_pending()
+    assert len(tg._graphs) == 1
+    assert torch.allclose(me.flat.flat, mg.flat.flat, rtol=0, atol=1e-6)
+
+
+def test_graph_accum_grad_matches_eager(dev):
+    """accum_grad=2 in graph mode (a micro-batch graph and an update graph) equals eager."""
+    te, me, oe, _ = _trainer(dev, False, accum=2)
+    tg, mg, og, _ = _trainer(dev, True, accum=2)
+    b1, b2 = _batches_same_shapes(dev)
+    for b in (b1, b2, b2, b1, b1, b2):
+        le = te.train_one_step(_copy(b))["loss"].item()
+        lg = tg.train_one_step(_copy(b))["loss"].item()
+        assert abs(le - lg) <= 1e-6 * max(1.0, abs(le)), (le, lg)
+    te.resolve_pending()
+    tg.sync_host_state()
+    assert len(tg._graphs) == 2
+    assert og.n_steps == oe.n_steps == 3 and tg.n_updates == te.n_updates == 3
+    assert torch.allclose(me.flat.flat, mg.flat.flat, rtol=0, atol=1e-6)
+
+
+def test_skipped_steps_counted_in_graph_mode(dev):
+    """A non-finite gradient norm skips the update on device; the trainer counts it
+    (all_steps_are_invalid of trainer.py:436-440) in graph and eager mode alike."""
+    for graph in (False, True):
+        t, m, o, _ = _trainer(dev, graph)
+        b = _batches_same_shapes(dev)[0]
+        t.train_one_step(_copy(b))
+        bad = _copy(b)
+        bad["speech"][0, 0, 0] = float("inf")
+        t.train_one_step(bad)
+        t.resolve_pending()
+        t.sync_host_state()
+        assert t.n_updates == 2 and t.n_skipped == 1, (graph, t.n_updates, t.n_skipped)
+        assert o.n_steps == 1
+        assert t.train_one_epoch([(None, bad)]) is True
+        assert t.train_one_epoch([(None, _copy(b))]) is False
