@@ -1,4 +1,4 @@
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread > gpurun_out/r02a_pytest_gpu.log 2>&1
+timeout -k 10 300 python -u tools/relu_flip_diag.py > gpurun_out/r02c_flip.log 2>&1

@@ -101,6 +101,7 @@ def test_two_rank_training_matches_ddp_oracle(dev, tmp_path, mode, accum):
     # exactly its own replica's chain (rank 1 starts every forward from rank 0's copy)
     for n, b in res[0]["bufs"].items():
         if "running" in n:
-            assert np.abs(b.double().numpy() - ref_bn[n].double().numpy()).max() < 1e-5, n
+            r = ref_bn[n].double().numpy()
+            assert np.abs(b.double().numpy() - r).max() < 1e-5 * max(1.0, np.abs(r).max()) + 1e-5, n
     if mode == "graph":
         assert res[0]["graphs"] == accum  # one step graph (accum 2: micro-batch + update)
