@@ -100,19 +100,16 @@ __global__ void col2im_relu_kernel(const float* __restrict__ dcol, const float* 
 // finalize pass reads each output's partials contiguously.
 constexpr int C1_CHUNK = 2048, C1_SUB = 256;
 __global__ __launch_bounds__(1024) void conv1_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dz,
-                                                          double* __restrict__ part, int B, int T, int F, int T1, int F1,
+                                                          float* __restrict__ part, int B, int T, int F, int T1, int F1,
                                                           int D, int nb) {
   __shared__ float4 patch[C1_SUB][3];
   const long npix = (long)B * T1 * F1;
   const long p0 = (long)blockIdx.x * C1_CHUNK;
   const int o = threadIdx.x;  // blockDim == D rounded up to a wave
   const bool own = o < D;
-  // fp64 accumulators: each thread sums C1_CHUNK (2048) products whose signs cancel (the
-  // weight gradient is small against its terms), so a serial fp32 chain loses ~3x the
-  // reference's fp32 accuracy at T=1500; the kernel stays HBM-bound on the dz reads
-  double acc[10];
+  float acc[10];
 #pragma unroll
-  for (int k = 0; k < 10; ++k) acc[k] = 0.0;
+  for (int k = 0; k < 10; ++k) acc[k] = 0.f;
   for (long s0 = p0; s0 < p0 + C1_CHUNK && s0 < npix; s0 += C1_SUB) {
     __syncthreads();
     for (int e = threadIdx.x; e < C1_SUB * 12; e += blockDim.x) {
@@ -139,14 +136,13 @@ __global__ __launch_bounds__(1024) void conv1_wgrad_kernel(const float* __restri
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const float4 a = patch[q + u][0], bq = patch[q + u][1], c = patch[q + u][2];
-        const double gd = g[u];
-        acc[0] += gd * a.x; acc[1] += gd * a.y; acc[2] += gd * a.z; acc[3] += gd * a.w;
-        acc[4] += gd * bq.x; acc[5] += gd * bq.y; acc[6] += gd * bq.z; acc[7] += gd * bq.w;
-        acc[8] += gd * c.x; acc[9] += gd;
+        acc[0] += g[u] * a.x; acc[1] += g[u] * a.y; acc[2] += g[u] * a.z; acc[3] += g[u] * a.w;
+        acc[4] += g[u] * bq.x; acc[5] += g[u] * bq.y; acc[6] += g[u] * bq.z; acc[7] += g[u] * bq.w;
+        acc[8] += g[u] * c.x; acc[9] += g[u];
       }
     }
     for (; q < lim; ++q) {
-      const double gg = dzp[(long)q * D];
+      const float gg = dzp[(long)q * D];
       const float4 a = patch[q][0], bq = patch[q][1], c = patch[q][2];
       acc[0] += gg * a.x; acc[1] += gg * a.y; acc[2] += gg * a.z; acc[3] += gg * a.w;
       acc[4] += gg * bq.x; acc[5] += gg * bq.y; acc[6] += gg * bq.z; acc[7] += gg * bq.w;
@@ -155,21 +151,21 @@ __global__ __launch_bounds__(1024) void conv1_wgrad_kernel(const float* __restri
   }
   if (own)
 #pragma unroll
-    for (int k = 0; k < 10; ++k) part[((long)o * 10 + k) * nb + blockIdx.x] = acc[k];  // fp64 partials
+    for (int k = 0; k < 10; ++k) part[((long)o * 10 + k) * nb + blockIdx.x] = acc[k];
 }
 
 // one block per (o, k) output: fixed-order strided sum + LDS tree (deterministic)
-__global__ __launch_bounds__(256) void conv1_wgrad_finalize(const double* __restrict__ part, int nb, int D,
+__global__ __launch_bounds__(256) void conv1_wgrad_finalize(const float* __restrict__ part, int nb, int D,
                                                             float* __restrict__ dW, float* __restrict__ db) {
-  __shared__ double sh[16];
+  __shared__ float sh[16];
   const int e = blockIdx.x;
-  double s = 0.0;
+  float s = 0.f;
   for (int p = threadIdx.x; p < nb; p += blockDim.x) s += part[(long)e * nb + p];
-  s = esp::block_sum<double>(s, sh);
+  s = esp::block_sum(s, sh);
   if (threadIdx.x == 0) {
     const int o = e / 10, k = e - o * 10;
-    if (k < 9) dW[o * 9 + k] += (float)s;
-    else db[o] += (float)s;
+    if (k < 9) dW[o * 9 + k] += s;
+    else db[o] += s;
   }
 }
 
@@ -212,7 +208,7 @@ ESP_API int esp_col2im_relu(const float* dcol, const float* z1, float* dz1, int 
   return 0;
 }
 
-// workspace: >= ceil(B*T1*F1/2048) * D * 10 doubles.  dW (D,9) and db (D) accumulated.
+// workspace: >= ceil(B*T1*F1/2048) * D * 10 floats.  dW (D,9) and db (D) accumulated.
 ESP_API int esp_conv1_wgrad(const float* x, const float* dz1, float* dW, float* db, int B, int T, int F, int D,
                             float* work, void* stream) {
   const int T1 = (T - 3) / 2 + 1, F1 = (F - 3) / 2 + 1;
@@ -220,9 +216,8 @@ ESP_API int esp_conv1_wgrad(const float* x, const float* dz1, float* dW, float* 
   const int nb = (int)((npix + C1_CHUNK - 1) / C1_CHUNK);
   hipStream_t st = (hipStream_t)stream;
   ESP_ARG_CHECK(D <= 1024, "esp_conv1_wgrad: D > 1024");
-  double* part = reinterpret_cast<double*>(work);
-  hipLaunchKernelGGL(conv1_wgrad_kernel, dim3(nb), dim3((D + 63) / 64 * 64), 0, st, x, dz1, part, B, T, F, T1, F1, D, nb);
-  hipLaunchKernelGGL(conv1_wgrad_finalize, dim3(D * 10), dim3(256), 0, st, part, nb, D, dW, db);
+  hipLaunchKernelGGL(conv1_wgrad_kernel, dim3(nb), dim3((D + 63) / 64 * 64), 0, st, x, dz1, work, B, T, F, T1, F1, D, nb);
+  hipLaunchKernelGGL(conv1_wgrad_finalize, dim3(D * 10), dim3(256), 0, st, work, nb, D, dW, db);
   ESP_CHECK_LAUNCH("esp_conv1_wgrad");
   return 0;
 }

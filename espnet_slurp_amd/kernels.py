@@ -460,7 +460,7 @@ def col2im_relu(dcol, z1, dz1, B, T1, F1, D):
 def conv1_wgrad(x, dz1, dW, db, B, T, F, D):
     T1, F1 = (T - 3) // 2 + 1, (F - 3) // 2 + 1
     nb = (B * T1 * F1 + 2047) // 2048
-    ws = _work(8 * nb * D * 10, x.device)  # fp64 partial sums
+    ws = _work(4 * nb * D * 10, x.device)
     _native.call("esp_conv1_wgrad", _p(x), _p(dz1), _p(dW), _p(db), B, T, F, D, _p(ws), _st())
 
 

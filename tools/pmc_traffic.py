@@ -12,6 +12,12 @@ import sys
 
 def per_dispatch(d, counter):
     out = {}
+    for f in glob.glob(os.path.join(d, "*.db")):  # rocpd output (rocprofv3 default on ROCm 7.2)
+        import sqlite3
+        c = sqlite3.connect(f)
+        for did, name, val in c.execute("select dispatch_id, kernel_name, sum(value) from counters_collection "
+                                        "where counter_name = ? group by dispatch_id", (counter,)):
+            out[int(did)] = (name, float(val))
     for f in glob.glob(os.path.join(d, "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] == counter:
@@ -27,13 +33,16 @@ def main():
     wk = [v for n, v in write.values() if fam in n]
     fetch_b = 2.0 * 1024 * sum(fk) / len(fk)
     write_b = 1024 * sum(wk) / len(wk)
-    print(json.dumps({
+    out = {
         "kernel": fam + "<*>", "launches_fetch_pass": len(fk), "launches_write_pass": len(wk),
         "fetch_bytes_per_launch": round(fetch_b), "write_bytes_per_launch": round(write_b),
         "hbm_bytes_per_launch": round(fetch_b + write_b),
         "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate runs of bench.py --eager --steps 1 "
                   "--warmup 1; FETCH_SIZE x2 (gfx950 wide-read undercount), KB x1024",
-    }, indent=1))
+    }
+    if len(sys.argv) > 3:  # the workload the passes ran (bench.py matches on it)
+        out.update(batch=int(sys.argv[3]), workload=sys.argv[4] if len(sys.argv) > 4 else "C2 d=256 12L")
+    print(json.dumps(out, indent=1))
 
 
 if __name__ == "__main__":
