@@ -59,6 +59,9 @@ SIGNATURES = {
     "esp_relpos_attn_fwd": [P, P, P, L, P, L, I, I, F, P, P, P, F, U64, I, L, P],
     "esp_attn_softmax_bwd_relpos": [P, P, P, P, L, F, U64, F, L, I, L, P],
     "esp_relpos_attn_bwd": [P, L, P, L, P, P, P, L, I, I, F, F, U64, I, L, P],
+    "esp_relpos_flash_fwd": [P, P, P, L, P, L, P, L, I, I, I, F, P, P, L, P, F, U64, I, P],
+    "esp_relpos_flash_bwd": [P, P, P, L, P, L, P, L, I, I, I, F, P, P, P, L, P, F, U64, I, P, L, P, P, L, P, P, P],
+    "esp_relpos_dp": [P, L, P, I, I, I, I, P, L, P, P, P, P, P, L, P, L, P],
     "esp_fbank_fwd": [P, L, P, I, I, I, I, P, P, P, P, P, I, P, I, P],
     "esp_global_mvn": [P, P, I, I, I, P, P, I, I, P],
     "esp_conv2_dgrad": [P, P, P, P, I, I, I, I, P, P, P],
@@ -77,7 +80,7 @@ SIGNATURES = {
 }
 _RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I, "esp_set_gemm_compute": I,
              "esp_get_gemm_compute": I}
-ABI_VERSION = 13  # bumped whenever a signature in include/espnet_mi355.h changes
+ABI_VERSION = 14  # bumped whenever a signature in include/espnet_mi355.h changes
 
 _lib = None
 

@@ -182,10 +182,22 @@ class RelPositionMultiHeadedAttention(nn.Module):
         q_v = empty(Z * T * dk, like=x2d)
         K.heads_split(qkv, 3 * D, 0, B, T, H, dk, self.pos_bias_u, q_u)
         K.heads_split(qkv, 3 * D, 0, B, T, H, dk, self.pos_bias_v, q_v)
-        Tp, Pp = K.pitch(T), K.pitch(P)  # 16-B aligned score rows
-        ac = empty(Z * T * Tp, like=x2d)
         pa = self.p if training else 0.0
         sa = seeds.next()
+        if K.flash_ok(T, dk):
+            # scores, softmax, dropout and P.V in one kernel: only ctx and 2 floats per row to HBM
+            ctx_ = empty(M, D, like=x2d)
+            stats = empty(Z * T * 2, like=x2d)
+            K.relpos_flash_fwd(q_u, q_v, qkv, 3 * D, qkv, 3 * D, p, D, relpos, B, H, math.sqrt(dk), klen, ctx_, D,
+                               stats, pa, sa, T, k_off=D, v_off=2 * D)
+            out = empty(M, D, like=x2d)
+            pr = p_res if training else 0.0
+            so = seeds.next()
+            self.linear_out.fwd(ctx_, out, drop_p=pr, seed=so, R=resid, beta=1.0)
+            return out, Ctx(x=x2d, qkv=qkv, p=p, pos=pos_emb, q_u=q_u, q_v=q_v, ctx=ctx_, stats=stats, klen=klen,
+                            flash=True, pa=pa, sa=sa, pr=pr, so=so, B=B, T=T, P=P)
+        Tp, Pp = K.pitch(T), K.pitch(P)  # 16-B aligned score rows
+        ac = empty(Z * T * Tp, like=x2d)
         pdrop = empty(Z * T * Tp, like=x2d) if pa > 0 else None
         if not self.legacy and K.relpos_fused_ok(T, dk):
             # ac and the bd band on the MFMA inside the softmax kernel: only attn reaches HBM
@@ -211,7 +223,7 @@ class RelPositionMultiHeadedAttention(nn.Module):
         so = seeds.next()
         self.linear_out.fwd(ctx_, out, drop_p=pr, seed=so, R=resid, beta=1.0)
         return out, Ctx(x=x2d, qkv=qkv, p=p, pos=pos_emb, q_u=q_u, q_v=q_v, attn=attn, pv=pv, ctx=ctx_,
-                        pa=pa, sa=sa, pr=pr, so=so, B=B, T=T, P=P)
+                        flash=False, pa=pa, sa=sa, pr=pr, so=so, B=B, T=T, P=P)
 
     def bwd(self, c, dout):
         H, dk = self.h, self.d_k
@@ -223,6 +235,8 @@ class RelPositionMultiHeadedAttention(nn.Module):
         K.scale_dropout(dout, dz, drop_p=c.pr, seed=c.so)
         dctx = self.linear_out.bwd(dz, c.ctx)
         dqkv = empty(M, 3 * D, like=dout)
+        if c.flash:
+            return self._bwd_flash(c, dctx, dqkv)
         Tp, Pp = K.pitch(T), K.pitch(P)
         dS = empty(Z * T * Tp, like=dout)
         dbd = empty(Z * T * Pp, like=dout)
@@ -269,6 +283,43 @@ class RelPositionMultiHeadedAttention(nn.Module):
         gw, gb = self._wqkv(grad=True)
         K.linear_bwd_weight(dqkv, c.x, gw, gb)
         dx = empty(M, D, like=dout)
+        K.linear_bwd_data(dqkv, w, dx)
+        return dx
+
+
+    def _bwd_flash(self, c, dctx, dqkv):
+        """Flash backward: scores recomputed per (z, 32 rows); dq (q_u and q_v paths) and the
+        pos_bias partials in-kernel; dK / dV as batched GEMMs over the dS / P_drop it writes;
+        linear_pos gradient from dS along its diagonals (no dbd tensor)."""
+        H, dk = self.h, self.d_k
+        D = H * dk
+        B, T, P = c.B, c.T, c.P
+        M, Z = B * T, H * B
+        rel = 2 if self.legacy else 1
+        Tp = K.pitch(T)
+        nqb = (T + 31) // 32
+        dS = empty(Z * T * Tp, like=dctx)
+        pd = empty(Z * T * Tp, like=dctx)
+        bias_part = empty(Z * nqb * 2 * dk, like=dctx)
+        carry = empty(Z * nqb * dk, like=dctx) if rel == 2 else None
+        K.relpos_flash_bwd(c.q_u, c.q_v, c.qkv, 3 * D, c.qkv, 3 * D, c.p, D, rel, B, H, math.sqrt(dk), c.klen, c.ctx,
+                           dctx, D, c.stats, c.pa, c.sa, T, dqkv, 3 * D, dS, pd, Tp, bias_part, carry,
+                           k_off=D, v_off=2 * D)
+        # dV = P_drop^T dctx -> dqkv[:, 2D:3D];  dK = dS^T q_u -> dqkv[:, D:2D]
+        K.gemm(T, dk, T, pd, dctx, dqkv, mode_a=K.RC, lda=Tp, mode_b=K.RC, ldb=D, ldc=3 * D, c_off=2 * D,
+               batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * D), sc=(dk, T * 3 * D))
+        K.gemm(T, dk, T, dS, c.q_u, dqkv, mode_a=K.RC, lda=Tp, mode_b=K.RC, ldb=dk, ldc=3 * D, c_off=D,
+               batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(B * T * dk, T * dk), sc=(dk, T * 3 * D))
+        dp = empty(P, D, like=dctx)
+        K.relpos_dp(dS, Tp, c.q_v, rel, B, H, T, dp, D, bias_part, carry, self.pos_bias_u.grad.view(-1),
+                    self.pos_bias_v.grad.view(-1), dqkv, 3 * D)
+        del dS, pd
+        K.gemm(D, D, P, dp, c.pos, self.linear_pos.weight.grad, mode_a=K.RC, lda=D, mode_b=K.RC, ldb=D, ldc=D,
+               R=self.linear_pos.weight.grad, beta=1.0)
+        w, _ = self._wqkv()
+        gw, gb = self._wqkv(grad=True)
+        K.linear_bwd_weight(dqkv, c.x, gw, gb)
+        dx = empty(M, D, like=dctx)
         K.linear_bwd_data(dqkv, w, dx)
         return dx
 

@@ -444,6 +444,46 @@ def relpos_attn_bwd(dctx, ldd, vmat, ldv, attn, dS, dbd, ldp, nb, H, sqrt_dk, dr
                  float(sqrt_dk), float(drop_p), int(seed) & (2 ** 64 - 1), T, lds, _st())
 
 
+# Flash-style rel-pos attention (csrc/flash_relpos.hip): the default for d_k = 64, T <= 512
+# (ESP_FLASH_ATTN=0 restores the materialised-probability path of attention.hip + GEMMs)
+FLASH_ATTN = os.environ.get("ESP_FLASH_ATTN", "1") == "1"
+_DP_WS = _Workspace()
+
+
+def flash_ok(T: int, dk: int) -> bool:
+    return FLASH_ATTN and dk == 64 and 1 <= T <= 512
+
+
+def relpos_flash_fwd(q_u, q_v, kmat, ldk, vmat, ldv, p, ldp_row, rel, nb, H, sqrt_dk, klen_i32, ctx, ldc, stats,
+                     drop_p, seed, T, k_off=0, v_off=0):
+    """ctx = dropout(softmax((q_u k^T + rel_shift(q_v p^T)) / sqrt_dk)) v in one kernel per
+    (z, 32 rows); stats (Z, T, 2) = row max and 1/sum for the backward."""
+    _f32(q_u, q_v, kmat, vmat, p, ctx, stats)
+    _native.call("esp_relpos_flash_fwd", _p(q_u), _p(q_v), _p(kmat, k_off), ldk, _p(vmat, v_off), ldv, _p(p), ldp_row,
+                 int(rel), nb, H, float(sqrt_dk), _p(klen_i32), _p(ctx), ldc, _p(stats), float(drop_p),
+                 int(seed) & (2 ** 64 - 1), T, _st())
+
+
+def relpos_flash_bwd(q_u, q_v, kmat, ldk, vmat, ldv, p, ldp_row, rel, nb, H, sqrt_dk, klen_i32, ctx, dctx, ldc,
+                     stats, drop_p, seed, T, dq, ldq, dS, pdrop, lds, bias_part, carry, k_off=0, v_off=0, dq_off=0):
+    _f32(q_u, q_v, kmat, vmat, p, ctx, dctx, stats, dq, dS, pdrop, bias_part, carry)
+    _native.call("esp_relpos_flash_bwd", _p(q_u), _p(q_v), _p(kmat, k_off), ldk, _p(vmat, v_off), ldv, _p(p),
+                 ldp_row, int(rel), nb, H, float(sqrt_dk), _p(klen_i32), _p(ctx), _p(dctx), ldc, _p(stats),
+                 float(drop_p), int(seed) & (2 ** 64 - 1), T, _p(dq, dq_off), ldq, _p(dS), _p(pdrop), lds,
+                 _p(bias_part), _p(carry), _st())
+
+
+def relpos_dp(dS, lds, q_v, rel, nb, H, T, dp, ldp, bias_part, carry, du, dv, dq, ldq, dq_off=0):
+    """linear_pos gradient input dp (P x 64H) from dS along its diagonals; pos_bias grads += the
+    flash backward's column sums; legacy carries into dq."""
+    _f32(dS, q_v, dp, bias_part, carry, du, dv, dq)
+    ng = (nb + 7) // 8
+    nfl = H * ng * (2 * T - 1) * 64
+    ws = _DP_WS.get(4 * nfl, dS.device)
+    _native.call("esp_relpos_dp", _p(dS), lds, _p(q_v), int(rel), nb, H, T, _p(dp), ldp, _p(bias_part), _p(carry),
+                 _p(du), _p(dv), _p(dq, dq_off), ldq, _p(ws), ws.numel() // 4, _st())
+
+
 def relshift_bwd(dS, dbd, relpos, Z, T, P, lds=None, ldp=None):
     _native.call("esp_relshift_bwd", _p(dS), lds or T, _p(dbd), ldp or P, relpos, Z, T, P, _st())
 

@@ -145,6 +145,34 @@ int esp_attn_softmax_bwd_relpos(const float* attn, const float* dP, float* dS, f
 int esp_relpos_attn_bwd(const float* dctx, long ldd, const float* vmat, long ldv, const float* attn,
                         float* dS, float* dbd, long ldp, int nb, int H, float sqrt_dk, float drop_p,
                         unsigned long long seed, int T, long lds, void* stream);
+/* Flash-style rel-pos self-attention (csrc/flash_relpos.hip), replacing attention.py:64-96 with
+ * the latest (rel = 1, attention.py:240-263, P = 2T-1 position rows) or legacy (rel = 2,
+ * attention.py:145-165 rel_shift, P = T rows) score assembly; d_k = 64, T <= 512.
+ * q_u = q + pos_bias_u, q_v = q + pos_bias_v: (Z, T, 64) head-major, z = h*nb + b.  k / v rows at
+ * kmat + (b*T + j)*ldk + 64h (vmat / ldv alike), p rows at p + row*ldp_row + 64h.
+ * Forward: ctx (rows b*T + i, pitch ldc, head slice 64h) = dropout(softmax(s)) v, and the row
+ * statistics stats (Z, T, 2) = {max, 1/sum} the backward recomputes P from.  No (Z,T,T) tensor. */
+int esp_relpos_flash_fwd(const float* qu, const float* qv, const float* kmat, long ldk, const float* vmat,
+                         long ldv, const float* p, long ldp_row, int rel, int nb, int H, float sqrt_dk,
+                         const int* klen, float* ctx, long ldc, float* stats, float drop_p,
+                         unsigned long long seed, int T, void* stream);
+/* Backward of esp_relpos_flash_fwd: recomputes the scores, writes dq (= dq_u + dq_v, rows b*T + i,
+ * pitch ldq, head slice 64h; overwritten), dS = dL/d(ac + bd) and the dropped probabilities
+ * pdrop (Z, T, lds) for the key-side GEMMs dK = dS^T q_u and dV = pdrop^T dctx, the per-block
+ * pos_bias column sums bias_part (Z, ceil(T/32), 2, 64) and, for legacy, carry (Z, ceil(T/32), 64).
+ * ctx / dctx: the forward output and its gradient (pitch ldc). */
+int esp_relpos_flash_bwd(const float* qu, const float* qv, const float* kmat, long ldk, const float* vmat,
+                         long ldv, const float* p, long ldp_row, int rel, int nb, int H, float sqrt_dk,
+                         const int* klen, const float* ctx, const float* dctx, long ldc, const float* stats,
+                         float drop_p, unsigned long long seed, int T, float* dq, long ldq, float* dS,
+                         float* pdrop, long lds, float* bias_part, float* carry, void* stream);
+/* linear_pos gradient input from dS and q_v: dp (P x 64H, pitch ldp; overwritten) =
+ * sum_{b,i} dbd^T q_v with the rel_shift adjoint read along the diagonals of dS (no dbd tensor);
+ * pos_bias_u / pos_bias_v gradients += the column sums of esp_relpos_flash_bwd (du, dv: H x 64);
+ * legacy: adds each block's carry to dq (pitch ldq).  work: >= H * ceil(nb/8) * (2T-1) * 64 floats. */
+int esp_relpos_dp(const float* dS, long lds, const float* qv, int rel, int nb, int H, int T, float* dp, long ldp,
+                  const float* bias_part, const float* carry, float* du, float* dv, float* dq, long ldq,
+                  float* work, long work_floats, void* stream);
 /* Fused latest rel-pos scores + softmax (attention.py:240-263 with the latest rel_shift,
  * embedding.py:173-244): bd_shift[i][j] = q_v[i] . p[j + T-1-i] is computed on the MFMA per
  * 32-row block inside the kernel (no (Z,T,2T-1) bd tensor), then s = (ac + bd_shift)/sqrt(dk),
