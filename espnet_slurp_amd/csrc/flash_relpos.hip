@@ -49,6 +49,7 @@ struct FlashArgs {
   float* bias_part;              // bwd: (Z, nqb, 2, 64) column sums of dq_u, dq_v
   float* carry;                  // bwd legacy: (Z, nqb, 64)
   int nb, T, WP, nqb, nblk, DSP;
+  int band_sz;                   // bwd: floats of the band / partials region (ds follows it)
   float sqrt_dk, dscale;
   uint32_t thr;
   uint64_t seed;
@@ -276,7 +277,7 @@ __global__ __launch_bounds__(BW_NT, 1) void relpos_flash_bwd_kernel(FlashArgs a)
   const int T = a.T;
   const int nbd = (T + FR - 1 + 31) / 32;
   float* sbd = smem;                                 // band window [33][WP]; later the dq partials [8][32][36]
-  float* ds = smem + (FR + 1) * a.WP;                // dS rows of the block [32][DSP] (keys >= T zero)
+  float* ds = smem + a.band_sz;                      // dS rows of the block [32][DSP] (keys >= T zero)
   float* qs = ds + FR * a.DSP;                       // q_u rows [32][RP]
   float* gs = qs + FR * RP;                          // dctx rows [32][RP]
   float* qst = gs + FR * RP;                         // [3][32] row max, 1/sum, D_i
@@ -618,7 +619,7 @@ static size_t flash_fwd_lds(int T, int rel, int* WP) {
   const size_t part = (size_t)4 * FR * (FDK + 4);
   return ((band > part ? band : part) + 8 * FR) * sizeof(float);
 }
-static size_t flash_bwd_lds(int T, int* WP, int* DSP) {
+static size_t flash_bwd_lds(int T, int* WP, int* DSP, int* band_sz) {
   const int nbd = (T + FR - 1 + 31) / 32;
   *WP = nbd * 32 + 4;
   const int nac = (T + 31) / 32;
@@ -627,6 +628,7 @@ static size_t flash_bwd_lds(int T, int* WP, int* DSP) {
   const size_t part = (size_t)BW_WAVES * FR * 36;
   if (band < part) band = part;
   if (band < (size_t)BW_WAVES * FDK) band = BW_WAVES * FDK;
+  *band_sz = (int)band;
   return (band + (size_t)FR * *DSP + 2 * (size_t)FR * RP + 3 * FR) * sizeof(float);
 }
 
@@ -688,7 +690,7 @@ ESP_API int esp_relpos_flash_bwd(const float* qu, const float* qv, const float* 
   a.dscale = a.thr ? 1.f / (1.f - drop_p) : 1.f;
   a.seed = seed;
   a.key = esp::rng_key_ptr();
-  const size_t shm = flash_bwd_lds(T, &a.WP, &a.DSP);
+  const size_t shm = flash_bwd_lds(T, &a.WP, &a.DSP, &a.band_sz);
   ESP_ARG_CHECK(shm <= 160 * 1024, "esp_relpos_flash_bwd: T=%d needs %zu B of LDS", T, shm);
   hipStream_t st = (hipStream_t)stream;
   if (rel == 1) hipLaunchKernelGGL(relpos_flash_bwd_kernel<1>, dim3(a.nblk), dim3(BW_NT), shm, st, a);

@@ -70,6 +70,7 @@ def test_relpos_mha_fused_dk64(dev, T, klens, fused_bwd, monkeypatch):
     several 32-row blocks incl. a partial last block, against the fp64 oracle."""
     from espnet_slurp_amd import kernels as K
     monkeypatch.setattr(K, "FUSED_ATTN_BWD", fused_bwd)
+    monkeypatch.setattr(K, "FLASH_ATTN", False)  # the materialised paths (flash: tests/test_gpu_flash.py)
     torch.manual_seed(3)
     B, D, H = 3, 256, 4
     assert K.relpos_fused_ok(T, D // H)
@@ -99,6 +100,7 @@ def test_relpos_fused_matches_unfused_with_dropout(dev, monkeypatch):
     """Same seeds -> the fused kernel reproduces the unfused path's attention probabilities and
     dropout masks (mask index row*T + j) and therefore the same block output."""
     from espnet_slurp_amd import kernels as K
+    monkeypatch.setattr(K, "FLASH_ATTN", False)  # the materialised paths (flash: tests/test_gpu_flash.py)
     torch.manual_seed(4)
     B, T, D, H = 2, 100, 256, 4
     klen = torch.tensor([100, 61]).int().to(dev)

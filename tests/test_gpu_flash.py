@@ -76,9 +76,13 @@ def test_flash_matches_materialised_path_with_dropout(dev, legacy, T, monkeypatc
     (o1, d1, g1), (o2, d2, g2) = outs
     assert rel_err(o1, o2) < 1e-5
     assert rel_err(d1, d2) < 1e-5
+    scale = max(float(v.abs().max()) for v in g2.values())
     for n in g1:
-        scale = max(float(v.abs().max()) for v in g2.values())
-        assert float((g1[n] - g2[n]).abs().max()) <= 2e-5 * max(float(g2[n].abs().max()), 1e-3 * scale), n
+        gm = float(g2[n].abs().max())
+        if gm < 1e-5 * scale:  # exactly-zero gradients (key bias): fp32 noise on both sides
+            assert float(g1[n].abs().max()) < 1e-5 * scale, n
+            continue
+        assert float((g1[n] - g2[n]).abs().max()) <= 2e-5 * gm, (n, float((g1[n] - g2[n]).abs().max()), gm)
 
 
 def test_flash_graph_replay_deterministic(dev):
