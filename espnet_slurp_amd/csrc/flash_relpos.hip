@@ -51,6 +51,7 @@ struct FlashArgs {
   int nb, T, WP, nqb, nblk, DSP;
   int band_sz;                   // bwd: floats of the band / partials region (ds follows it)
   float sqrt_dk, dscale;
+  float inv_sqrt_dk;             // 1/sqrt(d_k) = 1/8 exactly for d_k = 64: x * inv == x / sqrt(d_k)
   uint32_t thr;
   uint64_t seed;
   const uint64_t* key;
@@ -166,23 +167,36 @@ __global__ __launch_bounds__(256, 2) void relpos_flash_fwd_kernel(FlashArgs a) {
   // S^T tiles: key rows on registers (il), query on the lane
   const int i = i0 + l32;
   f32x16 sc[NTA];
+  float kf[2][16];  // k rows of the current tile; the next tile's are requested after its MFMAs
+  if (wave < nac) load_row64(a.kmat + ((long)b * T + min(wave * 32 + l32, T - 1)) * a.ldk + FDK * head, hf, kf);
 #pragma unroll
   for (int t = 0; t < NTA; ++t) {
     const int ct = wave + 4 * t;
     if (ct < nac) {
-      float kf[2][16];
-      load_row64(a.kmat + ((long)b * T + min(ct * 32 + l32, T - 1)) * a.ldk + FDK * head, hf, kf);
       const f32x16 acc = mfma_rows(kf, bq);
+      if (t + 1 < NTA && ct + 4 < nac)
+        load_row64(a.kmat + ((long)b * T + min((ct + 4) * 32 + l32, T - 1)) * a.ldk + FDK * head, hf, kf);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int j = ct * 32 + il_of(r, hf);
-        sc[t][r] = j < kl ? (acc[r] + band_at<REL>(sbd, a.WP, l32, i, j)) / a.sqrt_dk : -INFINITY;
+        sc[t][r] = j < kl ? (acc[r] + band_at<REL>(sbd, a.WP, l32, i, j)) * a.inv_sqrt_dk : -INFINITY;
       }
     } else {
 #pragma unroll
       for (int r = 0; r < 16; ++r) sc[t][r] = -INFINITY;
     }
   }
+  // v rows of the first tile fly during the softmax reductions
+  float vv[2][16];
+  auto load_v = [&](int ct) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float* vr = a.vmat + ((long)b * T + min(ct * 32 + il_of(r, hf), T - 1)) * a.ldv + FDK * head + l32;
+      vv[0][r] = vr[0];
+      vv[1][r] = vr[32];
+    }
+  };
+  if (wave < nac) load_v(wave);
   // row softmax of query i: in-lane over (t, r), across the lane halves, across the 4 waves
   float m = -INFINITY;
 #pragma unroll
@@ -219,23 +233,21 @@ __global__ __launch_bounds__(256, 2) void relpos_flash_fwd_kernel(FlashArgs a) {
   for (int t = 0; t < NTA; ++t) {
     const int ct = wave + 4 * t;
     if (ct >= nac) continue;
-    float vv[2][16];
+    float pe[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float* vr = a.vmat + ((long)b * T + min(ct * 32 + il_of(r, hf), T - 1)) * a.ldv + FDK * head + l32;
-      vv[0][r] = vr[0];
-      vv[1][r] = vr[32];
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      float pe = sc[t][r] * inv;
+      pe[r] = sc[t][r] * inv;
       if (a.thr) {
         const int j = ct * 32 + il_of(r, hf);
-        pe = esp::keep_elem(seed, rowbase + (uint64_t)j, a.thr) ? pe * a.dscale : 0.f;
+        pe[r] = esp::keep_elem(seed, rowbase + (uint64_t)j, a.thr) ? pe[r] * a.dscale : 0.f;
       }
-      cacc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(pe, vv[0][r], cacc[0], 0, 0, 0);
-      cacc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(pe, vv[1][r], cacc[1], 0, 0, 0);
     }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      cacc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(pe[r], vv[0][r], cacc[0], 0, 0, 0);
+      cacc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(pe[r], vv[1][r], cacc[1], 0, 0, 0);
+    }
+    if (t + 1 < NTA && ct + 4 < nac) load_v(ct + 4);
   }
   // fixed-order sum of the 4 waves' partials through LDS, float4 stores of the ctx rows
   constexpr int PP = FDK + 4;
@@ -314,11 +326,13 @@ __global__ __launch_bounds__(BW_NT, 1) void relpos_flash_bwd_kernel(FlashArgs a)
     const int kmin = T - FR - i0;
     float aq[2][16];
     load_row64(a.qv + ((long)z * T + min(i0 + l32, T - 1)) * FDK, hf, aq);
+    float bq[2][16];
+    if (wave < nbd) load_row64(p_virt_row<REL>(a, kmin + wave * 32 + l32, head), hf, bq);
 #pragma unroll 1
     for (int ct = wave; ct < nbd; ct += BW_WAVES) {
-      float bq[2][16];
-      load_row64(p_virt_row<REL>(a, kmin + ct * 32 + l32, head), hf, bq);
       const f32x16 acc = mfma_rows(aq, bq);
+      if (ct + BW_WAVES < nbd)  // next tile's p rows fly during this tile's stores
+        load_row64(p_virt_row<REL>(a, kmin + (ct + BW_WAVES) * 32 + l32, head), hf, bq);
 #pragma unroll
       for (int r = 0; r < 16; ++r) sbd[il_of(r, hf) * a.WP + ct * 32 + l32] = acc[r];
     }
@@ -343,30 +357,38 @@ __global__ __launch_bounds__(BW_NT, 1) void relpos_flash_bwd_kernel(FlashArgs a)
 
   // scores (keys on lanes), P, dP, dS per key tile (tiles 0..7 to waves 0..7, 8..15 to waves
   // 7..0: the waves with one band tile take the second score tile); dS / P_drop to HBM, dS to LDS
+  const int ct0 = wave, ct1 = 2 * BW_WAVES - 1 - wave;
+  float kf[2][16], vf[2][16];  // k / v rows of the current key tile; the next tile's are loaded
+  if (ct0 < nac) {             // as soon as the current tile's MFMAs have consumed them
+    load_row64(a.kmat + ((long)b * T + min(ct0 * 32 + l32, T - 1)) * a.ldk + FDK * head, hf, kf);
+    load_row64(a.vmat + ((long)b * T + min(ct0 * 32 + l32, T - 1)) * a.ldv + FDK * head, hf, vf);
+  }
 #pragma unroll 1
   for (int k = 0; k < 2; ++k) {
-    const int ct = k == 0 ? wave : 2 * BW_WAVES - 1 - wave;
+    const int ct = k == 0 ? ct0 : ct1;
     if (ct >= nac) continue;
     const int j = ct * 32 + l32;
+    const bool nxt = k == 0 && ct1 < nac;
+    const int jn = min(ct1 * 32 + l32, T - 1);
     f32x16 ac, dp;
     {
-      float af[2][16], kf[2][16];
-      load_row64(a.kmat + ((long)b * T + min(j, T - 1)) * a.ldk + FDK * head, hf, kf);
+      float af[2][16];
       load_row64(qs + l32 * RP, hf, af);
       ac = mfma_rows(af, kf);
+      if (nxt) load_row64(a.kmat + ((long)b * T + jn) * a.ldk + FDK * head, hf, kf);
     }
     {
-      float af[2][16], vf[2][16];
-      load_row64(a.vmat + ((long)b * T + min(j, T - 1)) * a.ldv + FDK * head, hf, vf);
+      float af[2][16];
       load_row64(gs + l32 * RP, hf, af);
       dp = mfma_rows(af, vf);
+      if (nxt) load_row64(a.vmat + ((long)b * T + jn) * a.ldv + FDK * head, hf, vf);
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int rr = il_of(r, hf), i = i0 + rr;
       float pe = 0.f;
       if (j < kl) {
-        const float sv = (ac[r] + band_at<REL>(sbd, a.WP, rr, i, j)) / a.sqrt_dk;
+        const float sv = (ac[r] + band_at<REL>(sbd, a.WP, rr, i, j)) * a.inv_sqrt_dk;
         pe = expf(sv - qst[rr]) * qst[FR + rr];
       }
       float pd = pe, g = dp[r];
@@ -375,7 +397,7 @@ __global__ __launch_bounds__(BW_NT, 1) void relpos_flash_bwd_kernel(FlashArgs a)
         pd = keep ? pe * a.dscale : 0.f;
         g = keep ? g * a.dscale : 0.f;
       }
-      const float dsv = pe * (g - qst[2 * FR + rr]) / a.sqrt_dk;
+      const float dsv = pe * (g - qst[2 * FR + rr]) * a.inv_sqrt_dk;
       ds[rr * a.DSP + j] = dsv;  // j < nac*32 <= DSP; zero beyond klen / T (pe == 0)
       if (i < T && j < T) {
         const long o = ((long)z * T + i) * a.lds + j;
@@ -394,28 +416,47 @@ __global__ __launch_bounds__(BW_NT, 1) void relpos_flash_bwd_kernel(FlashArgs a)
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   if (wave < 4) {
     const int k0 = half ? (nac + 1) / 2 : 0, k1 = half ? nac : (nac + 1) / 2;
+    const float* kcol = a.kmat + (long)b * T * a.ldk + FDK * head + 32 * c + l32;
+    float bf[16];  // k column slice of the chunk; the next chunk's is requested before the MFMAs
+    if (k0 < k1) {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) bf[s] = kcol[(long)min(k0 * 32 + 16 * hf + s, T - 1) * a.ldk];
+    }
 #pragma unroll 1
     for (int kc = k0; kc < k1; ++kc) {
-      float af[16], bf[16];
+      float af[16], bn[16];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const float4 v = *reinterpret_cast<const float4*>(ds + l32 * a.DSP + kc * 32 + 16 * hf + 4 * u);
         af[4 * u] = v.x; af[4 * u + 1] = v.y; af[4 * u + 2] = v.z; af[4 * u + 3] = v.w;
       }
+      if (kc + 1 < k1) {
 #pragma unroll
-      for (int s = 0; s < 16; ++s)
-        bf[s] = a.kmat[((long)b * T + min(kc * 32 + 16 * hf + s, T - 1)) * a.ldk + FDK * head + 32 * c + l32];
+        for (int s = 0; s < 16; ++s) bn[s] = kcol[(long)min((kc + 1) * 32 + 16 * hf + s, T - 1) * a.ldk];
+      }
 #pragma unroll
       for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) bf[s] = bn[s];
     }
   } else {
     // Dbd[rr][x] (window column x = position kmin + x): latest dS[rr][x + rr - 31]; legacy (q_v
     // row rr): the lower part j = x + rr - 31 <= i0 + rr from dS row rr, the upper part from row rr-1
     const int p0 = half ? (nbd + 1) / 2 : 0, p1 = half ? nbd : (nbd + 1) / 2;
     const int kmin = T - FR - i0;
+    float bf[16];  // p_win column slice of the chunk (next chunk requested before the MFMAs)
+    if (p0 < p1) {
+#pragma unroll
+      for (int s = 0; s < 16; ++s) bf[s] = p_virt_row<REL>(a, kmin + p0 * 32 + 16 * hf + s, head)[32 * c + l32];
+    }
 #pragma unroll 1
     for (int pc = p0; pc < p1; ++pc) {
-      float af[16], bf[16];
+      float af[16], bn[16];
+      if (pc + 1 < p1) {
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+          bn[s] = p_virt_row<REL>(a, kmin + (pc + 1) * 32 + 16 * hf + s, head)[32 * c + l32];
+      }
 #pragma unroll
       for (int s = 0; s < 16; ++s) {
         const int x = pc * 32 + 16 * hf + s;
@@ -426,10 +467,11 @@ __global__ __launch_bounds__(BW_NT, 1) void relpos_flash_bwd_kernel(FlashArgs a)
           else if (l32 >= 1 && jj >= i0 + l32 + 1) v = ds[(l32 - 1) * a.DSP + jj];
         }
         af[s] = v;
-        bf[s] = p_virt_row<REL>(a, kmin + x, head)[32 * c + l32];
       }
 #pragma unroll
       for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
+#pragma unroll
+      for (int s = 0; s < 16; ++s) bf[s] = bn[s];
     }
   }
   constexpr int QP = 36;
@@ -513,28 +555,41 @@ __global__ __launch_bounds__(256) void relpos_dp_kernel(const float* __restrict_
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   const int nrc = (T + 31) / 32;  // rho chunks of 32 (K dimension per batch element)
-  for (int bb = g * bpg; bb < min(nb, (g + 1) * bpg); ++bb) {
+  const int b0 = g * bpg, nbb = min(nb, (g + 1) * bpg) - b0;
+  const int nit = nbb * ((nrc - half + 1) / 2);  // (batch, this half's rho chunks) iterations
+  auto load_it = [&](int it, float (&af)[16], float (&bf)[16]) {
+    const int per = (nrc - half + 1) / 2;
+    const int bb = b0 + it / per, rc = half + 2 * (it % per);
     const long zrow = (long)(h * nb + bb) * T;
-    for (int rc = half; rc < nrc; rc += 2) {
-      float af[16], bf[16];
 #pragma unroll
-      for (int s = 0; s < 16; ++s) {
-        const int rho = rc * 32 + 16 * hf + s;
-        float v = 0.f;
-        if (rho < T && x < P2) {
-          const int jj = x - (T - 1) + rho;
-          if (REL == 1) {
-            if (jj >= 0 && jj < T) v = dS[(zrow + rho) * lds + jj];
-          } else {
-            if (jj >= 0 && jj <= rho) v = dS[(zrow + rho) * lds + jj];
-            else if (rho >= 1 && jj >= rho + 1 && jj < T) v = dS[(zrow + rho - 1) * lds + jj];
-          }
+    for (int s = 0; s < 16; ++s) {
+      const int rho = rc * 32 + 16 * hf + s;
+      float v = 0.f;
+      if (rho < T && x < P2) {
+        const int jj = x - (T - 1) + rho;
+        if (REL == 1) {
+          if (jj >= 0 && jj < T) v = dS[(zrow + rho) * lds + jj];
+        } else {
+          if (jj >= 0 && jj <= rho) v = dS[(zrow + rho) * lds + jj];
+          else if (rho >= 1 && jj >= rho + 1 && jj < T) v = dS[(zrow + rho - 1) * lds + jj];
         }
-        af[s] = v;
-        bf[s] = rho < T ? qv[(zrow + rho) * FDK + 32 * c + l32] : 0.f;
       }
+      af[s] = v;
+      bf[s] = rho < T ? qv[(zrow + rho) * FDK + 32 * c + l32] : 0.f;
+    }
+  };
+  float af[16], bf[16];
+  if (nit > 0) load_it(0, af, bf);
+#pragma unroll 1
+  for (int it = 0; it < nit; ++it) {
+    float an[16], bn[16];
+    if (it + 1 < nit) load_it(it + 1, an, bn);
 #pragma unroll
-      for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
+    for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(af[s], bf[s], acc, 0, 0, 0);
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      af[s] = an[s];
+      bf[s] = bn[s];
     }
   }
   // halves 0 / 1 of rho combined in fixed order
@@ -573,20 +628,23 @@ __global__ __launch_bounds__(256) void relpos_dp_reduce_kernel(const float* __re
   }
 }
 
-__global__ __launch_bounds__(64) void relpos_bias_reduce_kernel(const float* __restrict__ bias_part,
-                                                                const float* __restrict__ carry, int nb, int nqb,
-                                                                int T, float* __restrict__ du, float* __restrict__ dv) {
-  const int h = blockIdx.x, d = threadIdx.x;
-  float su = 0.f, sv = 0.f;
-  for (int bb = 0; bb < nb; ++bb)
-    for (int qb = 0; qb < nqb; ++qb) {
-      const long base = ((long)(h * nb + bb) * nqb + qb) * 2;
-      su += bias_part[base * FDK + d];
-      sv += bias_part[(base + 1) * FDK + d];
-      if (carry && (qb + 1) * FR < T) sv += carry[((long)(h * nb + bb) * nqb + qb) * FDK + d];
-    }
-  du[h * FDK + d] += su;
-  dv[h * FDK + d] += sv;
+// one block per (head, u|v, d): 256 threads split the (b, query block) partials, fixed-order
+// block reduction (deterministic)
+__global__ __launch_bounds__(256) void relpos_bias_reduce_kernel(const float* __restrict__ bias_part,
+                                                                 const float* __restrict__ carry, int nb, int nqb,
+                                                                 int T, float* __restrict__ du, float* __restrict__ dv) {
+  __shared__ float sh[16];
+  const int d = blockIdx.x & 63, which = (blockIdx.x >> 6) & 1, h = blockIdx.x >> 7;
+  const int n = nb * nqb;
+  float s = 0.f;
+  for (int e = threadIdx.x; e < n; e += blockDim.x) {
+    const int bb = e / nqb, qb = e - bb * nqb;
+    const long blk = (long)(h * nb + bb) * nqb + qb;
+    s += bias_part[(blk * 2 + which) * FDK + d];
+    if (which && carry && (qb + 1) * FR < T) s += carry[blk * FDK + d];
+  }
+  s = esp::block_sum(s, sh);
+  if (threadIdx.x == 0) (which ? dv : du)[h * FDK + d] += s;
 }
 
 // legacy: add each block's carry to q row i0+32 of the query gradient
@@ -647,6 +705,7 @@ ESP_API int esp_relpos_flash_fwd(const float* qu, const float* qv, const float* 
   a.klen = klen; a.out = ctx; a.stats = stats;
   a.nb = nb; a.T = T; a.nqb = (T + FR - 1) / FR; a.nblk = nb * H * a.nqb;
   a.sqrt_dk = sqrt_dk;
+  a.inv_sqrt_dk = 1.0f / sqrt_dk;
   a.thr = drop_thr(drop_p);
   a.dscale = a.thr ? 1.f / (1.f - drop_p) : 1.f;
   a.seed = seed;
@@ -686,6 +745,7 @@ ESP_API int esp_relpos_flash_bwd(const float* qu, const float* qv, const float* 
   a.dS = dS; a.pdrop = pdrop; a.lds = lds; a.bias_part = bias_part; a.carry = rel == 2 ? carry : nullptr;
   a.nb = nb; a.T = T; a.nqb = (T + FR - 1) / FR; a.nblk = nb * H * a.nqb;
   a.sqrt_dk = sqrt_dk;
+  a.inv_sqrt_dk = 1.0f / sqrt_dk;
   a.thr = drop_thr(drop_p);
   a.dscale = a.thr ? 1.f / (1.f - drop_p) : 1.f;
   a.seed = seed;
@@ -728,7 +788,7 @@ ESP_API int esp_relpos_dp(const float* dS, long lds, const float* qv, int rel, i
   else hipLaunchKernelGGL(relpos_dp_reduce_kernel<2>, dim3((unsigned)nb_red), dim3(256), 0, st, work, H, ng, T, dp, ldp);
   const int nqb = (T + FR - 1) / FR;
   if (bias_part)
-    hipLaunchKernelGGL(relpos_bias_reduce_kernel, dim3(H), dim3(64), 0, st, bias_part, rel == 2 ? carry : nullptr, nb,
+    hipLaunchKernelGGL(relpos_bias_reduce_kernel, dim3(H * 128), dim3(256), 0, st, bias_part, rel == 2 ? carry : nullptr, nb,
                        nqb, T, du, dv);
   if (rel == 2 && carry && dq)
     hipLaunchKernelGGL(relpos_carry_kernel, dim3(nb * H * nqb), dim3(64), 0, st, carry, nb, nqb, T, dq, ldq);

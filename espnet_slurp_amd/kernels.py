@@ -444,9 +444,12 @@ def relpos_attn_bwd(dctx, ldd, vmat, ldv, attn, dS, dbd, ldp, nb, H, sqrt_dk, dr
                  float(sqrt_dk), float(drop_p), int(seed) & (2 ** 64 - 1), T, lds, _st())
 
 
-# Flash-style rel-pos attention (csrc/flash_relpos.hip): the default for d_k = 64, T <= 512
-# (ESP_FLASH_ATTN=0 restores the materialised-probability path of attention.hip + GEMMs)
-FLASH_ATTN = os.environ.get("ESP_FLASH_ATTN", "1") == "1"
+# Flash-style rel-pos attention (csrc/flash_relpos.hip), d_k = 64, T <= 512, latest and legacy.
+# Opt-in (ESP_FLASH_ATTN=1): in fp32 at T' = 374 the recompute it trades for the (Z,T,T)
+# probability traffic costs about what that traffic did (fp32 MFMA is 157 TF against 8 TB/s:
+# 32 flop per P byte at d_k = 64), and measured per layer at C2 B=128 (tools/flash_bench.py):
+# forward 0.84 vs 0.99 ms (flash wins), backward 2.10 vs 1.79 ms (materialised wins) -> off.
+FLASH_ATTN = os.environ.get("ESP_FLASH_ATTN", "0") == "1"
 _DP_WS = _Workspace()
 
 

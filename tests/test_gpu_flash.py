@@ -18,6 +18,11 @@ from tests.test_gpu_blocks import _check_grads, _params64
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _flash_on(monkeypatch):
+    monkeypatch.setattr(K, "FLASH_ATTN", True)
+
+
 def _block(dev, legacy, D, H, seed, std=0.1):
     torch.manual_seed(seed)
     mod = RelPositionMultiHeadedAttention(H, D, 0.0, legacy).to(dev)
