@@ -95,12 +95,32 @@ def synthetic_batch(B, V, rank, device, variable=False):
     return dict(speech=speech, speech_lengths=speech_lengths, text=text, text_lengths=tl)
 
 
+def host_cores() -> int:
+    """Every core this process may run on (its affinity set), capped by OMP_NUM_THREADS when the
+    host sets it: the GPU box exports the per-GPU CPU share there (16), while os.cpu_count()
+    reports the whole machine."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(omp))) if omp.isdigit() and int(omp) > 0 else max(1, n)
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args):
     """The oracle (plain PyTorch CPU restatement, oracle/espnet_cpu.py) timed on the host
     cores: same C2 model shape, fp32, B=4 x 1500 frames, dropout 0.1, no SpecAug draws,
     1 warmup + 3 timed steps of fwd + bwd + clip + torch Adam."""
     from oracle import espnet_cpu as O
-    n = min(16, os.cpu_count() or 1)
+    n = host_cores()
     torch.set_num_threads(n)
     cfg = O.ModelCfg(vocab_size=args.vocab, enc=O.EncCfg(output_size=args.d, attention_heads=args.heads,
                                                           linear_units=args.ff, num_blocks=args.layers,
@@ -126,7 +146,7 @@ def cpu_baseline(args):
         opt.zero_grad()
         times.append(time.perf_counter() - t0)
     t = sum(times[1:]) / len(times[1:])
-    return {"value": round(B / t, 4), "unit": "utt/s", "cores": n, "kind": "port",
+    return {"value": round(B / t, 4), "unit": "utt/s", "cores": n, "kind": "port", "cpu_model": cpu_model(),
             "sample": f"oracle/espnet_cpu.py {workload_name(args).split()[0]}-shape step (fwd+bwd+clip+Adam), "
                       f"d={args.d} {args.layers}L, B=4 x 1500 frames, fp32, "
                       f"1 warmup + 3 timed steps, {t:.2f} s/step on {n} threads"}

@@ -117,23 +117,25 @@ class PositionwiseFeedForward(nn.Module):
         """returns resid + alpha * drop_res(w_2(drop(act(w_1 x))))  (new buffer)."""
         M = x2d.shape[0]
         H = self.w_1.weight.shape[0]
-        pre = empty(M, H, like=x2d)
+        # the w_1 epilogue stores h = drop(act(v)) and, instead of v, the local derivative
+        # dh/dv = keep * scale * act'(v): the backward epilogue is then a single multiply
+        dact = empty(M, H, like=x2d)
         h = empty(M, H, like=x2d)
         p_in = self.p if training else 0.0
         s1, s2 = seeds.next(), seeds.next()
-        self.w_1.fwd(x2d, h, act=self.act, aux=pre, drop_p=p_in, seed=s1)
+        self.w_1.fwd(x2d, h, act=self.act | K.ACT_AUX_DERIV, aux=dact, drop_p=p_in, seed=s1)
         out = empty(M, x2d.shape[1], like=x2d)
         pr = p_res if training else 0.0
         self.w_2.fwd(h, out, alpha=alpha, drop_p=pr, seed=s2, R=resid, beta=1.0)
-        return out, Ctx(x=x2d, pre=pre, h=h, s1=s1, s2=s2, p_in=p_in, pr=pr, alpha=alpha)
+        return out, Ctx(x=x2d, dact=dact, h=h, s1=s1, s2=s2, p_in=p_in, pr=pr, alpha=alpha)
 
     def bwd(self, c, dout):
         """dout: grad w.r.t. the residual output; returns grad w.r.t. x2d (new buffer)."""
         dz = torch.empty_like(dout)
         K.scale_dropout(dout, dz, alpha=c.alpha, drop_p=c.pr, seed=c.s2)
         K.linear_bwd_weight(dz, c.h, self.w_2.weight.grad, self.w_2.bias.grad)
-        dh = torch.empty_like(c.pre)
-        K.linear_bwd_data_act(dz, self.w_2.weight, dh, c.pre, self.act, drop_p=c.p_in, seed=c.s1)
+        dh = torch.empty_like(c.dact)
+        K.linear_bwd_data_act(dz, self.w_2.weight, dh, c.dact, K.ACT_MUL)
         return self.w_1.bwd(dh, c.x)
 
 

@@ -90,25 +90,55 @@ __global__ void embed_fwd_kernel(const int64_t* __restrict__ tok, const float* _
   }
 }
 
-// dE[v, :] += sum over rows with tok==v of dy*mask*scale*xscale   (deterministic: one block
-// per vocab row scans the token list in order)
-__global__ void embed_bwd_kernel(const int64_t* __restrict__ tok, const float* __restrict__ dy,
-                                 float* __restrict__ dE, int nrows, int D, float xscale, uint32_t thr,
-                                 float scale, uint64_t seed, const uint64_t* __restrict__ key) {
+// dE[v, :] += sum over rows with tok==v of dy*mask*scale*xscale.  One block per vocab row;
+// the block scans the token list 256 rows at a time (coalesced), compacts the matching row
+// indices into LDS in ascending order (wave ballot + per-wave prefix), then every thread
+// accumulates its columns over that list.  The summation order is ascending r, fixed, so
+// the result is deterministic (no atomics).
+constexpr int EMB_MAXD = 1024;  // D / 256 accumulators per thread
+__global__ void __launch_bounds__(256) embed_bwd_kernel(const int64_t* __restrict__ tok, const float* __restrict__ dy,
+                                                        float* __restrict__ dE, int nrows, int D, float xscale,
+                                                        uint32_t thr, float scale, uint64_t seed,
+                                                        const uint64_t* __restrict__ key) {
+  __shared__ int rows[256];
+  __shared__ int wcnt[4];
   seed = esp::keyed(seed, key);
   const int v = blockIdx.x;
-  for (int d = threadIdx.x; d < D; d += blockDim.x) {
-    float acc = 0.f;
-    bool any = false;
-    for (int r = 0; r < nrows; ++r) {
-      if (tok[r] != v) continue;
-      any = true;
-      const long i = (long)r * D + d;
-      float g = dy[i];
-      if (thr) g = esp::keep_elem(seed, (uint64_t)i, thr) ? g * scale : 0.f;
-      acc += g * xscale;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  float acc[EMB_MAXD / 256];
+#pragma unroll
+  for (int j = 0; j < EMB_MAXD / 256; ++j) acc[j] = 0.f;
+  bool any = false;
+  for (int c = 0; c < nrows; c += 256) {
+    const int r = c + tid;
+    const bool hit = r < nrows && tok[r] == v;
+    const uint64_t m = __ballot(hit);
+    if (lane == 0) wcnt[w] = __popcll(m);
+    __syncthreads();
+    const int base = (w > 0 ? wcnt[0] : 0) + (w > 1 ? wcnt[1] : 0) + (w > 2 ? wcnt[2] : 0);
+    const int n = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    if (hit) rows[base + __popcll(m & ((1ull << lane) - 1))] = r;
+    __syncthreads();
+    any |= n > 0;
+    for (int k = 0; k < n; ++k) {
+      const long rb = (long)rows[k] * D;
+#pragma unroll
+      for (int j = 0; j < EMB_MAXD / 256; ++j) {
+        const int d = tid + j * 256;
+        if (d < D) {
+          float g = dy[rb + d];
+          if (thr) g = esp::keep_elem(seed, (uint64_t)(rb + d), thr) ? g * scale : 0.f;
+          acc[j] += g * xscale;
+        }
+      }
     }
-    if (any) dE[(long)v * D + d] += acc;
+    __syncthreads();  // rows/wcnt reused by the next chunk
+  }
+  if (!any) return;
+#pragma unroll
+  for (int j = 0; j < EMB_MAXD / 256; ++j) {
+    const int d = tid + j * 256;
+    if (d < D) dE[(long)v * D + d] += acc[j];
   }
 }
 
@@ -303,6 +333,7 @@ ESP_API int esp_embed_fwd(const long long* tok, const float* E, const float* pe,
 
 ESP_API int esp_embed_bwd(const long long* tok, const float* dy, float* dE, int nrows, int V, int D, float xscale,
                           float drop_p, unsigned long long seed, void* stream) {
+  ESP_ARG_CHECK(D <= EMB_MAXD, "esp_embed_bwd: D > 1024");
   const uint32_t thr = drop_threshold(drop_p);
   hipLaunchKernelGGL(embed_bwd_kernel, dim3(V), dim3(256), 0, (hipStream_t)stream, (const int64_t*)tok, dy, dE, nrows,
                      D, xscale, thr, thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed, esp::rng_key_ptr());

@@ -1,1169 +1,14 @@
-// FP32 MFMA GEMM for gfx950 (v_mfma_f32_32x32x2_f32: exact f32 fma chain, 64 FLOP/clk/SIMD).
-//
-//   C[z](m,n) = alpha * epi( sum_k A[z](m,k) * B[z](k,n) + bias[n] ) + beta * R[z](m,n)
-//
-// Operand access modes (template):
-//   KC     element (r,k) at p[r*ld + k]      (A row-major [M][K] / B as [N][K] = W of nn.Linear)
-//   RC     element (r,k) at p[k*ld + r]      (A as [K][M] / B row-major [K][N])
-//   I2C_KC im2col view of an NHWC map, (r = output pixel, k = (kt,kf,c))   [conv2 forward, A]
-//   I2C_RC same map with roles swapped (r = (kt,kf,c), k = output pixel)   [conv2 dW, B]
-// Batches: z = z1*nb2 + z2, operand offset = z1*s1 + z2*s2 (two-level strides cover the
-// (batch, head) layouts of attention without copies).
-//
-// Tiling: 128x128 block tile, BK=16, 256 threads = 4 waves (2x2), each wave 64x64 =
-// 2x2 MFMA 32x32 tiles. A lane of half h uses k = 8h+s for MFMA step s (both operands agree);
-// see store_slab/load_frag for the two LDS images. Global->LDS is register-staged and double
-// buffered (next slab's loads are issued before the current slab's MFMAs).
-// Epilogue (fused): bias, ReLU/Swish (pre-activation optionally stored to `aux`),
-// counter-RNG dropout, alpha scale and beta*R residual.
+// FP32 / bf16 MFMA GEMM: host side (launch selection, split-K, tile choice, C-ABI) and the
+// register-staged fallback / split-K reduction kernels.  Device code: gemm_kernels.h.
 #include <stdlib.h>
 
 #include <algorithm>
 
-#include "common.h"
+#include "gemm_kernels.h"
+
+using namespace espg;
 
 namespace {
-
-constexpr int BM = 128, BN = 128, BK = 32, NT = 256;  // BK: split-K granularity
-
-enum Mode { KC = 0, RC = 1, I2C_KC = 2, I2C_RC = 3, I2CT_KC = 4 };
-enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_SWISH = 2 };
-
-struct FastDiv {  // n / d for n < 2^31: (n * m) >> s, m = ceil(2^s / d), s = 31 + ceil(log2 d)
-  uint64_t m;
-  uint32_t s, d;
-};
-static FastDiv make_fastdiv(uint32_t d) {
-  uint32_t l = 0;
-  while ((1ull << l) < d) ++l;
-  FastDiv f;
-  f.s = 31 + l;
-  f.m = ((1ull << f.s) + d - 1) / d;
-  f.d = d;
-  return f;
-}
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
-  return (uint32_t)(((uint64_t)n * f.m) >> f.s);
-}
-
-struct Im2col {  // NHWC input map [Bn][H][W][C], 3x3 kernel, stride 2, no padding
-  int H, W, C, Ho, Wo;
-};
-
-struct Operand {
-  const float* p;
-  long ld;
-  long s1, s2;
-  int vec;   // float4 along the contiguous dim is legal
-  Im2col ic;
-  int glds;  // 16-B LDS-DMA of any in-range quad stays inside the operand (see glds_ok)
-};
-
-struct GemmArgs {
-  int M, N, K, nb2;
-  Operand a, b;
-  float* c;
-  long ldc, c1, c2;
-  const float* r;  // residual (same layout as C), may alias c
-  float* aux;      // pre-activation store (same layout as C)
-  const float* bias;
-  float alpha, beta;
-  int act;
-  uint32_t drop_thresh;  // 0 = no dropout
-  float drop_scale;
-  uint64_t seed;
-  const uint64_t* key;  // device dropout key (esp_set_rng_key) or NULL
-  int batch;
-  int splits, kchunk;  // split-K: blockIdx.z = z*splits + split; partials -> work
-  float* work;
-  int bf16;  // bf16-input MFMA kernel (esp_set_gemm_compute(1)); fp32 operands rounded in LDS staging
-  int bnt;  // LDS-DMA kernel tile width (128, or 64 for narrow / mid-size grids); 0 = fallback kernel
-  int bwd_act;       // != 0: backward epilogue  v = drop'(acc) * act'(pre)  (act code, dropout regenerated)
-  const float* pre;  // pre-activation (same layout as C) for bwd_act
-  float* rowsum;     // != NULL: rowsum[m] += sum_k A(m,k)  (bias gradient of a weight-gradient GEMM)
-  float* rs_work;    // split-K partial row sums [split][M]
-  int wide;          // float4 epilogue legal (N, ldc, batch strides % 4 == 0, 16-B aligned C/R/aux/pre/bias/work)
-  // output row map (conv2 input gradient, one parity class (ph, pw) of the conv1 output grid):
-  // row m = (b, a, e) of the class grid (Ha x We) -> pixel (b, 2a+ph, 2e+pw) of the T1 x F1 map
-  int cmap;
-  FastDiv cm_hw, cm_w;
-  int cm_T1, cm_F1, cm_ph, cm_pw;
-};
-
-__device__ __forceinline__ long row_off(const GemmArgs& g, int m) {
-  if (!g.cmap) return (long)m * g.ldc;
-  const int b = (int)fdiv((uint32_t)m, g.cm_hw);
-  const int rem = m - b * (int)g.cm_hw.d;
-  const int a = (int)fdiv((uint32_t)rem, g.cm_w), e = rem - a * (int)g.cm_w.d;
-  return (((long)b * g.cm_T1 + 2 * a + g.cm_ph) * g.cm_F1 + 2 * e + g.cm_pw) * g.ldc;
-}
-
-// Fused epilogue for output element (m, n) of batch z with raw accumulator `acc`.  The kind is
-// chosen once per launch (a template argument), so the per-element path is straight-line:
-//   EPI 0: alpha*acc (+ beta*R)
-//   EPI 1: forward  alpha*drop(act(acc + bias)) (+ beta*R), pre-activation to aux
-//   EPI 2: backward  drop'(acc + bias) * act'(pre)  (dropout mask regenerated), alpha, R
-// cbase = offset of batch z in C/R/aux/pre, dbase = z*M*N (dropout index base).
-enum { EPI_PLAIN = 0, EPI_FWD = 1, EPI_BWD = 2 };
-__host__ __device__ inline int epi_kind(const GemmArgs& g) {
-  return g.bwd_act ? EPI_BWD : ((g.bias || g.aux || g.act || g.drop_thresh) ? EPI_FWD : EPI_PLAIN);
-}
-template <int EPI>
-__device__ __forceinline__ void epi_store(const GemmArgs& g, long cbase, uint64_t dbase, int m, int n, float acc) {
-  const long off = cbase + row_off(g, m) + n;
-  const uint64_t seed = g.drop_thresh ? esp::keyed(g.seed, g.key) : 0;
-  float v = acc;
-  if constexpr (EPI == EPI_FWD) {
-    if (g.bias) v += g.bias[n];
-    if (g.aux) g.aux[off] = v;
-    if (g.act == ACT_RELU) v = fmaxf(v, 0.f);
-    else if (g.act == ACT_SWISH) v = v / (1.0f + expf(-v));
-    if (g.drop_thresh) {
-      const uint64_t idx = dbase + (uint64_t)m * (uint64_t)g.N + n;
-      v = esp::keep_elem(seed, idx, g.drop_thresh) ? v * g.drop_scale : 0.f;
-    }
-  } else if constexpr (EPI == EPI_BWD) {
-    // gradient w.r.t. the pre-activation of  h = drop(act(pre))  given dL/dh = v
-    if (g.bias) v += g.bias[n];
-    if (g.drop_thresh) {
-      const uint64_t idx = dbase + (uint64_t)m * (uint64_t)g.N + n;
-      v = esp::keep_elem(seed, idx, g.drop_thresh) ? v * g.drop_scale : 0.f;
-    }
-    const float x = g.pre[off];
-    if (g.bwd_act == ACT_RELU) v = x > 0.f ? v : 0.f;
-    else {
-      const float sg = 1.0f / (1.0f + expf(-x));
-      v = v * (sg * (1.0f + x * (1.0f - sg)));
-    }
-  }
-  v *= g.alpha;
-  if (g.r) v += g.beta * g.r[off];
-  g.c[off] = v;
-}
-__device__ __forceinline__ long c_base(const GemmArgs& g, int z) {
-  const int z1 = z / g.nb2, z2 = z - z1 * g.nb2;
-  return (long)z1 * g.c1 + (long)z2 * g.c2;
-}
-
-// store a wave's TM x TN 32x32 accumulator tiles (rows mrow0 + 32i + ..., cols ncol0 + 32j + l32).
-// Per 32x32 tile, every load the epilogue needs (residual R, pre-activation) is issued, in
-// program order, before the tile's first store: R / pre may alias C, so a load placed after a
-// store cannot be hoisted by the compiler and each element would pay a memory round trip.
-template <int EPI, int TM, int TN>
-__device__ __forceinline__ void store_tiles(const GemmArgs& g, int z, int mrow0, int ncol0, int h, int l32,
-                                            const f32x16 (&acc)[TM][TN]) {
-  const long cbase = c_base(g, z);
-  const uint64_t dbase = (uint64_t)z * (uint64_t)g.M * (uint64_t)g.N;
-  const bool has_r = g.r != nullptr;
-  const uint64_t seed = (EPI != EPI_PLAIN && g.drop_thresh) ? esp::keyed(g.seed, g.key) : 0;  // before any store
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = ncol0 + j * 32 + l32;
-    if (n >= g.N) continue;
-    const float bn = (EPI != EPI_PLAIN && g.bias) ? g.bias[n] : 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      float rr[16], pp[EPI == EPI_BWD ? 16 : 1];
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = mrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const long off = cbase + row_off(g, m) + n;
-        rr[r] = (has_r && m < g.M) ? g.r[off] : 0.f;
-        if constexpr (EPI == EPI_BWD) pp[r] = m < g.M ? g.pre[off] : 0.f;
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = mrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (m >= g.M) continue;
-        const long off = cbase + row_off(g, m) + n;
-        float v = acc[i][j][r] + bn;
-        if constexpr (EPI == EPI_FWD) {
-          if (g.aux) g.aux[off] = v;
-          if (g.act == ACT_RELU) v = fmaxf(v, 0.f);
-          else if (g.act == ACT_SWISH) v = v / (1.0f + expf(-v));
-          if (g.drop_thresh) {
-            const uint64_t idx = dbase + (uint64_t)m * (uint64_t)g.N + n;
-            v = esp::keep_elem(seed, idx, g.drop_thresh) ? v * g.drop_scale : 0.f;
-          }
-        } else if constexpr (EPI == EPI_BWD) {
-          if (g.drop_thresh) {
-            const uint64_t idx = dbase + (uint64_t)m * (uint64_t)g.N + n;
-            v = esp::keep_elem(seed, idx, g.drop_thresh) ? v * g.drop_scale : 0.f;
-          }
-          const float x = pp[r];
-          if (g.bwd_act == ACT_RELU) v = x > 0.f ? v : 0.f;
-          else {
-            const float sg = 1.0f / (1.0f + expf(-x));
-            v = v * (sg * (1.0f + x * (1.0f - sg)));
-          }
-        }
-        v *= g.alpha;
-        if (has_r) v += g.beta * rr[r];
-        g.c[off] = v;
-      }
-    }
-  }
-}
-// ---------------------------------------------------------------- widened epilogue
-// A 32x32 f32 MFMA accumulator holds one COLUMN per lane (16 rows), so a direct store is 16
-// dword stores per tile.  Two DPP butterfly stages transpose 4x4 blocks inside each lane quad:
-// afterwards lane (h, l32 = 4q + j) holds in registers 4g..4g+3 the row 8g + 4h + j, columns
-// 4q..4q+3 — one float4 per group, 4 dwordx4 stores per tile (the store tail is issue-bound:
-// 4x fewer instructions for the same bytes).  Residual / pre-activation loads widen alike.
-__device__ __forceinline__ float dpp_xor1(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
-}
-__device__ __forceinline__ float dpp_xor2(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
-}
-__device__ __forceinline__ void quad_transpose(f32x16& v, int lane) {
-  const bool odd = lane & 1, hi = lane & 2;
-#pragma unroll
-  for (int g = 0; g < 4; ++g) {
-    const float a0 = v[4 * g], a1 = v[4 * g + 1], a2 = v[4 * g + 2], a3 = v[4 * g + 3];
-    // stage 1: reg k of lane j takes reg k^1 of lane j^1 where the parities of j and k differ
-    const float s0 = dpp_xor1(a1), s1 = dpp_xor1(a0), s2 = dpp_xor1(a3), s3 = dpp_xor1(a2);
-    const float b0 = odd ? s0 : a0, b1 = odd ? a1 : s1, b2 = odd ? s2 : a2, b3 = odd ? a3 : s3;
-    // stage 2: the same with bit 1
-    const float t0 = dpp_xor2(b2), t1 = dpp_xor2(b3), t2 = dpp_xor2(b0), t3 = dpp_xor2(b1);
-    v[4 * g] = hi ? t0 : b0;
-    v[4 * g + 1] = hi ? t1 : b1;
-    v[4 * g + 2] = hi ? b2 : t2;
-    v[4 * g + 3] = hi ? b3 : t3;
-  }
-}
-
-// 16-B output store; nt = streaming (non-temporal) hint, so the write does not displace the
-// operand panels the co-resident tiles still read from L2 (ESP_GEMM_ABL bit 32, measured)
-typedef float f32x4v __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void st4(float* p, const float (&v)[4], bool nt) {
-  const f32x4v w = {v[0], v[1], v[2], v[3]};
-  if (nt) __builtin_nontemporal_store(w, reinterpret_cast<f32x4v*>(p));
-  else *reinterpret_cast<f32x4v*>(p) = w;
-}
-// needs N % 4 == 0, ldc % 4 == 0 and 16-B aligned C / R / aux / pre / bias (host: g.wide)
-template <int EPI, int TM, int TN>
-__device__ __forceinline__ void store_tiles_wide(const GemmArgs& g, int z, int mrow0, int ncol0, int lane,
-                                                 f32x16 (&acc)[TM][TN], bool nt = false) {
-  const int h = lane >> 5, l32 = lane & 31;
-  const long cbase = c_base(g, z);
-  const uint64_t dbase = (uint64_t)z * (uint64_t)g.M * (uint64_t)g.N;
-  const bool has_r = g.r != nullptr;
-  const uint64_t seed = (EPI != EPI_PLAIN && g.drop_thresh) ? esp::keyed(g.seed, g.key) : 0;  // before any store
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = ncol0 + j * 32 + 4 * (l32 >> 2);
-    const bool nok = n < g.N;
-    float4 bn = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (EPI != EPI_PLAIN && g.bias && nok) bn = *reinterpret_cast<const float4*>(g.bias + n);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      quad_transpose(acc[i][j], lane);
-      float4 rr[4], pp[EPI == EPI_BWD ? 4 : 1];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int m = mrow0 + i * 32 + 8 * q + 4 * h + (l32 & 3);
-        const long off = cbase + row_off(g, m) + n;
-        const bool ok = nok && m < g.M;
-        rr[q] = (has_r && ok) ? *reinterpret_cast<const float4*>(g.r + off) : make_float4(0.f, 0.f, 0.f, 0.f);
-        if constexpr (EPI == EPI_BWD)
-          pp[q] = ok ? *reinterpret_cast<const float4*>(g.pre + off) : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int m = mrow0 + i * 32 + 8 * q + 4 * h + (l32 & 3);
-        if (!nok || m >= g.M) continue;
-        const long off = cbase + row_off(g, m) + n;
-        float v[4] = {acc[i][j][4 * q] + bn.x, acc[i][j][4 * q + 1] + bn.y, acc[i][j][4 * q + 2] + bn.z,
-                      acc[i][j][4 * q + 3] + bn.w};
-        const float r4[4] = {rr[q].x, rr[q].y, rr[q].z, rr[q].w};
-        if constexpr (EPI == EPI_FWD) {
-          if (g.aux) st4(g.aux + off, v, nt);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float w = v[e];
-          if constexpr (EPI == EPI_FWD) {
-            if (g.act == ACT_RELU) w = fmaxf(w, 0.f);
-            else if (g.act == ACT_SWISH) w = w / (1.0f + expf(-w));
-            if (g.drop_thresh) {
-              const uint64_t idx = dbase + (uint64_t)m * (uint64_t)g.N + n + e;
-              w = esp::keep_elem(seed, idx, g.drop_thresh) ? w * g.drop_scale : 0.f;
-            }
-          } else if constexpr (EPI == EPI_BWD) {
-            if (g.drop_thresh) {
-              const uint64_t idx = dbase + (uint64_t)m * (uint64_t)g.N + n + e;
-              w = esp::keep_elem(seed, idx, g.drop_thresh) ? w * g.drop_scale : 0.f;
-            }
-            const float xp = e == 0 ? pp[q].x : e == 1 ? pp[q].y : e == 2 ? pp[q].z : pp[q].w;
-            if (g.bwd_act == ACT_RELU) w = xp > 0.f ? w : 0.f;
-            else {
-              const float sg = 1.0f / (1.0f + expf(-xp));
-              w = w * (sg * (1.0f + xp * (1.0f - sg)));
-            }
-          }
-          w *= g.alpha;
-          if (has_r) w += g.beta * r4[e];
-          v[e] = w;
-        }
-        st4(g.c + off, v, nt);
-      }
-    }
-  }
-}
-template <int TM, int TN>
-__device__ __forceinline__ void store_partials_wide(const GemmArgs& g, float* W, int mrow0, int ncol0, int lane,
-                                                    f32x16 (&acc)[TM][TN]) {
-  const int h = lane >> 5, l32 = lane & 31;
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      quad_transpose(acc[i][j], lane);
-      const int n = ncol0 + j * 32 + 4 * (l32 >> 2);
-      if (n >= g.N) continue;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int m = mrow0 + i * 32 + 8 * q + 4 * h + (l32 & 3);
-        if (m < g.M)
-          *reinterpret_cast<float4*>(W + (long)m * g.N + n) =
-              make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]);
-      }
-    }
-}
-
-// split-K partial stores: W[split][z][M][N]
-template <int TM, int TN>
-__device__ __forceinline__ void store_partials(const GemmArgs& g, float* W, int mrow0, int ncol0, int h, int l32,
-                                               const f32x16 (&acc)[TM][TN]) {
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = ncol0 + j * 32 + l32;
-      if (n >= g.N) continue;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = mrow0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (m < g.M) W[(long)m * g.N + n] = acc[i][j][r];
-      }
-    }
-}
-template <int TM, int TN>
-__device__ __forceinline__ void epilogue(const GemmArgs& g, float* W, int z, int mrow0, int ncol0, int h, int l32,
-                                         const f32x16 (&acc)[TM][TN]) {
-  if (W) store_partials<TM, TN>(g, W, mrow0, ncol0, h, l32, acc);
-  else if (g.bwd_act) store_tiles<EPI_BWD, TM, TN>(g, z, mrow0, ncol0, h, l32, acc);
-  else if (g.bias || g.aux || g.act || g.drop_thresh) store_tiles<EPI_FWD, TM, TN>(g, z, mrow0, ncol0, h, l32, acc);
-  else store_tiles<EPI_PLAIN, TM, TN>(g, z, mrow0, ncol0, h, l32, acc);
-}
-
-// address of im2col element: pixel index `pix` of the output grid, column `col` = (kt,kf,c)
-__device__ __forceinline__ const float* i2c_ptr(const float* base, const Im2col& ic, long pix, int col) {
-  const int hw = ic.Ho * ic.Wo;
-  const long bi = pix / hw;
-  const int rem = (int)(pix - bi * hw);
-  const int ho = rem / ic.Wo, wo = rem - (rem / ic.Wo) * ic.Wo;
-  const int kk = col / ic.C, c = col - kk * ic.C;
-  const int kt = kk / 3, kf = kk - kt * 3;
-  return base + (((bi * ic.H + 2 * ho + kt) * (long)ic.W) + 2 * wo + kf) * ic.C + c;
-}
-
-// Load this thread's NL float4 pieces of a (128 rows x BKT) operand slab into registers.
-// rows = M (A) or N (B); row0 = tile origin; k0 = slab origin; K = end of this split's range.
-template <int MODE, int BKT>
-__device__ __forceinline__ void load_slab(const Operand& op, const float* base, int rows, int K,
-                                          int row0, int k0, float4 (&reg)[BKT / 8]) {
-  constexpr int QPR = BKT / 4;  // quads per row (KC)
-#pragma unroll
-  for (int it = 0; it < BKT / 8; ++it) {
-    const int idx = threadIdx.x + it * NT;
-    if constexpr (MODE == KC || MODE == I2C_KC) {
-      const int r = idx / QPR, kq = (idx % QPR) * 4;
-      const int gr = row0 + r, gk = k0 + kq;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (gr < rows) {
-        if (MODE == KC) {
-          const float* p = base + (long)gr * op.ld + gk;
-          if (op.vec && gk + 3 < K) {
-            v = *reinterpret_cast<const float4*>(p);
-          } else {
-            if (gk + 0 < K) v.x = p[0];
-            if (gk + 1 < K) v.y = p[1];
-            if (gk + 2 < K) v.z = p[2];
-            if (gk + 3 < K) v.w = p[3];
-          }
-        } else {
-          if (gk + 3 < K) {  // C % 4 == 0 enforced on host: quad never straddles a tap
-            v = *reinterpret_cast<const float4*>(i2c_ptr(base, op.ic, gr, gk));
-          } else {
-            if (gk + 0 < K) v.x = *i2c_ptr(base, op.ic, gr, gk + 0);
-            if (gk + 1 < K) v.y = *i2c_ptr(base, op.ic, gr, gk + 1);
-            if (gk + 2 < K) v.z = *i2c_ptr(base, op.ic, gr, gk + 2);
-          }
-        }
-      }
-      reg[it] = v;
-    } else {
-      // BKT k-rows x 32 quads along r
-      const int kr = idx >> 5, rq = (idx & 31) * 4;
-      const int gk = k0 + kr, gr = row0 + rq;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (gk < K) {
-        if (MODE == RC) {
-          const float* p = base + (long)gk * op.ld + gr;
-          if (op.vec && gr + 3 < rows) {
-            v = *reinterpret_cast<const float4*>(p);
-          } else {
-            if (gr + 0 < rows) v.x = p[0];
-            if (gr + 1 < rows) v.y = p[1];
-            if (gr + 2 < rows) v.z = p[2];
-            if (gr + 3 < rows) v.w = p[3];
-          }
-        } else {
-          if (gr + 3 < rows) {
-            v = *reinterpret_cast<const float4*>(i2c_ptr(base, op.ic, gk, gr));
-          } else {
-            if (gr + 0 < rows) v.x = *i2c_ptr(base, op.ic, gk, gr + 0);
-            if (gr + 1 < rows) v.y = *i2c_ptr(base, op.ic, gk, gr + 1);
-            if (gr + 2 < rows) v.z = *i2c_ptr(base, op.ic, gk, gr + 2);
-          }
-        }
-      }
-      reg[it] = v;
-    }
-  }
-}
-
-// LDS images (no transposition on either side):
-//   KC operands  [row][BKT+4] : float4 along k written as loaded; a lane's BKT/2 k-values are
-//                               BKT/8 ds_read_b128 (stride (BKT+4) floats = odd # of quads:
-//                               16 distinct rows hit 16 distinct 16-B slots, conflict-free)
-//   RC operands  [BKT][128+4] : float4 along rows written as loaded; a lane reads its row's
-//                               value per k with ds_read_b32 (32 consecutive floats per half)
-constexpr int LDS_RC = BM + 4;
-template <int BKT>
-struct Lds {
-  static constexpr int KC_S = BKT + 4;
-  static constexpr int TILE = (BM * KC_S > BKT * LDS_RC) ? BM * KC_S : BKT * LDS_RC;
-};
-
-template <int MODE, int BKT>
-__device__ __forceinline__ void store_slab(float* lds, const float4 (&reg)[BKT / 8]) {
-  constexpr int QPR = BKT / 4;
-#pragma unroll
-  for (int it = 0; it < BKT / 8; ++it) {
-    const int idx = threadIdx.x + it * NT;
-    if constexpr (MODE == KC || MODE == I2C_KC) {
-      const int r = idx / QPR, kq = idx % QPR;
-      *reinterpret_cast<float4*>(lds + r * Lds<BKT>::KC_S + kq * 4) = reg[it];
-    } else {
-      const int kr = idx >> 5, rq = (idx & 31) * 4;
-      *reinterpret_cast<float4*>(lds + kr * LDS_RC + rq) = reg[it];
-    }
-  }
-}
-
-// the KH = BKT/2 k-values (k = KH*h + s) of row `r` of the current slab
-template <int MODE, int BKT>
-__device__ __forceinline__ void load_frag(const float* lds, int r, int h, float (&f)[BKT / 2]) {
-  constexpr int KH = BKT / 2;
-  if constexpr (MODE == KC || MODE == I2C_KC) {
-#pragma unroll
-    for (int q = 0; q < KH / 4; ++q) {
-      const float4 v = *reinterpret_cast<const float4*>(lds + r * Lds<BKT>::KC_S + KH * h + 4 * q);
-      f[4 * q + 0] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
-    }
-  } else {
-#pragma unroll
-    for (int q = 0; q < KH; ++q) f[q] = lds[(KH * h + q) * LDS_RC + r];
-  }
-}
-
-// half hs (0/1) of the BK=32 fragment: k = 16h + 8hs + q, q = 0..7
-template <int MODE>
-__device__ __forceinline__ void load_frag_half(const float* lds, int r, int h, int hs, float (&f)[8]) {
-  if constexpr (MODE == KC || MODE == I2C_KC) {
-    const float* p = lds + r * Lds<32>::KC_S + 16 * h + 8 * hs;
-    const float4 v0 = *reinterpret_cast<const float4*>(p);
-    const float4 v1 = *reinterpret_cast<const float4*>(p + 4);
-    f[0] = v0.x; f[1] = v0.y; f[2] = v0.z; f[3] = v0.w;
-    f[4] = v1.x; f[5] = v1.y; f[6] = v1.z; f[7] = v1.w;
-  } else {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) f[q] = lds[(16 * h + 8 * hs + q) * LDS_RC + r];
-  }
-}
-
-// one slab of MFMAs on the fragments in registers
-template <int KH>
-__device__ __forceinline__ void mfma_slab(f32x16 (&acc)[2][2], const float (&af)[2][KH], const float (&bf)[2][KH]) {
-#pragma unroll
-  for (int s = 0; s < KH; ++s)
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
-}
-
-// VARIANT 0: BK=16, register-staged double-buffered LDS (next slab's global loads in flight
-//            during this slab's MFMAs), one barrier per slab.
-// VARIANT 1: BK=32, single LDS buffer, no software pipelining (two barriers per slab); the
-//            overlap comes from 4 resident blocks per CU (36 KB LDS, ~110 VGPRs each).
-// VARIANT 2: BK=32, register-staged prefetch of slab k+1 during slab k's MFMAs into a
-//            single LDS buffer (two barriers per slab; 2 waves/SIMD by VGPRs).
-// VARIANT 3: VARIANT 1 with the slab's MFMAs in two halves (fragments for 8 k-steps live at a
-//            time) so the kernel fits 128 VGPRs: 4 waves/SIMD.
-template <int MA, int MB, int VARIANT>
-__global__ __launch_bounds__(NT, VARIANT == 3 ? 4 : 2) void gemm_f32_kernel(GemmArgs g) {
-  constexpr int BKT = VARIANT == 0 ? 16 : 32;
-  constexpr int KH = BKT / 2;
-  constexpr int NBUF = VARIANT == 0 ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) float As[NBUF][Lds<BKT>::TILE];
-  __shared__ __attribute__((aligned(16))) float Bs[NBUF][Lds<BKT>::TILE];
-
-  const int split = blockIdx.z % g.splits;
-  const int z = blockIdx.z / g.splits;
-  const int z1 = z / g.nb2, z2 = z - z1 * g.nb2;
-  const int kbeg = split * g.kchunk;
-  const int kend = min(g.K, kbeg + g.kchunk);
-  const float* Ab = g.a.p + z1 * g.a.s1 + z2 * g.a.s2;
-  const float* Bb = g.b.p + z1 * g.b.s1 + z2 * g.b.s2;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int h = lane >> 5, l32 = lane & 31;
-
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  float4 ra[BKT / 8], rb[BKT / 8];
-  const int nk = kend > kbeg ? (kend - kbeg + BKT - 1) / BKT : 0;
-  if constexpr (VARIANT == 0) {
-    load_slab<MA, BKT>(g.a, Ab, g.M, kend, m0, kbeg, ra);
-    load_slab<MB, BKT>(g.b, Bb, g.N, kend, n0, kbeg, rb);
-    store_slab<MA, BKT>(As[0], ra);
-    store_slab<MB, BKT>(Bs[0], rb);
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < nk) {
-        load_slab<MA, BKT>(g.a, Ab, g.M, kend, m0, kbeg + (kt + 1) * BKT, ra);
-        load_slab<MB, BKT>(g.b, Bb, g.N, kend, n0, kbeg + (kt + 1) * BKT, rb);
-      }
-      float af[2][KH], bf[2][KH];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        load_frag<MA, BKT>(As[cur], wm * 64 + t * 32 + l32, h, af[t]);
-        load_frag<MB, BKT>(Bs[cur], wn * 64 + t * 32 + l32, h, bf[t]);
-      }
-      mfma_slab<KH>(acc, af, bf);
-      if (kt + 1 < nk) {
-        store_slab<MA, BKT>(As[cur ^ 1], ra);
-        store_slab<MB, BKT>(Bs[cur ^ 1], rb);
-      }
-      __syncthreads();
-    }
-  } else if constexpr (VARIANT == 2) {  // NOLINT
-    if (nk > 0) {
-      load_slab<MA, BKT>(g.a, Ab, g.M, kend, m0, kbeg, ra);
-      load_slab<MB, BKT>(g.b, Bb, g.N, kend, n0, kbeg, rb);
-    }
-    for (int kt = 0; kt < nk; ++kt) {
-      if (kt > 0) __syncthreads();  // previous slab fully read
-      store_slab<MA, BKT>(As[0], ra);
-      store_slab<MB, BKT>(Bs[0], rb);
-      __syncthreads();
-      if (kt + 1 < nk) {  // next slab's global loads fly during this slab's MFMAs
-        load_slab<MA, BKT>(g.a, Ab, g.M, kend, m0, kbeg + (kt + 1) * BKT, ra);
-        load_slab<MB, BKT>(g.b, Bb, g.N, kend, n0, kbeg + (kt + 1) * BKT, rb);
-      }
-      float af[2][KH], bf[2][KH];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        load_frag<MA, BKT>(As[0], wm * 64 + t * 32 + l32, h, af[t]);
-        load_frag<MB, BKT>(Bs[0], wn * 64 + t * 32 + l32, h, bf[t]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_slab<KH>(acc, af, bf);
-    }
-  } else {
-    for (int kt = 0; kt < nk; ++kt) {
-      load_slab<MA, BKT>(g.a, Ab, g.M, kend, m0, kbeg + kt * BKT, ra);
-      load_slab<MB, BKT>(g.b, Bb, g.N, kend, n0, kbeg + kt * BKT, rb);
-      if (kt > 0) __syncthreads();  // everyone finished reading the previous slab
-      store_slab<MA, BKT>(As[0], ra);
-      store_slab<MB, BKT>(Bs[0], rb);
-      __syncthreads();
-      if constexpr (VARIANT == 3) {
-#pragma unroll
-        for (int hs = 0; hs < 2; ++hs) {
-          float af[2][8], bf[2][8];
-#pragma unroll
-          for (int t = 0; t < 2; ++t) {
-            load_frag_half<MA>(As[0], wm * 64 + t * 32 + l32, h, hs, af[t]);
-            load_frag_half<MB>(Bs[0], wn * 64 + t * 32 + l32, h, hs, bf[t]);
-          }
-          mfma_slab<8>(acc, af, bf);
-        }
-      } else {
-        float af[2][KH], bf[2][KH];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          load_frag<MA, BKT>(As[0], wm * 64 + t * 32 + l32, h, af[t]);
-          load_frag<MB, BKT>(Bs[0], wn * 64 + t * 32 + l32, h, bf[t]);
-        }
-        // issue every LDS read of the slab before the first MFMA (one latency per slab
-        // instead of one per MFMA group); the MFMA chain then runs back to back
-        __builtin_amdgcn_sched_barrier(0);
-        mfma_slab<KH>(acc, af, bf);
-      }
-    }
-  }
-
-// ---------------------------------------------------------------- epilogue
-  float* W = g.splits > 1 ? g.work + ((long)split * g.batch + z) * (long)g.M * g.N : nullptr;  // [split][z][M][N]
-  epilogue<2, 2>(g, W, z, m0 + wm * 64, n0 + wn * 64, h, l32, acc);
-}
-
-// ============================================================================ bf16 kernel
-// bf16-input MFMA GEMM (v_mfma_f32_32x32x16_bf16, fp32 accumulate) for the reduced-precision
-// training mode (bf16 GEMM inputs, fp32 master weights / activations in HBM).
-// Register-staged FALLBACK for operands the LDS-DMA kernel cannot take (unaligned pitches);
-// the production bf16 path is gemm_glds_kernel<..., BF16 = true> below.
-// Operands stay fp32 in HBM; each 128 x 32 slab is loaded as float4, rounded to bf16 (RNE,
-// v_cvt_pk_bf16_f32) and written to LDS as [row][k] with a 40-element (80 B) row pitch, so the
-// per-lane fragment of a 32x32x16 step (8 consecutive k of one row, k = 16s + 8h + j) is one
-// conflict-free ds_read_b128 (row pitch 20 dwords: 16 rows cover the 64 banks once).
-//   KC operands: the thread's float4 is 4 consecutive k of one row -> one ds_write_b64.
-//   RC operands: the thread loads 4 float4 (k .. k+3) x (rows r .. r+3) and transposes in
-//                registers -> four ds_write_b64 (row r+i, k .. k+3).
-// The next slab's global loads fly during this slab's MFMAs (single LDS buffer, two barriers
-// per slab).  Epilogues, split-K partials and the row-sum side pass are those of the fp32 path.
-typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
-typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
-constexpr int BF_KS = 32 + 8;  // LDS row pitch in bf16 elements
-
-template <int MODE>
-__device__ __forceinline__ float4 ld4_rc(const Operand& op, const float* base, int rows, int K, int gk, int gr) {
-  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (gk >= K) return v;
-  if constexpr (MODE == RC) {
-    const float* p = base + (long)gk * op.ld + gr;
-    if (op.vec && gr + 3 < rows) return *reinterpret_cast<const float4*>(p);
-    if (gr + 0 < rows) v.x = p[0];
-    if (gr + 1 < rows) v.y = p[1];
-    if (gr + 2 < rows) v.z = p[2];
-    if (gr + 3 < rows) v.w = p[3];
-  } else {  // I2C_RC
-    if (gr + 3 < rows) return *reinterpret_cast<const float4*>(i2c_ptr(base, op.ic, gk, gr));
-    if (gr + 0 < rows) v.x = *i2c_ptr(base, op.ic, gk, gr + 0);
-    if (gr + 1 < rows) v.y = *i2c_ptr(base, op.ic, gk, gr + 1);
-    if (gr + 2 < rows) v.z = *i2c_ptr(base, op.ic, gk, gr + 2);
-  }
-  return v;
-}
-
-// this thread's 16 elements of a (128 rows x 32 k) slab
-template <int MODE>
-__device__ __forceinline__ void load_slab_bf(const Operand& op, const float* base, int rows, int K, int row0,
-                                             int k0, float4 (&reg)[4]) {
-  if constexpr (MODE == KC || MODE == I2C_KC) {
-    load_slab<MODE, 32>(op, base, rows, K, row0, k0, reg);  // reg[it]: row (t + 256 it) / 8, k 4 * (t % 8)
-  } else {
-    const int rq = (threadIdx.x & 31) * 4, kq = (threadIdx.x >> 5) * 4;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) reg[j] = ld4_rc<MODE>(op, base, rows, K, k0 + kq + j, row0 + rq);
-  }
-}
-
-__device__ __forceinline__ bf16x4 to_bf4(float a, float b, float c, float d) {
-  bf16x4 r;
-  r[0] = (__bf16)a; r[1] = (__bf16)b; r[2] = (__bf16)c; r[3] = (__bf16)d;
-  return r;
-}
-
-template <int MODE>
-__device__ __forceinline__ void store_slab_bf(__bf16* lds, const float4 (&reg)[4]) {
-  if constexpr (MODE == KC || MODE == I2C_KC) {
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int idx = threadIdx.x + it * NT;
-      const int r = idx >> 3, kq = (idx & 7) * 4;
-      *reinterpret_cast<bf16x4*>(lds + r * BF_KS + kq) = to_bf4(reg[it].x, reg[it].y, reg[it].z, reg[it].w);
-    }
-  } else {
-    const int rq = (threadIdx.x & 31) * 4, kq = (threadIdx.x >> 5) * 4;
-    *reinterpret_cast<bf16x4*>(lds + (rq + 0) * BF_KS + kq) = to_bf4(reg[0].x, reg[1].x, reg[2].x, reg[3].x);
-    *reinterpret_cast<bf16x4*>(lds + (rq + 1) * BF_KS + kq) = to_bf4(reg[0].y, reg[1].y, reg[2].y, reg[3].y);
-    *reinterpret_cast<bf16x4*>(lds + (rq + 2) * BF_KS + kq) = to_bf4(reg[0].z, reg[1].z, reg[2].z, reg[3].z);
-    *reinterpret_cast<bf16x4*>(lds + (rq + 3) * BF_KS + kq) = to_bf4(reg[0].w, reg[1].w, reg[2].w, reg[3].w);
-  }
-}
-
-template <int MA, int MB>
-__global__ __launch_bounds__(NT, 2) void gemm_bf16_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) __bf16 lds[(BM + BN) * BF_KS];
-  __bf16* As = lds;
-  __bf16* Bs = lds + BM * BF_KS;
-
-  const int split = blockIdx.z % g.splits;
-  const int z = blockIdx.z / g.splits;
-  const int z1 = z / g.nb2, z2 = z - z1 * g.nb2;
-  const int kbeg = split * g.kchunk;
-  const int kend = min(g.K, kbeg + g.kchunk);
-  const float* Ab = g.a.p + z1 * g.a.s1 + z2 * g.a.s2;
-  const float* Bb = g.b.p + z1 * g.b.s1 + z2 * g.b.s2;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const int h = lane >> 5, l32 = lane & 31;
-
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  float4 ra[4], rb[4];
-  const int nk = kend > kbeg ? (kend - kbeg + 31) / 32 : 0;
-  if (nk > 0) {
-    load_slab_bf<MA>(g.a, Ab, g.M, kend, m0, kbeg, ra);
-    load_slab_bf<MB>(g.b, Bb, g.N, kend, n0, kbeg, rb);
-  }
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt > 0) __syncthreads();  // previous slab fully read
-    store_slab_bf<MA>(As, ra);
-    store_slab_bf<MB>(Bs, rb);
-    __syncthreads();
-    if (kt + 1 < nk) {
-      load_slab_bf<MA>(g.a, Ab, g.M, kend, m0, kbeg + (kt + 1) * 32, ra);
-      load_slab_bf<MB>(g.b, Bb, g.N, kend, n0, kbeg + (kt + 1) * 32, rb);
-    }
-    bf16x8 af[2][2], bf[2][2];  // [tile][k-step]
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        af[t][s] = *reinterpret_cast<const bf16x8*>(As + (wm * 64 + t * 32 + l32) * BF_KS + 16 * s + 8 * h);
-        bf[t][s] = *reinterpret_cast<const bf16x8*>(Bs + (wn * 64 + t * 32 + l32) * BF_KS + 16 * s + 8 * h);
-      }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
-  }
-
-  float* W = g.splits > 1 ? g.work + ((long)split * g.batch + z) * (long)g.M * g.N : nullptr;
-  if (g.wide) {
-    if (W) store_partials_wide<2, 2>(g, W, m0 + wm * 64, n0 + wn * 64, lane, acc);
-    else if (g.bwd_act) store_tiles_wide<EPI_BWD, 2, 2>(g, z, m0 + wm * 64, n0 + wn * 64, lane, acc);
-    else if (g.bias || g.aux || g.act || g.drop_thresh)
-      store_tiles_wide<EPI_FWD, 2, 2>(g, z, m0 + wm * 64, n0 + wn * 64, lane, acc);
-    else store_tiles_wide<EPI_PLAIN, 2, 2>(g, z, m0 + wm * 64, n0 + wn * 64, lane, acc);
-  } else {
-    epilogue<2, 2>(g, W, z, m0 + wm * 64, n0 + wn * 64, h, l32, acc);
-  }
-}
-
-// ============================================================================ glds kernel
-// The production path.  Global->LDS staging with global_load_lds_dwordx4 (LDS-DMA: no VGPR
-// round trip, asynchronous until its vmcnt), two LDS buffers, raw s_barrier with explicit
-// waits, so slab k+1 streams in while slab k's MFMAs run.  All LDS in ONE __shared__ array
-// (a second object makes hipcc drain vmcnt before every ds_read).  Requires 16-B aligned
-// operands with ld % 4 == 0 (the host falls back to the register-staged kernel otherwise).
-//
-// LDS images are lane-linear per wave instruction (1 KB = 64 lanes x 16 B); the swizzle is
-// applied to the per-lane GLOBAL source address:
-//   KC [rows][32]: quad q of row r at slot r*8 + (q ^ (r&7))   -> ds_read_b128 conflict-free
-//   RC [32][rows]: element (k,r) at k*rows + (r ^ ((k>>4)<<5)) -> the two lane halves
-//                  (k and k+16) land on opposite 32-bank halves, ds_read_b32 conflict-free
-// Out-of-range rows / k are clamped to in-bounds addresses (their products only reach
-// discarded outputs); the K tail of the last slab is zeroed in LDS before use.
-// Block ids are remapped so that consecutive tiles (same A row panel) share an XCD's L2.
-
-
-struct GldsArgs {
-  FastDiv c_a, c_b;    // im2col channel count C
-  FastDiv hw_b, wo_b;  // I2C_RC: output pixels per map (Ho*Wo), Wo
-  FastDiv hw_a, wo_a;  // I2C_KC
-  int ntx, nty;        // tile grid (N tiles, M tiles)
-  int ntiles;          // ntx * nty * batch * splits
-  // I2CT_KC (conv2 input gradient as an implicit GEMM per parity class): A(r, k) =
-  // dY[b, a - dt[t], e - df[t], o] (0 outside the T2 x F2 grid), r = (b, a, e) over Ha x We,
-  // k = t*C + o (tap t of the class, channel o); C % 32 == 0 so a slab never straddles taps
-  FastDiv t_hw, t_w;
-  int t_T2, t_F2, t_C;
-  int t_dt[4], t_df[4];
-  const float* t_zeros;  // >= 16 zero bytes: the DMA source of lanes outside the grid
-  int abl;             // diagnostic ablation bits (ESP_GEMM_ABL, timing only): 1 no DMA after the
-                       // first slab, 2 no epilogue stores, 4 no k-loop barrier / waits, 16 dword
-                       // (not float4) epilogue stores, 32 non-temporal epilogue stores
-};
-
-constexpr int GL_BK = 32;
-
-// One global_load_lds_dwordx4: lane l's 16 B at gptr land at lds_wave_base + 16*l.  Issued from
-// inline asm so that hipcc does not see an LDS-DMA store: with the builtin it cannot prove
-// the DMA target (the other buffer) disjoint from this slab's ds_reads and drains vmcnt(0)
-// before every slab's first ds_read, serialising the pipeline.  The ordering the compiler
-// no longer sees is made explicit: wait_vm0() + raw_barrier() before a slab is read, and the
-// "memory" clobber keeps LDS accesses on their side of the asm.  M0 is set per instruction.
-__device__ __forceinline__ void lds_dma16(const float* gptr, float* lds_wave_base) {
-  const uint32_t m0 = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds_wave_base);
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gptr), "s"(m0) : "memory", "m0");
-}
-
-// element offset of im2col column `col` (= (kt,kf,c)) relative to the receptive field origin
-__device__ __forceinline__ long i2c_col_off(const Im2col& ic, const FastDiv& fc, int col) {
-  const int kk = (int)fdiv((uint32_t)col, fc), c = col - kk * ic.C;
-  const int kt = kk / 3, kf = kk - kt * 3;
-  return ((long)kt * ic.W + kf) * ic.C + c;
-}
-// element offset of output pixel `pix`'s receptive field origin
-__device__ __forceinline__ long i2c_pix_off(const Im2col& ic, const FastDiv& fhw, const FastDiv& fwo, int pix) {
-  const int bi = (int)fdiv((uint32_t)pix, fhw);
-  const int rem = pix - bi * (int)fhw.d;
-  const int ho = (int)fdiv((uint32_t)rem, fwo), wo = rem - ho * (int)fwo.d;
-  return (((long)bi * ic.H + 2 * ho) * ic.W + 2 * wo) * ic.C;
-}
-
-// Per-lane source bookkeeping for one operand: NI wave-instructions per slab.
-template <int MODE, int ROWS, int NI>
-struct Stage {
-  static constexpr bool kKC = MODE == KC || MODE == I2C_KC || MODE == I2CT_KC;
-  const float* p[NI];  // per instruction: base incl. the slab-invariant part
-  int q[NI];           // KC: k offset inside the slab (4*quad) ; RC: k-row inside the slab
-  int ga[MODE == I2CT_KC ? NI : 1], ge[MODE == I2CT_KC ? NI : 1];  // I2CT: class-grid row / column
-  __device__ __forceinline__ void init(const Operand& op, const float* base, int rows, int K, int row0,
-                                       const FastDiv& fc, const FastDiv& fhw, const FastDiv& fwo, int wave,
-                                       int lane, const GldsArgs* x = nullptr) {
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int slot = (i * 4 + wave) * 64 + lane;
-      if constexpr (kKC) {
-        const int r = slot >> 3, qs = slot & 7;
-        const int qq = qs ^ (r & 7);
-        const int gr = min(row0 + r, rows - 1);
-        q[i] = 4 * qq;
-        if constexpr (MODE == KC) p[i] = base + (long)gr * op.ld;
-        else if constexpr (MODE == I2C_KC) p[i] = base + i2c_pix_off(op.ic, fhw, fwo, gr);
-        else {
-          const int bb = (int)fdiv((uint32_t)gr, x->t_hw);
-          const int rem = gr - bb * (int)x->t_hw.d;
-          const int a = (int)fdiv((uint32_t)rem, x->t_w), e = rem - a * (int)x->t_w.d;
-          ga[i] = a;
-          ge[i] = e;
-          p[i] = base + (((long)bb * x->t_T2 + a) * x->t_F2 + e) * x->t_C;
-        }
-      } else {
-        constexpr int QPR = ROWS / 4;  // quads per k-row
-        const int kr = slot / QPR, rs = slot % QPR;
-        const int rq = rs ^ (((kr >> 4) & 1) << 3);
-        const int gr = min(row0 + 4 * rq, (rows - 1) & ~3);
-        q[i] = kr;
-        if constexpr (MODE == RC) p[i] = base + gr;
-        else p[i] = base + i2c_col_off(op.ic, fc, gr);
-      }
-    }
-  }
-  // issue this lane's NI LDS-DMA loads of the slab starting at k0 into `dst`
-  __device__ __forceinline__ void issue(const Operand& op, int K, int k0, float* dst, int wave, const FastDiv& fc,
-                                        const FastDiv& fhw, const FastDiv& fwo, const GldsArgs* x = nullptr) const {
-    int dt = 0, df = 0, o0 = 0;
-    if constexpr (MODE == I2CT_KC) {  // the slab's tap (uniform: C % 32 == 0)
-      const int t = k0 / x->t_C;
-      o0 = k0 - t * x->t_C;
-      dt = x->t_dt[t];
-      df = x->t_df[t];
-    }
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      float* ldsw = dst + (i * 4 + wave) * 256;
-      if constexpr (kKC) {
-        const int k = min(k0 + q[i], (K - 1) & ~3);
-        if constexpr (MODE == KC) lds_dma16(p[i] + k, ldsw);
-        else if constexpr (MODE == I2C_KC) lds_dma16(p[i] + i2c_col_off(op.ic, fc, k), ldsw);
-        else {
-          const int a = ga[i] - dt, e = ge[i] - df;
-          const bool in = a >= 0 && a < x->t_T2 && e >= 0 && e < x->t_F2;
-          lds_dma16(in ? p[i] - ((long)dt * x->t_F2 + df) * x->t_C + o0 + q[i] : x->t_zeros, ldsw);
-        }
-      } else {
-        const int k = min(k0 + q[i], K - 1);
-        if constexpr (MODE == RC) lds_dma16(p[i] + (long)k * op.ld, ldsw);
-        else lds_dma16(p[i] + i2c_pix_off(op.ic, fhw, fwo, k), ldsw);
-      }
-    }
-  }
-};
-
-// zero k >= kv of a staged slab (last slab of a K range that is not a multiple of 32)
-template <int MODE, int ROWS>
-__device__ __forceinline__ void zero_tail(float* slab, int kv) {
-  for (int idx = threadIdx.x; idx < ROWS * GL_BK; idx += NT) {
-    if constexpr (MODE == KC || MODE == I2C_KC || MODE == I2CT_KC) {
-      const int r = idx >> 5, k = idx & 31;
-      if (k >= kv) slab[(r * 8 + ((k >> 2) ^ (r & 7))) * 4 + (k & 3)] = 0.f;
-    } else {
-      const int k = idx / ROWS;
-      if (k >= kv) slab[idx] = 0.f;
-    }
-  }
-}
-
-// the 16 k-values (k = 16h + s) of tile row r
-template <int MODE, int ROWS>
-__device__ __forceinline__ void frag16(const float* slab, int r, int h, float (&f)[16]) {
-  if constexpr (MODE == KC || MODE == I2C_KC || MODE == I2CT_KC) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float4 v = *reinterpret_cast<const float4*>(slab + (r * 8 + ((4 * h + j) ^ (r & 7))) * 4);
-      f[4 * j + 0] = v.x; f[4 * j + 1] = v.y; f[4 * j + 2] = v.z; f[4 * j + 3] = v.w;
-    }
-  } else {
-    const int rr = r ^ (h << 5);
-#pragma unroll
-    for (int s = 0; s < 16; ++s) f[s] = slab[(16 * h + s) * ROWS + rr];
-  }
-}
-
-__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-// s_barrier without __syncthreads()'s fence (which would drain vmcnt); the empty asm keeps
-// the compiler from moving LDS accesses across it
-__device__ __forceinline__ void raw_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-// Tile t of the launch -> coordinates.  Tiles are processed in rounds of G (the grid): tile t
-// runs on block t % G, which the hardware placed on XCD (t % G) & 7; inside a round the tile
-// order is remapped (bijectively, also for a partial last round) so that the tiles resident on
-// one XCD at the same time are consecutive: they share A row panels in that XCD's L2.
-struct TileCoord {
-  int m0, n0, tn, z, split, kbeg, kend, nk;
-};
-template <int BNT>
-__device__ __forceinline__ TileCoord tile_coord(const GemmArgs& g, const GldsArgs& x, int t, int G) {
-  const int round = t / G, b = t - round * G;
-  const int nr = min(G, x.ntiles - round * G);
-  const int xcd = b & 7, per = nr >> 3, rem = nr & 7;
-  const int wg = round * G + (xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per) + (b >> 3);
-  TileCoord c;
-  c.tn = wg % x.ntx;
-  const int t2 = wg / x.ntx;
-  const int tm = t2 % x.nty;
-  const int zz = t2 / x.nty;
-  c.split = zz % g.splits;
-  c.z = zz / g.splits;
-  c.kbeg = c.split * g.kchunk;
-  c.kend = min(g.K, c.kbeg + g.kchunk);
-  c.nk = (c.kend - c.kbeg + GL_BK - 1) / GL_BK;  // >= 1: the host routes K == 0 elsewhere
-  c.m0 = tm * BM;
-  c.n0 = c.tn * BNT;
-  return c;
-}
-
-// resident blocks per CU: 128x64 tiles (48 KB LDS) fit three, 128x128 tiles (64 KB) two; the
-// fused epilogues need the registers of two
-template <int BNT, int EPI>
-constexpr int glds_occupancy() { return (BNT == 64 && EPI == 0) ? 3 : 2; }
-
-// Persistent: block b processes tiles b, b+G, b+2G, ... as ONE continuous slab pipeline — the
-// first slab of the next tile streams in during the last slab of the current one, and the
-// current tile's epilogue stores drain while the next tile's MFMAs run (on this and the other
-// resident blocks' waves).  With G = #tiles every block runs one tile (the classic launch).
-//
-// BF16 = true (esp_set_gemm_compute(1)): the same fp32 LDS-DMA pipeline, but each lane's 16
-// staged k-values per tile row are rounded to bf16 in registers (v_cvt_pk_bf16_f32) and fed to
-// two v_mfma_f32_32x32x16_bf16 per (i, j) tile pair instead of sixteen 32x32x2 f32 MFMAs: k-step
-// 0 takes the lane's values s = 0..7 (k = 16h + s), step 1 s = 8..15, identically for A and B,
-// so the two steps cover the slab's 32 k once.  The fused row sums stay fp32.
-template <int MA, int MB, int BNT, bool RS, int EPI, bool BF16 = false>
-__global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_kernel(GemmArgs g, GldsArgs x) {
-  constexpr int WN = BNT / 64, WM = 4 / WN, TM = BM / (WM * 32), TN = 2;
-  constexpr int A_SZ = BM * GL_BK, B_SZ = BNT * GL_BK, BUF = A_SZ + B_SZ;
-  constexpr int NIA = A_SZ / 4 / NT, NIB = B_SZ / 4 / NT;
-  __shared__ __attribute__((aligned(16))) float smem[2 * BUF];
-
-  const int G = gridDim.x;
-  int t = blockIdx.x;
-  if (t >= x.ntiles) return;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave / WN, wn = wave % WN;
-  const int h = lane >> 5, l32 = lane & 31;
-
-  auto a_base = [&](const TileCoord& c) {
-    const int z1 = c.z / g.nb2, z2 = c.z - z1 * g.nb2;
-    return g.a.p + z1 * g.a.s1 + z2 * g.a.s2;
-  };
-  auto b_base = [&](const TileCoord& c) {
-    const int z1 = c.z / g.nb2, z2 = c.z - z1 * g.nb2;
-    return g.b.p + z1 * g.b.s1 + z2 * g.b.s2;
-  };
-
-  TileCoord c = tile_coord<BNT>(g, x, t, G);
-  Stage<MA, BM, NIA> sa;
-  Stage<MB, BNT, NIB> sb;
-  sa.init(g.a, a_base(c), g.M, g.K, c.m0, x.c_a, x.hw_a, x.wo_a, wave, lane, &x);
-  sb.init(g.b, b_base(c), g.N, g.K, c.n0, x.c_b, x.hw_b, x.wo_b, wave, lane);
-  sa.issue(g.a, g.K, c.kbeg, smem, wave, x.c_a, x.hw_a, x.wo_a, &x);
-  sb.issue(g.b, g.K, c.kbeg, smem + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
-  wait_vm0();
-  raw_barrier();
-  int buf = 0;
-
-  for (;;) {
-    f32x16 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-    // fused bias gradient (A = dy in RC mode): the first column tile's wn==0 waves sum their A
-    // fragments over k; halves combined and splits reduced in fixed order (deterministic)
-    const bool do_rs = RS && c.tn == 0 && wn == 0;
-    float rs[TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) rs[i] = 0.f;
-    const int tnext = t + G;
-    const bool has_next = tnext < x.ntiles;
-    TileCoord cn = c;
-
-    // frags + MFMAs of one staged slab (and the fused row sums)
-    auto compute = [&](const float* cur) {
-      float af[TM][16], bf[TN][16];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) frag16<MA, BM>(cur, wm * TM * 32 + i * 32 + l32, h, af[i]);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) frag16<MB, BNT>(cur + A_SZ, wn * 64 + j * 32 + l32, h, bf[j]);
-      if constexpr (BF16) {
-        bf16x8 ah[TM][2], bh[TN][2];
-#pragma unroll
-        for (int hs = 0; hs < 2; ++hs) {
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) ah[i][hs][e] = (__bf16)af[i][8 * hs + e];
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) bh[j][hs][e] = (__bf16)bf[j][8 * hs + e];
-        }
-#pragma unroll
-        for (int hs = 0; hs < 2; ++hs)
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][hs], bh[j][hs], acc[i][j], 0, 0, 0);
-      } else {
-#pragma unroll
-        for (int s = 0; s < 16; ++s)
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][s], bf[j][s], acc[i][j], 0, 0, 0);
-      }
-      if constexpr (RS) {
-        if (do_rs) {  // after the MFMAs were issued: the adds ride in their shadow
-#pragma unroll
-          for (int i = 0; i < TM; ++i) {
-            float a0 = 0.f;
-#pragma unroll
-            for (int s = 0; s < 16; ++s) a0 += af[i][s];
-            rs[i] += a0;
-          }
-        }
-      }
-    };
-    auto finish_slab = [&]() {
-      if (!(x.abl & 4)) {
-        wait_vm0();     // this wave's DMA of the next slab has landed
-        wait_lgkm0();   // this wave's reads of this slab are done
-        raw_barrier();  // -> everyone's: next slab readable, this buffer free for the one after
-      }
-      buf ^= 1;
-    };
-
-    for (int kt = 0; kt + 1 < c.nk; ++kt) {  // all but the last slab: slab kt+1 streams in
-      const int k1 = c.kbeg + (kt + 1) * GL_BK;
-      float* nxt = smem + (buf ^ 1) * BUF;  // last read before the previous barrier
-      if (!(x.abl & 1)) {
-        sa.issue(g.a, g.K, k1, nxt, wave, x.c_a, x.hw_a, x.wo_a, &x);
-        sb.issue(g.b, g.K, k1, nxt + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
-      }
-      compute(smem + buf * BUF);
-      finish_slab();
-    }
-    {  // last slab: the next tile's first slab streams in (this tile's stages are done)
-      float* cur = smem + buf * BUF;
-      float* nxt = smem + (buf ^ 1) * BUF;
-      if (has_next) {
-        cn = tile_coord<BNT>(g, x, tnext, G);
-        sa.init(g.a, a_base(cn), g.M, g.K, cn.m0, x.c_a, x.hw_a, x.wo_a, wave, lane, &x);
-        sb.init(g.b, b_base(cn), g.N, g.K, cn.n0, x.c_b, x.hw_b, x.wo_b, wave, lane);
-        sa.issue(g.a, g.K, cn.kbeg, nxt, wave, x.c_a, x.hw_a, x.wo_a, &x);
-        sb.issue(g.b, g.K, cn.kbeg, nxt + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
-      }
-      const int kv = c.kend - (c.kbeg + (c.nk - 1) * GL_BK);
-      if (kv < GL_BK) {
-        zero_tail<MA, BM>(cur, kv);
-        zero_tail<MB, BNT>(cur + A_SZ, kv);
-        wait_lgkm0();
-        raw_barrier();
-      }
-      compute(cur);
-      finish_slab();
-    }
-    // epilogue: fire-and-forget stores that drain under the next tile's first slab
-    if (RS && do_rs) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const float v = rs[i] + __shfl_xor(rs[i], 32, 64);  // k halves 0-15 / 16-31 of every slab
-        const int m = c.m0 + wm * TM * 32 + i * 32 + l32;
-        if (h == 0 && m < g.M) {
-          if (g.splits > 1) g.rs_work[(long)c.split * g.M + m] = v;
-          else g.rowsum[m] += v;
-        }
-      }
-    }
-    if (!(x.abl & 2)) {
-      float* W = g.splits > 1 ? g.work + ((long)c.split * g.batch + c.z) * (long)g.M * g.N : nullptr;
-      if (g.wide) {
-        if (W) store_partials_wide<TM, TN>(g, W, c.m0 + wm * TM * 32, c.n0 + wn * 64, lane, acc);
-        else store_tiles_wide<EPI, TM, TN>(g, c.z, c.m0 + wm * TM * 32, c.n0 + wn * 64, lane, acc, (x.abl & 32) != 0);
-      } else {
-        if (W) store_partials<TM, TN>(g, W, c.m0 + wm * TM * 32, c.n0 + wn * 64, h, l32, acc);
-        else store_tiles<EPI, TM, TN>(g, c.z, c.m0 + wm * TM * 32, c.n0 + wn * 64, h, l32, acc);
-      }
-    }
-    if (!has_next) break;
-    t = tnext;
-    c = cn;
-  }
-}
 
 // split-K reduction in fixed split order + the fused epilogue (4 outputs per thread when
 // N % 4 == 0: float4 partial loads)
@@ -1290,6 +135,7 @@ long persist_blocks(int per_cu) {
 
 int g_compute = 0;  // 0: fp32 MFMA (exact f32 fma chain), 1: bf16-input MFMA with fp32 accumulate
 
+// ESP_GEMM_VARIANT != 4 forces the register-staged fallback kernel (diagnostics)
 int g_variant = -1;
 int variant() {
   if (g_variant < 0) {
@@ -1300,14 +146,20 @@ int variant() {
 }
 
 // Launch the LDS-DMA kernel with the epilogue kind compiled in (each kind is its own kernel,
-// so the plain GEMMs carry none of the fused epilogues' registers).  Returns false when the
-// mode pair has no instantiation of the needed kind (the caller falls back).
-template <int MA, int MB, int BNT, bool BF>
-bool launch_glds_t(const GemmArgs& g, int batch, hipStream_t st, const GldsArgs* tconv) {
-  constexpr bool can_rs = MA == RC;
-  constexpr bool can_fwd = (MA == KC && (MB == KC || MB == RC)) || (MA == I2C_KC && MB == KC);
-  constexpr bool can_bwd = (MA == KC || MA == I2CT_KC) && MB == RC;
-  const int kind = g.splits > 1 ? EPI_PLAIN : epi_kind(g);
+// so the plain GEMMs carry none of the fused epilogues' registers; the instantiations live in
+// the gemm_glds_*.hip units).  Returns false when the mode pair has no instantiation of the
+// needed kind (the caller falls back to the register-staged kernel).
+bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, const GldsArgs* tconv = nullptr) {
+  const int BNT = g.bnt;
+  const bool can_rs = MA == RC;
+  const bool can_fwd = (MA == KC && (MB == KC || MB == RC)) || (MA == I2C_KC && MB == KC);
+  const bool can_bwd = (MA == KC || MA == I2CT_KC) && MB == RC;
+  const bool can_spec_fwd = MA == KC && MB == KC, can_spec_bwd = MA == KC && MB == RC;
+  const bool can_pspec = (MA == KC || MA == RC) && (MB == KC || MB == RC);
+  int kind = g.splits > 1 ? EPI_PLAIN : epi_kind_spec(g);
+  if ((kind == EPI_BMUL && !can_spec_bwd) || ((kind == EPI_P0 || kind == EPI_PR) && !can_pspec) ||
+      (kind >= EPI_BIAS && kind <= EPI_FFN_RELU && !can_spec_fwd))
+    kind = epi_kind(g);
   if ((kind == EPI_FWD && !can_fwd) || (kind == EPI_BWD && !can_bwd)) return false;
   GldsArgs x{};
   if (MA == I2CT_KC) x = *tconv;  // the transposed-conv gather parameters
@@ -1329,34 +181,20 @@ bool launch_glds_t(const GemmArgs& g, int batch, hipStream_t st, const GldsArgs*
     if (abl < 0) abl = getenv("ESP_GEMM_ABL") ? atoi(getenv("ESP_GEMM_ABL")) : 0;
     x.abl = abl;
   }
-  auto grid = [&](int per_cu) { return dim3((unsigned)std::min<long>(x.ntiles, persist_blocks(per_cu))); };
-  if (can_rs && g.rowsum)
-    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, can_rs, EPI_PLAIN, BF>), grid(glds_occupancy<BNT, EPI_PLAIN>()),
-                       dim3(NT), 0, st, g, x);
-  else if (kind == EPI_PLAIN)
-    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_PLAIN, BF>), grid(glds_occupancy<BNT, EPI_PLAIN>()),
-                       dim3(NT), 0, st, g, x);
-  else if (kind == EPI_FWD) {
-    if constexpr (can_fwd)
-      hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_FWD, BF>), grid(glds_occupancy<BNT, EPI_FWD>()),
-                         dim3(NT), 0, st, g, x);
-  } else if constexpr (can_bwd) {
-    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_BWD, BF>), grid(glds_occupancy<BNT, EPI_BWD>()),
-                       dim3(NT), 0, st, g, x);
-  }
-  return true;
-}
-template <int MA, int MB, int BNT>
-bool launch_glds(const GemmArgs& g, int batch, hipStream_t st, const GldsArgs* tconv = nullptr) {
-  if (g.bf16) return launch_glds_t<MA, MB, BNT, true>(g, batch, st, tconv);
-  return launch_glds_t<MA, MB, BNT, false>(g, batch, st, tconv);
+  const bool rs = can_rs && g.rowsum;
+  if (rs) kind = EPI_PLAIN;
+  const dim3 grid((unsigned)std::min<long>(x.ntiles, persist_blocks(glds_occupancy_rt(BNT, kind))));
+  const bool bf = g.bf16 != 0;
+  if (kind == EPI_PLAIN) return glds_launch_plain(MA, MB, BNT, bf, rs, grid, st, g, x);
+  if (kind == EPI_FWD || kind == EPI_BWD) return glds_launch_epi(MA, MB, BNT, bf, kind, grid, st, g, x);
+  if (kind == EPI_P0 || kind == EPI_PR) return glds_launch_pspec(MA, MB, BNT, bf, kind, grid, st, g, x);
+  return glds_launch_spec(MA, MB, BNT, bf, kind, grid, st, g, x);
 }
 
 template <int MA, int MB>
 int launch(const GemmArgs& g0, int batch, hipStream_t st) {
   bool done = false;
-  if (g0.bnt == 64) done = launch_glds<MA, MB, 64>(g0, batch, st);
-  else if (g0.bnt == 128) done = launch_glds<MA, MB, 128>(g0, batch, st);
+  if (g0.bnt == 64 || g0.bnt == 128) done = launch_glds(MA, MB, g0, batch, st);
   GemmArgs g = g0;
   if (!done) {
     g.rs_work = nullptr;
@@ -1365,9 +203,6 @@ int launch(const GemmArgs& g0, int batch, hipStream_t st) {
                          g.rowsum);
     dim3 grid((g.N + BN - 1) / BN, (g.M + BM - 1) / BM, batch * g.splits);
     if (g.bf16) hipLaunchKernelGGL((gemm_bf16_kernel<MA, MB>), grid, dim3(NT), 0, st, g);
-    else if (variant() == 0) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 0>), grid, dim3(NT), 0, st, g);
-    else if (variant() == 2) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 2>), grid, dim3(NT), 0, st, g);
-    else if (variant() == 3) hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 3>), grid, dim3(NT), 0, st, g);
     else hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 1>), grid, dim3(NT), 0, st, g);
   }
   if (g.splits > 1) {
@@ -1422,6 +257,9 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
   ESP_ARG_CHECK(mode_a >= 0 && mode_a <= 3 && mode_b >= 0 && mode_b <= 3, "esp_gemm_f32: bad mode");
   ESP_ARG_CHECK(drop_p >= 0.f && drop_p < 1.f, "esp_gemm_f32: bad dropout p");
   ESP_ARG_CHECK(!bwd_act || (pre && !aux && act == 0), "esp_gemm_f32: bwd_act needs pre and no forward activation");
+  ESP_ARG_CHECK(bwd_act >= 0 && bwd_act <= ACT_MUL && (act & ~(3 | ACT_AUX_DERIV)) == 0 && (act & 3) <= ACT_SWISH,
+                "esp_gemm_f32: bad act / bwd_act code");
+  ESP_ARG_CHECK(!(act & ACT_AUX_DERIV) || aux, "esp_gemm_f32: ACT_AUX_DERIV needs aux");
   ESP_ARG_CHECK(!rowsum || (mode_a == 1 && batch == 1), "esp_gemm_f32: rowsum needs an RC-mode A and batch 1");
   if (M == 0 || N == 0) return 0;
   GemmArgs g{};
@@ -1593,7 +431,7 @@ ESP_API int esp_conv2_dgrad(const float* dz2, const float* W, const float* z1, f
     g.cmap = 1;
     g.cm_hw = t.t_hw; g.cm_w = t.t_w;
     g.cm_T1 = T1; g.cm_F1 = F1; g.cm_ph = ph; g.cm_pw = pw;
-    if (!launch_glds<I2CT_KC, RC, 64>(g, 1, st, &t)) {
+    if (!launch_glds(I2CT_KC, RC, g, 1, st, &t)) {
       esp::set_error("esp_conv2_dgrad: no kernel for the class GEMM");
       return -1;
     }

@@ -1,0 +1,23 @@
+// Instantiations of gemm_glds_kernel with the plain epilogue (alpha*acc + beta*R, split-K
+// partials, fused row sums).  Compiled separately from gemm.hip so the GEMM family builds in
+// parallel; device code in gemm_kernels.h.
+#include "gemm_kernels.h"
+
+namespace espg {
+
+bool glds_launch_plain(int ma, int mb, int bnt, bool bf, bool rs, dim3 grid, hipStream_t st, const GemmArgs& g,
+                       const GldsArgs& x) {
+  return glds_switch(ma, mb, bnt, bf, [&](auto A, auto B, auto N, auto F) {
+    constexpr int MA = decltype(A)::value, MB = decltype(B)::value, BNT = decltype(N)::value;
+    constexpr bool BF = decltype(F)::value;
+    if constexpr (MA == RC) {
+      if (rs) {
+        hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, true, EPI_PLAIN, BF>), grid, dim3(NT), 0, st, g, x);
+        return;
+      }
+    }
+    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_PLAIN, BF>), grid, dim3(NT), 0, st, g, x);
+  });
+}
+
+}  // namespace espg

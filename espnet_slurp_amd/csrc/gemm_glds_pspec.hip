@@ -1,0 +1,27 @@
+// Instantiations of gemm_glds_kernel with the specialised plain epilogues (EPI_P0: alpha*acc,
+// EPI_PR: alpha*acc + beta*R; unsplit, wide stores) for the linear / attention mode pairs.
+// See store_spec in gemm_kernels.h.
+#include "gemm_kernels.h"
+
+namespace espg {
+
+bool glds_launch_pspec(int ma, int mb, int bnt, bool bf, int epi, dim3 grid, hipStream_t st, const GemmArgs& g,
+                       const GldsArgs& x) {
+  bool ok = false;
+  const bool known = glds_switch(ma, mb, bnt, bf, [&](auto A, auto B, auto N, auto F) {
+    constexpr int MA = decltype(A)::value, MB = decltype(B)::value, BNT = decltype(N)::value;
+    constexpr bool BF = decltype(F)::value;
+    if constexpr ((MA == KC || MA == RC) && (MB == KC || MB == RC)) {
+      if (epi == EPI_P0) {
+        hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_P0, BF>), grid, dim3(NT), 0, st, g, x);
+        ok = true;
+      } else if (epi == EPI_PR) {
+        hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_PR, BF>), grid, dim3(NT), 0, st, g, x);
+        ok = true;
+      }
+    }
+  });
+  return known && ok;
+}
+
+}  // namespace espg

@@ -1,0 +1,32 @@
+// Instantiations of gemm_glds_kernel with the specialised (compile-time feature set) epilogues
+// of the production call sites: EPI_BIAS / EPI_BDR / EPI_FFN_SWISH / EPI_FFN_RELU for the linear
+// forward (KC x KC), EPI_BMUL for the FFN input gradient (KC x RC).  See store_spec.
+#include "gemm_kernels.h"
+
+namespace espg {
+
+bool glds_launch_spec(int ma, int mb, int bnt, bool bf, int epi, dim3 grid, hipStream_t st, const GemmArgs& g,
+                      const GldsArgs& x) {
+  bool ok = false;
+  const bool known = glds_switch(ma, mb, bnt, bf, [&](auto A, auto B, auto N, auto F) {
+    constexpr int MA = decltype(A)::value, MB = decltype(B)::value, BNT = decltype(N)::value;
+    constexpr bool BF = decltype(F)::value;
+#define ESP_SPEC(K)                                                                                   \
+  if (epi == K) {                                                                                     \
+    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, K, BF>), grid, dim3(NT), 0, st, g, x); \
+    ok = true;                                                                                        \
+  }
+    if constexpr (MA == KC && MB == KC) {
+      ESP_SPEC(EPI_BIAS)
+      ESP_SPEC(EPI_BDR)
+      ESP_SPEC(EPI_FFN_SWISH)
+      ESP_SPEC(EPI_FFN_RELU)
+    } else if constexpr (MA == KC && MB == RC) {
+      ESP_SPEC(EPI_BMUL)
+    }
+#undef ESP_SPEC
+  });
+  return known && ok;
+}
+
+}  // namespace espg

@@ -15,6 +15,8 @@ from . import _native
 
 KC, RC, I2C_KC, I2C_RC = 0, 1, 2, 3
 ACT_NONE, ACT_RELU, ACT_SWISH = 0, 1, 2
+ACT_MUL = 3          # bwd_act: dx = (dy W) * pre, pre holding dh/dv from an ACT_AUX_DERIV forward
+ACT_AUX_DERIV = 16   # act flag: aux <- dh/dv of h = drop(act(v)) instead of v (gemm.hip fwd_elem)
 
 
 def _p(t: Optional[torch.Tensor], off: int = 0):

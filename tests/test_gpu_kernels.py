@@ -131,6 +131,34 @@ def test_gemm_backward_activation_epilogue(dev, act):
     assert (out.cpu().double() - g * mask * d).abs().max().item() < 1e-4
 
 
+@pytest.mark.parametrize("act", [K.ACT_RELU, K.ACT_SWISH])
+@pytest.mark.parametrize("M,N,Kk", [(300, 96, 160), (1000, 1024, 256)])
+def test_gemm_aux_derivative_then_multiply(dev, act, M, N, Kk):
+    """FFN path: the w_1 forward epilogue stores h = drop(act(v)) and dh/dv = keep*scale*act'(v)
+    (ACT_AUX_DERIV); the w_2 input-gradient epilogue multiplies by it (ACT_MUL).  Equals the
+    pre-activation path (aux = v, bwd_act = act with the mask regenerated)."""
+    X, W1, b1 = _r(M, Kk, seed=21), _r(N, Kk, seed=22), _r(N, seed=23)
+    dz, W2 = _r(M, Kk, seed=24), _r(Kk, N, seed=25)
+    Xd, W1d, b1d, dzd, W2d = X.to(dev), W1.to(dev), b1.to(dev), dz.to(dev), W2.to(dev)
+    h1, pre = torch.empty(M, N, device=dev), torch.empty(M, N, device=dev)
+    h2, der = torch.empty(M, N, device=dev), torch.empty(M, N, device=dev)
+    K.linear_fwd(Xd, W1d, b1d, h1, act=act, aux=pre, drop_p=0.1, seed=99)
+    K.linear_fwd(Xd, W1d, b1d, h2, act=act | K.ACT_AUX_DERIV, aux=der, drop_p=0.1, seed=99)
+    assert torch.equal(h1, h2)
+    v = pre.cpu().double()
+    keep = (h1.cpu() != 0) | (v <= 0 if act == K.ACT_RELU else torch.zeros_like(v, dtype=torch.bool))
+    d = torch.where(v > 0, 1.0, 0.0) if act == K.ACT_RELU else torch.sigmoid(v) * (1 + v * (1 - torch.sigmoid(v)))
+    ref_der = torch.where(der.cpu() != 0, d / 0.9, 0.0)
+    assert (der.cpu().double() - ref_der).abs().max().item() < 1e-5
+    assert torch.equal((der.cpu() != 0), keep & (d != 0))
+    g1, g2 = torch.empty(M, N, device=dev), torch.empty(M, N, device=dev)
+    K.linear_bwd_data_act(dzd, W2d, g1, pre, act, drop_p=0.1, seed=99)
+    K.linear_bwd_data_act(dzd, W2d, g2, der, K.ACT_MUL)
+    torch.cuda.synchronize()
+    assert torch.equal(g1 == 0, g2 == 0)
+    assert (g1 - g2).abs().max().item() <= 2e-6 * max(1.0, g1.abs().max().item())
+
+
 @pytest.mark.parametrize("M,N,Kk,pad", [(64, 48, 40, 0), (23936 // 8, 256, 64, 0), (5000, 100, 36, 0),
                                         (777, 33, 20, 3)])
 def test_gemm_weight_grad_fused_bias(dev, M, N, Kk, pad):
@@ -443,6 +471,38 @@ def test_specaug_and_mvn_golden(dev):
     xm = torch.from_numpy(g["mvn_x"]).to(dev).contiguous()
     K.utterance_mvn(xm, torch.from_numpy(g["mvn_lens"]).int().to(dev))
     assert np.abs(xm.cpu().numpy() - g["mvn_y"]).max() < 1e-5
+
+
+def test_embed_bwd_many_rows(dev):
+    """Embedding gradient over > 256 token rows (several compaction chunks per vocab row), D not
+    a multiple of 256, repeated and absent tokens: equals index_add in fp64."""
+    nrows, V, D = 1000, 50, 320
+    g = torch.Generator().manual_seed(43)
+    tok = torch.randint(0, V - 5, (nrows,), generator=g)  # the last 5 rows of dE stay untouched
+    dy = _r(nrows, D, seed=44)
+    dE = _r(V, D, seed=45)
+    ref = dE.double().index_add(0, tok, dy.double() * 16.0)
+    out = dE.to(dev)
+    K.embed_bwd(tok.to(dev), dy.to(dev), out, 16.0, 0.0, 0)
+    assert (out.cpu().double() - ref).abs().max().item() < 1e-4
+
+
+def test_specaug_time_warp_unequal_lengths(dev):
+    """Per-utterance branch of TimeWarp.forward (time_warp.py:76-86): each x[b, :len_b] is warped
+    with its own (center, warped), the result zero-padded (pad_list(ys, 0.0)); an utterance too
+    short to warp (center 0) is copied."""
+    B, T, F_ = 3, 200, 16
+    x = _r(B, T, F_, seed=41)
+    lens = [200, 150, 9]
+    warp = [(60, 64), (100, 93), (0, 0)]
+    ref = torch.zeros(B, T, F_)
+    for b, (n, (c, w)) in enumerate(zip(lens, warp)):
+        xb = x[b:b + 1, :n]
+        ref[b, :n] = (O.time_warp_fixed(xb, c, w) if c > 0 else xb)[0]
+    y = torch.empty(B, T, F_, device=dev)
+    K.specaug(x.to(dev), y, torch.tensor(lens, dtype=torch.int32).to(dev),
+              torch.tensor(warp, dtype=torch.int32).to(dev), None, None)
+    assert (y.cpu() - ref).abs().max().item() < 1e-5
 
 
 def test_adam_and_clip(dev):

@@ -29,6 +29,11 @@ def main():
         "dgrad bwd_act": lambda: K.linear_bwd_data_act(dy, W2, out, aux, K.ACT_SWISH),
         "dgrad bwd_act+drop": lambda: K.linear_bwd_data_act(dy, W2, out, aux, K.ACT_SWISH, drop_p=0.1, seed=5),
         "act_bwd kernel+drop": lambda: K.act_bwd(out, aux, out, K.ACT_SWISH, drop_p=0.1, seed=5),
+        "swish+deriv+drop": lambda: K.linear_fwd(x, W, b, out, act=K.ACT_SWISH | K.ACT_AUX_DERIV, aux=aux,
+                                                 drop_p=0.1, seed=5),
+        "dgrad mul": lambda: K.linear_bwd_data_act(dy, W2, out, aux, K.ACT_MUL),
+        "dgrad plain +R": lambda: K.linear_bwd_data(dy, W2, out, accumulate=True),
+        "fwd bias+drop+R": lambda: K.linear_fwd(x, W, b, out, drop_p=0.1, seed=5, alpha=0.5, R=aux, beta=1.0),
     }
     for name, fn in cases.items():
         for _ in range(3):
