@@ -180,10 +180,10 @@ class ESPnetASRModel(AbsESPnetModel):
             state["inv_denom"] = out4[4:5]
         return out4, state
 
-    def _heads_backward(self, state, g_loss):
+    def _heads_backward(self, state, g_loss, hook=None):
         hs2d = state["hs2d"]
         dhs = torch.zeros_like(hs2d) if self.ctc is None else torch.empty_like(hs2d)
-        hook = getattr(self, "_grad_hook", None)
+        hook = hook or getattr(self, "_grad_hook", None)
         if self.ctc is not None:
             g = state["grad_ctc"]
             K.scale_by_dev(g, g_loss)
@@ -271,6 +271,45 @@ class ESPnetASRModel(AbsESPnetModel):
         if not self.training and self.error_calculator is not None:
             stats.update(self._error_rates(encoder_out, prep))
         return loss, stats, d["weight"]
+
+    def forward_explicit(self, speech: torch.Tensor, prep: Prepared):
+        """forward_prepared without autograd nodes, for a caller that runs the backward itself
+        (backward_explicit) on its own thread: the segmented HIP-graph capture of the
+        data-parallel step ends and begins captures inside the module-done hook, which the
+        autograd engine would call from its device thread.  Same kernels, same order."""
+        d = prep.dev
+        with torch.no_grad():
+            if self.frontend is not None:
+                feats = self.frontend.apply_prepared(speech, d["wav_lens"], prep.n_samples)
+            else:
+                feats = speech[:, : prep.T].contiguous().float()
+            if self.specaug is not None and self.training:
+                draws = {k[3:]: v for k, v in d.items() if k.startswith("sa_")}
+                feats = self.specaug.apply_prepared(feats, d["lens"], draws)
+            if self.normalize is not None:
+                feats = self.normalize.apply_prepared(feats, d["lens"])
+            enc = self.encoder
+            hs, _olens, saved = enc.run_forward(feats, prep.sl_cpu, Seeds(prep.enc_seed), enc.training, klen=d["hlens"])
+            out4, state = self._heads_forward(hs, prep, Seeds(prep.heads_seed), True)
+        loss, others = out4[3:4], out4[0:3]
+        stats = dict(
+            loss_ctc=others[0:1] if self.ctc is not None else None,
+            cer_ctc=None,
+            loss_att=others[1:2] if self.decoder is not None else None,
+            acc=others[2:3] if self.decoder is not None else None,
+            cer=None, wer=None,
+            loss=loss,
+        )
+        return loss, stats, d["weight"], (saved, state)
+
+    def backward_explicit(self, ctx, g_loss: torch.Tensor, hook=None):
+        """The backward of forward_explicit for d loss = g_loss (a device scalar): heads, then
+        encoder (HeadsFn.backward + EncoderFn.backward), `hook(module)` at each module done."""
+        saved, state = ctx
+        dhs = self._heads_backward(state, g_loss, hook)
+        K.join_side(dhs.device)
+        self.encoder.run_backward(saved, dhs.contiguous(), hook)
+        K.join_side(dhs.device)
 
     def _error_rates(self, encoder_out, prep) -> Dict[str, Optional[torch.Tensor]]:
         """Eval-mode error rates (espnet_model.py:515-521, 536-539): greedy CTC and decoder

@@ -110,6 +110,43 @@ class FlatGradReducer:
         for h in hs:
             h.wait()
 
+    def launch_sum(self, bucket_ids):
+        """Asynchronous SUM all-reduces of the given buckets (the HIP-graph path, whose replicas
+        pre-scaled their gradients by w_r / sum w); returns the work handles."""
+        if self.flat.grad.is_cuda:
+            K.join_side(self.flat.grad.device)
+        return [dist.all_reduce(self.flat.grad[self.buckets[b][0]:self.buckets[b][1]], op=dist.ReduceOp.SUM,
+                                group=self.group, async_op=True) for b in bucket_ids]
+
+    def plan_hook(self, on_ready):
+        """A module-done hook that launches nothing: it tracks bucket readiness like
+        module_done and calls on_ready(bucket_ids) whenever the in-order launch front advances
+        (used while capturing the backward in segments, one segment per launch point)."""
+        ready = [0] * len(self.buckets)
+        seen = set()
+        front = [0]
+
+        def hook(module):
+            for p in module.parameters():
+                if id(p) in seen or id(p) not in self.param_bucket:
+                    continue
+                seen.add(id(p))
+                ready[self.param_bucket[id(p)]] += 1
+            ids = []
+            while front[0] < len(self.buckets) and ready[front[0]] == self.bucket_count[front[0]]:
+                ids.append(front[0])
+                front[0] += 1
+            if ids:
+                on_ready(ids)
+
+        def rest():
+            ids = list(range(front[0], len(self.buckets)))
+            front[0] = len(self.buckets)
+            return ids
+
+        hook.rest = rest
+        return hook
+
     def broadcast_buffers(self, model):
         """DDP's broadcast_buffers (X7): rank 0's floating buffers (BatchNorm running stats) to
         every replica before the forward, as ONE broadcast of the flat buffer they are views

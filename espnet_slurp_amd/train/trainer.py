@@ -36,8 +36,10 @@ class TrainerOptions:
 
 
 class _GraphEntry:
-    """One captured training step for a batch signature (shapes): static inputs + outputs."""
-    __slots__ = ("graph", "speech", "prep", "stats", "weight")
+    """One captured training step for a batch signature (shapes): static inputs + outputs.
+    Data-parallel entries hold the forward graph and the backward as segments, each followed
+    by the gradient buckets that become complete with it."""
+    __slots__ = ("graph", "speech", "prep", "stats", "weight", "fwd", "segs")
 
 
 class Trainer:
@@ -49,14 +51,17 @@ class Trainer:
         self.options = options or TrainerOptions()
         self.distributed = distributed and dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size() if self.distributed else 1
-        # HIP-graph mode: the whole step (forward, backward, clip, Adam, zero_grad; with DDP the
-        # forward + backward, then the gradient exchange and the update eagerly) is captured once
-        # per batch signature and replayed: ~1500 launches per step cost one graph launch
+        # HIP-graph mode: the whole step (forward, backward, clip, Adam, zero_grad) is captured
+        # once per batch signature and replayed: ~1500 launches per step cost one graph launch.
+        # With DDP the forward and the backward segments are graphs, the collectives between
+        # them eager (_dp_replay)
         self.cuda_graph = bool(cuda_graph) and model.flat.flat.is_cuda
         self._graphs = {}
         self.max_graphs = 32  # LRU bound on captured step graphs (each pins its workspace)
         self._key = None
-        self._acc = None      # DDP + graph + accum_grad > 1: prescaled gradient of earlier micro-batches
+        # DDP + graph: d loss of this replica = w_r / sum_r w / accum_grad, set on device between
+        # the forward and the backward segments (the backward then yields pre-scaled gradients)
+        self._scale = torch.ones(1, dtype=torch.float32, device=model.flat.flat.device)
         self.reducer = (FlatGradReducer(model, model.flat, bucket_mb, hooks=not self.cuda_graph)
                         if self.distributed else None)
         self.iiter = 0          # micro-batches (trainer.py:502 iiter)
@@ -137,22 +142,17 @@ class Trainer:
         e = self._graphs.pop(sig, None)
         if self.distributed:  # DDP broadcast_buffers (X7), outside the graph (a collective)
             self.reducer.broadcast_buffers(model)
-        dp_accum = self.distributed and opts.accum_grad > 1
-        if dp_accum:  # this micro-batch's gradient is computed alone, then prescaled and added
-            if self._acc is None:
-                self._acc = torch.zeros_like(model.flat.grad)
-            self._acc.copy_(model.flat.grad)
-            model.flat.grad.zero_()
         if last:
             self.n_updates += 1
         if e is None:  # the capture call's eager warm-up IS this iteration's step
-            e = self._capture(speech, prep, last)
+            e = self._capture_dp(speech, prep, last) if self.distributed else self._capture(speech, prep, last)
         else:
             e.speech.copy_(speech, non_blocking=True)
             prep.copy_into(e.prep)
-            e.graph.replay()
             if self.distributed:
-                self._dp_tail(e.stats, e.weight, last)
+                self._dp_replay(e, last)
+            else:
+                e.graph.replay()
         self._graphs[sig] = e  # most recently used last
         while len(self._graphs) > self.max_graphs:
             self._graphs.pop(next(iter(self._graphs)))
@@ -174,19 +174,95 @@ class Trainer:
         self.optimizer.step_device(self._clip, self.scheduler)  # counts itself only if finite
         self.model.flat.grad.zero_()
 
-    def _dp_tail(self, stats, weight, last: bool = True):
-        """DDP semantics after a replayed forward+backward (trainer.py:594-608 + DDP average):
-        grad = sum_r (w_r / sum w) grad_r, stats weighted-averaged, then clip + Adam."""
+    # ---------------------------------------------------------------- DDP + HIP graph
+    # DDP semantics (trainer.py:594-608 + DDP's bucketed average, overlapped with backward):
+    #   replay forward graph -> stats all-reduce (recursive_average) and d loss_r = w_r / sum w
+    #   (/ accum_grad) on device -> replay the backward in segments; after each segment the
+    #   gradient buckets it completed are SUM-all-reduced asynchronously while the next segment
+    #   runs -> wait -> clip + Adam.  Pre-scaling by d loss makes the SUM the weighted average,
+    #   and accumulation over micro-batches is plain gradient accumulation (no_sync).
+    def _dp_scale(self, stats, weight):
         avg, wsum = fused_stats_allreduce({k: v for k, v in stats.items() if k != "grad_norm"}, weight)
         for k, v in avg.items():
             stats[k].copy_(v)
-        scale = weight.to(torch.float32).view(1) / wsum
-        K.scale_by_dev(self.model.flat.grad, scale)
-        if self._acc is not None and self.options.accum_grad > 1:
-            K.scale_dropout(self.model.flat.grad, self.model.flat.grad, alpha=1.0, r=self._acc, beta=1.0)
+        torch.div(weight.to(torch.float32).view(1), wsum, out=self._scale)
+        if self.options.accum_grad > 1:
+            self._scale.mul_(1.0 / self.options.accum_grad)
+
+    def _dp_replay(self, e, last: bool):
+        e.fwd.replay()
+        self._dp_scale(e.stats, e.weight)
+        handles = []
+        for g, buckets in e.segs:
+            g.replay()
+            if last and buckets:
+                handles += self.reducer.launch_sum(buckets)
+        for h in handles:
+            h.wait()
         if last:
-            self.reducer.allreduce_sum()
             self._opt_tail()
+
+    def _dp_body(self, speech, prep):
+        K.rng_advance(self._key)
+        loss, stats, weight, ctx = self.model.forward_explicit(speech, prep)
+        stats = {k: v for k, v in stats.items() if v is not None}
+        stats["grad_norm"] = self._clip[0:1]
+        return stats, weight, ctx
+
+    def _capture_dp(self, speech, prep, last: bool):
+        dev = self.model.flat.flat.device
+        if self._key is None:
+            self._key = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).to(dev)
+        e = _GraphEntry()
+        e.speech = speech.to(dev).clone()
+        e.prep = prep.to_device(dev)
+        model = self.model
+        K.set_rng_key(self._key)
+        try:
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):  # warm-up = this iteration's step (allocates workspaces)
+                stats, w, ctx = self._dp_body(e.speech, e.prep)
+                self._dp_scale(stats, w)
+                model.backward_explicit(ctx, self._scale)
+                del ctx
+                if last:
+                    self.reducer.allreduce_sum()
+                    self._opt_tail()
+                warm = {k: v.clone() for k, v in stats.items()}
+            torch.cuda.current_stream(dev).wait_stream(side)
+            torch.cuda.synchronize(dev)
+            pool = torch.cuda.graph_pool_handle()
+            cap = torch.cuda.Stream(device=dev)
+            segs = []
+            cur = [torch.cuda.CUDAGraph()]
+
+            def cut(ids):  # end the running segment where these buckets became complete
+                K.join_side(dev)
+                cur[0].capture_end()
+                segs.append((cur[0], list(ids)))
+                cur[0] = torch.cuda.CUDAGraph()
+                cur[0].capture_begin(pool=pool, capture_error_mode="thread_local")
+
+            hook = self.reducer.plan_hook(cut)
+            with torch.cuda.stream(cap):
+                gf = torch.cuda.CUDAGraph()
+                gf.capture_begin(pool=pool, capture_error_mode="thread_local")
+                e.stats, e.weight, ctx = self._dp_body(e.speech, e.prep)
+                gf.capture_end()
+                cur[0].capture_begin(pool=pool, capture_error_mode="thread_local")
+                model.backward_explicit(ctx, self._scale, hook)
+                del ctx
+                K.join_side(dev)
+                cur[0].capture_end()
+                segs.append((cur[0], hook.rest()))
+            torch.cuda.current_stream(dev).wait_stream(cap)
+            e.fwd, e.segs = gf, segs
+        finally:
+            K.set_rng_key(None)
+        for k, v in warm.items():  # the warm-up step's values are this call's results
+            e.stats[k].copy_(v)
+        return e
 
     def _capture(self, speech, prep, last: bool = True):
         dev = self.model.flat.flat.device
@@ -195,7 +271,7 @@ class Trainer:
         e = _GraphEntry()
         e.speech = speech.to(dev).clone()
         e.prep = prep.to_device(dev)
-        with_opt = last and not self.distributed
+        with_opt = last
         K.set_rng_key(self._key)
         grad_save = None
         try:
@@ -203,8 +279,6 @@ class Trainer:
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):  # warm-up = this iteration's step (allocates workspaces)
                 stats, w = self._device_body(e.speech, e.prep, with_opt)
-                if self.distributed:
-                    self._dp_tail(stats, w, last)
                 if not with_opt:  # the capture below must start from the same gradient state
                     grad_save = self.model.flat.grad.clone()
                     self.model.flat.grad.zero_()

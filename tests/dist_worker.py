@@ -46,8 +46,10 @@ def main():
     model.train()
     opt = FusedAdam(model.parameters(), model.flat, lr=2e-3, weight_decay=1e-6)
     sch = WarmupLR(opt, warmup_steps=10)
+    # small buckets (~20 KB): the model's gradient spans several, so the graph path's backward
+    # is captured in several segments with bucket all-reduces between them
     tr = Trainer(model, opt, sch, TrainerOptions(grad_clip=5.0, accum_grad=accum), distributed=True,
-                 cuda_graph=(mode == "graph"))
+                 cuda_graph=(mode == "graph"), bucket_mb=0.02)
     stats = []
     for step in range(len(GLOBAL)):
         speech, slen, text, tlen = shard(step, rank, world)
@@ -59,7 +61,8 @@ def main():
     torch.save({"params": {n: p.detach().cpu() for n, p in model.named_parameters()},
                 "bufs": {n: b.detach().cpu() for n, b in model.named_buffers()},
                 "stats": stats, "n_steps": opt.n_steps, "n_updates": tr.n_updates,
-                "graphs": len(tr._graphs)}, out)
+                "graphs": len(tr._graphs), "buckets": len(tr.reducer.buckets),
+                "segments": max([len(e.segs) for e in tr._graphs.values()], default=0)}, out)
     dist.barrier()
     dist.destroy_process_group()
 
