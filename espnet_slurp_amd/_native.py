@@ -45,11 +45,11 @@ SIGNATURES = {
     "esp_colsum": [P, I, I, L, P, I, P, P],
     "esp_glu_fwd": [P, P, L, I, P],
     "esp_glu_bwd": [P, P, P, L, I, P],
-    "esp_dwconv1d": [P, P, P, P, I, I, I, I, I, P],
-    "esp_dwconv1d_wgrad": [P, P, P, I, I, I, I, P, P],
-    "esp_bn_swish_fwd": [P, P, P, P, P, P, P, P, F, F, I, I, P, P],
+    "esp_dwconv1d": [P, P, P, P, I, I, I, I, I, P, P],
+    "esp_dwconv1d_wgrad": [P, P, P, I, I, I, I, P, P, P],
+    "esp_bn_swish_fwd": [P, P, P, P, P, P, P, P, F, F, I, I, P, I, P, P],
     "esp_bn_swish_eval": [P, P, P, P, P, P, F, I, I, P, P, P],
-    "esp_bn_swish_bwd": [P, P, P, P, P, P, P, P, P, I, I, P, P, P],
+    "esp_bn_swish_bwd": [P, P, P, P, P, P, P, P, P, I, I, P, P, I, P, P],
     "esp_heads_split": [P, L, I, I, I, I, I, P, P, P],
     "esp_add2d": [P, L, P, L, I, I, P],
     "esp_attn_softmax_fwd": [P, P, I, I, F, P, I, I, P, P, F, U64, I, I, I, L, L, P],
@@ -80,7 +80,7 @@ SIGNATURES = {
 }
 _RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I, "esp_set_gemm_compute": I,
              "esp_get_gemm_compute": I}
-ABI_VERSION = 14  # bumped whenever a signature in include/espnet_mi355.h changes
+ABI_VERSION = 15  # bumped whenever a signature in include/espnet_mi355.h changes
 
 _lib = None
 

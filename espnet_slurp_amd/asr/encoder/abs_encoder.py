@@ -103,8 +103,8 @@ class EncoderFn(torch.autograd.Function):
     flat gradient buffer (flat.py) and returns no input gradient (fbank needs none)."""
 
     @staticmethod
-    def forward(ctx, feats, anchor, enc, ilens_cpu, seed, grad_hook, klen=None):
-        hs, olens, saved = enc.run_forward(feats, ilens_cpu, Seeds(seed), enc.training, klen=klen)
+    def forward(ctx, feats, anchor, enc, ilens_cpu, seed, grad_hook, klen=None, tvalid=None):
+        hs, olens, saved = enc.run_forward(feats, ilens_cpu, Seeds(seed), enc.training, klen=klen, tvalid=tvalid)
         ctx.enc = enc
         ctx.saved = saved
         ctx.grad_hook = grad_hook
@@ -116,4 +116,4 @@ class EncoderFn(torch.autograd.Function):
         ctx.enc.run_backward(ctx.saved, dhs.contiguous(), ctx.grad_hook)
         K.join_side(dhs.device)  # weight gradients on the side stream are complete after this
         ctx.saved = None
-        return None, None, None, None, None, None, None
+        return None, None, None, None, None, None, None, None

@@ -45,7 +45,7 @@ class EncoderLayer(nn.Module):
         self.p = dropout_rate
         self.size = size
 
-    def fwd(self, x, pos, klen, B, T, seeds: Seeds, training: bool):
+    def fwd(self, x, pos, klen, B, T, seeds: Seeds, training: bool, tvalid=None):
         c = Ctx()
         p = self.p
         if self.feed_forward_macaron is not None:
@@ -55,7 +55,7 @@ class EncoderLayer(nn.Module):
         x, c.mha = self.self_attn.fwd(h, x, pos, klen, B, T, p, seeds, training)
         if self.conv_module is not None:
             h, c.ln_conv = self.norm_conv.fwd(x)
-            x, c.conv = self.conv_module.fwd(h, x, B, T, p, seeds, training)
+            x, c.conv = self.conv_module.fwd(h, x, B, T, p, seeds, training, tvalid=tvalid)
         h, c.ln_ff = self.norm_ff.fwd(x)
         x, c.ff = self.feed_forward.fwd(h, x, self.ff_scale, p, seeds, training)
         if self.conv_module is not None:
@@ -167,7 +167,12 @@ class ConformerEncoder(AbsEncoder):
             l.self_attn.flat = flat
 
     # ---------------------------------------------------------------- explicit passes
-    def run_forward(self, feats, ilens_cpu, seeds: Seeds, training: bool, klen=None):
+    def run_forward(self, feats, ilens_cpu, seeds: Seeds, training: bool, klen=None, tvalid=None):
+        """tvalid: optional device int32 (1,) = the reference batch's T' when feats are padded
+        to a length bucket (frames beyond are excluded from the convolution module's depthwise
+        padding and BatchNorm statistics; every other op is per frame or masked by klen)."""
+        if tvalid is not None and self.legacy:
+            raise NotImplementedError("length buckets need the latest rel_pos (legacy rel_shift depends on T')")
         B, T, _ = feats.shape
         if T < 7:
             raise TooShortUttError(
@@ -189,7 +194,7 @@ class ConformerEncoder(AbsEncoder):
             pos = tab
         ctxs = []
         for layer in self.encoders:
-            x, c = layer.fwd(x, pos, klen, B, T2, seeds, training)
+            x, c = layer.fwd(x, pos, klen, B, T2, seeds, training, tvalid=tvalid)
             ctxs.append(c)
         hs, c_after = self.after_norm.fwd(x)
         return hs.view(B, T2, D), olens, Ctx(emb=c_emb, layers=ctxs, after=c_after)
@@ -217,14 +222,15 @@ class ConformerEncoder(AbsEncoder):
         hs = self.forward_prepared(feats, ilens_cpu, lengths_to_device(olens, feats.device), draw_seed())
         return hs, K.h2d(olens, xs_pad.device), None
 
-    def forward_prepared(self, feats: torch.Tensor, ilens_cpu: torch.Tensor, klen: torch.Tensor, seed: int):
+    def forward_prepared(self, feats: torch.Tensor, ilens_cpu: torch.Tensor, klen: torch.Tensor, seed: int,
+                         tvalid: torch.Tensor = None):
         """Encoder output hs (B, T', D) from device-resident inputs only (klen: int32 output
         lengths on device): no host->device traffic, so it can be captured in a HIP graph."""
         anchor = self.after_norm.weight
         hook = getattr(self, "_grad_hook", None)
         if torch.is_grad_enabled() and anchor.requires_grad:
-            return EncoderFn.apply(feats, anchor, self, ilens_cpu, seed, hook, klen)
-        return self.run_forward(feats, ilens_cpu, Seeds(seed), self.training, klen=klen)[0]
+            return EncoderFn.apply(feats, anchor, self, ilens_cpu, seed, hook, klen, tvalid)
+        return self.run_forward(feats, ilens_cpu, Seeds(seed), self.training, klen=klen, tvalid=tvalid)[0]
 
     def output_lengths(self, ilens_cpu: torch.Tensor, T: int) -> torch.Tensor:
         """Valid output frames per utterance (host, no device round trip)."""

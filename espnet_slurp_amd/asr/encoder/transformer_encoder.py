@@ -70,7 +70,8 @@ class TransformerEncoder(AbsEncoder):
         for l in self.encoders:
             l.self_attn.flat = flat
 
-    def run_forward(self, feats, ilens_cpu, seeds: Seeds, training: bool, klen=None):
+    def run_forward(self, feats, ilens_cpu, seeds: Seeds, training: bool, klen=None, tvalid=None):
+        # tvalid (length buckets) needs no handling here: every op is per frame or masked by klen
         B, T, _ = feats.shape
         if T < 7:
             raise TooShortUttError(f"has {T} frames and is too short for subsampling", T, 7)
@@ -124,14 +125,15 @@ class TransformerEncoder(AbsEncoder):
         hs = self.forward_prepared(feats, ilens_cpu, lengths_to_device(olens, feats.device), draw_seed())
         return hs, K.h2d(olens, xs_pad.device), None
 
-    def forward_prepared(self, feats: torch.Tensor, ilens_cpu: torch.Tensor, klen: torch.Tensor, seed: int):
+    def forward_prepared(self, feats: torch.Tensor, ilens_cpu: torch.Tensor, klen: torch.Tensor, seed: int,
+                         tvalid: torch.Tensor = None):
         """Encoder output hs (B, T', D) from device-resident inputs only (klen: int32 output
         lengths on device): no host->device traffic, so it can be captured in a HIP graph."""
         anchor = self.after_norm.weight
         hook = getattr(self, "_grad_hook", None)
         if torch.is_grad_enabled() and anchor.requires_grad:
-            return EncoderFn.apply(feats, anchor, self, ilens_cpu, seed, hook, klen)
-        return self.run_forward(feats, ilens_cpu, Seeds(seed), self.training, klen=klen)[0]
+            return EncoderFn.apply(feats, anchor, self, ilens_cpu, seed, hook, klen, tvalid)
+        return self.run_forward(feats, ilens_cpu, Seeds(seed), self.training, klen=klen, tvalid=tvalid)[0]
 
     def output_lengths(self, ilens_cpu: torch.Tensor, T: int) -> torch.Tensor:
         """Valid output frames per utterance (host, no device round trip)."""

@@ -200,10 +200,18 @@ class ESPnetASRModel(AbsESPnetModel):
 
     # ------------------------------------------------------------------ forward
     def prepare(self, speech_lengths: torch.Tensor, text: torch.Tensor, text_lengths: torch.Tensor, T_in: int,
-                F_in: int, specaug_draws: Optional[dict] = None) -> Prepared:
+                F_in: int, specaug_draws: Optional[dict] = None, t_bucket: Optional[int] = None,
+                u_bucket: Optional[int] = None) -> Prepared:
         """All host-side work of a step (espnet_model.py:169-297 before any kernel): lengths,
         the target slice, add_sos_eos, SpecAug draws (CPU generator, as time_warp.py), the
-        dropout seeds.  Returns host tensors; `.to_device()` moves them (pinned, async)."""
+        dropout seeds.  Returns host tensors; `.to_device()` moves them (pinned, async).
+
+        t_bucket / u_bucket (HIP-graph trainer, length buckets): pad the frame axis to t_bucket
+        frames and the target axis to u_bucket tokens (ys padded with ignore_id, ys_in with eos,
+        ys_out with ignore_id: one decoder row more per token of padding, all ignored).  Every
+        length-derived quantity (SpecAug draws, encoder lengths, the valid frame count
+        `tvalid` the convolution module bounds itself with) is still taken from this batch's
+        own padded length, so the step computes what the reference computes on it."""
         assert text_lengths.dim() == 1, text_lengths.shape
         B = int(speech_lengths.shape[0])
         text = text.detach().cpu().clone()
@@ -227,7 +235,18 @@ class ESPnetASRModel(AbsESPnetModel):
             for k, v in draws.items():
                 host["sa_" + k] = v.to(torch.int32)
         host["hlens"] = self.encoder.output_lengths(sl_cpu, T).to(torch.int32)
-        prep = Prepared(B=B, T=T, Umax=int(text_cpu.shape[1]), denom=float(B), L=0, host=host,
+        T_true = T
+        if t_bucket is not None:
+            if self.frontend is not None:
+                raise NotImplementedError("length buckets: feature input only (frontend: null)")
+            assert t_bucket >= T, (t_bucket, T)
+            T = int(t_bucket)
+            # valid frames after Conv2dSubsampling of the batch's own padded length
+            host["tvalid"] = torch.tensor([((T_true - 1) // 2 - 1) // 2], dtype=torch.int32)
+        if u_bucket is not None and u_bucket > text_cpu.shape[1]:
+            pad = torch.full((B, int(u_bucket) - text_cpu.shape[1]), self.ignore_id, dtype=text_cpu.dtype)
+            text_cpu = torch.cat([text_cpu, pad], 1)
+        prep = Prepared(B=B, T=T, T_true=T_true, Umax=int(text_cpu.shape[1]), denom=float(B), L=0, host=host,
                         enc_seed=draw_seed(), heads_seed=draw_seed(), sl_cpu=sl_cpu, n_samples=n_samples,
                         ys_pad_cpu=text_cpu)
         if self.ctc is not None:
@@ -235,6 +254,10 @@ class ESPnetASRModel(AbsESPnetModel):
             host["tlens"] = tl_cpu.to(torch.int32)
         if self.decoder is not None:
             ys_in, ys_out, ys_in_lens = add_sos_eos(text_cpu, tl_cpu, self.sos, self.eos, self.ignore_id)
+            if u_bucket is not None and ys_in.shape[1] < int(u_bucket) + 1:
+                extra = int(u_bucket) + 1 - ys_in.shape[1]
+                ys_in = torch.cat([ys_in, torch.full((B, extra), self.eos, dtype=ys_in.dtype)], 1)
+                ys_out = torch.cat([ys_out, torch.full((B, extra), self.ignore_id, dtype=ys_out.dtype)], 1)
             prep["L"] = int(ys_in.shape[1])
             host["ys_in"], host["ys_out"] = ys_in, ys_out
             host["ys_in_lens"] = ys_in_lens.to(torch.int32)
@@ -253,7 +276,7 @@ class ESPnetASRModel(AbsESPnetModel):
             feats = self.specaug.apply_prepared(feats, d["lens"], draws)
         if self.normalize is not None:
             feats = self.normalize.apply_prepared(feats, d["lens"])
-        encoder_out = self.encoder.forward_prepared(feats, prep.sl_cpu, d["hlens"], prep.enc_seed)
+        encoder_out = self.encoder.forward_prepared(feats, prep.sl_cpu, d["hlens"], prep.enc_seed, d.get("tvalid"))
         anchor = next(p for p in (self.ctc or self.decoder).parameters())
         if torch.is_grad_enabled() and anchor.requires_grad:
             loss, others = HeadsFn.apply(encoder_out, anchor, self, prep, prep.heads_seed)
@@ -289,7 +312,8 @@ class ESPnetASRModel(AbsESPnetModel):
             if self.normalize is not None:
                 feats = self.normalize.apply_prepared(feats, d["lens"])
             enc = self.encoder
-            hs, _olens, saved = enc.run_forward(feats, prep.sl_cpu, Seeds(prep.enc_seed), enc.training, klen=d["hlens"])
+            hs, _olens, saved = enc.run_forward(feats, prep.sl_cpu, Seeds(prep.enc_seed), enc.training, klen=d["hlens"],
+                                                tvalid=d.get("tvalid"))
             out4, state = self._heads_forward(hs, prep, Seeds(prep.heads_seed), True)
         loss, others = out4[3:4], out4[0:3]
         stats = dict(

@@ -448,7 +448,8 @@ class ConvolutionModule(nn.Module):
         self.pointwise_conv2 = nn.Conv1d(channels, channels, 1)
         self.kernel_size = kernel_size
 
-    def fwd(self, x2d, resid, B, T, p_res, seeds: Seeds, training: bool):
+    def fwd(self, x2d, resid, B, T, p_res, seeds: Seeds, training: bool, tvalid=None):
+        """tvalid: see ConformerEncoder.run_forward (length-bucketed batch)."""
         M, D = x2d.shape
         w1 = self.pointwise_conv1.weight.view(2 * D, D)
         u = empty(M, 2 * D, like=x2d)
@@ -456,14 +457,14 @@ class ConvolutionModule(nn.Module):
         g = empty(M, D, like=x2d)
         K.glu_fwd(u, g)
         y = empty(M, D, like=x2d)
-        K.dwconv1d(g, self.depthwise_conv.weight, self.depthwise_conv.bias, y, B, T, D, self.kernel_size)
+        K.dwconv1d(g, self.depthwise_conv.weight, self.depthwise_conv.bias, y, B, T, D, self.kernel_size, tvalid=tvalid)
         s = empty(M, D, like=x2d)
         mean = empty(D, like=x2d)
         rstd = empty(D, like=x2d)
         bn = self.norm
         if training:
             K.bn_swish_fwd(y, bn.weight, bn.bias, s, mean, rstd, bn.running_mean, bn.running_var,
-                           momentum=bn.momentum, eps=bn.eps)
+                           momentum=bn.momentum, eps=bn.eps, T=T, tvalid=tvalid)
             bn.num_batches_tracked.add_(1)
         else:  # inference: running statistics (no backward is taken in eval mode)
             K.bn_swish_eval(y, bn.weight, bn.bias, s, bn.running_mean, bn.running_var, mean, rstd, eps=bn.eps)
@@ -472,7 +473,7 @@ class ConvolutionModule(nn.Module):
         so = seeds.next()
         K.linear_fwd(s, self.pointwise_conv2.weight.view(D, D), self.pointwise_conv2.bias, out, drop_p=pr, seed=so,
                      R=resid, beta=1.0)
-        return out, Ctx(x=x2d, u=u, g=g, y=y, s=s, mean=mean, rstd=rstd, pr=pr, so=so, B=B, T=T)
+        return out, Ctx(x=x2d, u=u, g=g, y=y, s=s, mean=mean, rstd=rstd, pr=pr, so=so, B=B, T=T, tvalid=tvalid)
 
     def bwd(self, c, dout):
         M, D = dout.shape
@@ -485,12 +486,13 @@ class ConvolutionModule(nn.Module):
         dy = empty(M, D, like=dout)
         sums = empty(2 * D, like=dout)
         bn = self.norm
-        K.bn_swish_bwd(ds, c.y, c.mean, c.rstd, bn.weight, bn.bias, dy, bn.weight.grad, bn.bias.grad, sums)
+        K.bn_swish_bwd(ds, c.y, c.mean, c.rstd, bn.weight, bn.bias, dy, bn.weight.grad, bn.bias.grad, sums,
+                       T=c.T, tvalid=c.tvalid)
         dw = self.depthwise_conv
-        K.colsum(dy, dw.bias.grad, accumulate=True)
-        K.dwconv1d_wgrad(dy, c.g, dw.weight.grad, c.B, c.T, D, self.kernel_size)
+        K.colsum(dy, dw.bias.grad, accumulate=True)  # rows beyond tvalid hold 0
+        K.dwconv1d_wgrad(dy, c.g, dw.weight.grad, c.B, c.T, D, self.kernel_size, tvalid=c.tvalid)
         dg = ds  # reuse
-        K.dwconv1d(dy, dw.weight, None, dg, c.B, c.T, D, self.kernel_size, flip=True)
+        K.dwconv1d(dy, dw.weight, None, dg, c.B, c.T, D, self.kernel_size, flip=True, tvalid=c.tvalid)
         du = empty(M, 2 * D, like=dout)
         K.glu_bwd(c.u, dg, du)
         w1 = self.pointwise_conv1.weight

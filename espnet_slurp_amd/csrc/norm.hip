@@ -261,6 +261,13 @@ __global__ void glu_bwd_kernel(const float* __restrict__ u, const float* __restr
   }
 }
 
+// Valid-frame bound of a length-bucketed batch (HIP-graph trainer): a batch padded to T frames
+// per utterance whose true padded length is *tvalid < T.  The frames t >= *tvalid do not exist
+// in the reference batch: the depthwise convolution reads them as its zero padding and writes
+// 0 there, BatchNorm statistics and gradients exclude them (their gradient is 0).  NULL: all
+// T frames are real.
+__device__ __forceinline__ int valid_T(const int* tvalid, int T) { return tvalid ? min(T, *tvalid) : T; }
+
 // y[b,t,c] = bias[c] + sum_k W[c,k] * x[b, t + k - pad, c]   (flip=0, forward)
 // y[b,t,c] = sum_k W[c,k] * x[b, t - k + pad, c]             (flip=1, input grad)
 // Block = 64 channels x DW_TT time steps; the input window (DW_TT + K - 1 rows) and the
@@ -268,8 +275,9 @@ __global__ void glu_bwd_kernel(const float* __restrict__ u, const float* __restr
 constexpr int DW_TT = 32, DW_KMAX = 64;
 __global__ __launch_bounds__(256) void dwconv_kernel(const float* __restrict__ x, const float* __restrict__ W,
                                                      const float* __restrict__ bias, float* __restrict__ y, int Bn,
-                                                     int T, int D, int K, int flip) {
+                                                     int T, int D, int K, int flip, const int* __restrict__ tvalid) {
   __shared__ float xs[DW_TT + DW_KMAX][64];
+  const int Tv = valid_T(tvalid, T);
   __shared__ float ws[64][DW_KMAX + 1];
   const int c0 = blockIdx.x * 64, t0 = blockIdx.y * DW_TT, b = blockIdx.z;
   const int pad = (K - 1) / 2;
@@ -279,7 +287,7 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const float* __restrict__ x
   const int rows = DW_TT + K - 1;
   for (int r = tg; r < rows; r += 4) {
     const int t = t0 - pad + r;
-    xs[r][cl] = (c < D && t >= 0 && t < T) ? xb[(long)t * D + c] : 0.f;
+    xs[r][cl] = (c < D && t >= 0 && t < Tv) ? xb[(long)t * D + c] : 0.f;
   }
   for (int e = threadIdx.x; e < 64 * K; e += 256) {
     const int cc = e / K, k = e - cc * K;
@@ -301,7 +309,7 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const float* __restrict__ x
 #pragma unroll
   for (int j = 0; j < PT; ++j) {
     const int t = t0 + base + j;
-    if (t < T) y[((long)b * T + t) * D + c] = acc[j];
+    if (t < T) y[((long)b * T + t) * D + c] = t < Tv ? acc[j] : 0.f;
   }
 }
 
@@ -309,8 +317,10 @@ __global__ __launch_bounds__(256) void dwconv_kernel(const float* __restrict__ x
 // Block = 64 channels; 4 tap groups (k = kg, kg+4, ...); dy and x windows in LDS.
 constexpr int DWW_TCH = 64;
 __global__ __launch_bounds__(256) void dwconv_wgrad_kernel(const float* __restrict__ dy, const float* __restrict__ x,
-                                                           float* __restrict__ part, int T, int D, int K) {
+                                                           float* __restrict__ part, int T, int D, int K,
+                                                           const int* __restrict__ tvalid) {
   __shared__ float xs[DWW_TCH + DW_KMAX][64];
+  const int Tv = valid_T(tvalid, T);
   __shared__ float gs[DWW_TCH][64];
   const int c0 = blockIdx.x * 64, ch = blockIdx.y, b = blockIdx.z, nch = gridDim.y;
   const int t0 = ch * DWW_TCH;
@@ -321,11 +331,11 @@ __global__ __launch_bounds__(256) void dwconv_wgrad_kernel(const float* __restri
   const float* db = dy + (long)b * T * D;
   for (int r = kg; r < DWW_TCH + K - 1; r += 4) {
     const int t = t0 - pad + r;
-    xs[r][cl] = (c < D && t >= 0 && t < T) ? xb[(long)t * D + c] : 0.f;
+    xs[r][cl] = (c < D && t >= 0 && t < Tv) ? xb[(long)t * D + c] : 0.f;
   }
   for (int r = kg; r < DWW_TCH; r += 4) {
     const int t = t0 + r;
-    gs[r][cl] = (c < D && t < T) ? db[(long)t * D + c] : 0.f;
+    gs[r][cl] = (c < D && t < Tv) ? db[(long)t * D + c] : 0.f;
   }
   __syncthreads();
   if (c >= D) return;
@@ -381,8 +391,9 @@ __device__ __forceinline__ void dw_stage(float (*xs)[64], const float* __restric
 template <int KT>
 __global__ __launch_bounds__(256) void dwconv_rb_kernel(const float* __restrict__ x, const float* __restrict__ W,
                                                         const float* __restrict__ bias, float* __restrict__ y, int T,
-                                                        int D, int flip) {
+                                                        int D, int flip, const int* __restrict__ tvalid) {
   __shared__ __attribute__((aligned(16))) float xs[DWR_TT + KT - 1][64];
+  const int Tv = valid_T(tvalid, T);
   __shared__ float ws[KT][64];
   constexpr int pad = (KT - 1) / 2;
   const int c0 = blockIdx.x * 64, t0 = blockIdx.y * DWR_TT, b = blockIdx.z;
@@ -395,7 +406,7 @@ __global__ __launch_bounds__(256) void dwconv_rb_kernel(const float* __restrict_
     const int cc = i / KT, kk = i - cc * KT;
     ws[flip ? (KT - 1 - kk) : kk][cc] = W[(long)c0 * KT + i];
   }
-  dw_stage<KT>(xs, xb, t0 - pad, T, D, c0);
+  dw_stage<KT>(xs, xb, t0 - pad, Tv, D, c0);
   __syncthreads();
   if (c >= D) return;
   float w[KT];
@@ -411,7 +422,7 @@ __global__ __launch_bounds__(256) void dwconv_rb_kernel(const float* __restrict_
 #pragma unroll
     for (int k = 0; k < KT; ++k) a += w[k] * win[j + k];
     const int t = t0 + tg * DWR_PT + j;
-    if (t < T) y[((long)b * T + t) * D + c] = a;
+    if (t < T) y[((long)b * T + t) * D + c] = t < Tv ? a : 0.f;
   }
 }
 
@@ -420,9 +431,11 @@ __global__ __launch_bounds__(256) void dwconv_rb_kernel(const float* __restrict_
 template <int KT>
 __global__ __launch_bounds__(256) void dwconv_wgrad_rb_kernel(const float* __restrict__ dy,
                                                               const float* __restrict__ x,
-                                                              float* __restrict__ part, int T, int D) {
+                                                              float* __restrict__ part, int T, int D,
+                                                              const int* __restrict__ tvalid) {
   __shared__ __attribute__((aligned(16))) float xs[DWR_TT + KT - 1][64];
   __shared__ float red[3][KT][64];
+  const int Tv = valid_T(tvalid, T);
   constexpr int pad = (KT - 1) / 2;
   const int c0 = blockIdx.x * 64, ch = blockIdx.y, b = blockIdx.z, nch = gridDim.y;
   const int t0 = ch * DWR_TT;
@@ -430,12 +443,12 @@ __global__ __launch_bounds__(256) void dwconv_wgrad_rb_kernel(const float* __res
   const int c = c0 + cl;
   const float* xb = x + (long)b * T * D;
   const float* db = dy + (long)b * T * D;
-  dw_stage<KT>(xs, xb, t0 - pad, T, D, c0);
+  dw_stage<KT>(xs, xb, t0 - pad, Tv, D, c0);
   float g[DWR_PT];
 #pragma unroll
   for (int j = 0; j < DWR_PT; ++j) {
     const int t = t0 + tg * DWR_PT + j;
-    g[j] = (c < D && t < T) ? db[(long)t * D + c] : 0.f;
+    g[j] = (c < D && t < Tv) ? db[(long)t * D + c] : 0.f;
   }
   __syncthreads();
   float win[DWR_PT + KT - 1];
@@ -463,14 +476,19 @@ __global__ __launch_bounds__(256) void dwconv_wgrad_rb_kernel(const float* __res
 
 // BatchNorm statistics, stage 1: per row-chunk partial sums (double) of x and, given a
 // mean, of (x-mean)^2.  mode 0: sum x ; mode 1: sum (x-mean)^2
+// (rows r = b*T + t; with tvalid only t < *tvalid count)
 __global__ void bn_part_kernel(const float* __restrict__ x, int M, int D, int rows_per_block,
-                               const float* __restrict__ mean, int mode, double* __restrict__ part) {
+                               const float* __restrict__ mean, int mode, double* __restrict__ part, int T,
+                               const int* __restrict__ tvalid) {
   const int c = blockIdx.y * blockDim.x + threadIdx.x;
   if (c >= D) return;
+  const int Tv = valid_T(tvalid, T);
   const int r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
   double s = 0.0;
   const float mu = mode ? mean[c] : 0.f;
-  for (int r = r0; r < r1; ++r) {
+  int t = r0 % T;
+  for (int r = r0; r < r1; ++r, t = (t + 1 == T ? 0 : t + 1)) {
+    if (t >= Tv) continue;
     const float v = x[(long)r * D + c];
     if (mode) {
       const double d = (double)v - (double)mu;
@@ -500,8 +518,10 @@ __device__ __forceinline__ double sum_parts16(const double* __restrict__ part, i
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(const double* __restrict__ part, int nb, int D, int M, int mode,
                                                            float* __restrict__ mean, float* __restrict__ rstd,
                                                            float* __restrict__ run_mean, float* __restrict__ run_var,
-                                                           float momentum, float eps) {
+                                                           float momentum, float eps, int T,
+                                                           const int* __restrict__ tvalid) {
   __shared__ double sh[16][64];
+  if (tvalid) M = (M / T) * valid_T(tvalid, T);  // B * T' rows of the reference batch
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const double s = sum_parts16(part, nb, D, c, c < D, sh);
   if ((threadIdx.x >> 6) != 0 || c >= D) return;
@@ -534,14 +554,20 @@ __global__ void bn_swish_bwd_part_kernel(const float* __restrict__ ds, const flo
                                          const float* __restrict__ mean, const float* __restrict__ rstd,
                                          const float* __restrict__ gamma, const float* __restrict__ beta,
                                          float* __restrict__ dz, int M, int D, int rows_per_block,
-                                         double* __restrict__ part) {
+                                         double* __restrict__ part, int T, const int* __restrict__ tvalid) {
   const int c = blockIdx.y * blockDim.x + threadIdx.x;
   if (c >= D) return;
+  const int Tv = valid_T(tvalid, T);
   const int r0 = blockIdx.x * rows_per_block, r1 = min(M, r0 + rows_per_block);
   const float mu = mean[c], rs = rstd[c], ga = gamma[c], be = beta[c];
   double s1 = 0.0, s2 = 0.0;
-  for (int r = r0; r < r1; ++r) {
+  int t = r0 % T;
+  for (int r = r0; r < r1; ++r, t = (t + 1 == T ? 0 : t + 1)) {
     const long i = (long)r * D + c;
+    if (t >= Tv) {  // not a frame of the reference batch: zero gradient, not in the sums
+      dz[i] = 0.f;
+      continue;
+    }
     const float xh = (y[i] - mu) * rs;
     const float z = xh * ga + be;
     const float sg = 1.0f / (1.0f + expf(-z));
@@ -572,9 +598,13 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const double* __r
 // dy = gamma*rstd*(dz - S1/M - xhat*S2/M)   (in place over dz)
 __global__ void bn_bwd_apply_kernel(float* __restrict__ dz, const float* __restrict__ y, const float* __restrict__ mean,
                                     const float* __restrict__ rstd, const float* __restrict__ gamma,
-                                    const float* __restrict__ sums, long n, int D, int M) {
+                                    const float* __restrict__ sums, long n, int D, int M, int T,
+                                    const int* __restrict__ tvalid) {
+  const int Tv = valid_T(tvalid, T);
+  if (tvalid) M = (M / T) * Tv;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const int c = (int)(i % D);
+    if (tvalid && (int)((i / D) % T) >= Tv) continue;  // stays 0 (bn_swish_bwd_part_kernel)
     const float xh = (y[i] - mean[c]) * rstd[c];
     dz[i] = gamma[c] * rstd[c] * (dz[i] - sums[c] / M - xh * sums[D + c] / M);
   }
@@ -657,39 +687,42 @@ ESP_API int esp_glu_bwd(const float* u, const float* dg, float* du, long rows, i
 
 // flip=0: y = dwconv(x) + bias ; flip=1: input-gradient (bias ignored)
 ESP_API int esp_dwconv1d(const float* x, const float* W, const float* bias, float* y, int Bn, int T, int D, int K,
-                         int flip, void* stream) {
+                         int flip, const int* tvalid, void* stream) {
   ESP_ARG_CHECK(K % 2 == 1 && K <= 64, "esp_dwconv1d: K must be odd and <= 64");
   if (K == 31 || K == 15) {
     dim3 g2((D + 63) / 64, (T + DWR_TT - 1) / DWR_TT, Bn);
     if (K == 31)
       hipLaunchKernelGGL(dwconv_rb_kernel<31>, g2, dim3(256), 0, (hipStream_t)stream, x, W, flip ? nullptr : bias, y, T,
-                         D, flip);
+                         D, flip, tvalid);
     else
       hipLaunchKernelGGL(dwconv_rb_kernel<15>, g2, dim3(256), 0, (hipStream_t)stream, x, W, flip ? nullptr : bias, y, T,
-                         D, flip);
+                         D, flip, tvalid);
     ESP_CHECK_LAUNCH("esp_dwconv1d");
     return 0;
   }
   dim3 grid((D + 63) / 64, (T + DW_TT - 1) / DW_TT, Bn);
   hipLaunchKernelGGL(dwconv_kernel, grid, dim3(256), 0, (hipStream_t)stream, x, W, flip ? nullptr : bias, y, Bn, T, D, K,
-                     flip);
+                     flip, tvalid);
   ESP_CHECK_LAUNCH("esp_dwconv1d");
   return 0;
 }
 
 // dW[c,k] += sum_{b,t} dy[b,t,c]*x[b,t+k-pad,c].  workspace >= Bn*ceil(T/64)*D*K floats
 ESP_API int esp_dwconv1d_wgrad(const float* dy, const float* x, float* dW, int Bn, int T, int D, int K, float* work,
-                               void* stream) {
+                               const int* tvalid, void* stream) {
   ESP_ARG_CHECK(K % 2 == 1 && K <= 64, "esp_dwconv1d_wgrad: K must be odd and <= 64");
   const bool rb = K == 31 || K == 15;
   const int nch = rb ? (T + DWR_TT - 1) / DWR_TT : (T + DWW_TCH - 1) / DWW_TCH;
   hipStream_t st = (hipStream_t)stream;
   if (K == 31)
-    hipLaunchKernelGGL(dwconv_wgrad_rb_kernel<31>, dim3((D + 63) / 64, nch, Bn), dim3(256), 0, st, dy, x, work, T, D);
+    hipLaunchKernelGGL(dwconv_wgrad_rb_kernel<31>, dim3((D + 63) / 64, nch, Bn), dim3(256), 0, st, dy, x, work, T, D,
+                       tvalid);
   else if (K == 15)
-    hipLaunchKernelGGL(dwconv_wgrad_rb_kernel<15>, dim3((D + 63) / 64, nch, Bn), dim3(256), 0, st, dy, x, work, T, D);
+    hipLaunchKernelGGL(dwconv_wgrad_rb_kernel<15>, dim3((D + 63) / 64, nch, Bn), dim3(256), 0, st, dy, x, work, T, D,
+                       tvalid);
   else
-    hipLaunchKernelGGL(dwconv_wgrad_kernel, dim3((D + 63) / 64, nch, Bn), dim3(256), 0, st, dy, x, work, T, D, K);
+    hipLaunchKernelGGL(dwconv_wgrad_kernel, dim3((D + 63) / 64, nch, Bn), dim3(256), 0, st, dy, x, work, T, D, K,
+                       tvalid);
   hipLaunchKernelGGL(finalize_cols_kernel<float>, fin_grid(D * K), dim3(1024), 0, st, work, Bn * nch, (long)D * K,
                      D * K, dW, 1);
   ESP_CHECK_LAUNCH("esp_dwconv1d_wgrad");
@@ -700,16 +733,18 @@ ESP_API int esp_dwconv1d_wgrad(const float* dy, const float* x, float* dW, int B
 // run_mean != NULL.  workspace: >= D*ceil(M/64) doubles
 ESP_API int esp_bn_swish_fwd(const float* y, const float* gamma, const float* beta, float* s, float* mean, float* rstd,
                              float* run_mean, float* run_var, float momentum, float eps, int M, int D, double* work,
-                             void* stream) {
+                             int T, const int* tvalid, void* stream) {
+  ESP_ARG_CHECK(!tvalid || (T > 0 && M % T == 0), "esp_bn_swish_fwd: M must be a multiple of T with tvalid");
+  if (!tvalid) T = M > 0 ? M : 1;
   const int rpb = rows_per_block(M), nb = nchunks(M, rpb);
   hipStream_t st = (hipStream_t)stream;
   dim3 g1(nb, (D + 255) / 256), gf((D + 255) / 256);
-  hipLaunchKernelGGL(bn_part_kernel, g1, dim3(256), 0, st, y, M, D, rpb, nullptr, 0, work);
+  hipLaunchKernelGGL(bn_part_kernel, g1, dim3(256), 0, st, y, M, D, rpb, nullptr, 0, work, T, tvalid);
   hipLaunchKernelGGL(bn_finalize_kernel, fin_grid(D), dim3(1024), 0, st, work, nb, D, M, 0, mean, rstd, nullptr,
-                     nullptr, momentum, eps);
-  hipLaunchKernelGGL(bn_part_kernel, g1, dim3(256), 0, st, y, M, D, rpb, mean, 1, work);
+                     nullptr, momentum, eps, T, tvalid);
+  hipLaunchKernelGGL(bn_part_kernel, g1, dim3(256), 0, st, y, M, D, rpb, mean, 1, work, T, tvalid);
   hipLaunchKernelGGL(bn_finalize_kernel, fin_grid(D), dim3(1024), 0, st, work, nb, D, M, 1, mean, rstd, run_mean,
-                     run_var, momentum, eps);
+                     run_var, momentum, eps, T, tvalid);
   hipLaunchKernelGGL(bn_swish_fwd_kernel, dim3(gridn((long)M * D)), dim3(256), 0, st, y, mean, rstd, gamma, beta, s,
                      (long)M * D, D);
   ESP_CHECK_LAUNCH("esp_bn_swish_fwd");
@@ -742,14 +777,16 @@ ESP_API int esp_bn_swish_eval(const float* y, const float* gamma, const float* b
 // workspace: >= 2*D*ceil(M/64) doubles + 2*D floats (sums) passed separately
 ESP_API int esp_bn_swish_bwd(const float* ds, const float* y, const float* mean, const float* rstd, const float* gamma,
                              const float* beta, float* dy, float* dgamma, float* dbeta, int M, int D, double* work,
-                             float* sums, void* stream) {
+                             float* sums, int T, const int* tvalid, void* stream) {
+  ESP_ARG_CHECK(!tvalid || (T > 0 && M % T == 0), "esp_bn_swish_bwd: M must be a multiple of T with tvalid");
+  if (!tvalid) T = M > 0 ? M : 1;
   const int rpb = rows_per_block(M), nb = nchunks(M, rpb);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(bn_swish_bwd_part_kernel, dim3(nb, (D + 255) / 256), dim3(256), 0, st, ds, y, mean, rstd, gamma,
-                     beta, dy, M, D, rpb, work);
+                     beta, dy, M, D, rpb, work, T, tvalid);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, fin_grid(D), dim3(1024), 0, st, work, nb, D, sums, dgamma, dbeta);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(gridn((long)M * D)), dim3(256), 0, st, dy, y, mean, rstd, gamma, sums,
-                     (long)M * D, D, M);
+                     (long)M * D, D, M, T, tvalid);
   ESP_CHECK_LAUNCH("esp_bn_swish_bwd");
   return 0;
 }

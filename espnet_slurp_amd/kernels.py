@@ -350,22 +350,24 @@ def glu_bwd(u, dg, du):
     _native.call("esp_glu_bwd", _p(u), _p(dg), _p(du), rows, D, _st())
 
 
-def dwconv1d(x, W, bias, y, Bn, T, D, K, flip=False):
-    _native.call("esp_dwconv1d", _p(x), _p(W), _p(bias), _p(y), Bn, T, D, K, int(flip), _st())
+# tvalid: optional device int32 (1,) — the batch is padded to T frames per utterance, only the
+# first tvalid[0] are frames of the reference batch (length-bucketed graphs, norm.hip valid_T)
+def dwconv1d(x, W, bias, y, Bn, T, D, K, flip=False, tvalid=None):
+    _native.call("esp_dwconv1d", _p(x), _p(W), _p(bias), _p(y), Bn, T, D, K, int(flip), _p(tvalid), _st())
 
 
-def dwconv1d_wgrad(dy, x, dW, Bn, T, D, K):
+def dwconv1d_wgrad(dy, x, dW, Bn, T, D, K, tvalid=None):
     nch = (T + 63) // 64
     ws = _work(4 * Bn * nch * D * K, x.device)
-    _native.call("esp_dwconv1d_wgrad", _p(dy), _p(x), _p(dW), Bn, T, D, K, _p(ws), _st())
+    _native.call("esp_dwconv1d_wgrad", _p(dy), _p(x), _p(dW), Bn, T, D, K, _p(ws), _p(tvalid), _st())
 
 
-def bn_swish_fwd(y, gamma, beta, s, mean, rstd, run_mean, run_var, momentum=0.1, eps=1e-5):
+def bn_swish_fwd(y, gamma, beta, s, mean, rstd, run_mean, run_var, momentum=0.1, eps=1e-5, T=0, tvalid=None):
     M, D = y.shape
     nb = (M + 63) // 64
     ws = _work(8 * D * max(nb, 1), y.device)
     _native.call("esp_bn_swish_fwd", _p(y), _p(gamma), _p(beta), _p(s), _p(mean), _p(rstd), _p(run_mean),
-                 _p(run_var), float(momentum), float(eps), M, D, _p(ws), _st())
+                 _p(run_var), float(momentum), float(eps), M, D, _p(ws), int(T), _p(tvalid), _st())
 
 
 def bn_swish_eval(y, gamma, beta, s, run_mean, run_var, mean, rstd, eps=1e-5):
@@ -375,12 +377,12 @@ def bn_swish_eval(y, gamma, beta, s, run_mean, run_var, mean, rstd, eps=1e-5):
                  _p(mean), _p(rstd), _st())
 
 
-def bn_swish_bwd(ds, y, mean, rstd, gamma, beta, dy, dgamma, dbeta, sums):
+def bn_swish_bwd(ds, y, mean, rstd, gamma, beta, dy, dgamma, dbeta, sums, T=0, tvalid=None):
     M, D = y.shape
     nb = (M + 63) // 64
     ws = _work(8 * 2 * D * max(nb, 1), y.device)
     _native.call("esp_bn_swish_bwd", _p(ds), _p(y), _p(mean), _p(rstd), _p(gamma), _p(beta), _p(dy), _p(dgamma),
-                 _p(dbeta), M, D, _p(ws), _p(sums), _st())
+                 _p(dbeta), M, D, _p(ws), _p(sums), int(T), _p(tvalid), _st())
 
 
 # ----------------------------------------------------------------------------- attention

@@ -10,7 +10,7 @@ from __future__ import annotations
 
 import dataclasses
 import time
-from typing import Dict, Iterable, Optional
+from typing import Dict, Iterable, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -33,6 +33,12 @@ class TrainerOptions:
     # parameters, gradients, optimizer state and all non-GEMM kernels stay fp32.  bf16 has the
     # fp32 exponent range, so no loss scaler is needed.  SURVEY §8(d) C5.
     use_amp: bool = False
+    # HIP-graph mode with variable-length data: pad each batch's frame axis up to a multiple of
+    # graph_buckets[0] frames and its target axis to a multiple of graph_buckets[1] tokens, so
+    # batches of nearby shapes replay one captured graph (bounded graph count over an epoch).
+    # The padding is invisible to the result: lengths, SpecAug draws, BatchNorm statistics and
+    # the depthwise-convolution boundary use the batch's own padded length (device tvalid).
+    graph_buckets: Optional[Tuple[int, int]] = None
 
 
 class _GraphEntry:
@@ -135,8 +141,18 @@ class Trainer:
         speech = batch["speech"]
         self.iiter += 1
         last = self.iiter % opts.accum_grad == 0
+        tb = ub = None
+        if opts.graph_buckets is not None:
+            bf, bu = opts.graph_buckets
+            t_true = min(speech.shape[1], int(batch["speech_lengths"].max()))
+            tb = -(-t_true // bf) * bf
+            ub = max(1, -(-int(batch["text_lengths"].max()) // bu)) * bu
+            if speech.shape[1] < tb:
+                speech = torch.nn.functional.pad(speech, (0, 0, 0, tb - speech.shape[1]))
+            elif speech.shape[1] > tb:
+                speech = speech[:, :tb]
         prep = model.prepare(batch["speech_lengths"], batch["text"], batch["text_lengths"], speech.shape[1],
-                             speech.shape[2] if speech.dim() == 3 else 0)
+                             speech.shape[2] if speech.dim() == 3 else 0, t_bucket=tb, u_bucket=ub)
         sig = (tuple(speech.shape), prep.T, prep.Umax, prep.L, prep.get("n_samples", 0), last,
                tuple((k, tuple(v.shape)) for k, v in sorted(prep.host.items())))
         e = self._graphs.pop(sig, None)

@@ -104,19 +104,24 @@ int esp_colsum(const float* x, int M, int N, long ld, float* out, int accumulate
                void* stream);
 int esp_glu_fwd(const float* u, float* g, long rows, int D, void* stream);
 int esp_glu_bwd(const float* u, const float* dg, float* du, long rows, int D, void* stream);
+/* tvalid (device int, nullable): the batch is padded to T frames per utterance but only the
+ * first *tvalid exist in the reference batch (length-bucketed HIP graphs).  The depthwise
+ * convolution reads frames >= *tvalid as its zero padding and writes 0 there; BatchNorm
+ * statistics count B * (*tvalid) rows and the excluded rows get a zero gradient.  With tvalid,
+ * M = B * T rows for the BatchNorm calls. */
 int esp_dwconv1d(const float* x, const float* W, const float* bias, float* y, int Bn, int T, int D,
-                 int K, int flip, void* stream);
+                 int K, int flip, const int* tvalid, void* stream);
 int esp_dwconv1d_wgrad(const float* dy, const float* x, float* dW, int Bn, int T, int D, int K,
-                       float* work, void* stream);
+                       float* work, const int* tvalid, void* stream);
 int esp_bn_swish_fwd(const float* y, const float* gamma, const float* beta, float* s, float* mean,
                      float* rstd, float* run_mean, float* run_var, float momentum, float eps, int M,
-                     int D, double* work, void* stream);
+                     int D, double* work, int T, const int* tvalid, void* stream);
 /* eval mode: statistics from run_mean / run_var (mean / rstd written for inspection) */
 int esp_bn_swish_eval(const float* y, const float* gamma, const float* beta, float* s, const float* run_mean,
                       const float* run_var, float eps, int M, int D, float* mean, float* rstd, void* stream);
 int esp_bn_swish_bwd(const float* ds, const float* y, const float* mean, const float* rstd,
                      const float* gamma, const float* beta, float* dy, float* dgamma, float* dbeta,
-                     int M, int D, double* work, float* sums, void* stream);
+                     int M, int D, double* work, float* sums, int T, const int* tvalid, void* stream);
 
 /* ---- attention glue (attention.py:64-96,145-165,240-263) */
 int esp_heads_split(const float* src, long ld, int col0, int B, int T, int H, int dk,

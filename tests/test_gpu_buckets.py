@@ -1,0 +1,202 @@
+"""Length-bucketed HIP graphs (TrainerOptions.graph_buckets): a batch padded up to a bucket
+(frames to a multiple of bf, targets to a multiple of bu) and replayed on the bucket's graph
+must compute exactly what the reference computes on the batch itself, padded only to its own
+maximum length: BatchNorm statistics over B x T' of THIS batch and the depthwise convolution's
+zero padding at T' (convolution.py:56-79), CTC / label-smoothing denominators and SpecAug draws
+from this batch's lengths (espnet_model.py:199,379-396; time_warp.py; mask_along_axis.py).
+Kernel level: esp_dwconv1d / esp_bn_swish_* with the device valid-frame bound `tvalid`."""
+import pytest
+import torch
+
+from oracle import espnet_cpu as O
+from tests.helpers import build_model, load_seeded, small_cfg
+
+pytestmark = pytest.mark.gpu
+
+
+def _r(*shape, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g)
+
+
+@pytest.mark.parametrize("Kw", [31, 15, 7])
+def test_dwconv_and_bn_with_valid_frames(dev, Kw):
+    """Padded (T=80, garbage beyond Tv=57) == unpadded (T=57) on the valid frames; the padded
+    frames are written 0 (conv), get a zero gradient (BN) and do not enter statistics."""
+    from espnet_slurp_amd import kernels as K
+    B, Tv, T, D = 3, 57, 80, 96
+    x = _r(B, Tv, D, seed=1)
+    xp = _r(B, T, D, seed=2) * 50.0
+    xp[:, :Tv] = x
+    W, bias = _r(D, Kw, seed=3), _r(D, seed=4)
+    tv = torch.tensor([Tv], dtype=torch.int32, device=dev)
+    y_ref = torch.empty(B, Tv, D, device=dev)
+    y_pad = torch.empty(B, T, D, device=dev)
+    K.dwconv1d(x.to(dev), W.to(dev), bias.to(dev), y_ref, B, Tv, D, Kw)
+    K.dwconv1d(xp.to(dev), W.to(dev), bias.to(dev), y_pad, B, T, D, Kw, tvalid=tv)
+    assert torch.equal(y_pad[:, :Tv], y_ref)
+    assert torch.count_nonzero(y_pad[:, Tv:]) == 0
+    # BatchNorm + Swish forward / backward
+    gamma, beta = _r(D, seed=5).to(dev), _r(D, seed=6).to(dev)
+    yr = _r(B, Tv, D, seed=7)
+    yp = _r(B, T, D, seed=8) * 30.0
+    yp[:, :Tv] = yr
+    outs = []
+    for y, TT, t in ((yr, Tv, None), (yp, T, tv)):
+        M = B * TT
+        y2 = y.reshape(M, D).to(dev)
+        s = torch.empty(M, D, device=dev)
+        mean, rstd = torch.empty(D, device=dev), torch.empty(D, device=dev)
+        rm, rv = torch.zeros(D, device=dev), torch.ones(D, device=dev)
+        K.bn_swish_fwd(y2, gamma, beta, s, mean, rstd, rm, rv, T=TT, tvalid=t)
+        ds = _r(B, TT, D, seed=9)
+        ds[:, :Tv] = _r(B, Tv, D, seed=10)
+        ds = ds.reshape(M, D).to(dev)
+        dy = torch.empty(M, D, device=dev)
+        dg, db = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
+        sums = torch.empty(2 * D, device=dev)
+        K.bn_swish_bwd(ds, y2, mean, rstd, gamma, beta, dy, dg, db, sums, T=TT, tvalid=t)
+        outs.append((s.view(B, TT, D), mean, rstd, rm, rv, dy.view(B, TT, D), dg, db))
+    (s0, m0, r0, rm0, rv0, dy0, dg0, db0), (s1, m1, r1, rm1, rv1, dy1, dg1, db1) = outs
+    for a, b in ((m0, m1), (r0, r1), (rm0, rm1), (rv0, rv1), (dg0, dg1), (db0, db1), (s0, s1[:, :Tv]),
+                 (dy0, dy1[:, :Tv])):
+        assert (a - b).abs().max().item() <= 1e-6 * max(1.0, a.abs().max().item())
+    assert torch.count_nonzero(dy1[:, Tv:]) == 0
+    # depthwise weight gradient: padded frames contribute nothing
+    g0, g1 = torch.zeros(D, Kw, device=dev), torch.zeros(D, Kw, device=dev)
+    dyr = _r(B, Tv, D, seed=11)
+    dyp = torch.zeros(B, T, D)
+    dyp[:, :Tv] = dyr
+    K.dwconv1d_wgrad(dyr.to(dev), x.to(dev), g0, B, Tv, D, Kw)
+    K.dwconv1d_wgrad(dyp.to(dev), xp.to(dev), g1, B, T, D, Kw, tvalid=tv)
+    assert (g0 - g1).abs().max().item() <= 1e-5 * max(1.0, g0.abs().max().item())
+
+
+def _trainer(dev, graph, buckets=None, specaug=None):
+    from espnet_slurp_amd.optimizers.fused_adam import FusedAdam
+    from espnet_slurp_amd.schedulers.warmup_lr import WarmupLR
+    from espnet_slurp_amd.train.trainer import Trainer, TrainerOptions
+    cfg = small_cfg("latest")
+    model = build_model(cfg, dev, dropout=0.0, specaug=specaug)
+    load_seeded(model, cfg, 11)
+    model.train()
+    opt = FusedAdam(model.parameters(), model.flat, lr=1e-3)
+    tr = Trainer(model, opt, WarmupLR(opt, warmup_steps=10),
+                 TrainerOptions(grad_clip=5.0, graph_buckets=buckets), cuda_graph=graph)
+    return tr, model
+
+
+def _batch(dev, T, lens, ulens, seed):
+    speech, slen, text, tlen = O.synthetic_batch(len(lens), T, 80, 32, lens, ulens, seed)
+    return dict(speech=speech.to(dev), speech_lengths=slen, text=text, text_lengths=tlen)
+
+
+def _copy(b):
+    return dict(b, speech=b["speech"].clone(), text=b["text"].clone())
+
+
+@pytest.mark.parametrize("with_specaug", [False, True])
+def test_bucketed_graph_equals_eager_unpadded(dev, with_specaug):
+    """Batches of different frame / token lengths in one bucket (T <= 128, U <= 8) replay one
+    graph; a longer batch captures a second.  Every step equals the eager step on the batch as
+    the reference pads it (its own max lengths) to 1e-6: losses and parameters."""
+    specaug = None
+    if with_specaug:
+        from espnet_slurp_amd.asr.specaug.specaug import SpecAug
+        specaug = SpecAug(time_warp_window=5, freq_mask_width_range=(0, 10), num_freq_mask=2,
+                          time_mask_width_range=(0, 12), num_time_mask=2)
+    te, me = _trainer(dev, False, specaug=specaug)
+    tg, mg = _trainer(dev, True, buckets=(64, 8), specaug=specaug)
+    batches = [
+        _batch(dev, 112, [112, 90, 71], [6, 5, 4], 21),   # bucket (128, 8): captured
+        _batch(dev, 97, [97, 97, 97], [7, 3, 5], 22),      # same bucket, equal lengths (whole-batch warp)
+        _batch(dev, 80, [80, 66, 79], [2, 8, 1], 23),      # same bucket, shorter
+        _batch(dev, 150, [150, 131, 140], [9, 4, 6], 24),  # bucket (192, 16): second graph
+        _batch(dev, 120, [100, 120, 77], [3, 3, 3], 25),   # back to the first bucket
+    ]
+    for i, b in enumerate(batches):
+        torch.manual_seed(100 + i)  # SpecAug draws (CPU generator) identical for both trainers
+        le = te.train_one_step(_copy(b))["loss"].item()
+        torch.manual_seed(100 + i)
+        lg = tg.train_one_step(_copy(b))["loss"].item()
+        assert abs(le - lg) <= 1e-6 * max(1.0, abs(le)), (i, le, lg)
+    te.resolve_pending()
+    tg.sync_host_state()
+    assert len(tg._graphs) == 2
+    # Parameters after 5 Adam steps.  Adam turns a gradient that is zero in exact arithmetic
+    # (key biases: softmax is shift-invariant; the depthwise bias in front of BatchNorm) or
+    # nearly so (low-frequency rel-pos columns of linear_pos) into ~lr-sized steps driven by
+    # rounding noise, which depends on the summation length; those get the Adam bound.
+    # The other tensors: 5e-6 (the weight-gradient GEMMs reduce over B x T rows, so their
+    # split-K boundaries move with the padding; ~1e-7 relative gradient differences reach the
+    # parameters through Adam's normalisation).  The gradients themselves agree to 1e-6
+    # (test_bucketed_gradients_equal_unpadded), the losses of every step above to 1e-6.
+    lr_sum = sum(2e-4 * (i + 1) for i in range(len(batches)))
+    for (n, a), (_, b) in zip(me.named_parameters(), mg.named_parameters()):
+        gauge = n.endswith("linear_k.bias") or n.endswith("depthwise_conv.bias") or n.endswith("linear_pos.weight")
+        tol = lr_sum if gauge else 5e-6
+        assert (a - b).abs().max().item() <= tol, (n, (a - b).abs().max().item())
+
+
+@pytest.mark.parametrize("T,lens,ulens", [(112, [112, 90, 71], [6, 5, 4]), (128, [128, 100, 90], [8, 5, 4]),
+                                          (70, [70, 70, 70], [1, 2, 3]), (129, [129, 64, 100], [9, 9, 9])])
+def test_bucketed_gradients_equal_unpadded(dev, T, lens, ulens):
+    """One forward + backward on the batch padded to its bucket (64 frames, 8 tokens) vs on the
+    batch itself: the loss and every parameter gradient agree to 1e-6 (relative to the
+    tensor's largest gradient)."""
+    grads, losses = [], []
+    for buck in (None, (64, 8)):
+        _, m = _trainer(dev, False)
+        m.flat.grad.zero_()
+        b = _batch(dev, T, lens, ulens, 31)
+        speech = b["speech"]
+        tb = ub = None
+        if buck:
+            tb = -(-max(lens) // buck[0]) * buck[0]
+            ub = -(-max(ulens) // buck[1]) * buck[1]
+            speech = torch.nn.functional.pad(speech, (0, 0, 0, tb - speech.shape[1]))
+        prep = m.prepare(b["speech_lengths"], b["text"], b["text_lengths"], speech.shape[1], 80,
+                         t_bucket=tb, u_bucket=ub)
+        prep.to_device(dev)
+        loss, _, _ = m.forward_prepared(speech, prep)
+        loss.backward()
+        losses.append(loss.item())
+        grads.append({n: p.grad.clone() for n, p in m.named_parameters()})
+    assert abs(losses[0] - losses[1]) <= 1e-6 * max(1.0, abs(losses[0]))
+    for n, g0 in grads[0].items():
+        d = (g0 - grads[1][n]).abs().max().item()
+        assert d <= 1e-6 * max(1.0, g0.abs().max().item()), (n, d)
+
+
+def test_bucketed_graph_count_bounded_over_epoch(dev):
+    """A sampler epoch of variable-length utterances: the number of captured graphs is bounded
+    by the number of (frame, token) buckets, far below the number of distinct batch shapes."""
+    import numpy as np
+    from espnet_slurp_amd.samplers.num_elements_batch_sampler import NumElementsBatchSampler
+    rng = np.random.default_rng(5)
+    n = 48
+    lens = rng.integers(40, 260, n)
+    ulens = rng.integers(1, 14, n)
+    import tempfile, os
+    with tempfile.TemporaryDirectory() as d:
+        sf = os.path.join(d, "speech_shape")
+        tf = os.path.join(d, "text_shape")
+        with open(sf, "w") as f:
+            f.writelines(f"u{i} {int(l)},80\n" for i, l in enumerate(lens))
+        with open(tf, "w") as f:
+            f.writelines(f"u{i} {int(u)}\n" for i, u in enumerate(ulens))
+        sampler = NumElementsBatchSampler(batch_bins=80 * 700, shape_files=[sf, tf], min_batch_size=1)
+        batches = list(sampler)
+    tg, _ = _trainer(dev, True, buckets=(64, 8))
+    shapes = set()
+    for bi, keys in enumerate(batches):
+        idx = [int(k[1:]) for k in keys]
+        bl = [int(lens[i]) for i in idx]
+        ul = [int(ulens[i]) for i in idx]
+        b = _batch(dev, max(bl), bl, ul, 300 + bi)
+        shapes.add((len(idx), max(bl), max(ul)))
+        tg.train_one_step(b)
+    tg.sync_host_state()
+    buckets = {(len(k), -(-max(int(lens[int(u[1:])]) for u in k) // 64), -(-max(int(ulens[int(u[1:])]) for u in k) // 8))
+               for k in batches}
+    assert len(tg._graphs) <= len(buckets) < len(shapes), (len(tg._graphs), len(buckets), len(shapes))
