@@ -166,13 +166,14 @@ def workload_name(args) -> str:
 
 def gemm_algorithmic_bytes(shapes) -> float:
     """Sum over the profiled GEMM launches of the bytes each must move at least once: A, B read,
-    C written (fp32).  An implicit-im2col operand counts its NHWC source map (~ 4/9 of the
+    C written (fp32), plus the fused epilogue's own M x N streams (residual / pre-activation
+    reads, aux writes).  An implicit-im2col operand counts its NHWC source map (~ 4/9 of the
     virtual M x K matrix for the 3x3 / stride-2 convolution)."""
     tot = 0.0
-    for (ma, mb, M, N, Kd, batch), (n, _ms, _f) in shapes.items():
+    for (ma, mb, M, N, Kd, batch), (n, _ms, _f, extra) in shapes.items():
         a = M * Kd * (4 / 9 if ma >= 2 else 1.0)
         b = N * Kd * (4 / 9 if mb >= 2 else 1.0)
-        tot += n * 4.0 * batch * (a + b + M * N)
+        tot += n * 4.0 * batch * (a + b + M * N) + extra
     return tot
 
 

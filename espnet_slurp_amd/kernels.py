@@ -86,20 +86,21 @@ def profile_gemm_start():
 
 def profile_gemm_stop(by_shape: bool = False):
     """-> (total algorithmic FLOPs, total kernel ms, launches) since profile_gemm_start();
-    with by_shape, also {(modes, M, N, K, batch): [launches, ms, flops]}."""
+    with by_shape, also {(modes, M, N, K, batch): [launches, ms, flops, epilogue bytes]}."""
     global _PROF
     prof, _PROF = _PROF or [], None
     torch.cuda.synchronize()
     flops = sum(p[0] for p in prof)
     ms = 0.0
     shapes = {}
-    for f, a, b, key in prof:
+    for f, a, b, key, extra in prof:
         t = a.elapsed_time(b)
         ms += t
-        s = shapes.setdefault(key, [0, 0.0, 0.0])
+        s = shapes.setdefault(key, [0, 0.0, 0.0, 0.0])
         s[0] += 1
         s[1] += t
         s[2] += f
+        s[3] += extra
     if by_shape:
         return flops, ms, len(prof), shapes
     return flops, ms, len(prof)
@@ -130,7 +131,10 @@ def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc
                  ctypes_ptr(ica), ctypes_ptr(icb), _p(ws), ws.numel(), _st())
     if _PROF is not None:
         ev1.record()
-        _PROF.append((2.0 * M * N * K * batch, ev0, ev1, (mode_a, mode_b, M, N, K, batch)))
+        # fused-epilogue streams the launch must move besides A, B, C: residual R and
+        # pre-activation / derivative reads, aux writes (each one M x N fp32 tensor per batch)
+        extra = 4.0 * M * N * batch * ((R is not None) + (aux is not None) + (pre is not None))
+        _PROF.append((2.0 * M * N * K * batch, ev0, ev1, (mode_a, mode_b, M, N, K, batch), extra))
 
 
 def ctypes_ptr(arr):

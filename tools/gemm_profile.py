@@ -35,7 +35,7 @@ def main():
     step_ms = t0.elapsed_time(t1)
     print(f"step {step_ms:.1f} ms, gemm {ms:.1f} ms in {n} launches, {flops / ms / 1e9:.1f} TFLOP/s")
     rows = sorted(shapes.items(), key=lambda kv: -kv[1][1])
-    for key, (cnt, t, f) in rows[:40]:
+    for key, (cnt, t, f, _extra) in rows[:40]:
         print(f"{str(key):48s} n={cnt:4d} {t:8.2f} ms  {f / t / 1e9:7.1f} TF/s")
 
 
