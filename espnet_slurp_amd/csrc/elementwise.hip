@@ -20,7 +20,7 @@ void set_error(const char* fmt, ...) {
 }  // namespace esp
 
 ESP_API const char* esp_last_error(void) { return esp::g_err; }
-ESP_API int esp_abi_version(void) { return 15; }
+ESP_API int esp_abi_version(void) { return 16; }
 ESP_API int esp_set_rng_key(const unsigned long long* key) {
   esp::g_rng_key = (const uint64_t*)key;
   return 0;
@@ -427,5 +427,66 @@ ESP_API int esp_opt_advance(double* state, const float* clip, void* stream) {
 ESP_API int esp_rng_advance(unsigned long long* key, void* stream) {
   hipLaunchKernelGGL(rng_advance_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, key);
   ESP_CHECK_LAUNCH("esp_rng_advance");
+  return 0;
+}
+
+// ------------------------------------------------------------------------- bf16 operand casts
+// Operands of the bf16-operand GEMM (esp_gemm_bf16), round-to-nearest-even.  Plain: y[r, c] =
+// bf16(x[r, c]) with 4 columns per thread; transposed: y[c, r] through a 64 x 64 LDS tile
+// (coalesced on both sides), for the weight-gradient operands dY^T and X^T and for W^T.
+namespace {
+__device__ __forceinline__ uint16_t bf16_rne(float f) {
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffffu) ? 0x40u : 0u));  // inf/nan
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+__global__ void f32_to_bf16_kernel(const float* __restrict__ x, uint16_t* __restrict__ y, long rows, int cols, long ldx,
+                                   long ldy) {
+  const int cq = (cols + 3) / 4;
+  const long n = rows * cq;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cq;
+    const int c = (int)(i - r * cq) * 4;
+    const float* src = x + r * ldx + c;
+    uint16_t* dst = y + r * ldy + c;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (c + e < cols) dst[e] = bf16_rne(src[e]);
+  }
+}
+__global__ __launch_bounds__(256) void f32_to_bf16_t_kernel(const float* __restrict__ x, uint16_t* __restrict__ y,
+                                                            long rows, int cols, long ldx, long ldy) {
+  __shared__ uint16_t tile[64][66];
+  const long r0 = (long)blockIdx.y * 64;
+  const int c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int k = ty; k < 64; k += 4) {
+    const long r = r0 + k;
+    const int c = c0 + tx;
+    tile[k][tx] = (r < rows && c < cols) ? bf16_rne(x[r * ldx + c]) : (uint16_t)0;
+  }
+  __syncthreads();
+  for (int k = ty; k < 64; k += 4) {
+    const int c = c0 + k;
+    const long r = r0 + tx;
+    if (c < cols && r < rows) y[(long)c * ldy + r] = tile[tx][k];
+  }
+}
+}  // namespace
+
+ESP_API int esp_f32_to_bf16(const float* x, void* y, long rows, int cols, long ldx, long ldy, int transpose,
+                            void* stream) {
+  ESP_ARG_CHECK(rows >= 0 && cols >= 0, "esp_f32_to_bf16: bad sizes");
+  if (rows == 0 || cols == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (transpose) {
+    ESP_ARG_CHECK((rows + 63) / 64 <= 65535, "esp_f32_to_bf16: too many rows for the transposed cast");
+    hipLaunchKernelGGL(f32_to_bf16_t_kernel, dim3((cols + 63) / 64, (unsigned)((rows + 63) / 64)), dim3(256), 0, st,
+                       x, (uint16_t*)y, rows, cols, ldx, ldy);
+  } else {
+    hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(grid_for(rows * ((cols + 3) / 4))), dim3(256), 0, st, x,
+                       (uint16_t*)y, rows, cols, ldx, ldy);
+  }
+  ESP_CHECK_LAUNCH("esp_f32_to_bf16");
   return 0;
 }

@@ -184,11 +184,11 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
   const bool rs = can_rs && g.rowsum;
   if (rs) kind = EPI_PLAIN;
   const dim3 grid((unsigned)std::min<long>(x.ntiles, persist_blocks(glds_occupancy_rt(BNT, kind))));
-  const bool bf = g.bf16 != 0;
-  if (kind == EPI_PLAIN) return glds_launch_plain(MA, MB, BNT, bf, rs, grid, st, g, x);
-  if (kind == EPI_FWD || kind == EPI_BWD) return glds_launch_epi(MA, MB, BNT, bf, kind, grid, st, g, x);
-  if (kind == EPI_P0 || kind == EPI_PR) return glds_launch_pspec(MA, MB, BNT, bf, kind, grid, st, g, x);
-  return glds_launch_spec(MA, MB, BNT, bf, kind, grid, st, g, x);
+  const int prec = g.bf16;
+  if (kind == EPI_PLAIN) return glds_launch_plain(MA, MB, BNT, prec, rs, grid, st, g, x);
+  if (kind == EPI_FWD || kind == EPI_BWD) return glds_launch_epi(MA, MB, BNT, prec, kind, grid, st, g, x);
+  if (kind == EPI_P0 || kind == EPI_PR) return glds_launch_pspec(MA, MB, BNT, prec, kind, grid, st, g, x);
+  return glds_launch_spec(MA, MB, BNT, prec, kind, grid, st, g, x);
 }
 
 template <int MA, int MB>
@@ -196,6 +196,10 @@ int launch(const GemmArgs& g0, int batch, hipStream_t st) {
   bool done = false;
   if (g0.bnt == 64 || g0.bnt == 128) done = launch_glds(MA, MB, g0, batch, st);
   GemmArgs g = g0;
+  if (!done && g.bf16 == 2) {
+    esp::set_error("esp_gemm_bf16: operands not eligible for the LDS-DMA kernel (16-B alignment, ld %% 8)");
+    return -1;
+  }
   if (!done) {
     g.rs_work = nullptr;
     if (g.rowsum && MA == RC)  // the register-staged kernel does not fuse the row sums
@@ -243,6 +247,13 @@ ESP_API int esp_set_gemm_compute(int dtype) {
 }
 ESP_API int esp_get_gemm_compute(void) { return g_compute; }
 
+static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2, const float* A, long lda,
+                    long sa1, long sa2, const float* B, long ldb, long sb1, long sb2, float* C, long ldc, long sc1,
+                    long sc2, const float* bias, float alpha, float beta, const float* R, int act, float* aux,
+                    float drop_p, unsigned long long seed, int bwd_act, const float* pre, float* rowsum,
+                    const int* im2col_a, const int* im2col_b, float* work, long work_bytes, void* stream,
+                    int prec_in);
+
 ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2,
                          const float* A, long lda, long sa1, long sa2,
                          const float* B, long ldb, long sb1, long sb2,
@@ -252,6 +263,31 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
                          int bwd_act, const float* pre, float* rowsum,
                          const int* im2col_a, const int* im2col_b, float* work, long work_bytes,
                          void* stream) {
+  return gemm_run(mode_a, mode_b, M, N, K, batch, nb2, A, lda, sa1, sa2, B, ldb, sb1, sb2, C, ldc, sc1, sc2, bias,
+                  alpha, beta, R, act, aux, drop_p, seed, bwd_act, pre, rowsum, im2col_a, im2col_b, work, work_bytes,
+                  stream, -1);
+}
+
+ESP_API int esp_gemm_bf16(int M, int N, int K, int batch, int nb2, const void* A, long lda, long sa1, long sa2,
+                          const void* B, long ldb, long sb1, long sb2, float* C, long ldc, long sc1, long sc2,
+                          const float* bias, float alpha, float beta, const float* R, int act, float* aux,
+                          float drop_p, unsigned long long seed, int bwd_act, const float* pre, float* work,
+                          long work_bytes, void* stream) {
+  ESP_ARG_CHECK(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && sa1 % 8 == 0 && sa2 % 8 == 0 && sb1 % 8 == 0 &&
+                    sb2 % 8 == 0 && aligned16(A) && aligned16(B),
+                "esp_gemm_bf16: K, ld and strides must be multiples of 8 bf16 and A, B 16-B aligned");
+  // bf16 pairs viewed as fp32 elements by the staging code (PREC 2)
+  return gemm_run(KC, KC, M, N, K / 2, batch, nb2, (const float*)A, lda / 2, sa1 / 2, sa2 / 2, (const float*)B,
+                  ldb / 2, sb1 / 2, sb2 / 2, C, ldc, sc1, sc2, bias, alpha, beta, R, act, aux, drop_p, seed, bwd_act,
+                  pre, nullptr, nullptr, nullptr, work, work_bytes, stream, 2);
+}
+
+static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2, const float* A, long lda,
+                    long sa1, long sa2, const float* B, long ldb, long sb1, long sb2, float* C, long ldc, long sc1,
+                    long sc2, const float* bias, float alpha, float beta, const float* R, int act, float* aux,
+                    float drop_p, unsigned long long seed, int bwd_act, const float* pre, float* rowsum,
+                    const int* im2col_a, const int* im2col_b, float* work, long work_bytes, void* stream,
+                    int prec_in) {
   ESP_ARG_CHECK(M >= 0 && N >= 0 && K >= 0 && batch >= 1 && nb2 >= 1 && batch % nb2 == 0,
                 "esp_gemm_f32: bad sizes M=%d N=%d K=%d batch=%d nb2=%d", M, N, K, batch, nb2);
   ESP_ARG_CHECK(mode_a >= 0 && mode_a <= 3 && mode_b >= 0 && mode_b <= 3, "esp_gemm_f32: bad mode");
@@ -307,7 +343,7 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
   const long target = 2 * 256;
   auto ntiles = [&](int bn) { return (long)((N + bn - 1) / bn) * ((M + BM - 1) / BM) * batch; };
   g.bnt = 0;
-  g.bf16 = g_compute == 1;
+  g.bf16 = prec_in >= 0 ? prec_in : (g_compute == 1 ? 1 : 0);
   if (variant() == 4 && g.a.glds && g.b.glds && K > 0) {
     // per-CU time model: ceil(tiles / CUs) tiles of bn/64 units each, x1.3 when the grid
     // leaves CUs with a single resident block (one wave per SIMD); ties keep 128 (intensity)

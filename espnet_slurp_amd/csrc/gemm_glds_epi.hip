@@ -5,12 +5,12 @@
 
 namespace espg {
 
-bool glds_launch_epi(int ma, int mb, int bnt, bool bf, int epi, dim3 grid, hipStream_t st, const GemmArgs& g,
+bool glds_launch_epi(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hipStream_t st, const GemmArgs& g,
                      const GldsArgs& x) {
   bool ok = false;
-  const bool known = glds_switch(ma, mb, bnt, bf, [&](auto A, auto B, auto N, auto F) {
+  const bool known = glds_switch(ma, mb, bnt, prec, [&](auto A, auto B, auto N, auto F) {
     constexpr int MA = decltype(A)::value, MB = decltype(B)::value, BNT = decltype(N)::value;
-    constexpr bool BF = decltype(F)::value;
+    constexpr int BF = decltype(F)::value;
     constexpr bool can_fwd = (MA == KC && (MB == KC || MB == RC)) || (MA == I2C_KC && MB == KC);
     constexpr bool can_bwd = (MA == KC || MA == I2CT_KC) && MB == RC;
     if constexpr (can_fwd) {

@@ -5,11 +5,11 @@
 
 namespace espg {
 
-bool glds_launch_plain(int ma, int mb, int bnt, bool bf, bool rs, dim3 grid, hipStream_t st, const GemmArgs& g,
+bool glds_launch_plain(int ma, int mb, int bnt, int prec, bool rs, dim3 grid, hipStream_t st, const GemmArgs& g,
                        const GldsArgs& x) {
-  return glds_switch(ma, mb, bnt, bf, [&](auto A, auto B, auto N, auto F) {
+  return glds_switch(ma, mb, bnt, prec, [&](auto A, auto B, auto N, auto F) {
     constexpr int MA = decltype(A)::value, MB = decltype(B)::value, BNT = decltype(N)::value;
-    constexpr bool BF = decltype(F)::value;
+    constexpr int BF = decltype(F)::value;
     if constexpr (MA == RC) {
       if (rs) {
         hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, true, EPI_PLAIN, BF>), grid, dim3(NT), 0, st, g, x);

@@ -86,7 +86,9 @@ struct GemmArgs {
   int batch;
   int splits, kchunk;  // split-K: blockIdx.z = z*splits + split; partials -> work
   float* work;
-  int bf16;  // bf16-input MFMA kernel (esp_set_gemm_compute(1)); fp32 operands rounded in LDS staging
+  int bf16;  // MFMA precision: 0 fp32; 1 bf16 MFMA on fp32 operands rounded after staging
+             // (esp_set_gemm_compute(1)); 2 bf16 operands in HBM (esp_gemm_bf16: K, ld, strides
+             // given in fp32 units, i.e. bf16 pairs; KC x KC only)
   int bnt;  // LDS-DMA kernel tile width (128, or 64 for narrow / mid-size grids); 0 = fallback kernel
   int bwd_act;       // != 0: backward epilogue  v = drop'(acc) * act'(pre)  (act code, dropout regenerated)
   const float* pre;  // pre-activation (same layout as C) for bwd_act
@@ -1138,7 +1140,13 @@ constexpr int glds_occupancy() { return (BNT == 64 && (EPI == EPI_PLAIN || EPI >
 // two v_mfma_f32_32x32x16_bf16 per (i, j) tile pair instead of sixteen 32x32x2 f32 MFMAs: k-step
 // 0 takes the lane's values s = 0..7 (k = 16h + s), step 1 s = 8..15, identically for A and B,
 // so the two steps cover the slab's 32 k once.  The fused row sums stay fp32.
-template <int MA, int MB, int BNT, bool RS, int EPI, bool BF16 = false>
+// PREC = 2 (esp_gemm_bf16): the operands are bf16 in HBM, viewed by the staging code as fp32
+// arrays of bf16 PAIRS (K, ld and strides in pairs), so the LDS-DMA pipeline, the swizzle and
+// the fragment reads are those of the fp32 path unchanged: a slab holds 64 bf16 k per row and
+// a lane's 16 fetched "floats" are 32 bf16 k-values, fed as four bf16x8 operands to four
+// v_mfma_f32_32x32x16_bf16 per (i, j) tile pair (k-step t takes values 8t..8t+7, identically
+// for A and B, so the four steps cover the slab's 64 k once).  No conversion in the k-loop.
+template <int MA, int MB, int BNT, bool RS, int EPI, int PREC = 0>
 __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_kernel(GemmArgs g, GldsArgs x) {
   constexpr int WN = BNT / 64, WM = 4 / WN, TM = BM / (WM * 32), TN = 2;
   constexpr int A_SZ = BM * GL_BK, B_SZ = BNT * GL_BK, BUF = A_SZ + B_SZ;
@@ -1199,7 +1207,20 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_ke
       for (int i = 0; i < TM; ++i) frag16<MA, BM>(cur, wm * TM * 32 + i * 32 + l32, h, af[i]);
 #pragma unroll
       for (int j = 0; j < TN; ++j) frag16<MB, BNT>(cur + A_SZ, wn * 64 + j * 32 + l32, h, bf[j]);
-      if constexpr (BF16) {
+      if constexpr (PREC == 2) {
+        static_assert(!RS, "row sums of packed bf16 operands");
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              const float4 a4 = make_float4(af[i][4 * t], af[i][4 * t + 1], af[i][4 * t + 2], af[i][4 * t + 3]);
+              const float4 b4 = make_float4(bf[j][4 * t], bf[j][4 * t + 1], bf[j][4 * t + 2], bf[j][4 * t + 3]);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a4),
+                                                                  __builtin_bit_cast(bf16x8, b4), acc[i][j], 0, 0, 0);
+            }
+      } else if constexpr (PREC == 1) {
         bf16x8 ah[TM][2], bh[TN][2];
 #pragma unroll
         for (int hs = 0; hs < 2; ++hs) {
@@ -1312,23 +1333,28 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_ke
 // resident blocks per CU of a gemm_glds_kernel<.., BNT, .., EPI, ..> launch (host side)
 inline int glds_occupancy_rt(int bnt, int epi) { return (bnt == 64 && (epi == EPI_PLAIN || epi >= EPI_BIAS)) ? 3 : 2; }
 
-// Map run-time (mode_a, mode_b, tile width, bf16) onto compile-time constants for the mode pairs
-// the host issues; calls f(MA, MB, BNT, BF) with std::integral_constant arguments.  false: no
-// such instantiation.
+// Map run-time (mode_a, mode_b, tile width, precision) onto compile-time constants for the mode
+// pairs the host issues; calls f(MA, MB, BNT, PREC) with std::integral_constant arguments.
+// false: no such instantiation (PREC 2 exists for KC x KC only).
 template <int V>
 using IC = std::integral_constant<int, V>;
 template <class F>
-bool glds_switch(int ma, int mb, int bnt, bool bf, F&& f) {
+bool glds_switch(int ma, int mb, int bnt, int prec, F&& f) {
   auto tile = [&](auto A, auto B) {
     if (bnt != 64 && bnt != 128) return false;
-    if (bnt == 64) {
-      if (bf) f(A, B, IC<64>{}, std::true_type{});
-      else f(A, B, IC<64>{}, std::false_type{});
-    } else {
-      if (bf) f(A, B, IC<128>{}, std::true_type{});
-      else f(A, B, IC<128>{}, std::false_type{});
-    }
-    return true;
+    auto by_prec = [&](auto N) {
+      if (prec == 0) {
+        f(A, B, N, IC<0>{});
+      } else if (prec == 1) {
+        f(A, B, N, IC<1>{});
+      } else if constexpr (decltype(A)::value == KC && decltype(B)::value == KC) {
+        f(A, B, N, IC<2>{});
+      } else {
+        return false;
+      }
+      return true;
+    };
+    return bnt == 64 ? by_prec(IC<64>{}) : by_prec(IC<128>{});
   };
   switch (ma * 8 + mb) {
     case KC * 8 + KC: return tile(IC<KC>{}, IC<KC>{});
@@ -1348,13 +1374,13 @@ bool glds_switch(int ma, int mb, int bnt, bool bf, F&& f) {
 //   gemm_glds_epi.hip   : generic EPI_FWD / EPI_BWD
 //   gemm_glds_spec.hip  : specialised kinds (EPI_BIAS .. EPI_BMUL)
 //   gemm_glds_pspec.hip : specialised plain kinds (EPI_P0, EPI_PR)
-bool glds_launch_plain(int ma, int mb, int bnt, bool bf, bool rs, dim3 grid, hipStream_t st, const GemmArgs& g,
+bool glds_launch_plain(int ma, int mb, int bnt, int prec, bool rs, dim3 grid, hipStream_t st, const GemmArgs& g,
                        const GldsArgs& x);
-bool glds_launch_epi(int ma, int mb, int bnt, bool bf, int epi, dim3 grid, hipStream_t st, const GemmArgs& g,
+bool glds_launch_epi(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hipStream_t st, const GemmArgs& g,
                      const GldsArgs& x);
-bool glds_launch_spec(int ma, int mb, int bnt, bool bf, int epi, dim3 grid, hipStream_t st, const GemmArgs& g,
+bool glds_launch_spec(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hipStream_t st, const GemmArgs& g,
                       const GldsArgs& x);
-bool glds_launch_pspec(int ma, int mb, int bnt, bool bf, int epi, dim3 grid, hipStream_t st, const GemmArgs& g,
+bool glds_launch_pspec(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hipStream_t st, const GemmArgs& g,
                        const GldsArgs& x);
 
 }  // namespace espg

@@ -137,6 +137,35 @@ def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc
         _PROF.append((2.0 * M * N * K * batch, ev0, ev1, (mode_a, mode_b, M, N, K, batch), extra))
 
 
+def gemm_bf16(M: int, N: int, K: int, A16, B16, C, *, lda, ldb, ldc, c_off=0, bias=None, alpha=1.0, beta=0.0,
+              R=None, act=ACT_NONE, aux=None, drop_p=0.0, seed=0, bwd_act=ACT_NONE, pre=None):
+    """C = alpha*epi(A B^T + bias) + beta*R with bf16 operands A [M][K], B [N][K] (torch.bfloat16,
+    K-contiguous) and the fp32 epilogue of gemm() (esp_gemm_bf16)."""
+    assert A16.dtype == torch.bfloat16 and B16.dtype == torch.bfloat16
+    ws = _GEMM_WS.get(_GEMM_WS_BYTES, C.device)
+    if _PROF is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    _native.call("esp_gemm_bf16", M, N, K, 1, 1, _p(A16), lda, 0, 0, _p(B16), ldb, 0, 0,
+                 _p(C, c_off), ldc, 0, 0, _p(bias), float(alpha), float(beta), _p(R, c_off) if R is not None else None,
+                 act, _p(aux, c_off) if aux is not None else None, float(drop_p), seed & 0xFFFFFFFFFFFFFFFF,
+                 int(bwd_act), _p(pre, c_off) if pre is not None else None, _p(ws), ws.numel(), _st())
+    if _PROF is not None:
+        ev1.record()
+        extra = 4.0 * M * N * ((R is not None) + (aux is not None) + (pre is not None))
+        _PROF.append((2.0 * M * N * K, ev0, ev1, (KC, KC, M, N, K, 1, "bf16"), extra))
+
+
+def to_bf16(x, rows: int, cols: int, ldx: int, transpose: bool = False, out=None):
+    """bf16 copy (round to nearest even) of a rows x cols fp32 matrix with row pitch ldx;
+    transpose: the cols x rows matrix (esp_f32_to_bf16)."""
+    if out is None:
+        out = torch.empty((cols, rows) if transpose else (rows, cols), dtype=torch.bfloat16, device=x.device)
+    _native.call("esp_f32_to_bf16", _p(x), _p(out), rows, cols, ldx, out.stride(0), int(transpose), _st())
+    return out
+
+
 def ctypes_ptr(arr):
     import ctypes
     return ctypes.cast(arr, ctypes.c_void_p) if arr is not None else None

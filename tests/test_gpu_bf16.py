@@ -143,3 +143,61 @@ def test_bf16_trainer_graph_matches_eager(dev):
     assert K.get_gemm_compute() == 0  # the trainer restores the process-wide setting
     torch.cuda.synchronize()
     assert torch.allclose(me.flat.flat, mg.flat.flat, rtol=0, atol=1e-6)
+
+
+# ------------------------------------------------------------------ bf16-operand GEMM (PREC 2)
+@pytest.mark.parametrize("M,N,Kd", [(300, 200, 136), (11968, 512, 512), (64, 64, 4096), (1000, 1024, 8),
+                                    (257, 130, 520)])
+def test_bf16_operand_gemm(dev, M, N, Kd):
+    """esp_gemm_bf16: bf16 A [M][K] x B [N][K]^T with fp32 accumulate == fp64 GEMM of the same
+    bf16 values up to accumulation order (ragged M / N edges, a K tail inside the last 64-wide
+    slab, split-K for the small-M x N, long-K case)."""
+    A, B = _r(M, Kd, seed=31), _r(N, Kd, seed=32)
+    A16, B16 = A.to(torch.bfloat16).to(dev), B.to(torch.bfloat16).to(dev)
+    C = torch.full((M, N), float("nan"), device=dev)
+    K.gemm_bf16(M, N, Kd, A16, B16, C, lda=Kd, ldb=Kd, ldc=N)
+    ref = A16.double().cpu() @ B16.double().cpu().t()
+    err = (C.cpu().double() - ref).abs().max().item()
+    assert err <= 4e-6 * math.sqrt(Kd) * max(1.0, A.abs().max().item() * B.abs().max().item()), err
+
+
+def test_bf16_operand_gemm_epilogues(dev):
+    """The fused epilogues on the bf16-operand kernel: bias + Swish + dropout with the derivative
+    stored (FFN w_1), bias + dropout + residual (linear_out), plain + residual; each equals the
+    fp32-operand kernel applied to the same (bf16-valued) operands."""
+    M, N, Kd = 517, 256, 192
+    A = _r(M, Kd, seed=41).to(torch.bfloat16).float().to(dev)
+    B = _r(N, Kd, seed=42).to(torch.bfloat16).float().to(dev)
+    A16, B16 = A.to(torch.bfloat16), B.to(torch.bfloat16)
+    b, R = _r(N, seed=43).to(dev), _r(M, N, seed=44).to(dev)
+    cases = [dict(bias=b, act=K.ACT_SWISH | K.ACT_AUX_DERIV, aux=True, drop_p=0.1, seed=5),
+             dict(bias=b, R=R, beta=1.0, alpha=0.5, drop_p=0.1, seed=6),
+             dict(R=R, beta=1.0)]
+    for kw in cases:
+        outs = []
+        for bf in (False, True):
+            C = torch.empty(M, N, device=dev)
+            aux = torch.empty(M, N, device=dev) if kw.get("aux") else None
+            args = {k: v for k, v in kw.items() if k != "aux"}
+            if bf:
+                K.gemm_bf16(M, N, Kd, A16, B16, C, lda=Kd, ldb=Kd, ldc=N, aux=aux, **args)
+            else:
+                K.gemm(M, N, Kd, A, B, C, lda=Kd, ldb=Kd, ldc=N, aux=aux, **args)
+            outs.append((C, aux))
+        (c0, a0), (c1, a1) = outs
+        assert torch.equal(c0 == 0, c1 == 0)  # same dropout masks
+        assert (c0 - c1).abs().max().item() <= 1e-4 * max(1.0, c0.abs().max().item())
+        if a0 is not None:
+            assert (a0 - a1).abs().max().item() <= 1e-4
+
+
+@pytest.mark.parametrize("rows,cols", [(1000, 520), (37, 64), (4096, 2048)])
+def test_f32_to_bf16_casts(dev, rows, cols):
+    """esp_f32_to_bf16: round-to-nearest-even, plain and transposed, bit-equal to torch."""
+    x = (_r(rows, cols, seed=51) * 100).to(dev)
+    x[0, :4] = torch.tensor([float("inf"), -float("inf"), 0.0, -0.0])
+    ref = x.to(torch.bfloat16)
+    y = K.to_bf16(x, rows, cols, cols)
+    assert torch.equal(y.view(torch.int16), ref.view(torch.int16))
+    yt = K.to_bf16(x, rows, cols, cols, transpose=True)
+    assert torch.equal(yt.view(torch.int16), ref.t().contiguous().view(torch.int16))
