@@ -730,7 +730,7 @@ ESP_API int esp_dwconv1d_wgrad(const float* dy, const float* x, float* dW, int B
 }
 
 // BatchNorm1d training forward + Swish. mean/rstd (D) outputs; running stats updated when
-// run_mean != NULL.  workspace: >= D*ceil(M/64) doubles
+// run_mean != NULL.  workspace: >= D*384 doubles (at most 384 row chunks, rows_per_block)
 ESP_API int esp_bn_swish_fwd(const float* y, const float* gamma, const float* beta, float* s, float* mean, float* rstd,
                              float* run_mean, float* run_var, float momentum, float eps, int M, int D, double* work,
                              int T, const int* tvalid, void* stream) {
@@ -774,7 +774,7 @@ ESP_API int esp_bn_swish_eval(const float* y, const float* gamma, const float* b
 }
 
 // given ds = dL/ds, writes dy (grad wrt BN input) into `dy`; dgamma/dbeta accumulated.
-// workspace: >= 2*D*ceil(M/64) doubles + 2*D floats (sums) passed separately
+// workspace: >= 2*D*384 doubles (at most 384 row chunks) + 2*D floats (sums) passed separately
 ESP_API int esp_bn_swish_bwd(const float* ds, const float* y, const float* mean, const float* rstd, const float* gamma,
                              const float* beta, float* dy, float* dgamma, float* dbeta, int M, int D, double* work,
                              float* sums, int T, const int* tvalid, void* stream) {

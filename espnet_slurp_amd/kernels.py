@@ -395,10 +395,14 @@ def dwconv1d_wgrad(dy, x, dW, Bn, T, D, K, tvalid=None):
     _native.call("esp_dwconv1d_wgrad", _p(dy), _p(x), _p(dW), Bn, T, D, K, _p(ws), _p(tvalid), _st())
 
 
+# BatchNorm statistics are reduced in at most 384 row chunks (norm.hip rows_per_block): the
+# workspace holds D (forward) / 2D (backward) fp64 partials per chunk
+BN_MAX_CHUNKS = 384
+
+
 def bn_swish_fwd(y, gamma, beta, s, mean, rstd, run_mean, run_var, momentum=0.1, eps=1e-5, T=0, tvalid=None):
     M, D = y.shape
-    nb = (M + 63) // 64
-    ws = _work(8 * D * max(nb, 1), y.device)
+    ws = _work(8 * D * BN_MAX_CHUNKS, y.device)
     _native.call("esp_bn_swish_fwd", _p(y), _p(gamma), _p(beta), _p(s), _p(mean), _p(rstd), _p(run_mean),
                  _p(run_var), float(momentum), float(eps), M, D, _p(ws), int(T), _p(tvalid), _st())
 
@@ -412,8 +416,7 @@ def bn_swish_eval(y, gamma, beta, s, run_mean, run_var, mean, rstd, eps=1e-5):
 
 def bn_swish_bwd(ds, y, mean, rstd, gamma, beta, dy, dgamma, dbeta, sums, T=0, tvalid=None):
     M, D = y.shape
-    nb = (M + 63) // 64
-    ws = _work(8 * 2 * D * max(nb, 1), y.device)
+    ws = _work(8 * 2 * D * BN_MAX_CHUNKS, y.device)
     _native.call("esp_bn_swish_bwd", _p(ds), _p(y), _p(mean), _p(rstd), _p(gamma), _p(beta), _p(dy), _p(dgamma),
                  _p(dbeta), M, D, _p(ws), _p(sums), int(T), _p(tvalid), _st())
 

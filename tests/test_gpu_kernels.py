@@ -573,3 +573,35 @@ def test_conv2_dgrad_parity_classes_vs_column_path(dev, T1, F1):
     torch.cuda.synchronize()
     assert not torch.isnan(got).any()
     assert rel_err(got.cpu(), ref.cpu()) < 1e-5
+
+
+@pytest.mark.parametrize("M,D", [(11968, 512), (3000, 768), (47872, 256)])
+def test_bn_swish_large_rows_and_channels(dev, M, D):
+    """BatchNorm + Swish statistics at the C4 / C5 shapes (B*T' = 32*374 rows, D = 512): the
+    reduction uses up to 384 row chunks of fp64 partials, D (2D) per chunk — the workspace the
+    wrapper reserves must cover that (a D=512, B=32 undersized workspace once corrupted
+    neighbouring allocations).  Forward / backward vs fp64 torch."""
+    y = _r(M, D, seed=61) * 2 + 0.5
+    g, b = _r(D, seed=62) * 0.1 + 1, _r(D, seed=63) * 0.1
+    ds = _r(M, D, seed=64)
+    yd = y.to(dev)
+    s = torch.empty(M, D, device=dev)
+    mean, rstd = torch.empty(D, device=dev), torch.empty(D, device=dev)
+    rm, rv = torch.zeros(D, device=dev), torch.ones(D, device=dev)
+    guard = torch.full((1 << 20,), 7.0, device=dev)  # allocated next: must stay untouched
+    K.bn_swish_fwd(yd, g.to(dev), b.to(dev), s, mean, rstd, rm, rv)
+    dy = torch.empty(M, D, device=dev)
+    dg, db = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
+    sums = torch.empty(2 * D, device=dev)
+    K.bn_swish_bwd(ds.to(dev), yd, mean, rstd, g.to(dev), b.to(dev), dy, dg, db, sums)
+    torch.cuda.synchronize()
+    assert torch.all(guard == 7.0)
+    y64 = y.double().requires_grad_(True)
+    mu = y64.mean(0)
+    var = y64.var(0, unbiased=False)
+    z = (y64 - mu) / torch.sqrt(var + 1e-5) * g.double() + b.double()
+    out = z * torch.sigmoid(z)
+    out.backward(ds.double())
+    assert (s.cpu().double() - out.detach()).abs().max().item() < 1e-4
+    assert (dy.cpu().double() - y64.grad).abs().max().item() < 1e-4 * max(1.0, y64.grad.abs().max().item())
+    assert torch.isfinite(mean).all() and torch.isfinite(rm).all()
