@@ -22,6 +22,11 @@ def read_wav(path: Union[str, Path], normalize: bool = True, dtype=np.int16,
              always_2d: bool = False) -> Tuple[np.ndarray, int]:
     with open(path, "rb") as f:
         blob = f.read()
+    if blob[:4] == b"fLaC":
+        # the SLURP recipe dumps FLAC by default (asr.sh --audio_format flac); no FLAC decoder is
+        # available here (soundfile / libFLAC are absent): dump the corpus as WAV instead
+        raise NotImplementedError(f"{path}: FLAC audio is not supported; re-run the recipe's data dump with "
+                                  "--audio_format wav (asr.sh stage 3) or convert the files to PCM WAV")
     if len(blob) < 12 or blob[:4] != b"RIFF" or blob[8:12] != b"WAVE":
         raise NotImplementedError(f"{path}: not a RIFF/WAVE file (only PCM WAV is supported)")
     pos, fmt, data = 12, None, None

@@ -165,7 +165,7 @@ def test_wav_reader(tmp_path):
     z, _ = read_wav(str(tmp_path / "p24.wav"))
     np.testing.assert_array_equal(z, v / float(1 << 23))
     (tmp_path / "x.flac").write_bytes(b"fLaC" + b"\0" * 40)
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(NotImplementedError, match="audio_format wav"):  # actionable: SLURP dumps FLAC by default
         read_wav(str(tmp_path / "x.flac"))
 
 
