@@ -322,9 +322,11 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
   g.wide = N % 4 == 0 && ldc % 4 == 0 && sc1 % 4 == 0 && sc2 % 4 == 0 && aligned16(C) && (!R || aligned16(R)) &&
            (!aux || aligned16(aux)) && (!pre || aligned16(pre)) && (!bias || aligned16(bias)) &&
            (!work || aligned16(work));
+  g.ragged4 = !g.wide && N % 4 != 0 && ldc % 4 == 0 && sc1 % 4 == 0 && sc2 % 4 == 0 && aligned16(C) &&
+              (!R || aligned16(R)) && !aux && !pre && !bias;
   {
     const char* e = getenv("ESP_GEMM_ABL");
-    if (e && (atoi(e) & 16)) g.wide = 0;
+    if (e && (atoi(e) & 16)) g.wide = g.ragged4 = 0;
   }
   if (drop_p > 0.f) {
     double t = (double)drop_p * 4294967296.0;

@@ -95,6 +95,8 @@ struct GemmArgs {
   float* rowsum;     // != NULL: rowsum[m] += sum_k A(m,k)  (bias gradient of a weight-gradient GEMM)
   float* rs_work;    // split-K partial row sums [split][M]
   int wide;          // float4 epilogue legal (N, ldc, batch strides % 4 == 0, 16-B aligned C/R/aux/pre/bias/work)
+  int ragged4;       // the same except N % 4 != 0 (ldc % 4 == 0 pads every row to whole quads): the
+                     // plain specialised kinds store the last quad of a row element by element
   // output row map (conv2 input gradient, one parity class (ph, pw) of the conv1 output grid):
   // row m = (b, a, e) of the class grid (Ha x We) -> pixel (b, 2a+ph, 2e+pw) of the T1 x F1 map
   int cmap;
@@ -125,7 +127,11 @@ __host__ __device__ inline int epi_kind(const GemmArgs& g) {
 // generic kind; only for wide (float4) epilogues without the conv2 output row map
 __host__ inline int epi_kind_spec(const GemmArgs& g) {
   const int k = epi_kind(g);
-  if (!g.wide || g.cmap) return k;
+  if (g.cmap) return k;
+  if (!g.wide) {
+    if (g.ragged4 && k == EPI_PLAIN && g.splits == 1 && !g.rowsum) return g.r ? EPI_PR : EPI_P0;
+    return k;
+  }
   if (k == EPI_PLAIN) return (g.splits > 1 || g.rowsum) ? k : (g.r ? EPI_PR : EPI_P0);
   if (k == EPI_BWD)
     return (g.bwd_act == ACT_MUL && !g.drop_thresh && !g.r && !g.bias && g.alpha == 1.0f) ? EPI_BMUL : k;
@@ -444,7 +450,13 @@ __device__ __forceinline__ void store_spec(const GemmArgs& g, int z, int mrow0, 
           d[e] = dd;
         }
         if constexpr (S::act != ACT_NONE) st4(g.aux + off, d, false);
-        st4(g.c + off, v, false);
+        if (FULL || n + 4 <= g.N) {
+          st4(g.c + off, v, false);
+        } else {  // last quad of a row with N % 4 != 0 (EPI_P0 / EPI_PR only): loads stayed inside ldc
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (n + e < g.N) g.c[off + e] = v[e];
+        }
       }
     }
   }

@@ -605,3 +605,23 @@ def test_bn_swish_large_rows_and_channels(dev, M, D):
     assert (s.cpu().double() - out.detach()).abs().max().item() < 1e-4
     assert (dy.cpu().double() - y64.grad).abs().max().item() < 1e-4 * max(1.0, y64.grad.abs().max().item())
     assert torch.isfinite(mean).all() and torch.isfinite(rm).all()
+
+
+@pytest.mark.parametrize("with_r", [False, True])
+def test_gemm_ragged_n_padded_rows(dev, with_r):
+    """N % 4 != 0 with a row pitch padded to whole quads (the attention probability layout,
+    T'=374 in rows of 376): the specialised plain epilogue stores the last quad element by
+    element and never touches the padding columns."""
+    Z, M, N, Kd, ld = 6, 374, 374, 64, 376
+    A, B = _r(Z, M, Kd, seed=71), _r(Z, N, Kd, seed=72)
+    C = torch.full((Z, M, ld), 7.5, device=dev)
+    R = _r(Z, M, ld, seed=73).to(dev) if with_r else None
+    R0 = R.clone() if with_r else None
+    K.gemm(M, N, Kd, A.to(dev), B.to(dev), C, lda=Kd, ldb=Kd, ldc=ld, batch=Z, nb2=1, sa=(M * Kd, 0),
+           sb=(N * Kd, 0), sc=(M * ld, 0), R=R, beta=1.0 if with_r else 0.0)
+    ref = A.double() @ B.double().transpose(1, 2)
+    if with_r:
+        ref = ref + R0.cpu().double()[:, :, :N]
+    out = C.cpu()
+    assert (out[:, :, :N].double() - ref).abs().max().item() < 1e-4
+    assert torch.all(out[:, :, N:] == 7.5)
