@@ -426,7 +426,11 @@ __global__ __launch_bounds__(256) void relpos_softmax_fwd_kernel(
 //   3. s = (ac + Sbd[r][j-r+31]) / sqrt(dk), key mask, row max / sum by xor-shuffles inside the
 //      32-lane halves + a 4-wave LDS exchange, p = e/sum -> attn (+ dropout copy pdrop).
 // k rows are read from the fused qkv projection: k[z][j] = kmat[(b*T + j)*ldk + 64*head].
-template <int NTA>  // key tiles per wave: ceil(ceil(T/32)/4) <= 4
+// P2: sqrt(d_k) is a power of two (d_k = 64 in every configuration here), so s / sqrt(d_k) is
+// computed exactly as s * (1 / sqrt(d_k)); exp(s - m) as exp2((s - m) * log2 e) on v_exp_f32
+// (the score assembly and softmax are VALU-bound: ~100 instructions per score element with the
+// IEEE division and the range-reduced expf, SQ_INSTS_VALU in profiles/r02h PMC passes).
+template <int NTA, bool P2>  // key tiles per wave: ceil(ceil(T/32)/4) <= 4
 __global__ __launch_bounds__(256) void relpos_attn_fwd_kernel(
     const float* __restrict__ qu, const float* __restrict__ qv, const float* __restrict__ kmat, long ldk,
     const float* __restrict__ pm, long ldpm, int nb, float sqrt_dk, const int* __restrict__ klen,
@@ -446,6 +450,7 @@ __global__ __launch_bounds__(256) void relpos_attn_fwd_kernel(
   const int kmin = T - RP_ROWS - i0;
   const int nbd = (T + RP_ROWS - 1 + 31) / 32;
   const int nac = (T + 31) / 32;
+  const float inv_sqrt_dk = 1.0f / sqrt_dk;
 
   auto load_row32 = [&](const float* row, float (&f)[2][16]) {  // d = 32c + 16hf + s
 #pragma unroll
@@ -505,7 +510,8 @@ __global__ __launch_bounds__(256) void relpos_attn_fwd_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int il = (r & 3) + 8 * (r >> 2) + 4 * hf;
-        sc[t][r] = (j < kl) ? (acc[r] + sbd[il * WP + j - il + RP_ROWS - 1]) / sqrt_dk : -INFINITY;
+        const float sv = acc[r] + sbd[il * WP + j - il + RP_ROWS - 1];
+        sc[t][r] = (j < kl) ? (P2 ? sv * inv_sqrt_dk : sv / sqrt_dk) : -INFINITY;
       }
     } else {
 #pragma unroll
@@ -539,7 +545,8 @@ __global__ __launch_bounds__(256) void relpos_attn_fwd_kernel(
     float v = 0.f;
 #pragma unroll
     for (int t = 0; t < NTA; ++t) {
-      const float e = sc[t][r] == -INFINITY ? 0.f : expf(sc[t][r] - m[r]);
+      const float e = sc[t][r] == -INFINITY ? 0.f
+                      : (P2 ? __builtin_amdgcn_exp2f((sc[t][r] - m[r]) * 1.4426950408889634f) : expf(sc[t][r] - m[r]));
       sc[t][r] = e;
       v += e;
     }
@@ -711,9 +718,16 @@ ESP_API int esp_relpos_attn_fwd(const float* qu, const float* qv, const float* k
   const int nta = ((T + 31) / 32 + 3) / 4;
   dim3 grid((unsigned)((T + RP_ROWS - 1) / RP_ROWS), (unsigned)(nb * H));
   hipStream_t st = (hipStream_t)stream;
+  const bool p2 = sqrt_dk > 0.f && (__builtin_bit_cast(uint32_t, sqrt_dk) & 0x7fffffu) == 0;
 #define ESP_RA(N)                                                                                                    \
-  hipLaunchKernelGGL(relpos_attn_fwd_kernel<N>, grid, dim3(256), shm, st, qu, qv, kmat, ldk, p, ldp_row, nb, sqrt_dk, \
-                     klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, WP, esp::rng_key_ptr())
+  do {                                                                                                               \
+    if (p2)                                                                                                          \
+      hipLaunchKernelGGL((relpos_attn_fwd_kernel<N, true>), grid, dim3(256), shm, st, qu, qv, kmat, ldk, p, ldp_row,  \
+                         nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, WP, esp::rng_key_ptr());    \
+    else                                                                                                             \
+      hipLaunchKernelGGL((relpos_attn_fwd_kernel<N, false>), grid, dim3(256), shm, st, qu, qv, kmat, ldk, p, ldp_row, \
+                         nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, WP, esp::rng_key_ptr());    \
+  } while (0)
   if (nta <= 1) ESP_RA(1);
   else if (nta == 2) ESP_RA(2);
   else if (nta == 3) ESP_RA(3);
