@@ -370,11 +370,18 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
       // (conv2 weight gradient) leave a third of the chip idle in the last round; take the
       // smallest sp up to 4x the target-derived one whose last round is >= 95 % full.
       if (sp >= 2 && !getenv("ESP_SPLITK_NOBALANCE")) {
+        // score the split count that is actually launched: the chunk is rounded up to BK, so
+        // ceil(K / chunk) can be smaller than the candidate
+        auto launched = [&](long s) {
+          const long chunk = ((K + s - 1) / s + BK - 1) / BK * BK;
+          return (K + chunk - 1) / chunk;
+        };
         auto imb = [&](long s) { const long t = tiles * s; return (double)((t + 255) / 256 * 256) / (double)t; };
         const long hi = std::min(std::min(by_k, cap), std::min<long>(64, 4 * sp));
-        long best = sp;
+        long best = launched(sp);
         for (long s = sp; s <= hi; ++s) {
-          if (imb(s) < imb(best) - 1e-9) best = s;
+          const long e = launched(s);
+          if (imb(e) < imb(best) - 1e-9) best = e;
           if (imb(best) <= 1.05) break;
         }
         sp = best;

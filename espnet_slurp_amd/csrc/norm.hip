@@ -514,17 +514,34 @@ __device__ __forceinline__ double sum_parts16(const double* __restrict__ part, i
   return t;
 }
 
+// fixed-order sum of nb partial rows for 16 columns: 64 groups of 16 lanes (the BatchNorm
+// statistics have up to BN_CHUNKS partial rows per column, so the rows, not the columns, need
+// the parallelism)
+constexpr int BNF_COLS = 16, BNF_GROUPS = 64;
+__device__ __forceinline__ double sum_parts_rows(const double* __restrict__ part, int nb, long stride, int c, bool ok,
+                                                 double (*sh)[BNF_COLS]) {
+  const int cl = threadIdx.x % BNF_COLS, g = threadIdx.x / BNF_COLS;
+  double s = 0.0;
+  if (ok)
+    for (int p = g; p < nb; p += BNF_GROUPS) s += part[(long)p * stride + c];
+  sh[g][cl] = s;
+  __syncthreads();
+  double t = 0.0;
+  for (int k = 0; k < BNF_GROUPS; ++k) t += sh[k][cl];
+  return t;
+}
+
 // finalize: mode 0 -> mean[c] = S/M ; mode 1 -> rstd[c], running stats update
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(const double* __restrict__ part, int nb, int D, int M, int mode,
                                                            float* __restrict__ mean, float* __restrict__ rstd,
                                                            float* __restrict__ run_mean, float* __restrict__ run_var,
                                                            float momentum, float eps, int T,
                                                            const int* __restrict__ tvalid) {
-  __shared__ double sh[16][64];
+  __shared__ double sh[BNF_GROUPS][BNF_COLS];
   if (tvalid) M = (M / T) * valid_T(tvalid, T);  // B * T' rows of the reference batch
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const double s = sum_parts16(part, nb, D, c, c < D, sh);
-  if ((threadIdx.x >> 6) != 0 || c >= D) return;
+  const int c = blockIdx.x * BNF_COLS + threadIdx.x % BNF_COLS;
+  const double s = sum_parts_rows(part, nb, D, c, c < D, sh);
+  if (threadIdx.x / BNF_COLS != 0 || c >= D) return;
   if (mode == 0) {
     mean[c] = (float)(s / M);
   } else {
@@ -583,12 +600,12 @@ __global__ void bn_swish_bwd_part_kernel(const float* __restrict__ ds, const flo
 __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const double* __restrict__ part, int nb, int D,
                                                                float* __restrict__ sums, float* __restrict__ dgamma,
                                                                float* __restrict__ dbeta) {
-  __shared__ double sh[16][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const double s1 = sum_parts16(part, nb, 2L * D, c, c < D, sh);
+  __shared__ double sh[BNF_GROUPS][BNF_COLS];
+  const int c = blockIdx.x * BNF_COLS + threadIdx.x % BNF_COLS;
+  const double s1 = sum_parts_rows(part, nb, 2L * D, c, c < D, sh);
   __syncthreads();
-  const double s2 = sum_parts16(part + D, nb, 2L * D, c, c < D, sh);
-  if ((threadIdx.x >> 6) != 0 || c >= D) return;
+  const double s2 = sum_parts_rows(part + D, nb, 2L * D, c, c < D, sh);
+  if (threadIdx.x / BNF_COLS != 0 || c >= D) return;
   sums[c] = (float)s1;
   sums[D + c] = (float)s2;
   dbeta[c] += (float)s1;
@@ -615,12 +632,16 @@ inline int gridn(long n) {
   return (int)(b > 65536 ? 65536 : (b < 1 ? 1 : b));
 }
 inline int nchunks(int M, int target_rows) { return (M + target_rows - 1) / target_rows; }
-// rows per block so that about 384 blocks share the rows (fills 256 CUs, bounded partials)
+// rows per block so that about 1536 blocks share the rows: each thread walks its channel down
+// the chunk serially, so the statistics passes are latency-bound unless every CU holds several
+// blocks (384 chunks measured 1.2 TB/s on 47872 x 256; the workspace bound is BN_CHUNKS)
+constexpr int BN_CHUNKS = 1536;
 inline int rows_per_block(int M) {
-  int r = (M + 383) / 384;
+  int r = (M + BN_CHUNKS - 1) / BN_CHUNKS;
   return r < 8 ? 8 : r;
 }
 inline dim3 fin_grid(int N) { return dim3((N + 63) / 64); }
+inline dim3 bnf_grid(int D) { return dim3((D + BNF_COLS - 1) / BNF_COLS); }
 
 }  // namespace
 
@@ -730,7 +751,7 @@ ESP_API int esp_dwconv1d_wgrad(const float* dy, const float* x, float* dW, int B
 }
 
 // BatchNorm1d training forward + Swish. mean/rstd (D) outputs; running stats updated when
-// run_mean != NULL.  workspace: >= D*384 doubles (at most 384 row chunks, rows_per_block)
+// run_mean != NULL.  workspace: >= D*1536 doubles (at most BN_CHUNKS row chunks, rows_per_block)
 ESP_API int esp_bn_swish_fwd(const float* y, const float* gamma, const float* beta, float* s, float* mean, float* rstd,
                              float* run_mean, float* run_var, float momentum, float eps, int M, int D, double* work,
                              int T, const int* tvalid, void* stream) {
@@ -740,10 +761,10 @@ ESP_API int esp_bn_swish_fwd(const float* y, const float* gamma, const float* be
   hipStream_t st = (hipStream_t)stream;
   dim3 g1(nb, (D + 255) / 256), gf((D + 255) / 256);
   hipLaunchKernelGGL(bn_part_kernel, g1, dim3(256), 0, st, y, M, D, rpb, nullptr, 0, work, T, tvalid);
-  hipLaunchKernelGGL(bn_finalize_kernel, fin_grid(D), dim3(1024), 0, st, work, nb, D, M, 0, mean, rstd, nullptr,
+  hipLaunchKernelGGL(bn_finalize_kernel, bnf_grid(D), dim3(1024), 0, st, work, nb, D, M, 0, mean, rstd, nullptr,
                      nullptr, momentum, eps, T, tvalid);
   hipLaunchKernelGGL(bn_part_kernel, g1, dim3(256), 0, st, y, M, D, rpb, mean, 1, work, T, tvalid);
-  hipLaunchKernelGGL(bn_finalize_kernel, fin_grid(D), dim3(1024), 0, st, work, nb, D, M, 1, mean, rstd, run_mean,
+  hipLaunchKernelGGL(bn_finalize_kernel, bnf_grid(D), dim3(1024), 0, st, work, nb, D, M, 1, mean, rstd, run_mean,
                      run_var, momentum, eps, T, tvalid);
   hipLaunchKernelGGL(bn_swish_fwd_kernel, dim3(gridn((long)M * D)), dim3(256), 0, st, y, mean, rstd, gamma, beta, s,
                      (long)M * D, D);
@@ -774,7 +795,7 @@ ESP_API int esp_bn_swish_eval(const float* y, const float* gamma, const float* b
 }
 
 // given ds = dL/ds, writes dy (grad wrt BN input) into `dy`; dgamma/dbeta accumulated.
-// workspace: >= 2*D*384 doubles (at most 384 row chunks) + 2*D floats (sums) passed separately
+// workspace: >= 2*D*1536 doubles (at most BN_CHUNKS row chunks) + 2*D floats (sums) passed separately
 ESP_API int esp_bn_swish_bwd(const float* ds, const float* y, const float* mean, const float* rstd, const float* gamma,
                              const float* beta, float* dy, float* dgamma, float* dbeta, int M, int D, double* work,
                              float* sums, int T, const int* tvalid, void* stream) {
@@ -784,7 +805,7 @@ ESP_API int esp_bn_swish_bwd(const float* ds, const float* y, const float* mean,
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(bn_swish_bwd_part_kernel, dim3(nb, (D + 255) / 256), dim3(256), 0, st, ds, y, mean, rstd, gamma,
                      beta, dy, M, D, rpb, work, T, tvalid);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, fin_grid(D), dim3(1024), 0, st, work, nb, D, sums, dgamma, dbeta);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, bnf_grid(D), dim3(1024), 0, st, work, nb, D, sums, dgamma, dbeta);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(gridn((long)M * D)), dim3(256), 0, st, dy, y, mean, rstd, gamma, sums,
                      (long)M * D, D, M, T, tvalid);
   ESP_CHECK_LAUNCH("esp_bn_swish_bwd");

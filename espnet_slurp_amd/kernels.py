@@ -395,9 +395,9 @@ def dwconv1d_wgrad(dy, x, dW, Bn, T, D, K, tvalid=None):
     _native.call("esp_dwconv1d_wgrad", _p(dy), _p(x), _p(dW), Bn, T, D, K, _p(ws), _p(tvalid), _st())
 
 
-# BatchNorm statistics are reduced in at most 384 row chunks (norm.hip rows_per_block): the
+# BatchNorm statistics are reduced in at most 1536 row chunks (norm.hip BN_CHUNKS): the
 # workspace holds D (forward) / 2D (backward) fp64 partials per chunk
-BN_MAX_CHUNKS = 384
+BN_MAX_CHUNKS = 1536
 
 
 def bn_swish_fwd(y, gamma, beta, s, mean, rstd, run_mean, run_var, momentum=0.1, eps=1e-5, T=0, tvalid=None):

@@ -123,8 +123,8 @@ int esp_glu_bwd(const float* u, const float* dg, float* du, long rows, int D, vo
  * first *tvalid exist in the reference batch (length-bucketed HIP graphs).  The depthwise
  * convolution reads frames >= *tvalid as its zero padding and writes 0 there; BatchNorm
  * statistics count B * (*tvalid) rows and the excluded rows get a zero gradient.  With tvalid,
- * M = B * T rows for the BatchNorm calls.  BatchNorm workspaces: D * 384 (forward) and
- * 2 * D * 384 (backward) doubles — the statistics are reduced in at most 384 row chunks. */
+ * M = B * T rows for the BatchNorm calls.  BatchNorm workspaces: D * 1536 (forward) and
+ * 2 * D * 1536 (backward) doubles — the statistics are reduced in at most 1536 row chunks. */
 int esp_dwconv1d(const float* x, const float* W, const float* bias, float* y, int Bn, int T, int D,
                  int K, int flip, const int* tvalid, void* stream);
 int esp_dwconv1d_wgrad(const float* dy, const float* x, float* dW, int Bn, int T, int D, int K,

@@ -98,8 +98,14 @@ def test_gemm_compute_setter(dev):
     K.set_gemm_compute(prev)
 
 
-def _loss_and_grad(dev, use_amp):
-    cfg = small_cfg("latest", D=128, blocks=2, V=64)
+def _loss_and_grad(dev, use_amp, wide=False):
+    if wide:  # the C5 shape (SLURP-entity Conformer: d=512, H=8, FF 2048), two blocks
+        cfg = O.ModelCfg(vocab_size=64, enc=O.EncCfg(output_size=512, attention_heads=8, linear_units=2048,
+                                                     num_blocks=2, rel_pos_type="latest"),
+                         dec=O.DecCfg(attention_heads=8, linear_units=2048, num_blocks=1), ctc_weight=0.3,
+                         lsm_weight=0.1)
+    else:
+        cfg = small_cfg("latest", D=128, blocks=2, V=64)
     model = build_model(cfg, dev, dropout=0.0)
     load_seeded(model, cfg, 5)
     model.train()
@@ -111,9 +117,10 @@ def _loss_and_grad(dev, use_amp):
     return loss.item(), model.flat.grad.detach().double().cpu().clone()
 
 
-def test_bf16_model_step_close_to_fp32(dev):
-    l32, g32 = _loss_and_grad(dev, False)
-    l16, g16 = _loss_and_grad(dev, True)
+@pytest.mark.parametrize("wide", [False, True])
+def test_bf16_model_step_close_to_fp32(dev, wide):
+    l32, g32 = _loss_and_grad(dev, False, wide)
+    l16, g16 = _loss_and_grad(dev, True, wide)
     assert abs(l16 - l32) <= 1e-2 * abs(l32), (l16, l32)
     cos = float((g16 @ g32) / (g16.norm() * g32.norm()))
     assert cos > 0.999, cos

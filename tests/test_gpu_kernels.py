@@ -578,7 +578,7 @@ def test_conv2_dgrad_parity_classes_vs_column_path(dev, T1, F1):
 @pytest.mark.parametrize("M,D", [(11968, 512), (3000, 768), (47872, 256)])
 def test_bn_swish_large_rows_and_channels(dev, M, D):
     """BatchNorm + Swish statistics at the C4 / C5 shapes (B*T' = 32*374 rows, D = 512): the
-    reduction uses up to 384 row chunks of fp64 partials, D (2D) per chunk — the workspace the
+    reduction uses up to 1536 row chunks of fp64 partials, D (2D) per chunk — the workspace the
     wrapper reserves must cover that (a D=512, B=32 undersized workspace once corrupted
     neighbouring allocations).  Forward / backward vs fp64 torch."""
     y = _r(M, D, seed=61) * 2 + 0.5
