@@ -53,13 +53,15 @@ SIGNATURES = {
     "esp_bn_swish_eval": [P, P, P, P, P, P, F, I, I, P, P, P],
     "esp_bn_swish_bwd": [P, P, P, P, P, P, P, P, P, I, I, P, P, I, P, P],
     "esp_heads_split": [P, L, I, I, I, I, I, P, P, P],
+    "esp_heads_split2": [P, L, I, I, I, I, I, P, P, P, P, P],
     "esp_add2d": [P, L, P, L, I, I, P],
     "esp_attn_softmax_fwd": [P, P, I, I, F, P, I, I, P, P, F, U64, I, I, I, L, L, P],
     "esp_attn_softmax_bwd": [P, P, P, F, U64, F, L, I, L, P],
     "esp_relshift_bwd": [P, L, P, L, I, I, I, I, P],
     "esp_relpos_softmax_fwd": [P, P, L, I, I, P, F, P, P, P, F, U64, I, L, P],
     "esp_relpos_attn_fwd": [P, P, P, L, P, L, I, I, F, P, P, P, F, U64, I, L, P],
-    "esp_attn_softmax_bwd_relpos": [P, P, P, P, L, F, U64, F, L, I, L, P],
+    "esp_relpos_attn_probs": [P, P, P, L, P, L, I, I, I, F, P, P, P, F, U64, I, L, P],
+    "esp_attn_softmax_bwd_relpos": [P, P, P, P, L, I, F, U64, F, L, I, L, P],
     "esp_relpos_attn_bwd": [P, L, P, L, P, P, P, L, I, I, F, F, U64, I, L, P],
     "esp_relpos_flash_fwd": [P, P, P, L, P, L, P, L, I, I, I, F, P, P, L, P, F, U64, I, P],
     "esp_relpos_flash_bwd": [P, P, P, L, P, L, P, L, I, I, I, F, P, P, P, L, P, F, U64, I, P, L, P, P, L, P, P, P],
@@ -82,7 +84,7 @@ SIGNATURES = {
 }
 _RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I, "esp_set_gemm_compute": I,
              "esp_get_gemm_compute": I}
-ABI_VERSION = 16  # bumped whenever a signature in include/espnet_mi355.h changes
+ABI_VERSION = 17  # bumped whenever a signature in include/espnet_mi355.h changes
 
 _lib = None
 

@@ -182,8 +182,7 @@ class RelPositionMultiHeadedAttention(nn.Module):
         K.linear_fwd(pos_emb, self.linear_pos.weight, None, p)
         q_u = empty(Z * T * dk, like=x2d)
         q_v = empty(Z * T * dk, like=x2d)
-        K.heads_split(qkv, 3 * D, 0, B, T, H, dk, self.pos_bias_u, q_u)
-        K.heads_split(qkv, 3 * D, 0, B, T, H, dk, self.pos_bias_v, q_v)
+        K.heads_split2(qkv, 3 * D, 0, B, T, H, dk, self.pos_bias_u, q_u, self.pos_bias_v, q_v)
         pa = self.p if training else 0.0
         sa = seeds.next()
         if K.flash_ok(T, dk):
@@ -201,8 +200,12 @@ class RelPositionMultiHeadedAttention(nn.Module):
         Tp, Pp = K.pitch(T), K.pitch(P)  # 16-B aligned score rows
         ac = empty(Z * T * Tp, like=x2d)
         pdrop = empty(Z * T * Tp, like=x2d) if pa > 0 else None
-        if not self.legacy and K.relpos_fused_ok(T, dk):
-            # ac and the bd band on the MFMA inside the softmax kernel: only attn reaches HBM
+        if K.relpos_probs_ok(T, dk) and not K.ATTN_FWD32:
+            # ac and the bd band on the MFMA inside the softmax kernel (latest and legacy
+            # rel_shift): only attn and its dropout copy reach HBM
+            K.relpos_attn_probs(q_u, q_v, qkv, 3 * D, p, D, relpos, B, H, math.sqrt(dk), klen, ac, pdrop, pa, sa, T,
+                                Tp, k_off=D)
+        elif not self.legacy and K.relpos_fused_ok(T, dk):
             K.relpos_attn_fwd(q_u, q_v, qkv, 3 * D, p, D, B, H, math.sqrt(dk), klen, ac, pdrop, pa, sa, T, Tp,
                               k_off=D)
         else:
@@ -256,11 +259,8 @@ class RelPositionMultiHeadedAttention(nn.Module):
                batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * D), sc=(dk, T * 3 * D))
         if fused:
             pass
-        elif not self.legacy:
-            K.attn_softmax_bwd_relpos(c.attn, dS, dS, dbd, Pp, c.pa, c.sa, math.sqrt(dk), Z * T, T, Tp)
-        else:
-            K.attn_softmax_bwd(c.attn, dS, dS, c.pa, c.sa, math.sqrt(dk), Z * T, T, lds=Tp)
-            K.relshift_bwd(dS, dbd, relpos, Z, T, P, lds=Tp, ldp=Pp)
+        else:  # softmax + rel_shift adjoints in one pass (latest and legacy)
+            K.attn_softmax_bwd_relpos(c.attn, dS, dS, dbd, Pp, c.pa, c.sa, math.sqrt(dk), Z * T, T, Tp, relpos=relpos)
         # dq_u = dS k -> dqkv[:, 0:D]
         K.gemm(T, dk, T, dS, c.qkv, dqkv, mode_a=K.KC, lda=Tp, mode_b=K.RC, ldb=3 * D, ldc=3 * D, b_off=D,
                batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * 3 * D), sc=(dk, T * 3 * D))

@@ -34,6 +34,26 @@ __global__ void heads_split_kernel(const float* __restrict__ src, long ld, int c
   }
 }
 
+// q + pos_bias_u AND q + pos_bias_v in one pass (one read of q, two head-major writes), a float4
+// per thread: thread (row = b*T + t, head h, quad d4) of the (B*T, H*dk) source block.
+__global__ void heads_split2_kernel(const float* __restrict__ src, long ld, int col0, int B, int T, int H, int dk,
+                                    const float* __restrict__ bias_a, float* __restrict__ dst_a,
+                                    const float* __restrict__ bias_b, float* __restrict__ dst_b) {
+  const int q4n = dk >> 2, perrow = H * q4n;
+  const long n = (long)B * T * perrow;
+  for (long g = blockIdx.x * (long)blockDim.x + threadIdx.x; g < n; g += (long)gridDim.x * blockDim.x) {
+    const int row = (int)(g / perrow), rem = (int)(g - (long)row * perrow);
+    const int h = rem / q4n, d = 4 * (rem - h * q4n);
+    const int b = row / T, t = row - b * T;
+    const float4 v = *reinterpret_cast<const float4*>(src + (long)row * ld + col0 + h * dk + d);
+    const float4 ua = *reinterpret_cast<const float4*>(bias_a + h * dk + d);
+    const float4 ub = *reinterpret_cast<const float4*>(bias_b + h * dk + d);
+    const long o = (((long)h * B + b) * T + t) * dk + d;
+    *reinterpret_cast<float4*>(dst_a + o) = make_float4(v.x + ua.x, v.y + ua.y, v.z + ua.z, v.w + ua.w);
+    *reinterpret_cast<float4*>(dst_b + o) = make_float4(v.x + ub.x, v.y + ub.y, v.z + ub.z, v.w + ub.w);
+  }
+}
+
 // y[r*ldy + c] += x[r*ldx + c]
 __global__ void add2d_kernel(const float* __restrict__ x, long ldx, float* __restrict__ y, long ldy, int M, int N) {
   const long n = (long)M * N;
@@ -139,10 +159,14 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(const float* __restric
   }
 }
 
-// softmax backward fused with the latest rel_shift adjoint: the wave that owns score row
-// (z, i) writes dS[i][j] and the whole dbd row  dbd[i][k] = dS[i][k - (T-1-i)]  (0 outside the
-// band), so dS is not re-read by a separate relshift pass.  dS may alias dP.
-template <int PER>
+// softmax backward fused with the rel_shift adjoint, so dS is not re-read by a separate relshift
+// pass.  dS may alias dP.  The wave that owns score row (z, i) writes dS[i][j] and
+//   latest (REL 1): the whole dbd row  dbd[i][k] = dS[i][k - (T-1-i)]  (0 outside the band);
+//   legacy (REL 2): dbd[i][j + T-1-i] = dS[i][j] for j <= i (the upper part of row i) and
+//                   dbd[i+1][j - i - 2] = dS[i][j] for j >= i+2 (the lower part of row i+1);
+//                   row 0's lower part has no source and is zeroed by row 0's wave.
+// Each dbd element has exactly one source (relshift_bwd_kernel's gather), so no atomics.
+template <int PER, int REL>
 __global__ __launch_bounds__(256) void softmax_bwd_relpos_kernel(const float* __restrict__ attn, const float* dP,
                                                                  float* dS, float* __restrict__ dbd, long ldp,
                                                                  uint32_t thr, float dscale, uint64_t seed,
@@ -180,11 +204,16 @@ __global__ __launch_bounds__(256) void softmax_bwd_relpos_kernel(const float* __
     if (j < T) {
       const float v = a[e] * (g[e] - dot) / sqrt_dk;
       sr[j] = v;
-      br[j + sh] = v;
+      if (REL == 1 || j <= i) br[j + sh] = v;
+      else if (j >= i + 2) br[ldp + j - i - 2] = v;  // row i+1 of the same z (i + 1 < T here)
     }
   }
-  for (int k = lane; k < sh; k += 64) br[k] = 0.f;
-  for (int k = sh + T + lane; k < 2 * T - 1; k += 64) br[k] = 0.f;
+  if (REL == 1) {
+    for (int k = lane; k < sh; k += 64) br[k] = 0.f;
+    for (int k = sh + T + lane; k < 2 * T - 1; k += 64) br[k] = 0.f;
+  } else if (i == 0) {
+    for (int k = lane; k < sh; k += 64) br[k] = 0.f;
+  }
 }
 
 // Fused latest rel-pos attention backward, one block per (32 query rows, z):
@@ -581,6 +610,198 @@ __global__ __launch_bounds__(256) void relpos_attn_fwd_kernel(
   }
 }
 
+// ---------------------------------------------------------------- rel-pos attention probabilities, one wave per 16 rows
+// Same result as relpos_attn_fwd_kernel, restructured so that no block-level synchronisation
+// serialises the phases: each wave owns (z, 16 query rows) and walks the key tiles of 16 with
+// v_mfma_f32_16x16x4_f32, holding its full score rows in registers (4 per tile per lane).
+// Per key tile t:
+//   ac(t)    = q_u[i0..i0+15] . k[16t..16t+15]                         (16 MFMAs, registers)
+//   band(t+1)= q_v[i0..i0+15] . p[kb0+16(t+1) .. +15]                   (16 MFMAs, interleaved)
+//   the band block goes to a per-wave 32-position LDS ring; the rel_shift read of tile t,
+//   bd_shift[ii][jj] = band[ii][jj - ii + 15] (offset from block t), touches blocks t and t+1.
+// The next tile's k / p fragments are fetched one tile ahead (64 B contiguous per lane, k order
+// permuted identically in both operands: lane quarter q supplies d = 16q + c at step c).
+// Legacy rel_shift (attention.py:145-165): j <= i reads band rows q_v[i]; j == i+1 is 0;
+// j >= i+2 reads q_v[i+1] . p[j-i-2].  In table positions k = j + T-1-i the first case is k < T,
+// the last k > T with p at k - T - 1, and band block m covers T-16-16g+16m + [0,16) (g = i0/16):
+// blocks m <= g lie wholly below T (A rows q_v[i]), blocks m >= g+1 wholly at or above T (A rows
+// q_v[i+1], the shifted twin), so legacy selects the A operand per block and shares the ring.
+// LDS: ring rows of RW_PITCH floats (row groups r and r+4 of a 32-lane half 16 banks apart).
+constexpr int RW_ROWS = 16, RW_PITCH = 37;
+constexpr int RW_SPITCH = 68;  // store-transpose rows: the two row groups of a ds_write_b32 half 16 banks apart
+template <int NTA, bool P2, bool LEGACY>  // NTA >= ceil(T/16) key tiles held in registers
+__global__ __launch_bounds__(256, 2) void relpos_attn_fwd16_kernel(
+    const float* __restrict__ qu, const float* __restrict__ qv, const float* __restrict__ kmat, long ldk,
+    const float* __restrict__ pm, long ldpm, int nb, float sqrt_dk, const int* __restrict__ klen,
+    float* __restrict__ attn, float* __restrict__ pdrop, uint32_t thr, float dscale, uint64_t seed, int T, long lds,
+    const uint64_t* __restrict__ key) {
+  __shared__ float ring[4][RW_ROWS * RW_PITCH];
+  __shared__ __attribute__((aligned(16))) float stage[4][RW_ROWS * RW_SPITCH];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int z = blockIdx.y;
+  const int i0 = (blockIdx.x * 4 + wave) * RW_ROWS;
+  if (i0 >= T) return;  // the whole wave: nothing below synchronises the block
+  seed = esp::keyed(seed, key);
+  const int head = z / nb, b = z - head * nb;
+  const int li = lane & 15, q4 = lane >> 4;
+  const int nt = (T + 15) >> 4;
+  const int g = i0 >> 4;
+  const int kb0 = T - RW_ROWS - i0;  // table position of band block 0, column 0
+  const int P = LEGACY ? T : 2 * T - 1;
+  const float inv_sqrt_dk = 1.0f / sqrt_dk;
+  float* ring0 = ring[wave];
+
+  auto ld16 = [&](const float* row, float (&f)[16]) {
+    const float4* r4 = reinterpret_cast<const float4*>(row + 16 * q4);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float4 v = r4[u];
+      f[4 * u] = v.x; f[4 * u + 1] = v.y; f[4 * u + 2] = v.z; f[4 * u + 3] = v.w;
+    }
+  };
+  auto k_row = [&](int t) { return kmat + ((long)b * T + min(t * 16 + li, T - 1)) * ldk + head * RP_DK; };
+  auto p_row = [&](int m) {
+    int pos = kb0 + 16 * m + li;
+    if (LEGACY && pos > T) pos -= T + 1;  // the shifted band's table: p[j - i - 2]
+    return pm + (long)min(max(pos, 0), P - 1) * ldpm + head * RP_DK;
+  };
+  float au[16], av[16], av2[16];
+  ld16(qu + ((long)z * T + min(i0 + li, T - 1)) * RP_DK, au);
+  ld16(qv + ((long)z * T + min(i0 + li, T - 1)) * RP_DK, av);
+  if (LEGACY) ld16(qv + ((long)z * T + min(i0 + 1 + li, T - 1)) * RP_DK, av2);
+  int kl = klen ? klen[b] : T;
+  if (kl > T) kl = T;
+
+  auto put_band = [&](float* rg, int m, const f32x4& s) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rg[(4 * q4 + r) * RW_PITCH + ((16 * m + li) & 31)] = s[r];
+  };
+  // fragments DEPTH tiles ahead: K(t) in kb[t % NB], band-block p rows P(m) in pb[m % NB]
+  constexpr int DEPTH = 2, NB = DEPTH + 1;
+  float kb[NB][16], pb[NB][16];
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d) ld16(k_row(d), kb[d]);
+#pragma unroll
+  for (int d = 0; d <= DEPTH; ++d) ld16(p_row(d), pb[d]);
+  {  // band block 0 (below T for every g: A rows q_v[i] in both variants)
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 16; ++c) s = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c], pb[0][c], s, 0, 0, 0);
+    put_band(ring0, 0, s);
+  }
+
+  f32x4 sc[NTA];
+#pragma unroll
+  for (int t = 0; t < NTA; ++t) {
+    // no `t < nt` branch: tiles past the last key are computed on clamped rows and masked
+    // (j >= T > kl), which keeps every s_waitcnt vmcnt counted across the whole unrolled loop
+    // (a conditional tile makes the compiler merge its counts pessimistically: vmcnt(4) at every
+    // tile, i.e. the prefetched fragments waited for one tile early)
+    {
+      const float(&kf)[16] = kb[t % NB];
+      const float(&pf)[16] = pb[(t + 1) % NB];
+      const bool shifted = LEGACY && t + 1 > g;  // legacy band block t+1 at/above table position T
+      f32x4 a = {0.f, 0.f, 0.f, 0.f}, s = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        a = __builtin_amdgcn_mfma_f32_16x16x4f32(au[c], kf[c], a, 0, 0, 0);
+        s = __builtin_amdgcn_mfma_f32_16x16x4f32(shifted ? av2[c] : av[c], pf[c], s, 0, 0, 0);
+      }
+      ld16(k_row(t + DEPTH), kb[(t + DEPTH) % NB]);  // clamped rows: always safe to fetch
+      ld16(p_row(t + 1 + DEPTH), pb[(t + 1 + DEPTH) % NB]);
+      put_band(ring0, t + 1, s);
+      asm volatile("" ::: "memory");  // ring writes before the shifted reads (LDS is in order per wave)
+      const int j = t * 16 + li;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ii = 4 * q4 + r, i = i0 + ii;
+        const int at = ii * RW_PITCH + ((t * 16 + li - ii + 15) & 31);
+        float bd = ring0[at];
+        if (LEGACY && j == i + 1) bd = 0.f;
+        const float sv = a[r] + bd;
+        sc[t][r] = j < kl ? (P2 ? sv * inv_sqrt_dk : sv / sqrt_dk) : -INFINITY;
+      }
+      asm volatile("" ::: "memory");  // ... and these reads before the next tile's ring writes
+    }
+  }
+
+  // softmax over each row: a row's keys sit in the 16 lanes of one quarter x NTA tiles
+  float m[4], inv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float v = sc[0][r];
+#pragma unroll
+    for (int t = 1; t < NTA; ++t) v = fmaxf(v, sc[t][r]);
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    m[r] = v;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float v = 0.f;
+#pragma unroll
+    for (int t = 0; t < NTA; ++t) {
+      const float x = sc[t][r];
+      const float e = x == -INFINITY ? 0.f
+                      : (P2 ? __builtin_amdgcn_exp2f((x - m[r]) * 1.4426950408889634f) : expf(x - m[r]));
+      sc[t][r] = e;
+      v += e;
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+    inv[r] = v > 0.f ? 1.0f / v : 0.f;
+  }
+  // probabilities -> HBM through a per-wave LDS transpose, 64 columns (4 key tiles) at a time:
+  // lane L then holds 4 consecutive columns of row 4p + (L >> 4), so one store instruction writes
+  // 4 rows x 256 contiguous bytes (instead of 4 rows x 64 B from the accumulator layout)
+  float* stg = stage[wave];
+  const int sr = lane >> 4, sc4 = 4 * (lane & 15);
+  long rowo[4];
+  bool rok[4];
+#pragma unroll
+  for (int ps = 0; ps < 4; ++ps) {
+    const int i = i0 + 4 * ps + sr;
+    rok[ps] = i < T;
+    rowo[ps] = (long)z * T + min(i, T - 1);
+  }
+#pragma unroll
+  for (int t4 = 0; t4 < NTA; t4 += 4) {
+    if (16 * t4 >= T) break;
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) stg[(4 * q4 + r) * RW_SPITCH + 16 * tt + li] = sc[t4 + tt][r] * inv[r];
+    asm volatile("" ::: "memory");
+    const int j = 16 * t4 + sc4;
+#pragma unroll
+    for (int ps = 0; ps < 4; ++ps) {
+      const float4 v = *reinterpret_cast<const float4*>(stg + (4 * ps + sr) * RW_SPITCH + sc4);
+      if (!rok[ps] || j >= T) continue;
+      float* ar = attn + rowo[ps] * lds + j;
+      float4 d = v;
+      if (pdrop) {
+        const uint64_t ix = (uint64_t)(rowo[ps] * T + j);
+        d.x = esp::keep_elem(seed, ix, thr) ? v.x * dscale : 0.f;
+        d.y = esp::keep_elem(seed, ix + 1, thr) ? v.y * dscale : 0.f;
+        d.z = esp::keep_elem(seed, ix + 2, thr) ? v.z * dscale : 0.f;
+        d.w = esp::keep_elem(seed, ix + 3, thr) ? v.w * dscale : 0.f;
+      }
+      float* dr = pdrop ? pdrop + rowo[ps] * lds + j : nullptr;
+      if (j + 4 <= T) {
+        *reinterpret_cast<float4*>(ar) = v;
+        if (pdrop) *reinterpret_cast<float4*>(dr) = d;
+      } else {
+        const float vv[4] = {v.x, v.y, v.z, v.w}, dd[4] = {d.x, d.y, d.z, d.w};
+        for (int e = 0; e < T - j; ++e) {
+          ar[e] = vv[e];
+          if (pdrop) dr[e] = dd[e];
+        }
+      }
+    }
+    asm volatile("" ::: "memory");  // the reads above before the next chunk's writes
+  }
+}
+
 inline int gridn(long n) {
   long b = (n + 255) / 256;
   return (int)(b > 65536 ? 65536 : (b < 1 ? 1 : b));
@@ -599,6 +820,18 @@ ESP_API int esp_heads_split(const float* src, long ld, int col0, int B, int T, i
   hipLaunchKernelGGL(heads_split_kernel, dim3(gridn((long)H * B * T * dk)), dim3(256), 0, (hipStream_t)stream, src, ld,
                      col0, B, T, H, dk, bias, dst);
   ESP_CHECK_LAUNCH("esp_heads_split");
+  return 0;
+}
+
+ESP_API int esp_heads_split2(const float* src, long ld, int col0, int B, int T, int H, int dk, const float* bias_a,
+                             float* dst_a, const float* bias_b, float* dst_b, void* stream) {
+  ESP_ARG_CHECK(dk % 4 == 0 && ld % 4 == 0 && col0 % 4 == 0 && ((uintptr_t)src & 15) == 0 &&
+                    ((uintptr_t)dst_a & 15) == 0 && ((uintptr_t)dst_b & 15) == 0 && ((uintptr_t)bias_a & 15) == 0 &&
+                    ((uintptr_t)bias_b & 15) == 0,
+                "esp_heads_split2: 16-B aligned operands with dk, ld, col0 multiples of 4 required");
+  hipLaunchKernelGGL(heads_split2_kernel, dim3(gridn((long)H * B * T * dk / 4)), dim3(256), 0, (hipStream_t)stream,
+                     src, ld, col0, B, T, H, dk, bias_a, dst_a, bias_b, dst_b);
+  ESP_CHECK_LAUNCH("esp_heads_split2");
   return 0;
 }
 
@@ -737,18 +970,71 @@ ESP_API int esp_relpos_attn_fwd(const float* qu, const float* qv, const float* k
   return 0;
 }
 
+// Rel-pos attention probabilities, latest (relpos 1, P = 2T-1 table rows) or legacy (relpos 2,
+// P = T rows), one wave per 16 query rows (relpos_attn_fwd16_kernel).  T <= 512.
+ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float* kmat, long ldk, const float* p,
+                                  long ldp_row, int relpos, int nb, int H, float sqrt_dk, const int* klen,
+                                  float* attn, float* pdrop, float drop_p, unsigned long long seed, int T, long lds,
+                                  void* stream) {
+  ESP_ARG_CHECK(T >= 1 && T <= 512 && lds >= T && nb >= 1 && H >= 1, "esp_relpos_attn_probs: bad sizes T=%d", T);
+  ESP_ARG_CHECK(relpos == 1 || relpos == 2, "esp_relpos_attn_probs: relpos must be 1 (latest) or 2 (legacy)");
+  ESP_ARG_CHECK(ldp_row % 4 == 0 && ldk % 4 == 0 && ((uintptr_t)p & 15) == 0 && ((uintptr_t)qv & 15) == 0 &&
+                    ((uintptr_t)qu & 15) == 0 && ((uintptr_t)kmat & 15) == 0,
+                "esp_relpos_attn_probs: operands must be 16-B aligned with ld %% 4 == 0");
+  const uint32_t thr = drop_threshold(drop_p);
+  if (!thr) pdrop = nullptr;
+  const float ds = thr ? 1.f / (1.f - drop_p) : 1.f;
+  const int nt = (T + 15) / 16;
+  dim3 grid((unsigned)((T + 4 * RW_ROWS - 1) / (4 * RW_ROWS)), (unsigned)(nb * H));
+  hipStream_t st = (hipStream_t)stream;
+  const bool p2 = sqrt_dk > 0.f && (__builtin_bit_cast(uint32_t, sqrt_dk) & 0x7fffffu) == 0;
+#define ESP_RW3(N, P2_, L_)                                                                                         \
+  hipLaunchKernelGGL((relpos_attn_fwd16_kernel<N, P2_, L_>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p, ldp_row, \
+                     nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr())
+#define ESP_RW(N)                             \
+  do {                                        \
+    if (relpos == 2) {                        \
+      if (p2) ESP_RW3(N, true, true);         \
+      else ESP_RW3(N, false, true);           \
+    } else {                                  \
+      if (p2) ESP_RW3(N, true, false);        \
+      else ESP_RW3(N, false, false);          \
+    }                                         \
+  } while (0)
+  if (nt <= 4) ESP_RW(4);
+  else if (nt <= 8) ESP_RW(8);
+  else if (nt <= 12) ESP_RW(12);
+  else if (nt <= 16) ESP_RW(16);
+  else if (nt <= 20) ESP_RW(20);
+  else if (nt <= 24) ESP_RW(24);
+  else if (nt <= 28) ESP_RW(28);
+  else ESP_RW(32);
+#undef ESP_RW
+#undef ESP_RW3
+  ESP_CHECK_LAUNCH("esp_relpos_attn_probs");
+  return 0;
+}
+
 // softmax backward + latest rel_shift adjoint in one pass (see softmax_bwd_relpos_kernel)
 ESP_API int esp_attn_softmax_bwd_relpos(const float* attn, const float* dP, float* dS, float* dbd, long ldp,
-                                        float drop_p, unsigned long long seed, float sqrt_dk, long rows, int T,
-                                        long lds, void* stream) {
-  ESP_ARG_CHECK(T >= 1 && T <= 1024 && lds >= T && ldp >= 2 * T - 1, "esp_attn_softmax_bwd_relpos: bad sizes");
+                                        int relpos, float drop_p, unsigned long long seed, float sqrt_dk, long rows,
+                                        int T, long lds, void* stream) {
+  ESP_ARG_CHECK(relpos == 1 || relpos == 2, "esp_attn_softmax_bwd_relpos: relpos must be 1 or 2");
+  ESP_ARG_CHECK(T >= 1 && T <= 1024 && lds >= T && ldp >= (relpos == 1 ? 2 * T - 1 : T) && rows % T == 0,
+                "esp_attn_softmax_bwd_relpos: bad sizes");
   const uint32_t thr = drop_threshold(drop_p);
   const float ds = thr ? 1.f / (1.f - drop_p) : 1.f;
   dim3 grid((unsigned)((rows + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
-#define ESP_SBR(PER)                                                                                          \
-  hipLaunchKernelGGL(softmax_bwd_relpos_kernel<PER>, grid, dim3(256), 0, st, attn, dP, dS, dbd, ldp, thr, ds, \
-                     (uint64_t)seed, sqrt_dk, rows, T, lds, esp::rng_key_ptr())
+#define ESP_SBR(PER)                                                                                         \
+  do {                                                                                                       \
+    if (relpos == 1)                                                                                         \
+      hipLaunchKernelGGL((softmax_bwd_relpos_kernel<PER, 1>), grid, dim3(256), 0, st, attn, dP, dS, dbd, ldp, \
+                         thr, ds, (uint64_t)seed, sqrt_dk, rows, T, lds, esp::rng_key_ptr());                \
+    else                                                                                                     \
+      hipLaunchKernelGGL((softmax_bwd_relpos_kernel<PER, 2>), grid, dim3(256), 0, st, attn, dP, dS, dbd, ldp, \
+                         thr, ds, (uint64_t)seed, sqrt_dk, rows, T, lds, esp::rng_key_ptr());                \
+  } while (0)
   if (T <= 64) ESP_SBR(1);
   else if (T <= 128) ESP_SBR(2);
   else if (T <= 256) ESP_SBR(4);

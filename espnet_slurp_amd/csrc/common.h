@@ -17,11 +17,14 @@ namespace esp {
 void set_error(const char* fmt, ...);
 
 // ---------------------------------------------------------------- counter RNG
-// Counter hash (seed, index) -> 32 random bits, 32-bit arithmetic only (4 v_mul_lo_u32 per
-// element instead of splitmix64's 64-bit multiplies: dropout masks are generated inside MFMA
-// epilogues and softmax passes, where the hash is the dominant VALU cost).  Two rounds of
-// Wellons' lowbias32 finaliser, the seed's halves injected before each.  Stateless, so the
-// backward pass regenerates the forward dropout mask from the same (seed, index).
+// Counter hash (seed, index) -> 32 random bits, 32-bit arithmetic only: one round of Wellons'
+// lowbias32 finaliser (2 v_mul_lo_u32, quarter-rate on CDNA) over the index with the seed's
+// halves injected (xor low, add high) and the index's high word folded in by a rotate.  Dropout
+// masks are generated inside MFMA epilogues and softmax passes, where the hash is the dominant
+// VALU cost (round 1 used two rounds + a multiply for the high word: 5 v_mul_lo_u32 per
+// element; the fused attention kernel spent ~100 us of 410 per layer on it at C2).  A bijection
+// of the low index word for a fixed seed.  Stateless, so the backward pass regenerates the
+// forward dropout mask from the same (seed, index).
 __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7feb352du;
@@ -31,9 +34,9 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   return x;
 }
 __device__ __forceinline__ uint32_t rng_u32(uint64_t seed, uint64_t idx) {
-  uint32_t x = (uint32_t)idx + 0x9E3779B9u * (uint32_t)(idx >> 32);
-  x = mix32(x ^ (uint32_t)seed);
-  return mix32(x + (uint32_t)(seed >> 32));
+  const uint32_t hi = (uint32_t)(idx >> 32);
+  const uint32_t x = ((uint32_t)idx ^ (uint32_t)seed ^ ((hi << 16) | (hi >> 16))) + (uint32_t)(seed >> 32);
+  return mix32(x);
 }
 // Optional device-resident dropout key (esp_set_rng_key): every dropout kernel XORs its seed
 // with *key, so a captured HIP graph draws fresh masks on every replay (the key is advanced

@@ -426,6 +426,12 @@ def heads_split(src, ld, col0, B, T, H, dk, bias, dst):
     _native.call("esp_heads_split", _p(src), ld, col0, B, T, H, dk, _p(bias), _p(dst), _st())
 
 
+def heads_split2(src, ld, col0, B, T, H, dk, bias_a, dst_a, bias_b, dst_b):
+    """dst_a = head-major(src) + bias_a and dst_b = head-major(src) + bias_b in one pass."""
+    _native.call("esp_heads_split2", _p(src), ld, col0, B, T, H, dk, _p(bias_a), _p(dst_a), _p(bias_b), _p(dst_b),
+                 _st())
+
+
 def add2d(x, ldx, y, ldy, M, N, x_off=0, y_off=0):
     _native.call("esp_add2d", _p(x, x_off), ldx, _p(y, y_off), ldy, M, N, _st())
 
@@ -458,6 +464,21 @@ def relpos_attn_fwd(q_u, q_v, kmat, ldk, p, ldp_row, nb, H, sqrt_dk, klen_i32, a
                  _st())
 
 
+def relpos_attn_probs(q_u, q_v, kmat, ldk, p, ldp_row, relpos, nb, H, sqrt_dk, klen_i32, attn, pdrop, drop_p, seed,
+                      T, lds, k_off=0):
+    """Rel-pos attention probabilities, latest (relpos 1) or legacy (relpos 2), one wave per 16
+    query rows (esp_relpos_attn_probs)."""
+    _f32(q_u, q_v, kmat, p, attn, pdrop)
+    _native.call("esp_relpos_attn_probs", _p(q_u), _p(q_v), _p(kmat, k_off), ldk, _p(p), ldp_row, int(relpos), nb, H,
+                 float(sqrt_dk), _p(klen_i32), _p(attn), _p(pdrop), float(drop_p), int(seed) & (2 ** 64 - 1), T, lds,
+                 _st())
+
+
+def relpos_probs_ok(T: int, dk: int) -> bool:
+    """Whether esp_relpos_attn_probs covers this shape (d_k 64, T <= 512)."""
+    return dk == 64 and T <= 512
+
+
 def relpos_fused_ok(T: int, dk: int) -> bool:
     """Whether esp_relpos_softmax_fwd covers this shape (d_k 64, 32-row window in 64 KB LDS)."""
     return dk == 64 and (32 * (32 * ((T + 62) // 32) + 4) + 256) * 4 <= 65536
@@ -468,13 +489,17 @@ def attn_softmax_bwd(attn, dP, dS, drop_p, seed, sqrt_dk, rows, Tk, lds=None):
                  lds or Tk, _st())
 
 
-def attn_softmax_bwd_relpos(attn, dP, dS, dbd, ldp, drop_p, seed, sqrt_dk, rows, T, lds):
-    """Softmax backward fused with the latest rel_shift adjoint (writes dS and dbd)."""
-    _native.call("esp_attn_softmax_bwd_relpos", _p(attn), _p(dP), _p(dS), _p(dbd), ldp, float(drop_p), seed,
-                 float(sqrt_dk), rows, T, lds, _st())
+def attn_softmax_bwd_relpos(attn, dP, dS, dbd, ldp, drop_p, seed, sqrt_dk, rows, T, lds, relpos=1):
+    """Softmax backward fused with the latest (relpos 1) or legacy (relpos 2) rel_shift adjoint
+    (writes dS and dbd)."""
+    _native.call("esp_attn_softmax_bwd_relpos", _p(attn), _p(dP), _p(dS), _p(dbd), ldp, int(relpos), float(drop_p),
+                 seed, float(sqrt_dk), rows, T, lds, _st())
 
 
 FUSED_ATTN_BWD = os.environ.get("ESP_FUSED_ATTN_BWD", "0") == "1"
+# ESP_ATTN_FWD32=1: the 32-row-block fused forward (relpos_attn_fwd_kernel, latest only) instead of
+# the 16-row-wave kernel (esp_relpos_attn_probs); kept for A/B measurements
+ATTN_FWD32 = os.environ.get("ESP_ATTN_FWD32", "0") == "1"
 
 
 def relpos_attn_bwd(dctx, ldd, vmat, ldv, attn, dS, dbd, ldp, nb, H, sqrt_dk, drop_p, seed, T, lds, v_off=0):

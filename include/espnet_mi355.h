@@ -142,6 +142,10 @@ int esp_bn_swish_bwd(const float* ds, const float* y, const float* mean, const f
 /* ---- attention glue (attention.py:64-96,145-165,240-263) */
 int esp_heads_split(const float* src, long ld, int col0, int B, int T, int H, int dk,
                     const float* bias, float* dst, void* stream);
+/* both head-major splits of esp_heads_split in one pass: dst_a = q + bias_a, dst_b = q + bias_b
+ * (q + pos_bias_u, q + pos_bias_v; attention.py:240-250).  16-B aligned, dk, ld, col0 % 4 == 0. */
+int esp_heads_split2(const float* src, long ld, int col0, int B, int T, int H, int dk, const float* bias_a,
+                     float* dst_a, const float* bias_b, float* dst_b, void* stream);
 int esp_add2d(const float* x, long ldx, float* y, long ldy, int M, int N, void* stream);
 /* score rows (ac / attn / pdrop / dP / dS) have pitch lds >= Tk, bd / dbd rows pitch ldp >= P
  * (multiples of 4 keep every row 16-B aligned for the GEMMs' LDS-DMA staging); dropout
@@ -155,11 +159,12 @@ int esp_attn_softmax_bwd(const float* attn, const float* dP, float* dS, float dr
                          void* stream);
 int esp_relshift_bwd(const float* dS, long lds, float* dbd, long ldp, int relpos, int Z, int T, int P,
                      void* stream);
-/* esp_attn_softmax_bwd fused with the latest (relpos 1) esp_relshift_bwd: writes dS and the
- * full dbd rows (P = 2T-1 columns, pitch ldp) in one pass. */
+/* esp_attn_softmax_bwd fused with esp_relshift_bwd (relpos 1 latest: P = 2T-1 columns; relpos 2
+ * legacy: P = T columns): writes dS and every dbd element of the rows (pitch ldp) in one pass.
+ * rows = Z*T. */
 int esp_attn_softmax_bwd_relpos(const float* attn, const float* dP, float* dS, float* dbd, long ldp,
-                                float drop_p, unsigned long long seed, float sqrt_dk, long rows,
-                                int T, long lds, void* stream);
+                                int relpos, float drop_p, unsigned long long seed, float sqrt_dk,
+                                long rows, int T, long lds, void* stream);
 /* Fused latest rel-pos attention backward: dP = dctx V^T on the MFMA per 32-row block, attention
  * dropout adjoint, softmax adjoint, rel_shift adjoint -> dS (pitch lds) and dbd (pitch ldp).
  * dctx rows at dctx + (b*T+i)*ldd + 64h, V rows at vmat + (b*T+j)*ldv + 64h; d_k = 64, T <= 512. */
@@ -212,6 +217,17 @@ int esp_relpos_attn_fwd(const float* qu, const float* qv, const float* kmat, lon
                         long ldp_row, int nb, int H, float sqrt_dk, const int* klen, float* attn,
                         float* pdrop, float drop_p, unsigned long long seed, int T, long lds,
                         void* stream);
+/* Rel-pos attention probabilities for latest (relpos 1: p has P = 2T-1 rows) AND legacy
+ * (relpos 2: p has P = T rows, legacy rel_shift attention.py:145-165) rel_shift, one wave per
+ * 16 query rows with every score row in registers (no block synchronisation): ac and the bd band
+ * on v_mfma_f32_16x16x4_f32, rel_shift through a per-wave LDS ring, key mask, softmax, dropout
+ * copy.  Operands as esp_relpos_attn_fwd; d_k = 64, T <= 512.  Replaces, for these shapes, the
+ * reference's matrix_ac / matrix_bd matmuls + rel_shift + softmax + dropout
+ * (attention.py:240-263, 64-96). */
+int esp_relpos_attn_probs(const float* qu, const float* qv, const float* kmat, long ldk, const float* p,
+                          long ldp_row, int relpos, int nb, int H, float sqrt_dk, const int* klen,
+                          float* attn, float* pdrop, float drop_p, unsigned long long seed, int T,
+                          long lds, void* stream);
 
 /* ---- feature front end: DefaultFrontend + GlobalMVN
  * esp_fbank_fwd: STFT (center, reflect, window of length n_fft, onesided) -> power -> mel

@@ -63,19 +63,24 @@ def test_relpos_mha_block(dev, legacy):
     _check_grads(mod, P, "a")
 
 
-@pytest.mark.parametrize("fused_bwd", [False, True])
+@pytest.mark.parametrize("fwd,legacy,fused_bwd", [("wave16", False, False), ("wave16", True, False),
+                                                   ("wave16", False, True), ("block32", False, False),
+                                                   ("block32", False, True)])
 @pytest.mark.parametrize("T,klens", [(29, [29, 23, 15]), (77, [77, 40, 9]), (130, [130, 129, 64])])
-def test_relpos_mha_fused_dk64(dev, T, klens, fused_bwd, monkeypatch):
-    """d_k = 64 latest rel-pos: the fused bd-window + softmax kernel (esp_relpos_softmax_fwd),
-    several 32-row blocks incl. a partial last block, against the fp64 oracle."""
+def test_relpos_mha_fused_dk64(dev, T, klens, fwd, legacy, fused_bwd, monkeypatch):
+    """d_k = 64 rel-pos attention through the fused score kernels — the 16-row-wave kernel
+    (esp_relpos_attn_probs, latest and legacy rel_shift) and the 32-row-block kernel
+    (esp_relpos_attn_fwd, latest) — several row groups incl. a partial last one, against the
+    fp64 oracle."""
     from espnet_slurp_amd import kernels as K
     monkeypatch.setattr(K, "FUSED_ATTN_BWD", fused_bwd)
     monkeypatch.setattr(K, "FLASH_ATTN", False)  # the materialised paths (flash: tests/test_gpu_flash.py)
+    monkeypatch.setattr(K, "ATTN_FWD32", fwd == "block32")
     torch.manual_seed(3)
     B, D, H = 3, 256, 4
-    assert K.relpos_fused_ok(T, D // H)
+    assert K.relpos_fused_ok(T, D // H) and K.relpos_probs_ok(T, D // H)
     klen = torch.tensor(klens)
-    mod = RelPositionMultiHeadedAttention(H, D, 0.0, False).to(dev)
+    mod = RelPositionMultiHeadedAttention(H, D, 0.0, legacy).to(dev)
     with torch.no_grad():
         for p in mod.parameters():
             p.normal_(0, 0.1)
@@ -83,43 +88,54 @@ def test_relpos_mha_fused_dk64(dev, T, klens, fused_bwd, monkeypatch):
     x = torch.randn(B * T, D)
     res = torch.randn(B * T, D)
     dout = torch.randn(B * T, D)
-    pos = pos_table("latest", T, D, dev)
+    pos = pos_table("legacy" if legacy else "latest", T, D, dev)
     out, c = mod.fwd(x.to(dev), res.to(dev), pos, klen.int().to(dev), B, T, 0.0, Seeds(1), True)
     dx = mod.bwd(c, dout.to(dev))
     P = _params64(mod, "a")
     xt = x.double().view(B, T, D).requires_grad_(True)
     mask = (~O.make_pad_mask(klen, T))[:, None, :]
-    ref = O.rel_mha(P, "a", xt, pos.cpu().double()[None], mask, H, False) + res.double().view(B, T, D)
+    ref = O.rel_mha(P, "a", xt, pos.cpu().double()[None], mask, H, legacy) + res.double().view(B, T, D)
     ref.backward(dout.double().view(B, T, D))
     assert rel_err(out.cpu(), ref.detach().reshape(B * T, D)) < 1e-5
     assert rel_err(dx.cpu(), xt.grad.reshape(B * T, D)) < 1e-5
     _check_grads(mod, P, "a")
 
 
-def test_relpos_fused_matches_unfused_with_dropout(dev, monkeypatch):
-    """Same seeds -> the fused kernel reproduces the unfused path's attention probabilities and
-    dropout masks (mask index row*T + j) and therefore the same block output."""
+def _unfused(K, monkeypatch):
+    monkeypatch.setattr(K, "relpos_fused_ok", lambda T, dk: False)
+    monkeypatch.setattr(K, "relpos_probs_ok", lambda T, dk: False)
+
+
+@pytest.mark.parametrize("fwd,legacy,T", [("block32", False, 100), ("wave16", False, 100), ("wave16", True, 100),
+                                          ("wave16", False, 374), ("wave16", True, 374)])
+def test_relpos_fused_matches_unfused_with_dropout(dev, monkeypatch, fwd, legacy, T):
+    """Same seeds -> the fused kernels reproduce the unfused path's (ac GEMM, bd GEMM, rel_shift +
+    softmax pass) attention probabilities and dropout masks (mask index row*T + j) and therefore
+    the same block output; T = 374 is the C2/C4/C5 subsampled length (score rows of pitch 376)."""
     from espnet_slurp_amd import kernels as K
     monkeypatch.setattr(K, "FLASH_ATTN", False)  # the materialised paths (flash: tests/test_gpu_flash.py)
+    monkeypatch.setattr(K, "ATTN_FWD32", fwd == "block32")
     torch.manual_seed(4)
-    B, T, D, H = 2, 100, 256, 4
-    klen = torch.tensor([100, 61]).int().to(dev)
-    mod = RelPositionMultiHeadedAttention(H, D, 0.1, False).to(dev)
+    B, D, H = 2, 256, 4
+    klen = torch.tensor([T, (T * 3) // 5]).int().to(dev)
+    mod = RelPositionMultiHeadedAttention(H, D, 0.1, legacy).to(dev)
     mod.flat = FlatParams(mod, dev)
     x = torch.randn(B * T, D, device=dev)
     res = torch.randn(B * T, D, device=dev)
-    pos = pos_table("latest", T, D, dev)
+    pos = pos_table("legacy" if legacy else "latest", T, D, dev)
     dout = torch.randn(B * T, D, device=dev)
-    monkeypatch.setattr(K, "FUSED_ATTN_BWD", True)
+    monkeypatch.setattr(K, "FUSED_ATTN_BWD", not legacy)
     out_f, c_f = mod.fwd(x, res, pos, klen, B, T, 0.0, Seeds(7), True)
     dx_f = mod.bwd(c_f, dout)
     g_f = mod.flat.grad.clone()
     mod.flat.grad.zero_()
-    monkeypatch.setattr(K, "relpos_fused_ok", lambda T, dk: False)
+    _unfused(K, monkeypatch)
     out_u, c_u = mod.fwd(x, res, pos, klen, B, T, 0.0, Seeds(7), True)
     dx_u = mod.bwd(c_u, dout)
-    assert float((c_f.attn - c_u.attn).abs().max()) < 1e-6
-    assert bool(((c_f.pv == 0) == (c_u.pv == 0)).all())
+    Tp = K.pitch(T)
+    rows = lambda t: t.view(-1, Tp)[:, :T]  # noqa: E731  (the pitch columns are never written)
+    assert float((rows(c_f.attn) - rows(c_u.attn)).abs().max()) < 1e-6
+    assert bool(((rows(c_f.pv) == 0) == (rows(c_u.pv) == 0)).all())
     assert float((out_f - out_u).abs().max()) < 1e-4
     # backward: the fused dP / dropout / softmax / rel_shift adjoint kernel regenerates the same masks
     assert rel_err(dx_f.cpu(), dx_u.cpu()) < 1e-5

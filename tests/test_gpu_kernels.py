@@ -366,12 +366,13 @@ def test_relpos_softmax_and_adjoint(dev, legacy, padded):
     dbd = torch.empty(Z * T * Pp, device=dev)
     K.relshift_bwd(dS, dbd, 2 if legacy else 1, Z, T, P, lds=Tp, ldp=Pp)
     assert rel_err(dbd.cpu().view(Z, T, Pp)[:, :, :P], bdt.grad) < 1e-5
-    if not legacy:  # the fused softmax-backward + rel_shift-adjoint pass gives the same dS and dbd
-        dS2 = put(dP, T, Tp)
-        dbd2 = torch.full((Z * T * Pp,), float("nan"), device=dev)
-        K.attn_softmax_bwd_relpos(att, dS2, dS2, dbd2, Pp, 0.0, 0, math.sqrt(dk), Z * T, T, Tp)
-        assert torch.equal(dS2.view(Z, T, Tp)[:, :, :T], dS.view(Z, T, Tp)[:, :, :T])
-        assert torch.equal(dbd2.view(Z, T, Pp)[:, :, :P], dbd.view(Z, T, Pp)[:, :, :P])
+    # the fused softmax-backward + rel_shift-adjoint pass gives the same dS and every dbd element
+    dS2 = put(dP, T, Tp)
+    dbd2 = torch.full((Z * T * Pp,), float("nan"), device=dev)
+    K.attn_softmax_bwd_relpos(att, dS2, dS2, dbd2, Pp, 0.0, 0, math.sqrt(dk), Z * T, T, Tp,
+                              relpos=2 if legacy else 1)
+    assert torch.equal(dS2.view(Z, T, Tp)[:, :, :T], dS.view(Z, T, Tp)[:, :, :T])
+    assert torch.equal(dbd2.view(Z, T, Pp)[:, :, :P], dbd.view(Z, T, Pp)[:, :, :P])
 
 
 def test_causal_softmax_with_dropout(dev):
