@@ -12,6 +12,8 @@
 // One wave per score row; rows of <= 64*PER keys live in registers.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -726,7 +728,7 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd16_kernel(
   }
 
   // softmax over each row: a row's keys sit in the 16 lanes of one quarter x NTA tiles
-  float m[4], inv[4];
+  float nm[4], inv[4];  // -max * log2(e) (P2) or -max, and 1 / sum
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     float v = sc[0][r];
@@ -734,7 +736,8 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd16_kernel(
     for (int t = 1; t < NTA; ++t) v = fmaxf(v, sc[t][r]);
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    m[r] = v;
+    if (v == -INFINITY) v = 0.f;  // fully masked row: every e below is exp(-inf) = 0
+    nm[r] = P2 ? -v * 1.4426950408889634f : -v;
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -742,8 +745,7 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd16_kernel(
 #pragma unroll
     for (int t = 0; t < NTA; ++t) {
       const float x = sc[t][r];
-      const float e = x == -INFINITY ? 0.f
-                      : (P2 ? __builtin_amdgcn_exp2f((x - m[r]) * 1.4426950408889634f) : expf(x - m[r]));
+      const float e = P2 ? __builtin_amdgcn_exp2f(fmaf(x, 1.4426950408889634f, nm[r])) : expf(x + nm[r]);
       sc[t][r] = e;
       v += e;
     }
@@ -753,53 +755,57 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd16_kernel(
   }
   // probabilities -> HBM through a per-wave LDS transpose, 64 columns (4 key tiles) at a time:
   // lane L then holds 4 consecutive columns of row 4p + (L >> 4), so one store instruction writes
-  // 4 rows x 256 contiguous bytes (instead of 4 rows x 64 B from the accumulator layout)
+  // 4 rows x 256 contiguous bytes (instead of 4 rows x 64 B from the accumulator layout).  A quad
+  // that straddles T also writes the row pitch's padding columns (p = 0 there: keys >= T are
+  // masked), so every store is a whole float4 and the only guard is j < T.
   float* stg = stage[wave];
   const int sr = lane >> 4, sc4 = 4 * (lane & 15);
-  long rowo[4];
+  float* abase[4];
+  float* dbase[4];
+  uint64_t ibase[4];
   bool rok[4];
 #pragma unroll
   for (int ps = 0; ps < 4; ++ps) {
     const int i = i0 + 4 * ps + sr;
     rok[ps] = i < T;
-    rowo[ps] = (long)z * T + min(i, T - 1);
+    const long row = (long)z * T + min(i, T - 1);
+    abase[ps] = attn + row * lds + sc4;
+    dbase[ps] = pdrop ? pdrop + row * lds + sc4 : nullptr;
+    ibase[ps] = (uint64_t)(row * T + sc4);
   }
+  auto store_rows = [&](auto drop_c) {
+    constexpr bool DROP = decltype(drop_c)::value;
 #pragma unroll
-  for (int t4 = 0; t4 < NTA; t4 += 4) {
-    if (16 * t4 >= T) break;
+    for (int t4 = 0; t4 < NTA; t4 += 4) {
+      if (16 * t4 >= T) break;
 #pragma unroll
-    for (int tt = 0; tt < 4; ++tt)
+      for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) stg[(4 * q4 + r) * RW_SPITCH + 16 * tt + li] = sc[t4 + tt][r] * inv[r];
-    asm volatile("" ::: "memory");
-    const int j = 16 * t4 + sc4;
+        for (int r = 0; r < 4; ++r) stg[(4 * q4 + r) * RW_SPITCH + 16 * tt + li] = sc[t4 + tt][r] * inv[r];
+      asm volatile("" ::: "memory");
+      const bool jok = 16 * t4 + sc4 < T;
 #pragma unroll
-    for (int ps = 0; ps < 4; ++ps) {
-      const float4 v = *reinterpret_cast<const float4*>(stg + (4 * ps + sr) * RW_SPITCH + sc4);
-      if (!rok[ps] || j >= T) continue;
-      float* ar = attn + rowo[ps] * lds + j;
-      float4 d = v;
-      if (pdrop) {
-        const uint64_t ix = (uint64_t)(rowo[ps] * T + j);
-        d.x = esp::keep_elem(seed, ix, thr) ? v.x * dscale : 0.f;
-        d.y = esp::keep_elem(seed, ix + 1, thr) ? v.y * dscale : 0.f;
-        d.z = esp::keep_elem(seed, ix + 2, thr) ? v.z * dscale : 0.f;
-        d.w = esp::keep_elem(seed, ix + 3, thr) ? v.w * dscale : 0.f;
-      }
-      float* dr = pdrop ? pdrop + rowo[ps] * lds + j : nullptr;
-      if (j + 4 <= T) {
-        *reinterpret_cast<float4*>(ar) = v;
-        if (pdrop) *reinterpret_cast<float4*>(dr) = d;
-      } else {
-        const float vv[4] = {v.x, v.y, v.z, v.w}, dd[4] = {d.x, d.y, d.z, d.w};
-        for (int e = 0; e < T - j; ++e) {
-          ar[e] = vv[e];
-          if (pdrop) dr[e] = dd[e];
+      for (int ps = 0; ps < 4; ++ps) {
+        const float4 v = *reinterpret_cast<const float4*>(stg + (4 * ps + sr) * RW_SPITCH + sc4);
+        if (rok[ps] && jok) {
+          float* ar = abase[ps] + 16 * t4;
+          *reinterpret_cast<float4*>(ar) = v;
+          if (DROP) {
+            const uint64_t ix = ibase[ps] + 16 * t4;
+            float4 d;
+            d.x = esp::keep_elem(seed, ix, thr) ? v.x * dscale : 0.f;
+            d.y = esp::keep_elem(seed, ix + 1, thr) ? v.y * dscale : 0.f;
+            d.z = esp::keep_elem(seed, ix + 2, thr) ? v.z * dscale : 0.f;
+            d.w = esp::keep_elem(seed, ix + 3, thr) ? v.w * dscale : 0.f;
+            *reinterpret_cast<float4*>(dbase[ps] + 16 * t4) = d;
+          }
         }
       }
+      asm volatile("" ::: "memory");  // the reads above before the next chunk's writes
     }
-    asm volatile("" ::: "memory");  // the reads above before the next chunk's writes
-  }
+  };
+  if (pdrop) store_rows(std::true_type{});
+  else store_rows(std::false_type{});
 }
 
 inline int gridn(long n) {
@@ -978,6 +984,9 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
                                   void* stream) {
   ESP_ARG_CHECK(T >= 1 && T <= 512 && lds >= T && nb >= 1 && H >= 1, "esp_relpos_attn_probs: bad sizes T=%d", T);
   ESP_ARG_CHECK(relpos == 1 || relpos == 2, "esp_relpos_attn_probs: relpos must be 1 (latest) or 2 (legacy)");
+  ESP_ARG_CHECK(lds % 4 == 0 && ((uintptr_t)attn & 15) == 0 && ((uintptr_t)pdrop & 15) == 0,
+                "esp_relpos_attn_probs: attn / pdrop rows must be 16-B aligned (whole float4s are written, up to "
+                "the pitch lds rounded to 4)");
   ESP_ARG_CHECK(ldp_row % 4 == 0 && ldk % 4 == 0 && ((uintptr_t)p & 15) == 0 && ((uintptr_t)qv & 15) == 0 &&
                     ((uintptr_t)qu & 15) == 0 && ((uintptr_t)kmat & 15) == 0,
                 "esp_relpos_attn_probs: operands must be 16-B aligned with ld %% 4 == 0");

@@ -153,12 +153,9 @@ __device__ __forceinline__ float fwd_elem(const GemmArgs& g, uint64_t seed, uint
     w = fmaxf(v, 0.f);
     if (deriv) d = v > 0.f ? 1.f : 0.f;
   } else if (a == ACT_SWISH) {
-    const float den = 1.0f + expf(-v);
-    w = v / den;
-    if (deriv) {
-      const float sg = 1.0f / den;
-      d = sg * (1.0f + v * (1.0f - sg));
-    }
+    const float sg = esp::fast_sigmoid(v);
+    w = v * sg;
+    if (deriv) d = sg * (1.0f + v * (1.0f - sg));
   }
   if (g.drop_thresh) {
     const bool keep = esp::keep_elem(seed, idx, g.drop_thresh);
@@ -189,7 +186,7 @@ __device__ __forceinline__ void epi_store(const GemmArgs& g, long cbase, uint64_
     if (g.bwd_act == ACT_MUL) v *= x;
     else if (g.bwd_act == ACT_RELU) v = x > 0.f ? v : 0.f;
     else {
-      const float sg = 1.0f / (1.0f + expf(-x));
+      const float sg = esp::fast_sigmoid(x);
       v = v * (sg * (1.0f + x * (1.0f - sg)));
     }
   }
@@ -248,7 +245,7 @@ __device__ __forceinline__ void store_tiles(const GemmArgs& g, int z, int mrow0,
           if (g.bwd_act == ACT_MUL) v *= x;
           else if (g.bwd_act == ACT_RELU) v = x > 0.f ? v : 0.f;
           else {
-            const float sg = 1.0f / (1.0f + expf(-x));
+            const float sg = esp::fast_sigmoid(x);
             v = v * (sg * (1.0f + x * (1.0f - sg)));
           }
         }
@@ -351,7 +348,7 @@ __device__ __forceinline__ void store_tiles_wide(const GemmArgs& g, int z, int m
             if (g.bwd_act == ACT_MUL) w *= xp;
             else if (g.bwd_act == ACT_RELU) w = xp > 0.f ? w : 0.f;
             else {
-              const float sg = 1.0f / (1.0f + expf(-xp));
+              const float sg = esp::fast_sigmoid(xp);
               w = w * (sg * (1.0f + xp * (1.0f - sg)));
             }
           }
@@ -433,10 +430,9 @@ __device__ __forceinline__ void store_spec(const GemmArgs& g, int z, int mrow0, 
             dd = w > 0.f ? 1.f : 0.f;
             w = fmaxf(w, 0.f);
           } else if constexpr (S::act == ACT_SWISH) {
-            const float den = 1.0f + expf(-w);
-            const float sg = 1.0f / den;
+            const float sg = esp::fast_sigmoid(w);
             dd = sg * (1.0f + w * (1.0f - sg));
-            w = w / den;
+            w = w * sg;
           }
           if constexpr (S::drop) {
             const bool keep = esp::keep_elem(seed, row + e, g.drop_thresh);

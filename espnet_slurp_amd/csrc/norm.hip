@@ -5,6 +5,8 @@
 // (conformer/convolution.py:56-79).  Row-major [rows][channels] everywhere; one wave per
 // row for row reductions; column reductions go through per-block partials and a fixed-
 // order finalize, so every result is bitwise reproducible run to run.
+#include <initializer_list>
+
 #include "common.h"
 
 namespace {
@@ -243,7 +245,37 @@ __global__ void glu_fwd_kernel(const float* __restrict__ u, float* __restrict__ 
     const long r = i / D;
     const int c = (int)(i - r * D);
     const float a = u[r * 2 * D + c], b = u[r * 2 * D + D + c];
-    g[i] = a * (1.0f / (1.0f + expf(-b)));
+    g[i] = a * esp::fast_sigmoid(b);
+  }
+}
+
+// float4 forms (D % 4 == 0, 16-B aligned, rows*D/4 < 2^31): one 32-bit division per 4 elements
+// instead of a 64-bit division per element, hardware exp2 / rcp sigmoid
+__global__ void glu_fwd4_kernel(const float* __restrict__ u, float* __restrict__ g, int rows, int D) {
+  const int nq = D >> 2, n = rows * nq;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int r = i / nq, c = 4 * (i - r * nq);
+    const float4 a = *reinterpret_cast<const float4*>(u + (long)r * 2 * D + c);
+    const float4 b = *reinterpret_cast<const float4*>(u + (long)r * 2 * D + D + c);
+    *reinterpret_cast<float4*>(g + (long)r * D + c) =
+        make_float4(a.x * esp::fast_sigmoid(b.x), a.y * esp::fast_sigmoid(b.y), a.z * esp::fast_sigmoid(b.z),
+                    a.w * esp::fast_sigmoid(b.w));
+  }
+}
+__global__ void glu_bwd4_kernel(const float* __restrict__ u, const float* __restrict__ dg, float* __restrict__ du,
+                                int rows, int D) {
+  const int nq = D >> 2, n = rows * nq;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int r = i / nq, c = 4 * (i - r * nq);
+    const float4 a = *reinterpret_cast<const float4*>(u + (long)r * 2 * D + c);
+    const float4 b = *reinterpret_cast<const float4*>(u + (long)r * 2 * D + D + c);
+    const float4 d = *reinterpret_cast<const float4*>(dg + (long)r * D + c);
+    const float sx = esp::fast_sigmoid(b.x), sy = esp::fast_sigmoid(b.y), sz = esp::fast_sigmoid(b.z),
+                sw = esp::fast_sigmoid(b.w);
+    *reinterpret_cast<float4*>(du + (long)r * 2 * D + c) = make_float4(d.x * sx, d.y * sy, d.z * sz, d.w * sw);
+    *reinterpret_cast<float4*>(du + (long)r * 2 * D + D + c) =
+        make_float4(d.x * a.x * sx * (1.0f - sx), d.y * a.y * sy * (1.0f - sy), d.z * a.z * sz * (1.0f - sz),
+                    d.w * a.w * sw * (1.0f - sw));
   }
 }
 
@@ -254,7 +286,7 @@ __global__ void glu_bwd_kernel(const float* __restrict__ u, const float* __restr
     const long r = i / D;
     const int c = (int)(i - r * D);
     const float a = u[r * 2 * D + c], b = u[r * 2 * D + D + c];
-    const float s = 1.0f / (1.0f + expf(-b));
+    const float s = esp::fast_sigmoid(b);
     const float d = dg[i];
     du[r * 2 * D + c] = d * s;
     du[r * 2 * D + D + c] = d * a * s * (1.0f - s);
@@ -555,6 +587,23 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(const double* __restr
   }
 }
 
+// s = swish(gamma*(y-mean)*rstd + beta), float4 form (D % 4 == 0, 16-B aligned, M*D/4 < 2^31)
+__global__ void bn_swish_fwd4_kernel(const float* __restrict__ y, const float* __restrict__ mean,
+                                     const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                     const float* __restrict__ beta, float* __restrict__ s, int n4, int D) {
+  const int nq = D >> 2;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    const int c = 4 * (i % nq);
+    const float4 v = reinterpret_cast<const float4*>(y)[i];
+    const float4 mu = *reinterpret_cast<const float4*>(mean + c), rs = *reinterpret_cast<const float4*>(rstd + c);
+    const float4 ga = *reinterpret_cast<const float4*>(gamma + c), be = *reinterpret_cast<const float4*>(beta + c);
+    const float zx = (v.x - mu.x) * rs.x * ga.x + be.x, zy = (v.y - mu.y) * rs.y * ga.y + be.y;
+    const float zz = (v.z - mu.z) * rs.z * ga.z + be.z, zw = (v.w - mu.w) * rs.w * ga.w + be.w;
+    reinterpret_cast<float4*>(s)[i] = make_float4(zx * esp::fast_sigmoid(zx), zy * esp::fast_sigmoid(zy),
+                                                  zz * esp::fast_sigmoid(zz), zw * esp::fast_sigmoid(zw));
+  }
+}
+
 // s = swish(gamma*(y-mean)*rstd + beta)
 __global__ void bn_swish_fwd_kernel(const float* __restrict__ y, const float* __restrict__ mean,
                                     const float* __restrict__ rstd, const float* __restrict__ gamma,
@@ -562,7 +611,7 @@ __global__ void bn_swish_fwd_kernel(const float* __restrict__ y, const float* __
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const int c = (int)(i % D);
     const float z = (y[i] - mean[c]) * rstd[c] * gamma[c] + beta[c];
-    s[i] = z / (1.0f + expf(-z));
+    s[i] = z * esp::fast_sigmoid(z);
   }
 }
 
@@ -587,7 +636,7 @@ __global__ void bn_swish_bwd_part_kernel(const float* __restrict__ ds, const flo
     }
     const float xh = (y[i] - mu) * rs;
     const float z = xh * ga + be;
-    const float sg = 1.0f / (1.0f + expf(-z));
+    const float sg = esp::fast_sigmoid(z);
     const float d = ds[i] * (sg * (1.0f + z * (1.0f - sg)));
     dz[i] = d;
     s1 += d;
@@ -694,14 +743,29 @@ ESP_API int esp_colsum(const float* x, int M, int N, long ld, float* out, int ac
   return 0;
 }
 
+static bool vec4_ok(long n, int D, std::initializer_list<const void*> ps) {
+  if (D % 4 || n / 4 >= (1L << 31)) return false;
+  for (const void* p : ps)
+    if ((uintptr_t)p & 15) return false;
+  return true;
+}
+
 ESP_API int esp_glu_fwd(const float* u, float* g, long rows, int D, void* stream) {
-  hipLaunchKernelGGL(glu_fwd_kernel, dim3(gridn(rows * D)), dim3(256), 0, (hipStream_t)stream, u, g, rows, D);
+  if (vec4_ok(rows * 2 * D, D, {u, g}))
+    hipLaunchKernelGGL(glu_fwd4_kernel, dim3(gridn(rows * D / 4)), dim3(256), 0, (hipStream_t)stream, u, g,
+                       (int)rows, D);
+  else
+    hipLaunchKernelGGL(glu_fwd_kernel, dim3(gridn(rows * D)), dim3(256), 0, (hipStream_t)stream, u, g, rows, D);
   ESP_CHECK_LAUNCH("esp_glu_fwd");
   return 0;
 }
 
 ESP_API int esp_glu_bwd(const float* u, const float* dg, float* du, long rows, int D, void* stream) {
-  hipLaunchKernelGGL(glu_bwd_kernel, dim3(gridn(rows * D)), dim3(256), 0, (hipStream_t)stream, u, dg, du, rows, D);
+  if (vec4_ok(rows * 2 * D, D, {u, dg, du}))
+    hipLaunchKernelGGL(glu_bwd4_kernel, dim3(gridn(rows * D / 4)), dim3(256), 0, (hipStream_t)stream, u, dg, du,
+                       (int)rows, D);
+  else
+    hipLaunchKernelGGL(glu_bwd_kernel, dim3(gridn(rows * D)), dim3(256), 0, (hipStream_t)stream, u, dg, du, rows, D);
   ESP_CHECK_LAUNCH("esp_glu_bwd");
   return 0;
 }
@@ -766,8 +830,12 @@ ESP_API int esp_bn_swish_fwd(const float* y, const float* gamma, const float* be
   hipLaunchKernelGGL(bn_part_kernel, g1, dim3(256), 0, st, y, M, D, rpb, mean, 1, work, T, tvalid);
   hipLaunchKernelGGL(bn_finalize_kernel, bnf_grid(D), dim3(1024), 0, st, work, nb, D, M, 1, mean, rstd, run_mean,
                      run_var, momentum, eps, T, tvalid);
-  hipLaunchKernelGGL(bn_swish_fwd_kernel, dim3(gridn((long)M * D)), dim3(256), 0, st, y, mean, rstd, gamma, beta, s,
-                     (long)M * D, D);
+  if (vec4_ok((long)M * D, D, {y, mean, rstd, gamma, beta, s}))
+    hipLaunchKernelGGL(bn_swish_fwd4_kernel, dim3(gridn((long)M * D / 4)), dim3(256), 0, st, y, mean, rstd, gamma,
+                       beta, s, (int)((long)M * D / 4), D);
+  else
+    hipLaunchKernelGGL(bn_swish_fwd_kernel, dim3(gridn((long)M * D)), dim3(256), 0, st, y, mean, rstd, gamma, beta,
+                       s, (long)M * D, D);
   ESP_CHECK_LAUNCH("esp_bn_swish_fwd");
   return 0;
 }

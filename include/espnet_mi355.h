@@ -221,7 +221,8 @@ int esp_relpos_attn_fwd(const float* qu, const float* qv, const float* kmat, lon
  * (relpos 2: p has P = T rows, legacy rel_shift attention.py:145-165) rel_shift, one wave per
  * 16 query rows with every score row in registers (no block synchronisation): ac and the bd band
  * on v_mfma_f32_16x16x4_f32, rel_shift through a per-wave LDS ring, key mask, softmax, dropout
- * copy.  Operands as esp_relpos_attn_fwd; d_k = 64, T <= 512.  Replaces, for these shapes, the
+ * copy.  Operands as esp_relpos_attn_fwd; d_k = 64, T <= 512; attn / pdrop 16-B aligned with
+ * lds % 4 == 0 (columns T .. round_up(T, 4) - 1 of the pitch are written as 0).  Replaces, for these shapes, the
  * reference's matrix_ac / matrix_bd matmuls + rel_shift + softmax + dropout
  * (attention.py:240-263, 64-96). */
 int esp_relpos_attn_probs(const float* qu, const float* qv, const float* kmat, long ldk, const float* p,

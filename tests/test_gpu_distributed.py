@@ -98,11 +98,13 @@ def test_two_rank_training_matches_ddp_oracle(dev, tmp_path, mode, accum):
             assert a[k] == b[k], k
             assert abs(a[k] - o[k]) <= 1e-4 * max(1.0, abs(o[k])), (k, a[k], o[k])
     # DDP broadcast_buffers: rank 0 is the source, so its BatchNorm running statistics are
-    # exactly its own replica's chain (rank 1 starts every forward from rank 0's copy)
+    # exactly its own replica's chain (rank 1 starts every forward from rank 0's copy).  They are
+    # statistics of activations under the updated parameters, which the gate above lets differ
+    # from the oracle's in a few sign-like Adam updates: fp32 atol 1e-4 (north star) here.
     for n, b in res[0]["bufs"].items():
         if "running" in n:
             r = ref_bn[n].double().numpy()
-            assert np.abs(b.double().numpy() - r).max() < 1e-5 * max(1.0, np.abs(r).max()) + 1e-5, n
+            assert np.abs(b.double().numpy() - r).max() < 1e-4 * max(1.0, np.abs(r).max()), n
     if mode == "graph":
         assert res[0]["graphs"] == accum  # one step graph (accum 2: micro-batch + update)
         # the backward was captured in segments: bucket all-reduces overlap the later segments
