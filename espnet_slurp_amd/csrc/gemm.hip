@@ -356,6 +356,13 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
       return c;
     };
     g.bnt = (N <= 64 || cost(64) < cost(128)) ? 64 : 128;
+    // the conv2 weight gradient (im2col-gathered B, K = B*T2*F2 ~ 1M): 128-wide tiles halve the
+    // gathered-B re-reads and split-K refills the chip (8.39 vs 9.22 ms at C2 B=128,
+    // tools/gemm_bench.py with ESP_GEMM_BNT; the K ~ 48k linear weight gradients keep 128x64)
+    if (mode_b == I2C_RC && work && K >= 65536) g.bnt = 128;
+    static int force_bnt = -1;  // ESP_GEMM_BNT=64|128: tile width override (diagnostics)
+    if (force_bnt < 0) force_bnt = getenv("ESP_GEMM_BNT") ? atoi(getenv("ESP_GEMM_BNT")) : 0;
+    if ((force_bnt == 64 || force_bnt == 128) && N > 64) g.bnt = force_bnt;
   }
   {
     const long tiles = ntiles(g.bnt ? g.bnt : BN);

@@ -7,7 +7,8 @@ import torch  # noqa: E402
 
 from espnet_slurp_amd import kernels as K  # noqa: E402
 
-M = 64 * 374
+NB = int(os.environ.get("GEMM_BENCH_B", "64"))  # utterances per batch
+M = NB * 374
 SHAPES = [  # (mode_a, mode_b, M, N, K, batch, label)
     (0, 1, M, 1024, 256, 1, "ffn w1 fwd"),
     (0, 1, M, 256, 1024, 1, "ffn w2 fwd"),
@@ -23,11 +24,11 @@ SHAPES = [  # (mode_a, mode_b, M, N, K, batch, label)
     (0, 1, 374, 64, 374, 256, "ctx pad376", 376),
     (1, 1, 374, 64, 374, 256, "dV pad376", 376),
     (0, 0, 374, 374, 64, 256, "scores ldc376", 376),
-    (1, 3, 256, 2304, 64 * 374 * 19, 1, "conv2 dW"),
-    (2, 0, 64 * 374 * 19, 256, 2304, 1, "conv2 fwd"),
-    (0, 1, 64 * 374 * 19, 2304, 256, 1, "conv2 dcol"),
-    (0, 1, 64 * 41, 256, 256, 1, "decoder q"),
-    (0, 1, 64 * 41, 256, 2048, 1, "decoder ffn w2"),
+    (1, 3, 256, 2304, NB * 374 * 19, 1, "conv2 dW"),
+    (2, 0, NB * 374 * 19, 256, 2304, 1, "conv2 fwd"),
+    (0, 1, NB * 374 * 19, 2304, 256, 1, "conv2 dcol"),
+    (0, 1, NB * 41, 256, 256, 1, "decoder q"),
+    (0, 1, NB * 41, 256, 2048, 1, "decoder ffn w2"),
 ]
 
 
@@ -46,12 +47,12 @@ def run(ma, mb, m, n, k, batch, pad=None, reps=20):
     ic_a = ic_b = None
     if ma == 2:  # conv2 forward: NHWC map (B, 749, 39, 256) -> pixels (B*374*19)
         ic_a = (749, 39, 256, 374, 19)
-        A = torch.randn(64 * 749 * 39 * 256, device=dev)
+        A = torch.randn(NB * 749 * 39 * 256, device=dev)
     else:
         A = torch.randn(batch * max(m, lda) * max(k, lda), device=dev) if pad else torch.randn(batch * m * k, device=dev)
     if mb == 3:
         ic_b = (749, 39, 256, 374, 19)
-        B = torch.randn(64 * 749 * 39 * 256, device=dev)
+        B = torch.randn(NB * 749 * 39 * 256, device=dev)
     else:
         B = torch.randn(batch * n * k, device=dev)
     C = torch.empty(batch * m * ldc, device=dev)
