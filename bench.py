@@ -170,7 +170,8 @@ def gemm_algorithmic_bytes(shapes) -> float:
     reads, aux writes).  An implicit-im2col operand counts its NHWC source map (~ 4/9 of the
     virtual M x K matrix for the 3x3 / stride-2 convolution)."""
     tot = 0.0
-    for (ma, mb, M, N, Kd, batch), (n, _ms, _f, extra) in shapes.items():
+    for key, (n, _ms, _f, extra) in shapes.items():
+        ma, mb, M, N, Kd, batch = key[:6]  # (+ a tag for the bf16-operand / score-gradient GEMMs)
         a = M * Kd * (4 / 9 if ma >= 2 else 1.0)
         b = N * Kd * (4 / 9 if mb >= 2 else 1.0)
         tot += n * 4.0 * batch * (a + b + M * N) + extra

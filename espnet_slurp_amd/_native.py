@@ -61,6 +61,8 @@ SIGNATURES = {
     "esp_relpos_softmax_fwd": [P, P, L, I, I, P, F, P, P, P, F, U64, I, L, P],
     "esp_relpos_attn_fwd": [P, P, P, L, P, L, I, I, F, P, P, P, F, U64, I, L, P],
     "esp_relpos_attn_probs": [P, P, P, L, P, L, I, I, I, F, P, P, P, F, U64, I, L, P],
+    "esp_attn_bwd_prep": [P, L, P, L, I, I, I, I, P, P, L, I, P],
+    "esp_attn_dscores": [P, L, P, L, P, P, P, P, L, I, I, I, I, F, F, U64, I, L, P],
     "esp_attn_softmax_bwd_relpos": [P, P, P, P, L, I, F, U64, F, L, I, L, P],
     "esp_relpos_attn_bwd": [P, L, P, L, P, P, P, L, I, I, F, F, U64, I, L, P],
     "esp_relpos_flash_fwd": [P, P, P, L, P, L, P, L, I, I, I, F, P, P, L, P, F, U64, I, P],
@@ -84,7 +86,7 @@ SIGNATURES = {
 }
 _RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I, "esp_set_gemm_compute": I,
              "esp_get_gemm_compute": I}
-ABI_VERSION = 17  # bumped whenever a signature in include/espnet_mi355.h changes
+ABI_VERSION = 18  # bumped whenever a signature in include/espnet_mi355.h changes
 
 _lib = None
 

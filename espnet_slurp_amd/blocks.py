@@ -248,7 +248,15 @@ class RelPositionMultiHeadedAttention(nn.Module):
         # the fused dP + softmax/rel_shift adjoint kernel measures slower than the K=64 GEMM + the
         # row-wise adjoint pass at C2 (198 vs 157 us per layer): opt-in until it is reworked
         fused = not self.legacy and K.relpos_fused_ok(T, dk) and K.FUSED_ATTN_BWD
-        if fused:  # dP = dctx v^T on the MFMA inside the softmax / rel_shift adjoint kernel
+        dscores = not fused and K.ATTN_DSCORES
+        if dscores:
+            # dS = P (drop'(dP) - dot) / sqrt(dk) and its rel_shift adjoint in the dP GEMM's epilogue,
+            # dot_i = dctx_i . ctx_i (= sum_j P_drop dP): no dP tensor, no row-wise pass
+            dot = empty(Z * T, like=dout)
+            K.attn_bwd_prep(dctx, D, c.ctx, D, B, H, dk, T, dot, dbd, Pp, relpos)
+            K.attn_dscores(dctx, D, c.qkv, 3 * D, c.attn, dot, dS, dbd, Pp, relpos, B, H, dk, math.sqrt(dk), c.pa,
+                           c.sa, T, Tp, v_off=2 * D)
+        elif fused:  # dP = dctx v^T on the MFMA inside the softmax / rel_shift adjoint kernel
             K.relpos_attn_bwd(dctx, D, c.qkv, 3 * D, c.attn, dS, dbd, Pp, B, H, math.sqrt(dk), c.pa, c.sa, T, Tp,
                               v_off=2 * D)
         else:  # dP = dctx v^T  (into a (Z,T,T) buffer)
@@ -257,7 +265,7 @@ class RelPositionMultiHeadedAttention(nn.Module):
         # dV = pv^T dctx -> dqkv[:, 2D:3D]
         K.gemm(T, dk, T, c.pv, dctx, dqkv, mode_a=K.RC, lda=Tp, mode_b=K.RC, ldb=D, ldc=3 * D, c_off=2 * D,
                batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * D), sc=(dk, T * 3 * D))
-        if fused:
+        if fused or dscores:
             pass
         else:  # softmax + rel_shift adjoints in one pass (latest and legacy)
             K.attn_softmax_bwd_relpos(c.attn, dS, dS, dbd, Pp, c.pa, c.sa, math.sqrt(dk), Z * T, T, Tp, relpos=relpos)

@@ -56,6 +56,35 @@ __global__ void heads_split2_kernel(const float* __restrict__ src, long ld, int 
   }
 }
 
+// Attention backward prep (esp_attn_bwd_prep), one wave per score row (z, i), z = h*nb + b:
+//   dot[z*T + i] = dctx[b*T+i][h*dk ..] . ctx[b*T+i][h*dk ..]  (= sum_j P_drop[i][j] dP[i][j])
+//   and the bd-gradient elements the score-gradient epilogue never writes set to 0:
+//   latest: k < T-1-i and k >= 2T-1-i;  legacy: row 0's k < T-1.
+__global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const float* __restrict__ dctx, long ldd,
+                                                            const float* __restrict__ ctx, long ldc, int nb, int H,
+                                                            int dk, int T, float* __restrict__ dot,
+                                                            float* __restrict__ dbd, long ldp, int relpos) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (long)nb * H * T) return;
+  const int i = (int)(row % T);
+  const int z = (int)(row / T);
+  const int h = z / nb, b = z - h * nb;
+  const long src = ((long)b * T + i);
+  float acc = 0.f;
+  for (int d = lane; d < dk; d += 64) acc += dctx[src * ldd + h * dk + d] * ctx[src * ldc + h * dk + d];
+  acc = esp::wave_sum(acc);
+  if (lane == 0) dot[row] = acc;
+  float* br = dbd + row * ldp;
+  const int sh = T - 1 - i;
+  if (relpos == 1) {
+    for (int k = lane; k < sh; k += 64) br[k] = 0.f;
+    for (int k = sh + T + lane; k < 2 * T - 1; k += 64) br[k] = 0.f;
+  } else if (i == 0) {
+    for (int k = lane; k < sh; k += 64) br[k] = 0.f;
+  }
+}
+
 // y[r*ldy + c] += x[r*ldx + c]
 __global__ void add2d_kernel(const float* __restrict__ x, long ldx, float* __restrict__ y, long ldy, int M, int N) {
   const long n = (long)M * N;
@@ -838,6 +867,18 @@ ESP_API int esp_heads_split2(const float* src, long ld, int col0, int B, int T, 
   hipLaunchKernelGGL(heads_split2_kernel, dim3(gridn((long)H * B * T * dk / 4)), dim3(256), 0, (hipStream_t)stream,
                      src, ld, col0, B, T, H, dk, bias_a, dst_a, bias_b, dst_b);
   ESP_CHECK_LAUNCH("esp_heads_split2");
+  return 0;
+}
+
+ESP_API int esp_attn_bwd_prep(const float* dctx, long ldd, const float* ctx, long ldc, int nb, int H, int dk, int T,
+                              float* dot, float* dbd, long ldp, int relpos, void* stream) {
+  ESP_ARG_CHECK(relpos == 1 || relpos == 2, "esp_attn_bwd_prep: relpos must be 1 or 2");
+  ESP_ARG_CHECK(T >= 1 && nb >= 1 && H >= 1 && dk >= 1 && ldp >= (relpos == 1 ? 2 * T - 1 : T),
+                "esp_attn_bwd_prep: bad sizes");
+  const long rows = (long)nb * H * T;
+  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, (hipStream_t)stream, dctx,
+                     ldd, ctx, ldc, nb, H, dk, T, dot, dbd, ldp, relpos);
+  ESP_CHECK_LAUNCH("esp_attn_bwd_prep");
   return 0;
 }
 

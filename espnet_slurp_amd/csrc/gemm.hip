@@ -157,6 +157,7 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
   const bool can_spec_fwd = MA == KC && MB == KC, can_spec_bwd = MA == KC && MB == RC;
   const bool can_pspec = (MA == KC || MA == RC) && (MB == KC || MB == RC);
   int kind = g.splits > 1 ? EPI_PLAIN : epi_kind_spec(g);
+  if (kind == EPI_SMB && !(MA == KC && MB == KC && g.bf16 == 0)) return false;
   if ((kind == EPI_BMUL && !can_spec_bwd) || ((kind == EPI_P0 || kind == EPI_PR) && !can_pspec) ||
       (kind >= EPI_BIAS && kind <= EPI_FFN_RELU && !can_spec_fwd))
     kind = epi_kind(g);
@@ -187,7 +188,7 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
   const int prec = g.bf16;
   if (kind == EPI_PLAIN) return glds_launch_plain(MA, MB, BNT, prec, rs, grid, st, g, x);
   if (kind == EPI_FWD || kind == EPI_BWD) return glds_launch_epi(MA, MB, BNT, prec, kind, grid, st, g, x);
-  if (kind == EPI_P0 || kind == EPI_PR) return glds_launch_pspec(MA, MB, BNT, prec, kind, grid, st, g, x);
+  if (kind == EPI_P0 || kind == EPI_PR || kind == EPI_SMB) return glds_launch_pspec(MA, MB, BNT, prec, kind, grid, st, g, x);
   return glds_launch_spec(MA, MB, BNT, prec, kind, grid, st, g, x);
 }
 
@@ -196,6 +197,10 @@ int launch(const GemmArgs& g0, int batch, hipStream_t st) {
   bool done = false;
   if (g0.bnt == 64 || g0.bnt == 128) done = launch_glds(MA, MB, g0, batch, st);
   GemmArgs g = g0;
+  if (!done && g.smb_rel) {
+    esp::set_error("esp_attn_dscores: operands not eligible for the LDS-DMA kernel (16-B alignment, ld %% 4)");
+    return -1;
+  }
   if (!done && g.bf16 == 2) {
     esp::set_error("esp_gemm_bf16: operands not eligible for the LDS-DMA kernel (16-B alignment, ld %% 8)");
     return -1;
@@ -252,7 +257,7 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
                     long sc2, const float* bias, float alpha, float beta, const float* R, int act, float* aux,
                     float drop_p, unsigned long long seed, int bwd_act, const float* pre, float* rowsum,
                     const int* im2col_a, const int* im2col_b, float* work, long work_bytes, void* stream,
-                    int prec_in);
+                    int prec_in, const GemmArgs* smb = nullptr);
 
 ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2,
                          const float* A, long lda, long sa1, long sa2,
@@ -282,12 +287,38 @@ ESP_API int esp_gemm_bf16(int M, int N, int K, int batch, int nb2, const void* A
                   pre, nullptr, nullptr, nullptr, work, work_bytes, stream, 2);
 }
 
+// Rel-pos attention score gradient in one GEMM: dP = dctx V^T per (head, utterance) with the
+// softmax + attention-dropout + rel_shift adjoints in the epilogue (EPI_SMB):
+//   dS[i][j] = P[i][j] * (drop'(dP[i][j]) - dot[i]) / sqrt(d_k),  dot[i] = dctx_i . ctx_i
+// (= sum_j P_drop[i][j] dP[i][j]: FlashAttention-2's row term, esp_attn_bwd_prep), and dS scattered
+// into the bd gradient rows (latest / legacy rel_shift adjoint; esp_attn_bwd_prep zeroes the
+// elements without a source).  Replaces the dP GEMM + the row-wise softmax / rel_shift pass
+// (attention.py:64-96, 145-165 backward): no dP tensor round trip through HBM.
+ESP_API int esp_attn_dscores(const float* dctx, long ldd, const float* vmat, long ldv, const float* attn,
+                             const float* dot, float* dS, float* dbd, long ldp, int relpos, int nb, int H, int dk,
+                             float sqrt_dk, float drop_p, unsigned long long seed, int T, long lds, void* stream) {
+  ESP_ARG_CHECK(relpos == 1 || relpos == 2, "esp_attn_dscores: relpos must be 1 or 2");
+  ESP_ARG_CHECK(T >= 1 && nb >= 1 && H >= 1 && dk >= 1 && lds >= T && lds % 4 == 0 &&
+                    ldp >= (relpos == 1 ? 2 * T - 1 : T) && sqrt_dk > 0.f,
+                "esp_attn_dscores: bad sizes T=%d lds=%ld ldp=%ld", T, lds, ldp);
+  ESP_ARG_CHECK(((uintptr_t)attn & 15) == 0 && ((uintptr_t)dS & 15) == 0, "esp_attn_dscores: attn / dS not 16-B aligned");
+  GemmArgs smb{};
+  smb.smb_rel = relpos;
+  smb.smb_dot = dot;
+  smb.smb_dbd = dbd;
+  smb.smb_ldp = ldp;
+  const int Z = nb * H;
+  return gemm_run(KC, KC, T, T, dk, Z, nb, dctx, ldd, dk, (long)T * ldd, vmat, ldv, dk, (long)T * ldv, dS, lds,
+                  (long)nb * T * lds, (long)T * lds, nullptr, 1.0f / sqrt_dk, 0.f, nullptr, 0, nullptr, drop_p, seed, 0,
+                  attn, nullptr, nullptr, nullptr, nullptr, 0, stream, 0, &smb);
+}
+
 static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2, const float* A, long lda,
                     long sa1, long sa2, const float* B, long ldb, long sb1, long sb2, float* C, long ldc, long sc1,
                     long sc2, const float* bias, float alpha, float beta, const float* R, int act, float* aux,
                     float drop_p, unsigned long long seed, int bwd_act, const float* pre, float* rowsum,
                     const int* im2col_a, const int* im2col_b, float* work, long work_bytes, void* stream,
-                    int prec_in) {
+                    int prec_in, const GemmArgs* smb) {
   ESP_ARG_CHECK(M >= 0 && N >= 0 && K >= 0 && batch >= 1 && nb2 >= 1 && batch % nb2 == 0,
                 "esp_gemm_f32: bad sizes M=%d N=%d K=%d batch=%d nb2=%d", M, N, K, batch, nb2);
   ESP_ARG_CHECK(mode_a >= 0 && mode_a <= 3 && mode_b >= 0 && mode_b <= 3, "esp_gemm_f32: bad mode");
@@ -319,6 +350,12 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
   g.bwd_act = bwd_act; g.pre = pre; g.rowsum = rowsum;
   g.seed = seed;
   g.key = esp::rng_key_ptr();
+  if (smb) {  // esp_attn_dscores: the softmax / rel_shift adjoint epilogue
+    g.smb_rel = smb->smb_rel;
+    g.smb_dot = smb->smb_dot;
+    g.smb_dbd = smb->smb_dbd;
+    g.smb_ldp = smb->smb_ldp;
+  }
   g.wide = N % 4 == 0 && ldc % 4 == 0 && sc1 % 4 == 0 && sc2 % 4 == 0 && aligned16(C) && (!R || aligned16(R)) &&
            (!aux || aligned16(aux)) && (!pre || aligned16(pre)) && (!bias || aligned16(bias)) &&
            (!work || aligned16(work));

@@ -1,5 +1,6 @@
 // Instantiations of gemm_glds_kernel with the specialised plain epilogues (EPI_P0: alpha*acc,
-// EPI_PR: alpha*acc + beta*R; unsplit, wide stores) for the linear / attention mode pairs.
+// EPI_PR: alpha*acc + beta*R; unsplit, wide stores) for the linear / attention mode pairs, and the
+// attention score-gradient epilogue (EPI_SMB, KC x KC fp32: esp_attn_dscores).
 // See store_spec in gemm_kernels.h.
 #include "gemm_kernels.h"
 
@@ -18,6 +19,11 @@ bool glds_launch_pspec(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hi
       } else if (epi == EPI_PR) {
         hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_PR, BF>), grid, dim3(NT), 0, st, g, x);
         ok = true;
+      } else if constexpr (MA == KC && MB == KC && BF == 0) {
+        if (epi == EPI_SMB) {
+          hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_SMB, BF>), grid, dim3(NT), 0, st, g, x);
+          ok = true;
+        }
       }
     }
   });

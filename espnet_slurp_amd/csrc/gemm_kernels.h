@@ -102,6 +102,12 @@ struct GemmArgs {
   int cmap;
   FastDiv cm_hw, cm_w;
   int cm_T1, cm_F1, cm_ph, cm_pw;
+  // EPI_SMB (esp_attn_dscores): the dP = dctx V^T GEMM of rel-pos attention finishes the softmax
+  // and rel_shift adjoints in its epilogue; pre = the attention probabilities (C's layout)
+  int smb_rel;           // 0 off, 1 latest, 2 legacy rel_shift adjoint
+  const float* smb_dot;  // [batch * M] row dots  sum_j P_drop[i][j] dP[i][j] = dctx_i . ctx_i
+  float* smb_dbd;        // bd gradient rows (batch*M rows of pitch smb_ldp)
+  long smb_ldp;
 };
 
 __device__ __forceinline__ long row_off(const GemmArgs& g, int m) {
@@ -119,13 +125,14 @@ __device__ __forceinline__ long row_off(const GemmArgs& g, int m) {
 //   EPI 2: backward  drop'(acc + bias) * act'(pre)  (dropout mask regenerated), alpha, R
 // cbase = offset of batch z in C/R/aux/pre, dbase = z*M*N (dropout index base).
 enum { EPI_PLAIN = 0, EPI_FWD = 1, EPI_BWD = 2, EPI_BIAS = 3, EPI_BDR = 4, EPI_FFN_SWISH = 5, EPI_FFN_RELU = 6,
-       EPI_BMUL = 7, EPI_P0 = 8, EPI_PR = 9 };
+       EPI_BMUL = 7, EPI_P0 = 8, EPI_PR = 9, EPI_SMB = 10 };
 __host__ __device__ inline int epi_kind(const GemmArgs& g) {
   return g.bwd_act ? EPI_BWD : ((g.bias || g.aux || g.act || g.drop_thresh) ? EPI_FWD : EPI_PLAIN);
 }
 // the specialised kind (store_spec) when the launch's features match one exactly, else the
 // generic kind; only for wide (float4) epilogues without the conv2 output row map
 __host__ inline int epi_kind_spec(const GemmArgs& g) {
+  if (g.smb_rel) return EPI_SMB;
   const int k = epi_kind(g);
   if (g.cmap) return k;
   if (!g.wide) {
@@ -376,6 +383,8 @@ __device__ __forceinline__ void store_tiles_wide(const GemmArgs& g, int z, int m
 //   EPI_BMUL       acc * pre                                     (FFN w_2 input gradient, ACT_MUL)
 //   EPI_P0         alpha * acc                                   (plain, unsplit)
 //   EPI_PR         alpha * acc + beta * R                        (gradient accumulation)
+//   EPI_SMB        dS = P * (drop'(acc) - dot_row) * alpha -> C, and its rel_shift adjoint -> dbd
+//                  (attention.py:64-96 + 145-165 backward; P in pre, FlashAttention-2's row dot)
 // (wide stores, no output row map; chosen by epi_kind on the host).  A wave whose 32-row /
 // 32-column sub-tiles are all in range takes a path without per-element bounds checks.
 template <int EPI>
@@ -403,6 +412,45 @@ __device__ __forceinline__ void store_spec(const GemmArgs& g, int z, int mrow0, 
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       quad_transpose(acc[i][j], lane);
+      if constexpr (EPI == EPI_SMB) {
+        // lane: rows m (q = 0..3) x columns n..n+3; M = N = T (one (head, utterance) per z)
+        const int T = g.M;
+        const uint64_t kseed = esp::keyed(g.seed, g.key);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int m = mrow0 + i * 32 + 8 * q + 4 * h + (l32 & 3);
+          if (!nok || m >= g.M) continue;
+          const long off = cbase + (long)m * g.ldc + n;
+          const float4 pa = *reinterpret_cast<const float4*>(g.pre + off);  // rows padded to whole quads
+          const float pr[4] = {pa.x, pa.y, pa.z, pa.w};
+          const long zr = (long)z * T + m;
+          const float dot = g.smb_dot[zr];
+          const uint64_t row = dbase + (uint64_t)m * (uint64_t)g.N + n;
+          float* db = g.smb_dbd + zr * g.smb_ldp;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float gv = acc[i][j][4 * q + e];
+            if (g.drop_thresh) gv = esp::keep_elem(kseed, row + e, g.drop_thresh) ? gv * g.drop_scale : 0.f;
+            v[e] = pr[e] * (gv - dot) * g.alpha;
+          }
+          if (n + 4 <= g.N) {
+            st4(g.c + off, v, false);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (n + e < g.N) g.c[off + e] = v[e];
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int jj = n + e;
+            if (jj >= g.N) continue;
+            if (g.smb_rel == 1 || jj <= m) db[jj + T - 1 - m] = v[e];
+            else if (jj >= m + 2) db[g.smb_ldp + jj - m - 2] = v[e];  // legacy: row m+1's lower part
+          }
+        }
+        continue;
+      }
       float4 x4[4];  // residual (BDR) or local derivative (BMUL)
       if constexpr (S::res || S::mul) {
         const float* src = S::res ? g.r : g.pre;

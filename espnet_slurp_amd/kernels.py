@@ -474,6 +474,30 @@ def relpos_attn_probs(q_u, q_v, kmat, ldk, p, ldp_row, relpos, nb, H, sqrt_dk, k
                  _st())
 
 
+def attn_bwd_prep(dctx, ldd, ctx, ldc, nb, H, dk, T, dot, dbd, ldp, relpos):
+    """Row dots dctx_i . ctx_i per head and the source-less bd-gradient elements zeroed."""
+    _f32(dctx, ctx, dot, dbd)
+    _native.call("esp_attn_bwd_prep", _p(dctx), ldd, _p(ctx), ldc, nb, H, dk, T, _p(dot), _p(dbd), ldp, int(relpos),
+                 _st())
+
+
+def attn_dscores(dctx, ldd, vmat, ldv, attn, dot, dS, dbd, ldp, relpos, nb, H, dk, sqrt_dk, drop_p, seed, T, lds,
+                 v_off=0):
+    """dS and the rel_shift-adjoint dbd straight from the dP = dctx V^T GEMM's epilogue."""
+    _f32(dctx, vmat, attn, dot, dS, dbd)
+    if _PROF is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    _native.call("esp_attn_dscores", _p(dctx), ldd, _p(vmat, v_off), ldv, _p(attn), _p(dot), _p(dS), _p(dbd), ldp,
+                 int(relpos), nb, H, dk, float(sqrt_dk), float(drop_p), int(seed) & (2 ** 64 - 1), T, lds, _st())
+    if _PROF is not None:
+        ev1.record()
+        # epilogue streams besides A, B, C: P read, dbd written (band) — M x N per batch each
+        _PROF.append((2.0 * T * T * dk * nb * H, ev0, ev1, (KC, KC, T, T, dk, nb * H, "dscores"),
+                      8.0 * T * T * nb * H))
+
+
 def relpos_probs_ok(T: int, dk: int) -> bool:
     """Whether esp_relpos_attn_probs covers this shape (d_k 64, T <= 512)."""
     return dk == 64 and T <= 512
@@ -500,6 +524,11 @@ FUSED_ATTN_BWD = os.environ.get("ESP_FUSED_ATTN_BWD", "0") == "1"
 # ESP_ATTN_FWD32=1: the 32-row-block fused forward (relpos_attn_fwd_kernel, latest only) instead of
 # the 16-row-wave kernel (esp_relpos_attn_probs); kept for A/B measurements
 ATTN_FWD32 = os.environ.get("ESP_ATTN_FWD32", "0") == "1"
+# ESP_ATTN_DSCORES=1: the softmax / rel_shift adjoints in the dP GEMM's epilogue (esp_attn_dscores,
+# FlashAttention-2's row dot) instead of the dP GEMM + the row-wise adjoint pass.  Opt-in: measured
+# at C2 B=128 it is 412 + 73 us per layer against 59 + 266 (the epilogue's rel_shift scatter is one
+# scalar store per element; the row-wise pass writes each shifted bd row contiguously)
+ATTN_DSCORES = os.environ.get("ESP_ATTN_DSCORES", "0") == "1"
 
 
 def relpos_attn_bwd(dctx, ldd, vmat, ldv, attn, dS, dbd, ldp, nb, H, sqrt_dk, drop_p, seed, T, lds, v_off=0):

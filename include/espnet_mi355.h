@@ -217,6 +217,19 @@ int esp_relpos_attn_fwd(const float* qu, const float* qv, const float* kmat, lon
                         long ldp_row, int nb, int H, float sqrt_dk, const int* klen, float* attn,
                         float* pdrop, float drop_p, unsigned long long seed, int T, long lds,
                         void* stream);
+/* Rel-pos attention backward without the (Z,T,T) dP tensor (FlashAttention-2's row term):
+ * esp_attn_bwd_prep: dot[z*T+i] = dctx_i . ctx_i per head (= sum_j P_drop[i][j] dP[i][j]) and
+ * the bd-gradient elements without a rel_shift source zeroed; esp_attn_dscores: dP = dctx V^T
+ * on the MFMA with dS = P (drop'(dP) - dot) / sqrt(d_k) -> dS (pitch lds) and its latest / legacy
+ * rel_shift adjoint -> dbd (pitch ldp) in the epilogue.  Layouts as esp_relpos_attn_probs (dctx,
+ * ctx (B*T, H*dk) rows of pitch ldd / ldc; V rows at vmat + (b*T + j)*ldv + h*dk; attn / dS
+ * (Z,T) rows of pitch lds, 16-B aligned).  Replaces the dP GEMM + esp_attn_softmax_bwd_relpos
+ * (attention.py:64-96, 145-165 backward). */
+int esp_attn_bwd_prep(const float* dctx, long ldd, const float* ctx, long ldc, int nb, int H, int dk, int T,
+                      float* dot, float* dbd, long ldp, int relpos, void* stream);
+int esp_attn_dscores(const float* dctx, long ldd, const float* vmat, long ldv, const float* attn, const float* dot,
+                     float* dS, float* dbd, long ldp, int relpos, int nb, int H, int dk, float sqrt_dk,
+                     float drop_p, unsigned long long seed, int T, long lds, void* stream);
 /* Rel-pos attention probabilities for latest (relpos 1: p has P = 2T-1 rows) AND legacy
  * (relpos 2: p has P = T rows, legacy rel_shift attention.py:145-165) rel_shift, one wave per
  * 16 query rows with every score row in registers (no block synchronisation): ac and the bd band

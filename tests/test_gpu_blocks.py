@@ -63,17 +63,21 @@ def test_relpos_mha_block(dev, legacy):
     _check_grads(mod, P, "a")
 
 
-@pytest.mark.parametrize("fwd,legacy,fused_bwd", [("wave16", False, False), ("wave16", True, False),
-                                                   ("wave16", False, True), ("block32", False, False),
-                                                   ("block32", False, True)])
+@pytest.mark.parametrize("fwd,legacy,bwd", [("wave16", False, "dscores"), ("wave16", True, "dscores"),
+                                            ("wave16", False, "rowpass"), ("wave16", True, "rowpass"),
+                                            ("wave16", False, "fused"), ("block32", False, "dscores"),
+                                            ("block32", False, "fused")])
 @pytest.mark.parametrize("T,klens", [(29, [29, 23, 15]), (77, [77, 40, 9]), (130, [130, 129, 64])])
-def test_relpos_mha_fused_dk64(dev, T, klens, fwd, legacy, fused_bwd, monkeypatch):
+def test_relpos_mha_fused_dk64(dev, T, klens, fwd, legacy, bwd, monkeypatch):
     """d_k = 64 rel-pos attention through the fused score kernels — the 16-row-wave kernel
     (esp_relpos_attn_probs, latest and legacy rel_shift) and the 32-row-block kernel
-    (esp_relpos_attn_fwd, latest) — several row groups incl. a partial last one, against the
-    fp64 oracle."""
+    (esp_relpos_attn_fwd, latest) — several row groups incl. a partial last one, and the three
+    score-gradient paths (dscores: the softmax / rel_shift adjoints in the dP GEMM epilogue;
+    rowpass: dP GEMM + row-wise adjoint pass; fused: esp_relpos_attn_bwd), against the fp64
+    oracle."""
     from espnet_slurp_amd import kernels as K
-    monkeypatch.setattr(K, "FUSED_ATTN_BWD", fused_bwd)
+    monkeypatch.setattr(K, "FUSED_ATTN_BWD", bwd == "fused")
+    monkeypatch.setattr(K, "ATTN_DSCORES", bwd == "dscores")
     monkeypatch.setattr(K, "FLASH_ATTN", False)  # the materialised paths (flash: tests/test_gpu_flash.py)
     monkeypatch.setattr(K, "ATTN_FWD32", fwd == "block32")
     torch.manual_seed(3)
@@ -106,15 +110,19 @@ def _unfused(K, monkeypatch):
     monkeypatch.setattr(K, "relpos_probs_ok", lambda T, dk: False)
 
 
-@pytest.mark.parametrize("fwd,legacy,T", [("block32", False, 100), ("wave16", False, 100), ("wave16", True, 100),
-                                          ("wave16", False, 374), ("wave16", True, 374)])
-def test_relpos_fused_matches_unfused_with_dropout(dev, monkeypatch, fwd, legacy, T):
+@pytest.mark.parametrize("fwd,legacy,T,bwd", [("block32", False, 100, "fused"), ("wave16", False, 100, "fused"),
+                                              ("wave16", False, 100, "dscores"), ("wave16", True, 100, "dscores"),
+                                              ("wave16", False, 374, "dscores"), ("wave16", True, 374, "dscores"),
+                                              ("wave16", False, 374, "fused")])
+def test_relpos_fused_matches_unfused_with_dropout(dev, monkeypatch, fwd, legacy, T, bwd):
     """Same seeds -> the fused kernels reproduce the unfused path's (ac GEMM, bd GEMM, rel_shift +
-    softmax pass) attention probabilities and dropout masks (mask index row*T + j) and therefore
-    the same block output; T = 374 is the C2/C4/C5 subsampled length (score rows of pitch 376)."""
+    softmax pass; dP GEMM + row-wise adjoint pass) attention probabilities and dropout masks (mask
+    index row*T + j), the same block output and the same gradients; T = 374 is the C2/C4/C5
+    subsampled length (score rows of pitch 376)."""
     from espnet_slurp_amd import kernels as K
     monkeypatch.setattr(K, "FLASH_ATTN", False)  # the materialised paths (flash: tests/test_gpu_flash.py)
     monkeypatch.setattr(K, "ATTN_FWD32", fwd == "block32")
+    monkeypatch.setattr(K, "ATTN_DSCORES", bwd == "dscores")
     torch.manual_seed(4)
     B, D, H = 2, 256, 4
     klen = torch.tensor([T, (T * 3) // 5]).int().to(dev)
@@ -124,12 +132,14 @@ def test_relpos_fused_matches_unfused_with_dropout(dev, monkeypatch, fwd, legacy
     res = torch.randn(B * T, D, device=dev)
     pos = pos_table("legacy" if legacy else "latest", T, D, dev)
     dout = torch.randn(B * T, D, device=dev)
-    monkeypatch.setattr(K, "FUSED_ATTN_BWD", not legacy)
+    monkeypatch.setattr(K, "FUSED_ATTN_BWD", bwd == "fused")
     out_f, c_f = mod.fwd(x, res, pos, klen, B, T, 0.0, Seeds(7), True)
     dx_f = mod.bwd(c_f, dout)
     g_f = mod.flat.grad.clone()
     mod.flat.grad.zero_()
     _unfused(K, monkeypatch)
+    monkeypatch.setattr(K, "FUSED_ATTN_BWD", False)
+    monkeypatch.setattr(K, "ATTN_DSCORES", False)
     out_u, c_u = mod.fwd(x, res, pos, klen, B, T, 0.0, Seeds(7), True)
     dx_u = mod.bwd(c_u, dout)
     Tp = K.pitch(T)
