@@ -30,12 +30,12 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict_
 #pragma unroll
     for (int k = 0; k < 9; ++k) w[q][k] = W[(o4 * 4 + q) * 9 + k];
   }
-  const long npix = (long)B * T1 * F1;
-  for (long p = tid / D4; p < npix; p += nthr / D4) {
-    const int f1 = (int)(p % F1);
-    const long r = p / F1;
-    const int t1 = (int)(r % T1);
-    const int b = (int)(r / T1);
+  const unsigned npix = (unsigned)B * T1 * F1;  // < 2^32 (host check): 32-bit index math
+  for (unsigned p = (unsigned)(tid / D4); p < npix; p += (unsigned)(nthr / D4)) {
+    const unsigned r = p / (unsigned)F1;
+    const int f1 = (int)(p - r * (unsigned)F1);
+    const int b = (int)(r / (unsigned)T1);
+    const int t1 = (int)(r - (unsigned)b * T1);
     const float* xp = x + ((long)b * T + 2 * t1) * F + 2 * f1;
     float patch[9];
 #pragma unroll
@@ -50,7 +50,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict_
       for (int k = 0; k < 9; ++k) a += w[q][k] * patch[k];
       out[q] = fmaxf(a, 0.f);
     }
-    *reinterpret_cast<float4*>(z + p * D + o4 * 4) = make_float4(out[0], out[1], out[2], out[3]);
+    *reinterpret_cast<float4*>(z + (long)p * D + o4 * 4) = make_float4(out[0], out[1], out[2], out[3]);
   }
 }
 
@@ -191,6 +191,7 @@ ESP_API int esp_conv1_fwd(const float* x, const float* W, const float* bias, flo
   const int T1 = (T - 3) / 2 + 1, F1 = (F - 3) / 2 + 1;
   ESP_ARG_CHECK(256 % (D / 4) == 0, "esp_conv1_fwd: D/4 must divide 256");
   const long npix = (long)B * T1 * F1;
+  ESP_ARG_CHECK(npix < (1L << 32), "esp_conv1_fwd: %ld output pixels (32-bit index math)", npix);
   long nblk = (npix * (D / 4) + 255) / 256;
   if (nblk > 8192) nblk = 8192;  // ~16 pixels per thread at the C2 sizes: weights amortised
   hipLaunchKernelGGL(conv1_fwd_kernel, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, x, W, bias, z, B, T,

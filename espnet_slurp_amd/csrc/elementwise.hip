@@ -73,6 +73,27 @@ __global__ void scale_drop_kernel(const float* __restrict__ x, float* __restrict
   }
 }
 
+// float4 form (n % 4 == 0, 16-B aligned): same element indices for the dropout hash
+__global__ void scale_drop4_kernel(const float* __restrict__ x, float* __restrict__ y, long n4, float alpha,
+                                   uint32_t thr, float scale, uint64_t seed, const float* __restrict__ r, float beta,
+                                   const uint64_t* __restrict__ key) {
+  seed = esp::keyed(seed, key);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const float4 v4 = reinterpret_cast<const float4*>(x)[i];
+    float v[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (thr) v[e] = esp::keep_elem(seed, (uint64_t)(4 * i + e), thr) ? v[e] * scale : 0.f;
+      v[e] *= alpha;
+    }
+    if (r) {
+      const float4 r4 = reinterpret_cast<const float4*>(r)[i];
+      v[0] += beta * r4.x; v[1] += beta * r4.y; v[2] += beta * r4.z; v[3] += beta * r4.w;
+    }
+    reinterpret_cast<float4*>(y)[i] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
 // encoder input of the blocks: x = drop(x * xscale); pos = drop(pos)  (embedding.py:228-244)
 // decoder: x = drop(E[tok] * xscale + pe[l])                            (embedding.py:81-94)
 __global__ void embed_fwd_kernel(const int64_t* __restrict__ tok, const float* __restrict__ E,
@@ -308,8 +329,12 @@ ESP_API int esp_act_bwd(const float* dy, const float* h, float* dx, long n, int 
 ESP_API int esp_scale_dropout(const float* x, float* y, long n, float alpha, float drop_p, unsigned long long seed,
                               const float* r, float beta, void* stream) {
   const uint32_t thr = drop_threshold(drop_p);
-  hipLaunchKernelGGL(scale_drop_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, y, n, alpha, thr,
-                     thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed, r, beta, esp::rng_key_ptr());
+  if (n % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 && ((uintptr_t)r & 15) == 0)
+    hipLaunchKernelGGL(scale_drop4_kernel, dim3(grid_for(n / 4)), dim3(256), 0, (hipStream_t)stream, x, y, n / 4,
+                       alpha, thr, thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed, r, beta, esp::rng_key_ptr());
+  else
+    hipLaunchKernelGGL(scale_drop_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, y, n, alpha, thr,
+                       thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed, r, beta, esp::rng_key_ptr());
   ESP_CHECK_LAUNCH("esp_scale_dropout");
   return 0;
 }

@@ -661,6 +661,32 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(const double* __r
   dgamma[c] += (float)s2;
 }
 
+// float4 form of bn_bwd_apply_kernel (D % 4 == 0, 16-B aligned, M*D/4 < 2^31): 32-bit index
+// math, 1/M hoisted (the scalar form divides per element)
+__global__ void bn_bwd_apply4_kernel(float* __restrict__ dz, const float* __restrict__ y,
+                                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                                     const float* __restrict__ gamma, const float* __restrict__ sums, int n4, int D,
+                                     int M, int T, const int* __restrict__ tvalid) {
+  const int Tv = valid_T(tvalid, T);
+  if (tvalid) M = (M / T) * Tv;
+  const float invM = 1.0f / (float)M;
+  const int nq = D >> 2;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    const int row = i / nq, c = 4 * (i - row * nq);
+    if (tvalid && row % T >= Tv) continue;  // stays 0 (bn_swish_bwd_part_kernel)
+    const float4 d4 = reinterpret_cast<const float4*>(dz)[i], y4 = reinterpret_cast<const float4*>(y)[i];
+    const float dv[4] = {d4.x, d4.y, d4.z, d4.w}, yv[4] = {y4.x, y4.y, y4.z, y4.w};
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float rs = rstd[c + e];
+      const float xh = (yv[e] - mean[c + e]) * rs;
+      o[e] = gamma[c + e] * rs * (dv[e] - sums[c + e] * invM - xh * sums[D + c + e] * invM);
+    }
+    reinterpret_cast<float4*>(dz)[i] = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 // dy = gamma*rstd*(dz - S1/M - xhat*S2/M)   (in place over dz)
 __global__ void bn_bwd_apply_kernel(float* __restrict__ dz, const float* __restrict__ y, const float* __restrict__ mean,
                                     const float* __restrict__ rstd, const float* __restrict__ gamma,
@@ -874,7 +900,11 @@ ESP_API int esp_bn_swish_bwd(const float* ds, const float* y, const float* mean,
   hipLaunchKernelGGL(bn_swish_bwd_part_kernel, dim3(nb, (D + 255) / 256), dim3(256), 0, st, ds, y, mean, rstd, gamma,
                      beta, dy, M, D, rpb, work, T, tvalid);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, bnf_grid(D), dim3(1024), 0, st, work, nb, D, sums, dgamma, dbeta);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(gridn((long)M * D)), dim3(256), 0, st, dy, y, mean, rstd, gamma, sums,
+  if (vec4_ok((long)M * D, D, {dy, y}))
+    hipLaunchKernelGGL(bn_bwd_apply4_kernel, dim3(gridn((long)M * D / 4)), dim3(256), 0, st, dy, y, mean, rstd, gamma,
+                       sums, (int)((long)M * D / 4), D, M, T, tvalid);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(gridn((long)M * D)), dim3(256), 0, st, dy, y, mean, rstd, gamma, sums,
                      (long)M * D, D, M, T, tvalid);
   ESP_CHECK_LAUNCH("esp_bn_swish_bwd");
   return 0;
