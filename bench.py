@@ -263,6 +263,11 @@ def main():
         # the graph's kernels cannot be bracketed one by one: time the same GEMM launches (same
         # kernels, shapes and inputs) in one eager step right after the timed region
         eager = Trainer(model, opt, sched, TrainerOptions(grad_clip=5.0, use_amp=args.amp), distributed=world > 1)
+        torch.cuda.synchronize()
+        # hold the GPU for ~200 ms so the host enqueues the whole eager step (~1,500 launches)
+        # before the first GEMM runs: each event pair then brackets its kernel back to back,
+        # not the host's launch latency (which made the eager-replay figure box-dependent)
+        torch.cuda._sleep(int(5e8))
         K.profile_gemm_start()
         eager.train_one_step(batch)
         eager.resolve_pending()

@@ -1017,6 +1017,14 @@ struct GldsArgs {
 
 constexpr int GL_BK = 32;
 
+// K-contiguous slab image: row r (128 B = 8 quads) holds global quad q at position q ^ kc_swz(r).
+// A ds_read_b128 of frag16 serves 16-lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32)
+// whose lanes read rows r = lane & 31 at one quad; rows r and r+1 share a 256-B bank row, so the
+// 16 reads are conflict-free iff (r & 1, swz(r)) is distinct within each group: (r >> 1) & 7 is
+// (the round-1 r & 7 repeats at r + 8 inside a group: 2-way, SQ_LDS_BANK_CONFLICT 4 cycles per
+// ds_read, profiles/r02x_pmc_gemm.txt).
+__device__ __forceinline__ int kc_swz(int r) { return (r >> 1) & 7; }
+
 // One global_load_lds_dwordx4: lane l's 16 B at gptr land at lds_wave_base + 16*l.  Issued from
 // inline asm so that hipcc does not see an LDS-DMA store: with the builtin it cannot prove
 // the DMA target (the other buffer) disjoint from this slab's ds_reads and drains vmcnt(0)
@@ -1058,7 +1066,7 @@ struct Stage {
       const int slot = (i * 4 + wave) * 64 + lane;
       if constexpr (kKC) {
         const int r = slot >> 3, qs = slot & 7;
-        const int qq = qs ^ (r & 7);
+        const int qq = qs ^ kc_swz(r);
         const int gr = min(row0 + r, rows - 1);
         q[i] = 4 * qq;
         if constexpr (MODE == KC) p[i] = base + (long)gr * op.ld;
@@ -1119,7 +1127,7 @@ __device__ __forceinline__ void zero_tail(float* slab, int kv) {
   for (int idx = threadIdx.x; idx < ROWS * GL_BK; idx += NT) {
     if constexpr (MODE == KC || MODE == I2C_KC || MODE == I2CT_KC) {
       const int r = idx >> 5, k = idx & 31;
-      if (k >= kv) slab[(r * 8 + ((k >> 2) ^ (r & 7))) * 4 + (k & 3)] = 0.f;
+      if (k >= kv) slab[(r * 8 + ((k >> 2) ^ kc_swz(r))) * 4 + (k & 3)] = 0.f;
     } else {
       const int k = idx / ROWS;
       if (k >= kv) slab[idx] = 0.f;
@@ -1133,7 +1141,7 @@ __device__ __forceinline__ void frag16(const float* slab, int r, int h, float (&
   if constexpr (MODE == KC || MODE == I2C_KC || MODE == I2CT_KC) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float4 v = *reinterpret_cast<const float4*>(slab + (r * 8 + ((4 * h + j) ^ (r & 7))) * 4);
+      const float4 v = *reinterpret_cast<const float4*>(slab + (r * 8 + ((4 * h + j) ^ kc_swz(r))) * 4);
       f[4 * j + 0] = v.x; f[4 * j + 1] = v.y; f[4 * j + 2] = v.z; f[4 * j + 3] = v.w;
     }
   } else {
