@@ -155,10 +155,12 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
   const bool can_fwd = (MA == KC && (MB == KC || MB == RC)) || (MA == I2C_KC && MB == KC);
   const bool can_bwd = (MA == KC || MA == I2CT_KC) && MB == RC;
   const bool can_spec_fwd = MA == KC && MB == KC, can_spec_bwd = MA == KC && MB == RC;
+  const bool can_brelu = (MA == KC || MA == I2C_KC) && MB == KC;
   const bool can_pspec = (MA == KC || MA == RC) && (MB == KC || MB == RC);
   int kind = g.splits > 1 ? EPI_PLAIN : epi_kind_spec(g);
   if (kind == EPI_SMB && !(MA == KC && MB == KC && g.bf16 == 0)) return false;
-  if ((kind == EPI_BMUL && !can_spec_bwd) || ((kind == EPI_P0 || kind == EPI_PR) && !can_pspec) ||
+  if (((kind == EPI_BMUL || kind == EPI_RMASK) && !can_spec_bwd) || ((kind == EPI_P0 || kind == EPI_PR) && !can_pspec) ||
+      (kind == EPI_BRELU && !can_brelu) ||
       (kind >= EPI_BIAS && kind <= EPI_FFN_RELU && !can_spec_fwd))
     kind = epi_kind(g);
   if ((kind == EPI_FWD && !can_fwd) || (kind == EPI_BWD && !can_bwd)) return false;
@@ -170,6 +172,7 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
     x.c_a = make_fastdiv(g.a.ic.C);
     x.hw_a = make_fastdiv(g.a.ic.Ho * g.a.ic.Wo);
     x.wo_a = make_fastdiv(g.a.ic.Wo);
+    x.i2c_tap = g.a.ic.C % GL_BK == 0 && g.K % GL_BK == 0 ? 1 : 0;
   }
   if (MB == I2C_RC) {
     x.c_b = make_fastdiv(g.b.ic.C);

@@ -1,6 +1,8 @@
 // Instantiations of gemm_glds_kernel with the specialised (compile-time feature set) epilogues
 // of the production call sites: EPI_BIAS / EPI_BDR / EPI_FFN_SWISH / EPI_FFN_RELU for the linear
-// forward (KC x KC), EPI_BMUL for the FFN input gradient (KC x RC).  See store_spec.
+// forward (KC x KC), EPI_BRELU (bias + ReLU) for the conv2 forward (implicit-im2col I2C_KC x KC)
+// and KC x KC, EPI_BMUL for the FFN input gradient and EPI_RMASK for the gradient through conv2's
+// ReLU (KC x RC).  See store_spec.
 #include "gemm_kernels.h"
 
 namespace espg {
@@ -21,8 +23,12 @@ bool glds_launch_spec(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hip
       ESP_SPEC(EPI_BDR)
       ESP_SPEC(EPI_FFN_SWISH)
       ESP_SPEC(EPI_FFN_RELU)
+      ESP_SPEC(EPI_BRELU)
+    } else if constexpr (MA == I2C_KC && MB == KC) {
+      ESP_SPEC(EPI_BRELU)
     } else if constexpr (MA == KC && MB == RC) {
       ESP_SPEC(EPI_BMUL)
+      ESP_SPEC(EPI_RMASK)
     }
 #undef ESP_SPEC
   });

@@ -125,7 +125,7 @@ __device__ __forceinline__ long row_off(const GemmArgs& g, int m) {
 //   EPI 2: backward  drop'(acc + bias) * act'(pre)  (dropout mask regenerated), alpha, R
 // cbase = offset of batch z in C/R/aux/pre, dbase = z*M*N (dropout index base).
 enum { EPI_PLAIN = 0, EPI_FWD = 1, EPI_BWD = 2, EPI_BIAS = 3, EPI_BDR = 4, EPI_FFN_SWISH = 5, EPI_FFN_RELU = 6,
-       EPI_BMUL = 7, EPI_P0 = 8, EPI_PR = 9, EPI_SMB = 10 };
+       EPI_BMUL = 7, EPI_P0 = 8, EPI_PR = 9, EPI_SMB = 10, EPI_BRELU = 11, EPI_RMASK = 12 };
 __host__ __device__ inline int epi_kind(const GemmArgs& g) {
   return g.bwd_act ? EPI_BWD : ((g.bias || g.aux || g.act || g.drop_thresh) ? EPI_FWD : EPI_PLAIN);
 }
@@ -140,9 +140,12 @@ __host__ inline int epi_kind_spec(const GemmArgs& g) {
     return k;
   }
   if (k == EPI_PLAIN) return (g.splits > 1 || g.rowsum) ? k : (g.r ? EPI_PR : EPI_P0);
-  if (k == EPI_BWD)
-    return (g.bwd_act == ACT_MUL && !g.drop_thresh && !g.r && !g.bias && g.alpha == 1.0f) ? EPI_BMUL : k;
+  if (k == EPI_BWD) {
+    if (g.drop_thresh || g.r || g.bias || g.alpha != 1.0f) return k;
+    return g.bwd_act == ACT_MUL ? EPI_BMUL : g.bwd_act == ACT_RELU ? EPI_RMASK : k;
+  }
   if (g.bias && !g.aux && !g.act && !g.drop_thresh && !g.r) return EPI_BIAS;
+  if (g.bias && !g.aux && g.act == ACT_RELU && !g.drop_thresh && !g.r && g.alpha == 1.0f) return EPI_BRELU;
   if (g.bias && !g.aux && !g.act && g.drop_thresh && g.r) return EPI_BDR;
   if (g.bias && g.aux && g.drop_thresh && !g.r && g.act == (ACT_SWISH | ACT_AUX_DERIV)) return EPI_FFN_SWISH;
   if (g.bias && g.aux && g.drop_thresh && !g.r && g.act == (ACT_RELU | ACT_AUX_DERIV)) return EPI_FFN_RELU;
@@ -377,10 +380,12 @@ __device__ __forceinline__ void store_tiles_wide(const GemmArgs& g, int z, int m
 // bounds) per element at run time: hundreds of branches per tile and VGPR pressure that spills.
 // The production call sites use fixed feature sets, compiled in:
 //   EPI_BIAS       acc + bias                                    (q/k/v, pointwise_conv1, ...)
+//   EPI_BRELU      relu(acc + bias)                              (conv2: Conv2d + ReLU, implicit im2col A)
 //   EPI_BDR        alpha * drop(acc + bias) + beta * R           (linear_out, FFN w_2, pointwise_conv2)
 //   EPI_FFN_SWISH  h = drop(swish(acc + bias)), aux = dh/dv      (FFN w_1, ACT_AUX_DERIV)
 //   EPI_FFN_RELU   the same with ReLU                            (decoder FFN w_1)
 //   EPI_BMUL       acc * pre                                     (FFN w_2 input gradient, ACT_MUL)
+//   EPI_RMASK      pre > 0 ? acc : 0                             (input gradient through a ReLU output)
 //   EPI_P0         alpha * acc                                   (plain, unsplit)
 //   EPI_PR         alpha * acc + beta * R                        (gradient accumulation)
 //   EPI_SMB        dS = P * (drop'(acc) - dot_row) * alpha -> C, and its rel_shift adjoint -> dbd
@@ -389,11 +394,13 @@ __device__ __forceinline__ void store_tiles_wide(const GemmArgs& g, int z, int m
 // 32-column sub-tiles are all in range takes a path without per-element bounds checks.
 template <int EPI>
 struct EpiSpec {
-  static constexpr int act = EPI == EPI_FFN_SWISH ? ACT_SWISH : EPI == EPI_FFN_RELU ? ACT_RELU : ACT_NONE;
+  static constexpr int act =
+      EPI == EPI_FFN_SWISH ? ACT_SWISH : (EPI == EPI_FFN_RELU || EPI == EPI_BRELU) ? ACT_RELU : ACT_NONE;
   static constexpr bool bias = EPI == EPI_BIAS || EPI == EPI_BDR || act != ACT_NONE;
   static constexpr bool res = EPI == EPI_BDR || EPI == EPI_PR;
-  static constexpr bool drop = EPI == EPI_BDR || act != ACT_NONE;
-  static constexpr bool mul = EPI == EPI_BMUL;
+  static constexpr bool drop = EPI == EPI_BDR || EPI == EPI_FFN_SWISH || EPI == EPI_FFN_RELU;
+  static constexpr bool aux = EPI == EPI_FFN_SWISH || EPI == EPI_FFN_RELU;  // derivative stream
+  static constexpr bool mul = EPI == EPI_BMUL || EPI == EPI_RMASK;
 };
 template <int EPI, int TM, int TN, bool FULL>
 __device__ __forceinline__ void store_spec(const GemmArgs& g, int z, int mrow0, int ncol0, int lane,
@@ -487,13 +494,14 @@ __device__ __forceinline__ void store_spec(const GemmArgs& g, int z, int mrow0, 
             w = keep ? w * g.drop_scale : 0.f;
             dd = keep ? dd * g.drop_scale : 0.f;
           }
-          if constexpr (S::mul) w *= xs[e];
+          if constexpr (EPI == EPI_RMASK) w = xs[e] > 0.f ? w : 0.f;
+          else if constexpr (S::mul) w *= xs[e];
           w *= g.alpha;
           if constexpr (S::res) w += g.beta * xs[e];
           v[e] = w;
           d[e] = dd;
         }
-        if constexpr (S::act != ACT_NONE) st4(g.aux + off, d, false);
+        if constexpr (S::aux) st4(g.aux + off, d, false);
         if (FULL || n + 4 <= g.N) {
           st4(g.c + off, v, false);
         } else {  // last quad of a row with N % 4 != 0 (EPI_P0 / EPI_PR only): loads stayed inside ldc
@@ -1010,6 +1018,8 @@ struct GldsArgs {
   int t_T2, t_F2, t_C;
   int t_dt[4], t_df[4];
   const float* t_zeros;  // >= 16 zero bytes: the DMA source of lanes outside the grid
+  int i2c_tap;           // I2C_KC with C % 32 == 0 and K % 32 == 0: a slab lies in one tap (kt, kf),
+                         // so its column offset is one scalar per slab, not a division per lane
   int abl;             // diagnostic ablation bits (ESP_GEMM_ABL, timing only): 1 no DMA after the
                        // first slab, 2 no epilogue stores, 4 no k-loop barrier / waits, 16 dword
                        // (not float4) epilogue stores, 32 non-temporal epilogue stores
@@ -1094,6 +1104,13 @@ struct Stage {
   __device__ __forceinline__ void issue(const Operand& op, int K, int k0, float* dst, int wave, const FastDiv& fc,
                                         const FastDiv& fhw, const FastDiv& fwo, const GldsArgs* x = nullptr) const {
     int dt = 0, df = 0, o0 = 0;
+    long tap_off = 0;
+    if constexpr (MODE == I2C_KC) {  // the slab's tap and channel offset (wave-uniform)
+      if (x && x->i2c_tap) {
+        const int t = k0 / op.ic.C, kt = t / 3, kf = t - 3 * kt;
+        tap_off = ((long)kt * op.ic.W + kf) * op.ic.C + (k0 - t * op.ic.C);
+      }
+    }
     if constexpr (MODE == I2CT_KC) {  // the slab's tap (uniform: C % 32 == 0)
       const int t = k0 / x->t_C;
       o0 = k0 - t * x->t_C;
@@ -1106,7 +1123,10 @@ struct Stage {
       if constexpr (kKC) {
         const int k = min(k0 + q[i], (K - 1) & ~3);
         if constexpr (MODE == KC) lds_dma16(p[i] + k, ldsw);
-        else if constexpr (MODE == I2C_KC) lds_dma16(p[i] + i2c_col_off(op.ic, fc, k), ldsw);
+        else if constexpr (MODE == I2C_KC) {
+          if (x && x->i2c_tap) lds_dma16(p[i] + tap_off + q[i], ldsw);
+          else lds_dma16(p[i] + i2c_col_off(op.ic, fc, k), ldsw);
+        }
         else {
           const int a = ga[i] - dt, e = ge[i] - df;
           const bool in = a >= 0 && a < x->t_T2 && e >= 0 && e < x->t_F2;
