@@ -157,6 +157,9 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
   const bool can_spec_fwd = MA == KC && MB == KC, can_spec_bwd = MA == KC && MB == RC;
   const bool can_brelu = (MA == KC || MA == I2C_KC) && MB == KC;
   const bool can_pspec = (MA == KC || MA == RC) && (MB == KC || MB == RC);
+  // implicit-im2col A: every slab lies inside one tap (kt, kf), so the LDS-DMA source offset is
+  // one scalar per slab; other channel counts take the register-staged kernel
+  if (MA == I2C_KC && (g.a.ic.C % GL_BK || g.K % GL_BK)) return false;
   int kind = g.splits > 1 ? EPI_PLAIN : epi_kind_spec(g);
   if (kind == EPI_SMB && !(MA == KC && MB == KC && g.bf16 == 0)) return false;
   if (((kind == EPI_BMUL || kind == EPI_RMASK) && !can_spec_bwd) || ((kind == EPI_P0 || kind == EPI_PR) && !can_pspec) ||
@@ -172,7 +175,6 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
     x.c_a = make_fastdiv(g.a.ic.C);
     x.hw_a = make_fastdiv(g.a.ic.Ho * g.a.ic.Wo);
     x.wo_a = make_fastdiv(g.a.ic.Wo);
-    x.i2c_tap = g.a.ic.C % GL_BK == 0 && g.K % GL_BK == 0 ? 1 : 0;
   }
   if (MB == I2C_RC) {
     x.c_b = make_fastdiv(g.b.ic.C);

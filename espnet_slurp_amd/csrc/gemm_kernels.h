@@ -39,21 +39,25 @@ enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_SWISH = 2, ACT_MUL = 3 /* bwd_act onl
 // instead of regenerating the dropout mask and re-evaluating act'.
 constexpr int ACT_AUX_DERIV = 16;
 
-struct FastDiv {  // n / d for n < 2^31: (n * m) >> s, m = ceil(2^s / d), s = 31 + ceil(log2 d)
-  uint64_t m;
-  uint32_t s, d;
+// n / d for n < 2^31: (n * m) >> (31 + l), m = ceil(2^(31+l) / d), l = ceil(log2 d).  For d >= 2
+// m < 2^32, so the quotient is umulhi(n, m) >> (l - 1): one v_mul_hi_u32 and a shift (the 64-bit
+// product compiled to two v_mad_u64_u32 per division, in the implicit-im2col GEMMs' k-loops).
+struct FastDiv {
+  uint32_t m;   // d >= 2: ceil(2^(31+l) / d); d == 1: unused
+  uint32_t sh;  // l - 1
+  uint32_t d;
 };
 static FastDiv make_fastdiv(uint32_t d) {
   uint32_t l = 0;
   while ((1ull << l) < d) ++l;
   FastDiv f;
-  f.s = 31 + l;
-  f.m = ((1ull << f.s) + d - 1) / d;
   f.d = d;
+  f.sh = l ? l - 1 : 0;
+  f.m = d >= 2 ? (uint32_t)(((1ull << (31 + l)) + d - 1) / d) : 0u;
   return f;
 }
 __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
-  return (uint32_t)(((uint64_t)n * f.m) >> f.s);
+  return f.d == 1 ? n : (__umulhi(n, f.m) >> f.sh);
 }
 
 struct Im2col {  // NHWC input map [Bn][H][W][C], 3x3 kernel, stride 2, no padding
@@ -1018,8 +1022,6 @@ struct GldsArgs {
   int t_T2, t_F2, t_C;
   int t_dt[4], t_df[4];
   const float* t_zeros;  // >= 16 zero bytes: the DMA source of lanes outside the grid
-  int i2c_tap;           // I2C_KC with C % 32 == 0 and K % 32 == 0: a slab lies in one tap (kt, kf),
-                         // so its column offset is one scalar per slab, not a division per lane
   int abl;             // diagnostic ablation bits (ESP_GEMM_ABL, timing only): 1 no DMA after the
                        // first slab, 2 no epilogue stores, 4 no k-loop barrier / waits, 16 dword
                        // (not float4) epilogue stores, 32 non-temporal epilogue stores
@@ -1105,11 +1107,9 @@ struct Stage {
                                         const FastDiv& fhw, const FastDiv& fwo, const GldsArgs* x = nullptr) const {
     int dt = 0, df = 0, o0 = 0;
     long tap_off = 0;
-    if constexpr (MODE == I2C_KC) {  // the slab's tap and channel offset (wave-uniform)
-      if (x && x->i2c_tap) {
-        const int t = k0 / op.ic.C, kt = t / 3, kf = t - 3 * kt;
-        tap_off = ((long)kt * op.ic.W + kf) * op.ic.C + (k0 - t * op.ic.C);
-      }
+    if constexpr (MODE == I2C_KC) {  // the slab's tap and channel offset (wave-uniform scalars)
+      const int t = k0 / op.ic.C, kt = t / 3, kf = t - 3 * kt;
+      tap_off = ((long)kt * op.ic.W + kf) * op.ic.C + (k0 - t * op.ic.C);
     }
     if constexpr (MODE == I2CT_KC) {  // the slab's tap (uniform: C % 32 == 0)
       const int t = k0 / x->t_C;
@@ -1124,8 +1124,7 @@ struct Stage {
         const int k = min(k0 + q[i], (K - 1) & ~3);
         if constexpr (MODE == KC) lds_dma16(p[i] + k, ldsw);
         else if constexpr (MODE == I2C_KC) {
-          if (x && x->i2c_tap) lds_dma16(p[i] + tap_off + q[i], ldsw);
-          else lds_dma16(p[i] + i2c_col_off(op.ic, fc, k), ldsw);
+          lds_dma16(p[i] + tap_off + q[i], ldsw);  // C % 32 == 0, K % 32 == 0 (host-checked)
         }
         else {
           const int a = ga[i] - dt, e = ge[i] - df;
@@ -1258,9 +1257,9 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_ke
   TileCoord c = tile_coord<BNT>(g, x, t, G);
   Stage<MA, BM, NIA> sa;
   Stage<MB, BNT, NIB> sb;
-  sa.init(g.a, a_base(c), g.M, g.K, c.m0, x.c_a, x.hw_a, x.wo_a, wave, lane, &x);
+  sa.init(g.a, a_base(c), g.M, g.K, c.m0, x.c_a, x.hw_a, x.wo_a, wave, lane, MA == I2CT_KC ? &x : nullptr);
   sb.init(g.b, b_base(c), g.N, g.K, c.n0, x.c_b, x.hw_b, x.wo_b, wave, lane);
-  sa.issue(g.a, g.K, c.kbeg, smem, wave, x.c_a, x.hw_a, x.wo_a, &x);
+  sa.issue(g.a, g.K, c.kbeg, smem, wave, x.c_a, x.hw_a, x.wo_a, MA == I2CT_KC ? &x : nullptr);
   sb.issue(g.b, g.K, c.kbeg, smem + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
   wait_vm0();
   raw_barrier();
@@ -1358,7 +1357,7 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_ke
       const int k1 = c.kbeg + (kt + 1) * GL_BK;
       float* nxt = smem + (buf ^ 1) * BUF;  // last read before the previous barrier
       if (!(x.abl & 1)) {
-        sa.issue(g.a, g.K, k1, nxt, wave, x.c_a, x.hw_a, x.wo_a, &x);
+        sa.issue(g.a, g.K, k1, nxt, wave, x.c_a, x.hw_a, x.wo_a, MA == I2CT_KC ? &x : nullptr);
         sb.issue(g.b, g.K, k1, nxt + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
       }
       compute(smem + buf * BUF);
@@ -1369,9 +1368,9 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_ke
       float* nxt = smem + (buf ^ 1) * BUF;
       if (has_next) {
         cn = tile_coord<BNT>(g, x, tnext, G);
-        sa.init(g.a, a_base(cn), g.M, g.K, cn.m0, x.c_a, x.hw_a, x.wo_a, wave, lane, &x);
+        sa.init(g.a, a_base(cn), g.M, g.K, cn.m0, x.c_a, x.hw_a, x.wo_a, wave, lane, MA == I2CT_KC ? &x : nullptr);
         sb.init(g.b, b_base(cn), g.N, g.K, cn.n0, x.c_b, x.hw_b, x.wo_b, wave, lane);
-        sa.issue(g.a, g.K, cn.kbeg, nxt, wave, x.c_a, x.hw_a, x.wo_a, &x);
+        sa.issue(g.a, g.K, cn.kbeg, nxt, wave, x.c_a, x.hw_a, x.wo_a, MA == I2CT_KC ? &x : nullptr);
         sb.issue(g.b, g.K, cn.kbeg, nxt + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
       }
       const int kv = c.kend - (c.kbeg + (c.nk - 1) * GL_BK);
