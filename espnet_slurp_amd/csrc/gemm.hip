@@ -160,6 +160,11 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
   // implicit-im2col A: every slab lies inside one tap (kt, kf), so the LDS-DMA source offset is
   // one scalar per slab; other channel counts take the register-staged kernel
   if (MA == I2C_KC && (g.a.ic.C % GL_BK || g.K % GL_BK)) return false;
+  // implicit-im2col B: pixel offsets on 24-bit multiplies (i2c_pix_off24)
+  if (MB == I2C_RC) {
+    const long rows = (long)g.K / ((long)g.b.ic.Ho * g.b.ic.Wo) * g.b.ic.H * g.b.ic.W;  // Bn * H * W
+    if (rows >= (1L << 24) || rows * g.b.ic.C >= (1L << 32)) return false;
+  }
   int kind = g.splits > 1 ? EPI_PLAIN : epi_kind_spec(g);
   if (kind == EPI_SMB && !(MA == KC && MB == KC && g.bf16 == 0)) return false;
   if (((kind == EPI_BMUL || kind == EPI_RMASK) && !can_spec_bwd) || ((kind == EPI_P0 || kind == EPI_PR) && !can_pspec) ||

@@ -1063,6 +1063,16 @@ __device__ __forceinline__ long i2c_pix_off(const Im2col& ic, const FastDiv& fhw
   return (((long)bi * ic.H + 2 * ho) * ic.W + 2 * wo) * ic.C;
 }
 
+// the same on 24-bit multiplies (v_mad_u32_u24, full rate; v_mul_lo_u32 is quarter rate): legal
+// when Bn*H*W < 2^24 and the map holds < 2^32 elements (host-checked for I2C_RC operands)
+__device__ __forceinline__ uint32_t i2c_pix_off24(const Im2col& ic, const FastDiv& fhw, const FastDiv& fwo,
+                                                  uint32_t pix) {
+  const uint32_t bi = fdiv(pix, fhw);
+  const uint32_t rem = pix - __umul24(bi, fhw.d);
+  const uint32_t ho = fdiv(rem, fwo), wo = rem - __umul24(ho, fwo.d);
+  return __umul24(__umul24(__umul24(bi, (uint32_t)ic.H) + 2 * ho, (uint32_t)ic.W) + 2 * wo, (uint32_t)ic.C);
+}
+
 // Per-lane source bookkeeping for one operand: NI wave-instructions per slab.
 template <int MODE, int ROWS, int NI>
 struct Stage {
@@ -1134,7 +1144,7 @@ struct Stage {
       } else {
         const int k = min(k0 + q[i], K - 1);
         if constexpr (MODE == RC) lds_dma16(p[i] + (long)k * op.ld, ldsw);
-        else lds_dma16(p[i] + i2c_pix_off(op.ic, fhw, fwo, k), ldsw);
+        else lds_dma16(p[i] + i2c_pix_off24(op.ic, fhw, fwo, (uint32_t)k), ldsw);
       }
     }
   }
