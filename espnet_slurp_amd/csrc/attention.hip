@@ -247,6 +247,79 @@ __global__ __launch_bounds__(256) void softmax_bwd_relpos_kernel(const float* __
   }
 }
 
+// float4 form of softmax_bwd_relpos_kernel (lds % 4 == 0, 16-B aligned rows): lane L loads the
+// quads 4L + 256q of P and dP (1 KB per wave instruction instead of 256 B), writes dS as float4
+// (the pitch's padding columns get 0), and hands its 4 values through a per-wave LDS row so the
+// rel_shift-adjoint dbd stores stay one contiguous 256-B run per instruction (j = lane + 64e).
+// P2: sqrt(d_k) a power of two -> exact multiply by 1/sqrt(d_k).
+template <int Q, int REL, bool P2>  // Q quads per lane: 256*Q >= T
+__global__ __launch_bounds__(256) void softmax_bwd_relpos4_kernel(const float* __restrict__ attn, const float* dP,
+                                                                  float* dS, float* __restrict__ dbd, long ldp,
+                                                                  uint32_t thr, float dscale, uint64_t seed,
+                                                                  float sqrt_dk, long rows, int T, long lds,
+                                                                  const uint64_t* __restrict__ key) {
+  __shared__ __attribute__((aligned(16))) float stage[4][256 * Q];
+  seed = esp::keyed(seed, key);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long row = (long)blockIdx.x * 4 + wave;
+  if (row >= rows) return;
+  const int i = (int)(row % T);
+  const float* ar = attn + row * lds;
+  const float* gr = dP + row * lds;
+  float a[Q][4], g[Q][4];
+  float dot = 0.f;
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int j0 = 4 * lane + 256 * q;
+    float4 av = make_float4(0.f, 0.f, 0.f, 0.f), gv = av;
+    if (j0 < T) {  // the quad stays inside the row pitch (lds >= round_up(T, 4))
+      av = *reinterpret_cast<const float4*>(ar + j0);
+      gv = *reinterpret_cast<const float4*>(gr + j0);
+    }
+    const float aa[4] = {av.x, av.y, av.z, av.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int j = j0 + e;
+      float x = j < T ? gg[e] : 0.f;
+      if (thr) x = esp::keep_elem(seed, (uint64_t)(row * T + j), thr) ? x * dscale : 0.f;
+      a[q][e] = j < T ? aa[e] : 0.f;
+      g[q][e] = x;
+      dot += a[q][e] * x;
+    }
+  }
+  dot = esp::wave_sum(dot);
+  const float inv = 1.0f / sqrt_dk;
+  float* sr = dS + row * lds;
+  float* st = stage[wave];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int j0 = 4 * lane + 256 * q;
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = P2 ? a[q][e] * (g[q][e] - dot) * inv : a[q][e] * (g[q][e] - dot) / sqrt_dk;
+    if (j0 < T) *reinterpret_cast<float4*>(sr + j0) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(st + j0) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+  asm volatile("" ::: "memory");  // wave-private LDS row: in-order within the wave
+  float* br = dbd + row * ldp;
+  const int sh = T - 1 - i;
+#pragma unroll
+  for (int e = 0; e < 4 * Q; ++e) {
+    const int j = lane + 64 * e;
+    if (j < T) {
+      const float v = st[j];
+      if (REL == 1 || j <= i) br[j + sh] = v;
+      else if (j >= i + 2) br[ldp + j - i - 2] = v;  // row i+1 of the same z (i + 1 < T here)
+    }
+  }
+  if (REL == 1) {
+    for (int k = lane; k < sh; k += 64) br[k] = 0.f;
+    for (int k = sh + T + lane; k < 2 * T - 1; k += 64) br[k] = 0.f;
+  } else if (i == 0) {
+    for (int k = lane; k < sh; k += 64) br[k] = 0.f;
+  }
+}
+
 // Fused latest rel-pos attention backward, one block per (32 query rows, z):
 //   dP = dctx V^T on the MFMA (key tiles w, w+4, ... per wave; V rows from the fused qkv),
 //   g  = dropout'(dP) (mask regenerated), dot_i = sum_j attn*g (xor shuffles + LDS exchange),
@@ -1076,6 +1149,31 @@ ESP_API int esp_attn_softmax_bwd_relpos(const float* attn, const float* dP, floa
   const float ds = thr ? 1.f / (1.f - drop_p) : 1.f;
   dim3 grid((unsigned)((rows + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
+  const bool p2 = sqrt_dk > 0.f && (__builtin_bit_cast(uint32_t, sqrt_dk) & 0x7fffffu) == 0;
+  if (T <= 1024 && lds % 4 == 0 && ((uintptr_t)attn & 15) == 0 && ((uintptr_t)dP & 15) == 0 &&
+      ((uintptr_t)dS & 15) == 0) {
+#define ESP_SB4(Q, R)                                                                                             \
+  do {                                                                                                            \
+    if (p2)                                                                                                       \
+      hipLaunchKernelGGL((softmax_bwd_relpos4_kernel<Q, R, true>), grid, dim3(256), 0, st, attn, dP, dS, dbd, ldp, \
+                         thr, ds, (uint64_t)seed, sqrt_dk, rows, T, lds, esp::rng_key_ptr());                     \
+    else                                                                                                          \
+      hipLaunchKernelGGL((softmax_bwd_relpos4_kernel<Q, R, false>), grid, dim3(256), 0, st, attn, dP, dS, dbd,     \
+                         ldp, thr, ds, (uint64_t)seed, sqrt_dk, rows, T, lds, esp::rng_key_ptr());                \
+  } while (0)
+#define ESP_SB4R(Q)              \
+  do {                           \
+    if (relpos == 1) ESP_SB4(Q, 1); \
+    else ESP_SB4(Q, 2);          \
+  } while (0)
+    if (T <= 256) ESP_SB4R(1);
+    else if (T <= 512) ESP_SB4R(2);
+    else ESP_SB4R(4);
+#undef ESP_SB4R
+#undef ESP_SB4
+    ESP_CHECK_LAUNCH("esp_attn_softmax_bwd_relpos");
+    return 0;
+  }
 #define ESP_SBR(PER)                                                                                         \
   do {                                                                                                       \
     if (relpos == 1)                                                                                         \

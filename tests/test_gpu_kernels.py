@@ -371,8 +371,10 @@ def test_relpos_softmax_and_adjoint(dev, legacy, padded):
     dbd2 = torch.full((Z * T * Pp,), float("nan"), device=dev)
     K.attn_softmax_bwd_relpos(att, dS2, dS2, dbd2, Pp, 0.0, 0, math.sqrt(dk), Z * T, T, Tp,
                               relpos=2 if legacy else 1)
-    assert torch.equal(dS2.view(Z, T, Tp)[:, :, :T], dS.view(Z, T, Tp)[:, :, :T])
-    assert torch.equal(dbd2.view(Z, T, Pp)[:, :, :P], dbd.view(Z, T, Pp)[:, :, :P])
+    # (the fused pass sums the row dot in quads: same terms, another order -> ulp-level differences)
+    assert rel_err(dS2.cpu().view(Z, T, Tp)[:, :, :T], dS.cpu().view(Z, T, Tp)[:, :, :T]) < 1e-6
+    assert rel_err(dbd2.cpu().view(Z, T, Pp)[:, :, :P], dbd.cpu().view(Z, T, Pp)[:, :, :P]) < 1e-6
+    assert rel_err(dbd2.cpu().view(Z, T, Pp)[:, :, :P], bdt.grad) < 1e-5
 
 
 def test_causal_softmax_with_dropout(dev):
