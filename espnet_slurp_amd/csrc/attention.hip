@@ -733,18 +733,25 @@ __global__ __launch_bounds__(256) void relpos_attn_fwd_kernel(
 // LDS: ring rows of RW_PITCH floats (row groups r and r+4 of a 32-lane half 16 banks apart).
 constexpr int RW_ROWS = 16, RW_PITCH = 37;
 constexpr int RW_SPITCH = 68;  // store-transpose rows: the two row groups of a ds_write_b32 half 16 banks apart
-template <int NTA, bool P2, bool LEGACY>  // NTA >= ceil(T/16) key tiles held in registers
-__global__ __launch_bounds__(256, 2) void relpos_attn_fwd16_kernel(
+// SPLIT = 2 (opt-in, ESP_ATTN_SPLIT=2): a row group's keys are shared by two waves of the block
+// (tiles [0, NTA) and [NTA, 2 NTA)), half the score registers each (3 waves per SIMD instead of
+// 2); the row max and sum are combined through LDS with one block barrier each.  Measured at C2
+// B=128: 398 vs 395 us (327 vs 309 without dropout) — the kernel is not latency-bound but bound
+// by the SIMD's shared f32 MFMA / VALU issue, so the extra occupancy buys nothing.
+template <int NTA, bool P2, bool LEGACY, int SPLIT = 1>  // SPLIT * NTA >= ceil(T/16) key tiles
+__global__ __launch_bounds__(256, SPLIT == 2 ? 3 : 2) void relpos_attn_fwd16_kernel(
     const float* __restrict__ qu, const float* __restrict__ qv, const float* __restrict__ kmat, long ldk,
     const float* __restrict__ pm, long ldpm, int nb, float sqrt_dk, const int* __restrict__ klen,
     float* __restrict__ attn, float* __restrict__ pdrop, uint32_t thr, float dscale, uint64_t seed, int T, long lds,
     const uint64_t* __restrict__ key) {
   __shared__ float ring[4][RW_ROWS * RW_PITCH];
   __shared__ __attribute__((aligned(16))) float stage[4][RW_ROWS * RW_SPITCH];
+  __shared__ float xch[2][4][RW_ROWS];  // SPLIT 2: per-wave row max / row sum partials
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int z = blockIdx.y;
-  const int i0 = (blockIdx.x * 4 + wave) * RW_ROWS;
-  if (i0 >= T) return;  // the whole wave: nothing below synchronises the block
+  const int i0 = (SPLIT == 1 ? blockIdx.x * 4 + wave : blockIdx.x * 2 + (wave >> 1)) * RW_ROWS;
+  const int t0 = SPLIT == 1 ? 0 : (wave & 1) * NTA;  // first key tile of this wave
+  if (SPLIT == 1 && i0 >= T) return;  // the whole wave: nothing below synchronises the block
   seed = esp::keyed(seed, key);
   const int head = z / nb, b = z - head * nb;
   const int li = lane & 15, q4 = lane >> 4;
@@ -781,29 +788,32 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd16_kernel(
     for (int r = 0; r < 4; ++r) rg[(4 * q4 + r) * RW_PITCH + ((16 * m + li) & 31)] = s[r];
   };
   // fragments DEPTH tiles ahead: K(t) in kb[t % NB], band-block p rows P(m) in pb[m % NB]
-  constexpr int DEPTH = 2, NB = DEPTH + 1;
-  float kb[NB][16], pb[NB][16];
+  constexpr int DEPTH = SPLIT == 2 ? 1 : 2, NB = DEPTH + 1;  // split: 3 waves per SIMD hide a tile less
+  float kb[NB][16], pb[NB][16];  // indexed by the tile / block offset from t0
 #pragma unroll
-  for (int d = 0; d < DEPTH; ++d) ld16(k_row(d), kb[d]);
+  for (int d = 0; d < DEPTH; ++d) ld16(k_row(t0 + d), kb[d]);
 #pragma unroll
-  for (int d = 0; d <= DEPTH; ++d) ld16(p_row(d), pb[d]);
-  {  // band block 0 (below T for every g: A rows q_v[i] in both variants)
+  for (int d = 0; d <= DEPTH; ++d) ld16(p_row(t0 + d), pb[d]);
+  {  // band block t0 (block 0 lies below T for every g: A rows q_v[i] in both variants)
+    const bool shifted = LEGACY && t0 > g;
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int c = 0; c < 16; ++c) s = __builtin_amdgcn_mfma_f32_16x16x4f32(av[c], pb[0][c], s, 0, 0, 0);
-    put_band(ring0, 0, s);
+    for (int c = 0; c < 16; ++c)
+      s = __builtin_amdgcn_mfma_f32_16x16x4f32(shifted ? av2[c] : av[c], pb[0][c], s, 0, 0, 0);
+    put_band(ring0, t0, s);
   }
 
   f32x4 sc[NTA];
 #pragma unroll
-  for (int t = 0; t < NTA; ++t) {
+  for (int tt = 0; tt < NTA; ++tt) {
+    const int t = t0 + tt;
     // no `t < nt` branch: tiles past the last key are computed on clamped rows and masked
     // (j >= T > kl), which keeps every s_waitcnt vmcnt counted across the whole unrolled loop
     // (a conditional tile makes the compiler merge its counts pessimistically: vmcnt(4) at every
     // tile, i.e. the prefetched fragments waited for one tile early)
     {
-      const float(&kf)[16] = kb[t % NB];
-      const float(&pf)[16] = pb[(t + 1) % NB];
+      const float(&kf)[16] = kb[tt % NB];
+      const float(&pf)[16] = pb[(tt + 1) % NB];
       const bool shifted = LEGACY && t + 1 > g;  // legacy band block t+1 at/above table position T
       f32x4 a = {0.f, 0.f, 0.f, 0.f}, s = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -811,8 +821,8 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd16_kernel(
         a = __builtin_amdgcn_mfma_f32_16x16x4f32(au[c], kf[c], a, 0, 0, 0);
         s = __builtin_amdgcn_mfma_f32_16x16x4f32(shifted ? av2[c] : av[c], pf[c], s, 0, 0, 0);
       }
-      ld16(k_row(t + DEPTH), kb[(t + DEPTH) % NB]);  // clamped rows: always safe to fetch
-      ld16(p_row(t + 1 + DEPTH), pb[(t + 1 + DEPTH) % NB]);
+      ld16(k_row(t + DEPTH), kb[(tt + DEPTH) % NB]);  // clamped rows: always safe to fetch
+      ld16(p_row(t + 1 + DEPTH), pb[(tt + 1 + DEPTH) % NB]);
       put_band(ring0, t + 1, s);
       asm volatile("" ::: "memory");  // ring writes before the shifted reads (LDS is in order per wave)
       const int j = t * 16 + li;
@@ -823,7 +833,7 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd16_kernel(
         float bd = ring0[at];
         if (LEGACY && j == i + 1) bd = 0.f;
         const float sv = a[r] + bd;
-        sc[t][r] = j < kl ? (P2 ? sv * inv_sqrt_dk : sv / sqrt_dk) : -INFINITY;
+        sc[tt][r] = j < kl ? (P2 ? sv * inv_sqrt_dk : sv / sqrt_dk) : -INFINITY;
       }
       asm volatile("" ::: "memory");  // ... and these reads before the next tile's ring writes
     }
@@ -838,7 +848,19 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd16_kernel(
     for (int t = 1; t < NTA; ++t) v = fmaxf(v, sc[t][r]);
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    if (v == -INFINITY) v = 0.f;  // fully masked row: every e below is exp(-inf) = 0
+    nm[r] = v;
+  }
+  if constexpr (SPLIT == 2) {  // combine with the partner wave's half of the keys
+    if (li == 0)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xch[0][wave][4 * q4 + r] = nm[r];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) nm[r] = fmaxf(nm[r], xch[0][wave ^ 1][4 * q4 + r]);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float v = nm[r] == -INFINITY ? 0.f : nm[r];  // fully masked row: every e below is exp(-inf) = 0
     nm[r] = P2 ? -v * 1.4426950408889634f : -v;
   }
 #pragma unroll
@@ -853,8 +875,21 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd16_kernel(
     }
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
-    inv[r] = v > 0.f ? 1.0f / v : 0.f;
+    inv[r] = v;
   }
+  if constexpr (SPLIT == 2) {
+    if (li == 0)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xch[1][wave][4 * q4 + r] = inv[r];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {  // the two halves in a fixed order (lower key half first)
+      const float o = xch[1][wave ^ 1][4 * q4 + r];
+      inv[r] = (wave & 1) ? o + inv[r] : inv[r] + o;
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) inv[r] = inv[r] > 0.f ? 1.0f / inv[r] : 0.f;
   // probabilities -> HBM through a per-wave LDS transpose, 64 columns (4 key tiles) at a time:
   // lane L then holds 4 consecutive columns of row 4p + (L >> 4), so one store instruction writes
   // 4 rows x 256 contiguous bytes (instead of 4 rows x 64 B from the accumulator layout).  A quad
@@ -879,27 +914,27 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd16_kernel(
     constexpr bool DROP = decltype(drop_c)::value;
 #pragma unroll
     for (int t4 = 0; t4 < NTA; t4 += 4) {
-      if (16 * t4 >= T) break;
+      if (16 * (t0 + t4) >= T) break;
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
         for (int r = 0; r < 4; ++r) stg[(4 * q4 + r) * RW_SPITCH + 16 * tt + li] = sc[t4 + tt][r] * inv[r];
       asm volatile("" ::: "memory");
-      const bool jok = 16 * t4 + sc4 < T;
+      const bool jok = 16 * (t0 + t4) + sc4 < T;
 #pragma unroll
       for (int ps = 0; ps < 4; ++ps) {
         const float4 v = *reinterpret_cast<const float4*>(stg + (4 * ps + sr) * RW_SPITCH + sc4);
         if (rok[ps] && jok) {
-          float* ar = abase[ps] + 16 * t4;
+          float* ar = abase[ps] + 16 * (t0 + t4);
           *reinterpret_cast<float4*>(ar) = v;
           if (DROP) {
-            const uint64_t ix = ibase[ps] + 16 * t4;
+            const uint64_t ix = ibase[ps] + 16 * (t0 + t4);
             float4 d;
             d.x = esp::keep_elem(seed, ix, thr) ? v.x * dscale : 0.f;
             d.y = esp::keep_elem(seed, ix + 1, thr) ? v.y * dscale : 0.f;
             d.z = esp::keep_elem(seed, ix + 2, thr) ? v.z * dscale : 0.f;
             d.w = esp::keep_elem(seed, ix + 3, thr) ? v.w * dscale : 0.f;
-            *reinterpret_cast<float4*>(dbase[ps] + 16 * t4) = d;
+            *reinterpret_cast<float4*>(dbase[ps] + 16 * (t0 + t4)) = d;
           }
         }
       }
@@ -1108,9 +1143,35 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
   if (!thr) pdrop = nullptr;
   const float ds = thr ? 1.f / (1.f - drop_p) : 1.f;
   const int nt = (T + 15) / 16;
-  dim3 grid((unsigned)((T + 4 * RW_ROWS - 1) / (4 * RW_ROWS)), (unsigned)(nb * H));
+  static int split_env = -1;  // ESP_ATTN_SPLIT=1|2: one wave per row group / two (key halves)
+  if (split_env < 0) split_env = getenv("ESP_ATTN_SPLIT") ? atoi(getenv("ESP_ATTN_SPLIT")) : 1;
+  const bool split = split_env == 2 && nt > 8 && nt <= 32;
+  dim3 grid((unsigned)((T + (split ? 2 : 4) * RW_ROWS - 1) / ((split ? 2 : 4) * RW_ROWS)), (unsigned)(nb * H));
   hipStream_t st = (hipStream_t)stream;
   const bool p2 = sqrt_dk > 0.f && (__builtin_bit_cast(uint32_t, sqrt_dk) & 0x7fffffu) == 0;
+  if (split) {
+#define ESP_RS3(N, P2_, L_)                                                                                            \
+  hipLaunchKernelGGL((relpos_attn_fwd16_kernel<N, P2_, L_, 2>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p, ldp_row, \
+                     nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr())
+#define ESP_RS(N)                     \
+  do {                                \
+    if (relpos == 2) {                \
+      if (p2) ESP_RS3(N, true, true); \
+      else ESP_RS3(N, false, true);   \
+    } else {                          \
+      if (p2) ESP_RS3(N, true, false); \
+      else ESP_RS3(N, false, false);  \
+    }                                 \
+  } while (0)
+    const int half = (nt + 1) / 2;
+    if (half <= 8) ESP_RS(8);
+    else if (half <= 12) ESP_RS(12);
+    else ESP_RS(16);
+#undef ESP_RS
+#undef ESP_RS3
+    ESP_CHECK_LAUNCH("esp_relpos_attn_probs");
+    return 0;
+  }
 #define ESP_RW3(N, P2_, L_)                                                                                         \
   hipLaunchKernelGGL((relpos_attn_fwd16_kernel<N, P2_, L_>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p, ldp_row, \
                      nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr())
