@@ -272,6 +272,7 @@ def main():
         eager.train_one_step(batch)
         eager.resolve_pending()
     gemm_flops, gemm_ms, gemm_launches, gemm_shapes = K.profile_gemm_stop(by_shape=True)
+    attn_flops, attn_bytes, attn_ms, attn_launches = K.profile_attn_stop()
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=device)
     if world > 1:
@@ -316,6 +317,14 @@ def main():
                                    + (" in the timed region)" if args.eager else " on an eager replay of the step)"),
                          "launches": gemm_launches,
                          "avg_launch_us": round(1e3 * gemm_ms / max(1, gemm_launches), 2)},
+            # the second kernel the round-1 verdict named: rel-pos attention probabilities
+            # (MFMA work of its ac + band tiles; P and its dropout copy written once)
+            "attention_roofline": None if not attn_launches else {
+                "kernel": "relpos_attn_fwd16_kernel (esp_relpos_attn_probs), HIP events on the same eager replay",
+                "launches": attn_launches, "avg_launch_us": round(1e3 * attn_ms / attn_launches, 2),
+                "achieved": round(attn_flops / (attn_ms * 1e-3) / 1e12, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(attn_flops / (attn_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+                "write_GBps": round(attn_bytes / (attn_ms * 1e-3) / 1e9, 1)},
             "step_roofline": {"train_gflop_per_utt": round(train / 1e9, 2),
                               "achieved_tflops": round(value / world * train / 1e12, 2),
                               "frac_of_mfma_peak": round(value / world * train / 1e12 / peak, 4)},

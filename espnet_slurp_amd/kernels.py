@@ -78,10 +78,24 @@ def h2d(t: torch.Tensor, device) -> torch.Tensor:
 _PROF = None  # when a list: (algorithmic flops, start event, end event) per GEMM launch
 
 
+_PROF_ATTN = None  # when a list: (MFMA flops, bytes written, start event, end event) per attention-probabilities launch
+
+
 def profile_gemm_start():
-    """Record a HIP event pair around every GEMM launch (on the launch stream) from now on."""
-    global _PROF
+    """Record a HIP event pair around every GEMM launch (on the launch stream) from now on, and
+    around every rel-pos attention-probabilities launch (profile_attn_stop)."""
+    global _PROF, _PROF_ATTN
     _PROF = []
+    _PROF_ATTN = []
+
+
+def profile_attn_stop():
+    """-> (MFMA flops, bytes written, kernel ms, launches) of the esp_relpos_attn_probs launches
+    since profile_gemm_start()."""
+    global _PROF_ATTN
+    prof, _PROF_ATTN = _PROF_ATTN or [], None
+    torch.cuda.synchronize()
+    return (sum(p[0] for p in prof), sum(p[1] for p in prof), sum(p[2].elapsed_time(p[3]) for p in prof), len(prof))
 
 
 def profile_gemm_stop(by_shape: bool = False):
@@ -469,9 +483,20 @@ def relpos_attn_probs(q_u, q_v, kmat, ldk, p, ldp_row, relpos, nb, H, sqrt_dk, k
     """Rel-pos attention probabilities, latest (relpos 1) or legacy (relpos 2), one wave per 16
     query rows (esp_relpos_attn_probs)."""
     _f32(q_u, q_v, kmat, p, attn, pdrop)
+    if _PROF_ATTN is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
     _native.call("esp_relpos_attn_probs", _p(q_u), _p(q_v), _p(kmat, k_off), ldk, _p(p), ldp_row, int(relpos), nb, H,
                  float(sqrt_dk), _p(klen_i32), _p(attn), _p(pdrop), float(drop_p), int(seed) & (2 ** 64 - 1), T, lds,
                  _st())
+    if _PROF_ATTN is not None:
+        ev1.record()
+        nt = (T + 15) // 16
+        # per (z, 16-row group): ac over nt key tiles + nt+1 band blocks, 16 x 16 x 64 MACs each
+        flops = 2.0 * 16 * 16 * 64 * (2 * nt + 1) * nt * nb * H
+        written = 4.0 * nb * H * T * T * (2 if (pdrop is not None and drop_p > 0) else 1)
+        _PROF_ATTN.append((flops, written, ev0, ev1))
 
 
 def attn_bwd_prep(dctx, ldd, ctx, ldc, nb, H, dk, T, dot, dbd, ldp, relpos):
