@@ -277,11 +277,22 @@ __global__ __launch_bounds__(256) void softmax_bwd_relpos4_kernel(const float* _
       gv = *reinterpret_cast<const float4*>(gr + j0);
     }
     const float aa[4] = {av.x, av.y, av.z, av.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w};
+    bool kp[4] = {true, true, true, true};
+    if (thr) {
+      const uint64_t ix = (uint64_t)(row * T + j0);
+      if ((T & 1) == 0) {  // row * T even: two hash pairs per quad (esp::keep_pair)
+        esp::keep_pair(seed, ix, thr, kp[0], kp[1]);
+        esp::keep_pair(seed, ix + 2, thr, kp[2], kp[3]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) kp[e] = esp::keep_elem(seed, ix + e, thr);
+      }
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int j = j0 + e;
       float x = j < T ? gg[e] : 0.f;
-      if (thr) x = esp::keep_elem(seed, (uint64_t)(row * T + j), thr) ? x * dscale : 0.f;
+      if (thr) x = kp[e] ? x * dscale : 0.f;
       a[q][e] = j < T ? aa[e] : 0.f;
       g[q][e] = x;
       dot += a[q][e] * x;
@@ -910,6 +921,7 @@ __global__ __launch_bounds__(256, SPLIT == 2 ? 3 : 2) void relpos_attn_fwd16_ker
     dbase[ps] = pdrop ? pdrop + row * lds + sc4 : nullptr;
     ibase[ps] = (uint64_t)(row * T + sc4);
   }
+  const bool even_T = (T & 1) == 0;  // uniform
   auto store_rows = [&](auto drop_c) {
     constexpr bool DROP = decltype(drop_c)::value;
 #pragma unroll
@@ -930,10 +942,20 @@ __global__ __launch_bounds__(256, SPLIT == 2 ? 3 : 2) void relpos_attn_fwd16_ker
           if (DROP) {
             const uint64_t ix = ibase[ps] + 16 * (t0 + t4);
             float4 d;
-            d.x = esp::keep_elem(seed, ix, thr) ? v.x * dscale : 0.f;
-            d.y = esp::keep_elem(seed, ix + 1, thr) ? v.y * dscale : 0.f;
-            d.z = esp::keep_elem(seed, ix + 2, thr) ? v.z * dscale : 0.f;
-            d.w = esp::keep_elem(seed, ix + 3, thr) ? v.w * dscale : 0.f;
+            bool k0, k1, k2, k3;
+            if (even_T) {  // row * T even: the quad is two hash pairs
+              esp::keep_pair(seed, ix, thr, k0, k1);
+              esp::keep_pair(seed, ix + 2, thr, k2, k3);
+            } else {
+              k0 = esp::keep_elem(seed, ix, thr);
+              k1 = esp::keep_elem(seed, ix + 1, thr);
+              k2 = esp::keep_elem(seed, ix + 2, thr);
+              k3 = esp::keep_elem(seed, ix + 3, thr);
+            }
+            d.x = k0 ? v.x * dscale : 0.f;
+            d.y = k1 ? v.y * dscale : 0.f;
+            d.z = k2 ? v.z * dscale : 0.f;
+            d.w = k3 ? v.w * dscale : 0.f;
             *reinterpret_cast<float4*>(dbase[ps] + 16 * (t0 + t4)) = d;
           }
         }

@@ -43,9 +43,22 @@ __device__ __forceinline__ uint32_t rng_u32(uint64_t seed, uint64_t idx) {
 // on device by esp_rng_advance) while the host-side seeds stay baked into the graph.
 const uint64_t* rng_key_ptr();
 __device__ __forceinline__ uint64_t keyed(uint64_t seed, const uint64_t* key) { return key ? seed ^ *key : seed; }
-// keep with probability (1-p): threshold = p * 2^32
+// Dropout keep decision, probability (1-p) with threshold = p * 2^32 (host).  Each 32-bit hash
+// serves an element PAIR (2k, 2k+1), 16 bits each against the threshold rounded to 1/65536
+// (p = 0.1 -> 0.1000061): kernels that own consecutive elements draw half the hashes
+// (keep_pair), and every other site still draws element by element — the same masks.
+__device__ __forceinline__ uint32_t thr16_of(uint32_t thresh) {
+  return (uint32_t)(((uint64_t)thresh + 32768u) >> 16);
+}
 __device__ __forceinline__ bool keep_elem(uint64_t seed, uint64_t idx, uint32_t thresh) {
-  return rng_u32(seed, idx) >= thresh;
+  const uint32_t h = rng_u32(seed, idx >> 1);
+  return ((idx & 1) ? (h >> 16) : (h & 0xffffu)) >= thr16_of(thresh);
+}
+// elements idx_even and idx_even + 1 (idx_even even) from one hash
+__device__ __forceinline__ void keep_pair(uint64_t seed, uint64_t idx_even, uint32_t thresh, bool& k0, bool& k1) {
+  const uint32_t h = rng_u32(seed, idx_even >> 1), t = thr16_of(thresh);
+  k0 = (h & 0xffffu) >= t;
+  k1 = (h >> 16) >= t;
 }
 
 // sigmoid on the hardware exp2 / reciprocal (v_exp_f32, v_rcp_f32, ~1 ulp each) instead of libm

@@ -81,9 +81,14 @@ __global__ void scale_drop4_kernel(const float* __restrict__ x, float* __restric
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
     const float4 v4 = reinterpret_cast<const float4*>(x)[i];
     float v[4] = {v4.x, v4.y, v4.z, v4.w};
+    bool kp[4] = {true, true, true, true};
+    if (thr) {
+      esp::keep_pair(seed, (uint64_t)(4 * i), thr, kp[0], kp[1]);
+      esp::keep_pair(seed, (uint64_t)(4 * i + 2), thr, kp[2], kp[3]);
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      if (thr) v[e] = esp::keep_elem(seed, (uint64_t)(4 * i + e), thr) ? v[e] * scale : 0.f;
+      if (thr) v[e] = kp[e] ? v[e] * scale : 0.f;
       v[e] *= alpha;
     }
     if (r) {

@@ -480,7 +480,12 @@ __device__ __forceinline__ void store_spec(const GemmArgs& g, int z, int mrow0, 
         const float xs[4] = {x4[q].x, x4[q].y, x4[q].z, x4[q].w};
         const float bs[4] = {bn.x, bn.y, bn.z, bn.w};
         float v[4], d[4];
-        const uint64_t row = dbase + (uint64_t)m * (uint64_t)g.N + n;
+        const uint64_t row = dbase + (uint64_t)m * (uint64_t)g.N + n;  // a multiple of 4 (N % 4 == 0)
+        bool kp[4] = {true, true, true, true};
+        if constexpr (S::drop) {
+          esp::keep_pair(seed, row, g.drop_thresh, kp[0], kp[1]);
+          esp::keep_pair(seed, row + 2, g.drop_thresh, kp[2], kp[3]);
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float w = acc[i][j][4 * q + e] + bs[e];
@@ -494,9 +499,8 @@ __device__ __forceinline__ void store_spec(const GemmArgs& g, int z, int mrow0, 
             w = w * sg;
           }
           if constexpr (S::drop) {
-            const bool keep = esp::keep_elem(seed, row + e, g.drop_thresh);
-            w = keep ? w * g.drop_scale : 0.f;
-            dd = keep ? dd * g.drop_scale : 0.f;
+            w = kp[e] ? w * g.drop_scale : 0.f;
+            dd = kp[e] ? dd * g.drop_scale : 0.f;
           }
           if constexpr (EPI == EPI_RMASK) w = xs[e] > 0.f ? w : 0.f;
           else if constexpr (S::mul) w *= xs[e];

@@ -628,3 +628,32 @@ def test_gemm_ragged_n_padded_rows(dev, with_r):
     out = C.cpu()
     assert (out[:, :, :N].double() - ref).abs().max().item() < 1e-4
     assert torch.all(out[:, :, N:] == 7.5)
+
+
+@pytest.mark.parametrize("T", [64, 75])
+def test_dropout_pair_hash_masks_agree(dev, T):
+    """One hash per element pair (esp::keep_pair) and one per element (esp::keep_elem) draw the same
+    mask: the float4 elementwise kernel, the scalar kernel (misaligned output), the GEMM
+    bias+dropout(+residual) epilogues all keep the same (row, col) elements; the keep rate is 1 - p.
+    T = 75 makes the GEMM M odd in quads of rows (the FULL / partial tile split)."""
+    p, seed = 0.1, 12345
+    M, N, Kk = 4 * T, 64, 32
+    ones = torch.ones(M * N, device=dev)
+    m4 = K.scale_dropout(ones, torch.empty_like(ones), drop_p=p, seed=seed)  # float4 pair path
+    buf = torch.empty(M * N + 1, device=dev)
+    m1 = K.scale_dropout(ones, buf[1:], drop_p=p, seed=seed)  # misaligned: scalar per-element path
+    torch.cuda.synchronize()
+    assert torch.equal(m4 != 0, m1 != 0)
+    rate = (m4 != 0).float().mean().item()
+    assert abs(rate - (1 - p)) < 4 * math.sqrt(p * (1 - p) / (M * N))
+    x = (_r(M, Kk, seed=3).abs() + 0.1).to(dev)
+    W = (_r(N, Kk, seed=4).abs() + 0.1).to(dev)
+    b = torch.zeros(N, device=dev)
+    y0 = K.linear_fwd(x, W, b, torch.empty(M, N, device=dev))
+    yd = K.linear_fwd(x, W, b, torch.empty(M, N, device=dev), drop_p=p, seed=seed)
+    yr = K.linear_fwd(x, W, b, torch.empty(M, N, device=dev), drop_p=p, seed=seed,
+                      R=torch.zeros(M, N, device=dev))
+    torch.cuda.synchronize()
+    mask = (m4 != 0).view(M, N)
+    assert torch.equal(yd != 0, mask) and torch.equal(yr != 0, mask)
+    assert rel_err(yd.cpu(), torch.where(mask, y0 / (1 - p), torch.zeros_like(y0)).cpu()) < 1e-6
