@@ -1,7 +1,9 @@
 #!/bin/bash
-# one-off GPU step list (edited per experiment): smoke, legacy rel-pos and C5 bench lines at HEAD
+# one-off GPU step list (edited per experiment): split-K occupancy target A/B
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 bash gpurun_steps.sh \
-  "timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")' > gpurun_out/smoke.log 2>&1" \
-  "timeout -k 10 300 python -u bench.py --rel-pos legacy --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/bench_legacy.log 2>&1" \
-  "timeout -k 10 300 python -u bench.py --config c5 --batch 64 --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/bench_c5_b64.log 2>&1"
+  "ESP_SPLITK_OCC=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_model.py -x -q --timeout 120 --timeout-method thread > gpurun_out/pt_occ.log 2>&1" \
+  "timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/bench_occ0.log 2>&1" \
+  "ESP_SPLITK_OCC=1 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/bench_occ1.log 2>&1" \
+  "timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/bench_occ0b.log 2>&1" \
+  "ESP_SPLITK_OCC=1 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/bench_occ1b.log 2>&1"
