@@ -254,11 +254,20 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        trainer.train_one_step(batch)
+        stats = trainer.train_one_step(batch)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # the timed steps must have trained: the last step's loss and gradient norm are finite and
+    # no optimizer step was skipped (read after the timed region: no host sync inside it)
+    last_loss, last_gn = float(stats["loss"].item()), float(stats["grad_norm"].item())
+    trainer.resolve_pending()
+    trainer.sync_host_state()
+    if not (math.isfinite(last_loss) and math.isfinite(last_gn)) or trainer.n_skipped:
+        print(json.dumps({"error": "non-finite training step", "loss": last_loss, "grad_norm": last_gn,
+                          "skipped_steps": trainer.n_skipped}), flush=True)
+        sys.exit(3)
     if not args.eager:
         # the graph's kernels cannot be bracketed one by one: time the same GEMM launches (same
         # kernels, shapes and inputs) in one eager step right after the timed region
@@ -302,6 +311,8 @@ def main():
             "dtype": "bf16-mfma/f32-accumulate" if args.amp else "f32",
             "data": "synthetic (N(0,1) fbank, random tokens U[20,40], random-init weights)",
             "launch": "eager" if args.eager else "hip_graph",
+            "last_step": {"loss": round(last_loss, 4), "grad_norm": round(last_gn, 4),
+                          "skipped_steps": trainer.n_skipped},
             "config": {"workload": f"{workload_name(args)} d={args.d} H={args.heads} FF={args.ff} "
                                    f"{args.layers}L enc / 6L dec, V={args.vocab}, rel_pos={args.rel_pos}, "
                                    "ctc 0.3, lsm 0.1, dropout 0.1, SpecAug on"

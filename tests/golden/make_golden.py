@@ -619,5 +619,10 @@ if __name__ == "__main__":
                                                      num_blocks=17, rel_pos_type="latest"),
                         dec=O.DecCfg(attention_heads=8, linear_units=2048, num_blocks=6))
         fullsize_train_fixture("fullsize_c4_loss", c4, seed=51, with_grads=False)
+    if "c4grad" in which:  # C4 shape with every parameter gradient (VERDICT r2 'missing' 3)
+        c4 = O.ModelCfg(vocab_size=600, enc=O.EncCfg(output_size=512, attention_heads=8, linear_units=2048,
+                                                     num_blocks=17, rel_pos_type="latest"),
+                        dec=O.DecCfg(attention_heads=8, linear_units=2048, num_blocks=6))
+        fullsize_train_fixture("fullsize_c4_grad_latest", c4, seed=53)
     if "slurp" in which:
         slurp_yaml_fixture()

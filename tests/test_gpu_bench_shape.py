@@ -1,0 +1,86 @@
+"""Correctness at the bench's own workload (VERDICT r2 "next" 1 / "weak" 2).
+
+Every other full-size parity test runs at B=2; bench.py runs B=128, where the GEMMs see other
+split-K counts and persistent-grid wrap-around (M = 47,872 linear rows, 909,568 conv2 rows),
+the implicit-im2col index ranges are 128x larger and the attention grids have z = 512.  Here
+the C2 step at exactly that shape (B=128 x 1500 frames, d=256, 12 blocks, latest rel-pos;
+dropout 0 and SpecAug off so the result is deterministic) is checked against the fp32 / fp64
+oracle fixture tests/golden/bench_c2_b128.npz (make_bench_fixture.py; the oracle is pinned to
+the reference at this model shape by fullsize_c2_grad_*.npz), with the gates of
+test_gpu_fullsize.py: |loss - ref64| <= max(1e-4, 2 |ref32 - ref64|), per-tensor gradient norm
+and slice within max(1e-4, 2 e_ref).  Then the HIP-graph trainer (the bench's launch mode)
+must replay the same steps as the eager trainer at that shape."""
+import pytest
+import torch
+
+from oracle import espnet_cpu as O
+from tests.helpers import build_model, golden, grad_gate, load_seeded, loss_gate
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg():
+    return O.ModelCfg(vocab_size=600,
+                      enc=O.EncCfg(output_size=256, attention_heads=4, linear_units=1024, num_blocks=12,
+                                   rel_pos_type="latest", dropout_rate=0.0, positional_dropout_rate=0.0,
+                                   attention_dropout_rate=0.0),
+                      dec=O.DecCfg(attention_heads=4, linear_units=2048, num_blocks=6))
+
+
+def _batch(g, dev):
+    speech, slen, text, tlen = O.synthetic_batch(int(g["B"]), int(g["T"]), 80, 600, [int(x) for x in g["lens"]],
+                                                 [int(x) for x in g["ulens"]], int(g["seed"]) + 1)
+    return speech.to(dev), slen, text, tlen
+
+
+def test_bench_shape_c2_b128_step_vs_oracle(dev):
+    g = golden("bench_c2_b128")
+    assert int(g["B"]) == 128 and int(g["T"]) == 1500
+    cfg = _cfg()
+    model = build_model(cfg, dev)
+    load_seeded(model, cfg, int(g["seed"]))
+    speech, slen, text, tlen = _batch(g, dev)
+    model.train()
+    loss, stats, _ = model(speech, slen, text, tlen)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).item()
+    for key, got, slack in (("loss", loss.item(), 0.0), ("loss_att", stats["loss_att"].item(), 0.0),
+                            ("loss_ctc", stats["loss_ctc"].item(), 2e-4)):
+        ok, info = loss_gate(got, g, key, slack)
+        assert ok, info
+    assert abs(stats["acc"].item() - float(g["acc_f64"])) < 1e-6
+    bad = grad_gate(model, g)
+    assert not bad, bad
+
+
+def test_bench_shape_graph_replay_matches_eager(dev):
+    """The bench's launch mode at the bench's shape: three HIP-graph trainer steps (capture,
+    two replays) equal three eager trainer steps (losses and the parameters after Adam)."""
+    from espnet_slurp_amd.optimizers.fused_adam import FusedAdam
+    from espnet_slurp_amd.schedulers.warmup_lr import WarmupLR
+    from espnet_slurp_amd.train.trainer import Trainer, TrainerOptions
+    g = golden("bench_c2_b128")
+    cfg = _cfg()
+    speech, slen, text, tlen = _batch(g, dev)
+    runs = []
+    for graph in (False, True):
+        model = build_model(cfg, dev)
+        load_seeded(model, cfg, int(g["seed"]))
+        model.train()
+        opt = FusedAdam(model.parameters(), model.flat, lr=1e-3)
+        t = Trainer(model, opt, WarmupLR(opt, 25000), TrainerOptions(grad_clip=5.0), cuda_graph=graph)
+        losses = []
+        for _ in range(3):
+            b = dict(speech=speech.clone(), speech_lengths=slen, text=text.clone(), text_lengths=tlen)
+            losses.append(t.train_one_step(b)["loss"].item())
+        t.resolve_pending()
+        t.sync_host_state()
+        assert t.n_skipped == 0
+        runs.append((losses, model.flat.flat.clone()))
+        del t, opt, model
+        torch.cuda.empty_cache()
+    (le, fe), (lg, fg) = runs
+    assert all(abs(a - b) <= 1e-6 * max(1.0, abs(a)) for a, b in zip(le, lg)), (le, lg)
+    assert le[2] < le[0], le  # Adam on a fixed batch lowers the loss
+    assert torch.allclose(fe, fg, rtol=0, atol=1e-6)
