@@ -35,7 +35,7 @@ SIGNATURES = {
     "esp_embed_bwd": [P, P, P, I, I, I, F, F, U64, P],
     "esp_specaug": [P, P, I, I, I, P, P, P, I, P, I, P],
     "esp_utterance_mvn": [P, I, I, I, P, P],
-    "esp_grad_norm": [P, L, F, P, P, P],
+    "esp_grad_norm": [P, L, F, P, L, P, P],
     "esp_adam": [P, P, P, P, L, P, F, F, F, F, F, I, P],
     "esp_opt_hyper": [P, ctypes.c_double, ctypes.c_double, F, F, P, P],
     "esp_adam_dev": [P, P, P, P, L, P, P, F, F, F, F, P],
@@ -43,15 +43,15 @@ SIGNATURES = {
     "esp_set_rng_key": [P],
     "esp_rng_advance": [P, P],
     "esp_layernorm_fwd": [P, P, P, P, P, P, I, I, F, P],
-    "esp_layernorm_bwd": [P, P, P, P, P, P, I, P, P, I, I, P, P],
-    "esp_colsum": [P, I, I, L, P, I, P, P],
+    "esp_layernorm_bwd": [P, P, P, P, P, P, I, P, P, I, I, P, L, P],
+    "esp_colsum": [P, I, I, L, P, I, P, L, P],
     "esp_glu_fwd": [P, P, L, I, P],
     "esp_glu_bwd": [P, P, P, L, I, P],
     "esp_dwconv1d": [P, P, P, P, I, I, I, I, I, P, P],
-    "esp_dwconv1d_wgrad": [P, P, P, I, I, I, I, P, P, P],
-    "esp_bn_swish_fwd": [P, P, P, P, P, P, P, P, F, F, I, I, P, I, P, P],
+    "esp_dwconv1d_wgrad": [P, P, P, I, I, I, I, P, L, P, P],
+    "esp_bn_swish_fwd": [P, P, P, P, P, P, P, P, F, F, I, I, P, L, I, P, P],
     "esp_bn_swish_eval": [P, P, P, P, P, P, F, I, I, P, P, P],
-    "esp_bn_swish_bwd": [P, P, P, P, P, P, P, P, P, I, I, P, P, I, P, P],
+    "esp_bn_swish_bwd": [P, P, P, P, P, P, P, P, P, I, I, P, L, P, I, P, P],
     "esp_heads_split": [P, L, I, I, I, I, I, P, P, P],
     "esp_heads_split2": [P, L, I, I, I, I, I, P, P, P, P, P],
     "esp_add2d": [P, L, P, L, I, I, P],
@@ -70,23 +70,35 @@ SIGNATURES = {
     "esp_relpos_dp": [P, L, P, I, I, I, I, P, L, P, P, P, P, P, L, P, L, P],
     "esp_fbank_fwd": [P, L, P, I, I, I, I, P, P, P, P, P, I, P, I, P],
     "esp_global_mvn": [P, P, I, I, I, P, P, I, I, P],
-    "esp_conv2_dgrad": [P, P, P, P, I, I, I, I, P, P, P],
+    "esp_conv2_dgrad": [P, P, P, P, I, I, I, I, P, P, L, P],
     "esp_conv1_fwd": [P, P, P, P, I, I, I, I, P],
     "esp_col2im_relu": [P, P, P, I, I, I, I, P],
-    "esp_conv1_wgrad": [P, P, P, P, I, I, I, I, P, P],
+    "esp_conv1_wgrad": [P, P, P, P, I, I, I, I, P, L, P],
     "esp_permute3": [P, P, I, I, I, I, P],
     "esp_log_softmax": [P, P, L, I, P],
-    "esp_ctc_loss": [P, P, I, P, P, I, I, I, I, F, I, P, P, P, P],
+    "esp_ctc_loss": [P, P, I, P, P, I, I, I, I, F, I, P, P, P, L, P],
     "esp_label_smoothing": [P, P, L, I, I, F, F, P, P, P, P],
     "esp_reduce_losses": [P, I, I, P, P, I, F, F, P, P],
     "esp_argmax": [P, P, L, I, P],
     "esp_ctc_forced_align": [P, I, I, P, I, I, P, P, P],
     "esp_ctc_prefix_init": [P, I, I, I, P, P],
     "esp_ctc_prefix_score": [P, I, I, P, P, I, P, I, I, I, I, P, P, P],
+    # workspace-size queries (host arithmetic; return bytes)
+    "esp_grad_norm_workspace_bytes": [L],
+    "esp_layernorm_bwd_workspace_bytes": [I, I],
+    "esp_colsum_workspace_bytes": [I, I],
+    "esp_dwconv1d_wgrad_workspace_bytes": [I, I, I, I],
+    "esp_bn_swish_fwd_workspace_bytes": [I, I],
+    "esp_bn_swish_bwd_workspace_bytes": [I, I],
+    "esp_conv1_wgrad_workspace_bytes": [I, I, I, I],
+    "esp_conv2_dgrad_workspace_bytes": [I],
+    "esp_ctc_loss_workspace_bytes": [I, I, I],
+    "esp_relpos_dp_workspace_bytes": [I, I, I],
 }
 _RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I, "esp_set_gemm_compute": I,
              "esp_get_gemm_compute": I}
-ABI_VERSION = 18  # bumped whenever a signature in include/espnet_mi355.h changes
+_RESTYPES.update({k: L for k in SIGNATURES if k.endswith("_workspace_bytes")})
+ABI_VERSION = 19  # bumped whenever a signature in include/espnet_mi355.h changes
 
 _lib = None
 
@@ -114,6 +126,15 @@ def load() -> ctypes.CDLL:
 
 class NativeError(RuntimeError):
     pass
+
+
+def workspace_bytes(launcher: str, *dims) -> int:
+    """Bytes of scratch the launcher `launcher` needs for these sizes (esp_<op>_workspace_bytes):
+    the same host code that picks the launcher's chunking answers, so callers never restate it."""
+    n = getattr(load(), launcher + "_workspace_bytes")(*dims)
+    if n < 0:
+        raise NativeError(f"{launcher}_workspace_bytes{dims} failed")
+    return int(n)
 
 
 def call(name: str, *args):

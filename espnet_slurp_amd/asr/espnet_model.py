@@ -171,8 +171,8 @@ class ESPnetASRModel(AbsESPnetModel):
                               (1.0 - self.ctc_weight) / (1.0 if ln else denom), grad_att, row_loss, row_stat)
             state["grad_att"] = grad_att
             state["dec"] = dsaved
-            if not self.training:  # eval-mode cer / wer read the decoder argmax (_error_rates)
-                prep["eval_logits"] = logits
+            if not self.training and self.error_calculator is not None:
+                prep["eval_logits"] = logits  # eval-mode cer / wer read the decoder argmax (_error_rates)
         out4 = empty(5, like=hs)
         K.reduce_losses(nll, B, self.ctc.zero_infinity if self.ctc is not None else True, row_loss, row_stat, R,
                         denom, self.ctc_weight, out4)

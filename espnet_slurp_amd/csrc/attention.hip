@@ -971,12 +971,6 @@ inline int gridn(long n) {
   long b = (n + 255) / 256;
   return (int)(b > 65536 ? 65536 : (b < 1 ? 1 : b));
 }
-inline uint32_t drop_threshold(float p) {
-  if (p <= 0.f) return 0;
-  double t = (double)p * 4294967296.0;
-  uint32_t r = (uint32_t)(t >= 4294967295.0 ? 4294967295.0 : t);
-  return r ? r : 1;
-}
 
 }  // namespace
 
@@ -1028,9 +1022,9 @@ ESP_API int esp_attn_softmax_fwd(const float* ac, const float* bd, int relpos, i
   ESP_ARG_CHECK(relpos != 1 || P == 2 * Tq - 1, "esp_attn_softmax_fwd: latest rel-pos needs P=2T-1");
   ESP_ARG_CHECK(relpos != 2 || P == Tq, "esp_attn_softmax_fwd: legacy rel-pos needs P=T");
   ESP_ARG_CHECK(lds >= Tk && (relpos == 0 || ldp >= P), "esp_attn_softmax_fwd: pitch < row length");
-  const uint32_t thr = drop_threshold(drop_p);
+  const uint32_t thr = esp::drop_threshold(drop_p);
   if (!thr) pdrop = nullptr;
-  const float ds = thr ? 1.f / (1.f - drop_p) : 1.f;
+  const float ds = esp::drop_scale(thr);
   const long rows = (long)Z * Tq;
   dim3 grid((unsigned)((rows + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
@@ -1051,8 +1045,8 @@ ESP_API int esp_attn_softmax_bwd(const float* attn, const float* dP, float* dS, 
                                  float sqrt_dk, long rows, int Tk, long lds, void* stream) {
   ESP_ARG_CHECK(Tk <= 1024, "esp_attn_softmax_bwd: Tk too large");
   ESP_ARG_CHECK(lds >= Tk, "esp_attn_softmax_bwd: pitch < Tk");
-  const uint32_t thr = drop_threshold(drop_p);
-  const float ds = thr ? 1.f / (1.f - drop_p) : 1.f;
+  const uint32_t thr = esp::drop_threshold(drop_p);
+  const float ds = esp::drop_scale(thr);
   dim3 grid((unsigned)((rows + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
 #define ESP_SB(PER) \
@@ -1086,9 +1080,9 @@ ESP_API int esp_relpos_softmax_fwd(const float* qv, const float* p, long ldp_row
   ESP_ARG_CHECK(T >= 1 && T <= 1024 && lds >= T && nb >= 1 && H >= 1, "esp_relpos_softmax_fwd: bad sizes T=%d", T);
   ESP_ARG_CHECK(ldp_row % 4 == 0 && ((uintptr_t)p & 15) == 0 && ((uintptr_t)qv & 15) == 0,
                 "esp_relpos_softmax_fwd: q_v / p must be 16-B aligned with ld %% 4 == 0");
-  const uint32_t thr = drop_threshold(drop_p);
+  const uint32_t thr = esp::drop_threshold(drop_p);
   if (!thr) pdrop = nullptr;
-  const float ds = thr ? 1.f / (1.f - drop_p) : 1.f;
+  const float ds = esp::drop_scale(thr);
   const int ntile = (T + RP_ROWS - 1 + 31) / 32;
   const int WP = ntile * 32 + 4;
   const size_t shm = (size_t)RP_ROWS * WP * sizeof(float);
@@ -1118,9 +1112,9 @@ ESP_API int esp_relpos_attn_fwd(const float* qu, const float* qv, const float* k
   ESP_ARG_CHECK(ldp_row % 4 == 0 && ldk % 4 == 0 && ((uintptr_t)p & 15) == 0 && ((uintptr_t)qv & 15) == 0 &&
                     ((uintptr_t)qu & 15) == 0 && ((uintptr_t)kmat & 15) == 0,
                 "esp_relpos_attn_fwd: operands must be 16-B aligned with ld %% 4 == 0");
-  const uint32_t thr = drop_threshold(drop_p);
+  const uint32_t thr = esp::drop_threshold(drop_p);
   if (!thr) pdrop = nullptr;
-  const float ds = thr ? 1.f / (1.f - drop_p) : 1.f;
+  const float ds = esp::drop_scale(thr);
   const int nbd = (T + RP_ROWS - 1 + 31) / 32;
   const int WP = nbd * 32 + 4;
   const size_t shm = ((size_t)RP_ROWS * WP + 8 * RP_ROWS) * sizeof(float);
@@ -1161,9 +1155,9 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
   ESP_ARG_CHECK(ldp_row % 4 == 0 && ldk % 4 == 0 && ((uintptr_t)p & 15) == 0 && ((uintptr_t)qv & 15) == 0 &&
                     ((uintptr_t)qu & 15) == 0 && ((uintptr_t)kmat & 15) == 0,
                 "esp_relpos_attn_probs: operands must be 16-B aligned with ld %% 4 == 0");
-  const uint32_t thr = drop_threshold(drop_p);
+  const uint32_t thr = esp::drop_threshold(drop_p);
   if (!thr) pdrop = nullptr;
-  const float ds = thr ? 1.f / (1.f - drop_p) : 1.f;
+  const float ds = esp::drop_scale(thr);
   const int nt = (T + 15) / 16;
   static int split_env = -1;  // ESP_ATTN_SPLIT=1|2: one wave per row group / two (key halves)
   if (split_env < 0) split_env = getenv("ESP_ATTN_SPLIT") ? atoi(getenv("ESP_ATTN_SPLIT")) : 1;
@@ -1228,8 +1222,8 @@ ESP_API int esp_attn_softmax_bwd_relpos(const float* attn, const float* dP, floa
   ESP_ARG_CHECK(relpos == 1 || relpos == 2, "esp_attn_softmax_bwd_relpos: relpos must be 1 or 2");
   ESP_ARG_CHECK(T >= 1 && T <= 1024 && lds >= T && ldp >= (relpos == 1 ? 2 * T - 1 : T) && rows % T == 0,
                 "esp_attn_softmax_bwd_relpos: bad sizes");
-  const uint32_t thr = drop_threshold(drop_p);
-  const float ds = thr ? 1.f / (1.f - drop_p) : 1.f;
+  const uint32_t thr = esp::drop_threshold(drop_p);
+  const float ds = esp::drop_scale(thr);
   dim3 grid((unsigned)((rows + 3) / 4));
   hipStream_t st = (hipStream_t)stream;
   const bool p2 = sqrt_dk > 0.f && (__builtin_bit_cast(uint32_t, sqrt_dk) & 0x7fffffu) == 0;
@@ -1285,8 +1279,8 @@ ESP_API int esp_relpos_attn_bwd(const float* dctx, long ldd, const float* vmat, 
                 "esp_relpos_attn_bwd: bad sizes T=%d", T);
   ESP_ARG_CHECK(ldd % 4 == 0 && ldv % 4 == 0 && ((uintptr_t)dctx & 15) == 0 && ((uintptr_t)vmat & 15) == 0,
                 "esp_relpos_attn_bwd: dctx / v must be 16-B aligned with ld %% 4 == 0");
-  const uint32_t thr = drop_threshold(drop_p);
-  const float ds = thr ? 1.f / (1.f - drop_p) : 1.f;
+  const uint32_t thr = esp::drop_threshold(drop_p);
+  const float ds = esp::drop_scale(thr);
   const int nta = ((T + 31) / 32 + 3) / 4;
   dim3 grid((unsigned)((T + RP_ROWS - 1) / RP_ROWS), (unsigned)(nb * H));
   hipStream_t st = (hipStream_t)stream;

@@ -50,6 +50,24 @@ __device__ __forceinline__ uint64_t keyed(uint64_t seed, const uint64_t* key) { 
 __device__ __forceinline__ uint32_t thr16_of(uint32_t thresh) {
   return (uint32_t)(((uint64_t)thresh + 32768u) >> 16);
 }
+// Host: the 32-bit threshold of dropout probability p, already on the 1/65536 grid the kernels
+// compare against (thr16 << 16, so thr16_of returns thr16 exactly).  p > 0 never quantizes to
+// "no dropout": p below half a quantum takes the smallest one (1/65536).  0 means no dropout.
+inline uint32_t drop_threshold(float p) {
+  if (!(p > 0.f)) return 0;
+  double q = (double)p * 65536.0 + 0.5;
+  uint32_t t16 = q >= 65535.0 ? 65535u : (uint32_t)q;
+  if (t16 == 0) t16 = 1;
+  return t16 << 16;
+}
+// Host: the inverted-dropout rescale matching the quantized keep probability exactly,
+// 1 / (1 - thr16 / 65536), so E[mask * scale] = 1 (1/(1-p) with the unrounded p would bias
+// every dropout site by ~7e-6 at p = 0.1).
+inline float drop_scale(uint32_t thresh) {
+  if (!thresh) return 1.f;
+  const uint32_t t16 = (uint32_t)(((uint64_t)thresh + 32768u) >> 16);
+  return (float)(65536.0 / (65536.0 - (double)t16));
+}
 __device__ __forceinline__ bool keep_elem(uint64_t seed, uint64_t idx, uint32_t thresh) {
   const uint32_t h = rng_u32(seed, idx >> 1);
   return ((idx & 1) ? (h >> 16) : (h & 0xffffu)) >= thr16_of(thresh);

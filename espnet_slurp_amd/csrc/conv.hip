@@ -209,9 +209,17 @@ ESP_API int esp_col2im_relu(const float* dcol, const float* z1, float* dz1, int 
   return 0;
 }
 
-// workspace: >= ceil(B*T1*F1/2048) * D * 10 floats.  dW (D,9) and db (D) accumulated.
+// workspace: ceil(B*T1*F1/2048) * D * 10 floats (esp_conv1_wgrad_workspace_bytes).  dW (D,9) and
+// db (D) accumulated.
+ESP_API long esp_conv1_wgrad_workspace_bytes(int B, int T, int F, int D) {
+  const int T1 = (T - 3) / 2 + 1, F1 = (F - 3) / 2 + 1;
+  if (B <= 0 || T1 <= 0 || F1 <= 0 || D <= 0) return 0;
+  return 4L * (((long)B * T1 * F1 + C1_CHUNK - 1) / C1_CHUNK) * D * 10;
+}
 ESP_API int esp_conv1_wgrad(const float* x, const float* dz1, float* dW, float* db, int B, int T, int F, int D,
-                            float* work, void* stream) {
+                            float* work, long work_bytes, void* stream) {
+  const long need__ = esp_conv1_wgrad_workspace_bytes(B, T, F, D);
+  ESP_ARG_CHECK(work_bytes >= need__, "esp_conv1_wgrad: workspace %ld B < %ld B required (esp_conv1_wgrad_workspace_bytes)", work_bytes, need__);
   const int T1 = (T - 3) / 2 + 1, F1 = (F - 3) / 2 + 1;
   const long npix = (long)B * T1 * F1;
   const int nb = (int)((npix + C1_CHUNK - 1) / C1_CHUNK);

@@ -20,7 +20,7 @@ void set_error(const char* fmt, ...) {
 }  // namespace esp
 
 ESP_API const char* esp_last_error(void) { return esp::g_err; }
-ESP_API int esp_abi_version(void) { return 18; }
+ESP_API int esp_abi_version(void) { return 19; }
 ESP_API int esp_set_rng_key(const unsigned long long* key) {
   esp::g_rng_key = (const uint64_t*)key;
   return 0;
@@ -28,12 +28,6 @@ ESP_API int esp_set_rng_key(const unsigned long long* key) {
 
 namespace {
 
-inline uint32_t drop_threshold(float p) {
-  if (p <= 0.f) return 0;
-  double t = (double)p * 4294967296.0;
-  uint32_t r = (uint32_t)(t >= 4294967295.0 ? 4294967295.0 : t);
-  return r ? r : 1;
-}
 
 inline int grid_for(long n, int per_thread = 1) {
   long b = (n / per_thread + 255) / 256;
@@ -324,22 +318,22 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
 
 ESP_API int esp_act_bwd(const float* dy, const float* h, float* dx, long n, int act, float drop_p,
                         unsigned long long seed, long idx_off, void* stream) {
-  const uint32_t thr = drop_threshold(drop_p);
+  const uint32_t thr = esp::drop_threshold(drop_p);
   hipLaunchKernelGGL(act_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, dy, h, dx, n, act,
-                     thr, thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed, idx_off, esp::rng_key_ptr());
+                     thr, esp::drop_scale(thr), (uint64_t)seed, idx_off, esp::rng_key_ptr());
   ESP_CHECK_LAUNCH("esp_act_bwd");
   return 0;
 }
 
 ESP_API int esp_scale_dropout(const float* x, float* y, long n, float alpha, float drop_p, unsigned long long seed,
                               const float* r, float beta, void* stream) {
-  const uint32_t thr = drop_threshold(drop_p);
+  const uint32_t thr = esp::drop_threshold(drop_p);
   if (n % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 && ((uintptr_t)r & 15) == 0)
     hipLaunchKernelGGL(scale_drop4_kernel, dim3(grid_for(n / 4)), dim3(256), 0, (hipStream_t)stream, x, y, n / 4,
-                       alpha, thr, thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed, r, beta, esp::rng_key_ptr());
+                       alpha, thr, esp::drop_scale(thr), (uint64_t)seed, r, beta, esp::rng_key_ptr());
   else
     hipLaunchKernelGGL(scale_drop_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, y, n, alpha, thr,
-                       thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed, r, beta, esp::rng_key_ptr());
+                       esp::drop_scale(thr), (uint64_t)seed, r, beta, esp::rng_key_ptr());
   ESP_CHECK_LAUNCH("esp_scale_dropout");
   return 0;
 }
@@ -353,10 +347,10 @@ ESP_API int esp_scale_by_dev(float* x, long n, const float* s, void* stream) {
 
 ESP_API int esp_embed_fwd(const long long* tok, const float* E, const float* pe, float* y, int nrows, int L, int D,
                           float xscale, float drop_p, unsigned long long seed, void* stream) {
-  const uint32_t thr = drop_threshold(drop_p);
+  const uint32_t thr = esp::drop_threshold(drop_p);
   const long n = (long)nrows * D;
   hipLaunchKernelGGL(embed_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const int64_t*)tok, E,
-                     pe, y, L, D, xscale, thr, thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed, n, esp::rng_key_ptr());
+                     pe, y, L, D, xscale, thr, esp::drop_scale(thr), (uint64_t)seed, n, esp::rng_key_ptr());
   ESP_CHECK_LAUNCH("esp_embed_fwd");
   return 0;
 }
@@ -364,9 +358,9 @@ ESP_API int esp_embed_fwd(const long long* tok, const float* E, const float* pe,
 ESP_API int esp_embed_bwd(const long long* tok, const float* dy, float* dE, int nrows, int V, int D, float xscale,
                           float drop_p, unsigned long long seed, void* stream) {
   ESP_ARG_CHECK(D <= EMB_MAXD, "esp_embed_bwd: D > 1024");
-  const uint32_t thr = drop_threshold(drop_p);
+  const uint32_t thr = esp::drop_threshold(drop_p);
   hipLaunchKernelGGL(embed_bwd_kernel, dim3(V), dim3(256), 0, (hipStream_t)stream, (const int64_t*)tok, dy, dE, nrows,
-                     D, xscale, thr, thr ? 1.f / (1.f - drop_p) : 1.f, (uint64_t)seed, esp::rng_key_ptr());
+                     D, xscale, thr, esp::drop_scale(thr), (uint64_t)seed, esp::rng_key_ptr());
   ESP_CHECK_LAUNCH("esp_embed_bwd");
   return 0;
 }
@@ -387,9 +381,15 @@ ESP_API int esp_utterance_mvn(float* x, int B, int T, int F, const int* lens, vo
   return 0;
 }
 
-// workspace: >= 1024 doubles; out: 3 floats (norm, clip coef, finite flag) on device
-ESP_API int esp_grad_norm(const float* g, long n, float max_norm, double* work, float* out, void* stream) {
-  const int nb = 1024;
+// workspace: 1024 doubles (esp_grad_norm_workspace_bytes); out: 3 floats (norm, clip coef, finite
+// flag) on device
+constexpr int GN_BLOCKS = 1024;
+ESP_API long esp_grad_norm_workspace_bytes(long n) { return n < 0 ? 0 : 8L * GN_BLOCKS; }
+ESP_API int esp_grad_norm(const float* g, long n, float max_norm, double* work, long work_bytes, float* out,
+                          void* stream) {
+  const int nb = GN_BLOCKS;
+  const long need__ = esp_grad_norm_workspace_bytes(n);
+  ESP_ARG_CHECK(work_bytes >= need__, "esp_grad_norm: workspace %ld B < %ld B required (esp_grad_norm_workspace_bytes)", work_bytes, need__);
   hipLaunchKernelGGL(sumsq_kernel, dim3(nb), dim3(256), 0, (hipStream_t)stream, g, n, work);
   hipLaunchKernelGGL(norm_finalize_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, work, nb, max_norm, out);
   ESP_CHECK_LAUNCH("esp_grad_norm");

@@ -658,13 +658,6 @@ __global__ __launch_bounds__(64) void relpos_carry_kernel(const float* __restric
   dq[((long)b * T + i) * ldq + FDK * h + threadIdx.x] += carry[(long)zq * FDK + threadIdx.x];
 }
 
-inline uint32_t drop_thr(float p) {
-  if (p <= 0.f) return 0;
-  double t = (double)p * 4294967296.0;
-  uint32_t r = (uint32_t)(t >= 4294967295.0 ? 4294967295.0 : t);
-  return r ? r : 1;
-}
-
 bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
@@ -706,8 +699,8 @@ ESP_API int esp_relpos_flash_fwd(const float* qu, const float* qv, const float* 
   a.nb = nb; a.T = T; a.nqb = (T + FR - 1) / FR; a.nblk = nb * H * a.nqb;
   a.sqrt_dk = sqrt_dk;
   a.inv_sqrt_dk = 1.0f / sqrt_dk;
-  a.thr = drop_thr(drop_p);
-  a.dscale = a.thr ? 1.f / (1.f - drop_p) : 1.f;
+  a.thr = esp::drop_threshold(drop_p);
+  a.dscale = esp::drop_scale(a.thr);
   a.seed = seed;
   a.key = esp::rng_key_ptr();
   const size_t shm = flash_fwd_lds(T, rel, &a.WP);
@@ -746,8 +739,8 @@ ESP_API int esp_relpos_flash_bwd(const float* qu, const float* qv, const float* 
   a.nb = nb; a.T = T; a.nqb = (T + FR - 1) / FR; a.nblk = nb * H * a.nqb;
   a.sqrt_dk = sqrt_dk;
   a.inv_sqrt_dk = 1.0f / sqrt_dk;
-  a.thr = drop_thr(drop_p);
-  a.dscale = a.thr ? 1.f / (1.f - drop_p) : 1.f;
+  a.thr = esp::drop_threshold(drop_p);
+  a.dscale = esp::drop_scale(a.thr);
   a.seed = seed;
   a.key = esp::rng_key_ptr();
   const size_t shm = flash_bwd_lds(T, &a.WP, &a.DSP, &a.band_sz);
@@ -763,6 +756,11 @@ ESP_API int esp_relpos_flash_bwd(const float* qu, const float* qv, const float* 
 // and q_v; work: (H * ceil((2T-1)/32) * ng) * 64 * 64 * 4 floats of partials, ng = ceil(nb / bpg).
 // Also reduces the flash backward's pos_bias partials into du / dv (accumulated) and, for
 // legacy, adds the carries into dq.
+// the workspace this call uses at its preferred grouping (8 utterances per partial); it works with
+// less (fewer, larger groups), down to the one-group minimum H * (2T-1) * 64 floats
+ESP_API long esp_relpos_dp_workspace_bytes(int nb, int H, int T) {
+  return nb <= 0 || H <= 0 || T <= 0 ? 0 : 4L * H * ((nb + 7) / 8) * (2L * T - 1) * FDK;
+}
 ESP_API int esp_relpos_dp(const float* dS, long lds, const float* qv, int rel, int nb, int H, int T, float* dp, long ldp,
                           const float* bias_part, const float* carry, float* du, float* dv, float* dq, long ldq,
                           float* work, long work_floats, void* stream) {

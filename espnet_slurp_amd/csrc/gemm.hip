@@ -376,10 +376,8 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
     if (e && (atoi(e) & 16)) g.wide = g.ragged4 = 0;
   }
   if (drop_p > 0.f) {
-    double t = (double)drop_p * 4294967296.0;
-    g.drop_thresh = (uint32_t)(t >= 4294967295.0 ? 4294967295.0 : t);
-    if (g.drop_thresh == 0) g.drop_thresh = 1;
-    g.drop_scale = 1.0f / (1.0f - drop_p);
+    g.drop_thresh = esp::drop_threshold(drop_p);
+    g.drop_scale = esp::drop_scale(g.drop_thresh);
   }
   // Tile choice: the LDS-DMA kernel when both operands allow it, 128x64 tiles when N <= 64
   // or when 128x128 tiles leave the grid under two blocks per CU but 128x64 tiles do not
@@ -494,9 +492,13 @@ __global__ void conv2_class_weights_kernel(const float* __restrict__ W, float* _
 }
 }  // namespace
 
+// wc_work: the four parity classes' re-laid weights, 9 * D * D floats (esp_conv2_dgrad_workspace_bytes)
+ESP_API long esp_conv2_dgrad_workspace_bytes(int D) { return D <= 0 ? 0 : 4L * 9 * D * D; }
 ESP_API int esp_conv2_dgrad(const float* dz2, const float* W, const float* z1, float* dz1, int B, int T1, int F1,
-                            int D, const float* zeros16, float* wc_work, void* stream) {
+                            int D, const float* zeros16, float* wc_work, long work_bytes, void* stream) {
   const int T2 = (T1 - 3) / 2 + 1, F2 = (F1 - 3) / 2 + 1;
+  const long need__ = esp_conv2_dgrad_workspace_bytes(D);
+  ESP_ARG_CHECK(work_bytes >= need__, "esp_conv2_dgrad: workspace %ld B < %ld B required (esp_conv2_dgrad_workspace_bytes)", work_bytes, need__);
   ESP_ARG_CHECK(B >= 1 && T2 >= 1 && F2 >= 1 && D % 32 == 0, "esp_conv2_dgrad: bad sizes (D %% 32 == 0 needed)");
   ESP_ARG_CHECK(aligned16(dz2) && aligned16(z1) && aligned16(dz1) && aligned16(zeros16) && aligned16(wc_work),
                 "esp_conv2_dgrad: operands must be 16-B aligned");

@@ -357,10 +357,16 @@ ESP_API int esp_log_softmax(const float* x, float* y, long rows, int V, void* st
 
 // lp (B,T,V) log-probs; labels (B,Umax) int64; ilen/tlen int32 device arrays.
 // Outputs: nll (B); grad (B,T,V) = gscale * d nll_b / d logits (zeroed where infinite
-// when zero_infinity).  work: >= 2*B*T*Smax doubles, Smax = 2*Umax+1 <= 1024.
+// when zero_infinity).  work: 2*B*T*Smax doubles, Smax = 2*Umax+1 <= 1024
+// (esp_ctc_loss_workspace_bytes).
+ESP_API long esp_ctc_loss_workspace_bytes(int B, int T, int Umax) {
+  return B <= 0 || T <= 0 || Umax < 0 ? 0 : 8L * 2 * B * T * (2L * Umax + 1);
+}
 ESP_API int esp_ctc_loss(const float* lp, const long long* labels, int Umax, const int* ilen, const int* tlen, int B,
                          int T, int V, int blank, float gscale, int zero_infinity, double* nll, float* grad,
-                         double* work, void* stream) {
+                         double* work, long work_bytes, void* stream) {
+  const long need__ = esp_ctc_loss_workspace_bytes(B, T, Umax);
+  ESP_ARG_CHECK(work_bytes >= need__, "esp_ctc_loss: workspace %ld B < %ld B required (esp_ctc_loss_workspace_bytes)", work_bytes, need__);
   const int Smax = 2 * Umax + 1;
   ESP_ARG_CHECK(Smax <= CTC_NT * CTC_SPT, "esp_ctc_loss: 2*Umax+1=%d > %d", Smax, CTC_NT * CTC_SPT);
   ESP_ARG_CHECK(V <= MAXV_LDS, "esp_ctc_loss: V=%d > %d", V, MAXV_LDS);

@@ -734,11 +734,16 @@ ESP_API int esp_layernorm_fwd(const float* x, const float* w, const float* b, fl
   return 0;
 }
 
-// workspace: >= 2*D*ceil(M/32) floats.  dw/db are accumulated (+=).
+// workspace: 2*D*ceil(M/32) floats (esp_layernorm_bwd_workspace_bytes).  dw/db are accumulated (+=).
+ESP_API long esp_layernorm_bwd_workspace_bytes(int M, int D) {
+  return M <= 0 || D <= 0 ? 0 : 4L * 2 * D * ((M + LN_BWD_ROWS - 1) / LN_BWD_ROWS);
+}
 ESP_API int esp_layernorm_bwd(const float* dy, const float* x, const float* w, const float* mean, const float* rstd,
                               float* dx, int accumulate, float* dw, float* db, int M, int D, float* work,
-                              void* stream) {
+                              long work_bytes, void* stream) {
   ESP_ARG_CHECK(D <= MAXD && D % 4 == 0, "esp_layernorm_bwd: D=%d must be a multiple of 4 and <= %d", D, MAXD);
+  const long need__ = esp_layernorm_bwd_workspace_bytes(M, D);
+  ESP_ARG_CHECK(work_bytes >= need__, "esp_layernorm_bwd: workspace %ld B < %ld B required (esp_layernorm_bwd_workspace_bytes)", work_bytes, need__);
   if (M <= 0) return 0;
   const int nb = (M + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
   hipStream_t st = (hipStream_t)stream;
@@ -754,8 +759,14 @@ ESP_API int esp_layernorm_bwd(const float* dy, const float* x, const float* w, c
   return 0;
 }
 
-// out[c] (+)= sum_r x[r*ld + c].  workspace: >= N*ceil(M/32) floats
-ESP_API int esp_colsum(const float* x, int M, int N, long ld, float* out, int accumulate, float* work, void* stream) {
+// out[c] (+)= sum_r x[r*ld + c].  workspace: N*ceil(M/32) floats (esp_colsum_workspace_bytes)
+ESP_API long esp_colsum_workspace_bytes(int M, int N) {
+  return M <= 0 || N <= 0 ? 0 : 4L * N * ((M + CS_ROWS - 1) / CS_ROWS);
+}
+ESP_API int esp_colsum(const float* x, int M, int N, long ld, float* out, int accumulate, float* work, long work_bytes,
+                       void* stream) {
+  const long need__ = esp_colsum_workspace_bytes(M, N);
+  ESP_ARG_CHECK(work_bytes >= need__, "esp_colsum: workspace %ld B < %ld B required (esp_colsum_workspace_bytes)", work_bytes, need__);
   hipStream_t st = (hipStream_t)stream;
   if (M == 0) {
     if (!accumulate) (void)hipMemsetAsync(out, 0, sizeof(float) * N, st);
@@ -818,12 +829,20 @@ ESP_API int esp_dwconv1d(const float* x, const float* W, const float* bias, floa
   return 0;
 }
 
-// dW[c,k] += sum_{b,t} dy[b,t,c]*x[b,t+k-pad,c].  workspace >= Bn*ceil(T/64)*D*K floats
+// dW[c,k] += sum_{b,t} dy[b,t,c]*x[b,t+k-pad,c].  workspace: Bn * (time chunks) * D * K floats
+// (esp_dwconv1d_wgrad_workspace_bytes)
+static int dww_chunks(int T, int K) {
+  return (K == 31 || K == 15) ? (T + DWR_TT - 1) / DWR_TT : (T + DWW_TCH - 1) / DWW_TCH;
+}
+ESP_API long esp_dwconv1d_wgrad_workspace_bytes(int Bn, int T, int D, int K) {
+  return Bn <= 0 || T <= 0 || D <= 0 || K <= 0 ? 0 : 4L * Bn * dww_chunks(T, K) * D * K;
+}
 ESP_API int esp_dwconv1d_wgrad(const float* dy, const float* x, float* dW, int Bn, int T, int D, int K, float* work,
-                               const int* tvalid, void* stream) {
+                               long work_bytes, const int* tvalid, void* stream) {
   ESP_ARG_CHECK(K % 2 == 1 && K <= 64, "esp_dwconv1d_wgrad: K must be odd and <= 64");
-  const bool rb = K == 31 || K == 15;
-  const int nch = rb ? (T + DWR_TT - 1) / DWR_TT : (T + DWW_TCH - 1) / DWW_TCH;
+  const long need__ = esp_dwconv1d_wgrad_workspace_bytes(Bn, T, D, K);
+  ESP_ARG_CHECK(work_bytes >= need__, "esp_dwconv1d_wgrad: workspace %ld B < %ld B required (esp_dwconv1d_wgrad_workspace_bytes)", work_bytes, need__);
+  const int nch = dww_chunks(T, K);
   hipStream_t st = (hipStream_t)stream;
   if (K == 31)
     hipLaunchKernelGGL(dwconv_wgrad_rb_kernel<31>, dim3((D + 63) / 64, nch, Bn), dim3(256), 0, st, dy, x, work, T, D,
@@ -841,11 +860,17 @@ ESP_API int esp_dwconv1d_wgrad(const float* dy, const float* x, float* dW, int B
 }
 
 // BatchNorm1d training forward + Swish. mean/rstd (D) outputs; running stats updated when
-// run_mean != NULL.  workspace: >= D*1536 doubles (at most BN_CHUNKS row chunks, rows_per_block)
+// run_mean != NULL.  workspace: D doubles per row chunk (esp_bn_swish_fwd_workspace_bytes; at
+// most BN_CHUNKS chunks of rows_per_block rows)
+ESP_API long esp_bn_swish_fwd_workspace_bytes(int M, int D) {
+  return M <= 0 || D <= 0 ? 0 : 8L * D * nchunks(M, rows_per_block(M));
+}
 ESP_API int esp_bn_swish_fwd(const float* y, const float* gamma, const float* beta, float* s, float* mean, float* rstd,
                              float* run_mean, float* run_var, float momentum, float eps, int M, int D, double* work,
-                             int T, const int* tvalid, void* stream) {
+                             long work_bytes, int T, const int* tvalid, void* stream) {
   ESP_ARG_CHECK(!tvalid || (T > 0 && M % T == 0), "esp_bn_swish_fwd: M must be a multiple of T with tvalid");
+  const long need__ = esp_bn_swish_fwd_workspace_bytes(M, D);
+  ESP_ARG_CHECK(work_bytes >= need__, "esp_bn_swish_fwd: workspace %ld B < %ld B required (esp_bn_swish_fwd_workspace_bytes)", work_bytes, need__);
   if (!tvalid) T = M > 0 ? M : 1;
   const int rpb = rows_per_block(M), nb = nchunks(M, rpb);
   hipStream_t st = (hipStream_t)stream;
@@ -889,11 +914,17 @@ ESP_API int esp_bn_swish_eval(const float* y, const float* gamma, const float* b
 }
 
 // given ds = dL/ds, writes dy (grad wrt BN input) into `dy`; dgamma/dbeta accumulated.
-// workspace: >= 2*D*1536 doubles (at most BN_CHUNKS row chunks) + 2*D floats (sums) passed separately
+// workspace: 2*D doubles per row chunk (esp_bn_swish_bwd_workspace_bytes) + 2*D floats (sums)
+// passed separately
+ESP_API long esp_bn_swish_bwd_workspace_bytes(int M, int D) {
+  return M <= 0 || D <= 0 ? 0 : 8L * 2 * D * nchunks(M, rows_per_block(M));
+}
 ESP_API int esp_bn_swish_bwd(const float* ds, const float* y, const float* mean, const float* rstd, const float* gamma,
                              const float* beta, float* dy, float* dgamma, float* dbeta, int M, int D, double* work,
-                             float* sums, int T, const int* tvalid, void* stream) {
+                             long work_bytes, float* sums, int T, const int* tvalid, void* stream) {
   ESP_ARG_CHECK(!tvalid || (T > 0 && M % T == 0), "esp_bn_swish_bwd: M must be a multiple of T with tvalid");
+  const long need__ = esp_bn_swish_bwd_workspace_bytes(M, D);
+  ESP_ARG_CHECK(work_bytes >= need__, "esp_bn_swish_bwd: workspace %ld B < %ld B required (esp_bn_swish_bwd_workspace_bytes)", work_bytes, need__);
   if (!tvalid) T = M > 0 ? M : 1;
   const int rpb = rows_per_block(M), nb = nchunks(M, rpb);
   hipStream_t st = (hipStream_t)stream;

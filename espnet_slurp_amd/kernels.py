@@ -65,6 +65,53 @@ def _work(nbytes, device):
     return WS.get(nbytes, device)
 
 
+# ESP_GUARD=1: every workspace handed to a launcher gets a 256-byte canary right after the bytes
+# the launcher asked for (esp_*_workspace_bytes); after the launch a stream-ordered (and graph-
+# capturable) compare folds "canary overwritten" into a per-launcher device flag, and
+# check_guards() -- called by the trainer after every step in this mode -- raises naming the
+# launcher.  A debug mode: it adds a fill + compare per workspace launch and a sync per step.
+GUARD = os.environ.get("ESP_GUARD", "0") == "1"
+GUARD_BYTES = 256
+_GUARD_NAMES: list = []
+_GUARD_FLAGS = {}
+
+
+def _ws(pool: "_Workspace", launcher: str, nbytes: int, device) -> torch.Tensor:
+    """A workspace of at least nbytes for `launcher` (+ its canary in guard mode)."""
+    if not GUARD:
+        return pool.get(nbytes, device)
+    buf = pool.get(nbytes + GUARD_BYTES, device)
+    buf[nbytes:nbytes + GUARD_BYTES].fill_(0xA5)
+    return buf
+
+
+def _guard_post(launcher: str, buf: torch.Tensor, nbytes: int):
+    if not GUARD:
+        return
+    if launcher not in _GUARD_NAMES:
+        _GUARD_NAMES.append(launcher)
+    i = _GUARD_NAMES.index(launcher)
+    key = str(buf.device)
+    if key not in _GUARD_FLAGS:
+        _GUARD_FLAGS[key] = torch.zeros(64, dtype=torch.int32, device=buf.device)
+    bad = (buf[nbytes:nbytes + GUARD_BYTES] != 0xA5).any()
+    _GUARD_FLAGS[key][i:i + 1].add_(bad.to(torch.int32).view(1))
+
+
+def check_guards():
+    """Raise if any workspace canary was overwritten since the last check (ESP_GUARD=1)."""
+    for key, f in _GUARD_FLAGS.items():
+        hit = f.nonzero().flatten().tolist()
+        if hit:
+            f.zero_()
+            raise RuntimeError("espnet_slurp_amd: workspace overrun by " + ", ".join(_GUARD_NAMES[i] for i in hit)
+                               + f" on {key}")
+
+
+def _wsize(launcher: str, *dims) -> int:
+    return _native.workspace_bytes(launcher, *dims)
+
+
 def h2d(t: torch.Tensor, device) -> torch.Tensor:
     """Host tensor -> device through pinned memory, non-blocking: a pageable H2D copy would
     make the host wait for the stream to drain (a hidden synchronisation per call)."""
@@ -129,7 +176,7 @@ def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc
     bwd_act/pre: epilogue drop'(.)*act'(pre) (FFN backward); rowsum: += sum_k A(m,k) (bias grad)."""
     if R is not None and r_off is None:
         r_off = c_off
-    ws = _GEMM_WS.get(_GEMM_WS_BYTES, C.device)
+    ws = _ws(_GEMM_WS, "esp_gemm_f32", _GEMM_WS_BYTES, C.device)
     ica = (_native.I * 5)(*ic_a) if ic_a is not None else None
     icb = (_native.I * 5)(*ic_b) if ic_b is not None else None
     if _PROF is not None:
@@ -142,7 +189,8 @@ def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc
                  _p(R, r_off or 0), act, _p(aux, c_off) if aux is not None else None,
                  float(drop_p), seed & 0xFFFFFFFFFFFFFFFF,
                  int(bwd_act), _p(pre, c_off) if pre is not None else None, _p(rowsum),
-                 ctypes_ptr(ica), ctypes_ptr(icb), _p(ws), ws.numel(), _st())
+                 ctypes_ptr(ica), ctypes_ptr(icb), _p(ws), _GEMM_WS_BYTES, _st())
+    _guard_post("esp_gemm_f32", ws, _GEMM_WS_BYTES)
     if _PROF is not None:
         ev1.record()
         # fused-epilogue streams the launch must move besides A, B, C: residual R and
@@ -156,7 +204,7 @@ def gemm_bf16(M: int, N: int, K: int, A16, B16, C, *, lda, ldb, ldc, c_off=0, bi
     """C = alpha*epi(A B^T + bias) + beta*R with bf16 operands A [M][K], B [N][K] (torch.bfloat16,
     K-contiguous) and the fp32 epilogue of gemm() (esp_gemm_bf16)."""
     assert A16.dtype == torch.bfloat16 and B16.dtype == torch.bfloat16
-    ws = _GEMM_WS.get(_GEMM_WS_BYTES, C.device)
+    ws = _ws(_GEMM_WS, "esp_gemm_bf16", _GEMM_WS_BYTES, C.device)
     if _PROF is not None:
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
@@ -164,7 +212,8 @@ def gemm_bf16(M: int, N: int, K: int, A16, B16, C, *, lda, ldb, ldc, c_off=0, bi
     _native.call("esp_gemm_bf16", M, N, K, 1, 1, _p(A16), lda, 0, 0, _p(B16), ldb, 0, 0,
                  _p(C, c_off), ldc, 0, 0, _p(bias), float(alpha), float(beta), _p(R, c_off) if R is not None else None,
                  act, _p(aux, c_off) if aux is not None else None, float(drop_p), seed & 0xFFFFFFFFFFFFFFFF,
-                 int(bwd_act), _p(pre, c_off) if pre is not None else None, _p(ws), ws.numel(), _st())
+                 int(bwd_act), _p(pre, c_off) if pre is not None else None, _p(ws), _GEMM_WS_BYTES, _st())
+    _guard_post("esp_gemm_bf16", ws, _GEMM_WS_BYTES)
     if _PROF is not None:
         ev1.record()
         extra = 4.0 * M * N * ((R is not None) + (aux is not None) + (pre is not None))
@@ -263,9 +312,10 @@ def colsum(x2d, out, accumulate=True, M=None, N=None, ld=None):
     M = M if M is not None else x2d.shape[0]
     N = N if N is not None else x2d.shape[1]
     ld = ld if ld is not None else x2d.stride(0)
-    nb = (M + 31) // 32
-    w = _work(4 * N * max(nb, 1), x2d.device)
-    _native.call("esp_colsum", _p(x2d), M, N, ld, _p(out), int(accumulate), _p(w), _st())
+    n = _wsize("esp_colsum", M, N)
+    w = _ws(WS, "esp_colsum", n, x2d.device)
+    _native.call("esp_colsum", _p(x2d), M, N, ld, _p(out), int(accumulate), _p(w), n, _st())
+    _guard_post("esp_colsum", w, n)
 
 
 # ----------------------------------------------------------------------------- elementwise
@@ -308,8 +358,10 @@ def utterance_mvn(x, lens_i32):
 
 
 def grad_norm(g, max_norm, out3):
-    w = _WS2.get(8 * 1024, g.device)
-    _native.call("esp_grad_norm", _p(g), g.numel(), float(max_norm), _p(w), _p(out3), _st())
+    n = _wsize("esp_grad_norm", g.numel())
+    w = _ws(_WS2, "esp_grad_norm", n, g.device)
+    _native.call("esp_grad_norm", _p(g), g.numel(), float(max_norm), _p(w), n, _p(out3), _st())
+    _guard_post("esp_grad_norm", w, n)
 
 
 def adam(p, g, m, v, clip3, lr, b1, b2, eps, wd, step):
@@ -381,10 +433,11 @@ def layernorm_fwd(x2d, w, b, y, mean, rstd, eps=1e-12):
 
 def layernorm_bwd(dy, x, w, mean, rstd, dx, dw, db, accumulate=False):
     M, D = x.shape
-    nb = (M + 31) // 32
-    ws = _work(4 * 2 * D * max(nb, 1), x.device)
+    n = _wsize("esp_layernorm_bwd", M, D)
+    ws = _ws(WS, "esp_layernorm_bwd", n, x.device)
     _native.call("esp_layernorm_bwd", _p(dy), _p(x), _p(w), _p(mean), _p(rstd), _p(dx), int(accumulate), _p(dw),
-                 _p(db), M, D, _p(ws), _st())
+                 _p(db), M, D, _p(ws), n, _st())
+    _guard_post("esp_layernorm_bwd", ws, n)
 
 
 def glu_fwd(u, g):
@@ -404,21 +457,19 @@ def dwconv1d(x, W, bias, y, Bn, T, D, K, flip=False, tvalid=None):
 
 
 def dwconv1d_wgrad(dy, x, dW, Bn, T, D, K, tvalid=None):
-    nch = (T + 63) // 64
-    ws = _work(4 * Bn * nch * D * K, x.device)
-    _native.call("esp_dwconv1d_wgrad", _p(dy), _p(x), _p(dW), Bn, T, D, K, _p(ws), _p(tvalid), _st())
-
-
-# BatchNorm statistics are reduced in at most 1536 row chunks (norm.hip BN_CHUNKS): the
-# workspace holds D (forward) / 2D (backward) fp64 partials per chunk
-BN_MAX_CHUNKS = 1536
+    n = _wsize("esp_dwconv1d_wgrad", Bn, T, D, K)
+    ws = _ws(WS, "esp_dwconv1d_wgrad", n, x.device)
+    _native.call("esp_dwconv1d_wgrad", _p(dy), _p(x), _p(dW), Bn, T, D, K, _p(ws), n, _p(tvalid), _st())
+    _guard_post("esp_dwconv1d_wgrad", ws, n)
 
 
 def bn_swish_fwd(y, gamma, beta, s, mean, rstd, run_mean, run_var, momentum=0.1, eps=1e-5, T=0, tvalid=None):
     M, D = y.shape
-    ws = _work(8 * D * BN_MAX_CHUNKS, y.device)
+    n = _wsize("esp_bn_swish_fwd", M, D)
+    ws = _ws(WS, "esp_bn_swish_fwd", n, y.device)
     _native.call("esp_bn_swish_fwd", _p(y), _p(gamma), _p(beta), _p(s), _p(mean), _p(rstd), _p(run_mean),
-                 _p(run_var), float(momentum), float(eps), M, D, _p(ws), int(T), _p(tvalid), _st())
+                 _p(run_var), float(momentum), float(eps), M, D, _p(ws), n, int(T), _p(tvalid), _st())
+    _guard_post("esp_bn_swish_fwd", ws, n)
 
 
 def bn_swish_eval(y, gamma, beta, s, run_mean, run_var, mean, rstd, eps=1e-5):
@@ -430,9 +481,11 @@ def bn_swish_eval(y, gamma, beta, s, run_mean, run_var, mean, rstd, eps=1e-5):
 
 def bn_swish_bwd(ds, y, mean, rstd, gamma, beta, dy, dgamma, dbeta, sums, T=0, tvalid=None):
     M, D = y.shape
-    ws = _work(8 * 2 * D * BN_MAX_CHUNKS, y.device)
+    n = _wsize("esp_bn_swish_bwd", M, D)
+    ws = _ws(WS, "esp_bn_swish_bwd", n, y.device)
     _native.call("esp_bn_swish_bwd", _p(ds), _p(y), _p(mean), _p(rstd), _p(gamma), _p(beta), _p(dy), _p(dgamma),
-                 _p(dbeta), M, D, _p(ws), _p(sums), int(T), _p(tvalid), _st())
+                 _p(dbeta), M, D, _p(ws), n, _p(sums), int(T), _p(tvalid), _st())
+    _guard_post("esp_bn_swish_bwd", ws, n)
 
 
 # ----------------------------------------------------------------------------- attention
@@ -599,11 +652,11 @@ def relpos_dp(dS, lds, q_v, rel, nb, H, T, dp, ldp, bias_part, carry, du, dv, dq
     """linear_pos gradient input dp (P x 64H) from dS along its diagonals; pos_bias grads += the
     flash backward's column sums; legacy carries into dq."""
     _f32(dS, q_v, dp, bias_part, carry, du, dv, dq)
-    ng = (nb + 7) // 8
-    nfl = H * ng * (2 * T - 1) * 64
-    ws = _DP_WS.get(4 * nfl, dS.device)
+    n = _wsize("esp_relpos_dp", nb, H, T)
+    ws = _ws(_DP_WS, "esp_relpos_dp", n, dS.device)
     _native.call("esp_relpos_dp", _p(dS), lds, _p(q_v), int(rel), nb, H, T, _p(dp), ldp, _p(bias_part), _p(carry),
-                 _p(du), _p(dv), _p(dq, dq_off), ldq, _p(ws), ws.numel() // 4, _st())
+                 _p(du), _p(dv), _p(dq, dq_off), ldq, _p(ws), n // 4, _st())
+    _guard_post("esp_relpos_dp", ws, n)
 
 
 def relshift_bwd(dS, dbd, relpos, Z, T, P, lds=None, ldp=None):
@@ -620,10 +673,10 @@ def col2im_relu(dcol, z1, dz1, B, T1, F1, D):
 
 
 def conv1_wgrad(x, dz1, dW, db, B, T, F, D):
-    T1, F1 = (T - 3) // 2 + 1, (F - 3) // 2 + 1
-    nb = (B * T1 * F1 + 2047) // 2048
-    ws = _work(4 * nb * D * 10, x.device)
-    _native.call("esp_conv1_wgrad", _p(x), _p(dz1), _p(dW), _p(db), B, T, F, D, _p(ws), _st())
+    n = _wsize("esp_conv1_wgrad", B, T, F, D)
+    ws = _ws(WS, "esp_conv1_wgrad", n, x.device)
+    _native.call("esp_conv1_wgrad", _p(x), _p(dz1), _p(dW), _p(db), B, T, F, D, _p(ws), n, _st())
+    _guard_post("esp_conv1_wgrad", ws, n)
 
 
 def permute3(inp, out, O, Bd, Ad, accumulate=False):
@@ -643,10 +696,11 @@ def _need_f64(*ts):
 
 def ctc_loss(lp, labels, Umax, ilen_i32, tlen_i32, B, T, V, blank, gscale, zero_infinity, nll, grad):
     _need_f64(nll)
-    S = 2 * Umax + 1
-    ws = _work(8 * 2 * B * T * S, lp.device)  # fp64 alpha / beta
+    n = _wsize("esp_ctc_loss", B, T, Umax)  # fp64 alpha / beta
+    ws = _ws(WS, "esp_ctc_loss", n, lp.device)
     _native.call("esp_ctc_loss", _p(lp), _p(labels), Umax, _p(ilen_i32), _p(tlen_i32), B, T, V, blank,
-                 float(gscale), int(zero_infinity), _p(nll), _p(grad), _p(ws), _st())
+                 float(gscale), int(zero_infinity), _p(nll), _p(grad), _p(ws), n, _st())
+    _guard_post("esp_ctc_loss", ws, n)
 
 
 def label_smoothing(x, target, V, ignore, smoothing, gscale, grad, row_loss, row_stat):
@@ -727,5 +781,7 @@ def conv2_dgrad(dz2, W, z1, dz1, B, T1, F1, D):
     key = str(dz2.device)
     if key not in _ZEROS:
         _ZEROS[key] = torch.zeros(64, dtype=torch.float32, device=dz2.device)
-    wc = _WS2.get(9 * D * D * 4, dz2.device)
-    _native.call("esp_conv2_dgrad", _p(dz2), _p(W), _p(z1), _p(dz1), B, T1, F1, D, _p(_ZEROS[key]), _p(wc), _st())
+    n = _wsize("esp_conv2_dgrad", D)
+    wc = _ws(_WS2, "esp_conv2_dgrad", n, dz2.device)
+    _native.call("esp_conv2_dgrad", _p(dz2), _p(W), _p(z1), _p(dz1), B, T1, F1, D, _p(_ZEROS[key]), _p(wc), n, _st())
+    _guard_post("esp_conv2_dgrad", wc, n)

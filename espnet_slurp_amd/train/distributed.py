@@ -145,6 +145,7 @@ class FlatGradReducer:
             return ids
 
         hook.rest = rest
+        hook.done = lambda: front[0] >= len(self.buckets)
         return hook
 
     def broadcast_buffers(self, model):

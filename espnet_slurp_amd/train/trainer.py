@@ -91,7 +91,10 @@ class Trainer:
     def train_one_step(self, batch: Dict[str, torch.Tensor], check_finite: bool = True) -> Dict[str, torch.Tensor]:
         """One iteration of train_one_epoch's loop body; returns device-side stats."""
         with K.gemm_compute("bf16" if self.options.use_amp else "fp32"):
-            return self._train_one_step(batch, check_finite)
+            stats = self._train_one_step(batch, check_finite)
+        if K.GUARD:  # ESP_GUARD=1: workspace canaries checked after every step (syncs)
+            K.check_guards()
+        return stats
 
     def _train_one_step(self, batch, check_finite):
         if self.cuda_graph:
@@ -252,8 +255,14 @@ class Trainer:
             cap = torch.cuda.Stream(device=dev)
             segs = []
             cur = [torch.cuda.CUDAGraph()]
+            final = []
 
             def cut(ids):  # end the running segment where these buckets became complete
+                if hook.done():
+                    # the last buckets: nothing after them writes a gradient, so they ride the
+                    # trailing segment (ending it here would capture an empty graph)
+                    final.extend(ids)
+                    return
                 K.join_side(dev)
                 cur[0].capture_end()
                 segs.append((cur[0], list(ids)))
@@ -271,7 +280,7 @@ class Trainer:
                 del ctx
                 K.join_side(dev)
                 cur[0].capture_end()
-                segs.append((cur[0], hook.rest()))
+                segs.append((cur[0], final + hook.rest()))
             torch.cuda.current_stream(dev).wait_stream(cap)
             e.fwd, e.segs = gf, segs
         finally:
@@ -358,17 +367,25 @@ class Trainer:
         """iterator_stop (X1, trainer.py:505-510, 716-719): every rank stops when the first one
         runs out of batches.  The reference all-reduces a flag before EVERY batch (a host sync
         per step); here the ranks agree once on the shortest shard length up front, which
-        gives the same batches when the iterator knows its length (the sharded sampler
-        iterators do); an iterator without len() falls back to the per-step flag."""
+        gives the same batches when every rank's iterator knows its exact length (the sharded
+        sampler iterators do: `exact_len`).  If ANY rank's iterator has no exact length (no
+        len(), or a len() that is only a hint, e.g. an IterableDataset), every rank uses the
+        reference's per-batch flag protocol, so a rank that runs out early cannot leave the
+        others waiting in a collective."""
         if not self.distributed:
             yield from iterator
             return
         dev = self.model.flat.flat.device
-        n = len(iterator) if hasattr(iterator, "__len__") else -1
-        t = torch.tensor([n if n >= 0 else 2 ** 62], dtype=torch.int64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MIN)
-        n_min = int(t.item())
-        if n >= 0 or n_min < 2 ** 62:
+        exact = hasattr(iterator, "__len__") and getattr(iterator, "exact_len", True) \
+            and not isinstance(iterator, torch.utils.data.IterableDataset)
+        n = len(iterator) if exact else 0
+        # [shortest length, number of ranks WITHOUT an exact length]: one MIN and one SUM
+        t = torch.tensor([n if exact else 2 ** 62, 0 if exact else 1], dtype=torch.int64, device=dev)
+        t_min, t_cnt = t[:1].clone(), t[1:].clone()
+        dist.all_reduce(t_min, op=dist.ReduceOp.MIN)
+        dist.all_reduce(t_cnt, op=dist.ReduceOp.SUM)
+        if int(t_cnt.item()) == 0:
+            n_min = int(t_min.item())
             for i, item in enumerate(iterator):
                 if i >= n_min:
                     break

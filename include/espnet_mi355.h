@@ -30,7 +30,9 @@ int esp_abi_version(void);
  *   mode 2/3: im2col of an NHWC map (3x3, stride 2); im2col_x = {H, W, C, Ho, Wo}
  *   z = z1*nb2+z2 ; operand offset = z1*s1 + z2*s2
  *   act: 0 none, 1 ReLU, 2 Swish (pre-activation stored to aux if non-NULL); dropout with
- *   probability drop_p keyed by (seed, (z*M+m)*N+n).
+ *   probability drop_p keyed by (seed, (z*M+m)*N+n).  Every dropout site of this ABI rounds
+ *   drop_p to the nearest multiple of 1/65536 (at least 1/65536 when drop_p > 0: a positive p
+ *   never turns dropout off) and scales kept values by 1 / (1 - rounded p), so E[out] = in.
  *   bwd_act != 0 (backward of h = drop(act(pre)), positionwise_feed_forward.py:32): the
  *   epilogue is  v = drop'(acc + bias) * act'(pre)  with the dropout mask regenerated from
  *   (drop_p, seed); act must be 0 and aux NULL.
@@ -90,7 +92,8 @@ int esp_specaug(const float* x, float* y, int B, int T, int F, const int* lens, 
 /* UtteranceMVN(norm_means=True, norm_vars=False), in place (utterance_mvn.py:45-80) */
 int esp_utterance_mvn(float* x, int B, int T, int F, const int* lens, void* stream);
 /* clip_grad_norm_ + Adam over flat buffers (trainer.py:642-686, abs_task.py:78-79) */
-int esp_grad_norm(const float* g, long n, float max_norm, double* work, float* out3, void* stream);
+int esp_grad_norm(const float* g, long n, float max_norm, double* work, long work_bytes, float* out3,
+                  void* stream);
 int esp_adam(float* p, const float* g, float* m, float* v, long n, const float* clip3, float lr,
              float b1, float b2, float eps, float wd, int step, void* stream);
 /* Device-resident optimizer bookkeeping (a whole training step as one HIP graph):
@@ -114,9 +117,9 @@ int esp_layernorm_fwd(const float* x, const float* w, const float* b, float* y, 
                       float* rstd, int M, int D, float eps, void* stream);
 int esp_layernorm_bwd(const float* dy, const float* x, const float* w, const float* mean,
                       const float* rstd, float* dx, int accumulate, float* dw, float* db, int M,
-                      int D, float* work, void* stream);
+                      int D, float* work, long work_bytes, void* stream);
 int esp_colsum(const float* x, int M, int N, long ld, float* out, int accumulate, float* work,
-               void* stream);
+               long work_bytes, void* stream);
 int esp_glu_fwd(const float* u, float* g, long rows, int D, void* stream);
 int esp_glu_bwd(const float* u, const float* dg, float* du, long rows, int D, void* stream);
 /* tvalid (device int, nullable): the batch is padded to T frames per utterance but only the
@@ -128,16 +131,17 @@ int esp_glu_bwd(const float* u, const float* dg, float* du, long rows, int D, vo
 int esp_dwconv1d(const float* x, const float* W, const float* bias, float* y, int Bn, int T, int D,
                  int K, int flip, const int* tvalid, void* stream);
 int esp_dwconv1d_wgrad(const float* dy, const float* x, float* dW, int Bn, int T, int D, int K,
-                       float* work, const int* tvalid, void* stream);
+                       float* work, long work_bytes, const int* tvalid, void* stream);
 int esp_bn_swish_fwd(const float* y, const float* gamma, const float* beta, float* s, float* mean,
                      float* rstd, float* run_mean, float* run_var, float momentum, float eps, int M,
-                     int D, double* work, int T, const int* tvalid, void* stream);
+                     int D, double* work, long work_bytes, int T, const int* tvalid, void* stream);
 /* eval mode: statistics from run_mean / run_var (mean / rstd written for inspection) */
 int esp_bn_swish_eval(const float* y, const float* gamma, const float* beta, float* s, const float* run_mean,
                       const float* run_var, float eps, int M, int D, float* mean, float* rstd, void* stream);
 int esp_bn_swish_bwd(const float* ds, const float* y, const float* mean, const float* rstd,
                      const float* gamma, const float* beta, float* dy, float* dgamma, float* dbeta,
-                     int M, int D, double* work, float* sums, int T, const int* tvalid, void* stream);
+                     int M, int D, double* work, long work_bytes, float* sums, int T, const int* tvalid,
+                     void* stream);
 
 /* ---- attention glue (attention.py:64-96,145-165,240-263) */
 int esp_heads_split(const float* src, long ld, int col0, int B, int T, int H, int dk,
@@ -266,11 +270,11 @@ int esp_conv1_fwd(const float* x, const float* W, const float* bias, float* z, i
  * reference stores it; no 9x column buffer.  zeros16: >= 16 B of zeros (device); wc_work:
  * 9*D*D floats (the per-class weight re-layout).  D % 32 == 0. */
 int esp_conv2_dgrad(const float* dz2, const float* W, const float* z1, float* dz1, int B, int T1, int F1,
-                    int D, const float* zeros16, float* wc_work, void* stream);
+                    int D, const float* zeros16, float* wc_work, long work_bytes, void* stream);
 int esp_col2im_relu(const float* dcol, const float* z1, float* dz1, int B, int T1, int F1, int D,
                     void* stream);
 int esp_conv1_wgrad(const float* x, const float* dz1, float* dW, float* db, int B, int T, int F,
-                    int D, float* work, void* stream);
+                    int D, float* work, long work_bytes, void* stream);
 int esp_permute3(const float* in, float* out, int O, int Bd, int Ad, int accumulate, void* stream);
 
 /* ---- losses (ctc.py:39-97, label_smoothing_loss.py:41-63, nets_utils.py:299-320,
@@ -281,7 +285,7 @@ int esp_log_softmax(const float* x, float* y, long rows, int V, void* stream);
  * the final reductions.  nll (B) and row_loss (R) are fp64; work >= 2*B*T*(2*Umax+1) doubles. */
 int esp_ctc_loss(const float* lp, const long long* labels, int Umax, const int* ilen,
                  const int* tlen, int B, int T, int V, int blank, float gscale, int zero_infinity,
-                 double* nll, float* grad, double* work, void* stream);
+                 double* nll, float* grad, double* work, long work_bytes, void* stream);
 int esp_label_smoothing(const float* x, const long long* target, long rows, int V, int ignore,
                         float smoothing, float gscale, float* grad, double* row_loss, int* row_stat,
                         void* stream);
@@ -306,6 +310,22 @@ int esp_ctc_prefix_init(const float* lp, int T, int V, int blank, float* r0, voi
 int esp_ctc_prefix_score(const float* lp, int T, int V, const float* r_prev, const long long* last,
                          int out_len, const long long* cands, int NH, int C, int blank, int eos,
                          float* r_new, float* log_psi, void* stream);
+
+/* ---- workspace sizes.  Every launcher that takes a scratch `work` buffer also takes its size
+ * in bytes and fails (status -1, esp_last_error) when it is smaller than the size below, which is
+ * computed by the same code that picks the launcher's chunking: callers size their buffers from
+ * these queries, never from a restated formula.  Pure host arithmetic (no device call). */
+long esp_grad_norm_workspace_bytes(long n);
+long esp_layernorm_bwd_workspace_bytes(int M, int D);
+long esp_colsum_workspace_bytes(int M, int N);
+long esp_dwconv1d_wgrad_workspace_bytes(int Bn, int T, int D, int K);
+long esp_bn_swish_fwd_workspace_bytes(int M, int D);
+long esp_bn_swish_bwd_workspace_bytes(int M, int D);
+long esp_conv1_wgrad_workspace_bytes(int B, int T, int F, int D);
+long esp_conv2_dgrad_workspace_bytes(int D);
+long esp_ctc_loss_workspace_bytes(int B, int T, int Umax);
+/* esp_relpos_dp adapts its grouping to the buffer it gets; this is its preferred size */
+long esp_relpos_dp_workspace_bytes(int nb, int H, int T);
 
 #ifdef __cplusplus
 }

@@ -147,6 +147,27 @@ def test_library_exports_every_header_symbol():
     assert lib.esp_abi_version() == _native.ABI_VERSION
 
 
+def test_workspace_size_queries():
+    """esp_*_workspace_bytes (host arithmetic, no device call): the sizes the launchers check
+    against, from the same code that picks their chunking."""
+    from espnet_slurp_amd import _native
+    W = _native.workspace_bytes
+    M = 128 * 374
+    bn = W("esp_bn_swish_fwd", M, 256)
+    assert bn % (8 * 256) == 0 and 1 <= bn // (8 * 256) <= 1536      # <= BN_CHUNKS partial rows
+    assert W("esp_bn_swish_bwd", M, 256) == 2 * bn
+    assert W("esp_layernorm_bwd", M, 256) == 4 * 2 * 256 * ((M + 31) // 32)
+    assert W("esp_colsum", 100, 7) == 4 * 7 * 4
+    assert W("esp_ctc_loss", 128, 374, 40) == 8 * 2 * 128 * 374 * 81
+    assert W("esp_conv2_dgrad", 256) == 4 * 9 * 256 * 256
+    assert W("esp_grad_norm", 10 ** 8) == 8 * 1024
+    assert W("esp_dwconv1d_wgrad", 128, 374, 256, 31) == 4 * 128 * ((374 + 63) // 64) * 256 * 31
+    assert W("esp_relpos_dp", 128, 4, 374) == 4 * 4 * 16 * (2 * 374 - 1) * 64
+    assert W("esp_conv1_wgrad", 128, 1500, 80, 256) == 4 * ((128 * 749 * 39 + 2047) // 2048) * 256 * 10
+    for name in ("esp_bn_swish_fwd", "esp_layernorm_bwd", "esp_colsum"):
+        assert W(name, 0, 256) == 0
+
+
 def test_product_never_imports_oracle():
     pkg = os.path.join(ROOT, "espnet_slurp_amd")
     for dp, _, fs in os.walk(pkg):
@@ -293,6 +314,53 @@ def test_flat_grad_reducer_gloo_world2():
         p.join(timeout=60)
     assert sorted(r[0] for r in res) == [0, 1]
     assert all(r[1] and r[2] for r in res), res
+
+
+def _stop_worker(rank, world, port, q):
+    """Trainer._stop_aligned (iterator_stop, trainer.py:505-510): exact lengths on every rank
+    -> counted stop at the shortest; any rank without an exact length -> the per-batch flag."""
+    import types
+
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = []
+    try:
+        from espnet_slurp_amd.train.trainer import Trainer
+        fake = types.SimpleNamespace(distributed=True,
+                                     model=types.SimpleNamespace(flat=types.SimpleNamespace(flat=torch.zeros(1))))
+
+        class Hint(list):  # a len() that is only a hint: the iterator yields fewer items
+            exact_len = False
+
+            def __len__(self):
+                return 10
+
+        cases = [list(range(3 + 2 * rank)),                        # exact: 3 vs 5 -> 3
+                 list(range(4)) if rank == 0 else iter(range(2)),  # rank 1 has no len() -> 2
+                 Hint(range(2)) if rank == 1 else list(range(6))]  # rank 1 hints 10, yields 2 -> 2
+        for it in cases:
+            out.append(len(list(Trainer._stop_aligned(fake, it))))
+    except Exception as e:  # report instead of hanging the parent
+        print("worker", rank, "failed:", repr(e))
+    finally:
+        q.put((rank, out))
+        dist.destroy_process_group()
+
+
+def test_stop_aligned_gloo_world2():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stop_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] == [3, 2, 2] for r in res), res
 
 
 # ----------------------------------------------------------------------------- front end (§8(f) rank 1)

@@ -91,7 +91,12 @@ def test_two_rank_training_matches_ddp_oracle(dev, tmp_path, mode, accum):
     # parameters vs the fp64 DDP oracle (Adam's sign-like first steps: see test_gpu_trainer)
     diffs = np.concatenate([np.abs(res[0]["params"][n].double().numpy() - ref[n].numpy()).ravel() for n in ref])
     assert (diffs < 5e-6).mean() > 0.995, (diffs < 5e-6).mean()
-    assert diffs.max() <= 2e-3 * 4
+    # the elements that differ are Adam's sign-like updates of near-zero gradients: each
+    # update moves an element by about lr (exactly lr at step 1), so two trajectories that
+    # disagree on a sign differ by at most ~2 x the summed learning rates of the updates
+    lrs = [2e-3 * 10 ** 0.5 * min(n ** -0.5, n * 10 ** -1.5) for n in range(1, len(W.GLOBAL) // accum + 1)]
+    print(f"max |param - oracle| {diffs.max():.3g}, sign-flip bound {2 * sum(lrs):.3g}")
+    assert diffs.max() <= 2 * sum(lrs), (diffs.max(), 2 * sum(lrs))
     # recursive_average: the same weighted stats on every rank
     for a, b, o in zip(res[0]["stats"], res[1]["stats"], ref_stats):
         for k in ("loss", "loss_ctc", "loss_att", "acc"):

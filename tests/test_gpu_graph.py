@@ -102,6 +102,41 @@ def test_graph_distributed_world1(dev):
         dist.destroy_process_group()
 
 
+def test_eager_distributed_world1_rccl(dev):
+    """The eager DDP path on a 1-rank RCCL ("nccl") group: the bucket hooks launch
+    ReduceOp.AVG all-reduces (the branch the gloo tests cannot reach, distributed.py) while the
+    explicit backward runs; the steps equal the single-GPU eager steps."""
+    import socket
+
+    import torch.distributed as dist
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        from espnet_slurp_amd.optimizers.fused_adam import FusedAdam
+        from espnet_slurp_amd.schedulers.warmup_lr import WarmupLR
+        from espnet_slurp_amd.train.trainer import Trainer, TrainerOptions
+        cfg = small_cfg("latest")
+        model = build_model(cfg, dev)
+        load_seeded(model, cfg, 11)
+        model.train()
+        opt = FusedAdam(model.parameters(), model.flat, lr=1e-3)
+        td = Trainer(model, opt, WarmupLR(opt, 10), TrainerOptions(grad_clip=5.0), distributed=True,
+                     bucket_mb=0.02)
+        assert td.reducer is not None and td.reducer.backend == "nccl" and len(td.reducer.buckets) > 2
+        te, me, _, _ = _trainer(dev, False)
+        for _ in range(3):
+            a = td.train_one_step(_batch(dev))["loss"].item()
+            b = te.train_one_step(_batch(dev))["loss"].item()
+            assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (a, b)
+        td.resolve_pending()
+        te.resolve_pending()
+        assert torch.allclose(model.flat.flat, me.flat.flat, rtol=0, atol=1e-6)
+    finally:
+        dist.destroy_process_group()
+
+
 def test_graph_and_eager_with_weight_gradient_stream(dev, monkeypatch):
     """ESP_WGRAD_STREAM: weight gradients forked to a side stream (joined before any reader)
     give the same steps as the single-stream path, eager and captured."""

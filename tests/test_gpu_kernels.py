@@ -656,4 +656,63 @@ def test_dropout_pair_hash_masks_agree(dev, T):
     torch.cuda.synchronize()
     mask = (m4 != 0).view(M, N)
     assert torch.equal(yd != 0, mask) and torch.equal(yr != 0, mask)
-    assert rel_err(yd.cpu(), torch.where(mask, y0 / (1 - p), torch.zeros_like(y0)).cpu()) < 1e-6
+    pq = round(p * 65536) / 65536  # the ABI's quantized p (include/espnet_mi355.h, esp_gemm_f32)
+    assert rel_err(yd.cpu(), torch.where(mask, y0 / (1 - pq), torch.zeros_like(y0)).cpu()) < 1e-6
+
+
+def test_dropout_quantized_p_scale_and_tiny_p(dev):
+    """The rescale matches the quantized keep probability (1/(1 - round(p*65536)/65536)), and a
+    p below half a quantum still drops (it takes the smallest quantum, 1/65536)."""
+    n = 1 << 22
+    ones = torch.ones(n, device=dev)
+    y = K.scale_dropout(ones, torch.empty_like(ones), drop_p=0.1, seed=7)
+    kept = y[y != 0]
+    assert torch.all(kept == kept[0])
+    assert abs(kept[0].item() - 65536.0 / (65536 - 6554)) < 1e-6
+    y = K.scale_dropout(ones, torch.empty_like(ones), drop_p=1e-7, seed=7)
+    dropped = int((y == 0).sum().item())
+    assert 0 < dropped < 8 * n / 65536, dropped  # ~n/65536 = 64 expected
+
+
+def test_workspace_too_small_is_rejected(dev):
+    """A launcher given less scratch than esp_*_workspace_bytes reports fails loudly before
+    launching (no silent overrun, VERDICT r2 'weak' 8)."""
+    from espnet_slurp_amd import _native
+    M, N = 1000, 64
+    x = torch.randn(M, N, device=dev)
+    out = torch.zeros(N, device=dev)
+    need = _native.workspace_bytes("esp_colsum", M, N)
+    ws = torch.empty(need, dtype=torch.uint8, device=dev)
+    with pytest.raises(_native.NativeError, match="workspace"):
+        _native.call("esp_colsum", x.data_ptr(), M, N, N, out.data_ptr(), 0, ws.data_ptr(), need - 4,
+                     torch.cuda.current_stream().cuda_stream)
+    _native.call("esp_colsum", x.data_ptr(), M, N, N, out.data_ptr(), 0, ws.data_ptr(), need,
+                 torch.cuda.current_stream().cuda_stream)
+    assert torch.allclose(out, x.sum(0), atol=1e-4)
+
+
+def test_guard_mode_canaries(dev, monkeypatch):
+    """ESP_GUARD=1: workspace launches leave their canaries intact (a BatchNorm / LayerNorm /
+    GEMM step at a ragged size), and a canary overwrite is reported naming the launcher."""
+    monkeypatch.setattr(K, "GUARD", True)
+    M, D = 1013, 256
+    y = torch.randn(M, D, device=dev)
+    g, b = torch.ones(D, device=dev), torch.zeros(D, device=dev)
+    s, mean, rstd = torch.empty_like(y), torch.empty(D, device=dev), torch.empty(D, device=dev)
+    K.bn_swish_fwd(y, g, b, s, mean, rstd, None, None)
+    dw, db, dx = torch.zeros(D, device=dev), torch.zeros(D, device=dev), torch.empty_like(y)
+    K.layernorm_bwd(y, y, g, mean[:1].expand(M).contiguous(), rstd[:1].expand(M).contiguous(), dx, dw, db)
+    K.linear_fwd(y, torch.randn(64, D, device=dev), None, torch.empty(M, 64, device=dev))
+    K.check_guards()  # clean
+    n = _native_ws("esp_bn_swish_fwd", M, D)
+    buf = K.WS.get(n + K.GUARD_BYTES, dev)
+    K.bn_swish_fwd(y, g, b, s, mean, rstd, None, None)
+    buf[n + 3] = 0  # an overrun of one byte past the launcher's workspace
+    K._guard_post("esp_bn_swish_fwd", buf, n)
+    with pytest.raises(RuntimeError, match="esp_bn_swish_fwd"):
+        K.check_guards()
+
+
+def _native_ws(name, *dims):
+    from espnet_slurp_amd import _native
+    return _native.workspace_bytes(name, *dims)
