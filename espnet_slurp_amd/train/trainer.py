@@ -1,22 +1,27 @@
-"""Trainer step — the hot loop of espnet2/train/trainer.py:463-720 (train_one_epoch).
+"""Trainer — espnet2/train/trainer.py: the hot loop train_one_epoch (:463-720), its valid
+pass validate_one_epoch (:724-772) and the epoch driver run (:154-447).
 
 Per batch: forward (model(**batch)), weighted loss normalisation (:594-608), backward,
 bucketed RCCL gradient average (replaces DDP), clip_grad_norm_(grad_clip) on device,
 non-finite skip (:651-667), Adam + WarmupLR batch step (:671-686), zero_grad.
-Host synchronisation: one 3-float read (grad norm / finite flag) per optimizer step, which
-the reference also needs (torch.isfinite(grad_norm) on the host, :651).
+Host synchronisation: the finite flag of each optimizer step is read back asynchronously
+(the reference reads torch.isfinite(grad_norm) on the host, :651, a sync per step); the
+reporter's per-step values are snapshotted on device and read in one copy every
+log_interval steps.
 """
 from __future__ import annotations
 
 import dataclasses
+import logging
 import time
-from typing import Dict, Iterable, Optional, Tuple
+from pathlib import Path
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple, Union
 
 import torch
 import torch.distributed as dist
 
 from ..optimizers.fused_adam import FusedAdam, clip_grad_norm_
-from ..schedulers.warmup_lr import AbsBatchStepScheduler
+from ..schedulers.warmup_lr import AbsBatchStepScheduler, AbsEpochStepScheduler, AbsValEpochStepScheduler
 from .. import kernels as K
 from .distributed import FlatGradReducer, fused_stats_allreduce
 
@@ -39,6 +44,18 @@ class TrainerOptions:
     # The padding is invisible to the result: lengths, SpecAug draws, BatchNorm statistics and
     # the depthwise-convolution boundary use the batch's own padded length (device tvalid).
     graph_buckets: Optional[Tuple[int, int]] = None
+    # ---- epoch driver (Trainer.run, trainer.py:154-447; defaults of abs_task.py's arguments)
+    resume: bool = True
+    output_dir: Union[Path, str, None] = None
+    max_epoch: int = 40
+    seed: int = 0
+    patience: Optional[int] = None
+    keep_nbest_models: Union[int, List[int]] = 10
+    nbest_averaging_interval: int = 0
+    early_stopping_criterion: Sequence[str] = ("valid", "loss", "min")
+    best_model_criterion: Sequence[Sequence[str]] = (("train", "loss", "min"), ("valid", "loss", "min"),
+                                                     ("train", "acc", "max"), ("valid", "acc", "max"))
+    val_scheduler_criterion: Sequence[str] = ("valid", "loss")
 
 
 class _GraphEntry:
@@ -81,6 +98,7 @@ class Trainer:
         self._flag_host = torch.empty(1, dtype=torch.float32, pin_memory=cuda)
         self._flag_event = torch.cuda.Event() if cuda else None
         self._pending = False
+        self._last_weight = None  # the (all-reduced) weight of the last step, for the reporter
 
     @staticmethod
     def resume(checkpoint, model, reporter, optimizers, schedulers, scaler=None, ngpu: int = 0):
@@ -111,9 +129,11 @@ class Trainer:
             self.reducer.broadcast_buffers(model)
         loss, stats, weight = model(**batch)
         stats = {k: v for k, v in stats.items() if v is not None}
+        self._last_weight = weight
         if self.distributed:
             w = weight.to(torch.float32).view(1)
             stats, wsum = fused_stats_allreduce(stats, weight)
+            self._last_weight = wsum
             # (loss*weight).sum()/sum(weight)*world_size, DDP then averages  (trainer.py:594-606)
             loss = (loss * w).sum() / wsum * self.world
         loss = loss / opts.accum_grad
@@ -175,6 +195,8 @@ class Trainer:
         self._graphs[sig] = e  # most recently used last
         while len(self._graphs) > self.max_graphs:
             self._graphs.pop(next(iter(self._graphs)))
+        if not self.distributed:
+            self._last_weight = e.weight
         return e.stats
 
     def _device_body(self, speech, prep, with_opt: bool):
@@ -204,6 +226,7 @@ class Trainer:
         avg, wsum = fused_stats_allreduce({k: v for k, v in stats.items() if k != "grad_norm"}, weight)
         for k, v in avg.items():
             stats[k].copy_(v)
+        self._last_weight = wsum
         torch.div(weight.to(torch.float32).view(1), wsum, out=self._scale)
         if self.options.accum_grad > 1:
             self._scale.mul_(1.0 / self.options.accum_grad)
@@ -350,18 +373,119 @@ class Trainer:
 
     def train_one_epoch(self, iterator: Iterable, reporter=None) -> bool:
         """Loop over (utt_id, batch) like trainer.py:502-714; returns True if every step was
-        skipped (all_steps_are_invalid)."""
+        skipped (all_steps_are_invalid).  `reporter`: a SubReporter (train/reporter.py) gets,
+        per batch, iter_time, the model's stats weighted by the batch weight, and on every
+        optimizer step optim{i}_lr{j} + train_time, then next() (trainer.py:610,694-707);
+        any other callable gets the step's device stats."""
         self.model.train()
         self.sync_host_state()
         up0, sk0 = self.n_updates, self.n_skipped
-        for _, batch in self._stop_aligned(iterator):
+        rec = _EpochRecorder(self, reporter, train=True) if hasattr(reporter, "register") else None
+        it = iter(self._stop_aligned(iterator))
+        t_step = time.perf_counter()
+        while True:
+            t0 = time.perf_counter()
+            try:
+                _, batch = next(it)
+            except StopIteration:
+                break
+            t_load = time.perf_counter() - t0
+            if self.options.no_forward_run:  # trainer.py:530-532
+                if rec is not None:
+                    rec.push_empty(t_load)
+                continue
             stats = self.train_one_step(batch)
-            if reporter is not None:
+            if rec is not None:
+                update = self.iiter % self.options.accum_grad == 0
+                now = time.perf_counter()
+                rec.push(stats, self._last_weight, t_load, update, now - t_step if update else None)
+                if update:
+                    t_step = now
+            elif reporter is not None:
                 reporter(stats)
         self.resolve_pending()
         self.sync_host_state()
+        if rec is not None:
+            rec.flush()
         # trainer.py:436-440: True when no optimizer step of the epoch was applied
         return (self.n_skipped - sk0) == (self.n_updates - up0)
+
+    @torch.no_grad()
+    def validate_one_epoch(self, iterator: Iterable, reporter=None) -> None:
+        """trainer.py:724-772: the model in eval mode (no dropout / SpecAug, BatchNorm from its
+        running statistics), per batch the stats weighted by the batch weight (recursive_average
+        over the ranks: one fused all-reduce), iterator_stop across ranks."""
+        self.model.eval()
+        rec = _EpochRecorder(self, reporter, train=False) if reporter is not None else None
+        for _, batch in self._stop_aligned(iterator):
+            if self.options.no_forward_run:
+                continue
+            _, stats, weight = self.model(**batch)
+            stats = {k: v for k, v in stats.items() if v is not None}
+            if self.distributed:
+                stats, weight = fused_stats_allreduce(stats, weight)
+            if rec is not None:
+                rec.push(stats, weight, None, False, None)
+        if rec is not None:
+            rec.flush()
+
+    def run(self, train_iter_factory, valid_iter_factory, reporter=None, scaler=None) -> "object":
+        """Trainer.run (trainer.py:154-447) for this trainer's model / optimizer / scheduler:
+        resume from output_dir/checkpoint.pth, then per epoch: seed (seed + epoch), train, valid,
+        epoch-step schedulers, and on rank 0 the checkpoint, {epoch}epoch.pth, latest.pth, the
+        best-model links, n-best averaging and pruning; stop when every step of an epoch was
+        invalid or on early stopping; finally the n-best averages.  Returns the Reporter."""
+        from ..torch_utils.set_all_random_seed import set_all_random_seed
+        from . import checkpoint as CK
+        from .reporter import Reporter
+        o = self.options
+        keep = [o.keep_nbest_models] if isinstance(o.keep_nbest_models, int) else list(o.keep_nbest_models)
+        if len(keep) == 0:
+            logging.warning("No keep_nbest_models is given. Change to [1]")
+            keep = [1]
+        out = Path(o.output_dir) if o.output_dir is not None else None
+        rank0 = not self.distributed or dist.get_rank() == 0
+        reporter = reporter if reporter is not None else Reporter()
+        schedulers = [self.scheduler]
+        if out is not None and rank0:
+            out.mkdir(parents=True, exist_ok=True)
+        if o.resume and out is not None and (out / "checkpoint.pth").exists():
+            CK.resume(out / "checkpoint.pth", self.model, reporter, [self.optimizer], schedulers, scaler,
+                      ngpu=1 if self.model.flat.flat.is_cuda else 0)
+        start_epoch = reporter.get_epoch() + 1
+        if start_epoch == o.max_epoch + 1:
+            logging.warning(f"The training has already reached at max_epoch: {start_epoch}")
+        crit = [tuple(c) for c in o.best_model_criterion]
+        for iepoch in range(start_epoch, o.max_epoch + 1):
+            logging.info(f"{iepoch}/{o.max_epoch}epoch started")
+            set_all_random_seed(o.seed + iepoch)
+            reporter.set_epoch(iepoch)
+            with reporter.observe("train") as sub:
+                all_invalid = self.train_one_epoch(train_iter_factory.build_iter(iepoch), reporter=sub)
+            with reporter.observe("valid") as sub:
+                self.validate_one_epoch(valid_iter_factory.build_iter(iepoch), reporter=sub)
+            for sch in schedulers:
+                if isinstance(sch, AbsValEpochStepScheduler):
+                    sch.step(reporter.get_value(*o.val_scheduler_criterion))
+                elif isinstance(sch, AbsEpochStepScheduler):
+                    sch.step()
+            if rank0:
+                logging.info(reporter.log_message())
+                if out is not None:
+                    CK.save_checkpoint(out / "checkpoint.pth", self.model, reporter, [self.optimizer], schedulers,
+                                       scaler, trainer=self)
+                    CK.save_epoch(out, iepoch, self.model, reporter, crit, keep, o.nbest_averaging_interval)
+            if all_invalid:
+                logging.warning("The gradients at all steps are invalid in this epoch. Something seems wrong. "
+                                f"This training was stopped at {iepoch}epoch")
+                break
+            if o.patience is not None and reporter.check_early_stopping(o.patience, *o.early_stopping_criterion):
+                break
+        else:
+            logging.info(f"The training was finished at {o.max_epoch} epochs ")
+        if rank0 and out is not None:
+            CK.average_nbest_models(output_dir=out, reporter=reporter, best_model_criterion=crit, nbest=keep)
+        return reporter
 
     def _stop_aligned(self, iterator):
         """iterator_stop (X1, trainer.py:505-510, 716-719): every rank stops when the first one
@@ -399,3 +523,74 @@ class Trainer:
             yield item
         stop.fill_(1)
         dist.all_reduce(stop)
+
+
+class _EpochRecorder:
+    """Reporter bookkeeping of one epoch pass without a host sync per step: each step's stats,
+    weight and gradient-norm triple are copied into one small device tensor; every
+    log_interval steps (and at the end) the snapshots come to the host in one copy and are
+    registered in order, one reporter.next() per batch as the reference does."""
+
+    def __init__(self, trainer: Trainer, reporter, train: bool):
+        self.t = trainer
+        self.rep = reporter
+        self.train = train
+        self.items = []
+        li = trainer.options.log_interval
+        self.log_interval = li if li is not None else 100
+        sch = trainer.scheduler
+        self.sched_last = getattr(sch, "last_epoch", 0)
+        self.n_logged = 0
+
+    def push_empty(self, t_load):
+        self.items.append(("empty", t_load))
+
+    def push(self, stats, weight, t_load, update: bool, train_time):
+        keys = [k for k, v in stats.items() if v is not None and k != "grad_norm"]
+        dev = self.t.model.flat.flat.device
+        vals = [stats[k].detach().reshape(-1)[:1].to(torch.float32) if torch.is_tensor(stats[k])
+                else torch.tensor([float(stats[k])], dtype=torch.float32, device=dev) for k in keys]
+        w = weight if torch.is_tensor(weight) else torch.tensor([float(weight)])
+        w = w.detach().reshape(-1)[:1].to(device=dev, dtype=torch.float32)
+        parts = vals + [w] + ([self.t._clip.detach().clone()] if update else [])
+        snap = torch.cat([p.to(dev) for p in parts])
+        self.items.append(("step", keys, snap, t_load, update, train_time))
+        if len(self.items) >= self.log_interval:
+            self.flush()
+            if self.train and hasattr(self.rep, "log_message"):
+                logging.info(self.rep.log_message(-self.log_interval))
+
+    def flush(self):
+        if not self.items:
+            return
+        snaps = [it[2] for it in self.items if it[0] == "step"]
+        host = torch.cat(snaps).cpu().tolist() if snaps else []
+        pos = 0
+        for it in self.items:
+            if it[0] == "empty":
+                self.rep.register({"iter_time": it[1]})
+                self.rep.next()
+                continue
+            _, keys, snap, t_load, update, train_time = it
+            n = snap.numel()
+            v = host[pos:pos + n]
+            pos += n
+            if t_load is not None:
+                self.rep.register({"iter_time": t_load})
+            self.rep.register(dict(zip(keys, v[:len(keys)])), v[len(keys)])
+            if update:
+                finite = v[len(keys) + 3] != 0.0
+                lrs = self._lrs(finite)
+                self.rep.register(dict({f"optim0_lr{j}": lr for j, lr in enumerate(lrs)}, train_time=train_time))
+            self.rep.next()
+        self.items = []
+
+    def _lrs(self, finite: bool):
+        """optim0_lr{j} after this optimizer step (trainer.py:694-705): the scheduler stepped iff
+        the step was finite; WarmupLR's value is reconstructed from its step count."""
+        sch = self.t.scheduler
+        if finite and isinstance(sch, AbsBatchStepScheduler):
+            self.sched_last += 1
+        if hasattr(sch, "lr_at"):
+            return sch.lr_at(self.sched_last)
+        return [g["lr"] for g in self.t.optimizer.param_groups]

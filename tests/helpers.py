@@ -79,6 +79,12 @@ def load_seeded(model, cfg, seed):
     return P
 
 
+def keep_scale(p: float) -> float:
+    """The inverted-dropout rescale the C ABI applies: 1 / (1 - p rounded to 1/65536)
+    (include/espnet_mi355.h, esp_gemm_f32)."""
+    return 65536.0 / (65536.0 - max(1, round(p * 65536)))
+
+
 def rel_err(a, b):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)

@@ -10,7 +10,7 @@ import torch.nn.functional as F
 from espnet_slurp_amd import kernels as K
 from oracle import ctc_np
 from oracle import espnet_cpu as O
-from tests.helpers import golden, rel_err
+from tests.helpers import golden, keep_scale, rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -101,7 +101,7 @@ def test_gemm_epilogue(dev):
     pos = relu > 0
     frac = (kept & pos).sum().item() / pos.sum().item()
     assert abs(frac - 0.75) < 0.02, frac
-    assert torch.allclose(o1c[kept], relu[kept] / 0.75, atol=1e-4)
+    assert torch.allclose(o1c[kept], relu[kept] * keep_scale(0.25), atol=1e-4)
     # the element-wise backward regenerates the same mask
     g = torch.ones(M, N, device=dev)
     dx = torch.empty(M, N, device=dev)
@@ -126,7 +126,7 @@ def test_gemm_backward_activation_epilogue(dev, act):
     assert (out - ref).abs().max().item() <= 1e-5 * max(1.0, ref.abs().max().item())
     x = pre.double()
     g = (dy.double() @ W.double())
-    mask = (ref.cpu() != 0).double() / 0.8
+    mask = (ref.cpu() != 0).double() * keep_scale(0.2)
     d = torch.where(x > 0, 1.0, 0.0) if act == K.ACT_RELU else torch.sigmoid(x) * (1 + x * (1 - torch.sigmoid(x)))
     assert (out.cpu().double() - g * mask * d).abs().max().item() < 1e-4
 
@@ -148,7 +148,7 @@ def test_gemm_aux_derivative_then_multiply(dev, act, M, N, Kk):
     v = pre.cpu().double()
     keep = (h1.cpu() != 0) | (v <= 0 if act == K.ACT_RELU else torch.zeros_like(v, dtype=torch.bool))
     d = torch.where(v > 0, 1.0, 0.0) if act == K.ACT_RELU else torch.sigmoid(v) * (1 + v * (1 - torch.sigmoid(v)))
-    ref_der = torch.where(der.cpu() != 0, d / 0.9, 0.0)
+    ref_der = torch.where(der.cpu() != 0, d * keep_scale(0.1), 0.0)
     assert (der.cpu().double() - ref_der).abs().max().item() < 1e-5
     assert torch.equal((der.cpu() != 0), keep & (d != 0))
     g1, g2 = torch.empty(M, N, device=dev), torch.empty(M, N, device=dev)
@@ -656,8 +656,7 @@ def test_dropout_pair_hash_masks_agree(dev, T):
     torch.cuda.synchronize()
     mask = (m4 != 0).view(M, N)
     assert torch.equal(yd != 0, mask) and torch.equal(yr != 0, mask)
-    pq = round(p * 65536) / 65536  # the ABI's quantized p (include/espnet_mi355.h, esp_gemm_f32)
-    assert rel_err(yd.cpu(), torch.where(mask, y0 / (1 - pq), torch.zeros_like(y0)).cpu()) < 1e-6
+    assert rel_err(yd.cpu(), torch.where(mask, y0 * keep_scale(p), torch.zeros_like(y0)).cpu()) < 1e-6
 
 
 def test_dropout_quantized_p_scale_and_tiny_p(dev):
