@@ -55,20 +55,20 @@ SIGNATURES = {
     "esp_heads_split": [P, L, I, I, I, I, I, P, P, P],
     "esp_heads_split2": [P, L, I, I, I, I, I, P, P, P, P, P],
     "esp_add2d": [P, L, P, L, I, I, P],
-    "esp_attn_softmax_fwd": [P, P, I, I, F, P, I, I, P, P, F, U64, I, I, I, L, L, P],
+    "esp_attn_softmax_fwd": [P, P, I, I, F, P, I, I, P, P, F, U64, I, I, I, L, L, P, P],
     "esp_attn_softmax_bwd": [P, P, P, F, U64, F, L, I, L, P],
     "esp_relshift_bwd": [P, L, P, L, I, I, I, I, P],
     "esp_relpos_softmax_fwd": [P, P, L, I, I, P, F, P, P, P, F, U64, I, L, P],
     "esp_relpos_attn_fwd": [P, P, P, L, P, L, I, I, F, P, P, P, F, U64, I, L, P],
-    "esp_relpos_attn_probs": [P, P, P, L, P, L, I, I, I, F, P, P, P, F, U64, I, L, P],
+    "esp_relpos_attn_probs": [P, P, P, L, P, L, I, I, I, F, P, P, P, F, U64, I, L, P, P],
     "esp_attn_bwd_prep": [P, L, P, L, I, I, I, I, P, P, L, I, P],
     "esp_attn_dscores": [P, L, P, L, P, P, P, P, L, I, I, I, I, F, F, U64, I, L, P],
-    "esp_attn_softmax_bwd_relpos": [P, P, P, P, L, I, F, U64, F, L, I, L, P],
+    "esp_attn_softmax_bwd_relpos": [P, P, P, P, L, I, F, U64, F, L, I, L, P, P],
     "esp_relpos_attn_bwd": [P, L, P, L, P, P, P, L, I, I, F, F, U64, I, L, P],
     "esp_relpos_flash_fwd": [P, P, P, L, P, L, P, L, I, I, I, F, P, P, L, P, F, U64, I, P],
     "esp_relpos_flash_bwd": [P, P, P, L, P, L, P, L, I, I, I, F, P, P, P, L, P, F, U64, I, P, L, P, P, L, P, P, P],
     "esp_relpos_dp": [P, L, P, I, I, I, I, P, L, P, P, P, P, P, L, P, L, P],
-    "esp_fbank_fwd": [P, L, P, I, I, I, I, P, P, P, P, P, I, P, I, P],
+    "esp_fbank_fwd": [P, L, P, I, I, I, I, P, P, P, P, P, I, P, I, P, P],
     "esp_global_mvn": [P, P, I, I, I, P, P, I, I, P],
     "esp_conv2_dgrad": [P, P, P, P, I, I, I, I, P, P, L, P],
     "esp_conv1_fwd": [P, P, P, P, I, I, I, I, P],
@@ -98,7 +98,7 @@ SIGNATURES = {
 _RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I, "esp_set_gemm_compute": I,
              "esp_get_gemm_compute": I}
 _RESTYPES.update({k: L for k in SIGNATURES if k.endswith("_workspace_bytes")})
-ABI_VERSION = 19  # bumped whenever a signature in include/espnet_mi355.h changes
+ABI_VERSION = 20  # bumped whenever a signature in include/espnet_mi355.h changes
 
 _lib = None
 

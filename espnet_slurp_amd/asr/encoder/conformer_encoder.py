@@ -52,7 +52,7 @@ class EncoderLayer(nn.Module):
             h, c.ln_mac = self.norm_ff_macaron.fwd(x)
             x, c.ffm = self.feed_forward_macaron.fwd(h, x, self.ff_scale, p, seeds, training)
         h, c.ln_mha = self.norm_mha.fwd(x)
-        x, c.mha = self.self_attn.fwd(h, x, pos, klen, B, T, p, seeds, training)
+        x, c.mha = self.self_attn.fwd(h, x, pos, klen, B, T, p, seeds, training, tvalid=tvalid)
         if self.conv_module is not None:
             h, c.ln_conv = self.norm_conv.fwd(x)
             x, c.conv = self.conv_module.fwd(h, x, B, T, p, seeds, training, tvalid=tvalid)
@@ -170,9 +170,8 @@ class ConformerEncoder(AbsEncoder):
     def run_forward(self, feats, ilens_cpu, seeds: Seeds, training: bool, klen=None, tvalid=None):
         """tvalid: optional device int32 (1,) = the reference batch's T' when feats are padded
         to a length bucket (frames beyond are excluded from the convolution module's depthwise
-        padding and BatchNorm statistics; every other op is per frame or masked by klen)."""
-        if tvalid is not None and self.legacy:
-            raise NotImplementedError("length buckets need the latest rel_pos (legacy rel_shift depends on T')")
+        padding and BatchNorm statistics, and the legacy rel_shift is taken at T'; every other op
+        is per frame or masked by klen)."""
         B, T, _ = feats.shape
         if T < 7:
             raise TooShortUttError(

@@ -237,10 +237,14 @@ class ESPnetASRModel(AbsESPnetModel):
         host["hlens"] = self.encoder.output_lengths(sl_cpu, T).to(torch.int32)
         T_true = T
         if t_bucket is not None:
-            if self.frontend is not None:
-                raise NotImplementedError("length buckets: feature input only (frontend: null)")
             assert t_bucket >= T, (t_bucket, T)
             T = int(t_bucket)
+            if self.frontend is not None:
+                # raw samples padded to the frame bucket's sample count; the STFT's centre padding
+                # still reflects at this batch's own sample count (device nvalid)
+                host["nvalid"] = torch.tensor([n_samples], dtype=torch.int32)
+                n_samples = self.frontend.samples_for_frames(T)
+                assert n_samples <= T_in, (n_samples, T_in)
             # valid frames after Conv2dSubsampling of the batch's own padded length
             host["tvalid"] = torch.tensor([((T_true - 1) // 2 - 1) // 2], dtype=torch.int32)
         if u_bucket is not None and u_bucket > text_cpu.shape[1]:
@@ -268,7 +272,7 @@ class ESPnetASRModel(AbsESPnetModel):
         synchronisation, so the forward + backward can be captured as one HIP graph."""
         d = prep.dev
         if self.frontend is not None:  # raw samples -> log-mel on device (one kernel)
-            feats = self.frontend.apply_prepared(speech, d["wav_lens"], prep.n_samples)
+            feats = self.frontend.apply_prepared(speech, d["wav_lens"], prep.n_samples, d.get("nvalid"))
         else:
             feats = speech[:, : prep.T].contiguous().float()
         if self.specaug is not None and self.training:
@@ -303,7 +307,7 @@ class ESPnetASRModel(AbsESPnetModel):
         d = prep.dev
         with torch.no_grad():
             if self.frontend is not None:
-                feats = self.frontend.apply_prepared(speech, d["wav_lens"], prep.n_samples)
+                feats = self.frontend.apply_prepared(speech, d["wav_lens"], prep.n_samples, d.get("nvalid"))
             else:
                 feats = speech[:, : prep.T].contiguous().float()
             if self.specaug is not None and self.training:

@@ -114,6 +114,11 @@ class DefaultFrontend(torch.nn.Module):
     def num_frames(self, n_samples: int) -> int:
         return n_samples // self.hop_length + 1  # center=True: (N + 2*(n_fft//2) - n_fft)//hop + 1
 
+    def samples_for_frames(self, frames: int) -> int:
+        """The sample count a length bucket of `frames` frames pads a batch to: the largest N with
+        num_frames(N) == frames, so every batch whose frame count fits the bucket fits its samples."""
+        return frames * self.hop_length - 1
+
     def output_lengths(self, speech_lengths: torch.Tensor) -> torch.Tensor:
         return speech_lengths // self.hop_length + 1  # stft.py:150-155
 
@@ -125,8 +130,10 @@ class DefaultFrontend(torch.nn.Module):
             self._dev[key] = t
         return self._dev[key]
 
-    def apply_prepared(self, speech: torch.Tensor, wav_lens_i32: torch.Tensor, n_samples: int) -> torch.Tensor:
-        """speech (B, >= n_samples) on device, wav_lens device int32 -> (B, T, n_mels) log-mel."""
+    def apply_prepared(self, speech: torch.Tensor, wav_lens_i32: torch.Tensor, n_samples: int,
+                       nvalid: torch.Tensor = None) -> torch.Tensor:
+        """speech (B, >= n_samples) on device, wav_lens device int32 -> (B, T, n_mels) log-mel.
+        nvalid (length buckets): device int32, the batch's own sample count (reflection point)."""
         B = speech.shape[0]
         x = speech if speech.dtype == torch.float32 else speech.float()
         if x.stride(1) != 1:
@@ -135,7 +142,7 @@ class DefaultFrontend(torch.nn.Module):
         out = torch.empty(B, T, self.n_mels, dtype=torch.float32, device=x.device)
         t = self._device_tables(x.device)
         K.fbank_fwd(x, wav_lens_i32, B, n_samples, self.n_fft, self.hop_length, t["window"], t["twiddle"], t["melw"],
-                    t["lo"], t["hi"], self.n_mels, out, T)
+                    t["lo"], t["hi"], self.n_mels, out, T, nvalid=nvalid)
         return out
 
     def forward(self, input: torch.Tensor, input_lengths: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:

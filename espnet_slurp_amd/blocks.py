@@ -168,7 +168,9 @@ class RelPositionMultiHeadedAttention(nn.Module):
         b = f.fused([self.linear_q.bias, self.linear_k.bias, self.linear_v.bias], (3 * D,), grad)
         return w, b
 
-    def fwd(self, x2d, resid, pos_emb, klen, B, T, p_res, seeds: Seeds, training: bool):
+    def fwd(self, x2d, resid, pos_emb, klen, B, T, p_res, seeds: Seeds, training: bool, tvalid=None):
+        """tvalid (legacy only): the length-bucket T' (ConformerEncoder.run_forward); the legacy
+        rel_shift is taken at T' inside esp_relpos_attn_probs / esp_attn_softmax_bwd_relpos."""
         H, dk = self.h, self.d_k
         D = H * dk
         M = B * T
@@ -185,6 +187,9 @@ class RelPositionMultiHeadedAttention(nn.Module):
         K.heads_split2(qkv, 3 * D, 0, B, T, H, dk, self.pos_bias_u, q_u, self.pos_bias_v, q_v)
         pa = self.p if training else 0.0
         sa = seeds.next()
+        tv = tvalid if self.legacy else None
+        if tv is not None and (K.flash_ok(T, dk) or K.ATTN_DSCORES):
+            raise NotImplementedError("legacy rel_pos with length buckets: not with ESP_FLASH_ATTN / ESP_ATTN_DSCORES")
         if K.flash_ok(T, dk):
             # scores, softmax, dropout and P.V in one kernel: only ctx and 2 floats per row to HBM
             ctx_ = empty(M, D, like=x2d)
@@ -204,7 +209,7 @@ class RelPositionMultiHeadedAttention(nn.Module):
             # ac and the bd band on the MFMA inside the softmax kernel (latest and legacy
             # rel_shift): only attn and its dropout copy reach HBM
             K.relpos_attn_probs(q_u, q_v, qkv, 3 * D, p, D, relpos, B, H, math.sqrt(dk), klen, ac, pdrop, pa, sa, T,
-                                Tp, k_off=D)
+                                Tp, k_off=D, tvalid=tv)
         elif not self.legacy and K.relpos_fused_ok(T, dk):
             K.relpos_attn_fwd(q_u, q_v, qkv, 3 * D, p, D, B, H, math.sqrt(dk), klen, ac, pdrop, pa, sa, T, Tp,
                               k_off=D)
@@ -216,7 +221,7 @@ class RelPositionMultiHeadedAttention(nn.Module):
             K.gemm(T, P, dk, q_v, p, bd, mode_a=K.KC, lda=dk, mode_b=K.KC, ldb=D, ldc=Pp,
                    batch=Z, nb2=B, sa=(B * T * dk, T * dk), sb=(dk, 0), sc=(B * T * Pp, T * Pp))
             K.attn_softmax_fwd(ac, bd, relpos, P, math.sqrt(dk), klen, B, False, ac, pdrop, pa, sa, Z, T, T,
-                               lds=Tp, ldp=Pp)
+                               lds=Tp, ldp=Pp, tvalid=tv)
             del bd
         attn = ac
         pv = pdrop if pdrop is not None else attn
@@ -228,7 +233,7 @@ class RelPositionMultiHeadedAttention(nn.Module):
         so = seeds.next()
         self.linear_out.fwd(ctx_, out, drop_p=pr, seed=so, R=resid, beta=1.0)
         return out, Ctx(x=x2d, qkv=qkv, p=p, pos=pos_emb, q_u=q_u, q_v=q_v, attn=attn, pv=pv, ctx=ctx_,
-                        flash=False, pa=pa, sa=sa, pr=pr, so=so, B=B, T=T, P=P)
+                        flash=False, pa=pa, sa=sa, pr=pr, so=so, B=B, T=T, P=P, tvalid=tv)
 
     def bwd(self, c, dout):
         H, dk = self.h, self.d_k
@@ -268,7 +273,8 @@ class RelPositionMultiHeadedAttention(nn.Module):
         if fused or dscores:
             pass
         else:  # softmax + rel_shift adjoints in one pass (latest and legacy)
-            K.attn_softmax_bwd_relpos(c.attn, dS, dS, dbd, Pp, c.pa, c.sa, math.sqrt(dk), Z * T, T, Tp, relpos=relpos)
+            K.attn_softmax_bwd_relpos(c.attn, dS, dS, dbd, Pp, c.pa, c.sa, math.sqrt(dk), Z * T, T, Tp, relpos=relpos,
+                                      tvalid=c.tvalid)
         # dq_u = dS k -> dqkv[:, 0:D]
         K.gemm(T, dk, T, dS, c.qkv, dqkv, mode_a=K.KC, lda=Tp, mode_b=K.RC, ldb=3 * D, ldc=3 * D, b_off=D,
                batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * 3 * D), sc=(dk, T * 3 * D))

@@ -100,12 +100,16 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(const float* ac, const
                                                           int P, float sqrt_dk, const int* __restrict__ klen, int nb,
                                                           int causal, float* attn, float* __restrict__ pdrop,
                                                           uint32_t thr, float dscale, uint64_t seed, int Z, int Tq,
-                                                          int Tk, long lds, long ldp, const uint64_t* __restrict__ key) {
+                                                          int Tk, long lds, long ldp, const uint64_t* __restrict__ key,
+                                                          const int* __restrict__ tvalid) {
   seed = esp::keyed(seed, key);
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= (long)Z * Tq) return;
   const int i = (int)(row % Tq);
+  // legacy + length bucket: the rel_shift of the reference batch, length T' = *tvalid; rows
+  // i >= T' are padding (their scores skip the band: finite, never read by a valid row)
+  const int Ts = relpos == 2 && tvalid ? min(max(*tvalid, 1), Tq) : Tq;
   const int z = (int)(row / Tq);
   const int b = z % nb;  // z = h*nb + b
   int kl = klen ? klen[b] : Tk;
@@ -122,10 +126,9 @@ __global__ __launch_bounds__(256) void softmax_fwd_kernel(const float* ac, const
       float a = acr[j];
       if (relpos == 1) {
         a += bdz[(long)i * ldp + (j + Tq - 1 - i)];
-      } else if (relpos == 2) {
-        if (j <= i) a += bdz[(long)i * ldp + (j + Tq - 1 - i)];
+      } else if (relpos == 2 && i < Ts) {
+        if (j <= i) a += bdz[(long)i * ldp + (j + Ts - 1 - i)];
         else if (j > i + 1) a += bdz[(long)(i + 1) * ldp + (j - i - 2)];
-        else a += 0.f;
       }
       s = a / sqrt_dk;
     }
@@ -197,12 +200,22 @@ __global__ __launch_bounds__(256) void softmax_bwd_kernel(const float* __restric
 //                   dbd[i+1][j - i - 2] = dS[i][j] for j >= i+2 (the lower part of row i+1);
 //                   row 0's lower part has no source and is zeroed by row 0's wave.
 // Each dbd element has exactly one source (relshift_bwd_kernel's gather), so no atomics.
+// Legacy with tvalid (a length-bucketed batch padded from T' = *tvalid to T frames): the shift
+// is the reference batch's, T' - 1 - i, rows i >= T' and columns >= T' of dbd are zero, and the
+// upper part only moves j < T' (the padded keys are masked: their dS is 0, and writing it would
+// land on elements row i+1's lower part owns) -- the unpadded adjoint, zero-extended.
+__device__ __forceinline__ int legacy_tv(const int* tvalid, int T) {
+  if (!tvalid) return T;
+  const int t = *tvalid;
+  return t < 1 ? 1 : (t > T ? T : t);
+}
 template <int PER, int REL>
 __global__ __launch_bounds__(256) void softmax_bwd_relpos_kernel(const float* __restrict__ attn, const float* dP,
                                                                  float* dS, float* __restrict__ dbd, long ldp,
                                                                  uint32_t thr, float dscale, uint64_t seed,
                                                                  float sqrt_dk, long rows, int T, long lds,
-                                                                 const uint64_t* __restrict__ key) {
+                                                                 const uint64_t* __restrict__ key,
+                                                                 const int* __restrict__ tvalid) {
   seed = esp::keyed(seed, key);
   const int lane = threadIdx.x & 63;
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -228,22 +241,31 @@ __global__ __launch_bounds__(256) void softmax_bwd_relpos_kernel(const float* __
   dot = esp::wave_sum(dot);
   float* sr = dS + row * lds;
   float* br = dbd + row * ldp;
-  const int sh = T - 1 - i;
+  const int Ts = REL == 2 ? legacy_tv(tvalid, T) : T;  // the rel_shift's length
+  const bool live = REL == 1 || i < Ts;
+  const int sh = Ts - 1 - i;
 #pragma unroll
   for (int e = 0; e < PER; ++e) {
     const int j = lane + 64 * e;
     if (j < T) {
       const float v = a[e] * (g[e] - dot) / sqrt_dk;
       sr[j] = v;
+      if (!live) continue;
       if (REL == 1 || j <= i) br[j + sh] = v;
-      else if (j >= i + 2) br[ldp + j - i - 2] = v;  // row i+1 of the same z (i + 1 < T here)
+      else if (j >= i + 2 && j < Ts) br[ldp + j - i - 2] = v;  // row i+1 of the same z (i + 1 < Ts here)
     }
   }
   if (REL == 1) {
     for (int k = lane; k < sh; k += 64) br[k] = 0.f;
     for (int k = sh + T + lane; k < 2 * T - 1; k += 64) br[k] = 0.f;
-  } else if (i == 0) {
-    for (int k = lane; k < sh; k += 64) br[k] = 0.f;
+  } else {
+    if (!live) {
+      for (int k = lane; k < T; k += 64) br[k] = 0.f;
+    } else {
+      if (i == 0)
+        for (int k = lane; k < sh; k += 64) br[k] = 0.f;
+      for (int k = Ts + lane; k < T; k += 64) br[k] = 0.f;
+    }
   }
 }
 
@@ -257,7 +279,8 @@ __global__ __launch_bounds__(256) void softmax_bwd_relpos4_kernel(const float* _
                                                                   float* dS, float* __restrict__ dbd, long ldp,
                                                                   uint32_t thr, float dscale, uint64_t seed,
                                                                   float sqrt_dk, long rows, int T, long lds,
-                                                                  const uint64_t* __restrict__ key) {
+                                                                  const uint64_t* __restrict__ key,
+                                                                  const int* __restrict__ tvalid) {
   __shared__ __attribute__((aligned(16))) float stage[4][256 * Q];
   seed = esp::keyed(seed, key);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -313,21 +336,31 @@ __global__ __launch_bounds__(256) void softmax_bwd_relpos4_kernel(const float* _
   }
   asm volatile("" ::: "memory");  // wave-private LDS row: in-order within the wave
   float* br = dbd + row * ldp;
-  const int sh = T - 1 - i;
+  const int Ts = REL == 2 ? legacy_tv(tvalid, T) : T;  // the rel_shift's length (see the scalar kernel)
+  const bool live = REL == 1 || i < Ts;
+  const int sh = Ts - 1 - i;
+  if (live) {
 #pragma unroll
-  for (int e = 0; e < 4 * Q; ++e) {
-    const int j = lane + 64 * e;
-    if (j < T) {
-      const float v = st[j];
-      if (REL == 1 || j <= i) br[j + sh] = v;
-      else if (j >= i + 2) br[ldp + j - i - 2] = v;  // row i+1 of the same z (i + 1 < T here)
+    for (int e = 0; e < 4 * Q; ++e) {
+      const int j = lane + 64 * e;
+      if (j < T) {
+        const float v = st[j];
+        if (REL == 1 || j <= i) br[j + sh] = v;
+        else if (j >= i + 2 && j < Ts) br[ldp + j - i - 2] = v;  // row i+1 of the same z (i + 1 < Ts here)
+      }
     }
   }
   if (REL == 1) {
     for (int k = lane; k < sh; k += 64) br[k] = 0.f;
     for (int k = sh + T + lane; k < 2 * T - 1; k += 64) br[k] = 0.f;
-  } else if (i == 0) {
-    for (int k = lane; k < sh; k += 64) br[k] = 0.f;
+  } else {
+    if (!live) {
+      for (int k = lane; k < T; k += 64) br[k] = 0.f;
+    } else {
+      if (i == 0)
+        for (int k = lane; k < sh; k += 64) br[k] = 0.f;
+      for (int k = Ts + lane; k < T; k += 64) br[k] = 0.f;
+    }
   }
 }
 
@@ -754,7 +787,7 @@ __global__ __launch_bounds__(256, SPLIT == 2 ? 3 : 2) void relpos_attn_fwd16_ker
     const float* __restrict__ qu, const float* __restrict__ qv, const float* __restrict__ kmat, long ldk,
     const float* __restrict__ pm, long ldpm, int nb, float sqrt_dk, const int* __restrict__ klen,
     float* __restrict__ attn, float* __restrict__ pdrop, uint32_t thr, float dscale, uint64_t seed, int T, long lds,
-    const uint64_t* __restrict__ key) {
+    const uint64_t* __restrict__ key, const int* __restrict__ tvalid) {
   __shared__ float ring[4][RW_ROWS * RW_PITCH];
   __shared__ __attribute__((aligned(16))) float stage[4][RW_ROWS * RW_SPITCH];
   __shared__ float xch[2][4][RW_ROWS];  // SPLIT 2: per-wave row max / row sum partials
@@ -768,7 +801,11 @@ __global__ __launch_bounds__(256, SPLIT == 2 ? 3 : 2) void relpos_attn_fwd16_ker
   const int li = lane & 15, q4 = lane >> 4;
   const int nt = (T + 15) >> 4;
   const int g = i0 >> 4;
-  const int kb0 = T - RW_ROWS - i0;  // table position of band block 0, column 0
+  // legacy rel_shift length: the reference batch's T' (tvalid) when the batch is padded to a
+  // length bucket -- its table positions j + T'-1-i depend on T' (the latest ones, i - j, do not);
+  // rows i >= T' are padding (finite, never read by a valid row), their positions are clamped
+  const int Ts = LEGACY ? legacy_tv(tvalid, T) : T;
+  const int kb0 = Ts - RW_ROWS - i0;  // table position of band block 0, column 0
   const int P = LEGACY ? T : 2 * T - 1;
   const float inv_sqrt_dk = 1.0f / sqrt_dk;
   float* ring0 = ring[wave];
@@ -784,7 +821,7 @@ __global__ __launch_bounds__(256, SPLIT == 2 ? 3 : 2) void relpos_attn_fwd16_ker
   auto k_row = [&](int t) { return kmat + ((long)b * T + min(t * 16 + li, T - 1)) * ldk + head * RP_DK; };
   auto p_row = [&](int m) {
     int pos = kb0 + 16 * m + li;
-    if (LEGACY && pos > T) pos -= T + 1;  // the shifted band's table: p[j - i - 2]
+    if (LEGACY && pos > Ts) pos -= Ts + 1;  // the shifted band's table: p[j - i - 2]
     return pm + (long)min(max(pos, 0), P - 1) * ldpm + head * RP_DK;
   };
   float au[16], av[16], av2[16];
@@ -1016,7 +1053,7 @@ ESP_API int esp_add2d(const float* x, long ldx, float* y, long ldy, int M, int N
 // lds: row pitch of ac/attn/pdrop (>= Tk), ldp: row pitch of bd (>= P).
 ESP_API int esp_attn_softmax_fwd(const float* ac, const float* bd, int relpos, int P, float sqrt_dk, const int* klen,
                                  int nb, int causal, float* attn, float* pdrop, float drop_p, unsigned long long seed,
-                                 int Z, int Tq, int Tk, long lds, long ldp, void* stream) {
+                                 int Z, int Tq, int Tk, long lds, long ldp, const int* tvalid, void* stream) {
   ESP_ARG_CHECK(Tk <= 1024, "esp_attn_softmax_fwd: Tk=%d > 1024", Tk);
   ESP_ARG_CHECK(relpos == 0 || (Tq == Tk && bd), "esp_attn_softmax_fwd: rel-pos needs Tq==Tk and bd");
   ESP_ARG_CHECK(relpos != 1 || P == 2 * Tq - 1, "esp_attn_softmax_fwd: latest rel-pos needs P=2T-1");
@@ -1030,7 +1067,7 @@ ESP_API int esp_attn_softmax_fwd(const float* ac, const float* bd, int relpos, i
   hipStream_t st = (hipStream_t)stream;
 #define ESP_SM(PER)                                                                                                 \
   hipLaunchKernelGGL(softmax_fwd_kernel<PER>, grid, dim3(256), 0, st, ac, bd, relpos, P, sqrt_dk, klen, nb, causal, \
-                     attn, pdrop, thr, ds, (uint64_t)seed, Z, Tq, Tk, lds, ldp, esp::rng_key_ptr())
+                     attn, pdrop, thr, ds, (uint64_t)seed, Z, Tq, Tk, lds, ldp, esp::rng_key_ptr(), tvalid)
   if (Tk <= 64) ESP_SM(1);
   else if (Tk <= 128) ESP_SM(2);
   else if (Tk <= 256) ESP_SM(4);
@@ -1146,7 +1183,7 @@ ESP_API int esp_relpos_attn_fwd(const float* qu, const float* qv, const float* k
 ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float* kmat, long ldk, const float* p,
                                   long ldp_row, int relpos, int nb, int H, float sqrt_dk, const int* klen,
                                   float* attn, float* pdrop, float drop_p, unsigned long long seed, int T, long lds,
-                                  void* stream) {
+                                  const int* tvalid, void* stream) {
   ESP_ARG_CHECK(T >= 1 && T <= 512 && lds >= T && nb >= 1 && H >= 1, "esp_relpos_attn_probs: bad sizes T=%d", T);
   ESP_ARG_CHECK(relpos == 1 || relpos == 2, "esp_relpos_attn_probs: relpos must be 1 (latest) or 2 (legacy)");
   ESP_ARG_CHECK(lds % 4 == 0 && ((uintptr_t)attn & 15) == 0 && ((uintptr_t)pdrop & 15) == 0,
@@ -1168,7 +1205,7 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
   if (split) {
 #define ESP_RS3(N, P2_, L_)                                                                                            \
   hipLaunchKernelGGL((relpos_attn_fwd16_kernel<N, P2_, L_, 2>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p, ldp_row, \
-                     nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr())
+                     nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid)
 #define ESP_RS(N)                     \
   do {                                \
     if (relpos == 2) {                \
@@ -1190,7 +1227,7 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
   }
 #define ESP_RW3(N, P2_, L_)                                                                                         \
   hipLaunchKernelGGL((relpos_attn_fwd16_kernel<N, P2_, L_>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p, ldp_row, \
-                     nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr())
+                     nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid)
 #define ESP_RW(N)                             \
   do {                                        \
     if (relpos == 2) {                        \
@@ -1218,7 +1255,7 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
 // softmax backward + latest rel_shift adjoint in one pass (see softmax_bwd_relpos_kernel)
 ESP_API int esp_attn_softmax_bwd_relpos(const float* attn, const float* dP, float* dS, float* dbd, long ldp,
                                         int relpos, float drop_p, unsigned long long seed, float sqrt_dk, long rows,
-                                        int T, long lds, void* stream) {
+                                        int T, long lds, const int* tvalid, void* stream) {
   ESP_ARG_CHECK(relpos == 1 || relpos == 2, "esp_attn_softmax_bwd_relpos: relpos must be 1 or 2");
   ESP_ARG_CHECK(T >= 1 && T <= 1024 && lds >= T && ldp >= (relpos == 1 ? 2 * T - 1 : T) && rows % T == 0,
                 "esp_attn_softmax_bwd_relpos: bad sizes");
@@ -1233,10 +1270,10 @@ ESP_API int esp_attn_softmax_bwd_relpos(const float* attn, const float* dP, floa
   do {                                                                                                            \
     if (p2)                                                                                                       \
       hipLaunchKernelGGL((softmax_bwd_relpos4_kernel<Q, R, true>), grid, dim3(256), 0, st, attn, dP, dS, dbd, ldp, \
-                         thr, ds, (uint64_t)seed, sqrt_dk, rows, T, lds, esp::rng_key_ptr());                     \
+                         thr, ds, (uint64_t)seed, sqrt_dk, rows, T, lds, esp::rng_key_ptr(), tvalid);                     \
     else                                                                                                          \
       hipLaunchKernelGGL((softmax_bwd_relpos4_kernel<Q, R, false>), grid, dim3(256), 0, st, attn, dP, dS, dbd,     \
-                         ldp, thr, ds, (uint64_t)seed, sqrt_dk, rows, T, lds, esp::rng_key_ptr());                \
+                         ldp, thr, ds, (uint64_t)seed, sqrt_dk, rows, T, lds, esp::rng_key_ptr(), tvalid);                \
   } while (0)
 #define ESP_SB4R(Q)              \
   do {                           \
@@ -1255,10 +1292,10 @@ ESP_API int esp_attn_softmax_bwd_relpos(const float* attn, const float* dP, floa
   do {                                                                                                       \
     if (relpos == 1)                                                                                         \
       hipLaunchKernelGGL((softmax_bwd_relpos_kernel<PER, 1>), grid, dim3(256), 0, st, attn, dP, dS, dbd, ldp, \
-                         thr, ds, (uint64_t)seed, sqrt_dk, rows, T, lds, esp::rng_key_ptr());                \
+                         thr, ds, (uint64_t)seed, sqrt_dk, rows, T, lds, esp::rng_key_ptr(), tvalid);                \
     else                                                                                                     \
       hipLaunchKernelGGL((softmax_bwd_relpos_kernel<PER, 2>), grid, dim3(256), 0, st, attn, dP, dS, dbd, ldp, \
-                         thr, ds, (uint64_t)seed, sqrt_dk, rows, T, lds, esp::rng_key_ptr());                \
+                         thr, ds, (uint64_t)seed, sqrt_dk, rows, T, lds, esp::rng_key_ptr(), tvalid);                \
   } while (0)
   if (T <= 64) ESP_SBR(1);
   else if (T <= 128) ESP_SBR(2);

@@ -5,7 +5,9 @@
 // esp_fbank_fwd: one wave per frame, the whole chain in LDS/registers — HBM sees the raw
 // samples once and the log-mel features once (memory-bound: ~(hop + n_mels) * 4 B per frame).
 //   1. frame t of utterance b: samples t*hop - n_fft/2 + k (torch.stft center=True: reflect
-//      padding at the edges of the (B, N) tensor, N = max length in the batch), x window
+//      padding at the edges of the (B, N) tensor, N = max length in the batch), x window.
+//      A length-bucketed batch (the HIP-graph trainer) pads the samples past N; the reflection
+//      point stays the reference batch's N, read from the device (nvalid)
 //   2. n_fft-point complex FFT (radix-2, decimation in time, bit-reversed load), fp32; for an
 //      n_fft that is not a power of two (e.g. 400) a direct DFT per bin over the same twiddle
 //      table (exp(-2 pi i j / n_fft), j < n_fft) instead
@@ -21,7 +23,8 @@ constexpr int FB_WAVES = 4;  // frames per block
 __global__ __launch_bounds__(64 * FB_WAVES) void fbank_kernel(
     const float* __restrict__ wave, long ldw, const int* __restrict__ lens, int N, int T, int n_fft, int log2n,
     int hop, const float* __restrict__ window, const float2* __restrict__ twiddle, const float* __restrict__ melw,
-    const int* __restrict__ mlo, const int* __restrict__ mhi, int n_mels, float* __restrict__ out) {
+    const int* __restrict__ mlo, const int* __restrict__ mhi, int n_mels, float* __restrict__ out,
+    const int* __restrict__ nvalid) {
   extern __shared__ __attribute__((aligned(16))) float2 fbuf[];  // [FB_WAVES][n_fft] complex + power
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int b = blockIdx.y;
@@ -30,6 +33,7 @@ __global__ __launch_bounds__(64 * FB_WAVES) void fbank_kernel(
   float* pw = reinterpret_cast<float*>(a + n_fft);
   const int olen = lens[b] / hop + 1;
   const bool live = t < T && t < olen;
+  if (nvalid) N = min(max(*nvalid, n_fft / 2 + 1), N);
 
   // 1. windowed frame, stored at bit-reversed positions
   const float* xb = wave + (long)b * ldw;
@@ -120,7 +124,7 @@ __global__ void global_mvn_kernel(float* __restrict__ x, const int* __restrict__
 
 ESP_API int esp_fbank_fwd(const float* wave, long ldw, const int* lens, int B, int N, int n_fft, int hop,
                           const float* window, const float* twiddle, const float* melw, const int* mel_lo,
-                          const int* mel_hi, int n_mels, float* out, int T, void* stream) {
+                          const int* mel_hi, int n_mels, float* out, int T, const int* nvalid, void* stream) {
   int log2n = 0;
   while ((1 << log2n) < n_fft) ++log2n;
   if ((1 << log2n) != n_fft) log2n = 0;  // direct-DFT path
@@ -131,7 +135,8 @@ ESP_API int esp_fbank_fwd(const float* wave, long ldw, const int* lens, int B, i
   const size_t shm = (size_t)FB_WAVES * (n_fft + n_fft / 2 + 1) * sizeof(float2);
   dim3 grid((unsigned)((T + FB_WAVES - 1) / FB_WAVES), (unsigned)B);
   hipLaunchKernelGGL(fbank_kernel, grid, dim3(64 * FB_WAVES), shm, (hipStream_t)stream, wave, ldw, lens, N, T, n_fft,
-                     log2n, hop, window, reinterpret_cast<const float2*>(twiddle), melw, mel_lo, mel_hi, n_mels, out);
+                     log2n, hop, window, reinterpret_cast<const float2*>(twiddle), melw, mel_lo, mel_hi, n_mels, out,
+                     nvalid);
   ESP_CHECK_LAUNCH("esp_fbank_fwd");
   return 0;
 }

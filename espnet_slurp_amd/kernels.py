@@ -510,9 +510,9 @@ def pitch(n: int) -> int:
 
 
 def attn_softmax_fwd(ac, bd, relpos, P, sqrt_dk, klen_i32, nb, causal, attn, pdrop, drop_p, seed, Z, Tq, Tk,
-                     lds=None, ldp=None):
+                     lds=None, ldp=None, tvalid=None):
     _native.call("esp_attn_softmax_fwd", _p(ac), _p(bd), relpos, P, float(sqrt_dk), _p(klen_i32), nb, int(causal),
-                 _p(attn), _p(pdrop), float(drop_p), seed, Z, Tq, Tk, lds or Tk, ldp or max(P, 1), _st())
+                 _p(attn), _p(pdrop), float(drop_p), seed, Z, Tq, Tk, lds or Tk, ldp or max(P, 1), _p(tvalid), _st())
 
 
 def relpos_softmax_fwd(q_v, p, ldp_row, nb, H, ac, sqrt_dk, klen_i32, attn, pdrop, drop_p, seed, T, lds):
@@ -532,9 +532,9 @@ def relpos_attn_fwd(q_u, q_v, kmat, ldk, p, ldp_row, nb, H, sqrt_dk, klen_i32, a
 
 
 def relpos_attn_probs(q_u, q_v, kmat, ldk, p, ldp_row, relpos, nb, H, sqrt_dk, klen_i32, attn, pdrop, drop_p, seed,
-                      T, lds, k_off=0):
+                      T, lds, k_off=0, tvalid=None):
     """Rel-pos attention probabilities, latest (relpos 1) or legacy (relpos 2), one wave per 16
-    query rows (esp_relpos_attn_probs)."""
+    query rows (esp_relpos_attn_probs); tvalid: legacy length-bucket T' (device int32)."""
     _f32(q_u, q_v, kmat, p, attn, pdrop)
     if _PROF_ATTN is not None:
         ev0 = torch.cuda.Event(enable_timing=True)
@@ -542,7 +542,7 @@ def relpos_attn_probs(q_u, q_v, kmat, ldk, p, ldp_row, relpos, nb, H, sqrt_dk, k
         ev0.record()
     _native.call("esp_relpos_attn_probs", _p(q_u), _p(q_v), _p(kmat, k_off), ldk, _p(p), ldp_row, int(relpos), nb, H,
                  float(sqrt_dk), _p(klen_i32), _p(attn), _p(pdrop), float(drop_p), int(seed) & (2 ** 64 - 1), T, lds,
-                 _st())
+                 _p(tvalid), _st())
     if _PROF_ATTN is not None:
         ev1.record()
         nt = (T + 15) // 16
@@ -591,11 +591,11 @@ def attn_softmax_bwd(attn, dP, dS, drop_p, seed, sqrt_dk, rows, Tk, lds=None):
                  lds or Tk, _st())
 
 
-def attn_softmax_bwd_relpos(attn, dP, dS, dbd, ldp, drop_p, seed, sqrt_dk, rows, T, lds, relpos=1):
+def attn_softmax_bwd_relpos(attn, dP, dS, dbd, ldp, drop_p, seed, sqrt_dk, rows, T, lds, relpos=1, tvalid=None):
     """Softmax backward fused with the latest (relpos 1) or legacy (relpos 2) rel_shift adjoint
-    (writes dS and dbd)."""
+    (writes dS and dbd); tvalid: legacy length-bucket T' (device int32)."""
     _native.call("esp_attn_softmax_bwd_relpos", _p(attn), _p(dP), _p(dS), _p(dbd), ldp, int(relpos), float(drop_p),
-                 seed, float(sqrt_dk), rows, T, lds, _st())
+                 seed, float(sqrt_dk), rows, T, lds, _p(tvalid), _st())
 
 
 FUSED_ATTN_BWD = os.environ.get("ESP_FUSED_ATTN_BWD", "0") == "1"
@@ -756,11 +756,12 @@ def reserve_workspace(nbytes, device):
 
 
 # ----------------------------------------------------------------------------- front end
-def fbank_fwd(wave, lens_i32, B, N, n_fft, hop, window, twiddle, melw, mel_lo, mel_hi, n_mels, out, T):
-    """STFT -> power -> log-mel in one kernel (esp_fbank_fwd); wave (B, ldw) fp32 on device."""
+def fbank_fwd(wave, lens_i32, B, N, n_fft, hop, window, twiddle, melw, mel_lo, mel_hi, n_mels, out, T, nvalid=None):
+    """STFT -> power -> log-mel in one kernel (esp_fbank_fwd); wave (B, ldw) fp32 on device;
+    nvalid: device int32, the reflection point of a length-bucketed batch."""
     _f32(wave, window, twiddle, melw, out)
     _native.call("esp_fbank_fwd", _p(wave), wave.stride(0), _p(lens_i32), B, N, n_fft, hop, _p(window), _p(twiddle),
-                 _p(melw), _p(mel_lo), _p(mel_hi), n_mels, _p(out), T, _st())
+                 _p(melw), _p(mel_lo), _p(mel_hi), n_mels, _p(out), T, _p(nvalid), _st())
 
 
 def global_mvn(x, lens_i32, mean, std, norm_means=True, norm_vars=True):

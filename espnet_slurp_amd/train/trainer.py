@@ -166,14 +166,20 @@ class Trainer:
         last = self.iiter % opts.accum_grad == 0
         tb = ub = None
         if opts.graph_buckets is not None:
+            # frames padded to a multiple of bf (raw audio: the samples to the frame bucket's
+            # sample count), targets to a multiple of bu
             bf, bu = opts.graph_buckets
+            fe = getattr(model, "frontend", None)
             t_true = min(speech.shape[1], int(batch["speech_lengths"].max()))
-            tb = -(-t_true // bf) * bf
+            frames = fe.num_frames(t_true) if fe is not None else t_true
+            tb = -(-frames // bf) * bf
+            width = fe.samples_for_frames(tb) if fe is not None else tb
             ub = max(1, -(-int(batch["text_lengths"].max()) // bu)) * bu
-            if speech.shape[1] < tb:
-                speech = torch.nn.functional.pad(speech, (0, 0, 0, tb - speech.shape[1]))
-            elif speech.shape[1] > tb:
-                speech = speech[:, :tb]
+            pad = (0, width - speech.shape[1]) if speech.dim() == 2 else (0, 0, 0, width - speech.shape[1])
+            if speech.shape[1] < width:
+                speech = torch.nn.functional.pad(speech, pad)
+            elif speech.shape[1] > width:
+                speech = speech[:, :width]
         prep = model.prepare(batch["speech_lengths"], batch["text"], batch["text_lengths"], speech.shape[1],
                              speech.shape[2] if speech.dim() == 3 else 0, t_bucket=tb, u_bucket=ub)
         sig = (tuple(speech.shape), prep.T, prep.Umax, prep.L, prep.get("n_samples", 0), last,

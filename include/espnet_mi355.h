@@ -157,7 +157,7 @@ int esp_add2d(const float* x, long ldx, float* y, long ldy, int M, int N, void* 
 int esp_attn_softmax_fwd(const float* ac, const float* bd, int relpos, int P, float sqrt_dk,
                          const int* klen, int nb, int causal, float* attn, float* pdrop,
                          float drop_p, unsigned long long seed, int Z, int Tq, int Tk, long lds,
-                         long ldp, void* stream);
+                         long ldp, const int* tvalid, void* stream);  /* tvalid: legacy length bucket, see below */
 int esp_attn_softmax_bwd(const float* attn, const float* dP, float* dS, float drop_p,
                          unsigned long long seed, float sqrt_dk, long rows, int Tk, long lds,
                          void* stream);
@@ -168,7 +168,7 @@ int esp_relshift_bwd(const float* dS, long lds, float* dbd, long ldp, int relpos
  * rows = Z*T. */
 int esp_attn_softmax_bwd_relpos(const float* attn, const float* dP, float* dS, float* dbd, long ldp,
                                 int relpos, float drop_p, unsigned long long seed, float sqrt_dk,
-                                long rows, int T, long lds, void* stream);
+                                long rows, int T, long lds, const int* tvalid, void* stream);
 /* Fused latest rel-pos attention backward: dP = dctx V^T on the MFMA per 32-row block, attention
  * dropout adjoint, softmax adjoint, rel_shift adjoint -> dS (pitch lds) and dbd (pitch ldp).
  * dctx rows at dctx + (b*T+i)*ldd + 64h, V rows at vmat + (b*T+j)*ldv + 64h; d_k = 64, T <= 512. */
@@ -245,7 +245,11 @@ int esp_attn_dscores(const float* dctx, long ldd, const float* vmat, long ldv, c
 int esp_relpos_attn_probs(const float* qu, const float* qv, const float* kmat, long ldk, const float* p,
                           long ldp_row, int relpos, int nb, int H, float sqrt_dk, const int* klen,
                           float* attn, float* pdrop, float drop_p, unsigned long long seed, int T,
-                          long lds, void* stream);
+                          long lds, const int* tvalid, void* stream);
+/* tvalid (esp_relpos_attn_probs, esp_attn_softmax_bwd_relpos; legacy only, may be NULL): device int
+ * T' <= T when the batch is a length bucket padded from T' to T frames.  The legacy rel_shift then
+ * uses the reference batch's table positions j + T'-1-i (they depend on T'; the latest ones, i - j,
+ * do not), and the adjoint writes the unpadded dbd zero-extended (rows and columns >= T' are 0). */
 
 /* ---- feature front end: DefaultFrontend + GlobalMVN
  * esp_fbank_fwd: STFT (center, reflect, window of length n_fft, onesided) -> power -> mel
@@ -253,10 +257,12 @@ int esp_relpos_attn_probs(const float* qu, const float* qv, const float* kmat, l
  * log; frames t >= lens[b]/hop + 1 written as 0 (default.py:82-131, stft.py:63-160,
  * log_mel.py:57-81).  wave (B, N) row pitch ldw; lens (device int32, samples); twiddle
  * n_fft (cos, -sin) pairs of exp(-2 pi i j / n_fft); out (B, T, n_mels), T = N/hop + 1.
- * n_fft even in [16, 2048]: radix-2 FFT when a power of two, direct DFT otherwise. */
+ * n_fft even in [16, 2048]: radix-2 FFT when a power of two, direct DFT otherwise.
+ * nvalid (may be NULL): device int N' <= N, the reference batch's sample count when the batch is
+ * padded to a length bucket: the centre padding reflects at N' (frames >= N'/hop + 1 are 0). */
 int esp_fbank_fwd(const float* wave, long ldw, const int* lens, int B, int N, int n_fft, int hop,
                   const float* window, const float* twiddle, const float* melw, const int* mel_lo,
-                  const int* mel_hi, int n_mels, float* out, int T, void* stream);
+                  const int* mel_hi, int n_mels, float* out, int T, const int* nvalid, void* stream);
 /* GlobalMVN in place: x (B,T,F) -> ((x - mean), frames t >= lens[b] zeroed) / std
  * (global_mvn.py:67-90). */
 int esp_global_mvn(float* x, const int* lens, int B, int T, int F, const float* mean,

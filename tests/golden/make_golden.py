@@ -583,6 +583,82 @@ def checkpoint_fixture():
     print("checkpoint: ref -> ours -> ref round trip identical;", os.path.getsize(path), "bytes")
 
 
+TRAINRUN_TRAIN = [([96, 90, 71], [6, 5, 4], 300), ([96, 96, 80], [6, 3, 5], 301), ([88, 70, 64], [5, 5, 2], 302)]
+TRAINRUN_VALID = [([96, 81, 77], [6, 4, 5], 310), ([90, 60, 50], [3, 5, 4], 311)]
+
+
+def trainrun_batches(spec, epoch=0):
+    """(utt_ids, batch) lists of the Trainer.run fixture; the train order rotates per epoch."""
+    out = []
+    for i, (lens, ulens, seed) in enumerate(spec):
+        speech, slen, text, tlen = O.synthetic_batch(len(lens), max(lens), 80, 32, lens, ulens, seed)
+        out.append(([f"u{seed}_{k}" for k in range(len(lens))],
+                    dict(speech=speech, speech_lengths=slen, text=text, text_lengths=tlen)))
+    r = epoch % len(out)
+    return out[r:] + out[:r]
+
+
+TRAINRUN_OPTS = dict(max_epoch=3, seed=0, keep_nbest_models=[1, 2], nbest_averaging_interval=2, patience=None,
+                     early_stopping_criterion=("valid", "loss", "min"),
+                     best_model_criterion=[("valid", "acc", "max"), ("valid", "loss", "min"), ("train", "loss", "min")],
+                     val_scheduler_criterion=("valid", "loss"))
+
+
+def trainrun_fixture():
+    """The reference's epoch driver (VERDICT r2 'next' 6): Trainer.run (trainer.py:154-447) with
+    train_one_epoch + validate_one_epoch (:724-772) on the small golden model (dropout 0, no
+    SpecAug), 3 epochs of 3 train / 2 valid batches, Adam + WarmupLR + clip 5, best-model links,
+    n-best pruning (keep 1 and 2) and n-best averaging every 2 epochs.  Stored (JSON): the
+    reporter's per-epoch train / valid values, the files Trainer.run left in output_dir and the
+    targets of its links."""
+    import json
+    import tempfile
+    from pathlib import Path
+
+    from espnet2.iterators.abs_iter_factory import AbsIterFactory
+    from espnet2.train.distributed_utils import DistributedOption
+    from espnet2.train.trainer import Trainer as RefTrainer
+    from espnet2.train.trainer import TrainerOptions as RefOptions
+
+    class Factory(AbsIterFactory):
+        def __init__(self, spec):
+            self.spec = spec
+
+        def build_iter(self, epoch, shuffle=None):
+            return trainrun_batches(self.spec, epoch)
+
+    cfg = small_cfg("latest")
+    model = build_reference(cfg)
+    load_params(model, cfg, 21)
+    opt = torch.optim.Adam(model.parameters(), lr=0.002, betas=(0.9, 0.98), eps=1e-9, weight_decay=1e-6)
+    sch = WarmupLR(opt, warmup_steps=10)
+    with tempfile.TemporaryDirectory() as td:
+        o = RefOptions(ngpu=0, resume=True, use_amp=False, train_dtype="float32", grad_noise=False, accum_grad=1,
+                       grad_clip=5.0, grad_clip_type=2.0, log_interval=None, no_forward_run=False,
+                       use_matplotlib=False, use_tensorboard=False, use_wandb=False, output_dir=td,
+                       sharded_ddp=False, unused_parameters=False, wandb_model_log_interval=-1,
+                       create_graph_in_tensorboard=False, **TRAINRUN_OPTS)
+        RefTrainer.run(model=model, optimizers=[opt], schedulers=[sch], train_iter_factory=Factory(TRAINRUN_TRAIN),
+                       valid_iter_factory=Factory(TRAINRUN_VALID), plot_attention_iter_factory=None,
+                       trainer_options=o, distributed_option=DistributedOption(distributed=False, ngpu=0))
+        out = Path(td)
+        from espnet_slurp_amd.train.checkpoint import safe_load
+        rep = safe_load(out / "checkpoint.pth")["reporter"]
+        values = {}
+        for e, per in rep["stats"].items():
+            values[str(e)] = {ph: {k: float(v) for k, v in d.items() if k in ("loss", "loss_att", "loss_ctc", "acc",
+                                                                                "optim0_lr0")}
+                              for ph, d in per.items() if ph in ("train", "valid")}
+        files = sorted(p.name for p in out.iterdir())
+        links = {p.name: str(p.readlink()) for p in out.iterdir() if p.is_symlink()}
+    meta = {"values": values, "files": files, "links": links, "seed": 21, "opts": TRAINRUN_OPTS,
+            "adam": {"lr": 0.002, "betas": [0.9, 0.98], "eps": 1e-9, "weight_decay": 1e-6}, "warmup_steps": 10}
+    with open(os.path.join(HERE, "trainrun_ref.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+    print("trainrun:", files, links)
+    print(json.dumps(values, indent=1)[:1500])
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["ctc", "align", "specaug", "small", "c1", "train", "full", "frontend", "checkpoint"]
     if "frontend" in which:
@@ -626,3 +702,5 @@ if __name__ == "__main__":
         fullsize_train_fixture("fullsize_c4_grad_latest", c4, seed=53)
     if "slurp" in which:
         slurp_yaml_fixture()
+    if "trainrun" in which:
+        trainrun_fixture()

@@ -4,7 +4,10 @@ must compute exactly what the reference computes on the batch itself, padded onl
 maximum length: BatchNorm statistics over B x T' of THIS batch and the depthwise convolution's
 zero padding at T' (convolution.py:56-79), CTC / label-smoothing denominators and SpecAug draws
 from this batch's lengths (espnet_model.py:199,379-396; time_warp.py; mask_along_axis.py).
-Kernel level: esp_dwconv1d / esp_bn_swish_* with the device valid-frame bound `tvalid`."""
+Kernel level: esp_dwconv1d / esp_bn_swish_* with the device valid-frame bound `tvalid`.
+Legacy rel-pos (the SLURP YAML's default, conformer_encoder.py:98,116-120): its rel_shift
+(attention.py:145-165) reads table positions j + T'-1-i, so the padded batch takes T' from
+`tvalid` in esp_relpos_attn_probs and esp_attn_softmax_bwd_relpos."""
 import pytest
 import torch
 
@@ -72,11 +75,11 @@ def test_dwconv_and_bn_with_valid_frames(dev, Kw):
     assert (g0 - g1).abs().max().item() <= 1e-5 * max(1.0, g0.abs().max().item())
 
 
-def _trainer(dev, graph, buckets=None, specaug=None):
+def _trainer(dev, graph, buckets=None, specaug=None, rel="latest"):
     from espnet_slurp_amd.optimizers.fused_adam import FusedAdam
     from espnet_slurp_amd.schedulers.warmup_lr import WarmupLR
     from espnet_slurp_amd.train.trainer import Trainer, TrainerOptions
-    cfg = small_cfg("latest")
+    cfg = small_cfg(rel)
     model = build_model(cfg, dev, dropout=0.0, specaug=specaug)
     load_seeded(model, cfg, 11)
     model.train()
@@ -95,8 +98,9 @@ def _copy(b):
     return dict(b, speech=b["speech"].clone(), text=b["text"].clone())
 
 
-@pytest.mark.parametrize("with_specaug", [False, True])
-def test_bucketed_graph_equals_eager_unpadded(dev, with_specaug):
+@pytest.mark.parametrize("with_specaug,rel", [(False, "latest"), (True, "latest"), (False, "legacy"),
+                                              (True, "legacy")])
+def test_bucketed_graph_equals_eager_unpadded(dev, with_specaug, rel):
     """Batches of different frame / token lengths in one bucket (T <= 128, U <= 8) replay one
     graph; a longer batch captures a second.  Every step equals the eager step on the batch as
     the reference pads it (its own max lengths) to 1e-6: losses and parameters."""
@@ -105,8 +109,8 @@ def test_bucketed_graph_equals_eager_unpadded(dev, with_specaug):
         from espnet_slurp_amd.asr.specaug.specaug import SpecAug
         specaug = SpecAug(time_warp_window=5, freq_mask_width_range=(0, 10), num_freq_mask=2,
                           time_mask_width_range=(0, 12), num_time_mask=2)
-    te, me = _trainer(dev, False, specaug=specaug)
-    tg, mg = _trainer(dev, True, buckets=(64, 8), specaug=specaug)
+    te, me = _trainer(dev, False, specaug=specaug, rel=rel)
+    tg, mg = _trainer(dev, True, buckets=(64, 8), specaug=specaug, rel=rel)
     batches = [
         _batch(dev, 112, [112, 90, 71], [6, 5, 4], 21),   # bucket (128, 8): captured
         _batch(dev, 97, [97, 97, 97], [7, 3, 5], 22),      # same bucket, equal lengths (whole-batch warp)
@@ -138,15 +142,16 @@ def test_bucketed_graph_equals_eager_unpadded(dev, with_specaug):
         assert (a - b).abs().max().item() <= tol, (n, (a - b).abs().max().item())
 
 
+@pytest.mark.parametrize("rel", ["latest", "legacy"])
 @pytest.mark.parametrize("T,lens,ulens", [(112, [112, 90, 71], [6, 5, 4]), (128, [128, 100, 90], [8, 5, 4]),
                                           (70, [70, 70, 70], [1, 2, 3]), (129, [129, 64, 100], [9, 9, 9])])
-def test_bucketed_gradients_equal_unpadded(dev, T, lens, ulens):
+def test_bucketed_gradients_equal_unpadded(dev, T, lens, ulens, rel):
     """One forward + backward on the batch padded to its bucket (64 frames, 8 tokens) vs on the
     batch itself: the loss and every parameter gradient agree to 1e-6 (relative to the
     tensor's largest gradient)."""
     grads, losses = [], []
     for buck in (None, (64, 8)):
-        _, m = _trainer(dev, False)
+        _, m = _trainer(dev, False, rel=rel)
         m.flat.grad.zero_()
         b = _batch(dev, T, lens, ulens, 31)
         speech = b["speech"]
@@ -200,3 +205,52 @@ def test_bucketed_graph_count_bounded_over_epoch(dev):
     buckets = {(len(k), -(-max(int(lens[int(u[1:])]) for u in k) // 64), -(-max(int(ulens[int(u[1:])]) for u in k) // 8))
                for k in batches}
     assert len(tg._graphs) <= len(buckets) < len(shapes), (len(tg._graphs), len(buckets), len(shapes))
+
+
+def _wave(lens, seed, U=6):
+    g = torch.Generator().manual_seed(seed)
+    n = max(lens)
+    x = torch.randn(len(lens), n, generator=g) * 0.3
+    for b, m in enumerate(lens):
+        x[b, m:] = 0.0
+    text = torch.randint(2, 31, (len(lens), U), generator=g)
+    tlen = torch.tensor([U, U - 2, U - 1][:len(lens)])
+    for b, m in enumerate(tlen.tolist()):
+        text[b, m:] = -1
+    return dict(speech=x, speech_lengths=torch.tensor(lens), text=text, text_lengths=tlen)
+
+
+@pytest.mark.parametrize("rel", ["latest", "legacy"])
+def test_bucketed_graph_with_frontend_equals_eager(dev, rel):
+    """frontend: default (raw samples, the slurp_entity recipe's feats_type raw,
+    egs2/slurp_entity/asr1/run.sh:23) with length buckets: the sample axis is padded to the frame
+    bucket's sample count and the STFT's centre padding reflects at the batch's own sample
+    count (device nvalid, esp_fbank_fwd).  Every step equals the eager step on the batch as the
+    reference pads it; three batches share one graph."""
+    from espnet_slurp_amd.asr.frontend.default import DefaultFrontend
+    from espnet_slurp_amd.optimizers.fused_adam import FusedAdam
+    from espnet_slurp_amd.schedulers.warmup_lr import WarmupLR
+    from espnet_slurp_amd.train.trainer import Trainer, TrainerOptions
+    runs = []
+    for graph, buckets in ((False, None), (True, (32, 8))):
+        cfg = small_cfg(rel)
+        model = build_model(cfg, dev, dropout=0.0, frontend=DefaultFrontend())
+        P = O.deterministic_params(cfg, 21)
+        P["frontend.logmel.melmat"] = model.state_dict()["frontend.logmel.melmat"].cpu()
+        model.load_state_dict(P, strict=True)
+        model.train()
+        opt = FusedAdam(model.parameters(), model.flat, lr=1e-3)
+        tr = Trainer(model, opt, WarmupLR(opt, warmup_steps=10), TrainerOptions(grad_clip=5.0, graph_buckets=buckets),
+                     cuda_graph=graph)
+        losses = []
+        for i, lens in enumerate(([9000, 7731, 6400], [8500, 8500, 3000], [11000, 5000, 9999], [6000, 5900, 4000])):
+            b = _wave(lens, 40 + i)
+            b["speech"] = b["speech"].to(dev)
+            losses.append(tr.train_one_step(b)["loss"].item())
+        tr.resolve_pending()
+        tr.sync_host_state()
+        runs.append((losses, model.flat.flat.clone(), len(tr._graphs)))
+    (le, fe, _), (lg, fg, ng) = runs
+    assert all(abs(a - b) <= 1e-6 * max(1.0, abs(a)) for a, b in zip(le, lg)), (le, lg)
+    assert ng == 2, ng  # frame buckets 96 (three batches) and 64
+    assert (fe - fg).abs().max().item() <= 4e-3  # Adam's sign-like steps: see the test above

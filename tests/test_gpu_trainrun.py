@@ -1,0 +1,97 @@
+"""The epoch driver (VERDICT r2 "next" 6): Trainer.run = train_one_epoch + validate_one_epoch +
+checkpoint / best links / n-best pruning / n-best averaging (espnet2/train/trainer.py:154-447,
+724-772) against the reference's own Trainer.run on the same model, data and options
+(tests/golden/trainrun_ref.json, make_golden.py trainrun): per-epoch reporter values, the
+files left in output_dir and the targets of every link; then resume from that output_dir."""
+import json
+import os
+
+import pytest
+import torch
+
+from oracle import espnet_cpu as O
+from tests.helpers import GOLDEN, build_model, load_seeded, small_cfg
+
+pytestmark = pytest.mark.gpu
+
+TRAIN = [([96, 90, 71], [6, 5, 4], 300), ([96, 96, 80], [6, 3, 5], 301), ([88, 70, 64], [5, 5, 2], 302)]
+VALID = [([96, 81, 77], [6, 4, 5], 310), ([90, 60, 50], [3, 5, 4], 311)]
+
+
+class _Factory:
+    """build_iter(epoch) -> [(utt_ids, batch)]: the train order rotates per epoch, as in the
+    fixture generator (make_golden.trainrun_batches)."""
+
+    def __init__(self, spec, dev):
+        self.items = []
+        for lens, ulens, seed in spec:
+            speech, slen, text, tlen = O.synthetic_batch(len(lens), max(lens), 80, 32, lens, ulens, seed)
+            self.items.append(([f"u{seed}_{k}" for k in range(len(lens))],
+                               dict(speech=speech.to(dev), speech_lengths=slen, text=text, text_lengths=tlen)))
+
+    def build_iter(self, epoch, shuffle=None):
+        r = epoch % len(self.items)
+        # UtteranceMVN normalises the batch in place (utterance_mvn.py:66-69): fresh copies
+        return [(ids, dict(b, speech=b["speech"].clone(), text=b["text"].clone()))
+                for ids, b in self.items[r:] + self.items[:r]]
+
+
+def _trainer(dev, out, graph, max_epoch=None):
+    from espnet_slurp_amd.optimizers.fused_adam import FusedAdam
+    from espnet_slurp_amd.schedulers.warmup_lr import WarmupLR
+    from espnet_slurp_amd.train.trainer import Trainer, TrainerOptions
+    ref = json.load(open(os.path.join(GOLDEN, "trainrun_ref.json")))
+    cfg = small_cfg("latest")
+    model = build_model(cfg, dev)
+    load_seeded(model, cfg, ref["seed"])
+    a = ref["adam"]
+    opt = FusedAdam(model.parameters(), model.flat, lr=a["lr"], betas=tuple(a["betas"]), eps=a["eps"],
+                    weight_decay=a["weight_decay"])
+    sch = WarmupLR(opt, warmup_steps=ref["warmup_steps"])
+    o = dict(ref["opts"])
+    if max_epoch is not None:
+        o["max_epoch"] = max_epoch
+    opts = TrainerOptions(grad_clip=5.0, output_dir=str(out), **o)
+    return Trainer(model, opt, sch, opts, cuda_graph=graph), ref
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_trainer_run_matches_reference(dev, tmp_path, graph):
+    tr, ref = _trainer(dev, tmp_path, graph)
+    rep = tr.run(_Factory(TRAIN, dev), _Factory(VALID, dev))
+    for e, per in ref["values"].items():
+        for ph, vals in per.items():
+            for k, v in vals.items():
+                got = rep.get_value(ph, k, epoch=int(e))
+                tol = 1e-9 if k.startswith("optim") else (2e-3 if k == "acc" else 2e-4 * max(1.0, abs(v)))
+                assert abs(got - v) <= tol, (e, ph, k, got, v)
+    files = sorted(p.name for p in tmp_path.iterdir())
+    assert files == ref["files"], (files, ref["files"])
+    links = {p.name: str(p.readlink()) for p in tmp_path.iterdir() if p.is_symlink()}
+    assert links == ref["links"]
+    # the averaged model is the mean of the kept epoch files (integer buffers summed)
+    from espnet_slurp_amd.train.checkpoint import safe_load
+    ave = safe_load(tmp_path / "valid.loss.ave_2best.pth")
+    ep = [safe_load(tmp_path / f"{e}epoch.pth") for e in (2, 3)]
+    for k, v in ave.items():
+        exp = ep[0][k] + ep[1][k]
+        exp = exp if not torch.is_floating_point(exp) else exp / 2
+        assert torch.allclose(v, exp, rtol=0, atol=1e-6), k
+    assert tr.n_updates == 9 and tr.n_skipped == 0
+
+
+def test_trainer_run_resume(dev, tmp_path):
+    """Stop after 2 epochs, resume from checkpoint.pth in a fresh trainer for the 3rd
+    (trainer.py:196-210): the same reporter values and files as one 3-epoch run."""
+    tr, ref = _trainer(dev, tmp_path, False, max_epoch=2)
+    tr.run(_Factory(TRAIN, dev), _Factory(VALID, dev))
+    tr2, _ = _trainer(dev, tmp_path, False)
+    rep = tr2.run(_Factory(TRAIN, dev), _Factory(VALID, dev))
+    assert rep.get_epoch() == 3
+    for e, per in ref["values"].items():
+        for ph, vals in per.items():
+            for k, v in vals.items():
+                got = rep.get_value(ph, k, epoch=int(e))
+                tol = 1e-9 if k.startswith("optim") else (2e-3 if k == "acc" else 2e-4 * max(1.0, abs(v)))
+                assert abs(got - v) <= tol, (e, ph, k, got, v)
+    assert sorted(p.name for p in tmp_path.iterdir()) == ref["files"]
