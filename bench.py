@@ -79,15 +79,15 @@ def build(args, device):
     return model
 
 
-def synthetic_batch(B, V, rank, device, variable=False):
+def synthetic_batch(B, V, rank, device, variable=False, index=0):
     """SURVEY §8(d) synthetic inputs: N(0,1) fbank, lengths 1500 (or U[1000,1500] sorted
-    descending with variable=True), tokens U[2, V-2], label lengths U[20,40] padded -1."""
-    g = torch.Generator().manual_seed(1234 + rank)
-    speech = torch.randn(B, 1500, 80, generator=g).to(device)
+    descending with variable=True: each batch padded to its own longest utterance, as the
+    reference's collate does), tokens U[2, V-2], label lengths U[20,40] padded -1."""
+    g = torch.Generator().manual_seed(1234 + rank + 7919 * index)
     speech_lengths = torch.full((B,), 1500, dtype=torch.long)
     if variable:
         speech_lengths = torch.sort(torch.randint(1000, 1501, (B,), generator=g), descending=True)[0]
-        speech_lengths[0] = 1500  # the padded width stays T = 1500
+    speech = torch.randn(B, int(speech_lengths.max()), 80, generator=g).to(device)
     tl = torch.randint(20, 41, (B,), generator=g)
     text = torch.full((B, int(tl.max())), -1, dtype=torch.long)
     for i in range(B):
@@ -210,7 +210,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch kernel by kernel instead of replaying a HIP graph")
     ap.add_argument("--variable-lengths", action="store_true",
-                    help="speech lengths U[1000,1500] sorted descending (SURVEY 8(d) variable variant)")
+                    help="speech lengths U[1000,1500] sorted descending (SURVEY 8(d) variable variant): "
+                         "4 batches of different lengths in turn, on length-bucketed HIP graphs")
+    ap.add_argument("--graph-buckets", default="100,8",
+                    help="frames,tokens bucket multiples of TrainerOptions.graph_buckets (--variable-lengths)")
     ap.add_argument("--amp", action="store_true", help="bf16 GEMM operands, fp32 accumulate (TrainerOptions.use_amp)")
     ap.add_argument("--config", choices=sorted(PRESETS), default=None,
                     help="BASELINE.json config preset (overrides --d/--heads/--ff/--layers; c5 implies --amp)")
@@ -239,12 +242,15 @@ def main():
     model.train()
     opt = FusedAdam(model.parameters(), model.flat, lr=2e-4)
     sched = WarmupLR(opt, warmup_steps=25000)
-    trainer = Trainer(model, opt, sched, TrainerOptions(grad_clip=5.0, use_amp=args.amp), distributed=world > 1,
-                      cuda_graph=not args.eager)
-    batch = synthetic_batch(args.batch, args.vocab, rank, device, args.variable_lengths)
+    buckets = tuple(int(v) for v in args.graph_buckets.split(",")) if args.variable_lengths else None
+    trainer = Trainer(model, opt, sched, TrainerOptions(grad_clip=5.0, use_amp=args.amp, graph_buckets=buckets),
+                      distributed=world > 1, cuda_graph=not args.eager)
+    batches = [synthetic_batch(args.batch, args.vocab, rank, device, args.variable_lengths, i)
+               for i in range(4 if args.variable_lengths else 1)]
+    batch = batches[0]
 
-    for _ in range(args.warmup):
-        trainer.train_one_step(batch)
+    for i in range(args.warmup):
+        trainer.train_one_step(batches[i % len(batches)])
     torch.cuda.synchronize()
 
     if args.eager:
@@ -253,8 +259,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        stats = trainer.train_one_step(batch)
+    for i in range(args.steps):
+        stats = trainer.train_one_step(batches[i % len(batches)])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -311,6 +317,7 @@ def main():
             "dtype": "bf16-mfma/f32-accumulate" if args.amp else "f32",
             "data": "synthetic (N(0,1) fbank, random tokens U[20,40], random-init weights)",
             "launch": "eager" if args.eager else "hip_graph",
+            "graphs_captured": len(trainer._graphs) if not args.eager else 0,
             "last_step": {"loss": round(last_loss, 4), "grad_norm": round(last_gn, 4),
                           "skipped_steps": trainer.n_skipped},
             "config": {"workload": f"{workload_name(args)} d={args.d} H={args.heads} FF={args.ff} "
