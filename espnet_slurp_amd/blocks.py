@@ -573,7 +573,7 @@ class Conv2dSubsampling(nn.Module):
         K.permute3(dw2r, c2.weight.grad, D, 9, D, accumulate=True)  # (o, kk, c) -> (o, c, kk)
         dz1 = empty(B * T1 * F1 * D, like=dx)
         # 4 implicit parity-class GEMMs with the ReLU mask in the epilogue (no 9x column buffer,
-        # 4.2 GB at C2): opt-in, it measures 6.6 ms against 6.4 ms for column GEMM + col2im at C2
+        # 8.4 GB at C2 B=128): 10.2 ms against 12.4 ms for column GEMM + col2im (kernels.py)
         if K.CONV2_IMPLICIT_DGRAD and D % 32 == 0:
             K.conv2_dgrad(dz2p, c2.weight, c.z1, dz1, B, T1, F1, D)
         else:

@@ -168,6 +168,7 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
   int kind = g.splits > 1 ? EPI_PLAIN : epi_kind_spec(g);
   if (kind == EPI_SMB && !(MA == KC && MB == KC && g.bf16 == 0)) return false;
   if (((kind == EPI_BMUL || kind == EPI_RMASK) && !can_spec_bwd) || ((kind == EPI_P0 || kind == EPI_PR) && !can_pspec) ||
+      (kind == EPI_RMASKMAP && !(MA == I2CT_KC && MB == RC)) ||
       (kind == EPI_BRELU && !can_brelu) ||
       (kind >= EPI_BIAS && kind <= EPI_FFN_RELU && !can_spec_fwd))
     kind = epi_kind(g);
@@ -528,7 +529,12 @@ ESP_API int esp_conv2_dgrad(const float* dz2, const float* W, const float* z1, f
     g.bwd_act = ACT_RELU; g.pre = z1;
     g.key = esp::rng_key_ptr();
     g.wide = 1;
-    g.batch = 1; g.splits = 1; g.kchunk = g.K; g.bnt = 64;
+    static int dgrad_bnt = -1;  // ESP_CONV2_DGRAD_BNT=64|128 (measurements)
+    if (dgrad_bnt < 0) {
+      const char* e = getenv("ESP_CONV2_DGRAD_BNT");
+      dgrad_bnt = (e && atoi(e) == 64) ? 64 : 128;
+    }
+    g.batch = 1; g.splits = 1; g.kchunk = g.K; g.bnt = D % dgrad_bnt == 0 ? dgrad_bnt : 64;
     g.cmap = 1;
     g.cm_hw = t.t_hw; g.cm_w = t.t_w;
     g.cm_T1 = T1; g.cm_F1 = F1; g.cm_ph = ph; g.cm_pw = pw;

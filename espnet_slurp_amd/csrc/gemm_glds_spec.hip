@@ -2,7 +2,8 @@
 // of the production call sites: EPI_BIAS / EPI_BDR / EPI_FFN_SWISH / EPI_FFN_RELU for the linear
 // forward (KC x KC), EPI_BRELU (bias + ReLU) for the conv2 forward (implicit-im2col I2C_KC x KC)
 // and KC x KC, EPI_BMUL for the FFN input gradient and EPI_RMASK for the gradient through conv2's
-// ReLU (KC x RC).  See store_spec.
+// ReLU (KC x RC) and its row-mapped form for the implicit conv2 input gradient (I2CT_KC x RC).
+// See store_spec.
 #include "gemm_kernels.h"
 
 namespace espg {
@@ -29,6 +30,8 @@ bool glds_launch_spec(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hip
     } else if constexpr (MA == KC && MB == RC) {
       ESP_SPEC(EPI_BMUL)
       ESP_SPEC(EPI_RMASK)
+    } else if constexpr (MA == I2CT_KC && MB == RC) {
+      ESP_SPEC(EPI_RMASKMAP)
     }
 #undef ESP_SPEC
   });

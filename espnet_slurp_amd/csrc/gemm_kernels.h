@@ -129,16 +129,20 @@ __device__ __forceinline__ long row_off(const GemmArgs& g, int m) {
 //   EPI 2: backward  drop'(acc + bias) * act'(pre)  (dropout mask regenerated), alpha, R
 // cbase = offset of batch z in C/R/aux/pre, dbase = z*M*N (dropout index base).
 enum { EPI_PLAIN = 0, EPI_FWD = 1, EPI_BWD = 2, EPI_BIAS = 3, EPI_BDR = 4, EPI_FFN_SWISH = 5, EPI_FFN_RELU = 6,
-       EPI_BMUL = 7, EPI_P0 = 8, EPI_PR = 9, EPI_SMB = 10, EPI_BRELU = 11, EPI_RMASK = 12 };
+       EPI_BMUL = 7, EPI_P0 = 8, EPI_PR = 9, EPI_SMB = 10, EPI_BRELU = 11, EPI_RMASK = 12, EPI_RMASKMAP = 13 };
 __host__ __device__ inline int epi_kind(const GemmArgs& g) {
   return g.bwd_act ? EPI_BWD : ((g.bias || g.aux || g.act || g.drop_thresh) ? EPI_FWD : EPI_PLAIN);
 }
 // the specialised kind (store_spec) when the launch's features match one exactly, else the
-// generic kind; only for wide (float4) epilogues without the conv2 output row map
+// generic kind; only for wide (float4) epilogues (the conv2 output row map: EPI_RMASKMAP only)
 __host__ inline int epi_kind_spec(const GemmArgs& g) {
   if (g.smb_rel) return EPI_SMB;
   const int k = epi_kind(g);
-  if (g.cmap) return k;
+  if (g.cmap)
+    return (g.wide && k == EPI_BWD && g.bwd_act == ACT_RELU && !g.drop_thresh && !g.r && !g.bias && g.alpha == 1.0f &&
+            g.splits == 1)
+               ? EPI_RMASKMAP
+               : k;
   if (!g.wide) {
     if (g.ragged4 && k == EPI_PLAIN && g.splits == 1 && !g.rowsum) return g.r ? EPI_PR : EPI_P0;
     return k;
@@ -390,11 +394,12 @@ __device__ __forceinline__ void store_tiles_wide(const GemmArgs& g, int z, int m
 //   EPI_FFN_RELU   the same with ReLU                            (decoder FFN w_1)
 //   EPI_BMUL       acc * pre                                     (FFN w_2 input gradient, ACT_MUL)
 //   EPI_RMASK      pre > 0 ? acc : 0                             (input gradient through a ReLU output)
+//   EPI_RMASKMAP   EPI_RMASK through the conv2 output row map    (implicit conv2 input gradient classes)
 //   EPI_P0         alpha * acc                                   (plain, unsplit)
 //   EPI_PR         alpha * acc + beta * R                        (gradient accumulation)
 //   EPI_SMB        dS = P * (drop'(acc) - dot_row) * alpha -> C, and its rel_shift adjoint -> dbd
 //                  (attention.py:64-96 + 145-165 backward; P in pre, FlashAttention-2's row dot)
-// (wide stores, no output row map; chosen by epi_kind on the host).  A wave whose 32-row /
+// (wide stores, no output row map but EPI_RMASKMAP's; chosen by epi_kind on the host).  A wave whose 32-row /
 // 32-column sub-tiles are all in range takes a path without per-element bounds checks.
 template <int EPI>
 struct EpiSpec {
@@ -404,7 +409,8 @@ struct EpiSpec {
   static constexpr bool res = EPI == EPI_BDR || EPI == EPI_PR;
   static constexpr bool drop = EPI == EPI_BDR || EPI == EPI_FFN_SWISH || EPI == EPI_FFN_RELU;
   static constexpr bool aux = EPI == EPI_FFN_SWISH || EPI == EPI_FFN_RELU;  // derivative stream
-  static constexpr bool mul = EPI == EPI_BMUL || EPI == EPI_RMASK;
+  static constexpr bool mul = EPI == EPI_BMUL || EPI == EPI_RMASK || EPI == EPI_RMASKMAP;
+  static constexpr bool rmap = EPI == EPI_RMASKMAP;
 };
 template <int EPI, int TM, int TN, bool FULL>
 __device__ __forceinline__ void store_spec(const GemmArgs& g, int z, int mrow0, int ncol0, int lane,
@@ -463,20 +469,25 @@ __device__ __forceinline__ void store_spec(const GemmArgs& g, int z, int mrow0, 
         continue;
       }
       float4 x4[4];  // residual (BDR) or local derivative (BMUL)
+      long roff[4];  // row offsets (EPI_RMASKMAP: through the class -> pixel row map)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int m = mrow0 + i * 32 + 8 * q + 4 * h + (l32 & 3);
+        roff[q] = S::rmap ? row_off(g, min(m, g.M - 1)) : (long)m * g.ldc;
+      }
       if constexpr (S::res || S::mul) {
         const float* src = S::res ? g.r : g.pre;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int m = mrow0 + i * 32 + 8 * q + 4 * h + (l32 & 3);
-          x4[q] = (FULL || (nok && m < g.M)) ? *reinterpret_cast<const float4*>(src + cbase + (long)m * g.ldc + n)
-                                             : zero4;
+          x4[q] = (FULL || (nok && m < g.M)) ? *reinterpret_cast<const float4*>(src + cbase + roff[q] + n) : zero4;
         }
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int m = mrow0 + i * 32 + 8 * q + 4 * h + (l32 & 3);
         if (!FULL && (!nok || m >= g.M)) continue;
-        const long off = cbase + (long)m * g.ldc + n;
+        const long off = cbase + roff[q] + n;
         const float xs[4] = {x4[q].x, x4[q].y, x4[q].z, x4[q].w};
         const float bs[4] = {bn.x, bn.y, bn.z, bn.w};
         float v[4], d[4];
@@ -502,7 +513,7 @@ __device__ __forceinline__ void store_spec(const GemmArgs& g, int z, int mrow0, 
             w = kp[e] ? w * g.drop_scale : 0.f;
             dd = kp[e] ? dd * g.drop_scale : 0.f;
           }
-          if constexpr (EPI == EPI_RMASK) w = xs[e] > 0.f ? w : 0.f;
+          if constexpr (EPI == EPI_RMASK || EPI == EPI_RMASKMAP) w = xs[e] > 0.f ? w : 0.f;
           else if constexpr (S::mul) w *= xs[e];
           w *= g.alpha;
           if constexpr (S::res) w += g.beta * xs[e];

@@ -773,7 +773,11 @@ def global_mvn(x, lens_i32, mean, std, norm_means=True, norm_vars=True):
 
 
 _ZEROS = {}
-CONV2_IMPLICIT_DGRAD = os.environ.get("ESP_CONV2_IMPLICIT_DGRAD", "0") == "1"
+# conv2 input gradient as 4 implicit parity-class GEMMs with the ReLU mask in a specialised
+# row-mapped epilogue (EPI_RMASKMAP, 128-wide tiles): 10.2 ms vs 12.4 ms for the column GEMM +
+# col2im at C2 B=128 (tools/conv2_dgrad_bench.py), bench 1067 vs 1050 utt/s.  ESP_CONV2_IMPLICIT_DGRAD=0:
+# the column path.
+CONV2_IMPLICIT_DGRAD = os.environ.get("ESP_CONV2_IMPLICIT_DGRAD", "1") == "1"
 
 
 def conv2_dgrad(dz2, W, z1, dz1, B, T1, F1, D):
@@ -784,5 +788,16 @@ def conv2_dgrad(dz2, W, z1, dz1, B, T1, F1, D):
         _ZEROS[key] = torch.zeros(64, dtype=torch.float32, device=dz2.device)
     n = _wsize("esp_conv2_dgrad", D)
     wc = _ws(_WS2, "esp_conv2_dgrad", n, dz2.device)
+    if _PROF is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
     _native.call("esp_conv2_dgrad", _p(dz2), _p(W), _p(z1), _p(dz1), B, T1, F1, D, _p(_ZEROS[key]), _p(wc), n, _st())
     _guard_post("esp_conv2_dgrad", wc, n)
+    if _PROF is not None:  # the 4 class GEMMs as one family entry: A = dz2 (gathered), B = W, C = dz1 + ReLU mask read
+        ev1.record()
+        T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
+        npix2 = B * T2 * F2
+        # algorithmic bytes (the whole entry): dz2 and W read, z1 (ReLU mask) read, dz1 written
+        _PROF.append((2.0 * npix2 * 9 * D * D, ev0, ev1, (4, RC, B * T1 * F1, D, 9 * D, 1, "conv2_dgrad"),
+                      4.0 * (npix2 * D + 9 * D * D + 2 * B * T1 * F1 * D)))
