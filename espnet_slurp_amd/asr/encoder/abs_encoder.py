@@ -114,6 +114,5 @@ class EncoderFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dhs):
         ctx.enc.run_backward(ctx.saved, dhs.contiguous(), ctx.grad_hook)
-        K.join_side(dhs.device)  # weight gradients on the side stream are complete after this
         ctx.saved = None
         return None, None, None, None, None, None, None, None

@@ -65,7 +65,6 @@ class HeadsFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_loss, g_others):
         dhs = ctx.model._heads_backward(ctx.state, g_loss.contiguous())
-        K.join_side(dhs.device)
         ctx.state = None
         return dhs, None, None, None, None
 
@@ -335,9 +334,7 @@ class ESPnetASRModel(AbsESPnetModel):
         encoder (HeadsFn.backward + EncoderFn.backward), `hook(module)` at each module done."""
         saved, state = ctx
         dhs = self._heads_backward(state, g_loss, hook)
-        K.join_side(dhs.device)
         self.encoder.run_backward(saved, dhs.contiguous(), hook)
-        K.join_side(dhs.device)
 
     def _error_rates(self, encoder_out, prep) -> Dict[str, Optional[torch.Tensor]]:
         """Eval-mode error rates (espnet_model.py:515-521, 536-539): greedy CTC and decoder

@@ -560,7 +560,6 @@ class Conv2dSubsampling(nn.Module):
         dwor = torch.zeros(D * F2 * D, dtype=torch.float32, device=dx.device)
         z2f = c.z2.view(B * T2, F2 * D)
         K.linear_bwd_weight(dv, z2f, dwor.view(D, F2 * D), lin.bias.grad)
-        K.join_side(dx.device)  # dwor is produced on the weight-gradient stream
         K.permute3(dwor, lin.weight.grad, D, F2, D, accumulate=True)  # (n, f, c) -> (n, c, f)
         dz2 = empty(B * T2, F2 * D, like=dx)
         K.linear_bwd_data_act(dv, c.wor.view(D, F2 * D), dz2, z2f, K.ACT_RELU)  # ReLU' from its output

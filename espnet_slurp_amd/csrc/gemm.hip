@@ -160,6 +160,8 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
   // implicit-im2col A: every slab lies inside one tap (kt, kf), so the LDS-DMA source offset is
   // one scalar per slab; other channel counts take the register-staged kernel
   if (MA == I2C_KC && (g.a.ic.C % GL_BK || g.K % GL_BK)) return false;
+  // StageS: the pixel offsets of a 128-pixel run (<= 2 maps) as 32-bit byte offsets
+  if (MA == I2C_KC && 8L * g.a.ic.H * g.a.ic.W * g.a.ic.C >= (1L << 32)) return false;
   // implicit-im2col B: pixel offsets on 24-bit multiplies (i2c_pix_off24)
   if (MB == I2C_RC) {
     const long rows = (long)g.K / ((long)g.b.ic.Ho * g.b.ic.Wo) * g.b.ic.H * g.b.ic.W;  // Bn * H * W
@@ -196,6 +198,11 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
   const bool rs = can_rs && g.rowsum;
   if (rs) kind = EPI_PLAIN;
   const dim3 grid((unsigned)std::min<long>(x.ntiles, persist_blocks(glds_occupancy_rt(BNT, kind))));
+  x.fd_grid = make_fastdiv(grid.x);
+  x.fd_ntx = make_fastdiv((uint32_t)x.ntx);
+  x.fd_nty = make_fastdiv((uint32_t)x.nty);
+  x.fd_splits = make_fastdiv((uint32_t)g.splits);
+  x.fd_nb2 = make_fastdiv((uint32_t)g.nb2);
   const int prec = g.bf16;
   if (kind == EPI_PLAIN) return glds_launch_plain(MA, MB, BNT, prec, rs, grid, st, g, x);
   if (kind == EPI_FWD || kind == EPI_BWD) return glds_launch_epi(MA, MB, BNT, prec, kind, grid, st, g, x);
@@ -249,6 +256,8 @@ bool glds_ok(int mode, const void* p, long ld, long s1, long s2, int rows, int K
   if (mode >= 2) return true;  // im2col: C % 4 == 0 checked by the caller
   const long cont = mode == 0 ? K : rows, lines = mode == 0 ? rows : K;
   if (lines == 1) return cont % 4 == 0;
+  // StageS per-lane byte offsets are 32-bit: 128 rows (KC) / 32 k-rows (RC) of pitch ld
+  if (ld > (mode == 0 ? 8000000L : 32000000L)) return false;
   return ld % 4 == 0 && ld >= cont;
 }
 

@@ -412,7 +412,7 @@ struct EpiSpec {
   static constexpr bool mul = EPI == EPI_BMUL || EPI == EPI_RMASK || EPI == EPI_RMASKMAP;
   static constexpr bool rmap = EPI == EPI_RMASKMAP;
 };
-template <int EPI, int TM, int TN, bool FULL>
+template <int EPI, int TM, int TN, bool FULL, bool A1 = false>  // A1: alpha == 1 (no scaling multiply)
 __device__ __forceinline__ void store_spec(const GemmArgs& g, int z, int mrow0, int ncol0, int lane,
                                            f32x16 (&acc)[TM][TN]) {
   using S = EpiSpec<EPI>;
@@ -499,7 +499,7 @@ __device__ __forceinline__ void store_spec(const GemmArgs& g, int z, int mrow0, 
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          float w = acc[i][j][4 * q + e] + bs[e];
+          float w = S::bias ? acc[i][j][4 * q + e] + bs[e] : acc[i][j][4 * q + e];  // (x + 0.f is not foldable)
           float dd = 1.f;
           if constexpr (S::act == ACT_RELU) {
             dd = w > 0.f ? 1.f : 0.f;
@@ -515,7 +515,7 @@ __device__ __forceinline__ void store_spec(const GemmArgs& g, int z, int mrow0, 
           }
           if constexpr (EPI == EPI_RMASK || EPI == EPI_RMASKMAP) w = xs[e] > 0.f ? w : 0.f;
           else if constexpr (S::mul) w *= xs[e];
-          w *= g.alpha;
+          if constexpr (!A1) w *= g.alpha;
           if constexpr (S::res) w += g.beta * xs[e];
           v[e] = w;
           d[e] = dd;
@@ -532,11 +532,43 @@ __device__ __forceinline__ void store_spec(const GemmArgs& g, int z, int mrow0, 
     }
   }
 }
+// Column stores straight from the accumulator layout (lane = one column, 16 rows per 32x32 tile),
+// no transpose: every store is global_store_dword with a wave-uniform row base (SGPR pair) and a
+// per-lane 32-bit column offset, so the epilogue of a full tile issues no VALU besides the
+// optional alpha scale (the float4 path pays 4 DPP/select VALU per element, and f32 MFMAs do not
+// hide VALU).  Rows m = mrow0 + 32i + 8g + 4h + jj; the 4h term is in the lane offset, columns
+// 32j in the instruction offset.  Needs 4 * (4 * ldc + 64) < 2^32 (host: ldc < 2^27).
+template <int OFF>
+__device__ __forceinline__ void st_col(const float* rowbase, uint32_t voff, float v) {
+  asm volatile("global_store_dword %0, %1, %2 offset:%3" ::"v"(voff), "v"(v), "s"(rowbase), "n"(OFF) : "memory");
+}
+template <int TM, int TN, bool A1>
+__device__ __forceinline__ void store_cols(float* cz, long ldc, int mrow0, int ncol0, int lane, float alpha,
+                                           const f32x16 (&acc)[TM][TN]) {
+  static_assert(TN == 2, "column offsets 0 / 128 B");
+  const int h = lane >> 5, l32 = lane & 31;
+  const uint32_t voff = (uint32_t)((4 * h * ldc + l32) * 4);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float* rb = cz + (long)(mrow0 + i * 32 + 8 * (r >> 2) + (r & 3)) * ldc + ncol0;
+      st_col<0>(rb, voff, A1 ? acc[i][0][r] : alpha * acc[i][0][r]);
+      st_col<128>(rb, voff, A1 ? acc[i][1][r] : alpha * acc[i][1][r]);
+    }
+}
+
 template <int EPI, int TM, int TN>
 __device__ __forceinline__ void store_spec_tiles(const GemmArgs& g, int z, int mrow0, int ncol0, int lane,
                                                  f32x16 (&acc)[TM][TN]) {
-  if (mrow0 + TM * 32 <= g.M && ncol0 + TN * 32 <= g.N) store_spec<EPI, TM, TN, true>(g, z, mrow0, ncol0, lane, acc);
-  else store_spec<EPI, TM, TN, false>(g, z, mrow0, ncol0, lane, acc);
+  const bool full = mrow0 + TM * 32 <= g.M && ncol0 + TN * 32 <= g.N;
+  if (EPI != EPI_SMB && g.alpha == 1.0f) {
+    if (full) store_spec<EPI, TM, TN, true, true>(g, z, mrow0, ncol0, lane, acc);
+    else store_spec<EPI, TM, TN, false, true>(g, z, mrow0, ncol0, lane, acc);
+  } else {
+    if (full) store_spec<EPI, TM, TN, true>(g, z, mrow0, ncol0, lane, acc);
+    else store_spec<EPI, TM, TN, false>(g, z, mrow0, ncol0, lane, acc);
+  }
 }
 template <int TM, int TN>
 __device__ __forceinline__ void store_partials_wide(const GemmArgs& g, float* W, int mrow0, int ncol0, int lane,
@@ -1030,6 +1062,10 @@ struct GldsArgs {
   FastDiv hw_a, wo_a;  // I2C_KC
   int ntx, nty;        // tile grid (N tiles, M tiles)
   int ntiles;          // ntx * nty * batch * splits
+  // the tile-coordinate divisors as multiply-high reciprocals (set by the host launcher): on
+  // wave-uniform operands they compile to s_mul_hi_u32, where an integer division took ~30
+  // instructions incl. VALU reciprocals per tile
+  FastDiv fd_grid, fd_ntx, fd_nty, fd_splits, fd_nb2;
   // I2CT_KC (conv2 input gradient as an implicit GEMM per parity class): A(r, k) =
   // dY[b, a - dt[t], e - df[t], o] (0 outside the T2 x F2 grid), r = (b, a, e) over Ha x We,
   // k = t*C + o (tap t of the class, channel o); C % 32 == 0 so a slab never straddles taps
@@ -1165,6 +1201,90 @@ struct Stage {
   }
 };
 
+// One global_load_lds_dwordx4 in the scalar-base form: address = sbase (wave-uniform, SGPR pair)
+// + voff (per-lane unsigned 32-bit byte offset).  The slab advance is scalar arithmetic on sbase,
+// so a slab's DMAs cost no VALU (the 64-bit per-lane form paid ~6 VALU per DMA, and f32 MFMAs do
+// not hide VALU: DESIGN §3.5).
+// lds_wave_base: LDS byte address (wave-uniform) of the wave's 1 KB destination.
+__device__ __forceinline__ void lds_dma16_s(const float* sbase, uint32_t voff, uint32_t lds_wave_base) {
+  asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds_wave_base)
+               : "memory", "m0");
+}
+__device__ __forceinline__ uint32_t lds_addr(const float* p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const float*)p);
+}
+
+// Per-lane source bookkeeping with a wave-uniform tile base (KC, RC, I2C_KC operands).  The
+// per-lane part is a 32-bit byte offset inside the tile's panel: KC rows r < 128 of pitch ld
+// (host: 127 * ld * 4 + 128 < 2^32), RC k-rows < 32 (32 * ld * 4 < 2^32), I2C_KC pixel offsets
+// relative to the tile's first pixel (a 128-pixel run spans <= 2 maps; host: 2 maps < 2^32 B).
+//   KC     sbase(k0) = base + (k0 - kb)               base = A_z + row0 * ld + kb
+//   RC     sbase(k0) = base + (k0 - kb) * ld          base = A_z + kb * ld
+//   I2C_KC sbase(k0) = base + tap_off(k0)             base = A_z + pix_off(row0)
+// Lanes past the last row read a clamped row (their products only reach discarded outputs).  Only
+// a slab that reaches past K clamps k per lane (KC: to the last whole quad, RC: to K - 1).
+template <int MODE, int ROWS, int NI>
+struct StageS {
+  static constexpr bool kKC = MODE == KC || MODE == I2C_KC;
+  const float* base;
+  long ld;
+  int kb;
+  uint32_t off[NI];
+  int q[NI];  // KC: k offset inside the slab (4 * quad); RC: k-row inside the slab
+  __device__ __forceinline__ void init(const Operand& op, const float* zbase, int rows, int K, int row0, int kbeg,
+                                       const FastDiv& fhw, const FastDiv& fwo, int wave, int lane) {
+    ld = op.ld;
+    kb = kbeg;
+    long pix0 = 0;
+    if constexpr (MODE == KC) base = zbase + (long)row0 * op.ld + kbeg;
+    else if constexpr (MODE == RC) base = zbase + (long)kbeg * op.ld;
+    else {
+      pix0 = i2c_pix_off(op.ic, fhw, fwo, row0);
+      base = zbase + pix0;
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int slot = (i * 4 + wave) * 64 + lane;
+      if constexpr (kKC) {
+        const int r = slot >> 3, qq = (slot & 7) ^ kc_swz(r);
+        const int gr = min(row0 + r, rows - 1);
+        q[i] = 4 * qq;
+        if constexpr (MODE == KC) off[i] = (uint32_t)(((uint32_t)(gr - row0) * (uint32_t)op.ld + 4 * qq) * 4u);
+        else off[i] = (uint32_t)((i2c_pix_off(op.ic, fhw, fwo, gr) - pix0 + 4 * qq) * 4);
+      } else {
+        constexpr int QPR = ROWS / 4;  // quads per k-row
+        const int kr = slot / QPR, rs = slot % QPR;
+        const int rq = rs ^ (((kr >> 4) & 1) << 3);
+        const int gr = min(row0 + 4 * rq, (rows - 1) & ~3);
+        q[i] = kr;
+        off[i] = (uint32_t)(((uint32_t)kr * (uint32_t)op.ld + (uint32_t)gr) * 4u);
+      }
+    }
+  }
+  // this lane's NI LDS-DMA loads of the slab starting at k0 into LDS byte address `dst`
+  __device__ __forceinline__ void issue(const Operand& op, int K, int k0, uint32_t dst, int wave) const {
+    const float* sb;
+    if constexpr (MODE == KC) sb = base + (k0 - kb);
+    else if constexpr (MODE == RC) sb = base + (long)(k0 - kb) * ld;
+    else {  // the slab's tap and channel offset (C % 32 == 0, K % 32 == 0: host-checked)
+      const int t = k0 / op.ic.C, kt = t / 3, kf = t - 3 * kt;
+      sb = base + ((long)kt * op.ic.W + kf) * op.ic.C + (k0 - t * op.ic.C);
+    }
+    if (MODE == I2C_KC || k0 + GL_BK <= K) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) lds_dma16_s(sb, off[i], dst + (i * 4 + wave) * 1024);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        uint32_t o = off[i];
+        if constexpr (MODE == KC) o -= 4u * (uint32_t)max(0, q[i] - (((K - 1) & ~3) - k0));
+        else o -= 4u * (uint32_t)ld * (uint32_t)max(0, q[i] - (K - 1 - k0));
+        lds_dma16_s(sb, o, dst + (i * 4 + wave) * 1024);
+      }
+    }
+  }
+};
+
 // zero k >= kv of a staged slab (last slab of a K range that is not a multiple of 32)
 template <int MODE, int ROWS>
 __device__ __forceinline__ void zero_tail(float* slab, int kv) {
@@ -1214,17 +1334,17 @@ struct TileCoord {
 };
 template <int BNT>
 __device__ __forceinline__ TileCoord tile_coord(const GemmArgs& g, const GldsArgs& x, int t, int G) {
-  const int round = t / G, b = t - round * G;
+  const int round = (int)fdiv((uint32_t)t, x.fd_grid), b = t - round * G;
   const int nr = min(G, x.ntiles - round * G);
   const int xcd = b & 7, per = nr >> 3, rem = nr & 7;
   const int wg = round * G + (xcd < rem ? xcd * (per + 1) : rem * (per + 1) + (xcd - rem) * per) + (b >> 3);
   TileCoord c;
-  c.tn = wg % x.ntx;
-  const int t2 = wg / x.ntx;
-  const int tm = t2 % x.nty;
-  const int zz = t2 / x.nty;
-  c.split = zz % g.splits;
-  c.z = zz / g.splits;
+  const int t2 = (int)fdiv((uint32_t)wg, x.fd_ntx);
+  c.tn = wg - t2 * x.ntx;
+  const int zz = (int)fdiv((uint32_t)t2, x.fd_nty);
+  const int tm = t2 - zz * x.nty;
+  c.z = (int)fdiv((uint32_t)zz, x.fd_splits);
+  c.split = zz - c.z * g.splits;
   c.kbeg = c.split * g.kchunk;
   c.kend = min(g.K, c.kbeg + g.kchunk);
   c.nk = (c.kend - c.kbeg + GL_BK - 1) / GL_BK;  // >= 1: the host routes K == 0 elsewhere
@@ -1271,21 +1391,39 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_ke
   const int h = lane >> 5, l32 = lane & 31;
 
   auto a_base = [&](const TileCoord& c) {
-    const int z1 = c.z / g.nb2, z2 = c.z - z1 * g.nb2;
+    const int z1 = (int)fdiv((uint32_t)c.z, x.fd_nb2), z2 = c.z - z1 * g.nb2;
     return g.a.p + z1 * g.a.s1 + z2 * g.a.s2;
   };
   auto b_base = [&](const TileCoord& c) {
-    const int z1 = c.z / g.nb2, z2 = c.z - z1 * g.nb2;
+    const int z1 = (int)fdiv((uint32_t)c.z, x.fd_nb2), z2 = c.z - z1 * g.nb2;
     return g.b.p + z1 * g.b.s1 + z2 * g.b.s2;
   };
 
+  // scalar-base staging (StageS) for KC / RC / implicit-im2col A; the gathered operands keep
+  // per-lane 64-bit addresses (Stage)
+  constexpr bool SA_S = MA == KC || MA == RC || MA == I2C_KC, SB_S = MB == KC || MB == RC;
+  using SAt = std::conditional_t<SA_S, StageS<MA, BM, NIA>, Stage<MA, BM, NIA>>;
+  using SBt = std::conditional_t<SB_S, StageS<MB, BNT, NIB>, Stage<MB, BNT, NIB>>;
+  SAt sa;
+  SBt sb;
+  auto init_ab = [&](const TileCoord& cc) {
+    if constexpr (SA_S) sa.init(g.a, a_base(cc), g.M, g.K, cc.m0, cc.kbeg, x.hw_a, x.wo_a, wave, lane);
+    else sa.init(g.a, a_base(cc), g.M, g.K, cc.m0, x.c_a, x.hw_a, x.wo_a, wave, lane, MA == I2CT_KC ? &x : nullptr);
+    if constexpr (SB_S) sb.init(g.b, b_base(cc), g.N, g.K, cc.n0, cc.kbeg, x.hw_b, x.wo_b, wave, lane);
+    else sb.init(g.b, b_base(cc), g.N, g.K, cc.n0, x.c_b, x.hw_b, x.wo_b, wave, lane);
+  };
+  const uint32_t smem_lds = lds_addr(smem);
+  auto issue_ab = [&](int k0, float* dst) {
+    const uint32_t dl = smem_lds + (uint32_t)(dst - smem) * 4u;
+    if constexpr (SA_S) sa.issue(g.a, g.K, k0, dl, wave);
+    else sa.issue(g.a, g.K, k0, dst, wave, x.c_a, x.hw_a, x.wo_a, MA == I2CT_KC ? &x : nullptr);
+    if constexpr (SB_S) sb.issue(g.b, g.K, k0, dl + 4u * A_SZ, wave);
+    else sb.issue(g.b, g.K, k0, dst + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
+  };
+
   TileCoord c = tile_coord<BNT>(g, x, t, G);
-  Stage<MA, BM, NIA> sa;
-  Stage<MB, BNT, NIB> sb;
-  sa.init(g.a, a_base(c), g.M, g.K, c.m0, x.c_a, x.hw_a, x.wo_a, wave, lane, MA == I2CT_KC ? &x : nullptr);
-  sb.init(g.b, b_base(c), g.N, g.K, c.n0, x.c_b, x.hw_b, x.wo_b, wave, lane);
-  sa.issue(g.a, g.K, c.kbeg, smem, wave, x.c_a, x.hw_a, x.wo_a, MA == I2CT_KC ? &x : nullptr);
-  sb.issue(g.b, g.K, c.kbeg, smem + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
+  init_ab(c);
+  issue_ab(c.kbeg, smem);
   wait_vm0();
   raw_barrier();
   int buf = 0;
@@ -1381,10 +1519,7 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_ke
     for (int kt = 0; kt + 1 < c.nk; ++kt) {  // all but the last slab: slab kt+1 streams in
       const int k1 = c.kbeg + (kt + 1) * GL_BK;
       float* nxt = smem + (buf ^ 1) * BUF;  // last read before the previous barrier
-      if (!(x.abl & 1)) {
-        sa.issue(g.a, g.K, k1, nxt, wave, x.c_a, x.hw_a, x.wo_a, MA == I2CT_KC ? &x : nullptr);
-        sb.issue(g.b, g.K, k1, nxt + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
-      }
+      if (!(x.abl & 1)) issue_ab(k1, nxt);
       compute(smem + buf * BUF);
       finish_slab();
     }
@@ -1393,10 +1528,8 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_ke
       float* nxt = smem + (buf ^ 1) * BUF;
       if (has_next) {
         cn = tile_coord<BNT>(g, x, tnext, G);
-        sa.init(g.a, a_base(cn), g.M, g.K, cn.m0, x.c_a, x.hw_a, x.wo_a, wave, lane, MA == I2CT_KC ? &x : nullptr);
-        sb.init(g.b, b_base(cn), g.N, g.K, cn.n0, x.c_b, x.hw_b, x.wo_b, wave, lane);
-        sa.issue(g.a, g.K, cn.kbeg, nxt, wave, x.c_a, x.hw_a, x.wo_a, MA == I2CT_KC ? &x : nullptr);
-        sb.issue(g.b, g.K, cn.kbeg, nxt + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
+        init_ab(cn);
+        issue_ab(cn.kbeg, nxt);
       }
       const int kv = c.kend - (c.kbeg + (c.nk - 1) * GL_BK);
       if (kv < GL_BK) {
@@ -1423,9 +1556,18 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_ke
     if (!(x.abl & 2)) {
       float* W = g.splits > 1 ? g.work + ((long)c.split * g.batch + c.z) * (long)g.M * g.N : nullptr;
       if constexpr (EPI >= EPI_BIAS) {  // specialised kinds: never split-K, always wide
-        store_spec_tiles<EPI, TM, TN>(g, c.z, c.m0 + wm * TM * 32, c.n0 + wn * 64, lane, acc);
+        const int mr0 = c.m0 + wm * TM * 32, nc0 = c.n0 + wn * 64;
+        if (EPI == EPI_P0 && (x.abl & 64) && mr0 + TM * 32 <= g.M && nc0 + TN * 32 <= g.N) {
+          float* cz = g.c + c_base(g, c.z);
+          if (g.alpha == 1.0f) store_cols<TM, TN, true>(cz, g.ldc, mr0, nc0, lane, 1.0f, acc);
+          else store_cols<TM, TN, false>(cz, g.ldc, mr0, nc0, lane, g.alpha, acc);
+        } else {
+          store_spec_tiles<EPI, TM, TN>(g, c.z, mr0, nc0, lane, acc);
+        }
       } else if (g.wide) {
-        if (W) store_partials_wide<TM, TN>(g, W, c.m0 + wm * TM * 32, c.n0 + wn * 64, lane, acc);
+        if (W && (x.abl & 64) && c.m0 + wm * TM * 32 + TM * 32 <= g.M && c.n0 + wn * 64 + TN * 32 <= g.N)
+          store_cols<TM, TN, true>(W, g.N, c.m0 + wm * TM * 32, c.n0 + wn * 64, lane, 1.0f, acc);
+        else if (W) store_partials_wide<TM, TN>(g, W, c.m0 + wm * TM * 32, c.n0 + wn * 64, lane, acc);
         else store_tiles_wide<EPI, TM, TN>(g, c.z, c.m0 + wm * TM * 32, c.n0 + wn * 64, lane, acc, (x.abl & 32) != 0);
       } else {
         if (W) store_partials<TM, TN>(g, W, c.m0 + wm * TM * 32, c.n0 + wn * 64, h, l32, acc);

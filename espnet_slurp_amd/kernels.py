@@ -264,46 +264,10 @@ def linear_bwd_data_act(dy, W, dx, pre, act, drop_p=0.0, seed=0):
     return dx
 
 
-# Opt-in (ESP_WGRAD_STREAM=1): weight gradients on a side stream, concurrently with the input-gradient GEMMs of the same
-# backward (they are independent: both only read dy): the two launch streams fill each other's
-# ramp-up / tail / split-K phases.  Forked with side.wait_stream(main), joined (main waits on
-# side) before anything reads the flat gradient (join_side: end of each explicit backward, the
-# DDP bucket launches, the clip norm).  Inputs stay referenced until the join, so the caching
-# allocator cannot hand their memory to the main stream while the side stream reads it.
-# HIP-graph capture records the fork / join as graph dependencies.
-WGRAD_STREAM = os.environ.get("ESP_WGRAD_STREAM", "0") == "1"  # measured: 810 vs 845 utt/s at C2 (graph)
-_SIDE = {}
-_SIDE_REFS = {}
-
-
-def _side_stream(device):
-    key = str(device)
-    if key not in _SIDE:
-        _SIDE[key] = torch.cuda.Stream(device=device)
-        _SIDE_REFS[key] = []
-    return _SIDE[key], _SIDE_REFS[key]
-
-
-def join_side(device=None):
-    """Make the current stream wait for the weight-gradient side stream (no-op when idle)."""
-    for key, refs in _SIDE_REFS.items():
-        if refs and (device is None or key == str(torch.device(device))):
-            torch.cuda.current_stream(torch.device(key)).wait_stream(_SIDE[key])
-            refs.clear()
-
-
 def linear_bwd_weight(dy, x, dW, db=None):
     """dW += dy^T x ; db += colsum(dy) (fused into the same GEMM pass over dy)."""
     M, N = dy.shape
     K = x.shape[1]
-    if WGRAD_STREAM and dy.is_cuda:
-        side, refs = _side_stream(dy.device)
-        side.wait_stream(torch.cuda.current_stream(dy.device))
-        refs.extend((dy, x))
-        with torch.cuda.stream(side):
-            gemm(N, K, M, dy, x, dW, mode_a=RC, lda=dy.stride(0), mode_b=RC, ldb=x.stride(0), ldc=dW.stride(0),
-                 R=dW, beta=1.0, rowsum=db)
-        return
     gemm(N, K, M, dy, x, dW, mode_a=RC, lda=dy.stride(0), mode_b=RC, ldb=x.stride(0), ldc=dW.stride(0),
          R=dW, beta=1.0, rowsum=db)
 

@@ -16,8 +16,6 @@ def clip_grad_norm_(flat: FlatParams, max_norm: float, out: torch.Tensor = None)
     coefficient is applied inside the Adam kernel."""
     if out is None:
         out = torch.empty(3, dtype=torch.float32, device=flat.grad.device)
-    if flat.grad.is_cuda:
-        K.join_side(flat.grad.device)
     K.grad_norm(flat.grad, max_norm, out)
     return out
 

@@ -70,8 +70,6 @@ class FlatGradReducer:
         while self.next_launch < len(self.buckets) and self.ready[self.next_launch] == self.bucket_count[self.next_launch]:
             s, e = self.buckets[self.next_launch]
             t = self.flat.grad[s:e]
-            if t.is_cuda:
-                K.join_side(t.device)  # the bucket's weight gradients may still be on the side stream
             op = dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM
             self.handles[self.next_launch] = dist.all_reduce(t, op=op, group=self.group, async_op=True)
             self.next_launch += 1
@@ -103,8 +101,6 @@ class FlatGradReducer:
     def allreduce_sum(self):
         """SUM all-reduce of the whole flat gradient in the same buckets (HIP-graph mode: the
         caller pre-scaled each replica's gradient by w_r / sum w)."""
-        if self.flat.grad.is_cuda:
-            K.join_side(self.flat.grad.device)
         hs = [dist.all_reduce(self.flat.grad[s:e], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
               for s, e in self.buckets]
         for h in hs:
@@ -113,8 +109,6 @@ class FlatGradReducer:
     def launch_sum(self, bucket_ids):
         """Asynchronous SUM all-reduces of the given buckets (the HIP-graph path, whose replicas
         pre-scaled their gradients by w_r / sum w); returns the work handles."""
-        if self.flat.grad.is_cuda:
-            K.join_side(self.flat.grad.device)
         return [dist.all_reduce(self.flat.grad[self.buckets[b][0]:self.buckets[b][1]], op=dist.ReduceOp.SUM,
                                 group=self.group, async_op=True) for b in bucket_ids]
 

@@ -292,7 +292,6 @@ class Trainer:
                     # trailing segment (ending it here would capture an empty graph)
                     final.extend(ids)
                     return
-                K.join_side(dev)
                 cur[0].capture_end()
                 segs.append((cur[0], list(ids)))
                 cur[0] = torch.cuda.CUDAGraph()
@@ -307,7 +306,6 @@ class Trainer:
                 cur[0].capture_begin(pool=pool, capture_error_mode="thread_local")
                 model.backward_explicit(ctx, self._scale, hook)
                 del ctx
-                K.join_side(dev)
                 cur[0].capture_end()
                 segs.append((cur[0], final + hook.rest()))
             torch.cuda.current_stream(dev).wait_stream(cap)

@@ -137,23 +137,6 @@ def test_eager_distributed_world1_rccl(dev):
         dist.destroy_process_group()
 
 
-def test_graph_and_eager_with_weight_gradient_stream(dev, monkeypatch):
-    """ESP_WGRAD_STREAM: weight gradients forked to a side stream (joined before any reader)
-    give the same steps as the single-stream path, eager and captured."""
-    from espnet_slurp_amd import kernels as K
-    ref = []
-    for side in (False, True):
-        monkeypatch.setattr(K, "WGRAD_STREAM", side)
-        for graph in (False, True):
-            t, m, _, _ = _trainer(dev, graph)
-            losses = [t.train_one_step(_batch(dev))["loss"].item() for _ in range(3)]
-            t.resolve_pending()
-            ref.append((losses, m.flat.flat.clone()))
-    for losses, flat in ref[1:]:
-        assert all(abs(a - b) <= 1e-6 * max(1.0, abs(a)) for a, b in zip(ref[0][0], losses))
-        assert torch.allclose(ref[0][1], flat, rtol=0, atol=1e-6)
-
-
 def _batches_same_shapes(dev):
     """Two batches with identical padded shapes but different lengths / target counts."""
     out = []
