@@ -28,6 +28,7 @@ SIGNATURES = {
                      P, P, P, L, P],
     "esp_set_gemm_compute": [I],
     "esp_get_gemm_compute": [],
+    "esp_set_splitk_mode": [I],
     "esp_act_bwd": [P, P, P, L, I, F, U64, L, P],
     "esp_scale_dropout": [P, P, L, F, F, U64, P, F, P],
     "esp_scale_by_dev": [P, L, P, P],
@@ -96,9 +97,9 @@ SIGNATURES = {
     "esp_relpos_dp_workspace_bytes": [I, I, I],
 }
 _RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I, "esp_set_gemm_compute": I,
-             "esp_get_gemm_compute": I}
+             "esp_get_gemm_compute": I, "esp_set_splitk_mode": I}
 _RESTYPES.update({k: L for k in SIGNATURES if k.endswith("_workspace_bytes")})
-ABI_VERSION = 20  # bumped whenever a signature in include/espnet_mi355.h changes
+ABI_VERSION = 21  # bumped whenever a signature in include/espnet_mi355.h changes
 
 _lib = None
 

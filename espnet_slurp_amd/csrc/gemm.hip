@@ -10,18 +10,6 @@ using namespace espg;
 
 namespace {
 
-// split-K reduction in fixed split order + the fused epilogue (4 outputs per thread when
-// N % 4 == 0: float4 partial loads)
-__device__ __forceinline__ void reduce_store(const GemmArgs& g, int z, int m, int n, float acc) {
-  const long cb = c_base(g, z);
-  const uint64_t db = (uint64_t)z * (uint64_t)g.M * (uint64_t)g.N;
-  switch (epi_kind(g)) {
-    case EPI_BWD: epi_store<EPI_BWD>(g, cb, db, m, n, acc); break;
-    case EPI_FWD: epi_store<EPI_FWD>(g, cb, db, m, n, acc); break;
-    default: epi_store<EPI_PLAIN>(g, cb, db, m, n, acc);
-  }
-}
-
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 // Split-K reduction + the fused epilogue.  Block = 64 float4 slots x 4 split groups: thread
@@ -135,6 +123,14 @@ long persist_blocks(int per_cu) {
 
 int g_compute = 0;  // 0: fp32 MFMA (exact f32 fma chain), 1: bf16-input MFMA with fp32 accumulate
 
+// split-K combine: 0 the reduction launch (default), 1 in-kernel (last-arriving unit per tile);
+// esp_set_splitk_mode, initialised from ESP_SPLITK_INKERNEL
+int g_splitk = -1;
+int splitk_mode() {
+  if (g_splitk < 0) g_splitk = (getenv("ESP_SPLITK_INKERNEL") && atoi(getenv("ESP_SPLITK_INKERNEL")) == 1) ? 1 : 0;
+  return g_splitk;
+}
+
 // ESP_GEMM_VARIANT != 4 forces the register-staged fallback kernel (diagnostics)
 int g_variant = -1;
 int variant() {
@@ -178,7 +174,8 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
   GldsArgs x{};
   if (MA == I2CT_KC) x = *tconv;  // the transposed-conv gather parameters
   x.ntx = (g.N + BNT - 1) / BNT;
-  x.nty = (g.M + BM - 1) / BM;
+  const int bm = g.bm == 64 ? 64 : BM;
+  x.nty = (g.M + bm - 1) / bm;
   if (MA == I2C_KC) {
     x.c_a = make_fastdiv(g.a.ic.C);
     x.hw_a = make_fastdiv(g.a.ic.Ho * g.a.ic.Wo);
@@ -197,7 +194,7 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
   }
   const bool rs = can_rs && g.rowsum;
   if (rs) kind = EPI_PLAIN;
-  const dim3 grid((unsigned)std::min<long>(x.ntiles, persist_blocks(glds_occupancy_rt(BNT, kind))));
+  const dim3 grid((unsigned)std::min<long>(x.ntiles, persist_blocks(glds_occupancy_rt(BNT, kind, bm))));
   x.fd_grid = make_fastdiv(grid.x);
   x.fd_ntx = make_fastdiv((uint32_t)x.ntx);
   x.fd_nty = make_fastdiv((uint32_t)x.nty);
@@ -225,6 +222,7 @@ int launch(const GemmArgs& g0, int batch, hipStream_t st) {
   }
   if (!done) {
     g.rs_work = nullptr;
+    g.tickets = nullptr;  // the register-staged kernel: [split][z][M][N] partials + the reduction launch
     if (g.rowsum && MA == RC)  // the register-staged kernel does not fuse the row sums
       hipLaunchKernelGGL(rowsum_rc_kernel, dim3((g.M + 255) / 256), dim3(256), 0, st, g.a.p, g.a.ld, g.M, g.K,
                          g.rowsum);
@@ -232,7 +230,7 @@ int launch(const GemmArgs& g0, int batch, hipStream_t st) {
     if (g.bf16) hipLaunchKernelGGL((gemm_bf16_kernel<MA, MB>), grid, dim3(NT), 0, st, g);
     else hipLaunchKernelGGL((gemm_f32_kernel<MA, MB, 1>), grid, dim3(NT), 0, st, g);
   }
-  if (g.splits > 1) {
+  if (g.splits > 1 && !g.tickets) {
     const long total = (long)g.M * g.N * batch;
     if ((g.N & 3) == 0 && aligned16(g.work)) {
       long nb = (total / 4 + RED_SLOTS - 1) / RED_SLOTS;
@@ -271,6 +269,12 @@ ESP_API int esp_set_gemm_compute(int dtype) {
   return prev;
 }
 ESP_API int esp_get_gemm_compute(void) { return g_compute; }
+ESP_API int esp_set_splitk_mode(int mode) {
+  ESP_ARG_CHECK(mode == 0 || mode == 1, "esp_set_splitk_mode: mode must be 0 or 1, got %d", mode);
+  const int prev = splitk_mode();
+  g_splitk = mode;
+  return prev;
+}
 
 static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2, const float* A, long lda,
                     long sa1, long sa2, const float* B, long ldb, long sb1, long sb2, float* C, long ldc, long sc1,
@@ -376,7 +380,7 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
     g.smb_dbd = smb->smb_dbd;
     g.smb_ldp = smb->smb_ldp;
   }
-  g.wide = N % 4 == 0 && ldc % 4 == 0 && sc1 % 4 == 0 && sc2 % 4 == 0 && aligned16(C) && (!R || aligned16(R)) &&
+  g.wide = N % 4 == 0 && ldc % 4 == 0 && ldc < (1L << 24) && sc1 % 4 == 0 && sc2 % 4 == 0 && aligned16(C) && (!R || aligned16(R)) &&
            (!aux || aligned16(aux)) && (!pre || aligned16(pre)) && (!bias || aligned16(bias)) &&
            (!work || aligned16(work));
   g.ragged4 = !g.wide && N % 4 != 0 && ldc % 4 == 0 && sc1 % 4 == 0 && sc2 % 4 == 0 && aligned16(C) &&
@@ -398,8 +402,9 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
   g.splits = 1;
   g.kchunk = K;
   const long target = 2 * 256;
-  auto ntiles = [&](int bn) { return (long)((N + bn - 1) / bn) * ((M + BM - 1) / BM) * batch; };
+  auto ntiles = [&](int bn, int bm = BM) { return (long)((N + bn - 1) / bn) * ((M + bm - 1) / bm) * batch; };
   g.bnt = 0;
+  g.bm = BM;
   g.bf16 = prec_in >= 0 ? prec_in : (g_compute == 1 ? 1 : 0);
   if (variant() == 4 && g.a.glds && g.b.glds && K > 0) {
     // per-CU time model: ceil(tiles / CUs) tiles of bn/64 units each, x1.3 when the grid
@@ -411,6 +416,14 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
       return c;
     };
     g.bnt = (N <= 64 || cost(64) < cost(128)) ? 64 : 128;
+    // 64 x 64 tiles for grids that 128-row tiles leave under-filled (decoder M ~ 5k tokens, the
+    // 41-query source attention): one work unit per tile, x1.15 for the halved operand reuse
+    if (g.bnt == 64 && mode_a <= RC && mode_b <= RC && g.bf16 != 2 && !smb && !getenv("ESP_GEMM_NO_BM64")) {
+      const long t = ntiles(64, 64);
+      double c = (double)((t + 255) / 256) * 1.15;
+      if (t < 2 * 256) c *= 1.3;
+      if (c < cost(64)) g.bm = 64;
+    }
     // the conv2 weight gradient (im2col-gathered B, K = B*T2*F2 ~ 1M): 128-wide tiles halve the
     // gathered-B re-reads and split-K refills the chip (8.39 vs 9.22 ms at C2 B=128,
     // tools/gemm_bench.py with ESP_GEMM_BNT; the K ~ 48k linear weight gradients keep 128x64)
@@ -420,12 +433,20 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
     if ((force_bnt == 64 || force_bnt == 128) && N > 64) g.bnt = force_bnt;
   }
   {
-    const long tiles = ntiles(g.bnt ? g.bnt : BN);
+    const long tiles = ntiles(g.bnt ? g.bnt : BN, g.bm);
     if (work && tiles < target && K >= 2 * 128) {
       long sp = (target + tiles - 1) / tiles;
       const long by_k = K / 128;  // keep >= 8 slabs of BK per split
       if (sp > by_k) sp = by_k;
-      const long cap = work_bytes / (4L * ((long)M * N * batch + (rowsum ? M : 0)));
+      // in-kernel combine (LDS-DMA kernel): partials on whole tiles + tickets in the last 64 KB
+      const int bmt = g.bm == 64 ? 64 : BM;
+      const long mp = (long)(M + bmt - 1) / bmt * bmt, np = g.bnt ? (long)(N + g.bnt - 1) / g.bnt * g.bnt : N;
+      // opt-in (ESP_SPLITK_INKERNEL=1): measured slower at C2 B=128 -- the last-arriving unit of a
+      // tile sums all of its splits alone (64 splits x 32 KB behind 8 tiles for the d x d weight
+      // gradients: 222 vs 68 us), where the separate reduction spreads them over the chip
+      const bool inkernel = splitk_mode() == 1 && g.bnt && tiles <= ESP_GEMM_TICKETS && work_bytes > ESP_GEMM_TICKET_BYTES;
+      const long part = inkernel ? mp * np : (long)M * N;
+      const long cap = (work_bytes - (inkernel ? ESP_GEMM_TICKET_BYTES : 0)) / (4L * (part * batch + (rowsum ? M : 0)));
       if (sp > cap) sp = cap;
       if (sp > 64) sp = 64;
       // CU balance: with ceil(tiles*sp / 256) tile-rounds on the busiest CU, 72 tiles x 8 splits
@@ -454,7 +475,12 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
         g.splits = (int)((K + chunk - 1) / chunk);
         g.kchunk = chunk;
         g.work = work;
-        if (rowsum && g.bnt) g.rs_work = work + (long)g.splits * batch * M * N;
+        if (rowsum && g.bnt) g.rs_work = work + (long)g.splits * batch * part;
+        if (inkernel) {
+          g.tickets = reinterpret_cast<int*>(reinterpret_cast<char*>(work) + work_bytes - ESP_GEMM_TICKET_BYTES);
+          g.sk_mp = (int)mp;
+          g.sk_np = (int)np;
+        }
       }
     }
   }
@@ -536,6 +562,7 @@ ESP_API int esp_conv2_dgrad(const float* dz2, const float* W, const float* z1, f
     g.b = Operand{wc_work + (long)slot0[cls] * D * D, D, 0, 0, 1, {}, 1};
     g.c = dz1; g.ldc = D; g.alpha = 1.f; g.beta = 0.f;
     g.bwd_act = ACT_RELU; g.pre = z1;
+    g.bf16 = g_compute;  // bf16 MFMA in the reduced-precision mode, as every other GEMM of the step
     g.key = esp::rng_key_ptr();
     g.wide = 1;
     static int dgrad_bnt = -1;  // ESP_CONV2_DGRAD_BNT=64|128 (measurements)
@@ -543,7 +570,7 @@ ESP_API int esp_conv2_dgrad(const float* dz2, const float* W, const float* z1, f
       const char* e = getenv("ESP_CONV2_DGRAD_BNT");
       dgrad_bnt = (e && atoi(e) == 64) ? 64 : 128;
     }
-    g.batch = 1; g.splits = 1; g.kchunk = g.K; g.bnt = D % dgrad_bnt == 0 ? dgrad_bnt : 64;
+    g.batch = 1; g.splits = 1; g.kchunk = g.K; g.bnt = D % dgrad_bnt == 0 ? dgrad_bnt : 64; g.bm = BM;
     g.cmap = 1;
     g.cm_hw = t.t_hw; g.cm_w = t.t_w;
     g.cm_T1 = T1; g.cm_F1 = F1; g.cm_ph = ph; g.cm_pw = pw;

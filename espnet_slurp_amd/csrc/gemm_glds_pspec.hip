@@ -9,19 +9,19 @@ namespace espg {
 bool glds_launch_pspec(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hipStream_t st, const GemmArgs& g,
                        const GldsArgs& x) {
   bool ok = false;
-  const bool known = glds_switch(ma, mb, bnt, prec, [&](auto A, auto B, auto N, auto F) {
+  const bool known = glds_switch(ma, mb, bnt, prec, g.bm, [&](auto A, auto B, auto N, auto F, auto R) {
     constexpr int MA = decltype(A)::value, MB = decltype(B)::value, BNT = decltype(N)::value;
-    constexpr int BF = decltype(F)::value;
+    constexpr int BF = decltype(F)::value, BMT = decltype(R)::value;
     if constexpr ((MA == KC || MA == RC) && (MB == KC || MB == RC)) {
       if (epi == EPI_P0) {
-        hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_P0, BF>), grid, dim3(NT), 0, st, g, x);
+        hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_P0, BF, BMT>), grid, dim3(NT), 0, st, g, x);
         ok = true;
       } else if (epi == EPI_PR) {
-        hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_PR, BF>), grid, dim3(NT), 0, st, g, x);
+        hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_PR, BF, BMT>), grid, dim3(NT), 0, st, g, x);
         ok = true;
       } else if constexpr (MA == KC && MB == KC && BF == 0) {
         if (epi == EPI_SMB) {
-          hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_SMB, BF>), grid, dim3(NT), 0, st, g, x);
+          hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_SMB, BF, BMT>), grid, dim3(NT), 0, st, g, x);
           ok = true;
         }
       }

@@ -11,12 +11,12 @@ namespace espg {
 bool glds_launch_spec(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hipStream_t st, const GemmArgs& g,
                       const GldsArgs& x) {
   bool ok = false;
-  const bool known = glds_switch(ma, mb, bnt, prec, [&](auto A, auto B, auto N, auto F) {
+  const bool known = glds_switch(ma, mb, bnt, prec, g.bm, [&](auto A, auto B, auto N, auto F, auto R) {
     constexpr int MA = decltype(A)::value, MB = decltype(B)::value, BNT = decltype(N)::value;
-    constexpr int BF = decltype(F)::value;
+    constexpr int BF = decltype(F)::value, BMT = decltype(R)::value;
 #define ESP_SPEC(K)                                                                                   \
   if (epi == K) {                                                                                     \
-    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, K, BF>), grid, dim3(NT), 0, st, g, x); \
+    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, K, BF, BMT>), grid, dim3(NT), 0, st, g, x); \
     ok = true;                                                                                        \
   }
     if constexpr (MA == KC && MB == KC) {

@@ -31,6 +31,10 @@
 namespace espg {
 
 constexpr int BM = 128, BN = 128, BK = 32, NT = 256;  // BK: split-K granularity
+// split-K arrival tickets: the last ESP_GEMM_TICKET_BYTES of the GEMM workspace (zero-filled by
+// the caller before first use; every launch leaves them zero), one int per output tile
+#define ESP_GEMM_TICKET_BYTES 65536L
+#define ESP_GEMM_TICKETS 16384L
 
 enum Mode { KC = 0, RC = 1, I2C_KC = 2, I2C_RC = 3, I2CT_KC = 4 };
 enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_SWISH = 2, ACT_MUL = 3 /* bwd_act only: v *= pre */ };
@@ -94,10 +98,16 @@ struct GemmArgs {
              // (esp_set_gemm_compute(1)); 2 bf16 operands in HBM (esp_gemm_bf16: K, ld, strides
              // given in fp32 units, i.e. bf16 pairs; KC x KC only)
   int bnt;  // LDS-DMA kernel tile width (128, or 64 for narrow / mid-size grids); 0 = fallback kernel
+  int bm;   // LDS-DMA kernel tile height: 128, or 64 (with bnt 64) for under-filled grids
   int bwd_act;       // != 0: backward epilogue  v = drop'(acc) * act'(pre)  (act code, dropout regenerated)
   const float* pre;  // pre-activation (same layout as C) for bwd_act
   float* rowsum;     // != NULL: rowsum[m] += sum_k A(m,k)  (bias gradient of a weight-gradient GEMM)
   float* rs_work;    // split-K partial row sums [split][M]
+  // in-kernel split-K combine (LDS-DMA kernel): partials W[split][z][Mp][Np] on whole tiles
+  // (Mp, Np: the tile grid's padded extent), one arrival ticket per output tile; the unit that
+  // arrives last sums the splits in fixed order and runs the epilogue (no reduction launch)
+  int* tickets;      // NULL: the separate splitk_reduce kernel (layout [split][z][M][N])
+  int sk_mp, sk_np;
   int wide;          // float4 epilogue legal (N, ldc, batch strides % 4 == 0, 16-B aligned C/R/aux/pre/bias/work)
   int ragged4;       // the same except N % 4 != 0 (ldc % 4 == 0 pads every row to whole quads): the
                      // plain specialised kinds store the last quad of a row element by element
@@ -532,30 +542,127 @@ __device__ __forceinline__ void store_spec(const GemmArgs& g, int z, int mrow0, 
     }
   }
 }
-// Column stores straight from the accumulator layout (lane = one column, 16 rows per 32x32 tile),
-// no transpose: every store is global_store_dword with a wave-uniform row base (SGPR pair) and a
-// per-lane 32-bit column offset, so the epilogue of a full tile issues no VALU besides the
-// optional alpha scale (the float4 path pays 4 DPP/select VALU per element, and f32 MFMAs do not
-// hide VALU).  Rows m = mrow0 + 32i + 8g + 4h + jj; the 4h term is in the lane offset, columns
-// 32j in the instruction offset.  Needs 4 * (4 * ldc + 64) < 2^32 (host: ldc < 2^27).
-template <int OFF>
-__device__ __forceinline__ void st_col(const float* rowbase, uint32_t voff, float v) {
-  asm volatile("global_store_dword %0, %1, %2 offset:%3" ::"v"(voff), "v"(v), "s"(rowbase), "n"(OFF) : "memory");
+// Column epilogue: stores (and residual / pre-activation loads) straight in the accumulator
+// layout (lane = one column, 16 rows per 32x32 tile), no transpose.  Every access is a
+// buffer_load/store_dword with a wave-uniform row offset in soffset and a per-lane column offset
+// in voffset, so a full tile's epilogue issues no VALU besides its arithmetic: the float4 path pays
+// 4 DPP / select VALU per element for the transpose, and f32 MFMAs do not hide VALU.
+// Rows m = mrow0 + 32i + 8g + 4h + jj (4h in voffset), columns 32j in the instruction offset.
+// Kinds without dropout (dropout keeps the float4 path and its one hash per element pair).
+// Host: the tile's rows span < 2^31 bytes (ldc < 2^24).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 0x7fffffff, 0x00020000);
 }
-template <int TM, int TN, bool A1>
-__device__ __forceinline__ void store_cols(float* cz, long ldc, int mrow0, int ncol0, int lane, float alpha,
-                                           const f32x16 (&acc)[TM][TN]) {
-  static_assert(TN == 2, "column offsets 0 / 128 B");
+template <int EPI>
+constexpr bool col_epi_ok() {
+  return EPI == EPI_P0 || EPI == EPI_PR || EPI == EPI_BIAS || EPI == EPI_BRELU || EPI == EPI_RMASK || EPI == EPI_BMUL;
+}
+// AUX: buffer cache policy of the stores (16 = sc1: write-through, for the split-K hand-off)
+template <int EPI, int TM, int TN, bool A1, int AUX = 0>
+__device__ __forceinline__ void store_cols(const GemmArgs& g, long cbase, long ldc, int mrow0, int ncol0, int lane,
+                                           const f32x16 (&acc)[TM][TN], float* cptr) {
+  using S = EpiSpec<EPI>;
   const int h = lane >> 5, l32 = lane & 31;
-  const uint32_t voff = (uint32_t)((4 * h * ldc + l32) * 4);
+  const long tile0 = cbase + (long)mrow0 * ldc + ncol0;
+  const __amdgpu_buffer_rsrc_t cr = buf_rsrc(cptr + tile0);
+  __amdgpu_buffer_rsrc_t xr = cr;
+  if constexpr (S::res) xr = buf_rsrc(g.r + tile0);
+  if constexpr (S::mul) xr = buf_rsrc(g.pre + tile0);
+  const int voff = (int)((4 * h * ldc + l32) * 4);
+  float bn[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bn[j] = S::bias ? g.bias[ncol0 + 32 * j + l32] : 0.f;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float* rb = cz + (long)(mrow0 + i * 32 + 8 * (r >> 2) + (r & 3)) * ldc + ncol0;
-      st_col<0>(rb, voff, A1 ? acc[i][0][r] : alpha * acc[i][0][r]);
-      st_col<128>(rb, voff, A1 ? acc[i][1][r] : alpha * acc[i][1][r]);
+    for (int j = 0; j < TN; ++j) {
+      float xs[16];
+      if constexpr (S::res || S::mul) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          xs[r] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                   xr, voff + 128 * j, (int)((i * 32 + 8 * (r >> 2) + (r & 3)) * ldc * 4), 0));
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float w = S::bias ? acc[i][j][r] + bn[j] : acc[i][j][r];
+        if constexpr (S::act == ACT_RELU) w = fmaxf(w, 0.f);
+        if constexpr (EPI == EPI_RMASK) w = xs[r] > 0.f ? w : 0.f;
+        else if constexpr (S::mul) w *= xs[r];
+        if constexpr (!A1) w *= g.alpha;
+        if constexpr (S::res) w += g.beta * xs[r];
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, w), cr, voff + 128 * j,
+                                              (int)((i * 32 + 8 * (r >> 2) + (r & 3)) * ldc * 4), AUX);
+      }
     }
+}
+
+// the generic per-element epilogue of a split-K combine (kind chosen at run time: the combine
+// runs once per output tile)
+__device__ __forceinline__ void reduce_store(const GemmArgs& g, int z, int m, int n, float acc) {
+  const long cb = c_base(g, z);
+  const uint64_t db = (uint64_t)z * (uint64_t)g.M * (uint64_t)g.N;
+  switch (epi_kind(g)) {
+    case EPI_BWD: epi_store<EPI_BWD>(g, cb, db, m, n, acc); break;
+    case EPI_FWD: epi_store<EPI_FWD>(g, cb, db, m, n, acc); break;
+    default: epi_store<EPI_PLAIN>(g, cb, db, m, n, acc);
+  }
+}
+
+// In-kernel split-K combine, run by every unit after it stored its partial tile write-through
+// (sc1) and drained (s_waitcnt vmcnt(0)): one agent-scope ticket add per unit; the unit whose add
+// returns splits - 1 re-reads the tile's partials with sc1 loads, in split order 0..splits-1
+// (deterministic whoever arrives last), applies the epilogue and re-arms the ticket to 0.
+// Hand-off form: MI355X_MICROARCH.md "Valid forms" (write-through stores, drained per wave, a
+// workgroup barrier, one lane's agent atomic add; the last adder's waves load after a barrier),
+// plus an agent acquire, since 2-3 workgroups share a CU here.
+template <int BMT, int BNT>
+__device__ __forceinline__ void splitk_combine(const GemmArgs& g, int z, int tm, int tn, int ntx, int nty,
+                                               int* flag_lds) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through partials are done
+  __builtin_amdgcn_s_barrier();
+  const int tile = (z * nty + tm) * ntx + tn;
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(g.tickets + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag_lds = old == g.splits - 1;
+  }
+  __syncthreads();
+  const bool last = *flag_lds != 0;
+  __syncthreads();  // everyone read the flag before a later tile's combine rewrites it
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const int m0 = tm * BMT, n0 = tn * BNT;
+  const long plane = (long)g.sk_mp * g.sk_np;
+  const long zoff = (long)z * plane + (long)m0 * g.sk_np + n0;
+  const long sstride = plane * g.batch;
+  constexpr int Q = BNT / 4;  // float4 slots per tile row
+  for (int e = threadIdx.x; e < BMT * Q; e += NT) {
+    const int r = e / Q, c = (e - r * Q) * 4;
+    const int m = m0 + r, n = n0 + c;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    const long off = zoff + (long)r * g.sk_np + c;
+    for (int sp = 0; sp < g.splits; ++sp) {
+      const float4 v = *reinterpret_cast<const float4*>(g.work + sp * sstride + off);
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    if (m < g.M) {
+      if (n + 0 < g.N) reduce_store(g, z, m, n + 0, a.x);
+      if (n + 1 < g.N) reduce_store(g, z, m, n + 1, a.y);
+      if (n + 2 < g.N) reduce_store(g, z, m, n + 2, a.z);
+      if (n + 3 < g.N) reduce_store(g, z, m, n + 3, a.w);
+    }
+  }
+  if (g.rowsum && tn == 0) {  // the fused bias gradient: the tile's rows, splits in order
+    for (int r = threadIdx.x; r < BMT; r += NT) {
+      const int m = m0 + r;
+      if (m >= g.M) continue;
+      float a = 0.f;
+      for (int sp = 0; sp < g.splits; ++sp)
+        a += __hip_atomic_load(g.rs_work + (long)sp * g.M + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      g.rowsum[m] += a;
+    }
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(g.tickets + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int EPI, int TM, int TN>
@@ -1075,7 +1182,8 @@ struct GldsArgs {
   const float* t_zeros;  // >= 16 zero bytes: the DMA source of lanes outside the grid
   int abl;             // diagnostic ablation bits (ESP_GEMM_ABL, timing only): 1 no DMA after the
                        // first slab, 2 no epilogue stores, 4 no k-loop barrier / waits, 16 dword
-                       // (not float4) epilogue stores, 32 non-temporal epilogue stores
+                       // (not float4) epilogue stores, 32 non-temporal epilogue stores, 64 the
+                       // float4 (transposed) epilogue instead of the column epilogue (store_cols)
 };
 
 constexpr int GL_BK = 32;
@@ -1285,20 +1393,6 @@ struct StageS {
   }
 };
 
-// zero k >= kv of a staged slab (last slab of a K range that is not a multiple of 32)
-template <int MODE, int ROWS>
-__device__ __forceinline__ void zero_tail(float* slab, int kv) {
-  for (int idx = threadIdx.x; idx < ROWS * GL_BK; idx += NT) {
-    if constexpr (MODE == KC || MODE == I2C_KC || MODE == I2CT_KC) {
-      const int r = idx >> 5, k = idx & 31;
-      if (k >= kv) slab[(r * 8 + ((k >> 2) ^ kc_swz(r))) * 4 + (k & 3)] = 0.f;
-    } else {
-      const int k = idx / ROWS;
-      if (k >= kv) slab[idx] = 0.f;
-    }
-  }
-}
-
 // the 16 k-values (k = 16h + s) of tile row r
 template <int MODE, int ROWS>
 __device__ __forceinline__ void frag16(const float* slab, int r, int h, float (&f)[16]) {
@@ -1332,7 +1426,7 @@ __device__ __forceinline__ void raw_barrier() {
 struct TileCoord {
   int m0, n0, tn, z, split, kbeg, kend, nk;
 };
-template <int BNT>
+template <int BNT, int BMT = BM>
 __device__ __forceinline__ TileCoord tile_coord(const GemmArgs& g, const GldsArgs& x, int t, int G) {
   const int round = (int)fdiv((uint32_t)t, x.fd_grid), b = t - round * G;
   const int nr = min(G, x.ntiles - round * G);
@@ -1348,15 +1442,17 @@ __device__ __forceinline__ TileCoord tile_coord(const GemmArgs& g, const GldsArg
   c.kbeg = c.split * g.kchunk;
   c.kend = min(g.K, c.kbeg + g.kchunk);
   c.nk = (c.kend - c.kbeg + GL_BK - 1) / GL_BK;  // >= 1: the host routes K == 0 elsewhere
-  c.m0 = tm * BM;
+  c.m0 = tm * BMT;
   c.n0 = c.tn * BNT;
   return c;
 }
 
 // resident blocks per CU: 128x64 tiles (48 KB LDS) fit three, 128x128 tiles (64 KB) two; the
 // generic fused epilogues need the registers of two (the specialised ones fit three)
-template <int BNT, int EPI>
-constexpr int glds_occupancy() { return (BNT == 64 && (EPI == EPI_PLAIN || EPI >= EPI_BIAS)) ? 3 : 2; }
+template <int BNT, int EPI, int BMT = BM>
+constexpr int glds_occupancy() {
+  return BMT == 64 ? 4 : (BNT == 64 && (EPI == EPI_PLAIN || EPI >= EPI_BIAS)) ? 3 : 2;
+}
 
 // Persistent: block b processes tiles b, b+G, b+2G, ... as ONE continuous slab pipeline — the
 // first slab of the next tile streams in during the last slab of the current one, and the
@@ -1374,12 +1470,15 @@ constexpr int glds_occupancy() { return (BNT == 64 && (EPI == EPI_PLAIN || EPI >
 // a lane's 16 fetched "floats" are 32 bf16 k-values, fed as four bf16x8 operands to four
 // v_mfma_f32_32x32x16_bf16 per (i, j) tile pair (k-step t takes values 8t..8t+7, identically
 // for A and B, so the four steps cover the slab's 64 k once).  No conversion in the k-loop.
-template <int MA, int MB, int BNT, bool RS, int EPI, int PREC = 0>
-__global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_kernel(GemmArgs g, GldsArgs x) {
-  constexpr int WN = BNT / 64, WM = 4 / WN, TM = BM / (WM * 32), TN = 2;
-  constexpr int A_SZ = BM * GL_BK, B_SZ = BNT * GL_BK, BUF = A_SZ + B_SZ;
+// BMT = 64 (with BNT = 64): 64 x 64 tiles, 2 x 2 waves of one 32 x 32 MFMA tile each, for the
+// grids that 128-row tiles leave under-filled (decoder M ~ 5k tokens, 41-query source attention).
+template <int MA, int MB, int BNT, bool RS, int EPI, int PREC = 0, int BMT = BM>
+__global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT>())) void gemm_glds_kernel(GemmArgs g, GldsArgs x) {
+  constexpr int WN = BMT == 64 ? 2 : BNT / 64, WM = 4 / WN, TM = BMT / (WM * 32), TN = BNT / (WN * 32);
+  static_assert(BMT == 128 || BNT == 64, "64-row tiles are 64 wide");
+  constexpr int A_SZ = BMT * GL_BK, B_SZ = BNT * GL_BK, BUF = A_SZ + B_SZ;
   constexpr int NIA = A_SZ / 4 / NT, NIB = B_SZ / 4 / NT;
-  __shared__ __attribute__((aligned(16))) float smem[2 * BUF];
+  __shared__ __attribute__((aligned(16))) float smem[2 * BUF + 4];  // + the split-K combine flag
 
   const int G = gridDim.x;
   int t = blockIdx.x;
@@ -1402,7 +1501,7 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_ke
   // scalar-base staging (StageS) for KC / RC / implicit-im2col A; the gathered operands keep
   // per-lane 64-bit addresses (Stage)
   constexpr bool SA_S = MA == KC || MA == RC || MA == I2C_KC, SB_S = MB == KC || MB == RC;
-  using SAt = std::conditional_t<SA_S, StageS<MA, BM, NIA>, Stage<MA, BM, NIA>>;
+  using SAt = std::conditional_t<SA_S, StageS<MA, BMT, NIA>, Stage<MA, BMT, NIA>>;
   using SBt = std::conditional_t<SB_S, StageS<MB, BNT, NIB>, Stage<MB, BNT, NIB>>;
   SAt sa;
   SBt sb;
@@ -1421,7 +1520,7 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_ke
     else sb.issue(g.b, g.K, k0, dst + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
   };
 
-  TileCoord c = tile_coord<BNT>(g, x, t, G);
+  TileCoord c = tile_coord<BNT, BMT>(g, x, t, G);
   init_ab(c);
   issue_ab(c.kbeg, smem);
   wait_vm0();
@@ -1447,12 +1546,21 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_ke
     TileCoord cn = c;
 
     // frags + MFMAs of one staged slab (and the fused row sums)
-    auto compute = [&](const float* cur) {
+    // kv < GL_BK (the last slab of a K range that is not a multiple of 32): the A fragment's
+    // k >= kv values are zeroed in registers (B's staged tail holds finite clamped elements), so
+    // no LDS zero pass and no extra barrier
+    auto compute = [&](const float* cur, int kv) {
       float af[TM][16], bf[TN][16];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) frag16<MA, BM>(cur, wm * TM * 32 + i * 32 + l32, h, af[i]);
+      for (int i = 0; i < TM; ++i) frag16<MA, BMT>(cur, wm * TM * 32 + i * 32 + l32, h, af[i]);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) frag16<MB, BNT>(cur + A_SZ, wn * 64 + j * 32 + l32, h, bf[j]);
+      for (int j = 0; j < TN; ++j) frag16<MB, BNT>(cur + A_SZ, wn * TN * 32 + j * 32 + l32, h, bf[j]);
+      if (kv < GL_BK) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int s2 = 0; s2 < 16; ++s2) af[i][s2] = 16 * h + s2 < kv ? af[i][s2] : 0.f;
+      }
       if constexpr (PREC == 2) {
         static_assert(!RS, "row sums of packed bf16 operands");
 #pragma unroll
@@ -1520,25 +1628,18 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_ke
       const int k1 = c.kbeg + (kt + 1) * GL_BK;
       float* nxt = smem + (buf ^ 1) * BUF;  // last read before the previous barrier
       if (!(x.abl & 1)) issue_ab(k1, nxt);
-      compute(smem + buf * BUF);
+      compute(smem + buf * BUF, GL_BK);
       finish_slab();
     }
     {  // last slab: the next tile's first slab streams in (this tile's stages are done)
       float* cur = smem + buf * BUF;
       float* nxt = smem + (buf ^ 1) * BUF;
       if (has_next) {
-        cn = tile_coord<BNT>(g, x, tnext, G);
+        cn = tile_coord<BNT, BMT>(g, x, tnext, G);
         init_ab(cn);
         issue_ab(cn.kbeg, nxt);
       }
-      const int kv = c.kend - (c.kbeg + (c.nk - 1) * GL_BK);
-      if (kv < GL_BK) {
-        zero_tail<MA, BM>(cur, kv);
-        zero_tail<MB, BNT>(cur + A_SZ, kv);
-        wait_lgkm0();
-        raw_barrier();
-      }
-      compute(cur);
+      compute(cur, c.kend - (c.kbeg + (c.nk - 1) * GL_BK));
       finish_slab();
     }
     // epilogue: fire-and-forget stores that drain under the next tile's first slab
@@ -1548,30 +1649,35 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_ke
         const float v = rs[i] + __shfl_xor(rs[i], 32, 64);  // k halves 0-15 / 16-31 of every slab
         const int m = c.m0 + wm * TM * 32 + i * 32 + l32;
         if (h == 0 && m < g.M) {
-          if (g.splits > 1) g.rs_work[(long)c.split * g.M + m] = v;
+          if (g.splits > 1) __hip_atomic_store(g.rs_work + (long)c.split * g.M + m, v, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);  // write-through (combine hand-off)
           else g.rowsum[m] += v;
         }
       }
     }
-    if (!(x.abl & 2)) {
+    if (g.tickets) {  // in-kernel split-K: write-through partial tile, ticket, last unit combines
+      float* Wz = g.work + ((long)c.split * g.batch + c.z) * ((long)g.sk_mp * g.sk_np);
+      store_cols<EPI_P0, TM, TN, true, 16>(g, 0, g.sk_np, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, lane, acc, Wz);
+      splitk_combine<BMT, BNT>(g, c.z, c.m0 / BMT, c.tn, x.ntx, x.nty, reinterpret_cast<int*>(smem + 2 * BUF));
+    } else if (!(x.abl & 2)) {
       float* W = g.splits > 1 ? g.work + ((long)c.split * g.batch + c.z) * (long)g.M * g.N : nullptr;
       if constexpr (EPI >= EPI_BIAS) {  // specialised kinds: never split-K, always wide
-        const int mr0 = c.m0 + wm * TM * 32, nc0 = c.n0 + wn * 64;
-        if (EPI == EPI_P0 && (x.abl & 64) && mr0 + TM * 32 <= g.M && nc0 + TN * 32 <= g.N) {
-          float* cz = g.c + c_base(g, c.z);
-          if (g.alpha == 1.0f) store_cols<TM, TN, true>(cz, g.ldc, mr0, nc0, lane, 1.0f, acc);
-          else store_cols<TM, TN, false>(cz, g.ldc, mr0, nc0, lane, g.alpha, acc);
+        const int mr0 = c.m0 + wm * TM * 32, nc0 = c.n0 + wn * TN * 32;
+        if (col_epi_ok<EPI>() && !(x.abl & 64) && mr0 + TM * 32 <= g.M && nc0 + TN * 32 <= g.N) {
+          const long cb = c_base(g, c.z);
+          if (g.alpha == 1.0f) store_cols<EPI, TM, TN, true>(g, cb, g.ldc, mr0, nc0, lane, acc, g.c);
+          else store_cols<EPI, TM, TN, false>(g, cb, g.ldc, mr0, nc0, lane, acc, g.c);
         } else {
           store_spec_tiles<EPI, TM, TN>(g, c.z, mr0, nc0, lane, acc);
         }
       } else if (g.wide) {
-        if (W && (x.abl & 64) && c.m0 + wm * TM * 32 + TM * 32 <= g.M && c.n0 + wn * 64 + TN * 32 <= g.N)
-          store_cols<TM, TN, true>(W, g.N, c.m0 + wm * TM * 32, c.n0 + wn * 64, lane, 1.0f, acc);
-        else if (W) store_partials_wide<TM, TN>(g, W, c.m0 + wm * TM * 32, c.n0 + wn * 64, lane, acc);
-        else store_tiles_wide<EPI, TM, TN>(g, c.z, c.m0 + wm * TM * 32, c.n0 + wn * 64, lane, acc, (x.abl & 32) != 0);
+        if (W && !(x.abl & 64) && c.m0 + wm * TM * 32 + TM * 32 <= g.M && c.n0 + wn * TN * 32 + TN * 32 <= g.N)
+          store_cols<EPI_P0, TM, TN, true>(g, 0, g.N, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, lane, acc, W);
+        else if (W) store_partials_wide<TM, TN>(g, W, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, lane, acc);
+        else store_tiles_wide<EPI, TM, TN>(g, c.z, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, lane, acc, (x.abl & 32) != 0);
       } else {
-        if (W) store_partials<TM, TN>(g, W, c.m0 + wm * TM * 32, c.n0 + wn * 64, h, l32, acc);
-        else store_tiles<EPI, TM, TN>(g, c.z, c.m0 + wm * TM * 32, c.n0 + wn * 64, h, l32, acc);
+        if (W) store_partials<TM, TN>(g, W, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, h, l32, acc);
+        else store_tiles<EPI, TM, TN>(g, c.z, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, h, l32, acc);
       }
     }
     if (!has_next) break;
@@ -1580,31 +1686,38 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI>())) void gemm_glds_ke
   }
 }
 
-// resident blocks per CU of a gemm_glds_kernel<.., BNT, .., EPI, ..> launch (host side)
-inline int glds_occupancy_rt(int bnt, int epi) { return (bnt == 64 && (epi == EPI_PLAIN || epi >= EPI_BIAS)) ? 3 : 2; }
 
 // Map run-time (mode_a, mode_b, tile width, precision) onto compile-time constants for the mode
 // pairs the host issues; calls f(MA, MB, BNT, PREC) with std::integral_constant arguments.
 // false: no such instantiation (PREC 2 exists for KC x KC only).
 template <int V>
 using IC = std::integral_constant<int, V>;
+// bm = 64 (64 x 64 tiles) exists for bnt = 64, KC / RC operand pairs and prec 0 / 1 only.
 template <class F>
-bool glds_switch(int ma, int mb, int bnt, int prec, F&& f) {
+bool glds_switch(int ma, int mb, int bnt, int prec, int bm, F&& f) {
   auto tile = [&](auto A, auto B) {
     if (bnt != 64 && bnt != 128) return false;
-    auto by_prec = [&](auto N) {
+    constexpr bool small_ok = (decltype(A)::value == KC || decltype(A)::value == RC) &&
+                              (decltype(B)::value == KC || decltype(B)::value == RC);
+    auto by_prec = [&](auto N, auto R) {
       if (prec == 0) {
-        f(A, B, N, IC<0>{});
+        f(A, B, N, IC<0>{}, R);
       } else if (prec == 1) {
-        f(A, B, N, IC<1>{});
-      } else if constexpr (decltype(A)::value == KC && decltype(B)::value == KC) {
-        f(A, B, N, IC<2>{});
+        f(A, B, N, IC<1>{}, R);
+      } else if constexpr (decltype(A)::value == KC && decltype(B)::value == KC && decltype(R)::value == BM) {
+        f(A, B, N, IC<2>{}, R);
       } else {
         return false;
       }
       return true;
     };
-    return bnt == 64 ? by_prec(IC<64>{}) : by_prec(IC<128>{});
+    if (bm == 64) {
+      if constexpr (small_ok) {
+        if (bnt == 64 && prec != 2) return by_prec(IC<64>{}, IC<64>{});
+      }
+      return false;
+    }
+    return bnt == 64 ? by_prec(IC<64>{}, IC<BM>{}) : by_prec(IC<128>{}, IC<BM>{});
   };
   switch (ma * 8 + mb) {
     case KC * 8 + KC: return tile(IC<KC>{}, IC<KC>{});
@@ -1624,6 +1737,7 @@ bool glds_switch(int ma, int mb, int bnt, int prec, F&& f) {
 //   gemm_glds_epi.hip   : generic EPI_FWD / EPI_BWD
 //   gemm_glds_spec.hip  : specialised kinds (EPI_BIAS .. EPI_BMUL)
 //   gemm_glds_pspec.hip : specialised plain kinds (EPI_P0, EPI_PR)
+// (bm = the tile height, g.bm)
 bool glds_launch_plain(int ma, int mb, int bnt, int prec, bool rs, dim3 grid, hipStream_t st, const GemmArgs& g,
                        const GldsArgs& x);
 bool glds_launch_epi(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hipStream_t st, const GemmArgs& g,
@@ -1632,5 +1746,9 @@ bool glds_launch_spec(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hip
                       const GldsArgs& x);
 bool glds_launch_pspec(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hipStream_t st, const GemmArgs& g,
                        const GldsArgs& x);
+// resident blocks per CU of a launch (host side)
+inline int glds_occupancy_rt(int bnt, int epi, int bm) {
+  return bm == 64 ? 4 : (bnt == 64 && (epi == EPI_PLAIN || epi >= EPI_BIAS)) ? 3 : 2;
+}
 
 }  // namespace espg

@@ -39,15 +39,16 @@ class _Workspace:
     """Grow-only scratch buffer per (device, stream): stream-ordered reuse is safe, and kernels
     on the weight-gradient side stream get their own buffer."""
 
-    def __init__(self):
+    def __init__(self, zero: bool = False):
         self.buf = {}
+        self.zero = zero  # zero-filled at allocation (the GEMM pool: split-K tickets, esp_gemm_f32)
 
     def get(self, nbytes: int, device) -> torch.Tensor:
         dev = torch.device(device)
         key = (str(dev), torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else 0)
         b = self.buf.get(key)
         if b is None or b.numel() < nbytes:
-            b = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+            b = (torch.zeros if self.zero else torch.empty)(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
             self.buf[key] = b
         return b
 
@@ -57,7 +58,7 @@ class _Workspace:
 
 WS = _Workspace()
 _WS2 = _Workspace()
-_GEMM_WS = _Workspace()          # split-K partials (stream-ordered reuse)
+_GEMM_WS = _Workspace(zero=True)  # split-K partials (stream-ordered reuse) + arrival tickets (last 64 KB)
 _GEMM_WS_BYTES = 64 << 20
 
 
@@ -359,6 +360,16 @@ def set_gemm_compute(dtype) -> int:
     prev = lib.esp_set_gemm_compute(int(code))
     if prev < 0:
         raise _native.NativeError(f"esp_set_gemm_compute failed: {lib.esp_last_error().decode()}")
+    return prev
+
+
+def set_splitk_mode(mode: int) -> int:
+    """0: split-K partials combined by a separate reduction launch (default); 1: in-kernel by the
+    last-arriving unit of each tile (esp_set_splitk_mode).  Returns the previous mode."""
+    lib = _native.load()
+    prev = lib.esp_set_splitk_mode(int(mode))
+    if prev < 0:
+        raise _native.NativeError(f"esp_set_splitk_mode failed: {lib.esp_last_error().decode()}")
     return prev
 
 

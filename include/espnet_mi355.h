@@ -39,7 +39,11 @@ int esp_abi_version(void);
  *   rowsum != NULL (mode_a RC, batch 1): rowsum[m] += sum_k A(m,k) — the bias gradient of a
  *   weight-gradient GEMM (dW = dy^T x, db = colsum dy) in the same pass over dy.
  *   work/work_bytes: optional scratch; when the tile grid is too small to fill the chip the
- *   K range is split over blocks and reduced (fixed order, deterministic) before the epilogue. */
+ *   K range is split over blocks and reduced (fixed order, deterministic) before the epilogue.
+ *   The last 64 KiB of work (work_bytes > 64 KiB) hold the split-K arrival tickets of the
+ *   in-kernel combine: the caller zero-fills them once before the first call that uses this
+ *   workspace and every launch leaves them zero; one workspace must not serve two launches
+ *   that run concurrently (e.g. on two streams). */
 int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2,
                  const float* A, long lda, long sa1, long sa2,
                  const float* B, long ldb, long sb1, long sb2,
@@ -57,6 +61,11 @@ int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2
  * knob is `use_amp` (fp16 autocast, trainer.py:181-195,554).  Returns the previous value. */
 int esp_set_gemm_compute(int dtype);
 int esp_get_gemm_compute(void);
+/* Split-K combine of every later esp_gemm_f32 launch (process-wide): 0 = a separate
+ * fixed-order reduction launch (default), 1 = in-kernel (the last-arriving unit of each output
+ * tile sums the splits in fixed order; needs the zeroed ticket area of `work`, see above).
+ * Initialised from ESP_SPLITK_INKERNEL.  Returns the previous mode. */
+int esp_set_splitk_mode(int mode);
 /* bf16-operand GEMM (the C5 reduced-precision path): A [M][K] and B [N][K] bf16 (bits of
  * __bf16 / torch.bfloat16), both K-contiguous (mode KC x KC), fp32 accumulate; C, the epilogue
  * (bias, act, aux, dropout, bwd_act / pre, residual) and split-K exactly as esp_gemm_f32.  K,

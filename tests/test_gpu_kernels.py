@@ -178,6 +178,47 @@ def test_gemm_weight_grad_fused_bias(dev, M, N, Kk, pad):
     assert (db.cpu().double() - refb).abs().max().item() <= 1e-5 * math.sqrt(M) * 4
 
 
+@pytest.mark.parametrize("M,N,Kk,batch", [(256, 1024, 47872 // 8, 1), (300, 260, 4000, 1), (96, 40, 3000, 3),
+                                          (130, 64, 2048, 2)])
+@pytest.mark.parametrize("inkernel", [0, 1])
+def test_gemm_splitk_combine(dev, M, N, Kk, batch, inkernel):
+    """Split-K with the separate reduction launch (0) and the in-kernel combine (1: write-through
+    partials, arrival tickets, the last unit sums the splits in fixed order): equals the fp64
+    product, is bit-identical run to run, leaves every ticket re-armed to 0, and runs the generic
+    fused epilogue (bias + Swish + aux) after the combine.  Batched z and ragged tiles included."""
+    prev = K.set_splitk_mode(inkernel)
+    try:
+        _splitk_case(dev, M, N, Kk, batch)
+    finally:
+        K.set_splitk_mode(prev)
+
+
+def _splitk_case(dev, M, N, Kk, batch):
+    A, B = _r(batch, M, Kk, seed=41), _r(batch, N, Kk, seed=42)
+    Ad, Bd = A.to(dev), B.to(dev)
+    C1 = torch.empty(batch, M, N, device=dev)
+    C2 = torch.empty(batch, M, N, device=dev)
+    for C in (C1, C2):
+        K.gemm(M, N, Kk, Ad, Bd, C, mode_a=K.KC, lda=Kk, mode_b=K.KC, ldb=Kk, ldc=N, batch=batch,
+               sa=(M * Kk, 0), sb=(N * Kk, 0), sc=(M * N, 0))
+    torch.cuda.synchronize()
+    ref = A.double() @ B.double().transpose(1, 2)
+    assert (C1.cpu().double() - ref).abs().max().item() <= 1e-5 * math.sqrt(Kk) * 4
+    assert torch.equal(C1, C2)
+    ws = K._GEMM_WS.get(K._GEMM_WS_BYTES, dev)
+    tickets = ws[K._GEMM_WS_BYTES - 65536:K._GEMM_WS_BYTES].view(torch.int32)
+    assert int(tickets.abs().sum().item()) == 0
+    if batch == 1:  # generic epilogue after the combine
+        b = _r(N, seed=43)
+        out, aux = torch.empty(M, N, device=dev), torch.empty(M, N, device=dev)
+        K.linear_fwd(Ad[0], Bd[0], b.to(dev), out, act=K.ACT_SWISH, aux=aux)
+        pre = ref[0] + b.double()
+        torch.cuda.synchronize()
+        tol = 1e-5 * math.sqrt(Kk) * 4
+        assert (aux.cpu().double() - pre).abs().max().item() <= tol
+        assert (out.cpu().double() - pre * torch.sigmoid(pre)).abs().max().item() <= 2 * tol
+
+
 def test_colsum_and_layernorm_bwd_shapes(dev):
     for (M, N, ld) in [(23936 // 4, 256, 256), (1001, 1024, 1024), (37, 30, 33), (3, 5, 8)]:
         x = _r(M, ld, seed=16)

@@ -16,12 +16,15 @@ def main():
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--config", choices=sorted(bench.PRESETS), default="c2")
     a = ap.parse_args()
-    args = argparse.Namespace(d=256, heads=4, ff=1024, layers=12, vocab=600, rel_pos="latest", batch=a.batch)
+    d, heads, ff, layers, amp = bench.PRESETS[a.config]
+    args = argparse.Namespace(d=d, heads=heads, ff=ff, layers=layers, vocab=600, rel_pos="latest", batch=a.batch)
     dev = torch.device("cuda:0")
     model = bench.build(args, dev)
     opt = FusedAdam(model.parameters(), model.flat, lr=2e-4)
-    tr = Trainer(model, opt, WarmupLR(opt, 25000))
+    from espnet_slurp_amd.train.trainer import TrainerOptions
+    tr = Trainer(model, opt, WarmupLR(opt, 25000), TrainerOptions(use_amp=amp))
     batch = bench.synthetic_batch(args.batch, 600, 0, dev)
     tr.train_one_step(batch)
     torch.cuda.synchronize()
