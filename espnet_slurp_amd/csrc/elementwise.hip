@@ -20,7 +20,7 @@ void set_error(const char* fmt, ...) {
 }  // namespace esp
 
 ESP_API const char* esp_last_error(void) { return esp::g_err; }
-ESP_API int esp_abi_version(void) { return 21; }
+ESP_API int esp_abi_version(void) { return 22; }
 ESP_API int esp_set_rng_key(const unsigned long long* key) {
   esp::g_rng_key = (const uint64_t*)key;
   return 0;
@@ -484,6 +484,25 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ x, uint16_t* __rest
       if (c + e < cols) dst[e] = bf16_rne(src[e]);
   }
 }
+// the wide form: 8 columns per thread (two float4 loads, one 16-B store); cols % 8 == 0, ldx and
+// ldy % 8 == 0, 16-B aligned x and y
+__global__ void f32_to_bf16_8_kernel(const float* __restrict__ x, uint16_t* __restrict__ y, long rows, int cols,
+                                     long ldx, long ldy) {
+  const int c8 = cols >> 3;
+  const long n = rows * c8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / c8;
+    const int c = (int)(i - r * c8) * 8;
+    const float4 a = *reinterpret_cast<const float4*>(x + r * ldx + c);
+    const float4 b = *reinterpret_cast<const float4*>(x + r * ldx + c + 4);
+    uint4 o;
+    o.x = bf16_rne(a.x) | ((uint32_t)bf16_rne(a.y) << 16);
+    o.y = bf16_rne(a.z) | ((uint32_t)bf16_rne(a.w) << 16);
+    o.z = bf16_rne(b.x) | ((uint32_t)bf16_rne(b.y) << 16);
+    o.w = bf16_rne(b.z) | ((uint32_t)bf16_rne(b.w) << 16);
+    *reinterpret_cast<uint4*>(y + r * ldy + c) = o;
+  }
+}
 __global__ __launch_bounds__(256) void f32_to_bf16_t_kernel(const float* __restrict__ x, uint16_t* __restrict__ y,
                                                             long rows, int cols, long ldx, long ldy) {
   __shared__ uint16_t tile[64][66];
@@ -513,6 +532,9 @@ ESP_API int esp_f32_to_bf16(const float* x, void* y, long rows, int cols, long l
     ESP_ARG_CHECK((rows + 63) / 64 <= 65535, "esp_f32_to_bf16: too many rows for the transposed cast");
     hipLaunchKernelGGL(f32_to_bf16_t_kernel, dim3((cols + 63) / 64, (unsigned)((rows + 63) / 64)), dim3(256), 0, st,
                        x, (uint16_t*)y, rows, cols, ldx, ldy);
+  } else if (cols % 8 == 0 && ldx % 8 == 0 && ldy % 8 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
+    hipLaunchKernelGGL(f32_to_bf16_8_kernel, dim3(grid_for(rows * (cols / 8))), dim3(256), 0, st, x, (uint16_t*)y,
+                       rows, cols, ldx, ldy);
   } else {
     hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(grid_for(rows * ((cols + 3) / 4))), dim3(256), 0, st, x,
                        (uint16_t*)y, rows, cols, ldx, ldy);

@@ -297,18 +297,22 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
                   stream, -1);
 }
 
-ESP_API int esp_gemm_bf16(int M, int N, int K, int batch, int nb2, const void* A, long lda, long sa1, long sa2,
-                          const void* B, long ldb, long sb1, long sb2, float* C, long ldc, long sc1, long sc2,
-                          const float* bias, float alpha, float beta, const float* R, int act, float* aux,
-                          float drop_p, unsigned long long seed, int bwd_act, const float* pre, float* work,
-                          long work_bytes, void* stream) {
+ESP_API int esp_gemm_bf16(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2, const void* A, long lda,
+                          long sa1, long sa2, const void* B, long ldb, long sb1, long sb2, float* C, long ldc,
+                          long sc1, long sc2, const float* bias, float alpha, float beta, const float* R, int act,
+                          float* aux, float drop_p, unsigned long long seed, int bwd_act, const float* pre,
+                          float* work, long work_bytes, void* stream) {
+  ESP_ARG_CHECK((mode_a == KC || mode_a == RC) && (mode_b == KC || mode_b == RC),
+                "esp_gemm_bf16: modes must be 0 (KC) or 1 (RC)");
   ESP_ARG_CHECK(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && sa1 % 8 == 0 && sa2 % 8 == 0 && sb1 % 8 == 0 &&
                     sb2 % 8 == 0 && aligned16(A) && aligned16(B),
                 "esp_gemm_bf16: K, ld and strides must be multiples of 8 bf16 and A, B 16-B aligned");
-  // bf16 pairs viewed as fp32 elements by the staging code (PREC 2)
-  return gemm_run(KC, KC, M, N, K / 2, batch, nb2, (const float*)A, lda / 2, sa1 / 2, sa2 / 2, (const float*)B,
-                  ldb / 2, sb1 / 2, sb2 / 2, C, ldc, sc1, sc2, bias, alpha, beta, R, act, aux, drop_p, seed, bwd_act,
-                  pre, nullptr, nullptr, nullptr, work, work_bytes, stream, 2);
+  ESP_ARG_CHECK((mode_a == KC || M % 8 == 0) && (mode_b == KC || N % 8 == 0),
+                "esp_gemm_bf16: an RC operand's row count must be a multiple of 8 (M=%d N=%d)", M, N);
+  // bf16 pairs viewed as fp32 elements by the staging code (PREC 2): K, ld and strides in pairs
+  return gemm_run(mode_a, mode_b, M, N, K / 2, batch, nb2, (const float*)A, lda / 2, sa1 / 2, sa2 / 2,
+                  (const float*)B, ldb / 2, sb1 / 2, sb2 / 2, C, ldc, sc1, sc2, bias, alpha, beta, R, act, aux, drop_p,
+                  seed, bwd_act, pre, nullptr, nullptr, nullptr, work, work_bytes, stream, 2);
 }
 
 // Rel-pos attention score gradient in one GEMM: dP = dctx V^T per (head, utterance) with the
@@ -359,8 +363,9 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
   g.b = Operand{B, ldb, sb1, sb2, 0, {}};
   g.a.vec = aligned16(A) && lda % 4 == 0 && sa1 % 4 == 0 && sa2 % 4 == 0;
   g.b.vec = aligned16(B) && ldb % 4 == 0 && sb1 % 4 == 0 && sb2 % 4 == 0;
-  g.a.glds = glds_ok(mode_a, A, lda, sa1, sa2, M, K);
-  g.b.glds = glds_ok(mode_b, B, ldb, sb1, sb2, N, K);
+  // (PREC 2: an RC operand's contiguous run is rows / 2 pairs)
+  g.a.glds = glds_ok(mode_a, A, lda, sa1, sa2, prec_in == 2 && mode_a == RC ? M / 2 : M, K);
+  g.b.glds = glds_ok(mode_b, B, ldb, sb1, sb2, prec_in == 2 && mode_b == RC ? N / 2 : N, K);
   if (mode_a >= 2) {
     ESP_ARG_CHECK(im2col_a && im2col_a[2] % 4 == 0 && aligned16(A), "esp_gemm_f32: im2col A needs C%%4==0");
     g.a.ic = Im2col{im2col_a[0], im2col_a[1], im2col_a[2], im2col_a[3], im2col_a[4]};

@@ -1331,9 +1331,19 @@ __device__ __forceinline__ uint32_t lds_addr(const float* p) {
 //   I2C_KC sbase(k0) = base + tap_off(k0)             base = A_z + pix_off(row0)
 // Lanes past the last row read a clamped row (their products only reach discarded outputs).  Only
 // a slab that reaches past K clamps k per lane (KC: to the last whole quad, RC: to K - 1).
-template <int MODE, int ROWS, int NI>
+// B16 (PREC 2, bf16 operands viewed as fp32 pairs): KC operands are staged as in fp32 (a slab
+// holds 32 pairs = 64 bf16 k per row); an RC operand's slab is 64 k-rows x ROWS bf16 (ROWS * 2
+// bytes per k-row, the same 16 KB / 8 KB as every other slab), its 16-byte chunks XOR-swizzled
+// by k-row (bf16_rc_swz) for the transposing reads of frag_tr16.  K and k0 count pairs; an RC
+// k-row index is 2 * k + (0..63).  `rows` and `ld` of an RC operand: bf16 rows, ld in pairs.
+__device__ __forceinline__ int bf16_rc_swz(int rowb, int kr) {
+  return rowb == 256 ? (kr & 3) << 2 : ((kr >> 1) & 1) << 2;
+}
+
+template <int MODE, int ROWS, int NI, bool B16 = false>
 struct StageS {
   static constexpr bool kKC = MODE == KC || MODE == I2C_KC;
+  static constexpr bool kT16 = B16 && MODE == RC;  // transposed-read bf16 image
   const float* base;
   long ld;
   int kb;
@@ -1345,6 +1355,7 @@ struct StageS {
     kb = kbeg;
     long pix0 = 0;
     if constexpr (MODE == KC) base = zbase + (long)row0 * op.ld + kbeg;
+    else if constexpr (kT16) base = zbase + (long)2 * kbeg * op.ld;
     else if constexpr (MODE == RC) base = zbase + (long)kbeg * op.ld;
     else {
       pix0 = i2c_pix_off(op.ic, fhw, fwo, row0);
@@ -1359,6 +1370,13 @@ struct StageS {
         q[i] = 4 * qq;
         if constexpr (MODE == KC) off[i] = (uint32_t)(((uint32_t)(gr - row0) * (uint32_t)op.ld + 4 * qq) * 4u);
         else off[i] = (uint32_t)((i2c_pix_off(op.ic, fhw, fwo, gr) - pix0 + 4 * qq) * 4);
+      } else if constexpr (kT16) {
+        constexpr int QPR = ROWS / 8;  // 16-byte chunks (8 bf16 rows) per k-row
+        const int kr = slot / QPR, c = slot % QPR;
+        const int cs = c ^ bf16_rc_swz(ROWS * 2, kr);
+        const int gp = min((row0 >> 1) + 4 * cs, ((rows >> 1) - 1) & ~3);  // first pair of the chunk
+        q[i] = kr;
+        off[i] = (uint32_t)(((uint32_t)kr * (uint32_t)op.ld + (uint32_t)gp) * 4u);
       } else {
         constexpr int QPR = ROWS / 4;  // quads per k-row
         const int kr = slot / QPR, rs = slot % QPR;
@@ -1373,6 +1391,7 @@ struct StageS {
   __device__ __forceinline__ void issue(const Operand& op, int K, int k0, uint32_t dst, int wave) const {
     const float* sb;
     if constexpr (MODE == KC) sb = base + (k0 - kb);
+    else if constexpr (kT16) sb = base + (long)2 * (k0 - kb) * ld;
     else if constexpr (MODE == RC) sb = base + (long)(k0 - kb) * ld;
     else {  // the slab's tap and channel offset (C % 32 == 0, K % 32 == 0: host-checked)
       const int t = k0 / op.ic.C, kt = t / 3, kf = t - 3 * kt;
@@ -1386,12 +1405,40 @@ struct StageS {
       for (int i = 0; i < NI; ++i) {
         uint32_t o = off[i];
         if constexpr (MODE == KC) o -= 4u * (uint32_t)max(0, q[i] - (((K - 1) & ~3) - k0));
+        else if constexpr (kT16) o -= 4u * (uint32_t)ld * (uint32_t)max(0, q[i] - (2 * (K - k0) - 1));
         else o -= 4u * (uint32_t)ld * (uint32_t)max(0, q[i] - (K - 1 - k0));
         lds_dma16_s(sb, o, dst + (i * 4 + wave) * 1024);
       }
     }
   }
 };
+
+// bf16 RC operand (PREC 2): the four 32x32x16 MFMA fragments of the 32 tile rows starting at
+// rbase, by ds_read_b64_tr_b16 (T10): a 16-lane group reads a 4 k-row x 16 row block and lane i
+// receives row i's 4 k values.  Lane (h, l32) gets rows rbase + l32 at bf16 k = 32h + 8t + 0..7
+// for step t -- the k a KC operand's lane supplies from its frag16 chunk t (both operands agree).
+// Lane 4q+p supplies the address of k-row kb + q, rows 4p..4p+3 of its group's 16; the chunk
+// swizzle of k-row kb + q is a function of q alone (kb % 4 == 0), so every read is the lane's
+// base address + an immediate.  Conflict-free: a 32-lane half covers the 64 banks once.
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+template <int ROWS>
+__device__ __forceinline__ void frag_tr16(const float* slab, int rbase, int lane, float4 (&f)[4]) {
+  constexpr int ROWB = ROWS * 2;
+  const int g1 = (lane >> 4) & 1, h = lane >> 5, q = (lane >> 2) & 3, p = lane & 3;
+  const int mloc = rbase + 16 * g1 + 4 * p;
+  const int base = (32 * h + q) * ROWB + (((mloc >> 3) ^ bf16_rc_swz(ROWB, q)) << 4) + 8 * (p & 1);
+  const __attribute__((address_space(3))) char* s =
+      (const __attribute__((address_space(3))) char*)(__attribute__((address_space(3))) const float*)slab;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) v4i16*)(s + base + 8 * t * ROWB));
+    const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) v4i16*)(s + base + (8 * t + 4) * ROWB));
+    const int2 a = __builtin_bit_cast(int2, lo), b = __builtin_bit_cast(int2, hi);
+    f[t] = make_float4(__int_as_float(a.x), __int_as_float(a.y), __int_as_float(b.x), __int_as_float(b.y));
+  }
+}
 
 // the 16 k-values (k = 16h + s) of tile row r
 template <int MODE, int ROWS>
@@ -1501,8 +1548,8 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT>())) void gemm_gl
   // scalar-base staging (StageS) for KC / RC / implicit-im2col A; the gathered operands keep
   // per-lane 64-bit addresses (Stage)
   constexpr bool SA_S = MA == KC || MA == RC || MA == I2C_KC, SB_S = MB == KC || MB == RC;
-  using SAt = std::conditional_t<SA_S, StageS<MA, BMT, NIA>, Stage<MA, BMT, NIA>>;
-  using SBt = std::conditional_t<SB_S, StageS<MB, BNT, NIB>, Stage<MB, BNT, NIB>>;
+  using SAt = std::conditional_t<SA_S, StageS<MA, BMT, NIA, PREC == 2>, Stage<MA, BMT, NIA>>;
+  using SBt = std::conditional_t<SB_S, StageS<MB, BNT, NIB, PREC == 2>, Stage<MB, BNT, NIB>>;
   SAt sa;
   SBt sb;
   auto init_ab = [&](const TileCoord& cc) {
@@ -1550,6 +1597,54 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT>())) void gemm_gl
     // k >= kv values are zeroed in registers (B's staged tail holds finite clamped elements), so
     // no LDS zero pass and no extra barrier
     auto compute = [&](const float* cur, int kv) {
+      if constexpr (PREC == 2) {
+        static_assert(!RS, "row sums of packed bf16 operands");
+        // fragments as 4 chunks of 8 bf16 per tile (k = 32h + 8t + 0..7 for chunk t)
+        float4 a4[TM][4], b4[TN][4];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          if constexpr (MA == RC) {
+            frag_tr16<BMT>(cur, wm * TM * 32 + i * 32, lane, a4[i]);
+          } else {
+            float f[16];
+            frag16<MA, BMT>(cur, wm * TM * 32 + i * 32 + l32, h, f);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) a4[i][t] = make_float4(f[4 * t], f[4 * t + 1], f[4 * t + 2], f[4 * t + 3]);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (MB == RC) {
+            frag_tr16<BNT>(cur + A_SZ, wn * TN * 32 + j * 32, lane, b4[j]);
+          } else {
+            float f[16];
+            frag16<MB, BNT>(cur + A_SZ, wn * TN * 32 + j * 32 + l32, h, f);
+#pragma unroll
+            for (int t = 0; t < 4; ++t) b4[j][t] = make_float4(f[4 * t], f[4 * t + 1], f[4 * t + 2], f[4 * t + 3]);
+          }
+        }
+        if (kv < GL_BK) {  // K tail (kv pairs): zero A's pairs at pair index >= kv
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+              const int k0p = 16 * h + 4 * t;  // pair index of the chunk's first value
+              a4[i][t].x = k0p + 0 < kv ? a4[i][t].x : 0.f;
+              a4[i][t].y = k0p + 1 < kv ? a4[i][t].y : 0.f;
+              a4[i][t].z = k0p + 2 < kv ? a4[i][t].z : 0.f;
+              a4[i][t].w = k0p + 3 < kv ? a4[i][t].w : 0.f;
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a4[i][t]),
+                                                                  __builtin_bit_cast(bf16x8, b4[j][t]), acc[i][j], 0, 0, 0);
+        return;
+      }
       float af[TM][16], bf[TN][16];
 #pragma unroll
       for (int i = 0; i < TM; ++i) frag16<MA, BMT>(cur, wm * TM * 32 + i * 32 + l32, h, af[i]);
@@ -1561,20 +1656,7 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT>())) void gemm_gl
 #pragma unroll
           for (int s2 = 0; s2 < 16; ++s2) af[i][s2] = 16 * h + s2 < kv ? af[i][s2] : 0.f;
       }
-      if constexpr (PREC == 2) {
-        static_assert(!RS, "row sums of packed bf16 operands");
-#pragma unroll
-        for (int t = 0; t < 4; ++t)
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              const float4 a4 = make_float4(af[i][4 * t], af[i][4 * t + 1], af[i][4 * t + 2], af[i][4 * t + 3]);
-              const float4 b4 = make_float4(bf[j][4 * t], bf[j][4 * t + 1], bf[j][4 * t + 2], bf[j][4 * t + 3]);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a4),
-                                                                  __builtin_bit_cast(bf16x8, b4), acc[i][j], 0, 0, 0);
-            }
-      } else if constexpr (PREC == 1) {
+      if constexpr (PREC == 1) {
         bf16x8 ah[TM][2], bh[TN][2];
 #pragma unroll
         for (int hs = 0; hs < 2; ++hs) {
@@ -1692,7 +1774,8 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT>())) void gemm_gl
 // false: no such instantiation (PREC 2 exists for KC x KC only).
 template <int V>
 using IC = std::integral_constant<int, V>;
-// bm = 64 (64 x 64 tiles) exists for bnt = 64, KC / RC operand pairs and prec 0 / 1 only.
+// bm = 64 (64 x 64 tiles) exists for bnt = 64, KC / RC operand pairs and prec 0 / 1 only;
+// prec 2 (bf16 operands) for the KC / RC pairs with 128-row tiles.
 template <class F>
 bool glds_switch(int ma, int mb, int bnt, int prec, int bm, F&& f) {
   auto tile = [&](auto A, auto B) {
@@ -1704,7 +1787,7 @@ bool glds_switch(int ma, int mb, int bnt, int prec, int bm, F&& f) {
         f(A, B, N, IC<0>{}, R);
       } else if (prec == 1) {
         f(A, B, N, IC<1>{}, R);
-      } else if constexpr (decltype(A)::value == KC && decltype(B)::value == KC && decltype(R)::value == BM) {
+      } else if constexpr (small_ok && decltype(R)::value == BM) {  // bf16 operands: KC / RC pairs
         f(A, B, N, IC<2>{}, R);
       } else {
         return false;

@@ -168,15 +168,86 @@ def profile_gemm_stop(by_shape: bool = False):
     return flops, ms, len(prof)
 
 
+# Reduced-precision mode (esp_set_gemm_compute(1), TrainerOptions.use_amp): the unbatched KC / RC
+# GEMMs (every nn.Linear forward / input / weight gradient) take bf16 operands from HBM
+# (esp_gemm_bf16: PREC 2 LDS-DMA staging, transposing LDS reads for RC operands) after a
+# round-to-nearest-even cast of each operand; the batched attention contractions and the conv2
+# implicit-im2col GEMMs keep fp32 operands rounded to bf16 in LDS staging (PREC 1).  Same
+# numerics either way: bf16-rounded operands, fp32 accumulate and epilogue.
+# ESP_AMP_BF16_OPERANDS=0 keeps every GEMM on PREC 1 (A/B measurements).
+_AMP_BF16_OPERANDS = os.environ.get("ESP_AMP_BF16_OPERANDS", "1") == "1"
+_COMPUTE = [0]  # mirror of esp_get_gemm_compute (set_gemm_compute)
+
+
+# The bf16 copy of a weight gradient's dy (A of dW = dy^T x) is handed to the input-gradient GEMM
+# that every nn.Linear backward runs right after it on the same dy (dx = dy W): linear_bwd_weight
+# leaves it in _DY16 and only the next GEMM launch may take it, when its A is the same region
+# (nothing runs between the two calls at any call site: blocks.py Linear / FFN / attention /
+# convolution-module backward).  Any other launch drops it.
+_DY16 = [None]
+
+
+def _bf16_copy(X, off: int, rows: int, cols: int, ld: int) -> torch.Tensor:
+    """bf16 (RNE) copy of the rows x cols fp32 matrix at X[off] with row pitch ld; the copy's row
+    pitch is cols rounded up to 8 (esp_f32_to_bf16)."""
+    key = (X.data_ptr() + off * 4, rows, cols, ld)
+    memo, _DY16[0] = _DY16[0], None
+    if memo is not None and memo[0] == key:
+        return memo[1], memo[2]
+    ldy = (cols + 7) // 8 * 8
+    out = torch.empty(rows * ldy, dtype=torch.bfloat16, device=X.device)
+    _native.call("esp_f32_to_bf16", _p(X, off), _p(out), rows, cols, ld, ldy, 0, _st())
+    return out, ldy
+
+
+def _gemm_amp_operands(M, N, K, A, B, C, mode_a, lda, mode_b, ldb, ldc, a_off, b_off, c_off, bias, alpha, beta,
+                       R, r_off, act, aux, drop_p, seed, bwd_act, pre, rowsum, keep_a=False):
+    """The bf16-operand form of gemm() (see _AMP_BF16_OPERANDS); False when not applicable."""
+    if K % 8 or (mode_a == RC and M % 8) or (mode_b == RC and N % 8) or K < 64:
+        _DY16[0] = None
+        return False
+    A16, la = _bf16_copy(A, a_off, M, K, lda) if mode_a == KC else _bf16_copy(A, a_off, K, M, lda)
+    B16, lb = _bf16_copy(B, b_off, N, K, ldb) if mode_b == KC else _bf16_copy(B, b_off, K, N, ldb)
+    if keep_a:
+        _DY16[0] = ((A.data_ptr() + a_off * 4, K, M, lda), A16, la)
+    if rowsum is not None:  # the fused bias gradient stays fp32: sum_k A(m, k) of the fp32 operand
+        assert mode_a == RC
+        n = _wsize("esp_colsum", K, M)
+        w = _ws(WS, "esp_colsum", n, C.device)
+        _native.call("esp_colsum", _p(A, a_off), K, M, lda, _p(rowsum), 1, _p(w), n, _st())
+        _guard_post("esp_colsum", w, n)
+    ws = _ws(_GEMM_WS, "esp_gemm_bf16", _GEMM_WS_BYTES, C.device)
+    _native.call("esp_gemm_bf16", mode_a, mode_b, M, N, K, 1, 1, _p(A16), la, 0, 0, _p(B16), lb, 0, 0,
+                 _p(C, c_off), ldc, 0, 0, _p(bias), float(alpha), float(beta), _p(R, r_off or 0), act,
+                 _p(aux, c_off) if aux is not None else None, float(drop_p), seed & 0xFFFFFFFFFFFFFFFF,
+                 int(bwd_act), _p(pre, c_off) if pre is not None else None, _p(ws), _GEMM_WS_BYTES, _st())
+    _guard_post("esp_gemm_bf16", ws, _GEMM_WS_BYTES)
+    return True
+
+
 def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc,
          a_off=0, b_off=0, c_off=0, batch=1, nb2=1, sa=(0, 0), sb=(0, 0), sc=(0, 0),
          bias=None, alpha=1.0, beta=0.0, R=None, r_off=None, act=ACT_NONE, aux=None,
          drop_p=0.0, seed=0, ic_a: Optional[Sequence[int]] = None, ic_b: Optional[Sequence[int]] = None,
-         bwd_act=ACT_NONE, pre=None, rowsum=None):
+         bwd_act=ACT_NONE, pre=None, rowsum=None, _keep_a16=False):
     """C[z](m,n) = alpha*epi(sum_k A(m,k)B(k,n) + bias) + beta*R (see gemm.hip).
     bwd_act/pre: epilogue drop'(.)*act'(pre) (FFN backward); rowsum: += sum_k A(m,k) (bias grad)."""
     if R is not None and r_off is None:
         r_off = c_off
+    if (_COMPUTE[0] == GEMM_BF16 and _AMP_BF16_OPERANDS and batch == 1 and mode_a in (KC, RC)
+            and mode_b in (KC, RC) and ic_a is None and ic_b is None and M > 0 and N > 0):
+        if _PROF is not None:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        if _gemm_amp_operands(M, N, K, A, B, C, mode_a, lda, mode_b, ldb, ldc, a_off, b_off, c_off, bias, alpha,
+                              beta, R, r_off, act, aux, drop_p, seed, bwd_act, pre, rowsum, _keep_a16):
+            if _PROF is not None:
+                ev1.record()
+                extra = 4.0 * M * N * ((R is not None) + (aux is not None) + (pre is not None))
+                _PROF.append((2.0 * M * N * K, ev0, ev1, (mode_a, mode_b, M, N, K, 1, "bf16"), extra))
+            return
+    _DY16[0] = None
     ws = _ws(_GEMM_WS, "esp_gemm_f32", _GEMM_WS_BYTES, C.device)
     ica = (_native.I * 5)(*ic_a) if ic_a is not None else None
     icb = (_native.I * 5)(*ic_b) if ic_b is not None else None
@@ -201,16 +272,17 @@ def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc
 
 
 def gemm_bf16(M: int, N: int, K: int, A16, B16, C, *, lda, ldb, ldc, c_off=0, bias=None, alpha=1.0, beta=0.0,
-              R=None, act=ACT_NONE, aux=None, drop_p=0.0, seed=0, bwd_act=ACT_NONE, pre=None):
-    """C = alpha*epi(A B^T + bias) + beta*R with bf16 operands A [M][K], B [N][K] (torch.bfloat16,
-    K-contiguous) and the fp32 epilogue of gemm() (esp_gemm_bf16)."""
+              R=None, act=ACT_NONE, aux=None, drop_p=0.0, seed=0, bwd_act=ACT_NONE, pre=None, mode_a=KC,
+              mode_b=KC):
+    """C = alpha*epi(sum_k A(m,k) B(k,n) + bias) + beta*R with bf16 operands (torch.bfloat16) in
+    mode KC ([rows][K]) or RC ([K][rows]) and the fp32 epilogue of gemm() (esp_gemm_bf16)."""
     assert A16.dtype == torch.bfloat16 and B16.dtype == torch.bfloat16
     ws = _ws(_GEMM_WS, "esp_gemm_bf16", _GEMM_WS_BYTES, C.device)
     if _PROF is not None:
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         ev0.record()
-    _native.call("esp_gemm_bf16", M, N, K, 1, 1, _p(A16), lda, 0, 0, _p(B16), ldb, 0, 0,
+    _native.call("esp_gemm_bf16", mode_a, mode_b, M, N, K, 1, 1, _p(A16), lda, 0, 0, _p(B16), ldb, 0, 0,
                  _p(C, c_off), ldc, 0, 0, _p(bias), float(alpha), float(beta), _p(R, c_off) if R is not None else None,
                  act, _p(aux, c_off) if aux is not None else None, float(drop_p), seed & 0xFFFFFFFFFFFFFFFF,
                  int(bwd_act), _p(pre, c_off) if pre is not None else None, _p(ws), _GEMM_WS_BYTES, _st())
@@ -218,7 +290,7 @@ def gemm_bf16(M: int, N: int, K: int, A16, B16, C, *, lda, ldb, ldc, c_off=0, bi
     if _PROF is not None:
         ev1.record()
         extra = 4.0 * M * N * ((R is not None) + (aux is not None) + (pre is not None))
-        _PROF.append((2.0 * M * N * K, ev0, ev1, (KC, KC, M, N, K, 1, "bf16"), extra))
+        _PROF.append((2.0 * M * N * K, ev0, ev1, (mode_a, mode_b, M, N, K, 1, "bf16"), extra))
 
 
 def to_bf16(x, rows: int, cols: int, ldx: int, transpose: bool = False, out=None):
@@ -270,7 +342,7 @@ def linear_bwd_weight(dy, x, dW, db=None):
     M, N = dy.shape
     K = x.shape[1]
     gemm(N, K, M, dy, x, dW, mode_a=RC, lda=dy.stride(0), mode_b=RC, ldb=x.stride(0), ldc=dW.stride(0),
-         R=dW, beta=1.0, rowsum=db)
+         R=dW, beta=1.0, rowsum=db, _keep_a16=True)
 
 
 def colsum(x2d, out, accumulate=True, M=None, N=None, ld=None):
@@ -360,6 +432,7 @@ def set_gemm_compute(dtype) -> int:
     prev = lib.esp_set_gemm_compute(int(code))
     if prev < 0:
         raise _native.NativeError(f"esp_set_gemm_compute failed: {lib.esp_last_error().decode()}")
+    _COMPUTE[0] = int(code)
     return prev
 
 

@@ -152,20 +152,87 @@ def test_bf16_trainer_graph_matches_eager(dev):
     assert torch.allclose(me.flat.flat, mg.flat.flat, rtol=0, atol=1e-6)
 
 
+def test_bf16_loss_curve_statistical_gate(dev):
+    """SURVEY §8(d) C5 gate (statistical, the reference's AMP path is fp16 autocast,
+    trainer.py:181-195,554): 50 HIP-graph Trainer steps at the C5 layer shape (d=512, H=8,
+    FF 2048; 2 encoder blocks, 1 decoder block) from the same init on the same 5 cycled batches,
+    bf16 GEMM operands vs the fp32 path.  Gates: every step's loss within 3 % of the fp32 step's,
+    the final losses within 2 %, and both curves descend (last-5 mean < 0.8 x first-5 mean)."""
+    from espnet_slurp_amd.optimizers.fused_adam import FusedAdam
+    from espnet_slurp_amd.train.trainer import Trainer, TrainerOptions
+
+    cfg = O.ModelCfg(vocab_size=64, enc=O.EncCfg(output_size=512, attention_heads=8, linear_units=2048,
+                                                 num_blocks=2, rel_pos_type="latest"),
+                     dec=O.DecCfg(attention_heads=8, linear_units=2048, num_blocks=1), ctc_weight=0.3,
+                     lsm_weight=0.1)
+    batches = [O.synthetic_batch(4, 160, 80, 64, [160, 150, 130, 120], [9, 8, 7, 5], 100 + i) for i in range(5)]
+
+    def curve(amp):
+        model = build_model(cfg, dev, dropout=0.0)
+        load_seeded(model, cfg, 7)
+        model.train()
+        opt = FusedAdam(model.parameters(), model.flat, lr=5e-4)
+        tr = Trainer(model, opt, None, TrainerOptions(grad_clip=5.0, use_amp=amp), cuda_graph=True)
+        out = []
+        for step in range(50):
+            speech, slen, text, tlen = batches[step % 5]
+            st = tr.train_one_step(dict(speech=speech.to(dev), speech_lengths=slen, text=text.clone(),
+                                        text_lengths=tlen))
+            out.append(st["loss"].detach().clone())  # graph-mode stats are rewritten by the next replay
+        return torch.stack([x.reshape(()) for x in out]).double().cpu()
+
+    l32, l16 = curve(False), curve(True)
+    assert torch.isfinite(l16).all() and torch.isfinite(l32).all()
+    rel = ((l16 - l32).abs() / l32.abs()).max().item()
+    assert rel <= 0.03, rel
+    assert abs(l16[-1] - l32[-1]).item() <= 0.02 * abs(l32[-1]).item(), (l16[-1], l32[-1])
+    for c in (l32, l16):
+        assert c[-5:].mean() < 0.8 * c[:5].mean(), c
+
+
 # ------------------------------------------------------------------ bf16-operand GEMM (PREC 2)
-@pytest.mark.parametrize("M,N,Kd", [(300, 200, 136), (11968, 512, 512), (64, 64, 4096), (1000, 1024, 8),
-                                    (257, 130, 520)])
-def test_bf16_operand_gemm(dev, M, N, Kd):
-    """esp_gemm_bf16: bf16 A [M][K] x B [N][K]^T with fp32 accumulate == fp64 GEMM of the same
-    bf16 values up to accumulation order (ragged M / N edges, a K tail inside the last 64-wide
-    slab, split-K for the small-M x N, long-K case)."""
+@pytest.mark.parametrize("M,N,Kd", [(304, 200, 136), (11968, 512, 512), (64, 64, 4096), (1000, 1024, 8),
+                                    (256, 136, 520), (512, 64, 23936), (296, 72, 200)])
+@pytest.mark.parametrize("modes", [(0, 0), (0, 1), (1, 0), (1, 1)])
+def test_bf16_operand_gemm(dev, M, N, Kd, modes):
+    """esp_gemm_bf16: bf16 operands in mode KC ([rows][K]) or RC ([K][rows], transposing LDS
+    reads) with fp32 accumulate == fp64 GEMM of the same bf16 values up to accumulation order
+    (ragged M / N edges, a K tail inside the last 64-wide slab, split-K for the small-M x N,
+    long-K cases: the weight-gradient shape RC x RC).  An RC operand's row count is a multiple of 8
+    (the ABI's contract); tile edges stay ragged (304, 296 rows)."""
+    ma, mb = modes
     A, B = _r(M, Kd, seed=31), _r(N, Kd, seed=32)
-    A16, B16 = A.to(torch.bfloat16).to(dev), B.to(torch.bfloat16).to(dev)
+    A16 = (A if ma == K.KC else A.t().contiguous()).to(torch.bfloat16).to(dev)
+    B16 = (B if mb == K.KC else B.t().contiguous()).to(torch.bfloat16).to(dev)
     C = torch.full((M, N), float("nan"), device=dev)
-    K.gemm_bf16(M, N, Kd, A16, B16, C, lda=Kd, ldb=Kd, ldc=N)
-    ref = A16.double().cpu() @ B16.double().cpu().t()
+    K.gemm_bf16(M, N, Kd, A16, B16, C, lda=Kd if ma == K.KC else M, ldb=Kd if mb == K.KC else N, ldc=N,
+                mode_a=ma, mode_b=mb)
+    a = A.to(torch.bfloat16).double()
+    b = B.to(torch.bfloat16).double()
+    ref = a @ b.t()
     err = (C.cpu().double() - ref).abs().max().item()
     assert err <= 4e-6 * math.sqrt(Kd) * max(1.0, A.abs().max().item() * B.abs().max().item()), err
+
+
+def test_amp_linear_paths_use_bf16_operands(dev):
+    """In the reduced-precision mode an nn.Linear forward / input gradient / weight gradient (with
+    the fused bias gradient) runs on bf16 operands (cast + esp_gemm_bf16) and equals the fp64 result
+    of the bf16-rounded operands; the bias gradient is the fp32 column sum of dy."""
+    M, Din, Dout = 1000, 512, 256
+    x, W, dy = _r(M, Din, seed=51), _r(Dout, Din, seed=52), _r(M, Dout, seed=53)
+    xd, Wd, dyd = x.to(dev), W.to(dev), dy.to(dev)
+    out, dx = torch.empty(M, Dout, device=dev), torch.empty(M, Din, device=dev)
+    dW, db = torch.zeros(Dout, Din, device=dev), torch.zeros(Dout, device=dev)
+    with K.gemm_compute("bf16"):
+        K.linear_fwd(xd, Wd, None, out)
+        K.linear_bwd_data(dyd, Wd, dx)
+        K.linear_bwd_weight(dyd, xd, dW, db)
+    torch.cuda.synchronize()
+    xb, Wb, dyb = _bf(x), _bf(W), _bf(dy)
+    for got, ref, k in ((out, xb @ Wb.t(), Din), (dx, dyb @ Wb, Dout), (dW, dyb.t() @ xb, M)):
+        err = (got.cpu().double() - ref).abs().max().item()
+        assert err <= 4e-6 * math.sqrt(k) * 16, err
+    assert (db.cpu().double() - dy.double().sum(0)).abs().max().item() <= 1e-5 * math.sqrt(M) * 4
 
 
 def test_bf16_operand_gemm_epilogues(dev):
