@@ -177,7 +177,8 @@ def gemm_algorithmic_bytes(shapes) -> float:
             continue
         a = M * Kd * (4 / 9 if ma >= 2 else 1.0)
         b = N * Kd * (4 / 9 if mb >= 2 else 1.0)
-        tot += n * 4.0 * batch * (a + b + M * N) + extra
+        ab = 2.0 if key[6:] == ("bf16",) else 4.0  # bf16-operand GEMMs read 2-byte A and B
+        tot += n * batch * (ab * (a + b) + 4.0 * M * N) + extra
     return tot
 
 
@@ -188,9 +189,10 @@ def measured_gemm_traffic(args) -> dict:
     import glob
     files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
                                           "*_gemm_traffic.json")))
-    for f in reversed(files):  # newest measurement of THIS workload (batch and model shape)
+    for f in reversed(files):  # newest measurement of THIS workload (batch, model shape, precision)
         d = json.load(open(f))
-        if d.get("batch") == args.batch and (args.d, args.layers) == (256, 12) and not args.amp:
+        shape = (d.get("d", 256), d.get("layers", 12), bool(d.get("amp", False)))
+        if d.get("batch") == args.batch and shape == (args.d, args.layers, bool(args.amp)):
             d["source"] = os.path.relpath(f, os.path.dirname(os.path.abspath(__file__)))
             return d
     return {}
@@ -339,9 +341,11 @@ def main():
                          "launches": gemm_launches,
                          "avg_launch_us": round(1e3 * gemm_ms / max(1, gemm_launches), 2)},
             # the second kernel the round-1 verdict named: rel-pos attention probabilities
-            # (MFMA work of its ac + band tiles; P and its dropout copy written once)
+            # (algorithmic ac + bd work, 4 T'^2 d_k per head and utterance, no padded tiles; P and
+            # its dropout copy written once)
             "attention_roofline": None if not attn_launches else {
                 "kernel": "relpos_attn_fwd16_kernel (esp_relpos_attn_probs), HIP events on the same eager replay",
+                "flops_per_launch": round(attn_flops / attn_launches),
                 "launches": attn_launches, "avg_launch_us": round(1e3 * attn_ms / attn_launches, 2),
                 "achieved": round(attn_flops / (attn_ms * 1e-3) / 1e12, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(attn_flops / (attn_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),

@@ -959,6 +959,9 @@ __global__ __launch_bounds__(256, SPLIT == 2 ? 3 : 2) void relpos_attn_fwd16_ker
     ibase[ps] = (uint64_t)(row * T + sc4);
   }
   const bool even_T = (T & 1) == 0;  // uniform
+  // every dropout index of the launch (z*T + i)*T + j below 2^32 (uniform): 32-bit hash inputs,
+  // the same masks (keep_pair32)
+  const bool idx32 = (uint64_t)gridDim.y * (uint64_t)T * (uint64_t)T <= 0xffffffffull;
   auto store_rows = [&](auto drop_c) {
     constexpr bool DROP = decltype(drop_c)::value;
 #pragma unroll
@@ -980,7 +983,10 @@ __global__ __launch_bounds__(256, SPLIT == 2 ? 3 : 2) void relpos_attn_fwd16_ker
             const uint64_t ix = ibase[ps] + 16 * (t0 + t4);
             float4 d;
             bool k0, k1, k2, k3;
-            if (even_T) {  // row * T even: the quad is two hash pairs
+            if (even_T && idx32) {  // row * T even: the quad is two hash pairs
+              esp::keep_pair32(seed, (uint32_t)ix, thr, k0, k1);
+              esp::keep_pair32(seed, (uint32_t)ix + 2, thr, k2, k3);
+            } else if (even_T) {
               esp::keep_pair(seed, ix, thr, k0, k1);
               esp::keep_pair(seed, ix + 2, thr, k2, k3);
             } else {

@@ -78,6 +78,17 @@ __device__ __forceinline__ void keep_pair(uint64_t seed, uint64_t idx_even, uint
   k0 = (h & 0xffffu) >= t;
   k1 = (h >> 16) >= t;
 }
+// the same for indices < 2^32 (the caller's whole index range): rng_u32's high-word fold is 0
+// there, so these draw exactly the masks of keep_pair, on 32-bit index arithmetic
+__device__ __forceinline__ void keep_pair32(uint64_t seed, uint32_t idx_even, uint32_t thresh, bool& k0, bool& k1) {
+  const uint32_t h = mix32(((idx_even >> 1) ^ (uint32_t)seed) + (uint32_t)(seed >> 32)), t = thr16_of(thresh);
+  k0 = (h & 0xffffu) >= t;
+  k1 = (h >> 16) >= t;
+}
+__device__ __forceinline__ bool keep_elem32(uint64_t seed, uint32_t idx, uint32_t thresh) {
+  const uint32_t h = mix32(((idx >> 1) ^ (uint32_t)seed) + (uint32_t)(seed >> 32));
+  return ((idx & 1) ? (h >> 16) : (h & 0xffffu)) >= thr16_of(thresh);
+}
 
 // sigmoid on the hardware exp2 / reciprocal (v_exp_f32, v_rcp_f32, ~1 ulp each) instead of libm
 // expf + an IEEE division (~30-45 VALU per element: the bulk of the FFN w_1 epilogue, 293 vs 210 us

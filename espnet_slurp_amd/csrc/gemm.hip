@@ -301,7 +301,7 @@ ESP_API int esp_gemm_bf16(int mode_a, int mode_b, int M, int N, int K, int batch
                           long sa1, long sa2, const void* B, long ldb, long sb1, long sb2, float* C, long ldc,
                           long sc1, long sc2, const float* bias, float alpha, float beta, const float* R, int act,
                           float* aux, float drop_p, unsigned long long seed, int bwd_act, const float* pre,
-                          float* work, long work_bytes, void* stream) {
+                          float* rowsum, float* work, long work_bytes, void* stream) {
   ESP_ARG_CHECK((mode_a == KC || mode_a == RC) && (mode_b == KC || mode_b == RC),
                 "esp_gemm_bf16: modes must be 0 (KC) or 1 (RC)");
   ESP_ARG_CHECK(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && sa1 % 8 == 0 && sa2 % 8 == 0 && sb1 % 8 == 0 &&
@@ -312,7 +312,7 @@ ESP_API int esp_gemm_bf16(int mode_a, int mode_b, int M, int N, int K, int batch
   // bf16 pairs viewed as fp32 elements by the staging code (PREC 2): K, ld and strides in pairs
   return gemm_run(mode_a, mode_b, M, N, K / 2, batch, nb2, (const float*)A, lda / 2, sa1 / 2, sa2 / 2,
                   (const float*)B, ldb / 2, sb1 / 2, sb2 / 2, C, ldc, sc1, sc2, bias, alpha, beta, R, act, aux, drop_p,
-                  seed, bwd_act, pre, nullptr, nullptr, nullptr, work, work_bytes, stream, 2);
+                  seed, bwd_act, pre, rowsum, nullptr, nullptr, work, work_bytes, stream, 2);
 }
 
 // Rel-pos attention score gradient in one GEMM: dP = dctx V^T per (head, utterance) with the

@@ -10,7 +10,7 @@ bool glds_launch_plain(int ma, int mb, int bnt, int prec, bool rs, dim3 grid, hi
   return glds_switch(ma, mb, bnt, prec, g.bm, [&](auto A, auto B, auto N, auto F, auto R) {
     constexpr int MA = decltype(A)::value, MB = decltype(B)::value, BNT = decltype(N)::value;
     constexpr int BF = decltype(F)::value, BMT = decltype(R)::value;
-    if constexpr (MA == RC && BF != 2) {  // (no fused row sums of packed bf16 operands)
+    if constexpr (MA == RC) {
       if (rs) {
         hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, true, EPI_PLAIN, BF, BMT>), grid, dim3(NT), 0, st, g, x);
         return;

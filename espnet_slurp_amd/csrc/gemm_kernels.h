@@ -1598,7 +1598,6 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT>())) void gemm_gl
     // no LDS zero pass and no extra barrier
     auto compute = [&](const float* cur, int kv) {
       if constexpr (PREC == 2) {
-        static_assert(!RS, "row sums of packed bf16 operands");
         // fragments as 4 chunks of 8 bf16 per tile (k = 32h + 8t + 0..7 for chunk t)
         float4 a4[TM][4], b4[TN][4];
 #pragma unroll
@@ -1643,6 +1642,24 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT>())) void gemm_gl
             for (int j = 0; j < TN; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a4[i][t]),
                                                                   __builtin_bit_cast(bf16x8, b4[j][t]), acc[i][j], 0, 0, 0);
+        if constexpr (RS) {  // fused bias gradient over the bf16 A values (torch AMP's bf16 dy sum)
+          if (do_rs) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+              float a0 = 0.f;
+#pragma unroll
+              for (int t = 0; t < 4; ++t) {
+                const float w[4] = {a4[i][t].x, a4[i][t].y, a4[i][t].z, a4[i][t].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  const uint32_t u = __float_as_uint(w[e]);
+                  a0 += __uint_as_float(u << 16) + __uint_as_float(u & 0xffff0000u);
+                }
+              }
+              rs[i] += a0;
+            }
+          }
+        }
         return;
       }
       float af[TM][16], bf[TN][16];

@@ -16,6 +16,8 @@ from __future__ import annotations
 from typing import Dict, List, Tuple
 
 import torch
+
+from . import kernels as K
 from torch import nn
 
 
@@ -54,6 +56,7 @@ class FlatParams:
             off += _align4(p.numel())
         self.numel = off
         self.flat = torch.zeros(off, dtype=torch.float32, device=device)
+        K.register_param_storage(self.flat)  # bf16 weight copies cached per training step (kernels)
         self.grad = torch.zeros(off, dtype=torch.float32, device=device)
         with torch.no_grad():
             for _, p in self.params:

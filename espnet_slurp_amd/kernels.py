@@ -126,7 +126,7 @@ def h2d(t: torch.Tensor, device) -> torch.Tensor:
 _PROF = None  # when a list: (algorithmic flops, start event, end event) per GEMM launch
 
 
-_PROF_ATTN = None  # when a list: (MFMA flops, bytes written, start event, end event) per attention-probabilities launch
+_PROF_ATTN = None  # when a list: (algorithmic flops, bytes written, start event, end event) per attention-probabilities launch
 
 
 def profile_gemm_start():
@@ -187,6 +187,33 @@ _COMPUTE = [0]  # mirror of esp_get_gemm_compute (set_gemm_compute)
 _DY16 = [None]
 
 
+# Parameter casts: inside param_cast_scope (the Trainer's step: forward + backward, weights
+# constant until the optimizer step that ends it) a weight's bf16 copy is made once and reused by
+# its forward and input-gradient GEMMs.  Parameter storage is registered by FlatParams (weakly:
+# a dead model's range is ignored).
+_W16 = [None]
+_PARAM_RANGES = []
+
+
+def register_param_storage(t: torch.Tensor):
+    import weakref
+    _PARAM_RANGES.append((weakref.ref(t), t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()))
+
+
+class param_cast_scope:
+    def __enter__(self):
+        self.prev = _W16[0]
+        _W16[0] = {}
+        return self
+
+    def __exit__(self, *exc):
+        _W16[0] = self.prev
+
+
+def _is_param(ptr: int, nbytes: int) -> bool:
+    return any(r() is not None and a <= ptr and ptr + nbytes <= b for r, a, b in _PARAM_RANGES)
+
+
 def _bf16_copy(X, off: int, rows: int, cols: int, ld: int) -> torch.Tensor:
     """bf16 (RNE) copy of the rows x cols fp32 matrix at X[off] with row pitch ld; the copy's row
     pitch is cols rounded up to 8 (esp_f32_to_bf16)."""
@@ -194,9 +221,19 @@ def _bf16_copy(X, off: int, rows: int, cols: int, ld: int) -> torch.Tensor:
     memo, _DY16[0] = _DY16[0], None
     if memo is not None and memo[0] == key:
         return memo[1], memo[2]
+    wc = _W16[0]
+    param = wc is not None and _is_param(key[0], ((rows - 1) * ld + cols) * 4)
+    if param:
+        # a copy made outside a HIP-graph capture (the capture's eager warm-up) is never replayed by
+        # the graph: entries are per capture state
+        key = key + (torch.cuda.is_current_stream_capturing(),)
+        if key in wc:
+            return wc[key]
     ldy = (cols + 7) // 8 * 8
     out = torch.empty(rows * ldy, dtype=torch.bfloat16, device=X.device)
     _native.call("esp_f32_to_bf16", _p(X, off), _p(out), rows, cols, ld, ldy, 0, _st())
+    if param:
+        wc[key] = (out, ldy)
     return out, ldy
 
 
@@ -210,18 +247,22 @@ def _gemm_amp_operands(M, N, K, A, B, C, mode_a, lda, mode_b, ldb, ldc, a_off, b
     B16, lb = _bf16_copy(B, b_off, N, K, ldb) if mode_b == KC else _bf16_copy(B, b_off, K, N, ldb)
     if keep_a:
         _DY16[0] = ((A.data_ptr() + a_off * 4, K, M, lda), A16, la)
-    if rowsum is not None:  # the fused bias gradient stays fp32: sum_k A(m, k) of the fp32 operand
-        assert mode_a == RC
-        n = _wsize("esp_colsum", K, M)
-        w = _ws(WS, "esp_colsum", n, C.device)
-        _native.call("esp_colsum", _p(A, a_off), K, M, lda, _p(rowsum), 1, _p(w), n, _st())
-        _guard_post("esp_colsum", w, n)
+    # (a fused bias gradient, rowsum, sums the bf16 A values in fp32: torch AMP's sum of a bf16 dy)
     ws = _ws(_GEMM_WS, "esp_gemm_bf16", _GEMM_WS_BYTES, C.device)
+    if _PROF is not None:  # the GEMM kernel alone (the operand casts are their own kernels)
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
     _native.call("esp_gemm_bf16", mode_a, mode_b, M, N, K, 1, 1, _p(A16), la, 0, 0, _p(B16), lb, 0, 0,
                  _p(C, c_off), ldc, 0, 0, _p(bias), float(alpha), float(beta), _p(R, r_off or 0), act,
                  _p(aux, c_off) if aux is not None else None, float(drop_p), seed & 0xFFFFFFFFFFFFFFFF,
-                 int(bwd_act), _p(pre, c_off) if pre is not None else None, _p(ws), _GEMM_WS_BYTES, _st())
+                 int(bwd_act), _p(pre, c_off) if pre is not None else None, _p(rowsum), _p(ws), _GEMM_WS_BYTES,
+                 _st())
     _guard_post("esp_gemm_bf16", ws, _GEMM_WS_BYTES)
+    if _PROF is not None:
+        ev1.record()
+        extra = 4.0 * M * N * ((R is not None) + (aux is not None) + (pre is not None))
+        _PROF.append((2.0 * M * N * K, ev0, ev1, (mode_a, mode_b, M, N, K, 1, "bf16"), extra))
     return True
 
 
@@ -236,16 +277,8 @@ def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc
         r_off = c_off
     if (_COMPUTE[0] == GEMM_BF16 and _AMP_BF16_OPERANDS and batch == 1 and mode_a in (KC, RC)
             and mode_b in (KC, RC) and ic_a is None and ic_b is None and M > 0 and N > 0):
-        if _PROF is not None:
-            ev0 = torch.cuda.Event(enable_timing=True)
-            ev1 = torch.cuda.Event(enable_timing=True)
-            ev0.record()
         if _gemm_amp_operands(M, N, K, A, B, C, mode_a, lda, mode_b, ldb, ldc, a_off, b_off, c_off, bias, alpha,
                               beta, R, r_off, act, aux, drop_p, seed, bwd_act, pre, rowsum, _keep_a16):
-            if _PROF is not None:
-                ev1.record()
-                extra = 4.0 * M * N * ((R is not None) + (aux is not None) + (pre is not None))
-                _PROF.append((2.0 * M * N * K, ev0, ev1, (mode_a, mode_b, M, N, K, 1, "bf16"), extra))
             return
     _DY16[0] = None
     ws = _ws(_GEMM_WS, "esp_gemm_f32", _GEMM_WS_BYTES, C.device)
@@ -285,7 +318,7 @@ def gemm_bf16(M: int, N: int, K: int, A16, B16, C, *, lda, ldb, ldc, c_off=0, bi
     _native.call("esp_gemm_bf16", mode_a, mode_b, M, N, K, 1, 1, _p(A16), lda, 0, 0, _p(B16), ldb, 0, 0,
                  _p(C, c_off), ldc, 0, 0, _p(bias), float(alpha), float(beta), _p(R, c_off) if R is not None else None,
                  act, _p(aux, c_off) if aux is not None else None, float(drop_p), seed & 0xFFFFFFFFFFFFFFFF,
-                 int(bwd_act), _p(pre, c_off) if pre is not None else None, _p(ws), _GEMM_WS_BYTES, _st())
+                 int(bwd_act), _p(pre, c_off) if pre is not None else None, None, _p(ws), _GEMM_WS_BYTES, _st())
     _guard_post("esp_gemm_bf16", ws, _GEMM_WS_BYTES)
     if _PROF is not None:
         ev1.record()
@@ -593,9 +626,9 @@ def relpos_attn_probs(q_u, q_v, kmat, ldk, p, ldp_row, relpos, nb, H, sqrt_dk, k
                  _p(tvalid), _st())
     if _PROF_ATTN is not None:
         ev1.record()
-        nt = (T + 15) // 16
-        # per (z, 16-row group): ac over nt key tiles + nt+1 band blocks, 16 x 16 x 64 MACs each
-        flops = 2.0 * 16 * 16 * 64 * (2 * nt + 1) * nt * nb * H
+        # algorithmic: per (head, utterance) ac = q_u k^T and the T' rel-pos (bd) columns each row
+        # keeps after rel_shift, 2 * T'^2 * d_k each (no padded tiles)
+        flops = 4.0 * T * T * 64 * nb * H
         written = 4.0 * nb * H * T * T * (2 if (pdrop is not None and drop_p > 0) else 1)
         _PROF_ATTN.append((flops, written, ev0, ev1))
 

@@ -108,7 +108,7 @@ class Trainer:
 
     def train_one_step(self, batch: Dict[str, torch.Tensor], check_finite: bool = True) -> Dict[str, torch.Tensor]:
         """One iteration of train_one_epoch's loop body; returns device-side stats."""
-        with K.gemm_compute("bf16" if self.options.use_amp else "fp32"):
+        with K.gemm_compute("bf16" if self.options.use_amp else "fp32"), K.param_cast_scope():
             stats = self._train_one_step(batch, check_finite)
         if K.GUARD:  # ESP_GUARD=1: workspace canaries checked after every step (syncs)
             K.check_guards()

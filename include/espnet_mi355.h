@@ -70,13 +70,14 @@ int esp_set_splitk_mode(int mode);
  * torch.bfloat16) in mode KC or RC as esp_gemm_f32 (KC: [rows][K]; RC: [K][rows], staged for
  * transposing LDS reads), fp32 accumulate; C, the epilogue (bias, act, aux, dropout, bwd_act /
  * pre, residual) and split-K exactly as esp_gemm_f32.  K, lda, ldb and the batch strides in bf16
- * elements, multiples of 8; A, B 16-B aligned; an RC operand's row count a multiple of 8.  The
+ * elements, multiples of 8; A, B 16-B aligned; an RC operand's row count a multiple of 8.
+ * rowsum != NULL (mode_a RC, batch 1): rowsum[m] += sum_k A(m,k) in fp32 over the bf16 values.  The
  * operands come from esp_f32_to_bf16 (activations, gradients) or bf16 weight copies. */
 int esp_gemm_bf16(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2, const void* A, long lda,
                   long sa1, long sa2, const void* B, long ldb, long sb1, long sb2, float* C, long ldc,
                   long sc1, long sc2, const float* bias, float alpha, float beta, const float* R, int act,
-                  float* aux, float drop_p, unsigned long long seed, int bwd_act, const float* pre, float* work,
-                  long work_bytes, void* stream);
+                  float* aux, float drop_p, unsigned long long seed, int bwd_act, const float* pre, float* rowsum,
+                  float* work, long work_bytes, void* stream);
 /* y = bf16(x) (round to nearest even) for a rows x cols fp32 matrix (row pitch ldx); transpose:
  * y[c * ldy + r] (a cols x rows bf16 matrix), else y[r * ldy + c]. */
 int esp_f32_to_bf16(const float* x, void* y, long rows, int cols, long ldx, long ldy, int transpose,

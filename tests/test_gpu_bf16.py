@@ -217,7 +217,8 @@ def test_bf16_operand_gemm(dev, M, N, Kd, modes):
 def test_amp_linear_paths_use_bf16_operands(dev):
     """In the reduced-precision mode an nn.Linear forward / input gradient / weight gradient (with
     the fused bias gradient) runs on bf16 operands (cast + esp_gemm_bf16) and equals the fp64 result
-    of the bf16-rounded operands; the bias gradient is the fp32 column sum of dy."""
+    of the bf16-rounded operands; the fused bias gradient is the fp32 sum of the bf16-rounded dy (as
+    torch AMP sums a bf16 grad_output)."""
     M, Din, Dout = 1000, 512, 256
     x, W, dy = _r(M, Din, seed=51), _r(Dout, Din, seed=52), _r(M, Dout, seed=53)
     xd, Wd, dyd = x.to(dev), W.to(dev), dy.to(dev)
@@ -232,7 +233,7 @@ def test_amp_linear_paths_use_bf16_operands(dev):
     for got, ref, k in ((out, xb @ Wb.t(), Din), (dx, dyb @ Wb, Dout), (dW, dyb.t() @ xb, M)):
         err = (got.cpu().double() - ref).abs().max().item()
         assert err <= 4e-6 * math.sqrt(k) * 16, err
-    assert (db.cpu().double() - dy.double().sum(0)).abs().max().item() <= 1e-5 * math.sqrt(M) * 4
+    assert (db.cpu().double() - dyb.sum(0)).abs().max().item() <= 1e-5 * math.sqrt(M) * 4
 
 
 def test_bf16_operand_gemm_epilogues(dev):

@@ -28,7 +28,7 @@ def per_dispatch(d, counter):
 def main():
     fetch = per_dispatch(sys.argv[1], "FETCH_SIZE")
     write = per_dispatch(sys.argv[2], "WRITE_SIZE")
-    fam = "gemm_glds_kernel"
+    fam = "gemm_glds_kernel"  # the fp32 / bf16-in-LDS and the bf16-operand GEMMs are all this template
     fk = [v for n, v in fetch.values() if fam in n]
     wk = [v for n, v in write.values() if fam in n]
     fetch_b = 2.0 * 1024 * sum(fk) / len(fk)
@@ -40,8 +40,11 @@ def main():
         "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate runs of bench.py --eager --steps 1 "
                   "--warmup 1; FETCH_SIZE x2 (gfx950 wide-read undercount), KB x1024",
     }
-    if len(sys.argv) > 3:  # the workload the passes ran (bench.py matches on it)
+    if len(sys.argv) > 3:  # the workload the passes ran (bench.py matches on batch, d, layers, amp)
         out.update(batch=int(sys.argv[3]), workload=sys.argv[4] if len(sys.argv) > 4 else "C2 d=256 12L")
+    if len(sys.argv) > 5:
+        d, layers, amp = sys.argv[5].split(",")
+        out.update(d=int(d), layers=int(layers), amp=amp == "1")
     print(json.dumps(out, indent=1))
 
 
