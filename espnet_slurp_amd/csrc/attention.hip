@@ -874,11 +874,18 @@ __global__ __launch_bounds__(256, SPLIT == 2 ? 3 : 2) void relpos_attn_fwd16_ker
       put_band(ring0, t + 1, s);
       asm volatile("" ::: "memory");  // ring writes before the shifted reads (LDS is in order per wave)
       const int j = t * 16 + li;
+      // the four shifted band reads first, then their uses: one LDS round trip per tile (reads
+      // interleaved with their uses cost a round trip each, `s_waitcnt lgkmcnt(0)` after every read)
+      float bdv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ii = 4 * q4 + r;
+        bdv[r] = ring0[ii * RW_PITCH + ((t * 16 + li - ii + 15) & 31)];
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int ii = 4 * q4 + r, i = i0 + ii;
-        const int at = ii * RW_PITCH + ((t * 16 + li - ii + 15) & 31);
-        float bd = ring0[at];
+        float bd = bdv[r];
         if (LEGACY && j == i + 1) bd = 0.f;
         const float sv = a[r] + bd;
         sc[tt][r] = j < kl ? (P2 ? sv * inv_sqrt_dk : sv / sqrt_dk) : -INFINITY;

@@ -176,6 +176,8 @@ def profile_gemm_stop(by_shape: bool = False):
 # numerics either way: bf16-rounded operands, fp32 accumulate and epilogue.
 # ESP_AMP_BF16_OPERANDS=0 keeps every GEMM on PREC 1 (A/B measurements).
 _AMP_BF16_OPERANDS = os.environ.get("ESP_AMP_BF16_OPERANDS", "1") == "1"
+# a Linear input's forward bf16 copy is kept for its weight gradient (_bf16_copy roles)
+_KEEP_X16 = os.environ.get("ESP_KEEP_X16", "1") == "1"
 _COMPUTE = [0]  # mirror of esp_get_gemm_compute (set_gemm_compute)
 
 
@@ -187,10 +189,11 @@ _COMPUTE = [0]  # mirror of esp_get_gemm_compute (set_gemm_compute)
 _DY16 = [None]
 
 
-# Parameter casts: inside param_cast_scope (the Trainer's step: forward + backward, weights
+# Step-scoped casts: inside param_cast_scope (the Trainer's step: forward + backward, weights
 # constant until the optimizer step that ends it) a weight's bf16 copy is made once and reused by
-# its forward and input-gradient GEMMs.  Parameter storage is registered by FlatParams (weakly:
-# a dead model's range is ignored).
+# its forward and input-gradient GEMMs, and a Linear input's forward copy by its weight gradient
+# (_bf16_copy roles).  Parameter storage is registered by FlatParams (weakly: a dead model's range
+# is ignored).
 _W16 = [None]
 _PARAM_RANGES = []
 
@@ -214,26 +217,33 @@ def _is_param(ptr: int, nbytes: int) -> bool:
     return any(r() is not None and a <= ptr and ptr + nbytes <= b for r, a, b in _PARAM_RANGES)
 
 
-def _bf16_copy(X, off: int, rows: int, cols: int, ld: int) -> torch.Tensor:
+def _bf16_copy(X, off: int, rows: int, cols: int, ld: int, role: str = "") -> torch.Tensor:
     """bf16 (RNE) copy of the rows x cols fp32 matrix at X[off] with row pitch ld; the copy's row
-    pitch is cols rounded up to 8 (esp_f32_to_bf16)."""
+    pitch is cols rounded up to 8 (esp_f32_to_bf16).  role "a_kc": the A operand of a KC GEMM (in
+    the forward: a Linear's input x), kept for the step; role "b_rc": the B operand of an RC GEMM
+    (a weight gradient's x), which takes the forward's copy of the same region.  Kept copies hold
+    a reference to their fp32 source, so its memory cannot be handed to another tensor while the
+    copy can be found; a Linear's input is never written between its forward and its weight
+    gradient (the fp32 path reads it there too)."""
     key = (X.data_ptr() + off * 4, rows, cols, ld)
     memo, _DY16[0] = _DY16[0], None
     if memo is not None and memo[0] == key:
         return memo[1], memo[2]
     wc = _W16[0]
-    param = wc is not None and _is_param(key[0], ((rows - 1) * ld + cols) * 4)
-    if param:
+    if wc is not None:
         # a copy made outside a HIP-graph capture (the capture's eager warm-up) is never replayed by
         # the graph: entries are per capture state
-        key = key + (torch.cuda.is_current_stream_capturing(),)
-        if key in wc:
-            return wc[key]
+        ckey = key + (torch.cuda.is_current_stream_capturing(),)
+        param = _is_param(key[0], ((rows - 1) * ld + cols) * 4)
+        if param or role == "b_rc":
+            hit = wc.get(ckey)
+            if hit is not None:
+                return hit[0], hit[1]
     ldy = (cols + 7) // 8 * 8
     out = torch.empty(rows * ldy, dtype=torch.bfloat16, device=X.device)
     _native.call("esp_f32_to_bf16", _p(X, off), _p(out), rows, cols, ld, ldy, 0, _st())
-    if param:
-        wc[key] = (out, ldy)
+    if wc is not None and (param or (role == "a_kc" and _KEEP_X16)):
+        wc[ckey] = (out, ldy, X)
     return out, ldy
 
 
@@ -243,8 +253,8 @@ def _gemm_amp_operands(M, N, K, A, B, C, mode_a, lda, mode_b, ldb, ldc, a_off, b
     if K % 8 or (mode_a == RC and M % 8) or (mode_b == RC and N % 8) or K < 64:
         _DY16[0] = None
         return False
-    A16, la = _bf16_copy(A, a_off, M, K, lda) if mode_a == KC else _bf16_copy(A, a_off, K, M, lda)
-    B16, lb = _bf16_copy(B, b_off, N, K, ldb) if mode_b == KC else _bf16_copy(B, b_off, K, N, ldb)
+    A16, la = _bf16_copy(A, a_off, M, K, lda, "a_kc") if mode_a == KC else _bf16_copy(A, a_off, K, M, lda)
+    B16, lb = _bf16_copy(B, b_off, N, K, ldb) if mode_b == KC else _bf16_copy(B, b_off, K, N, ldb, "b_rc")
     if keep_a:
         _DY16[0] = ((A.data_ptr() + a_off * 4, K, M, lda), A16, la)
     # (a fused bias gradient, rowsum, sums the bf16 A values in fp32: torch AMP's sum of a bf16 dy)

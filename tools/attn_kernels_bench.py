@@ -2,7 +2,7 @@
 (default 128): the probabilities kernel, the P.V and dS.K batched GEMMs and the softmax /
 rel_shift adjoint.  Used alone for timings and under rocprofv3 --pmc for per-kernel counters.
 
-    python tools/attn_kernels_bench.py [B] [--only probs|pv|sbwd|dsk] [--legacy]
+    python tools/attn_kernels_bench.py [B] [--only probs|pv|sbwd|dsk] [--legacy] [--nodrop]
 """
 import os
 import sys
@@ -53,6 +53,10 @@ def main():
     K.relpos_attn_probs(qu, qv, qkv, 3 * D, p, D, rel, B, H, 8.0, klen, attn, pdrop, pa, 1, T, Tp, k_off=D)
     nt = (T + 15) // 16
     res = {}
+    if "--nodrop" in sys.argv:  # the probabilities kernel without dropout and without the P_drop copy
+        us = timed(lambda: K.relpos_attn_probs(qu, qv, qkv, 3 * D, p, D, rel, B, H, 8.0, klen, attn, None, 0.0, 1, T,
+                                               Tp, k_off=D))
+        res["probs0"] = (us, f"{2.0 * Z * T * T * dk * 2 / us / 1e6:.1f} TF/s algorithmic, no dropout / no P_drop")
     if only in (None, "probs"):
         us = timed(lambda: K.relpos_attn_probs(qu, qv, qkv, 3 * D, p, D, rel, B, H, 8.0, klen, attn, pdrop, pa, 1, T,
                                                Tp, k_off=D))
