@@ -304,7 +304,12 @@ def main():
         fwd, train = conformer_flops_per_utt(args.d, args.heads, args.ff, args.layers, 2048, 6, args.vocab)
         value = world * args.batch * args.steps / elapsed
         achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
-        peak = BF16_MFMA_PEAK_TFLOPS if args.amp else FP32_MFMA_PEAK_TFLOPS
+        # fp32 GEMMs of a split build (esp_f32_gemm_products() == 6) issue six bf16 MFMA products
+        # per fp32 product: their ceiling is the bf16 MFMA peak / 6
+        from espnet_slurp_amd import _native
+        f32_products = _native.load().esp_f32_gemm_products()
+        peak = BF16_MFMA_PEAK_TFLOPS if args.amp else (
+            round(BF16_MFMA_PEAK_TFLOPS / 6, 2) if f32_products == 6 else FP32_MFMA_PEAK_TFLOPS)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args)
@@ -320,6 +325,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16-mfma/f32-accumulate" if args.amp else "f32",
+            "f32_gemm": None if args.amp else (
+                "bf16x6 split products on v_mfma_f32_32x32x16_bf16, fp32 accumulate (fp32-accurate: "
+                "profiles/r03h_f32_gemm_accuracy.txt)" if f32_products == 6 else "v_mfma_f32_32x32x2_f32"),
             "data": "synthetic (N(0,1) fbank, random tokens U[20,40], random-init weights)",
             "launch": "eager" if args.eager else "hip_graph",
             "graphs_captured": len(trainer._graphs) if not args.eager else 0,
@@ -332,8 +340,9 @@ def main():
                        "global_batch": world * args.batch, "seq_len": 1500, "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                          "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                         "traffic": None if args.amp else traffic.get("hbm_bytes_per_launch"),
-                         "traffic_source": None if args.amp else traffic.get("source"),
+                         "f32_mfma_peak_frac": None if args.amp else round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
+                         "traffic": traffic.get("hbm_bytes_per_launch"),
+                         "traffic_source": traffic.get("source"),
                          "algorithmic_bytes_per_launch": round(gemm_algorithmic_bytes(gemm_shapes) / max(1, gemm_launches)),
                          "kernel": ("gemm_glds_kernel<BF16> (bf16 MFMA)" if args.amp else "gemm_glds_kernel")
                                    + " family (all MFMA GEMM launches of one step, HIP events"

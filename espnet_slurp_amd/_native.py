@@ -10,7 +10,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libespnet_mi355.so")
+# ESP_LIB_VARIANT=_x: an experiment build of the same sources (make VARIANT=_x EXTRA=-D...), for
+# A/B runs on one box
+LIB_PATH = os.path.join(_HERE, "libespnet_mi355%s.so" % os.environ.get("ESP_LIB_VARIANT", ""))
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -29,6 +31,7 @@ SIGNATURES = {
                      P, P, P, L, P],
     "esp_set_gemm_compute": [I],
     "esp_get_gemm_compute": [],
+    "esp_f32_gemm_products": [],
     "esp_set_splitk_mode": [I],
     "esp_act_bwd": [P, P, P, L, I, F, U64, L, P],
     "esp_scale_dropout": [P, P, L, F, F, U64, P, F, P],
@@ -98,9 +101,10 @@ SIGNATURES = {
     "esp_relpos_dp_workspace_bytes": [I, I, I],
 }
 _RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I, "esp_set_gemm_compute": I,
-             "esp_get_gemm_compute": I, "esp_set_splitk_mode": I}
+             "esp_get_gemm_compute": I, "esp_set_splitk_mode": I,
+             "esp_f32_gemm_products": I}
 _RESTYPES.update({k: L for k in SIGNATURES if k.endswith("_workspace_bytes")})
-ABI_VERSION = 23  # bumped whenever a signature in include/espnet_mi355.h changes
+ABI_VERSION = 24  # bumped whenever a signature in include/espnet_mi355.h changes
 
 _lib = None
 

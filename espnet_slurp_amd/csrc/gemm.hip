@@ -269,6 +269,7 @@ ESP_API int esp_set_gemm_compute(int dtype) {
   return prev;
 }
 ESP_API int esp_get_gemm_compute(void) { return g_compute; }
+ESP_API int esp_f32_gemm_products(void) { return ESP_F32_SPLIT ? 6 : 1; }
 ESP_API int esp_set_splitk_mode(int mode) {
   ESP_ARG_CHECK(mode == 0 || mode == 1, "esp_set_splitk_mode: mode must be 0 or 1, got %d", mode);
   const int prev = splitk_mode();

@@ -35,6 +35,13 @@ constexpr int BM = 128, BN = 128, BK = 32, NT = 256;  // BK: split-K granularity
 // the caller before first use; every launch leaves them zero), one int per output tile
 #define ESP_GEMM_TICKET_BYTES 65536L
 #define ESP_GEMM_TICKETS 16384L
+// 1 (default): the fp32 GEMMs (PREC 0) of the LDS-DMA kernel run as bf16x6 split products on
+// the bf16 MFMA (split3_bf16; measured as accurate as the f32 MFMA against fp64,
+// profiles/r03h_f32_gemm_accuracy.txt); 0: v_mfma_f32_32x32x2_f32 (make VARIANT=_f32
+// EXTRA=-DESP_F32_SPLIT=0 builds libespnet_mi355_f32.so for A/B runs)
+#ifndef ESP_F32_SPLIT
+#define ESP_F32_SPLIT 1
+#endif
 
 enum Mode { KC = 0, RC = 1, I2C_KC = 2, I2C_RC = 3, I2CT_KC = 4 };
 enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_SWISH = 2, ACT_MUL = 3 /* bwd_act only: v *= pre */ };
@@ -1519,6 +1526,21 @@ constexpr int glds_occupancy() {
 // for A and B, so the four steps cover the slab's 64 k once).  No conversion in the k-loop.
 // BMT = 64 (with BNT = 64): 64 x 64 tiles, 2 x 2 waves of one 32 x 32 MFMA tile each, for the
 // grids that 128-row tiles leave under-filled (decoder M ~ 5k tokens, 41-query source attention).
+// fp32 operand split for the emulated fp32 MFMA (ESP_F32_SPLIT): v = hi + mid + lo exactly, each a
+// bf16 (round-to-nearest-even at every step, so |mid| <= 2^-8 |v| and |lo| <= 2^-16 |v|; the two
+// residuals are exact fp32 differences).
+__device__ __forceinline__ void split3_bf16(const float* v, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const __bf16 h = (__bf16)v[e];
+    const float r = v[e] - (float)h;
+    const __bf16 m = (__bf16)r;
+    hi[e] = h;
+    mid[e] = m;
+    lo[e] = (__bf16)(r - (float)m);
+  }
+}
+
 template <int MA, int MB, int BNT, bool RS, int EPI, int PREC = 0, int BMT = BM>
 __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT>())) void gemm_glds_kernel(GemmArgs g, GldsArgs x) {
   constexpr int WN = BMT == 64 ? 2 : BNT / 64, WM = 4 / WN, TM = BMT / (WM * 32), TN = BNT / (WN * 32);
@@ -1693,6 +1715,29 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT>())) void gemm_gl
 #pragma unroll
             for (int j = 0; j < TN; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][hs], bh[j][hs], acc[i][j], 0, 0, 0);
+      } else if constexpr (PREC == 0 && ESP_F32_SPLIT) {
+        // fp32 product emulated on the bf16 MFMA: the six split products down to 2^-16 relative
+        // (hi.hi, hi.mid, mid.hi, hi.lo, lo.hi, mid.mid), smallest first into the fp32 accumulator;
+        // the dropped mid.lo + lo.mid + lo.lo are <= 2^-23 of |a b| (k order as in PREC 1)
+#pragma unroll
+        for (int hs = 0; hs < 2; ++hs) {
+          bf16x8 ah[TM][3], bh[TN][3];
+#pragma unroll
+          for (int i = 0; i < TM; ++i) split3_bf16(&af[i][8 * hs], ah[i][0], ah[i][1], ah[i][2]);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) split3_bf16(&bf[j][8 * hs], bh[j][0], bh[j][1], bh[j][2]);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][1], bh[j][1], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][2], bh[j][0], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][2], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][1], bh[j][0], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][1], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][0], acc[i][j], 0, 0, 0);
+            }
+        }
       } else {
 #pragma unroll
         for (int s = 0; s < 16; ++s)

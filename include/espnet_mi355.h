@@ -61,6 +61,12 @@ int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2
  * knob is `use_amp` (fp16 autocast, trainer.py:181-195,554).  Returns the previous value. */
 int esp_set_gemm_compute(int dtype);
 int esp_get_gemm_compute(void);
+/* How the fp32 compute type (0) multiplies in the LDS-DMA GEMM kernel of this build: 6 = each
+ * fp32 operand split exactly into three bf16 (hi + mid + lo, round-to-nearest-even residuals)
+ * and the six products down to 2^-16 relative (hi.hi, hi.mid, mid.hi, hi.lo, lo.hi, mid.mid)
+ * accumulated in fp32 on v_mfma_f32_32x32x16_bf16 (the dropped terms are <= 2^-23 |a b|, below
+ * an fp32 rounding of the sum); 1 = v_mfma_f32_32x32x2_f32 (build flag ESP_F32_SPLIT=0). */
+int esp_f32_gemm_products(void);
 /* Split-K combine of every later esp_gemm_f32 launch (process-wide): 0 = a separate
  * fixed-order reduction launch (default), 1 = in-kernel (the last-arriving unit of each output
  * tile sums the splits in fixed order; needs the zeroed ticket area of `work`, see above).

@@ -77,6 +77,50 @@ def test_gemm_lds_dma_paths(dev, shape, modes):
     assert err <= 1e-5 * max(1.0, math.sqrt(Kk)) * 4, err
 
 
+@pytest.mark.parametrize("shape", [(2048, 1024, 256), (1024, 256, 2304), (256, 512, 47872)])
+@pytest.mark.parametrize("modes", [(0, 0), (0, 1), (1, 1)])
+def test_gemm_f32_accuracy_vs_fp64(dev, shape, modes):
+    """The fp32 GEMM (bf16x6 split products in the default build, esp_f32_gemm_products) is as
+    accurate as an fp32 GEMM: error / (|A| |B|) against fp64 within 2x (max) and 4x (rms) of the
+    CPU's own fp32 matmul on the same operands (measured ratios <= 1 and <= 2.8,
+    profiles/r03h_f32_gemm_accuracy.txt)."""
+    M, N, Kk = shape
+    ma, mb = modes
+    g = torch.Generator().manual_seed(Kk + M)
+    A = torch.randn(M, Kk, generator=g)
+    B = torch.randn(Kk, N, generator=g)
+    Ad = (A if ma == K.KC else A.t().contiguous()).to(dev)
+    Bd = (B.t().contiguous() if mb == K.KC else B).to(dev)
+    C = torch.empty(M, N, device=dev)
+    K.gemm(M, N, Kk, Ad, Bd, C, mode_a=ma, lda=Ad.stride(0), mode_b=mb, ldb=Bd.stride(0), ldc=N)
+    torch.cuda.synchronize()
+    ref = A.double() @ B.double()
+    den = A.double().abs() @ B.double().abs()
+    r = (C.cpu().double() - ref).abs() / den
+    r32 = ((A @ B).double() - ref).abs() / den
+    assert r.max().item() <= 2.0 * r32.max().item(), (r.max().item(), r32.max().item())
+    assert r.pow(2).mean().sqrt().item() <= 4.0 * r32.pow(2).mean().sqrt().item()
+
+
+def test_gemm_f32_nonfinite_operands(dev):
+    """A NaN or inf operand element makes its output row non-finite (the split of inf is NaN in
+    the bf16x6 build, inf on the f32 MFMA): the Trainer's finite check sees both."""
+    M, N, Kk = 64, 64, 96
+    A = _r(M, Kk, seed=3)
+    B = _r(N, Kk, seed=4)
+    A[5, 7] = float("nan")
+    A[9, 70] = float("inf")
+    Ad, Bd = A.to(dev), B.to(dev)
+    C = torch.empty(M, N, device=dev)
+    K.gemm(M, N, Kk, Ad, Bd, C, mode_a=K.KC, lda=Kk, mode_b=K.KC, ldb=Kk, ldc=N)
+    Cc = C.cpu()
+    assert not torch.isfinite(Cc[5]).any() and not torch.isfinite(Cc[9]).any()
+    others = torch.ones(M, dtype=torch.bool)
+    others[[5, 9]] = False
+    ref = (A[others].double() @ B.double().t())
+    assert (Cc[others].double() - ref).abs().max().item() < 1e-4
+
+
 def test_gemm_epilogue(dev):
     M, N, Kk = 257, 130, 64
     X, W, b = _r(M, Kk, seed=3), _r(N, Kk, seed=4), _r(N, seed=5)
