@@ -415,9 +415,15 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
   if (variant() == 4 && g.a.glds && g.b.glds && K > 0) {
     // per-CU time model: ceil(tiles / CUs) tiles of bn/64 units each, x1.3 when the grid
     // leaves CUs with a single resident block (one wave per SIMD); ties keep 128 (intensity)
+    // fp32 on split products (ESP_F32_SPLIT): a 64-wide tile costs ~3/4 of a 128-wide one (its
+    // waves split 1.5x the operand values per MFMA), and a grid that split-K will refill is
+    // priced by its total work (the K ~ 48k weight gradients: 3.8 vs 4.9 ms on 128-wide tiles)
+    const bool split_f32 = ESP_F32_SPLIT && g.bf16 == 0;
     auto cost = [&](int bn) {
       const long t = ntiles(bn);
-      double c = (double)((t + 255) / 256) * (bn / 64);
+      const double per = split_f32 && bn == 64 ? 1.5 : bn / 64;
+      if (split_f32 && work && t < target && K >= 2 * 128) return (double)t * per / 256.0;
+      double c = (double)((t + 255) / 256) * per;
       if (t < 2 * 256) c *= 1.3;
       return c;
     };
