@@ -58,8 +58,8 @@ def main():
     torch.cuda.init()
     for M, N, Kk, ma, mb in [(47872, 1024, 256, 0, 0), (47872, 256, 1024, 0, 0), (47872, 1024, 256, 0, 1),
                              (47872, 256, 1024, 0, 1), (4096, 4096, 4096, 0, 0), (4096, 4096, 4096, 1, 1),
-                             (4096, 4096, 4096, 0, 1), (4096, 4096, 4096, 1, 0), (1000, 300, 77, 0, 0),
-                             (1000, 300, 77, 1, 1), (130, 260, 45, 0, 1), (130, 260, 45, 1, 0)]:
+                             (4096, 4096, 4096, 0, 1), (4096, 4096, 4096, 1, 0), (1000, 300, 80, 0, 0),
+                             (1000, 300, 80, 1, 1), (132, 260, 48, 0, 1), (132, 260, 48, 1, 0), (47872, 512, 256, 0, 0), (1024, 256, 47872, 1, 1)]:
         case(M, N, Kk, ma, mb)
 
 
