@@ -1529,16 +1529,28 @@ constexpr int glds_occupancy() {
 // fp32 operand split for the emulated fp32 MFMA (ESP_F32_SPLIT): v = hi + mid + lo exactly, each a
 // bf16 (round-to-nearest-even at every step, so |mid| <= 2^-8 |v| and |lo| <= 2^-16 |v|; the two
 // residuals are exact fp32 differences).
+// Pairwise: one v_cvt_pk_bf16_f32 per part and pair, the parts' fp32 values taken back from the
+// packed bits (<< 16, & 0xffff0000): 11 VALU per pair.
+// (per element, hipcc converted each value twice: 12-13 VALU per pair; 1249.7 vs 1241.7 utt/s,
+// profiles/r03i_abc_split_code.txt)
 __device__ __forceinline__ void split3_bf16(const float* v, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+  typedef __attribute__((ext_vector_type(2))) float f2;
+  typedef __attribute__((ext_vector_type(2))) __bf16 b2;
+  uint32_t H[4], Md[4], L[4];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const __bf16 h = (__bf16)v[e];
-    const float r = v[e] - (float)h;
-    const __bf16 m = (__bf16)r;
-    hi[e] = h;
-    mid[e] = m;
-    lo[e] = (__bf16)(r - (float)m);
+  for (int p = 0; p < 4; ++p) {
+    const float a = v[2 * p], b = v[2 * p + 1];
+    const uint32_t hp = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){a, b}, b2));
+    const float ra = a - __uint_as_float(hp << 16), rb = b - __uint_as_float(hp & 0xffff0000u);
+    const uint32_t mp = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){ra, rb}, b2));
+    const float sa = ra - __uint_as_float(mp << 16), sb = rb - __uint_as_float(mp & 0xffff0000u);
+    H[p] = hp;
+    Md[p] = mp;
+    L[p] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){sa, sb}, b2));
   }
+  hi = __builtin_bit_cast(bf16x8, make_uint4(H[0], H[1], H[2], H[3]));
+  mid = __builtin_bit_cast(bf16x8, make_uint4(Md[0], Md[1], Md[2], Md[3]));
+  lo = __builtin_bit_cast(bf16x8, make_uint4(L[0], L[1], L[2], L[3]));
 }
 
 template <int MA, int MB, int BNT, bool RS, int EPI, int PREC = 0, int BMT = BM>
