@@ -42,9 +42,6 @@ constexpr int BM = 128, BN = 128, BK = 32, NT = 256;  // BK: split-K granularity
 #ifndef ESP_F32_SPLIT
 #define ESP_F32_SPLIT 1
 #endif
-#ifndef ESP_SPLIT_SCHED
-#define ESP_SPLIT_SCHED 0
-#endif
 
 enum Mode { KC = 0, RC = 1, I2C_KC = 2, I2C_RC = 3, I2CT_KC = 4 };
 enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_SWISH = 2, ACT_MUL = 3 /* bwd_act only: v *= pre */ };
@@ -1753,13 +1750,6 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT>())) void gemm_gl
               acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][0], acc[i][j], 0, 0, 0);
             }
         }
-#if ESP_SPLIT_SCHED  // experiment: one MFMA, then up to 5 VALU in its shadow, through the slab
-#pragma unroll
-        for (int q = 0; q < 12 * TM * TN; ++q) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
-        }
-#endif
       } else {
 #pragma unroll
         for (int s = 0; s < 16; ++s)
