@@ -407,7 +407,8 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
   g.batch = batch;
   g.splits = 1;
   g.kchunk = K;
-  const long target = 2 * 256;
+  static long target = -1;  // work units split-K aims for (ESP_SPLITK_TARGET: measurements)
+  if (target < 0) target = getenv("ESP_SPLITK_TARGET") ? atol(getenv("ESP_SPLITK_TARGET")) : 2 * 256;
   auto ntiles = [&](int bn, int bm = BM) { return (long)((N + bn - 1) / bn) * ((M + bm - 1) / bm) * batch; };
   g.bnt = 0;
   g.bm = BM;
