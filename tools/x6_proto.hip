@@ -5,6 +5,8 @@
 // 128 x 128 tiles, 4 waves (2 x 2, 64 x 64 each), BK = 32, planes double-buffered (120 KB: one
 // block per CU), one slab of register prefetch, one barrier per slab.
 // Build: hipcc --offload-arch=gfx950 -O3 -shared -fPIC tools/x6_proto.hip -o tools/libx6proto.so
+// Measurement record only: its K-tail path is wrong for K % 32 != 0 (the quad offset
+// is added twice); tools/x6_proto2.hip is the corrected 16-k-slab version.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
