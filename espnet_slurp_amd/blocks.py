@@ -539,14 +539,15 @@ class Conv2dSubsampling(nn.Module):
         z2 = empty(B * T2 * F2, D, like=feats)
         ic = (T1, F1, D, T2, F2)
         K.gemm(B * T2 * F2, D, 9 * D, z1, w2r, z2, mode_a=K.I2C_KC, lda=0, mode_b=K.KC, ldb=9 * D, ldc=D,
-               bias=c2.bias, act=K.ACT_RELU, ic_a=ic)
+               bias=c2.bias, act=K.ACT_RELU, ic_a=ic, b_weight=True)
         lin = self.out[0]
         wor = empty(D * F2 * D, like=feats)
         K.permute3(lin.weight, wor, D, D, F2)  # (n, c, f) -> (n, f, c)
         x = empty(B * T2, D, like=feats)
         pd = p_drop if training else 0.0
         sd = seeds.next()
-        K.linear_fwd(z2.view(B * T2, F2 * D), wor.view(D, F2 * D), lin.bias, x, alpha=xscale, drop_p=pd, seed=sd)
+        K.linear_fwd(z2.view(B * T2, F2 * D), wor.view(D, F2 * D), lin.bias, x, alpha=xscale, drop_p=pd, seed=sd,
+                     b_weight=True)
         return x, Ctx(feats=feats, z1=z1, w2r=w2r, z2=z2, wor=wor, pd=pd, sd=sd, xscale=xscale,
                       B=B, T=T, F=F, T1=T1, F1=F1, T2=T2, F2=F2)
 
@@ -562,7 +563,7 @@ class Conv2dSubsampling(nn.Module):
         K.linear_bwd_weight(dv, z2f, dwor.view(D, F2 * D), lin.bias.grad)
         K.permute3(dwor, lin.weight.grad, D, F2, D, accumulate=True)  # (n, f, c) -> (n, c, f)
         dz2 = empty(B * T2, F2 * D, like=dx)
-        K.linear_bwd_data_act(dv, c.wor.view(D, F2 * D), dz2, z2f, K.ACT_RELU)  # ReLU' from its output
+        K.linear_bwd_data_act(dv, c.wor.view(D, F2 * D), dz2, z2f, K.ACT_RELU, b_weight=True)  # ReLU' from its output
         npix2 = B * T2 * F2
         dz2p = dz2.view(npix2, D)
         ic = (T1, F1, D, T2, F2)
@@ -577,7 +578,8 @@ class Conv2dSubsampling(nn.Module):
             K.conv2_dgrad(dz2p, c2.weight, c.z1, dz1, B, T1, F1, D)
         else:
             dcol = empty(npix2, 9 * D, like=dx)
-            K.gemm(npix2, 9 * D, D, dz2p, c.w2r, dcol, mode_a=K.KC, lda=D, mode_b=K.RC, ldb=9 * D, ldc=9 * D)
+            K.gemm(npix2, 9 * D, D, dz2p, c.w2r, dcol, mode_a=K.KC, lda=D, mode_b=K.RC, ldb=9 * D, ldc=9 * D,
+                   b_weight=True)
             K.col2im_relu(dcol, c.z1, dz1, B, T1, F1, D)
             del dcol
         K.conv1_wgrad(c.feats, dz1, c0.weight.grad.view(D, 9), c0.bias.grad, B, c.T, c.F, D)

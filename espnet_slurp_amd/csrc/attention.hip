@@ -1072,6 +1072,7 @@ ESP_API int esp_attn_softmax_fwd(const float* ac, const float* bd, int relpos, i
   ESP_ARG_CHECK(relpos != 1 || P == 2 * Tq - 1, "esp_attn_softmax_fwd: latest rel-pos needs P=2T-1");
   ESP_ARG_CHECK(relpos != 2 || P == Tq, "esp_attn_softmax_fwd: legacy rel-pos needs P=T");
   ESP_ARG_CHECK(lds >= Tk && (relpos == 0 || ldp >= P), "esp_attn_softmax_fwd: pitch < row length");
+  ESP_ARG_CHECK(drop_p < 1.f, "dropout p must be < 1 (got %g)", (double)drop_p);
   const uint32_t thr = esp::drop_threshold(drop_p);
   if (!thr) pdrop = nullptr;
   const float ds = esp::drop_scale(thr);
@@ -1095,6 +1096,7 @@ ESP_API int esp_attn_softmax_bwd(const float* attn, const float* dP, float* dS, 
                                  float sqrt_dk, long rows, int Tk, long lds, void* stream) {
   ESP_ARG_CHECK(Tk <= 1024, "esp_attn_softmax_bwd: Tk too large");
   ESP_ARG_CHECK(lds >= Tk, "esp_attn_softmax_bwd: pitch < Tk");
+  ESP_ARG_CHECK(drop_p < 1.f, "dropout p must be < 1 (got %g)", (double)drop_p);
   const uint32_t thr = esp::drop_threshold(drop_p);
   const float ds = esp::drop_scale(thr);
   dim3 grid((unsigned)((rows + 3) / 4));
@@ -1130,6 +1132,7 @@ ESP_API int esp_relpos_softmax_fwd(const float* qv, const float* p, long ldp_row
   ESP_ARG_CHECK(T >= 1 && T <= 1024 && lds >= T && nb >= 1 && H >= 1, "esp_relpos_softmax_fwd: bad sizes T=%d", T);
   ESP_ARG_CHECK(ldp_row % 4 == 0 && ((uintptr_t)p & 15) == 0 && ((uintptr_t)qv & 15) == 0,
                 "esp_relpos_softmax_fwd: q_v / p must be 16-B aligned with ld %% 4 == 0");
+  ESP_ARG_CHECK(drop_p < 1.f, "dropout p must be < 1 (got %g)", (double)drop_p);
   const uint32_t thr = esp::drop_threshold(drop_p);
   if (!thr) pdrop = nullptr;
   const float ds = esp::drop_scale(thr);
@@ -1162,6 +1165,7 @@ ESP_API int esp_relpos_attn_fwd(const float* qu, const float* qv, const float* k
   ESP_ARG_CHECK(ldp_row % 4 == 0 && ldk % 4 == 0 && ((uintptr_t)p & 15) == 0 && ((uintptr_t)qv & 15) == 0 &&
                     ((uintptr_t)qu & 15) == 0 && ((uintptr_t)kmat & 15) == 0,
                 "esp_relpos_attn_fwd: operands must be 16-B aligned with ld %% 4 == 0");
+  ESP_ARG_CHECK(drop_p < 1.f, "dropout p must be < 1 (got %g)", (double)drop_p);
   const uint32_t thr = esp::drop_threshold(drop_p);
   if (!thr) pdrop = nullptr;
   const float ds = esp::drop_scale(thr);
@@ -1205,6 +1209,7 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
   ESP_ARG_CHECK(ldp_row % 4 == 0 && ldk % 4 == 0 && ((uintptr_t)p & 15) == 0 && ((uintptr_t)qv & 15) == 0 &&
                     ((uintptr_t)qu & 15) == 0 && ((uintptr_t)kmat & 15) == 0,
                 "esp_relpos_attn_probs: operands must be 16-B aligned with ld %% 4 == 0");
+  ESP_ARG_CHECK(drop_p < 1.f, "dropout p must be < 1 (got %g)", (double)drop_p);
   const uint32_t thr = esp::drop_threshold(drop_p);
   if (!thr) pdrop = nullptr;
   const float ds = esp::drop_scale(thr);
@@ -1272,6 +1277,7 @@ ESP_API int esp_attn_softmax_bwd_relpos(const float* attn, const float* dP, floa
   ESP_ARG_CHECK(relpos == 1 || relpos == 2, "esp_attn_softmax_bwd_relpos: relpos must be 1 or 2");
   ESP_ARG_CHECK(T >= 1 && T <= 1024 && lds >= T && ldp >= (relpos == 1 ? 2 * T - 1 : T) && rows % T == 0,
                 "esp_attn_softmax_bwd_relpos: bad sizes");
+  ESP_ARG_CHECK(drop_p < 1.f, "dropout p must be < 1 (got %g)", (double)drop_p);
   const uint32_t thr = esp::drop_threshold(drop_p);
   const float ds = esp::drop_scale(thr);
   dim3 grid((unsigned)((rows + 3) / 4));
@@ -1329,6 +1335,7 @@ ESP_API int esp_relpos_attn_bwd(const float* dctx, long ldd, const float* vmat, 
                 "esp_relpos_attn_bwd: bad sizes T=%d", T);
   ESP_ARG_CHECK(ldd % 4 == 0 && ldv % 4 == 0 && ((uintptr_t)dctx & 15) == 0 && ((uintptr_t)vmat & 15) == 0,
                 "esp_relpos_attn_bwd: dctx / v must be 16-B aligned with ld %% 4 == 0");
+  ESP_ARG_CHECK(drop_p < 1.f, "dropout p must be < 1 (got %g)", (double)drop_p);
   const uint32_t thr = esp::drop_threshold(drop_p);
   const float ds = esp::drop_scale(thr);
   const int nta = ((T + 31) / 32 + 3) / 4;

@@ -53,6 +53,7 @@ __device__ __forceinline__ uint32_t thr16_of(uint32_t thresh) {
 // Host: the 32-bit threshold of dropout probability p, already on the 1/65536 grid the kernels
 // compare against (thr16 << 16, so thr16_of returns thr16 exactly).  p > 0 never quantizes to
 // "no dropout": p below half a quantum takes the smallest one (1/65536).  0 means no dropout.
+// Callers reject p >= 1 (ESP_ARG_CHECK): the 16-bit grid has no all-drop threshold.
 inline uint32_t drop_threshold(float p) {
   if (!(p > 0.f)) return 0;
   double q = (double)p * 65536.0 + 0.5;

@@ -20,7 +20,7 @@ void set_error(const char* fmt, ...) {
 }  // namespace esp
 
 ESP_API const char* esp_last_error(void) { return esp::g_err; }
-ESP_API int esp_abi_version(void) { return 24; }
+ESP_API int esp_abi_version(void) { return 25; }
 ESP_API int esp_set_rng_key(const unsigned long long* key) {
   esp::g_rng_key = (const uint64_t*)key;
   return 0;
@@ -318,6 +318,7 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
 
 ESP_API int esp_act_bwd(const float* dy, const float* h, float* dx, long n, int act, float drop_p,
                         unsigned long long seed, long idx_off, void* stream) {
+  ESP_ARG_CHECK(drop_p < 1.f, "dropout p must be < 1 (got %g)", (double)drop_p);
   const uint32_t thr = esp::drop_threshold(drop_p);
   hipLaunchKernelGGL(act_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, dy, h, dx, n, act,
                      thr, esp::drop_scale(thr), (uint64_t)seed, idx_off, esp::rng_key_ptr());
@@ -327,6 +328,7 @@ ESP_API int esp_act_bwd(const float* dy, const float* h, float* dx, long n, int 
 
 ESP_API int esp_scale_dropout(const float* x, float* y, long n, float alpha, float drop_p, unsigned long long seed,
                               const float* r, float beta, void* stream) {
+  ESP_ARG_CHECK(drop_p < 1.f, "dropout p must be < 1 (got %g)", (double)drop_p);
   const uint32_t thr = esp::drop_threshold(drop_p);
   if (n % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0 && ((uintptr_t)r & 15) == 0)
     hipLaunchKernelGGL(scale_drop4_kernel, dim3(grid_for(n / 4)), dim3(256), 0, (hipStream_t)stream, x, y, n / 4,
@@ -347,6 +349,7 @@ ESP_API int esp_scale_by_dev(float* x, long n, const float* s, void* stream) {
 
 ESP_API int esp_embed_fwd(const long long* tok, const float* E, const float* pe, float* y, int nrows, int L, int D,
                           float xscale, float drop_p, unsigned long long seed, void* stream) {
+  ESP_ARG_CHECK(drop_p < 1.f, "dropout p must be < 1 (got %g)", (double)drop_p);
   const uint32_t thr = esp::drop_threshold(drop_p);
   const long n = (long)nrows * D;
   hipLaunchKernelGGL(embed_fwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, (const int64_t*)tok, E,
@@ -358,6 +361,7 @@ ESP_API int esp_embed_fwd(const long long* tok, const float* E, const float* pe,
 ESP_API int esp_embed_bwd(const long long* tok, const float* dy, float* dE, int nrows, int V, int D, float xscale,
                           float drop_p, unsigned long long seed, void* stream) {
   ESP_ARG_CHECK(D <= EMB_MAXD, "esp_embed_bwd: D > 1024");
+  ESP_ARG_CHECK(drop_p < 1.f, "dropout p must be < 1 (got %g)", (double)drop_p);
   const uint32_t thr = esp::drop_threshold(drop_p);
   hipLaunchKernelGGL(embed_bwd_kernel, dim3(V), dim3(256), 0, (hipStream_t)stream, (const int64_t*)tok, dy, dE, nrows,
                      D, xscale, thr, esp::drop_scale(thr), (uint64_t)seed, esp::rng_key_ptr());

@@ -699,6 +699,7 @@ ESP_API int esp_relpos_flash_fwd(const float* qu, const float* qv, const float* 
   a.nb = nb; a.T = T; a.nqb = (T + FR - 1) / FR; a.nblk = nb * H * a.nqb;
   a.sqrt_dk = sqrt_dk;
   a.inv_sqrt_dk = 1.0f / sqrt_dk;
+  ESP_ARG_CHECK(drop_p < 1.f, "dropout p must be < 1 (got %g)", (double)drop_p);
   a.thr = esp::drop_threshold(drop_p);
   a.dscale = esp::drop_scale(a.thr);
   a.seed = seed;
@@ -739,6 +740,7 @@ ESP_API int esp_relpos_flash_bwd(const float* qu, const float* qv, const float* 
   a.nb = nb; a.T = T; a.nqb = (T + FR - 1) / FR; a.nblk = nb * H * a.nqb;
   a.sqrt_dk = sqrt_dk;
   a.inv_sqrt_dk = 1.0f / sqrt_dk;
+  ESP_ARG_CHECK(drop_p < 1.f, "dropout p must be < 1 (got %g)", (double)drop_p);
   a.thr = esp::drop_threshold(drop_p);
   a.dscale = esp::drop_scale(a.thr);
   a.seed = seed;

@@ -194,7 +194,7 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
   }
   const bool rs = can_rs && g.rowsum;
   if (rs) kind = EPI_PLAIN;
-  const dim3 grid((unsigned)std::min<long>(x.ntiles, persist_blocks(glds_occupancy_rt(BNT, kind, bm))));
+  const dim3 grid((unsigned)std::min<long>(x.ntiles, persist_blocks(glds_occupancy_rt(BNT, kind, bm, g.bf16))));
   x.fd_grid = make_fastdiv(grid.x);
   x.fd_ntx = make_fastdiv((uint32_t)x.ntx);
   x.fd_nty = make_fastdiv((uint32_t)x.nty);
@@ -208,10 +208,19 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
 }
 
 template <int MA, int MB>
-int launch(const GemmArgs& g0, int batch, hipStream_t st) {
+int launch(const GemmArgs& g0, int batch, hipStream_t st, const Operand* b_fp32 = nullptr) {
   bool done = false;
   if (g0.bnt == 64 || g0.bnt == 128) done = launch_glds(MA, MB, g0, batch, st);
   GemmArgs g = g0;
+  if (!done && g.bf16 == 3) {  // no B-planes kernel for this epilogue kind: the fp32 B operand
+    if (!b_fp32 || !b_fp32->p) {
+      esp::set_error("esp_gemm_f32_bp: no B-planes kernel for this launch and no fp32 B to fall back to");
+      return -1;
+    }
+    g.b = *b_fp32;
+    g.bf16 = 0;
+    if (g.bnt == 64 || g.bnt == 128) done = launch_glds(MA, MB, g, batch, st);
+  }
   if (!done && g.smb_rel) {
     esp::set_error("esp_attn_dscores: operands not eligible for the LDS-DMA kernel (16-B alignment, ld %% 4)");
     return -1;
@@ -282,7 +291,8 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
                     long sc2, const float* bias, float alpha, float beta, const float* R, int act, float* aux,
                     float drop_p, unsigned long long seed, int bwd_act, const float* pre, float* rowsum,
                     const int* im2col_a, const int* im2col_b, float* work, long work_bytes, void* stream,
-                    int prec_in, const GemmArgs* smb = nullptr);
+                    int prec_in, const GemmArgs* smb = nullptr, const void* b_planes = nullptr, long ldbp = 0,
+                    long sbp1 = 0, long sbp2 = 0, long bps = 0);
 
 ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2,
                          const float* A, long lda, long sa1, long sa2,
@@ -296,6 +306,65 @@ ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch,
   return gemm_run(mode_a, mode_b, M, N, K, batch, nb2, A, lda, sa1, sa2, B, ldb, sb1, sb2, C, ldc, sc1, sc2, bias,
                   alpha, beta, R, act, aux, drop_p, seed, bwd_act, pre, rowsum, im2col_a, im2col_b, work, work_bytes,
                   stream, -1);
+}
+
+ESP_API int esp_gemm_f32_bp(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2, const float* A, long lda,
+                            long sa1, long sa2, const float* B, long ldb, long sb1, long sb2, float* C, long ldc,
+                            long sc1, long sc2, const float* bias, float alpha, float beta, const float* R, int act,
+                            float* aux, float drop_p, unsigned long long seed, int bwd_act, const float* pre,
+                            float* rowsum, const int* im2col_a, float* work, long work_bytes, const void* b_planes,
+                            long ldbp, long sbp1, long sbp2, long b_pstride, void* stream) {
+  ESP_ARG_CHECK(mode_b == KC || mode_b == RC, "esp_gemm_f32_bp: mode_b must be 0 (KC) or 1 (RC)");
+  ESP_ARG_CHECK(b_planes || B, "esp_gemm_f32_bp: B planes and B both NULL");
+  return gemm_run(mode_a, mode_b, M, N, K, batch, nb2, A, lda, sa1, sa2, B, ldb, sb1, sb2, C, ldc, sc1, sc2, bias,
+                  alpha, beta, R, act, aux, drop_p, seed, bwd_act, pre, rowsum, im2col_a, nullptr, work, work_bytes,
+                  stream, -1, nullptr, b_planes, ldbp, sbp1, sbp2, b_pstride);
+}
+
+namespace {
+// the three bf16 planes of an fp32 matrix, split3_bf16's split (so a B-planes GEMM multiplies the
+// values the in-register split would): 8 columns per thread, one 16-B store per plane; columns
+// cols..ldy-1 written 0
+__global__ void f32_to_planes_kernel(const float* __restrict__ x, uint4* __restrict__ y, long rows, int cols, long ldx,
+                                     long ldy, long ps, int vec) {
+  const long c8 = ldy >> 3;
+  const long n = rows * c8;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / c8;
+    const int c = (int)(i - r * c8) * 8;
+    const float* src = x + r * ldx + c;
+    float v[8];
+    if (vec && c + 8 <= cols) {
+      const float4 a = *reinterpret_cast<const float4*>(src);
+      const float4 b = *reinterpret_cast<const float4*>(src + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = c + e < cols ? src[e] : 0.f;
+    }
+    bf16x8 hi, mid, lo;
+    split3_bf16(v, hi, mid, lo);
+    const long o = (r * ldy + c) >> 3, po = ps >> 3;
+    y[o] = __builtin_bit_cast(uint4, hi);
+    y[o + po] = __builtin_bit_cast(uint4, mid);
+    y[o + 2 * po] = __builtin_bit_cast(uint4, lo);
+  }
+}
+}  // namespace
+
+ESP_API int esp_f32_to_planes(const float* x, void* y, long rows, int cols, long ldx, long ldy, long pstride,
+                              void* stream) {
+  ESP_ARG_CHECK(rows >= 0 && cols >= 0 && ldx >= cols && ldy >= cols && ldy % 8 == 0 && pstride % 8 == 0 &&
+                    pstride >= rows * ldy && aligned16(y),
+                "esp_f32_to_planes: bad sizes rows=%ld cols=%d ldx=%ld ldy=%ld pstride=%ld (ldy, pstride %% 8, y 16-B aligned)",
+                rows, cols, ldx, ldy, pstride);
+  if (rows == 0 || ldy == 0) return 0;
+  const long n = rows * (ldy >> 3);
+  const int vec = aligned16(x) && ldx % 4 == 0;
+  hipLaunchKernelGGL(f32_to_planes_kernel, dim3((unsigned)std::min<long>((n + 255) / 256, 8192)), dim3(256), 0,
+                     (hipStream_t)stream, x, (uint4*)y, rows, cols, ldx, ldy, pstride, vec);
+  ESP_CHECK_LAUNCH("esp_f32_to_planes");
+  return 0;
 }
 
 ESP_API int esp_gemm_bf16(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2, const void* A, long lda,
@@ -347,7 +416,8 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
                     long sc2, const float* bias, float alpha, float beta, const float* R, int act, float* aux,
                     float drop_p, unsigned long long seed, int bwd_act, const float* pre, float* rowsum,
                     const int* im2col_a, const int* im2col_b, float* work, long work_bytes, void* stream,
-                    int prec_in, const GemmArgs* smb) {
+                    int prec_in, const GemmArgs* smb, const void* b_planes, long ldbp, long sbp1, long sbp2,
+                    long bps) {
   ESP_ARG_CHECK(M >= 0 && N >= 0 && K >= 0 && batch >= 1 && nb2 >= 1 && batch % nb2 == 0,
                 "esp_gemm_f32: bad sizes M=%d N=%d K=%d batch=%d nb2=%d", M, N, K, batch, nb2);
   ESP_ARG_CHECK(mode_a >= 0 && mode_a <= 3 && mode_b >= 0 && mode_b <= 3, "esp_gemm_f32: bad mode");
@@ -413,6 +483,24 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
   g.bnt = 0;
   g.bm = BM;
   g.bf16 = prec_in >= 0 ? prec_in : (g_compute == 1 ? 1 : 0);
+  // B as three bf16 planes (esp_gemm_f32_bp): the fp32 split-product GEMM without B's split in the
+  // k-loop, when the fp32 compute type runs on split products and the planes suit the LDS-DMA
+  // kernel (else the fp32 B operand)
+  const Operand b_fp32 = g.b;
+  if (b_planes && prec_in < 0 && g.bf16 == 0 && ESP_F32_SPLIT && variant() == 4 && g.a.glds && K > 0 &&
+      (((mode_a == KC || mode_a == I2C_KC) && mode_b == KC) || ((mode_a == KC || mode_a == RC) && mode_b == RC)) &&
+      aligned16(b_planes) && ldbp % 8 == 0 && sbp1 % 8 == 0 && sbp2 % 8 == 0 && bps % 8 == 0 &&
+      (mode_b == KC ? (K % 8 == 0 && ldbp >= K && 128L * ldbp * 2 < (1L << 32))
+                    : (N % 8 == 0 && ldbp >= N && 32L * ldbp * 2 + 2L * N < (1L << 32)))) {
+    g.b = Operand{(const float*)b_planes, ldbp, sbp1, sbp2, 1, {}, 1};
+    g.b.ps = bps;
+    g.bf16 = 3;
+  }
+  if (!g.b.p) {
+    esp::set_error("esp_gemm_f32_bp: B planes not eligible (alignment, ld / strides %% 8, K or N %% 8) and B is NULL");
+    return -1;
+  }
+  const bool bplanes = g.bf16 == 3;
   if (variant() == 4 && g.a.glds && g.b.glds && K > 0) {
     // per-CU time model: ceil(tiles / CUs) tiles of bn/64 units each, x1.3 when the grid
     // leaves CUs with a single resident block (one wave per SIMD); ties keep 128 (intensity)
@@ -422,7 +510,8 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
     const bool split_f32 = ESP_F32_SPLIT && g.bf16 == 0;
     auto cost = [&](int bn) {
       const long t = ntiles(bn);
-      const double per = split_f32 && bn == 64 ? 1.5 : bn / 64;
+      // (B planes: only A is split, 3.7 split VALU per MFMA at either width)
+      const double per = split_f32 && !bplanes && bn == 64 ? 1.5 : bn / 64;
       if (split_f32 && work && t < target && K >= 2 * 128) return (double)t * per / 256.0;
       double c = (double)((t + 255) / 256) * per;
       if (t < 2 * 256) c *= 1.3;
@@ -457,7 +546,8 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
       // opt-in (ESP_SPLITK_INKERNEL=1): measured slower at C2 B=128 -- the last-arriving unit of a
       // tile sums all of its splits alone (64 splits x 32 KB behind 8 tiles for the d x d weight
       // gradients: 222 vs 68 us), where the separate reduction spreads them over the chip
-      const bool inkernel = splitk_mode() == 1 && g.bnt && tiles <= ESP_GEMM_TICKETS && work_bytes > ESP_GEMM_TICKET_BYTES;
+      const bool inkernel = splitk_mode() == 1 && g.bnt && !bplanes && tiles <= ESP_GEMM_TICKETS &&
+                            work_bytes > ESP_GEMM_TICKET_BYTES;
       const long part = inkernel ? mp * np : (long)M * N;
       const long cap = (work_bytes - (inkernel ? ESP_GEMM_TICKET_BYTES : 0)) / (4L * (part * batch + (rowsum ? M : 0)));
       if (sp > cap) sp = cap;
@@ -500,11 +590,11 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
   hipStream_t st = (hipStream_t)stream;
   const int key = mode_a * 4 + mode_b;
   switch (key) {
-    case KC * 4 + KC: return launch<KC, KC>(g, batch, st);
-    case KC * 4 + RC: return launch<KC, RC>(g, batch, st);
+    case KC * 4 + KC: return launch<KC, KC>(g, batch, st, &b_fp32);
+    case KC * 4 + RC: return launch<KC, RC>(g, batch, st, &b_fp32);
     case RC * 4 + KC: return launch<RC, KC>(g, batch, st);
-    case RC * 4 + RC: return launch<RC, RC>(g, batch, st);
-    case I2C_KC * 4 + KC: return launch<I2C_KC, KC>(g, batch, st);
+    case RC * 4 + RC: return launch<RC, RC>(g, batch, st, &b_fp32);
+    case I2C_KC * 4 + KC: return launch<I2C_KC, KC>(g, batch, st, &b_fp32);
     case RC * 4 + I2C_RC: return launch<RC, I2C_RC>(g, batch, st);
     default:
       esp::set_error("esp_gemm_f32: unsupported mode pair %d,%d", mode_a, mode_b);
@@ -541,8 +631,10 @@ __global__ void conv2_class_weights_kernel(const float* __restrict__ W, float* _
 }
 }  // namespace
 
-// wc_work: the four parity classes' re-laid weights, 9 * D * D floats (esp_conv2_dgrad_workspace_bytes)
-ESP_API long esp_conv2_dgrad_workspace_bytes(int D) { return D <= 0 ? 0 : 4L * 9 * D * D; }
+// wc_work: the four parity classes' re-laid weights, 9 * D * D floats, then their three bf16 split
+// planes (the B-planes class GEMMs of the fp32 split build), 3 * 9 * D * D bf16
+// (esp_conv2_dgrad_workspace_bytes)
+ESP_API long esp_conv2_dgrad_workspace_bytes(int D) { return D <= 0 ? 0 : 4L * 9 * D * D + 6L * 9 * D * D; }
 ESP_API int esp_conv2_dgrad(const float* dz2, const float* W, const float* z1, float* dz1, int B, int T1, int F1,
                             int D, const float* zeros16, float* wc_work, long work_bytes, void* stream) {
   const int T2 = (T1 - 3) / 2 + 1, F2 = (F1 - 3) / 2 + 1;
@@ -554,6 +646,15 @@ ESP_API int esp_conv2_dgrad(const float* dz2, const float* W, const float* z1, f
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(conv2_class_weights_kernel, dim3(1024), dim3(256), 0, st, W, wc_work, D);
   ESP_CHECK_LAUNCH("esp_conv2_dgrad (weights)");
+  // fp32 compute on split products: the class weights as B planes (PREC 3, no B split in the k-loop)
+  const bool bp = g_compute == 0 && ESP_F32_SPLIT && variant() == 4;
+  const long ps = 9L * D * D;
+  __bf16* planes = reinterpret_cast<__bf16*>(wc_work + ps);
+  if (bp) {
+    hipLaunchKernelGGL(f32_to_planes_kernel, dim3((unsigned)std::min<long>((ps / 8 + 255) / 256, 8192)), dim3(256), 0,
+                       st, wc_work, (uint4*)planes, 9L * D, D, (long)D, (long)D, ps, 1);
+    ESP_CHECK_LAUNCH("esp_conv2_dgrad (planes)");
+  }
   const int slot0[4] = {0, 4, 6, 8};
   for (int cls = 0; cls < 4; ++cls) {
     const int ph = cls >> 1, pw = cls & 1;
@@ -576,6 +677,11 @@ ESP_API int esp_conv2_dgrad(const float* dz2, const float* W, const float* z1, f
     g.c = dz1; g.ldc = D; g.alpha = 1.f; g.beta = 0.f;
     g.bwd_act = ACT_RELU; g.pre = z1;
     g.bf16 = g_compute;  // bf16 MFMA in the reduced-precision mode, as every other GEMM of the step
+    if (bp) {
+      g.b = Operand{reinterpret_cast<const float*>(planes + (long)slot0[cls] * D * D), D, 0, 0, 1, {}, 1};
+      g.b.ps = ps;
+      g.bf16 = 3;
+    }
     g.key = esp::rng_key_ptr();
     g.wide = 1;
     static int dgrad_bnt = -1;  // ESP_CONV2_DGRAD_BNT=64|128 (measurements)

@@ -82,6 +82,7 @@ struct Operand {
   int vec;   // float4 along the contiguous dim is legal
   Im2col ic;
   int glds;  // 16-B LDS-DMA of any in-range quad stays inside the operand (see glds_ok)
+  long ps = 0;  // PREC 3 B operand: plane stride in bf16 elements (p, ld, s1, s2 in bf16 elements)
 };
 
 struct GemmArgs {
@@ -103,7 +104,8 @@ struct GemmArgs {
   float* work;
   int bf16;  // MFMA precision: 0 fp32; 1 bf16 MFMA on fp32 operands rounded after staging
              // (esp_set_gemm_compute(1)); 2 bf16 operands in HBM (esp_gemm_bf16: K, ld, strides
-             // given in fp32 units, i.e. bf16 pairs; KC x KC only)
+             // given in fp32 units, i.e. bf16 pairs; KC x KC only); 3 fp32 with B given as its
+             // three bf16 split planes (esp_gemm_f32_bp: B's ld, strides, ps in bf16 elements)
   int bnt;  // LDS-DMA kernel tile width (128, or 64 for narrow / mid-size grids); 0 = fallback kernel
   int bm;   // LDS-DMA kernel tile height: 128, or 64 (with bnt 64) for under-filled grids
   int bwd_act;       // != 0: backward epilogue  v = drop'(acc) * act'(pre)  (act code, dropout regenerated)
@@ -1447,6 +1449,93 @@ __device__ __forceinline__ void frag_tr16(const float* slab, int rbase, int lane
   }
 }
 
+// ---------------------------------------------------------------- B as three bf16 planes (PREC 3)
+// An fp32 B operand stored as its exact three-way split (esp_f32_to_planes: v = hi + mid + lo with
+// split3_bf16's roundings), plane p at B + p * ps (bf16 elements; ld and batch strides in bf16
+// elements too).  The fp32 product is the PREC 0 one -- the same six split products in the same
+// order on the same values, bit for bit -- but only A is split in the k-loop: 3.7 instead of 7.3
+// split VALU per MFMA, under the ~5 an MFMA gap hides.  A slab holds the three planes' images of
+// ROWS x 32 k, PLB = ROWS * 64 bytes each:
+//   KC  row r (64 B = 4 chunks of 8 k) holds global chunk c at position c ^ pl_kc_swz(r).  The
+//       ds_read_b128 groups of frag_pl_kc ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32) read rows
+//       r = lane & 31 at one chunk; rows 4j..4j+3 share a 256-B bank row and (r & 3, swz(r)) is
+//       distinct in each group: conflict-free.
+//   RC  k-row kr (2 ROWS bytes) holds the 16-B chunk c (8 rows) at position c ^ bf16_rc_swz(2 ROWS, kr)
+//       and is read transposed (frag_pl_rc, ds_read_b64_tr_b16; conflict-free as frag_tr16).
+// Host: K % 8 == 0 (KC), N % 8 == 0 (RC), 16-B aligned planes, ld / strides / ps % 8 == 0.
+__device__ __forceinline__ int pl_kc_swz(int r) { return (r >> 2) & 3; }
+
+template <int MODE, int ROWS>
+struct StageP {
+  static constexpr int PLB = ROWS * 64;           // bytes of one plane's slab image
+  static constexpr int NI = PLB / 1024 / 4;       // wave instructions per plane per wave
+  const char* base;  // plane 0 at the tile's first row / k-row kb (bytes)
+  long ld, psb;      // ld in bf16 elements, plane stride in bytes
+  int kb;
+  uint32_t off[NI];
+  int q[NI];  // KC: k offset of the lane's chunk inside the slab; RC: k-row inside the slab
+  __device__ __forceinline__ void init(const Operand& op, const float* zbase, int rows, int row0, int kbeg, int wave,
+                                       int lane) {
+    const __bf16* zb = reinterpret_cast<const __bf16*>(zbase);
+    ld = op.ld;
+    psb = op.ps * 2;
+    kb = kbeg;
+    base = reinterpret_cast<const char*>(MODE == KC ? zb + (long)row0 * op.ld + kbeg : zb + (long)kbeg * op.ld);
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int slot = (i * 4 + wave) * 64 + lane;
+      if constexpr (MODE == KC) {
+        const int r = slot >> 2, gc = (slot & 3) ^ pl_kc_swz(r);
+        const int gr = min(row0 + r, rows - 1);
+        q[i] = 8 * gc;
+        off[i] = ((uint32_t)(gr - row0) * (uint32_t)op.ld + 8u * gc) * 2u;
+      } else {
+        constexpr int CPR = ROWS / 8;  // 16-B chunks per k-row
+        const int kr = slot / CPR, cs = (slot % CPR) ^ bf16_rc_swz(ROWS * 2, kr);
+        const int gr = min(row0 + 8 * cs, rows - 8);
+        q[i] = kr;
+        off[i] = ((uint32_t)kr * (uint32_t)op.ld + (uint32_t)gr) * 2u;
+      }
+    }
+  }
+  __device__ __forceinline__ void issue(int K, int k0, uint32_t dst, int wave) const {
+    const char* sb = MODE == KC ? base + 2L * (k0 - kb) : base + 2L * (long)(k0 - kb) * ld;
+    const bool full = k0 + GL_BK <= K;
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        uint32_t o = off[i];
+        if (!full) {  // clamp past-K chunks / k-rows to the last in-range one (finite values; A's tail is 0)
+          if constexpr (MODE == KC) o -= 2u * (uint32_t)max(0, q[i] - (K - 8 - k0));
+          else o -= 2u * (uint32_t)ld * (uint32_t)max(0, q[i] - (K - 1 - k0));
+        }
+        lds_dma16_s(reinterpret_cast<const float*>(sb + p * psb), o, dst + p * PLB + (i * 4 + wave) * 1024);
+      }
+  }
+};
+// KC plane image: the 8 bf16 at k = 16h + 8hs + 0..7 of tile row r (frag16's k order, split in halves)
+__device__ __forceinline__ bf16x8 frag_pl_kc(const float* plane, int r, int h, int hs) {
+  return *reinterpret_cast<const bf16x8*>(reinterpret_cast<const char*>(plane) + r * 64 +
+                                          (((2 * h + hs) ^ pl_kc_swz(r)) << 4));
+}
+// RC plane image: lane (h, l32) gets row rbase + l32 at k = 16h + 8hs + 0..7 (two transposing reads
+// of 4 k-rows; k-rows 16h + 8hs + q (+4) share the swizzle of q: 16h + 8hs % 8 == 0)
+template <int ROWS>
+__device__ __forceinline__ bf16x8 frag_pl_rc(const float* plane, int rbase, int lane, int hs) {
+  constexpr int ROWB = ROWS * 2;
+  const int g1 = (lane >> 4) & 1, h = lane >> 5, q = (lane >> 2) & 3, p = lane & 3;
+  const int mloc = rbase + 16 * g1 + 4 * p;
+  const int base = (16 * h + 8 * hs + q) * ROWB + (((mloc >> 3) ^ bf16_rc_swz(ROWB, q)) << 4) + 8 * (p & 1);
+  const __attribute__((address_space(3))) char* s =
+      (const __attribute__((address_space(3))) char*)(__attribute__((address_space(3))) const float*)plane;
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(s + base));
+  const v4i16 hi =
+      __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16*)(s + base + 4 * ROWB));
+  const int2 a = __builtin_bit_cast(int2, lo), b = __builtin_bit_cast(int2, hi);
+  return __builtin_bit_cast(bf16x8, make_int4(a.x, a.y, b.x, b.y));
+}
+
 // the 16 k-values (k = 16h + s) of tile row r
 template <int MODE, int ROWS>
 __device__ __forceinline__ void frag16(const float* slab, int r, int h, float (&f)[16]) {
@@ -1503,9 +1592,16 @@ __device__ __forceinline__ TileCoord tile_coord(const GemmArgs& g, const GldsArg
 
 // resident blocks per CU: 128x64 tiles (48 KB LDS) fit three, 128x128 tiles (64 KB) two; the
 // generic fused epilogues need the registers of two (the specialised ones fit three)
-template <int BNT, int EPI, int BMT = BM>
+// PREC 3 (B as three bf16 planes: 1.5x the B slab bytes) is also bounded by LDS: 128x128 tiles use
+// exactly 80 KB (two per CU), 128x64 56 KB (two), 64x64 40 KB (four)
+constexpr int glds_lds_bytes(int BNT, int BMT, int PREC) {
+  return 2 * 4 * (BMT * GL_BK + (PREC == 3 ? 48 * BNT : BNT * GL_BK)) + (PREC == 3 ? 0 : 16);
+}
+template <int BNT, int EPI, int BMT = BM, int PREC = 0>
 constexpr int glds_occupancy() {
-  return BMT == 64 ? 4 : (BNT == 64 && (EPI == EPI_PLAIN || EPI >= EPI_BIAS)) ? 3 : 2;
+  constexpr int by_regs = BMT == 64 ? 4 : (BNT == 64 && (EPI == EPI_PLAIN || EPI >= EPI_BIAS)) ? 3 : 2;
+  constexpr int by_lds = 163840 / glds_lds_bytes(BNT, BMT, PREC);
+  return by_regs < by_lds ? by_regs : by_lds;
 }
 
 // Persistent: block b processes tiles b, b+G, b+2G, ... as ONE continuous slab pipeline — the
@@ -1554,12 +1650,17 @@ __device__ __forceinline__ void split3_bf16(const float* v, bf16x8& hi, bf16x8& 
 }
 
 template <int MA, int MB, int BNT, bool RS, int EPI, int PREC = 0, int BMT = BM>
-__global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT>())) void gemm_glds_kernel(GemmArgs g, GldsArgs x) {
+__global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void gemm_glds_kernel(GemmArgs g, GldsArgs x) {
   constexpr int WN = BMT == 64 ? 2 : BNT / 64, WM = 4 / WN, TM = BMT / (WM * 32), TN = BNT / (WN * 32);
   static_assert(BMT == 128 || BNT == 64, "64-row tiles are 64 wide");
-  constexpr int A_SZ = BMT * GL_BK, B_SZ = BNT * GL_BK, BUF = A_SZ + B_SZ;
+  static_assert(PREC != 3 || MB == KC || MB == RC, "B planes: KC / RC operands");
+  constexpr bool BP = PREC == 3;                 // B as three bf16 planes (StageP)
+  constexpr int PLF = BNT * 16;                  // floats per plane image (BNT x 32 bf16)
+  constexpr int A_SZ = BMT * GL_BK, B_SZ = BP ? 3 * PLF : BNT * GL_BK, BUF = A_SZ + B_SZ;
   constexpr int NIA = A_SZ / 4 / NT, NIB = B_SZ / 4 / NT;
-  __shared__ __attribute__((aligned(16))) float smem[2 * BUF + 4];  // + the split-K combine flag
+  // + the split-K combine flag (the in-kernel combine is never used with B planes: their 128x128
+  // tiles need exactly 80 KB for two blocks per CU)
+  __shared__ __attribute__((aligned(16))) float smem[2 * BUF + (BP ? 0 : 4)];
 
   const int G = gridDim.x;
   int t = blockIdx.x;
@@ -1576,20 +1677,25 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT>())) void gemm_gl
   };
   auto b_base = [&](const TileCoord& c) {
     const int z1 = (int)fdiv((uint32_t)c.z, x.fd_nb2), z2 = c.z - z1 * g.nb2;
-    return g.b.p + z1 * g.b.s1 + z2 * g.b.s2;
+    if constexpr (BP)  // bf16 element strides
+      return reinterpret_cast<const float*>(reinterpret_cast<const __bf16*>(g.b.p) + z1 * g.b.s1 + z2 * g.b.s2);
+    else
+      return g.b.p + z1 * g.b.s1 + z2 * g.b.s2;
   };
 
   // scalar-base staging (StageS) for KC / RC / implicit-im2col A; the gathered operands keep
-  // per-lane 64-bit addresses (Stage)
+  // per-lane 64-bit addresses (Stage); B planes: StageP
   constexpr bool SA_S = MA == KC || MA == RC || MA == I2C_KC, SB_S = MB == KC || MB == RC;
   using SAt = std::conditional_t<SA_S, StageS<MA, BMT, NIA, PREC == 2>, Stage<MA, BMT, NIA>>;
-  using SBt = std::conditional_t<SB_S, StageS<MB, BNT, NIB, PREC == 2>, Stage<MB, BNT, NIB>>;
+  using SBt = std::conditional_t<BP, StageP<MB, BNT>,
+                                 std::conditional_t<SB_S, StageS<MB, BNT, NIB, PREC == 2>, Stage<MB, BNT, NIB>>>;
   SAt sa;
   SBt sb;
   auto init_ab = [&](const TileCoord& cc) {
     if constexpr (SA_S) sa.init(g.a, a_base(cc), g.M, g.K, cc.m0, cc.kbeg, x.hw_a, x.wo_a, wave, lane);
     else sa.init(g.a, a_base(cc), g.M, g.K, cc.m0, x.c_a, x.hw_a, x.wo_a, wave, lane, MA == I2CT_KC ? &x : nullptr);
-    if constexpr (SB_S) sb.init(g.b, b_base(cc), g.N, g.K, cc.n0, cc.kbeg, x.hw_b, x.wo_b, wave, lane);
+    if constexpr (BP) sb.init(g.b, b_base(cc), g.N, cc.n0, cc.kbeg, wave, lane);
+    else if constexpr (SB_S) sb.init(g.b, b_base(cc), g.N, g.K, cc.n0, cc.kbeg, x.hw_b, x.wo_b, wave, lane);
     else sb.init(g.b, b_base(cc), g.N, g.K, cc.n0, x.c_b, x.hw_b, x.wo_b, wave, lane);
   };
   const uint32_t smem_lds = lds_addr(smem);
@@ -1597,7 +1703,8 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT>())) void gemm_gl
     const uint32_t dl = smem_lds + (uint32_t)(dst - smem) * 4u;
     if constexpr (SA_S) sa.issue(g.a, g.K, k0, dl, wave);
     else sa.issue(g.a, g.K, k0, dst, wave, x.c_a, x.hw_a, x.wo_a, MA == I2CT_KC ? &x : nullptr);
-    if constexpr (SB_S) sb.issue(g.b, g.K, k0, dl + 4u * A_SZ, wave);
+    if constexpr (BP) sb.issue(g.K, k0, dl + 4u * A_SZ, wave);
+    else if constexpr (SB_S) sb.issue(g.b, g.K, k0, dl + 4u * A_SZ, wave);
     else sb.issue(g.b, g.K, k0, dst + A_SZ, wave, x.c_b, x.hw_b, x.wo_b);
   };
 
@@ -1690,6 +1797,56 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT>())) void gemm_gl
                   a0 += __uint_as_float(u << 16) + __uint_as_float(u & 0xffff0000u);
                 }
               }
+              rs[i] += a0;
+            }
+          }
+        }
+        return;
+      }
+      if constexpr (BP) {
+        // A split in registers (as PREC 0), B's three planes read from LDS: the PREC 0 products in
+        // the PREC 0 order on the same values
+        float af[TM][16];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) frag16<MA, BMT>(cur, wm * TM * 32 + i * 32 + l32, h, af[i]);
+        if (kv < GL_BK) {
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int s2 = 0; s2 < 16; ++s2) af[i][s2] = 16 * h + s2 < kv ? af[i][s2] : 0.f;
+        }
+        const float* bpl = cur + A_SZ;
+#pragma unroll
+        for (int hs = 0; hs < 2; ++hs) {
+          bf16x8 ah[TM][3], bh[TN][3];
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+              if constexpr (MB == KC) bh[j][p] = frag_pl_kc(bpl + p * PLF, wn * TN * 32 + j * 32 + l32, h, hs);
+              else bh[j][p] = frag_pl_rc<BNT>(bpl + p * PLF, wn * TN * 32 + j * 32, lane, hs);
+            }
+#pragma unroll
+          for (int i = 0; i < TM; ++i) split3_bf16(&af[i][8 * hs], ah[i][0], ah[i][1], ah[i][2]);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][1], bh[j][1], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][2], bh[j][0], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][2], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][1], bh[j][0], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][1], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][0], acc[i][j], 0, 0, 0);
+            }
+        }
+        if constexpr (RS) {
+          if (do_rs) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+              float a0 = 0.f;
+#pragma unroll
+              for (int s = 0; s < 16; ++s) a0 += af[i][s];
               rs[i] += a0;
             }
           }
@@ -1811,7 +1968,7 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT>())) void gemm_gl
         }
       }
     }
-    if (g.tickets) {  // in-kernel split-K: write-through partial tile, ticket, last unit combines
+    if (!BP && g.tickets) {  // in-kernel split-K: write-through partial tile, ticket, last unit combines
       float* Wz = g.work + ((long)c.split * g.batch + c.z) * ((long)g.sk_mp * g.sk_np);
       store_cols<EPI_P0, TM, TN, true, 16>(g, 0, g.sk_np, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, lane, acc, Wz);
       splitk_combine<BMT, BNT>(g, c.z, c.m0 / BMT, c.tn, x.ntx, x.nty, reinterpret_cast<int*>(smem + 2 * BUF));
@@ -1856,11 +2013,19 @@ bool glds_switch(int ma, int mb, int bnt, int prec, int bm, F&& f) {
     if (bnt != 64 && bnt != 128) return false;
     constexpr bool small_ok = (decltype(A)::value == KC || decltype(A)::value == RC) &&
                               (decltype(B)::value == KC || decltype(B)::value == RC);
+    // B planes (prec 3): the weight-B pairs (linear forward / input gradient, conv2 forward / input
+    // gradient) and RC x RC (weight gradients)
+    constexpr int MA_ = decltype(A)::value, MB_ = decltype(B)::value;
+    constexpr bool planes_ok = (MB_ == KC && (MA_ == KC || MA_ == I2C_KC)) ||
+                               (MB_ == RC && (MA_ == KC || MA_ == RC || MA_ == I2CT_KC));
     auto by_prec = [&](auto N, auto R) {
       if (prec == 0) {
         f(A, B, N, IC<0>{}, R);
       } else if (prec == 1) {
         f(A, B, N, IC<1>{}, R);
+      } else if (prec == 3) {
+        if constexpr (planes_ok) f(A, B, N, IC<3>{}, R);
+        else return false;
       } else if constexpr (small_ok && decltype(R)::value == BM) {  // bf16 operands: KC / RC pairs
         f(A, B, N, IC<2>{}, R);
       } else {
@@ -1904,8 +2069,10 @@ bool glds_launch_spec(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hip
 bool glds_launch_pspec(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hipStream_t st, const GemmArgs& g,
                        const GldsArgs& x);
 // resident blocks per CU of a launch (host side)
-inline int glds_occupancy_rt(int bnt, int epi, int bm) {
-  return bm == 64 ? 4 : (bnt == 64 && (epi == EPI_PLAIN || epi >= EPI_BIAS)) ? 3 : 2;
+inline int glds_occupancy_rt(int bnt, int epi, int bm, int prec) {
+  const int by_regs = bm == 64 ? 4 : (bnt == 64 && (epi == EPI_PLAIN || epi >= EPI_BIAS)) ? 3 : 2;
+  const int by_lds = 163840 / glds_lds_bytes(bnt, bm == 64 ? 64 : BM, prec);
+  return std::min(by_regs, by_lds);
 }
 
 }  // namespace espg

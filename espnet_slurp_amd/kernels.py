@@ -205,12 +205,41 @@ def register_param_storage(t: torch.Tensor):
 
 class param_cast_scope:
     def __enter__(self):
-        self.prev = _W16[0]
+        self.prev = _W16[0], _WP[0]
         _W16[0] = {}
+        _WP[0] = {}
         return self
 
     def __exit__(self, *exc):
-        _W16[0] = self.prev
+        _W16[0], _WP[0] = self.prev
+        _DY16[0] = None
+
+
+# fp32 GEMMs whose B operand is a weight take B as its three bf16 split planes (esp_gemm_f32_bp,
+# gemm_kernels.h PREC 3): the same split products as the in-register split, bit for bit, with only A
+# split in the k-loop.  A weight's planes are made once per step inside param_cast_scope (the
+# Trainer's step; keyed like _W16, holding the fp32 source), else per GEMM.  ESP_BPLANES=0: off
+# (A/B measurements).
+_BPLANES = os.environ.get("ESP_BPLANES", "1") == "1"
+_WP = [None]
+
+
+def planes(X, off: int, rows: int, cols: int, ld: int):
+    """(planes, ldp, pstride): the three bf16 planes (esp_f32_to_planes) of the rows x cols fp32
+    matrix at X[off] with row pitch ld; plane row pitch ldp = cols rounded up to 8."""
+    key = (X.data_ptr() + off * 4, rows, cols, ld, torch.cuda.is_current_stream_capturing())
+    wc = _WP[0]
+    if wc is not None:
+        hit = wc.get(key)
+        if hit is not None:
+            return hit[0], hit[1], hit[2]
+    ldp = (cols + 7) // 8 * 8
+    ps = rows * ldp
+    out = torch.empty(3 * ps, dtype=torch.bfloat16, device=X.device)
+    _native.call("esp_f32_to_planes", _p(X, off), _p(out), rows, cols, ld, ldp, ps, _st())
+    if wc is not None:
+        wc[key] = (out, ldp, ps, X)
+    return out, ldp, ps
 
 
 def _is_param(ptr: int, nbytes: int) -> bool:
@@ -255,8 +284,8 @@ def _gemm_amp_operands(M, N, K, A, B, C, mode_a, lda, mode_b, ldb, ldc, a_off, b
         return False
     A16, la = _bf16_copy(A, a_off, M, K, lda, "a_kc") if mode_a == KC else _bf16_copy(A, a_off, K, M, lda)
     B16, lb = _bf16_copy(B, b_off, N, K, ldb) if mode_b == KC else _bf16_copy(B, b_off, K, N, ldb, "b_rc")
-    if keep_a:
-        _DY16[0] = ((A.data_ptr() + a_off * 4, K, M, lda), A16, la)
+    if keep_a:  # (holding A: its memory cannot be handed to another tensor while the memo lives)
+        _DY16[0] = ((A.data_ptr() + a_off * 4, K, M, lda), A16, la, A)
     # (a fused bias gradient, rowsum, sums the bf16 A values in fp32: torch AMP's sum of a bf16 dy)
     ws = _ws(_GEMM_WS, "esp_gemm_bf16", _GEMM_WS_BYTES, C.device)
     if _PROF is not None:  # the GEMM kernel alone (the operand casts are their own kernels)
@@ -280,9 +309,11 @@ def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc
          a_off=0, b_off=0, c_off=0, batch=1, nb2=1, sa=(0, 0), sb=(0, 0), sc=(0, 0),
          bias=None, alpha=1.0, beta=0.0, R=None, r_off=None, act=ACT_NONE, aux=None,
          drop_p=0.0, seed=0, ic_a: Optional[Sequence[int]] = None, ic_b: Optional[Sequence[int]] = None,
-         bwd_act=ACT_NONE, pre=None, rowsum=None, _keep_a16=False):
+         bwd_act=ACT_NONE, pre=None, rowsum=None, _keep_a16=False, b_weight=False):
     """C[z](m,n) = alpha*epi(sum_k A(m,k)B(k,n) + bias) + beta*R (see gemm.hip).
-    bwd_act/pre: epilogue drop'(.)*act'(pre) (FFN backward); rowsum: += sum_k A(m,k) (bias grad)."""
+    bwd_act/pre: epilogue drop'(.)*act'(pre) (FFN backward); rowsum: += sum_k A(m,k) (bias grad).
+    b_weight: B is a weight-like operand, constant for the step (its split planes may be cached
+    like a parameter's, see planes())."""
     if R is not None and r_off is None:
         r_off = c_off
     if (_COMPUTE[0] == GEMM_BF16 and _AMP_BF16_OPERANDS and batch == 1 and mode_a in (KC, RC)
@@ -294,24 +325,40 @@ def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc
     ws = _ws(_GEMM_WS, "esp_gemm_f32", _GEMM_WS_BYTES, C.device)
     ica = (_native.I * 5)(*ic_a) if ic_a is not None else None
     icb = (_native.I * 5)(*ic_b) if ic_b is not None else None
+    bp = None
+    if (_BPLANES and _COMPUTE[0] == 0 and batch == 1 and mode_b in (KC, RC) and mode_a in (KC, RC, I2C_KC)
+            and ic_b is None and M > 0 and N > 0 and K > 0):
+        rows, cols = (N, K) if mode_b == KC else (K, N)
+        if b_weight or _is_param(B.data_ptr() + b_off * 4, ((rows - 1) * ldb + cols) * 4):
+            bp = planes(B, b_off, rows, cols, ldb)
     if _PROF is not None:
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         ev0.record()
-    _native.call("esp_gemm_f32", mode_a, mode_b, M, N, K, batch, nb2,
-                 _p(A, a_off), lda, sa[0], sa[1], _p(B, b_off), ldb, sb[0], sb[1],
-                 _p(C, c_off), ldc, sc[0], sc[1], _p(bias), float(alpha), float(beta),
-                 _p(R, r_off or 0), act, _p(aux, c_off) if aux is not None else None,
-                 float(drop_p), seed & 0xFFFFFFFFFFFFFFFF,
-                 int(bwd_act), _p(pre, c_off) if pre is not None else None, _p(rowsum),
-                 ctypes_ptr(ica), ctypes_ptr(icb), _p(ws), _GEMM_WS_BYTES, _st())
+    if bp is not None:
+        _native.call("esp_gemm_f32_bp", mode_a, mode_b, M, N, K, batch, nb2,
+                     _p(A, a_off), lda, sa[0], sa[1], _p(B, b_off), ldb, sb[0], sb[1],
+                     _p(C, c_off), ldc, sc[0], sc[1], _p(bias), float(alpha), float(beta),
+                     _p(R, r_off or 0), act, _p(aux, c_off) if aux is not None else None,
+                     float(drop_p), seed & 0xFFFFFFFFFFFFFFFF,
+                     int(bwd_act), _p(pre, c_off) if pre is not None else None, _p(rowsum),
+                     ctypes_ptr(ica), _p(ws), _GEMM_WS_BYTES, _p(bp[0]), bp[1], 0, 0, bp[2], _st())
+    else:
+        _native.call("esp_gemm_f32", mode_a, mode_b, M, N, K, batch, nb2,
+                     _p(A, a_off), lda, sa[0], sa[1], _p(B, b_off), ldb, sb[0], sb[1],
+                     _p(C, c_off), ldc, sc[0], sc[1], _p(bias), float(alpha), float(beta),
+                     _p(R, r_off or 0), act, _p(aux, c_off) if aux is not None else None,
+                     float(drop_p), seed & 0xFFFFFFFFFFFFFFFF,
+                     int(bwd_act), _p(pre, c_off) if pre is not None else None, _p(rowsum),
+                     ctypes_ptr(ica), ctypes_ptr(icb), _p(ws), _GEMM_WS_BYTES, _st())
     _guard_post("esp_gemm_f32", ws, _GEMM_WS_BYTES)
     if _PROF is not None:
         ev1.record()
         # fused-epilogue streams the launch must move besides A, B, C: residual R and
         # pre-activation / derivative reads, aux writes (each one M x N fp32 tensor per batch)
         extra = 4.0 * M * N * batch * ((R is not None) + (aux is not None) + (pre is not None))
-        _PROF.append((2.0 * M * N * K * batch, ev0, ev1, (mode_a, mode_b, M, N, K, batch), extra))
+        key = (mode_a, mode_b, M, N, K, batch) + (("bp",) if bp is not None else ())
+        _PROF.append((2.0 * M * N * K * batch, ev0, ev1, key, extra))
 
 
 def gemm_bf16(M: int, N: int, K: int, A16, B16, C, *, lda, ldb, ldc, c_off=0, bias=None, alpha=1.0, beta=0.0,
@@ -351,13 +398,14 @@ def ctypes_ptr(arr):
 
 
 def linear_fwd(x2d, W, b, out, *, act=ACT_NONE, aux=None, drop_p=0.0, seed=0, alpha=1.0, R=None, beta=1.0,
-               out_off=0, ldo=None):
-    """out = alpha*drop(act(x W^T + b)) (+ beta*R); x (M,K), W (N,K)."""
+               out_off=0, ldo=None, b_weight=False):
+    """out = alpha*drop(act(x W^T + b)) (+ beta*R); x (M,K), W (N,K).  b_weight: W is a step-constant
+    weight that is not a parameter view (a re-laid copy): its split planes are cached like one."""
     M, K = x2d.shape
     N = W.shape[0]
     gemm(M, N, K, x2d, W, out, mode_a=KC, lda=x2d.stride(0), mode_b=KC, ldb=W.stride(0),
          ldc=ldo or N, c_off=out_off, bias=b, alpha=alpha, beta=beta if R is not None else 0.0, R=R,
-         act=act, aux=aux, drop_p=drop_p, seed=seed)
+         act=act, aux=aux, drop_p=drop_p, seed=seed, b_weight=b_weight)
     return out
 
 
@@ -370,13 +418,13 @@ def linear_bwd_data(dy, W, dx, *, accumulate=False):
     return dx
 
 
-def linear_bwd_data_act(dy, W, dx, pre, act, drop_p=0.0, seed=0):
+def linear_bwd_data_act(dy, W, dx, pre, act, drop_p=0.0, seed=0, b_weight=False):
     """dx = drop'(dy W) * act'(pre): the input gradient of w_2 fused with the backward of
     h = drop(act(pre)) (positionwise_feed_forward.py:32)."""
     M, N = dy.shape
     K = W.shape[1]
     gemm(M, K, N, dy, W, dx, mode_a=KC, lda=dy.stride(0), mode_b=RC, ldb=W.stride(0), ldc=dx.stride(0),
-         bwd_act=act, pre=pre, drop_p=drop_p, seed=seed)
+         bwd_act=act, pre=pre, drop_p=drop_p, seed=seed, b_weight=b_weight)
     return dx
 
 

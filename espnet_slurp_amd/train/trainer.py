@@ -349,6 +349,21 @@ class Trainer:
             e.stats[k].copy_(v)
         return e
 
+    def reset_dropout_stream(self):
+        """HIP-graph mode: re-derive the device dropout key from the (just seeded) CPU generator and
+        drop the captured graphs, whose host seeds were drawn at their capture.  Trainer.run calls
+        it after each epoch's set_all_random_seed, so every epoch's masks follow from (seed, epoch)
+        alone and a resumed run draws the masks of an uninterrupted one (eager steps draw their
+        seeds from the CPU generator per step already)."""
+        if not self.cuda_graph:
+            return
+        v = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64)
+        if self._key is None:
+            self._key = v.to(self.model.flat.flat.device)
+        else:
+            self._key.copy_(v)
+        self._graphs.clear()
+
     def sync_host_state(self):
         """Bring the host-side optimizer / scheduler counters up to date after graph replays,
         and count the optimizer steps the device skipped (non-finite gradient norm)."""
@@ -384,8 +399,9 @@ class Trainer:
         self.model.train()
         self.sync_host_state()
         up0, sk0 = self.n_updates, self.n_skipped
-        rec = _EpochRecorder(self, reporter, train=True) if hasattr(reporter, "register") else None
+        rec = _EpochRecorder(self, reporter, train=True, iterator=iterator) if hasattr(reporter, "register") else None
         it = iter(self._stop_aligned(iterator))
+        no_forward = False  # trainer.py:515-517: a no_forward_run batch makes the epoch valid
         t_step = time.perf_counter()
         while True:
             t0 = time.perf_counter()
@@ -394,7 +410,8 @@ class Trainer:
             except StopIteration:
                 break
             t_load = time.perf_counter() - t0
-            if self.options.no_forward_run:  # trainer.py:530-532
+            if self.options.no_forward_run:  # trainer.py:515-517, 530-532
+                no_forward = True
                 if rec is not None:
                     rec.push_empty(t_load)
                 continue
@@ -411,8 +428,9 @@ class Trainer:
         self.sync_host_state()
         if rec is not None:
             rec.flush()
-        # trainer.py:436-440: True when no optimizer step of the epoch was applied
-        return (self.n_skipped - sk0) == (self.n_updates - up0)
+        # trainer.py:436-440: True when no optimizer step of the epoch was applied (and no batch
+        # was passed over by no_forward_run, which the reference counts as valid)
+        return not no_forward and (self.n_skipped - sk0) == (self.n_updates - up0)
 
     @torch.no_grad()
     def validate_one_epoch(self, iterator: Iterable, reporter=None) -> None:
@@ -420,7 +438,7 @@ class Trainer:
         running statistics), per batch the stats weighted by the batch weight (recursive_average
         over the ranks: one fused all-reduce), iterator_stop across ranks."""
         self.model.eval()
-        rec = _EpochRecorder(self, reporter, train=False) if reporter is not None else None
+        rec = _EpochRecorder(self, reporter, train=False, iterator=iterator) if reporter is not None else None
         for _, batch in self._stop_aligned(iterator):
             if self.options.no_forward_run:
                 continue
@@ -463,6 +481,7 @@ class Trainer:
         for iepoch in range(start_epoch, o.max_epoch + 1):
             logging.info(f"{iepoch}/{o.max_epoch}epoch started")
             set_all_random_seed(o.seed + iepoch)
+            self.reset_dropout_stream()
             reporter.set_epoch(iepoch)
             with reporter.observe("train") as sub:
                 all_invalid = self.train_one_epoch(train_iter_factory.build_iter(iepoch), reporter=sub)
@@ -535,13 +554,18 @@ class _EpochRecorder:
     log_interval steps (and at the end) the snapshots come to the host in one copy and are
     registered in order, one reporter.next() per batch as the reference does."""
 
-    def __init__(self, trainer: Trainer, reporter, train: bool):
+    def __init__(self, trainer: Trainer, reporter, train: bool, iterator=None):
         self.t = trainer
         self.rep = reporter
         self.train = train
         self.items = []
         li = trainer.options.log_interval
-        self.log_interval = li if li is not None else 100
+        if li is None:  # trainer.py:489-493: max(len(iterator) // 20, 10), 100 without a length
+            try:
+                li = max(len(iterator) // 20, 10)
+            except TypeError:
+                li = 100
+        self.log_interval = li
         sch = trainer.scheduler
         self.sched_last = getattr(sch, "last_epoch", 0)
         self.n_logged = 0

@@ -72,6 +72,26 @@ int esp_f32_gemm_products(void);
  * tile sums the splits in fixed order; needs the zeroed ticket area of `work`, see above).
  * Initialised from ESP_SPLITK_INKERNEL.  Returns the previous mode. */
 int esp_set_splitk_mode(int mode);
+/* esp_gemm_f32 with B also given as its three bf16 split planes (esp_f32_to_planes of the fp32 B,
+ * b = hi + mid + lo exactly): the same fp32 split products as esp_gemm_f32 on the fp32 B, in the same
+ * order, bit for bit (split-K counts may differ: a different tile width), without splitting B in the
+ * GEMM's k-loop.  b_planes: plane 0; plane p at b_planes + p * b_pstride bf16 elements; ldbp, sbp1,
+ * sbp2 in bf16 elements.  Used when the fp32 compute type is active, mode_b is KC or RC and the planes
+ * qualify (16-B aligned, ldbp / strides / pstride % 8 == 0, K % 8 == 0 for KC, N % 8 == 0 for RC);
+ * otherwise -- or when the epilogue kind has no B-planes kernel -- the fp32 B (which may then not
+ * be NULL) is used.  Reference: every nn.Linear / Conv weight operand of the step (weights are
+ * split once per step, kernels.py). */
+int esp_gemm_f32_bp(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2, const float* A, long lda,
+                    long sa1, long sa2, const float* B, long ldb, long sb1, long sb2, float* C, long ldc,
+                    long sc1, long sc2, const float* bias, float alpha, float beta, const float* R, int act,
+                    float* aux, float drop_p, unsigned long long seed, int bwd_act, const float* pre, float* rowsum,
+                    const int* im2col_a, float* work, long work_bytes, const void* b_planes, long ldbp, long sbp1,
+                    long sbp2, long b_pstride, void* stream);
+/* The three bf16 planes of a rows x cols fp32 matrix x (row pitch ldx): plane p at y + p * pstride
+ * (bf16 elements, row pitch ldy), hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid), round to
+ * nearest even with exact fp32 residuals, so x = hi + mid + lo for every finite x.  Columns
+ * cols..ldy-1 are written 0.  ldy, pstride % 8 == 0, pstride >= rows * ldy, y 16-B aligned. */
+int esp_f32_to_planes(const float* x, void* y, long rows, int cols, long ldx, long ldy, long pstride, void* stream);
 /* bf16-operand GEMM (the C5 reduced-precision path): A and B bf16 (bits of __bf16 /
  * torch.bfloat16) in mode KC or RC as esp_gemm_f32 (KC: [rows][K]; RC: [K][rows], staged for
  * transposing LDS reads), fp32 accumulate; C, the epilogue (bias, act, aux, dropout, bwd_act /

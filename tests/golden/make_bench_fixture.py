@@ -16,8 +16,9 @@ implicit-im2col index ranges, attention grids with z = 512).
 
 Stored: the seed, lengths and target lengths (the inputs are regenerated from the seed by
 O.synthetic_batch), loss / loss_ctc / loss_att / acc, and per parameter the gradient L2
-norm, max |g| and a fixed slice of elements, for both precisions (the format of
-make_golden.fullsize_train_fixture, read by tests/helpers.grad_gate / loss_gate).
+norm, max |g| and a fixed slice of elements, for both precisions, plus the ReLU flip records of
+conv.0 and the decoder norm3 slices (flipfix.py) (the format of make_golden.fullsize_train_fixture,
+read by tests/helpers.grad_gate / loss_gate).
 Test infrastructure only: never imported by the product.
 """
 import gc
@@ -28,13 +29,15 @@ import zlib
 
 import numpy as np
 import torch
-import torch.nn.functional as F
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 
 from oracle import espnet_cpu as O  # noqa: E402
+
+sys.path.insert(0, HERE)
+import flipfix  # noqa: E402
 
 B, T, V, SEED = 128, 1500, 600, 71
 N_SLICE = 16
@@ -63,72 +66,21 @@ def slice_indices(name: str, numel: int) -> np.ndarray:
     return idx.astype(np.int64)
 
 
-class DecoderReluProbe:
-    """Records, per decoder layer, the FFN's ReLU pre-activation (w_1 output), its input (the
-    norm3 output) and the gradient reaching the ReLU output, so the effect of ReLU decisions
-    that fp32 rounding can flip is bounded (flip_bounds).  Wraps O.ffn for the decoder only."""
-
-    def __init__(self):
-        self.rec = {}
-        self._orig = O.ffn
-
-    def __enter__(self):
-        def ffn(P, pre, x, act, p_drop=0.0, training=True):
-            if not (pre.startswith("decoder.") and act == "relu"):
-                return self._orig(P, pre, x, act, p_drop, training)
-            h = O.linear(P, pre + ".w_1", x)
-            r = F.relu(h)
-            r.retain_grad()
-            self.rec[pre] = (x, h, r)
-            return O.linear(P, pre + ".w_2", O.dropout(r, p_drop, training))
-        O.ffn = ffn
-        return self
-
-    def __exit__(self, *exc):
-        O.ffn = self._orig
-
-
-def flip_bounds(P64, rec64, pre32, out):
-    """Decoder norm3 (the LayerNorm feeding the ReLU FFN) gradient slices: bound the change a
-    flipped ReLU decision can make.  For every pre-activation within tau of 0 (tau = 4x the
-    largest |fp32 - fp64| difference of that layer's pre-activations in the oracle's own fp32
-    run), flipping it changes d norm3.weight[c] by g[r,u] W1[u,c] xhat[r,c] and d norm3.bias[c]
-    by g[r,u] W1[u,c] (g: the gradient at the ReLU output).  Stored per tensor: the largest
-    bound over its slice elements ("flipb/<name>") and the count of near-zero decisions."""
-    for pre, (x, h, r) in rec64.items():
-        lay = pre[: -len(".feed_forward")]
-        tau = 4.0 * float((pre32[pre] - h.detach()).abs().max())
-        near = (h.detach().abs() < tau).nonzero()
-        W1 = P64[pre + ".w_1.weight"].detach()
-        gam, bet = P64[lay + ".norm3.weight"].detach(), P64[lay + ".norm3.bias"].detach()
-        xs = x.detach().reshape(-1, x.size(-1))
-        rows = near[:, 0] * h.size(1) + near[:, 1] if h.dim() == 3 else near[:, 0]
-        u = near[:, -1]
-        g = r.grad.reshape(-1, r.size(-1))[rows, u].abs()                 # (n,)
-        xhat = (xs[rows] - bet) / gam                                      # (n, D)
-        contrib = g[:, None] * W1[u].abs()                                 # (n, D)
-        for name, c in ((lay + ".norm3.bias", contrib), (lay + ".norm3.weight", contrib * xhat.abs())):
-            idx = slice_indices(name, c.size(1))
-            out["flipb/" + name] = np.float64(c[:, torch.from_numpy(idx)].sum(0).max().item()) if len(u) else 0.0
-            out["flipn/" + name] = np.int64(len(u))
-        print(f"{lay}: tau {tau:.3g}, {len(u)} ReLU decisions within tau of 0, norm3 slice bounds "
-              f"w {float(out['flipb/' + lay + '.norm3.weight']):.3g} b {float(out['flipb/' + lay + '.norm3.bias']):.3g}",
-              flush=True)
-
-
-def run(dt, tag, out, probe_out=None):
+def run(dt, tag, out, recs):
     cfg = bench_cfg()
     lens, ulens = bench_lengths()
     P = {k: v.requires_grad_(v.is_floating_point() and "running" not in k)
          for k, v in O.deterministic_params(cfg, SEED, dt).items()}
     speech, slen, text, tlen = O.synthetic_batch(B, T, 80, V, lens, ulens, SEED + 1)
     t0 = time.time()
-    with DecoderReluProbe() as probe:
+    # the ReLU decisions near 0 (Conv2dSubsampling, decoder FFNs) and their slice contributions
+    with flipfix.OracleProbe(O, P) as probe:
         loss, stats, _ = O.asr_forward(P, speech.to(dt), slen, text, tlen, cfg, bn_state={})
     print(f"{tag}: forward {time.time() - t0:.1f} s, loss {loss.item():.8f}", flush=True)
     t0 = time.time()
     loss.backward()
     print(f"{tag}: backward {time.time() - t0:.1f} s", flush=True)
+    recs[tag] = probe.rec.detach()
     out[f"loss_{tag}"] = np.float64(loss.item())
     for k in ("loss_ctc", "loss_att", "acc"):
         out[f"{k}_{tag}"] = np.float64(float(stats[k]))
@@ -141,8 +93,6 @@ def run(dt, tag, out, probe_out=None):
         out[f"gmax_{tag}/{n}"] = np.float64(g.abs().max().item())
         out[f"gidx/{n}"] = idx
         out[f"gs_{tag}/{n}"] = g[torch.from_numpy(idx)].numpy()
-    if probe_out is not None:
-        probe_out.update(P=P, rec=probe.rec)
 
 
 def main():
@@ -150,14 +100,15 @@ def main():
     torch.set_num_threads(n)
     print(f"bench fixture: B={B} T={T} on {n} threads", flush=True)
     out = {}
-    p32, p64 = {}, {}
-    run(torch.float32, "f32", out, p32)
-    pre32 = {k: h.detach().double() for k, (_, h, _) in p32["rec"].items()}
-    del p32
+    recs = {}
+    run(torch.float32, "f32", out, recs)
     gc.collect()
-    run(torch.float64, "f64", out, p64)
-    flip_bounds(p64["P"], p64["rec"], pre32, out)
-    del p64
+    run(torch.float64, "f64", out, recs)
+    gc.collect()
+    gs32 = {k[len("gs_f32/"):]: v for k, v in out.items() if k.startswith("gs_f32/")}
+    flipfix.flip_records(recs["f64"], recs["f32"], lambda n: out["gidx/" + n], out, gs32,
+                         log=lambda m: print(m, flush=True))
+    del recs
     gc.collect()
     lens, ulens = bench_lengths()
     out.update(lens=np.array(lens), ulens=np.array(ulens), seed=np.int64(SEED), B=np.int64(B), T=np.int64(T))

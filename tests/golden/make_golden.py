@@ -327,8 +327,10 @@ def fullsize_train_fixture(name: str, cfg, B=2, T=1500, lens=(1500, 1337), ulens
     slice of its elements.  train=False runs the reference in eval mode (validation step:
     no dropout, no SpecAug, BatchNorm from its running statistics)."""
     import time as _t
+    import flipfix
     build = build or (lambda: build_reference(cfg))
     out = {}
+    recs = {}
     F_ = cfg.enc.input_size
     for dt, tag in ((torch.float32, "f32"), (torch.float64, "f64")):
         t0 = _t.time()
@@ -337,8 +339,11 @@ def fullsize_train_fixture(name: str, cfg, B=2, T=1500, lens=(1500, 1337), ulens
         model.train(train)
         speech, slen, text, tlen = O.synthetic_batch(B, T, F_, cfg.vocab_size, list(lens), list(ulens), seed + 1)
         if with_grads:
-            loss, stats, _ = model(speech.to(dt), slen, text, tlen)
+            # the ReLU decisions near 0 and their slice contributions (flipfix.py)
+            with flipfix.ReferenceProbe(model) as probe:
+                loss, stats, _ = model(speech.to(dt), slen, text, tlen)
             loss.backward()
+            recs[tag] = probe.rec.detach()
             grad_summary(model, tag, out)
         else:
             with torch.no_grad():
@@ -353,6 +358,10 @@ def fullsize_train_fixture(name: str, cfg, B=2, T=1500, lens=(1500, 1337), ulens
                 out[f"ctc_argmax_{tag}"] = model.ctc.argmax(hs).numpy()
         print(f"{name} {tag}: loss {loss.item():.6f} ({_t.time() - t0:.1f} s)", flush=True)
         del model
+    if with_grads:
+        gs32 = {k[len("gs_f32/"):]: v for k, v in out.items() if k.startswith("gs_f32/")}
+        flipfix.flip_records(recs["f64"], recs["f32"], lambda n: out["gidx/" + n], out, gs32,
+                             log=lambda m: print(f"{name}: {m}", flush=True))
     out.update(lens=np.array(lens), ulens=np.array(ulens), seed=np.int64(seed), B=np.int64(B), T=np.int64(T))
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
 
@@ -700,6 +709,12 @@ if __name__ == "__main__":
                                                      num_blocks=17, rel_pos_type="latest"),
                         dec=O.DecCfg(attention_heads=8, linear_units=2048, num_blocks=6))
         fullsize_train_fixture("fullsize_c4_grad_latest", c4, seed=53)
+    if "c5grad" in which:  # C5 shape (SLURP-entity: d=512, H=8, FF 2048, 12 blocks, latest) with every
+        # parameter gradient (VERDICT r3 'next' 1a): the fp32 step and the bf16 step are gated against it
+        c5 = O.ModelCfg(vocab_size=600, enc=O.EncCfg(output_size=512, attention_heads=8, linear_units=2048,
+                                                     num_blocks=12, rel_pos_type="latest"),
+                        dec=O.DecCfg(attention_heads=8, linear_units=2048, num_blocks=6))
+        fullsize_train_fixture("fullsize_c5_grad_latest", c5, seed=57)
     if "slurp" in which:
         slurp_yaml_fixture()
     if "trainrun" in which:

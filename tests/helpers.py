@@ -135,22 +135,82 @@ def cfg_from_config(conf, dropout_zero=False):
         length_normalized_loss=conf["model_conf"]["length_normalized_loss"])
 
 
-# Conv2dSubsampling's first conv sits below two ReLUs whose pre-activations come within
-# fp32 rounding of 0 at full size (tools/relu_flip_diag.py: 53 conv2 outputs within 1e-5 of 0
-# at C2, B=2; the GPU's fp32 sum lands on the other side of 0 than fp64 for 1 of them): one
-# such discrete mask decision moves single elements of conv.0's gradient by ~3e-4 of its
-# max.  The reference's own fp32 run flips different ones (its slice error is 1e-4), so the
-# slice gate for these two tensors is 2e-3; their norm gate stays at max(1e-4, 2 e_ref).
-RELU_FLIP_SLICE_TOL = {"encoder.embed.conv.0.weight": 2e-3, "encoder.embed.conv.0.bias": 2e-3}
+class FlipProbe:
+    """The GPU model's ReLU decisions at the flip sites of tests/golden/flipfix.py, read from the
+    tensors the forward keeps for its backward: conv1 from z1 (NHWC [B, T1, F1, D], post-ReLU), conv2
+    from z2 ([B*T2*F2, D], post-ReLU), decoder layer l from its FFN's dh/dv (dact: keep * scale *
+    (v > 0), rows b * L + position).  Use around the forward: `with FlipProbe(model) as fp: ...`."""
+
+    def __init__(self, model):
+        self.model = model
+        self.ctx = {}
+
+    def __enter__(self):
+        from espnet_slurp_amd import blocks
+        self._b = blocks
+        self._sub, self._ffn = blocks.Conv2dSubsampling.fwd, blocks.PositionwiseFeedForward.fwd
+        probe = self
+
+        def sub(mod, *a, **k):
+            x, c = probe._sub(mod, *a, **k)
+            probe.ctx["conv"] = c
+            return x, c
+
+        def ffn(mod, *a, **k):
+            out, c = probe._ffn(mod, *a, **k)
+            probe.ctx[id(mod)] = c
+            return out, c
+        blocks.Conv2dSubsampling.fwd, blocks.PositionwiseFeedForward.fwd = sub, ffn
+        return self
+
+    def __exit__(self, *exc):
+        self._b.Conv2dSubsampling.fwd, self._b.PositionwiseFeedForward.fwd = self._sub, self._ffn
+
+    def decisions(self, site: str, idx: np.ndarray) -> np.ndarray:
+        c = self.ctx["conv"]
+        ix = torch.from_numpy(idx).to(c.z1.device)
+        if site == "conv1":
+            z = c.z1.view(c.B, c.T1, c.F1, -1)
+            b, ch, t, f = ix.unbind(1)
+            return (z[b, t, f, ch] > 0).to(torch.int8).cpu().numpy()
+        if site == "conv2":
+            z = c.z2.view(c.B, c.T2, c.F2, -1)
+            b, o, t, f = ix.unbind(1)
+            return (z[b, t, f, o] > 0).to(torch.int8).cpu().numpy()
+        assert site.startswith("dec"), site
+        ff = self.model.decoder.decoders[int(site[3:])].feed_forward
+        dact = self.ctx[id(ff)].dact
+        L = dact.shape[0] // c.B
+        b, p, u = ix.unbind(1)
+        return (dact[b * L + p, u] > 0).to(torch.int8).cpu().numpy()
 
 
-def grad_gate(model, g, skip_rel=1e-6):
-    """Per-tensor gradient gate of a full-size fixture (make_golden.fullsize_train_fixture):
-    the L2 norm and a fixed element slice must be as close to the fp64 reference as the
-    reference's own fp32 result is (x2), or within 1e-4 relative.  A fixture may carry, per
-    tensor, "flipb/<name>": a computed bound on how far the slice elements can move when ReLU
-    decisions within fp32 rounding of 0 flip (make_bench_fixture.flip_bounds: the decoder's
-    norm3 feeds a ReLU FFN); it is added to the slice gate.  Returns the failures."""
+def flip_corrected_slice(name, got_slice, g, flips):
+    """got_slice with every recorded ReLU decision near 0 set to the fp64 one (flipfix.py): minus
+    (s_gpu - s64) x contribution per site; (slice, the fixture's corrected fp32 slice or None)."""
+    pre = f"flip/{name}/"
+    sites = sorted({k[len(pre):].split("/")[0] for k in g if k.startswith(pre)})
+    if not sites:
+        return got_slice, None
+    assert flips is not None, f"{name}: the fixture holds ReLU flip records, pass flips=FlipProbe(...)"
+    s = got_slice.astype(np.float64).copy()
+    for site in sites:
+        idx = g[f"{pre}{site}/idx"]
+        if len(idx) == 0:
+            continue
+        sg = flips.decisions(site, idx).astype(np.float64)
+        s -= ((sg - g[f"{pre}{site}/s64"].astype(np.float64))[:, None] * g[f"{pre}{site}/c"]).sum(0)
+    return s, g[f"gs_f32c/{name}"]
+
+
+def grad_gate(model, g, skip_rel=1e-6, flips=None):
+    """Per-tensor gradient gate of a full-size fixture (make_golden.fullsize_train_fixture): the L2
+    norm and a fixed element slice must be as close to the fp64 reference as the reference's own
+    fp32 result is (x2), or within 1e-4 relative.  Slices of tensors right below a ReLU
+    (Conv2dSubsampling's conv.0, the decoder layers' norm3) are compared after the ReLU decisions
+    within fp32 rounding of 0 are set to the fp64 ones on both sides -- the GPU's read by `flips`
+    (FlipProbe), the reference fp32 run's stored -- with their exact contributions from the fixture
+    (tests/golden/flipfix.py).  Returns the failures."""
     scale = max(float(g["gmax_f64/" + n]) for n, _ in model.named_parameters())
     bad = []
     for n, p in model.named_parameters():
@@ -166,10 +226,11 @@ def grad_gate(model, g, skip_rel=1e-6):
         if e_gpu > max(1e-4, 2 * e_ref):
             bad.append((n, "norm", e_gpu, e_ref))
         s = got[torch.from_numpy(g["gidx/" + n])].numpy()
+        s, s32 = flip_corrected_slice(n, s, g, flips)
+        s32 = g["gs_f32/" + n] if s32 is None else s32
         es = float(np.abs(s - g["gs_f64/" + n]).max()) / gm
-        er = float(np.abs(g["gs_f32/" + n] - g["gs_f64/" + n]).max()) / gm
-        flip = float(g["flipb/" + n]) / gm if ("flipb/" + n) in g else 0.0
-        if es > max(1e-4, 2 * er, RELU_FLIP_SLICE_TOL.get(n, 0.0)) + flip:
+        er = float(np.abs(s32 - g["gs_f64/" + n]).max()) / gm
+        if es > max(1e-4, 2 * er):
             bad.append((n, "slice", es, er))
     return bad
 

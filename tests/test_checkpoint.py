@@ -292,3 +292,22 @@ def test_unique_key_registration():
             sub.register({"x": 2.0})
         sub.next()
     assert r.get_all_keys()[0] == (key, "x")
+
+
+def test_trainer_run_no_forward_run_all_epochs(tmp_path):
+    """no_forward_run (trainer.py:515-517, 530-532): every batch is passed over and the epoch counts
+    as VALID (all_steps_are_invalid = False), so Trainer.run goes through every epoch instead of
+    stopping after the first with 'gradients at all steps are invalid'; the reporter gets one
+    iter_time entry per batch.  Host only: no forward runs."""
+    from espnet_slurp_amd.train.trainer import Trainer, TrainerOptions
+    model, opt, sch, _ = _ours()
+    tr = Trainer(model, opt, sch, TrainerOptions(no_forward_run=True, max_epoch=2, output_dir=str(tmp_path)))
+
+    class _It:
+        def build_iter(self, epoch, shuffle=None):
+            return [([f"u{i}"], {}) for i in range(3)]
+
+    rep = tr.run(_It(), _It())
+    assert rep.get_epoch() == 2
+    assert tr.n_updates == 0 and tr.n_skipped == 0
+    assert (tmp_path / "2epoch.pth").exists()

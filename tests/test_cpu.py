@@ -159,7 +159,7 @@ def test_workspace_size_queries():
     assert W("esp_layernorm_bwd", M, 256) == 4 * 2 * 256 * ((M + 31) // 32)
     assert W("esp_colsum", 100, 7) == 4 * 7 * 4
     assert W("esp_ctc_loss", 128, 374, 40) == 8 * 2 * 128 * 374 * 81
-    assert W("esp_conv2_dgrad", 256) == 4 * 9 * 256 * 256
+    assert W("esp_conv2_dgrad", 256) == (4 + 6) * 9 * 256 * 256  # class weights + their bf16 split planes
     assert W("esp_grad_norm", 10 ** 8) == 8 * 1024
     assert W("esp_dwconv1d_wgrad", 128, 374, 256, 31) == 4 * 128 * ((374 + 63) // 64) * 256 * 31
     assert W("esp_relpos_dp", 128, 4, 374) == 4 * 4 * 16 * (2 * 374 - 1) * 64

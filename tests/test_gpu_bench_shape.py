@@ -14,7 +14,7 @@ import pytest
 import torch
 
 from oracle import espnet_cpu as O
-from tests.helpers import build_model, golden, grad_gate, load_seeded, loss_gate
+from tests.helpers import FlipProbe, build_model, golden, grad_gate, load_seeded, loss_gate
 
 pytestmark = pytest.mark.gpu
 
@@ -41,7 +41,8 @@ def test_bench_shape_c2_b128_step_vs_oracle(dev):
     load_seeded(model, cfg, int(g["seed"]))
     speech, slen, text, tlen = _batch(g, dev)
     model.train()
-    loss, stats, _ = model(speech, slen, text, tlen)
+    with FlipProbe(model) as fp:
+        loss, stats, _ = model(speech, slen, text, tlen)
     loss.backward()
     torch.cuda.synchronize()
     assert torch.isfinite(loss).item()
@@ -50,7 +51,7 @@ def test_bench_shape_c2_b128_step_vs_oracle(dev):
         ok, info = loss_gate(got, g, key, slack)
         assert ok, info
     assert abs(stats["acc"].item() - float(g["acc_f64"])) < 1e-6
-    bad = grad_gate(model, g)
+    bad = grad_gate(model, g, flips=fp)
     assert not bad, bad
 
 

@@ -121,6 +121,111 @@ def test_gemm_f32_nonfinite_operands(dev):
     assert (Cc[others].double() - ref).abs().max().item() < 1e-4
 
 
+def _with_bplanes(on, fn):
+    prev = K._BPLANES
+    K._BPLANES = on
+    try:
+        return fn()
+    finally:
+        K._BPLANES = prev
+
+
+def test_f32_to_planes_exact_split(dev):
+    """esp_f32_to_planes: hi + mid + lo == x exactly (fp64 sum) for finite x over 40 binades,
+    hi == bf16(x) (round to nearest even, torch's cast), zeroed pitch padding."""
+    x = (_r(37, 203, seed=5) * torch.exp2(torch.randint(-20, 20, (37, 203), generator=torch.Generator().manual_seed(6)).float()))
+    xd = x.to(dev)
+    pl, ldp, ps = K.planes(xd, 0, 37, 203, 203)
+    torch.cuda.synchronize()
+    assert ldp == 208 and ps == 37 * 208
+    p = pl.cpu().view(3, 37, 208)
+    s = p[0, :, :203].double() + p[1, :, :203].double() + p[2, :, :203].double()
+    assert torch.equal(s, x.double())
+    assert torch.equal(p[0, :, :203], x.to(torch.bfloat16))
+    assert not p[:, :, 203:].float().any()
+
+
+@pytest.mark.parametrize("shape", [(300, 260, 128), (1000, 1024, 96), (129, 64, 200), (6000, 256, 192)])
+@pytest.mark.parametrize("mb", [0, 1])
+def test_gemm_b_planes_bit_exact(dev, shape, mb):
+    """B as its three split planes (esp_gemm_f32_bp) gives the in-register split's result bit for bit
+    (same six products, same order) on unsplit launches (K < 256: no split-K), with the fused
+    epilogues of the weight-B call sites: forward bias + Swish + dropout + derivative (FFN w_1),
+    bias + dropout + residual, input gradient * derivative (FFN w_2 backward), residual accumulation."""
+    M, N, Kk = shape
+    A = _r(M, Kk, seed=11).to(dev)
+    B = (_r(N, Kk, seed=12) if mb == K.KC else _r(Kk, N, seed=12)).to(dev)
+    bias = _r(N, seed=13).to(dev)
+    R = _r(M, N, seed=14).to(dev)
+    pre = _r(M, N, seed=15).to(dev)
+    cases = [dict()]
+    if mb == K.KC:
+        cases += [dict(bias=bias, act=K.ACT_SWISH | K.ACT_AUX_DERIV, aux="aux", drop_p=0.1, seed=7),
+                  dict(bias=bias, drop_p=0.1, seed=9, R=R, beta=1.0, alpha=0.5)]
+    else:
+        cases += [dict(bwd_act=K.ACT_MUL, pre=pre), dict(R=R, beta=1.0)]
+    for kw in cases:
+        outs = []
+        for on in (False, True):
+            C = torch.empty(M, N, device=dev)
+            aux = torch.empty(M, N, device=dev) if kw.get("aux") else None
+            k2 = dict(kw)
+            if aux is not None:
+                k2["aux"] = aux
+            _with_bplanes(on, lambda: K.gemm(M, N, Kk, A, B, C, mode_a=K.KC, lda=Kk, mode_b=mb, ldb=B.stride(0), ldc=N,
+                                             b_weight=True, **k2))
+            outs.append((C, aux))
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0][0], outs[1][0]), (kw.keys(), (outs[0][0] - outs[1][0]).abs().max().item())
+        if outs[0][1] is not None:
+            assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("shape", [(2048, 1024, 256), (47872 // 4, 256, 1024), (1000, 600, 2048), (512, 768, 4864)])
+@pytest.mark.parametrize("mb", [0, 1])
+def test_gemm_b_planes_split_k_accuracy(dev, shape, mb):
+    """Long-K weight-B GEMMs (split-K may differ from the fp32-B launch): as accurate as the host's
+    fp32 matmul against fp64 (the gate of test_gemm_f32_accuracy_vs_fp64) and within 2e-7 relative
+    of the in-register split."""
+    M, N, Kk = shape
+    g = torch.Generator().manual_seed(Kk + M + mb)
+    A = torch.randn(M, Kk, generator=g)
+    B = torch.randn(Kk, N, generator=g)
+    Bd = (B.t().contiguous() if mb == K.KC else B).to(dev)
+    Ad = A.to(dev)
+    Cs = []
+    for on in (False, True):
+        C = torch.empty(M, N, device=dev)
+        _with_bplanes(on, lambda: K.gemm(M, N, Kk, Ad, Bd, C, mode_a=K.KC, lda=Kk, mode_b=mb, ldb=Bd.stride(0),
+                                         ldc=N, b_weight=True))
+        Cs.append(C.cpu().double())
+    ref = A.double() @ B.double()
+    den = A.double().abs() @ B.double().abs()
+    r = (Cs[1] - ref).abs() / den
+    r32 = ((A @ B).double() - ref).abs() / den
+    assert r.max().item() <= 2.0 * r32.max().item(), (r.max().item(), r32.max().item())
+    assert ((Cs[1] - Cs[0]).abs() / den).max().item() <= 2e-7
+
+
+def test_gemm_b_planes_conv2_forward(dev):
+    """The conv2 forward (implicit-im2col A, bias + ReLU epilogue) on B planes equals the fp32-B launch
+    bit for bit (K = 9 C = 2304 slabs, no split-K: the grid fills the chip)."""
+    Bn, H, W, C = 4, 41, 39, 64
+    Ho, Wo = (H - 3) // 2 + 1, (W - 3) // 2 + 1
+    z1 = _r(Bn * H * W * C, seed=31).to(dev)
+    w = _r(C, 9 * C, seed=32, scale=0.05).to(dev)
+    bias = _r(C, seed=33).to(dev)
+    outs = []
+    for on in (False, True):
+        out = torch.empty(Bn * Ho * Wo, C, device=dev)
+        _with_bplanes(on, lambda: K.gemm(Bn * Ho * Wo, C, 9 * C, z1, w, out, mode_a=K.I2C_KC, lda=0, mode_b=K.KC,
+                                         ldb=9 * C, ldc=C, bias=bias, act=K.ACT_RELU, ic_a=(H, W, C, Ho, Wo),
+                                         b_weight=True))
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_gemm_epilogue(dev):
     M, N, Kk = 257, 130, 64
     X, W, b = _r(M, Kk, seed=3), _r(N, Kk, seed=4), _r(N, seed=5)

@@ -36,13 +36,13 @@ class _Factory:
                 for ids, b in self.items[r:] + self.items[:r]]
 
 
-def _trainer(dev, out, graph, max_epoch=None):
+def _trainer(dev, out, graph, max_epoch=None, dropout=None):
     from espnet_slurp_amd.optimizers.fused_adam import FusedAdam
     from espnet_slurp_amd.schedulers.warmup_lr import WarmupLR
     from espnet_slurp_amd.train.trainer import Trainer, TrainerOptions
     ref = json.load(open(os.path.join(GOLDEN, "trainrun_ref.json")))
     cfg = small_cfg("latest")
-    model = build_model(cfg, dev)
+    model = build_model(cfg, dev, dropout=dropout)
     load_seeded(model, cfg, ref["seed"])
     a = ref["adam"]
     opt = FusedAdam(model.parameters(), model.flat, lr=a["lr"], betas=tuple(a["betas"]), eps=a["eps"],
@@ -80,12 +80,13 @@ def test_trainer_run_matches_reference(dev, tmp_path, graph):
     assert tr.n_updates == 9 and tr.n_skipped == 0
 
 
-def test_trainer_run_resume(dev, tmp_path):
+@pytest.mark.parametrize("graph", [False, True])
+def test_trainer_run_resume(dev, tmp_path, graph):
     """Stop after 2 epochs, resume from checkpoint.pth in a fresh trainer for the 3rd
     (trainer.py:196-210): the same reporter values and files as one 3-epoch run."""
-    tr, ref = _trainer(dev, tmp_path, False, max_epoch=2)
+    tr, ref = _trainer(dev, tmp_path, graph, max_epoch=2)
     tr.run(_Factory(TRAIN, dev), _Factory(VALID, dev))
-    tr2, _ = _trainer(dev, tmp_path, False)
+    tr2, _ = _trainer(dev, tmp_path, graph)
     rep = tr2.run(_Factory(TRAIN, dev), _Factory(VALID, dev))
     assert rep.get_epoch() == 3
     for e, per in ref["values"].items():
@@ -95,3 +96,30 @@ def test_trainer_run_resume(dev, tmp_path):
                 tol = 1e-9 if k.startswith("optim") else (2e-3 if k == "acc" else 2e-4 * max(1.0, abs(v)))
                 assert abs(got - v) <= tol, (e, ph, k, got, v)
     assert sorted(p.name for p in tmp_path.iterdir()) == ref["files"]
+
+
+def test_trainer_run_resume_graph_dropout_masks(dev, tmp_path):
+    """HIP-graph mode WITH dropout: each epoch's device dropout key is re-derived from
+    the CPU generator right after set_all_random_seed(seed + epoch) and the graphs are recaptured
+    (Trainer.reset_dropout_stream), so 2 epochs + a resumed 3rd draw the masks of 3 uninterrupted
+    epochs: every epoch-3 reporter value is equal."""
+    a, b = tmp_path / "a", tmp_path / "b"
+    a.mkdir()
+    b.mkdir()
+    tr, _ = _trainer(dev, a, True, max_epoch=3, dropout=0.1)
+    rep_a = tr.run(_Factory(TRAIN, dev), _Factory(VALID, dev))
+    tr1, _ = _trainer(dev, b, True, max_epoch=2, dropout=0.1)
+    tr1.run(_Factory(TRAIN, dev), _Factory(VALID, dev))
+    tr2, _ = _trainer(dev, b, True, max_epoch=3, dropout=0.1)
+    rep_b = tr2.run(_Factory(TRAIN, dev), _Factory(VALID, dev))
+    assert rep_b.get_epoch() == 3
+    for ph in ("train", "valid"):
+        for k in ("loss", "loss_att", "loss_ctc", "acc"):
+            va, vb = rep_a.get_value(ph, k, epoch=3), rep_b.get_value(ph, k, epoch=3)
+            assert abs(va - vb) <= 1e-6 * max(1.0, abs(va)), (ph, k, va, vb)
+    # and dropout was on: epoch 3's training loss differs from a dropout-free run's
+    c = tmp_path / "c"
+    c.mkdir()
+    tr0, _ = _trainer(dev, c, True, max_epoch=3)
+    rep_c = tr0.run(_Factory(TRAIN, dev), _Factory(VALID, dev))
+    assert abs(rep_c.get_value("train", "loss", epoch=3) - rep_a.get_value("train", "loss", epoch=3)) > 1e-4

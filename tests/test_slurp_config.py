@@ -13,7 +13,7 @@ import pytest
 import torch
 
 from oracle import espnet_cpu as O
-from tests.helpers import cfg_from_config, golden, grad_gate, loss_gate, slurp_args, slurp_config
+from tests.helpers import FlipProbe, cfg_from_config, golden, grad_gate, loss_gate, slurp_args, slurp_config
 
 
 def _build(dev, **kw):
@@ -74,12 +74,13 @@ def test_slurp_yaml_train_step_grads(dev):
                           strict=True)
     model.train()
     speech, slen, text, tlen = _batch(g, conf)
-    loss, stats, _ = model(speech.to(dev), slen, text, tlen)
+    with FlipProbe(model) as fp:
+        loss, stats, _ = model(speech.to(dev), slen, text, tlen)
     loss.backward()
     torch.cuda.synchronize()
     for key, got, slack in (("loss", loss.item(), 0.0), ("loss_att", stats["loss_att"].item(), 0.0),
                             ("loss_ctc", stats["loss_ctc"].item(), 2e-4)):
         ok, info = loss_gate(got, g, key, slack)
         assert ok, info
-    bad = grad_gate(model, g)
+    bad = grad_gate(model, g, flips=fp)
     assert not bad, bad

@@ -1,0 +1,77 @@
+"""B-planes GEMM (esp_gemm_f32_bp, PREC 3) vs the in-register split (PREC 0) on the weight-B
+shapes of the C2 step at B=128: forward (KC x KC) and input-gradient (KC x RC) linears and the
+conv2 forward.  Planes made once (param_cast_scope), as in the Trainer step.  Prints per shape
+the kernel time of both and the max |difference| (0 when no split-K)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from espnet_slurp_amd import kernels as K  # noqa: E402
+
+NB = int(os.environ.get("BP_BENCH_B", "128"))
+M = NB * 374
+SHAPES = [  # (mode_a, mode_b, M, N, K, label)
+    (0, 0, M, 1024, 256, "ffn w1 fwd"),
+    (0, 0, M, 256, 1024, "ffn w2 fwd"),
+    (0, 1, M, 1024, 256, "ffn w2 dX"),
+    (0, 1, M, 256, 1024, "ffn w1 dX"),
+    (0, 0, M, 768, 256, "qkv fwd"),
+    (0, 1, M, 256, 768, "qkv dX"),
+    (0, 0, M, 256, 256, "out fwd"),
+    (0, 1, M, 256, 256, "out dX"),
+    (0, 0, M, 512, 256, "pw1 fwd"),
+    (0, 1, M, 256, 512, "pw1 dX"),
+    (2, 0, NB * 374 * 19, 256, 2304, "conv2 fwd"),
+    (0, 0, NB * 41, 256, 256, "dec q fwd"),
+    (0, 0, NB * 41, 2048, 256, "dec w1 fwd"),
+]
+
+
+def run(ma, mb, m, n, k, reps=10):
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(m + n + k)
+    ic_a = None
+    if ma == 2:
+        ic_a = (749, 39, 256, 374, 19)
+        A = torch.randn(NB * 749 * 39 * 256, device=dev, generator=g)
+        lda = 0
+    else:
+        A = torch.randn(m * k, device=dev, generator=g)
+        lda = k
+    B = torch.randn(n * k, device=dev, generator=g)
+    ldb = k if mb == 0 else n
+    out = {}
+    for bp in (False, True):
+        C = torch.empty(m * n, device=dev)
+        kw = dict(mode_a=ma, lda=lda, mode_b=mb, ldb=ldb, ldc=n, ic_a=ic_a, b_weight=bp)
+        with K.param_cast_scope():
+            for _ in range(2):
+                K.gemm(m, n, k, A, B, C, **kw)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                K.gemm(m, n, k, A, B, C, **kw)
+            e1.record()
+            torch.cuda.synchronize()
+        out[bp] = (e0.elapsed_time(e1) / reps, C)
+    d = (out[True][1] - out[False][1]).abs().max().item()
+    return out[False][0], out[True][0], d
+
+
+def main():
+    tot0 = tot1 = 0.0
+    for ma, mb, m, n, k, label in SHAPES:
+        t0, t1, d = run(ma, mb, m, n, k)
+        fl = 2.0 * m * n * k
+        tot0 += t0
+        tot1 += t1
+        print(f"{label:12s} ({ma},{mb},{m},{n},{k})  split {1e3 * t0:8.1f} us {fl / t0 / 1e9:6.1f} TF/s   "
+              f"planes {1e3 * t1:8.1f} us {fl / t1 / 1e9:6.1f} TF/s   x{t0 / t1:5.2f}  maxdiff {d:.3g}", flush=True)
+    print(f"total split {tot0:.3f} ms planes {tot1:.3f} ms")
+
+
+if __name__ == "__main__":
+    main()
