@@ -61,7 +61,26 @@ def run(ma, mb, m, n, k, reps=10):
     return out[False][0], out[True][0], d
 
 
+def one(i, bp, reps):
+    """one shape, one mode, `reps` launches (for rocprofv3 --pmc passes)"""
+    ma, mb, m, n, k, label = SHAPES[i]
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(m + n + k)
+    ic_a = (749, 39, 256, 374, 19) if ma == 2 else None
+    A = torch.randn(NB * 749 * 39 * 256 if ma == 2 else m * k, device=dev, generator=g)
+    B = torch.randn(n * k, device=dev, generator=g)
+    C = torch.empty(m * n, device=dev)
+    kw = dict(mode_a=ma, lda=0 if ma == 2 else k, mode_b=mb, ldb=k if mb == 0 else n, ldc=n, ic_a=ic_a, b_weight=bp)
+    with K.param_cast_scope():
+        for _ in range(reps):
+            K.gemm(m, n, k, A, B, C, **kw)
+    torch.cuda.synchronize()
+    print(label, "bp" if bp else "split", "done")
+
+
 def main():
+    if len(sys.argv) > 1:
+        return one(int(sys.argv[1]), sys.argv[2] == "1", int(sys.argv[3]) if len(sys.argv) > 3 else 5)
     tot0 = tot1 = 0.0
     for ma, mb, m, n, k, label in SHAPES:
         t0, t1, d = run(ma, mb, m, n, k)
