@@ -32,6 +32,8 @@ SIGNATURES = {
     "esp_gemm_f32_bp": [I, I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, L, P, F, F, P, I, P, F, U64, I, P, P,
                         P, P, L, P, L, L, L, L, P],
     "esp_f32_to_planes": [P, P, L, I, L, L, L, P],
+    "esp_gemm_f32_pl": [I, I, I, I, I, I, I, P, L, L, L, P, L, L, L, L, P, L, L, L, P, L, L, L, L, P, L, L, L, P, F, F,
+                        P, I, P, F, U64, I, P, P, I, L, P, L, P],
     "esp_set_gemm_compute": [I],
     "esp_get_gemm_compute": [],
     "esp_f32_gemm_products": [],
@@ -51,6 +53,7 @@ SIGNATURES = {
     "esp_set_rng_key": [P],
     "esp_rng_advance": [P, P],
     "esp_layernorm_fwd": [P, P, P, P, P, P, I, I, F, P],
+    "esp_layernorm_fwd_planes": [P, P, P, P, L, L, I, P, P, I, I, F, P],
     "esp_layernorm_bwd": [P, P, P, P, P, P, I, P, P, I, I, P, L, P],
     "esp_colsum": [P, I, I, L, P, I, P, L, P],
     "esp_glu_fwd": [P, P, L, I, P],
@@ -59,6 +62,7 @@ SIGNATURES = {
     "esp_dwconv1d_wgrad": [P, P, P, I, I, I, I, P, L, P, P],
     "esp_bn_swish_fwd": [P, P, P, P, P, P, P, P, F, F, I, I, P, L, I, P, P],
     "esp_bn_swish_eval": [P, P, P, P, P, P, F, I, I, P, P, P],
+    "esp_bn_swish_fwd_planes": [P, P, P, P, L, L, I, P, P, P, P, F, F, I, I, P, L, I, P, P],
     "esp_bn_swish_bwd": [P, P, P, P, P, P, P, P, P, I, I, P, L, P, I, P, P],
     "esp_heads_split": [P, L, I, I, I, I, I, P, P, P],
     "esp_heads_split2": [P, L, I, I, I, I, I, P, P, P, P, P],

@@ -41,11 +41,11 @@ class DecoderLayer(nn.Module):
 
     def fwd(self, x, mem, B, L, Tm, tgt_klen, mem_klen, seeds, training):
         c = Ctx()
-        h, c.ln1 = self.norm1.fwd(x)
+        h, c.ln1 = self.norm1.fwd(x, gemm_only=True)
         x, c.sa = self.self_attn.fwd(h, x, B, L, tgt_klen, True, self.p, seeds, training)
-        h, c.ln2 = self.norm2.fwd(x)
+        h, c.ln2 = self.norm2.fwd(x, gemm_only=True)
         x, c.src = self.src_attn.fwd(h, x, B, L, mem_klen, False, self.p, seeds, training, mem=mem, Tk=Tm)
-        h, c.ln3 = self.norm3.fwd(x)
+        h, c.ln3 = self.norm3.fwd(x, gemm_only=True)
         x, c.ff = self.feed_forward.fwd(h, x, 1.0, self.p, seeds, training)
         return x, c
 

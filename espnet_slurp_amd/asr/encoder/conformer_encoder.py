@@ -49,14 +49,14 @@ class EncoderLayer(nn.Module):
         c = Ctx()
         p = self.p
         if self.feed_forward_macaron is not None:
-            h, c.ln_mac = self.norm_ff_macaron.fwd(x)
+            h, c.ln_mac = self.norm_ff_macaron.fwd(x, gemm_only=True)
             x, c.ffm = self.feed_forward_macaron.fwd(h, x, self.ff_scale, p, seeds, training)
-        h, c.ln_mha = self.norm_mha.fwd(x)
+        h, c.ln_mha = self.norm_mha.fwd(x, gemm_only=True)
         x, c.mha = self.self_attn.fwd(h, x, pos, klen, B, T, p, seeds, training, tvalid=tvalid)
         if self.conv_module is not None:
-            h, c.ln_conv = self.norm_conv.fwd(x)
+            h, c.ln_conv = self.norm_conv.fwd(x, gemm_only=True)
             x, c.conv = self.conv_module.fwd(h, x, B, T, p, seeds, training, tvalid=tvalid)
-        h, c.ln_ff = self.norm_ff.fwd(x)
+        h, c.ln_ff = self.norm_ff.fwd(x, gemm_only=True)
         x, c.ff = self.feed_forward.fwd(h, x, self.ff_scale, p, seeds, training)
         if self.conv_module is not None:
             x, c.ln_final = self.norm_final.fwd(x)

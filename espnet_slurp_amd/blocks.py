@@ -83,12 +83,19 @@ class LayerNorm(nn.Module):
         self.bias = ref.bias
         self.eps = eps
 
-    def fwd(self, x2d):
+    def fwd(self, x2d, gemm_only: bool = False):
+        """gemm_only: y feeds only GEMMs (a projection and its weight gradient) -- written as
+        kernels.Planes in the current compute mode (kernels.planes_mode), else fp32."""
         M, D = x2d.shape
-        y = empty(M, D, like=x2d)
         mean = empty(M, like=x2d)
         rstd = empty(M, like=x2d)
-        K.layernorm_fwd(x2d, self.weight, self.bias, y, mean, rstd, self.eps)
+        n = K.planes_mode() if gemm_only and D % 4 == 0 else 0
+        if n:
+            y = K.Planes(M, D, x2d.device, n)
+            K.layernorm_fwd_planes(x2d, self.weight, self.bias, y, mean, rstd, self.eps)
+        else:
+            y = empty(M, D, like=x2d)
+            K.layernorm_fwd(x2d, self.weight, self.bias, y, mean, rstd, self.eps)
         return y, Ctx(x=x2d, mean=mean, rstd=rstd)
 
     def bwd(self, ctx, dy, dx_acc):
@@ -120,7 +127,8 @@ class PositionwiseFeedForward(nn.Module):
         # the w_1 epilogue stores h = drop(act(v)) and, instead of v, the local derivative
         # dh/dv = keep * scale * act'(v): the backward epilogue is then a single multiply
         dact = empty(M, H, like=x2d)
-        h = empty(M, H, like=x2d)
+        # h feeds only w_2 (forward and weight gradient): written as planes by the w_1 epilogue
+        h = K.Planes(M, H, x2d.device) if K.planes_mode() == 3 and H % 8 == 0 else empty(M, H, like=x2d)
         p_in = self.p if training else 0.0
         s1, s2 = seeds.next(), seeds.next()
         self.w_1.fwd(x2d, h, act=self.act | K.ACT_AUX_DERIV, aux=dact, drop_p=p_in, seed=s1)
@@ -225,7 +233,10 @@ class RelPositionMultiHeadedAttention(nn.Module):
             del bd
         attn = ac
         pv = pdrop if pdrop is not None else attn
-        ctx_ = empty(M, D, like=x2d)
+        # ctx feeds only linear_out (forward and weight gradient): planes from the P.V epilogue (the
+        # score-gradient epilogue, ESP_ATTN_DSCORES, reads it in fp32)
+        ctx_ = (K.Planes(M, D, x2d.device) if K.planes_mode() == 3 and D % 8 == 0 and not K.ATTN_DSCORES
+                else empty(M, D, like=x2d))
         K.gemm(T, dk, T, pv, qkv, ctx_, mode_a=K.KC, lda=Tp, mode_b=K.RC, ldb=3 * D, ldc=D, b_off=2 * D,
                batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * 3 * D), sc=(dk, T * D))
         out = empty(M, D, like=x2d)
@@ -391,7 +402,7 @@ class MultiHeadedAttention(nn.Module):
         pdrop = empty(Z * Tq * Tkp, like=xq) if pa > 0 else None
         K.attn_softmax_fwd(sc, None, 0, 0, math.sqrt(dk), klen, B, causal, sc, pdrop, pa, sa, Z, Tq, Tk, lds=Tkp)
         pv = pdrop if pdrop is not None else sc
-        ctx_ = empty(B * Tq, D, like=xq)
+        ctx_ = K.Planes(B * Tq, D, xq.device) if K.planes_mode() == 3 and D % 8 == 0 else empty(B * Tq, D, like=xq)
         K.gemm(Tq, dk, Tk, pv, kvb, ctx_, mode_a=K.KC, lda=Tkp, mode_b=K.RC, ldb=kvld, ldc=D, b_off=voff,
                batch=Z, nb2=B, sa=(B * Tq * Tkp, Tq * Tkp), sb=(dk, Tk * kvld), sc=(dk, Tq * D))
         out = empty(B * Tq, D, like=xq)
@@ -472,10 +483,12 @@ class ConvolutionModule(nn.Module):
         K.glu_fwd(u, g)
         y = empty(M, D, like=x2d)
         K.dwconv1d(g, self.depthwise_conv.weight, self.depthwise_conv.bias, y, B, T, D, self.kernel_size, tvalid=tvalid)
-        s = empty(M, D, like=x2d)
         mean = empty(D, like=x2d)
         rstd = empty(D, like=x2d)
         bn = self.norm
+        # s feeds only pointwise_conv2 (forward and weight gradient): planes in training mode
+        npl = K.planes_mode() if training and D % 8 == 0 else 0
+        s = K.Planes(M, D, x2d.device, npl) if npl else empty(M, D, like=x2d)
         if training:
             K.bn_swish_fwd(y, bn.weight, bn.bias, s, mean, rstd, bn.running_mean, bn.running_var,
                            momentum=bn.momentum, eps=bn.eps, T=T, tvalid=tvalid)

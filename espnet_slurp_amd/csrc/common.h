@@ -98,6 +98,45 @@ __device__ __forceinline__ float fast_sigmoid(float v) {
   return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(v * -1.4426950408889634f));
 }
 
+// ---------------------------------------------------------------- fp32 -> bf16 split planes
+// v = hi + mid + lo exactly (finite v): hi = bf16(v), mid = bf16(v - hi), lo = bf16(v - hi - mid),
+// round to nearest even, both residuals exact fp32 differences.  One element pair per call, each part
+// packed as bf16x2 (element a in the low half): one v_cvt_pk_bf16_f32 per part, the parts' fp32
+// values taken back from the packed bits.  The GEMMs' in-register split (gemm_kernels.h
+// split3_bf16) and every producer of planes (esp_f32_to_planes, LayerNorm, GEMM epilogues) use this,
+// so a planes operand holds exactly the values the in-register split would form.
+__device__ __forceinline__ void split3_pair(float a, float b, uint32_t& hi, uint32_t& mid, uint32_t& lo) {
+  typedef __attribute__((ext_vector_type(2))) float f2;
+  typedef __attribute__((ext_vector_type(2))) __bf16 b2;
+  const uint32_t hp = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){a, b}, b2));
+  const float ra = a - __uint_as_float(hp << 16), rb = b - __uint_as_float(hp & 0xffff0000u);
+  const uint32_t mp = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){ra, rb}, b2));
+  const float sa = ra - __uint_as_float(mp << 16), sb = rb - __uint_as_float(mp & 0xffff0000u);
+  hi = hp;
+  mid = mp;
+  lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){sa, sb}, b2));
+}
+// bf16x2 (round to nearest even) of a pair: the n = 1 "planes" (the reduced-precision operand)
+__device__ __forceinline__ uint32_t bf16_pair(float a, float b) {
+  typedef __attribute__((ext_vector_type(2))) float f2;
+  typedef __attribute__((ext_vector_type(2))) __bf16 b2;
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){a, b}, b2));
+}
+// store 4 consecutive values (c % 4 == 0) of a planes matrix: n = 3 split planes or n = 1 bf16 plane
+__device__ __forceinline__ void store_planes4(uint16_t* y, long off, long ps, int n, float a, float b, float c,
+                                              float d) {
+  if (n == 3) {
+    uint32_t h0, m0, l0, h1, m1, l1;
+    split3_pair(a, b, h0, m0, l0);
+    split3_pair(c, d, h1, m1, l1);
+    *reinterpret_cast<uint2*>(y + off) = make_uint2(h0, h1);
+    *reinterpret_cast<uint2*>(y + off + ps) = make_uint2(m0, m1);
+    *reinterpret_cast<uint2*>(y + off + 2 * ps) = make_uint2(l0, l1);
+  } else {
+    *reinterpret_cast<uint2*>(y + off) = make_uint2(bf16_pair(a, b), bf16_pair(c, d));
+  }
+}
+
 // ---------------------------------------------------------------- reductions (wave64)
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

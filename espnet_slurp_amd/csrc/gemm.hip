@@ -164,11 +164,16 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
     if (rows >= (1L << 24) || rows * g.b.ic.C >= (1L << 32)) return false;
   }
   int kind = g.splits > 1 ? EPI_PLAIN : epi_kind_spec(g);
+  if (g.cpn) {  // planes output: only its specialised kinds, no fallback kind
+    if (kind < 0 || !g.wide) return false;
+    if (kind == EPI_P0_PL && !(MA == KC && MB == RC)) return false;
+    if ((kind == EPI_FFN_SWISH_PL || kind == EPI_FFN_RELU_PL) && !(MA == KC && MB == KC)) return false;
+  }
   if (kind == EPI_SMB && !(MA == KC && MB == KC && g.bf16 == 0)) return false;
-  if (((kind == EPI_BMUL || kind == EPI_RMASK) && !can_spec_bwd) || ((kind == EPI_P0 || kind == EPI_PR) && !can_pspec) ||
+  if (!g.cpn && (((kind == EPI_BMUL || kind == EPI_RMASK) && !can_spec_bwd) || ((kind == EPI_P0 || kind == EPI_PR) && !can_pspec) ||
       (kind == EPI_RMASKMAP && !(MA == I2CT_KC && MB == RC)) ||
       (kind == EPI_BRELU && !can_brelu) ||
-      (kind >= EPI_BIAS && kind <= EPI_FFN_RELU && !can_spec_fwd))
+      (kind >= EPI_BIAS && kind <= EPI_FFN_RELU && !can_spec_fwd)))
     kind = epi_kind(g);
   if ((kind == EPI_FWD && !can_fwd) || (kind == EPI_BWD && !can_bwd)) return false;
   GldsArgs x{};
@@ -203,15 +208,26 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
   const int prec = g.bf16;
   if (kind == EPI_PLAIN) return glds_launch_plain(MA, MB, BNT, prec, rs, grid, st, g, x);
   if (kind == EPI_FWD || kind == EPI_BWD) return glds_launch_epi(MA, MB, BNT, prec, kind, grid, st, g, x);
-  if (kind == EPI_P0 || kind == EPI_PR || kind == EPI_SMB) return glds_launch_pspec(MA, MB, BNT, prec, kind, grid, st, g, x);
+  if (kind == EPI_P0 || kind == EPI_PR || kind == EPI_SMB || kind == EPI_P0_PL)
+    return glds_launch_pspec(MA, MB, BNT, prec, kind, grid, st, g, x);
   return glds_launch_spec(MA, MB, BNT, prec, kind, grid, st, g, x);
 }
 
 template <int MA, int MB>
-int launch(const GemmArgs& g0, int batch, hipStream_t st, const Operand* b_fp32 = nullptr) {
+int launch(const GemmArgs& g0, int batch, hipStream_t st, const Operand* b_fp32 = nullptr,
+           const Operand* a_fp32 = nullptr) {
   bool done = false;
   if (g0.bnt == 64 || g0.bnt == 128) done = launch_glds(MA, MB, g0, batch, st);
   GemmArgs g = g0;
+  if (!done && g.bf16 == 5) {  // no planes x planes kernel for this epilogue kind: the fp32 A operand
+    if (!a_fp32 || !a_fp32->p) {
+      esp::set_error("esp_gemm_f32_pl: no planes kernel for this launch and no fp32 A to fall back to");
+      return -1;
+    }
+    g.a = *a_fp32;
+    g.bf16 = 3;
+    if (g.bnt == 64 || g.bnt == 128) done = launch_glds(MA, MB, g, batch, st);
+  }
   if (!done && g.bf16 == 3) {  // no B-planes kernel for this epilogue kind: the fp32 B operand
     if (!b_fp32 || !b_fp32->p) {
       esp::set_error("esp_gemm_f32_bp: no B-planes kernel for this launch and no fp32 B to fall back to");
@@ -220,6 +236,11 @@ int launch(const GemmArgs& g0, int batch, hipStream_t st, const Operand* b_fp32 
     g.b = *b_fp32;
     g.bf16 = 0;
     if (g.bnt == 64 || g.bnt == 128) done = launch_glds(MA, MB, g, batch, st);
+  }
+  if (!done && g.cpn) {
+    esp::set_error("esp_gemm_f32_pl: no kernel writes this epilogue as planes (planes output: plain, or the FFN "
+                   "bias + activation + dropout + derivative; N %% 4 == 0, 16-B aligned, LDS-DMA operands)");
+    return -1;
   }
   if (!done && g.smb_rel) {
     esp::set_error("esp_attn_dscores: operands not eligible for the LDS-DMA kernel (16-B alignment, ld %% 4)");
@@ -292,7 +313,8 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
                     float drop_p, unsigned long long seed, int bwd_act, const float* pre, float* rowsum,
                     const int* im2col_a, const int* im2col_b, float* work, long work_bytes, void* stream,
                     int prec_in, const GemmArgs* smb = nullptr, const void* b_planes = nullptr, long ldbp = 0,
-                    long sbp1 = 0, long sbp2 = 0, long bps = 0);
+                    long sbp1 = 0, long sbp2 = 0, long bps = 0, const void* a_planes = nullptr, long ldap = 0,
+                    long sap1 = 0, long sap2 = 0, long aps = 0, int cpn = 0, long cps = 0);
 
 ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2,
                          const float* A, long lda, long sa1, long sa2,
@@ -319,6 +341,23 @@ ESP_API int esp_gemm_f32_bp(int mode_a, int mode_b, int M, int N, int K, int bat
   return gemm_run(mode_a, mode_b, M, N, K, batch, nb2, A, lda, sa1, sa2, B, ldb, sb1, sb2, C, ldc, sc1, sc2, bias,
                   alpha, beta, R, act, aux, drop_p, seed, bwd_act, pre, rowsum, im2col_a, nullptr, work, work_bytes,
                   stream, -1, nullptr, b_planes, ldbp, sbp1, sbp2, b_pstride);
+}
+
+// esp_gemm_f32 with either operand (or both) also given as its three bf16 split planes
+ESP_API int esp_gemm_f32_pl(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2, const float* A, long lda,
+                            long sa1, long sa2, const void* a_planes, long ldap, long sap1, long sap2, long a_pstride,
+                            const float* B, long ldb, long sb1, long sb2, const void* b_planes, long ldbp, long sbp1,
+                            long sbp2, long b_pstride, float* C, long ldc, long sc1, long sc2, const float* bias,
+                            float alpha, float beta, const float* R, int act, float* aux, float drop_p,
+                            unsigned long long seed, int bwd_act, const float* pre, float* rowsum, int c_nplanes,
+                            long c_pstride, float* work, long work_bytes, void* stream) {
+  ESP_ARG_CHECK(mode_a == KC || mode_a == RC, "esp_gemm_f32_pl: mode_a must be 0 (KC) or 1 (RC)");
+  ESP_ARG_CHECK(mode_b == KC || mode_b == RC, "esp_gemm_f32_pl: mode_b must be 0 (KC) or 1 (RC)");
+  ESP_ARG_CHECK((A || a_planes) && (B || b_planes), "esp_gemm_f32_pl: an operand has neither fp32 values nor planes");
+  return gemm_run(mode_a, mode_b, M, N, K, batch, nb2, A, lda, sa1, sa2, B, ldb, sb1, sb2, C, ldc, sc1, sc2, bias,
+                  alpha, beta, R, act, aux, drop_p, seed, bwd_act, pre, rowsum, nullptr, nullptr, work, work_bytes,
+                  stream, -1, nullptr, b_planes, ldbp, sbp1, sbp2, b_pstride, a_planes, ldap, sap1, sap2, a_pstride,
+                  c_nplanes, c_pstride);
 }
 
 namespace {
@@ -417,7 +456,7 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
                     float drop_p, unsigned long long seed, int bwd_act, const float* pre, float* rowsum,
                     const int* im2col_a, const int* im2col_b, float* work, long work_bytes, void* stream,
                     int prec_in, const GemmArgs* smb, const void* b_planes, long ldbp, long sbp1, long sbp2,
-                    long bps) {
+                    long bps, const void* a_planes, long ldap, long sap1, long sap2, long aps, int cpn, long cps) {
   ESP_ARG_CHECK(M >= 0 && N >= 0 && K >= 0 && batch >= 1 && nb2 >= 1 && batch % nb2 == 0,
                 "esp_gemm_f32: bad sizes M=%d N=%d K=%d batch=%d nb2=%d", M, N, K, batch, nb2);
   ESP_ARG_CHECK(mode_a >= 0 && mode_a <= 3 && mode_b >= 0 && mode_b <= 3, "esp_gemm_f32: bad mode");
@@ -456,7 +495,15 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
     g.smb_dbd = smb->smb_dbd;
     g.smb_ldp = smb->smb_ldp;
   }
-  g.wide = N % 4 == 0 && ldc % 4 == 0 && ldc < (1L << 24) && sc1 % 4 == 0 && sc2 % 4 == 0 && aligned16(C) && (!R || aligned16(R)) &&
+  g.cpn = cpn;
+  g.cps = cps;
+  if (cpn) {  // planes output: 8-B quads per plane (C is plane 0, bf16)
+    ESP_ARG_CHECK((cpn == 1 || cpn == 3) && N % 4 == 0 && ldc % 4 == 0 && cps % 4 == 0 && ((uintptr_t)C & 7) == 0 &&
+                      !R && !rowsum && (cpn == 1 || cps >= (long)M * ldc || batch > 1),
+                  "esp_gemm_f32_pl: planes output needs N %% 4 == 0, ldc / pstride %% 4 == 0, no residual / row sums");
+    work = nullptr;  // never split-K: the epilogue writes the planes once
+  }
+  g.wide = N % 4 == 0 && ldc % 4 == 0 && ldc < (1L << 24) && sc1 % 4 == 0 && sc2 % 4 == 0 && (cpn ? true : aligned16(C)) && (!R || aligned16(R)) &&
            (!aux || aligned16(aux)) && (!pre || aligned16(pre)) && (!bias || aligned16(bias)) &&
            (!work || aligned16(work));
   g.ragged4 = !g.wide && N % 4 != 0 && ldc % 4 == 0 && sc1 % 4 == 0 && sc2 % 4 == 0 && aligned16(C) &&
@@ -486,21 +533,36 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
   // B as three bf16 planes (esp_gemm_f32_bp): the fp32 split-product GEMM without B's split in the
   // k-loop, when the fp32 compute type runs on split products and the planes suit the LDS-DMA
   // kernel (else the fp32 B operand)
-  const Operand b_fp32 = g.b;
-  if (b_planes && prec_in < 0 && g.bf16 == 0 && ESP_F32_SPLIT && variant() == 4 && g.a.glds && K > 0 &&
-      (((mode_a == KC || mode_a == I2C_KC) && mode_b == KC) || ((mode_a == KC || mode_a == RC) && mode_b == RC)) &&
-      aligned16(b_planes) && ldbp % 8 == 0 && sbp1 % 8 == 0 && sbp2 % 8 == 0 && bps % 8 == 0 &&
-      (mode_b == KC ? (K % 8 == 0 && ldbp >= K && 128L * ldbp * 2 < (1L << 32))
-                    : (N % 8 == 0 && ldbp >= N && 32L * ldbp * 2 + 2L * N < (1L << 32)))) {
-    g.b = Operand{(const float*)b_planes, ldbp, sbp1, sbp2, 1, {}, 1};
-    g.b.ps = bps;
-    g.bf16 = 3;
+  // A as planes too (esp_gemm_f32_pl, PREC 5): no split in the k-loop at all (64-wide tiles: the
+  // two operands' planes fill 72 KB of LDS per block)
+  const Operand b_fp32 = g.b, a_fp32 = g.a;
+  auto planes_ok = [&](const void* pl, long ld, long s1, long s2, long ps, int mode, int rows) {
+    return pl && aligned16(pl) && ld % 8 == 0 && s1 % 8 == 0 && s2 % 8 == 0 && ps % 8 == 0 &&
+           (mode == KC ? (K % 8 == 0 && ld >= K && 128L * ld * 2 < (1L << 32))
+                       : (rows % 8 == 0 && ld >= rows && 32L * ld * 2 + 2L * rows < (1L << 32)));
+  };
+  const bool split_ok = prec_in < 0 && g.bf16 == 0 && ESP_F32_SPLIT && variant() == 4 && K > 0;
+  if (split_ok && mode_b <= RC && planes_ok(b_planes, ldbp, sbp1, sbp2, bps, mode_b, N) &&
+      (((mode_a == KC || mode_a == I2C_KC) && mode_b == KC) || ((mode_a == KC || mode_a == RC) && mode_b == RC) ||
+       (a_planes && mode_a <= RC))) {
+    if (mode_a <= RC && planes_ok(a_planes, ldap, sap1, sap2, aps, mode_a, M)) {
+      g.a = Operand{(const float*)a_planes, ldap, sap1, sap2, 1, {}, 1};
+      g.a.ps = aps;
+      g.bf16 = 5;
+    } else if (g.a.glds) {
+      g.bf16 = 3;
+    }
+    if (g.bf16 >= 3) {
+      g.b = Operand{(const float*)b_planes, ldbp, sbp1, sbp2, 1, {}, 1};
+      g.b.ps = bps;
+    }
   }
-  if (!g.b.p) {
-    esp::set_error("esp_gemm_f32_bp: B planes not eligible (alignment, ld / strides %% 8, K or N %% 8) and B is NULL");
+  if (!g.b.p || !g.a.p) {
+    esp::set_error("esp_gemm_f32_pl: operand planes not eligible (alignment, ld / strides %% 8, K / M / N %% 8) "
+                   "and the fp32 operand is NULL");
     return -1;
   }
-  const bool bplanes = g.bf16 == 3;
+  const bool bplanes = g.bf16 >= 3;
   if (variant() == 4 && g.a.glds && g.b.glds && K > 0) {
     // per-CU time model: ceil(tiles / CUs) tiles of bn/64 units each, x1.3 when the grid
     // leaves CUs with a single resident block (one wave per SIMD); ties keep 128 (intensity)
@@ -517,7 +579,7 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
       if (t < 2 * 256) c *= 1.3;
       return c;
     };
-    g.bnt = (N <= 64 || cost(64) < cost(128)) ? 64 : 128;
+    g.bnt = (N <= 64 || g.bf16 == 5 || cost(64) < cost(128)) ? 64 : 128;
     // 64 x 64 tiles for grids that 128-row tiles leave under-filled (decoder M ~ 5k tokens, the
     // 41-query source attention): one work unit per tile, x1.15 for the halved operand reuse
     if (g.bnt == 64 && mode_a <= RC && mode_b <= RC && g.bf16 != 2 && !smb && !getenv("ESP_GEMM_NO_BM64")) {
@@ -532,7 +594,7 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
     if (mode_b == I2C_RC && work && K >= 65536) g.bnt = 128;
     static int force_bnt = -1;  // ESP_GEMM_BNT=64|128: tile width override (diagnostics)
     if (force_bnt < 0) force_bnt = getenv("ESP_GEMM_BNT") ? atoi(getenv("ESP_GEMM_BNT")) : 0;
-    if ((force_bnt == 64 || force_bnt == 128) && N > 64) g.bnt = force_bnt;
+    if ((force_bnt == 64 || force_bnt == 128) && N > 64 && g.bf16 != 5) g.bnt = force_bnt;
   }
   {
     const long tiles = ntiles(g.bnt ? g.bnt : BN, g.bm);
@@ -590,10 +652,10 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
   hipStream_t st = (hipStream_t)stream;
   const int key = mode_a * 4 + mode_b;
   switch (key) {
-    case KC * 4 + KC: return launch<KC, KC>(g, batch, st, &b_fp32);
-    case KC * 4 + RC: return launch<KC, RC>(g, batch, st, &b_fp32);
-    case RC * 4 + KC: return launch<RC, KC>(g, batch, st);
-    case RC * 4 + RC: return launch<RC, RC>(g, batch, st, &b_fp32);
+    case KC * 4 + KC: return launch<KC, KC>(g, batch, st, &b_fp32, &a_fp32);
+    case KC * 4 + RC: return launch<KC, RC>(g, batch, st, &b_fp32, &a_fp32);
+    case RC * 4 + KC: return launch<RC, KC>(g, batch, st, &b_fp32, &a_fp32);
+    case RC * 4 + RC: return launch<RC, RC>(g, batch, st, &b_fp32, &a_fp32);
     case I2C_KC * 4 + KC: return launch<I2C_KC, KC>(g, batch, st, &b_fp32);
     case RC * 4 + I2C_RC: return launch<RC, I2C_RC>(g, batch, st);
     default:

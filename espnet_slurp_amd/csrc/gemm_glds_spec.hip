@@ -2,7 +2,8 @@
 // of the production call sites: EPI_BIAS / EPI_BDR / EPI_FFN_SWISH / EPI_FFN_RELU for the linear
 // forward (KC x KC), EPI_BRELU (bias + ReLU) for the conv2 forward (implicit-im2col I2C_KC x KC)
 // and KC x KC, EPI_BMUL for the FFN input gradient and EPI_RMASK for the gradient through conv2's
-// ReLU (KC x RC) and its row-mapped form for the implicit conv2 input gradient (I2CT_KC x RC).
+// ReLU (KC x RC) and its row-mapped form for the implicit conv2 input gradient (I2CT_KC x RC); the
+// FFN w_1 kinds with the hidden state written as bf16 planes (EPI_FFN_*_PL).
 // See store_spec.
 #include "gemm_kernels.h"
 
@@ -25,6 +26,8 @@ bool glds_launch_spec(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hip
       ESP_SPEC(EPI_FFN_SWISH)
       ESP_SPEC(EPI_FFN_RELU)
       ESP_SPEC(EPI_BRELU)
+      ESP_SPEC(EPI_FFN_SWISH_PL)
+      ESP_SPEC(EPI_FFN_RELU_PL)
     } else if constexpr (MA == I2C_KC && MB == KC) {
       ESP_SPEC(EPI_BRELU)
     } else if constexpr (MA == KC && MB == RC) {

@@ -131,6 +131,10 @@ struct GemmArgs {
   const float* smb_dot;  // [batch * M] row dots  sum_j P_drop[i][j] dP[i][j] = dctx_i . ctx_i
   float* smb_dbd;        // bd gradient rows (batch*M rows of pitch smb_ldp)
   long smb_ldp;
+  // planes output (the *_PL kinds): c points at plane 0 (bf16), ldc / c1 / c2 in bf16 elements, plane p
+  // at c + p * cps; cpn = 3 (exact split) or 1 (bf16)
+  int cpn;
+  long cps;
 };
 
 __device__ __forceinline__ long row_off(const GemmArgs& g, int m) {
@@ -148,7 +152,13 @@ __device__ __forceinline__ long row_off(const GemmArgs& g, int m) {
 //   EPI 2: backward  drop'(acc + bias) * act'(pre)  (dropout mask regenerated), alpha, R
 // cbase = offset of batch z in C/R/aux/pre, dbase = z*M*N (dropout index base).
 enum { EPI_PLAIN = 0, EPI_FWD = 1, EPI_BWD = 2, EPI_BIAS = 3, EPI_BDR = 4, EPI_FFN_SWISH = 5, EPI_FFN_RELU = 6,
-       EPI_BMUL = 7, EPI_P0 = 8, EPI_PR = 9, EPI_SMB = 10, EPI_BRELU = 11, EPI_RMASK = 12, EPI_RMASKMAP = 13 };
+       EPI_BMUL = 7, EPI_P0 = 8, EPI_PR = 9, EPI_SMB = 10, EPI_BRELU = 11, EPI_RMASK = 12, EPI_RMASKMAP = 13,
+       // the same kinds with C written as bf16 planes (GemmArgs cpn): the FFN hidden state, the attention context
+       EPI_FFN_SWISH_PL = 14, EPI_FFN_RELU_PL = 15, EPI_P0_PL = 16 };
+// the fp32-output kind a planes-output kind computes
+constexpr int epi_base(int e) {
+  return e == EPI_FFN_SWISH_PL ? EPI_FFN_SWISH : e == EPI_FFN_RELU_PL ? EPI_FFN_RELU : e == EPI_P0_PL ? EPI_P0 : e;
+}
 __host__ __device__ inline int epi_kind(const GemmArgs& g) {
   return g.bwd_act ? EPI_BWD : ((g.bias || g.aux || g.act || g.drop_thresh) ? EPI_FWD : EPI_PLAIN);
 }
@@ -157,6 +167,14 @@ __host__ __device__ inline int epi_kind(const GemmArgs& g) {
 __host__ inline int epi_kind_spec(const GemmArgs& g) {
   if (g.smb_rel) return EPI_SMB;
   const int k = epi_kind(g);
+  if (g.cpn) {  // planes output: the kinds that have a planes form, else none (-1)
+    if (g.splits > 1 || g.rowsum || g.r) return -1;
+    if (k == EPI_PLAIN) return EPI_P0_PL;
+    // (dropout p = 0 included: every element is kept, the scale is 1)
+    if (g.bias && g.aux && !g.bwd_act && g.act == (ACT_SWISH | ACT_AUX_DERIV)) return EPI_FFN_SWISH_PL;
+    if (g.bias && g.aux && !g.bwd_act && g.act == (ACT_RELU | ACT_AUX_DERIV)) return EPI_FFN_RELU_PL;
+    return -1;
+  }
   if (g.cmap)
     return (g.wide && k == EPI_BWD && g.bwd_act == ACT_RELU && !g.drop_thresh && !g.r && !g.bias && g.alpha == 1.0f &&
             g.splits == 1)
@@ -420,8 +438,10 @@ __device__ __forceinline__ void store_tiles_wide(const GemmArgs& g, int z, int m
 //                  (attention.py:64-96 + 145-165 backward; P in pre, FlashAttention-2's row dot)
 // (wide stores, no output row map but EPI_RMASKMAP's; chosen by epi_kind on the host).  A wave whose 32-row /
 // 32-column sub-tiles are all in range takes a path without per-element bounds checks.
-template <int EPI>
+template <int EPI_>
 struct EpiSpec {
+  static constexpr bool pl = EPI_ != epi_base(EPI_);  // C written as bf16 planes
+  static constexpr int EPI = epi_base(EPI_);
   static constexpr int act =
       EPI == EPI_FFN_SWISH ? ACT_SWISH : (EPI == EPI_FFN_RELU || EPI == EPI_BRELU) ? ACT_RELU : ACT_NONE;
   static constexpr bool bias = EPI == EPI_BIAS || EPI == EPI_BDR || act != ACT_NONE;
@@ -532,7 +552,7 @@ __device__ __forceinline__ void store_spec(const GemmArgs& g, int z, int mrow0, 
             w = kp[e] ? w * g.drop_scale : 0.f;
             dd = kp[e] ? dd * g.drop_scale : 0.f;
           }
-          if constexpr (EPI == EPI_RMASK || EPI == EPI_RMASKMAP) w = xs[e] > 0.f ? w : 0.f;
+          if constexpr (S::EPI == EPI_RMASK || S::EPI == EPI_RMASKMAP) w = xs[e] > 0.f ? w : 0.f;
           else if constexpr (S::mul) w *= xs[e];
           if constexpr (!A1) w *= g.alpha;
           if constexpr (S::res) w += g.beta * xs[e];
@@ -540,7 +560,9 @@ __device__ __forceinline__ void store_spec(const GemmArgs& g, int z, int mrow0, 
           d[e] = dd;
         }
         if constexpr (S::aux) st4(g.aux + off, d, false);
-        if (FULL || n + 4 <= g.N) {
+        if constexpr (S::pl) {  // N % 4 == 0 (host): whole quads; aux shares the offsets (ld = planes ld)
+          esp::store_planes4(reinterpret_cast<uint16_t*>(g.c), off, g.cps, g.cpn, v[0], v[1], v[2], v[3]);
+        } else if (FULL || n + 4 <= g.N) {
           st4(g.c + off, v, false);
         } else {  // last quad of a row with N % 4 != 0 (EPI_P0 / EPI_PR only): loads stayed inside ldc
 #pragma unroll
@@ -1593,9 +1615,10 @@ __device__ __forceinline__ TileCoord tile_coord(const GemmArgs& g, const GldsArg
 // resident blocks per CU: 128x64 tiles (48 KB LDS) fit three, 128x128 tiles (64 KB) two; the
 // generic fused epilogues need the registers of two (the specialised ones fit three)
 // PREC 3 (B as three bf16 planes: 1.5x the B slab bytes) is also bounded by LDS: 128x128 tiles use
-// exactly 80 KB (two per CU), 128x64 56 KB (two), 64x64 40 KB (four)
+// exactly 80 KB (two per CU), 128x64 56 KB (two), 64x64 40 KB (four); PREC 5 (both operands as
+// planes): 128x64 72 KB (two), 64x64 48 KB (three)
 constexpr int glds_lds_bytes(int BNT, int BMT, int PREC) {
-  return 2 * 4 * (BMT * GL_BK + (PREC == 3 ? 48 * BNT : BNT * GL_BK)) + (PREC == 3 ? 0 : 16);
+  return 2 * 4 * ((PREC == 5 ? 48 * BMT : BMT * GL_BK) + (PREC >= 3 ? 48 * BNT : BNT * GL_BK)) + (PREC >= 3 ? 0 : 16);
 }
 template <int BNT, int EPI, int BMT = BM, int PREC = 0>
 constexpr int glds_occupancy() {
@@ -1630,20 +1653,9 @@ constexpr int glds_occupancy() {
 // (per element, hipcc converted each value twice: 12-13 VALU per pair; 1249.7 vs 1241.7 utt/s,
 // profiles/r03i_abc_split_code.txt)
 __device__ __forceinline__ void split3_bf16(const float* v, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
-  typedef __attribute__((ext_vector_type(2))) float f2;
-  typedef __attribute__((ext_vector_type(2))) __bf16 b2;
   uint32_t H[4], Md[4], L[4];
 #pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const float a = v[2 * p], b = v[2 * p + 1];
-    const uint32_t hp = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){a, b}, b2));
-    const float ra = a - __uint_as_float(hp << 16), rb = b - __uint_as_float(hp & 0xffff0000u);
-    const uint32_t mp = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){ra, rb}, b2));
-    const float sa = ra - __uint_as_float(mp << 16), sb = rb - __uint_as_float(mp & 0xffff0000u);
-    H[p] = hp;
-    Md[p] = mp;
-    L[p] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){sa, sb}, b2));
-  }
+  for (int p = 0; p < 4; ++p) esp::split3_pair(v[2 * p], v[2 * p + 1], H[p], Md[p], L[p]);
   hi = __builtin_bit_cast(bf16x8, make_uint4(H[0], H[1], H[2], H[3]));
   mid = __builtin_bit_cast(bf16x8, make_uint4(Md[0], Md[1], Md[2], Md[3]));
   lo = __builtin_bit_cast(bf16x8, make_uint4(L[0], L[1], L[2], L[3]));
@@ -1653,10 +1665,13 @@ template <int MA, int MB, int BNT, bool RS, int EPI, int PREC = 0, int BMT = BM>
 __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void gemm_glds_kernel(GemmArgs g, GldsArgs x) {
   constexpr int WN = BMT == 64 ? 2 : BNT / 64, WM = 4 / WN, TM = BMT / (WM * 32), TN = BNT / (WN * 32);
   static_assert(BMT == 128 || BNT == 64, "64-row tiles are 64 wide");
-  static_assert(PREC != 3 || MB == KC || MB == RC, "B planes: KC / RC operands");
-  constexpr bool BP = PREC == 3;                 // B as three bf16 planes (StageP)
-  constexpr int PLF = BNT * 16;                  // floats per plane image (BNT x 32 bf16)
-  constexpr int A_SZ = BMT * GL_BK, B_SZ = BP ? 3 * PLF : BNT * GL_BK, BUF = A_SZ + B_SZ;
+  static_assert(PREC < 3 || MB == KC || MB == RC, "B planes: KC / RC operands");
+  static_assert(PREC != 5 || MA == KC || MA == RC, "A planes: KC / RC operands");
+  constexpr bool BP = PREC >= 3;                 // B as three bf16 planes (StageP)
+  constexpr bool AP = PREC == 5;                 // A as three bf16 planes too: no split in the k-loop
+  constexpr int PLF = BNT * 16;                  // floats per B plane image (BNT x 32 bf16)
+  constexpr int PLA = BMT * 16;                  // floats per A plane image
+  constexpr int A_SZ = AP ? 3 * PLA : BMT * GL_BK, B_SZ = BP ? 3 * PLF : BNT * GL_BK, BUF = A_SZ + B_SZ;
   constexpr int NIA = A_SZ / 4 / NT, NIB = B_SZ / 4 / NT;
   // + the split-K combine flag (the in-kernel combine is never used with B planes: their 128x128
   // tiles need exactly 80 KB for two blocks per CU)
@@ -1673,7 +1688,10 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
 
   auto a_base = [&](const TileCoord& c) {
     const int z1 = (int)fdiv((uint32_t)c.z, x.fd_nb2), z2 = c.z - z1 * g.nb2;
-    return g.a.p + z1 * g.a.s1 + z2 * g.a.s2;
+    if constexpr (AP)  // bf16 element strides
+      return reinterpret_cast<const float*>(reinterpret_cast<const __bf16*>(g.a.p) + z1 * g.a.s1 + z2 * g.a.s2);
+    else
+      return g.a.p + z1 * g.a.s1 + z2 * g.a.s2;
   };
   auto b_base = [&](const TileCoord& c) {
     const int z1 = (int)fdiv((uint32_t)c.z, x.fd_nb2), z2 = c.z - z1 * g.nb2;
@@ -1686,13 +1704,15 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
   // scalar-base staging (StageS) for KC / RC / implicit-im2col A; the gathered operands keep
   // per-lane 64-bit addresses (Stage); B planes: StageP
   constexpr bool SA_S = MA == KC || MA == RC || MA == I2C_KC, SB_S = MB == KC || MB == RC;
-  using SAt = std::conditional_t<SA_S, StageS<MA, BMT, NIA, PREC == 2>, Stage<MA, BMT, NIA>>;
+  using SAt = std::conditional_t<AP, StageP<MA, BMT>,
+                                 std::conditional_t<SA_S, StageS<MA, BMT, NIA, PREC == 2>, Stage<MA, BMT, NIA>>>;
   using SBt = std::conditional_t<BP, StageP<MB, BNT>,
                                  std::conditional_t<SB_S, StageS<MB, BNT, NIB, PREC == 2>, Stage<MB, BNT, NIB>>>;
   SAt sa;
   SBt sb;
   auto init_ab = [&](const TileCoord& cc) {
-    if constexpr (SA_S) sa.init(g.a, a_base(cc), g.M, g.K, cc.m0, cc.kbeg, x.hw_a, x.wo_a, wave, lane);
+    if constexpr (AP) sa.init(g.a, a_base(cc), g.M, cc.m0, cc.kbeg, wave, lane);
+    else if constexpr (SA_S) sa.init(g.a, a_base(cc), g.M, g.K, cc.m0, cc.kbeg, x.hw_a, x.wo_a, wave, lane);
     else sa.init(g.a, a_base(cc), g.M, g.K, cc.m0, x.c_a, x.hw_a, x.wo_a, wave, lane, MA == I2CT_KC ? &x : nullptr);
     if constexpr (BP) sb.init(g.b, b_base(cc), g.N, cc.n0, cc.kbeg, wave, lane);
     else if constexpr (SB_S) sb.init(g.b, b_base(cc), g.N, g.K, cc.n0, cc.kbeg, x.hw_b, x.wo_b, wave, lane);
@@ -1701,7 +1721,8 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
   const uint32_t smem_lds = lds_addr(smem);
   auto issue_ab = [&](int k0, float* dst) {
     const uint32_t dl = smem_lds + (uint32_t)(dst - smem) * 4u;
-    if constexpr (SA_S) sa.issue(g.a, g.K, k0, dl, wave);
+    if constexpr (AP) sa.issue(g.K, k0, dl, wave);
+    else if constexpr (SA_S) sa.issue(g.a, g.K, k0, dl, wave);
     else sa.issue(g.a, g.K, k0, dst, wave, x.c_a, x.hw_a, x.wo_a, MA == I2CT_KC ? &x : nullptr);
     if constexpr (BP) sb.issue(g.K, k0, dl + 4u * A_SZ, wave);
     else if constexpr (SB_S) sb.issue(g.b, g.K, k0, dl + 4u * A_SZ, wave);
@@ -1798,6 +1819,62 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
                 }
               }
               rs[i] += a0;
+            }
+          }
+        }
+        return;
+      }
+      if constexpr (AP) {
+        // both operands' three planes read from LDS: the PREC 0 products in the PREC 0 order on the
+        // same values, and no split VALU at all
+        const float* bpl = cur + A_SZ;
+#pragma unroll
+        for (int hs = 0; hs < 2; ++hs) {
+          bf16x8 ah[TM][3], bh[TN][3];
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+              if constexpr (MA == KC) ah[i][p] = frag_pl_kc(cur + p * PLA, wm * TM * 32 + i * 32 + l32, h, hs);
+              else ah[i][p] = frag_pl_rc<BMT>(cur + p * PLA, wm * TM * 32 + i * 32, lane, hs);
+            }
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+              if constexpr (MB == KC) bh[j][p] = frag_pl_kc(bpl + p * PLF, wn * TN * 32 + j * 32 + l32, h, hs);
+              else bh[j][p] = frag_pl_rc<BNT>(bpl + p * PLF, wn * TN * 32 + j * 32, lane, hs);
+            }
+          if (kv < GL_BK) {  // K tail: A's k >= kv are 0 (B's clamped tail holds finite values)
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (16 * h + 8 * hs + e >= kv)
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                  for (int p = 0; p < 3; ++p) ah[i][p][e] = (__bf16)0.0f;
+          }
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][1], bh[j][1], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][2], bh[j][0], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][2], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][1], bh[j][0], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][1], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][0], acc[i][j], 0, 0, 0);
+            }
+          if constexpr (RS) {  // fused bias gradient: the fp32 A values are hi + mid + lo exactly
+            if (do_rs) {
+#pragma unroll
+              for (int i = 0; i < TM; ++i) {
+                float a0 = 0.f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                  a0 += ((float)ah[i][0][e] + (float)ah[i][1][e]) + (float)ah[i][2][e];
+                rs[i] += a0;
+              }
             }
           }
         }
@@ -2026,6 +2103,9 @@ bool glds_switch(int ma, int mb, int bnt, int prec, int bm, F&& f) {
       } else if (prec == 3) {
         if constexpr (planes_ok) f(A, B, N, IC<3>{}, R);
         else return false;
+      } else if (prec == 5) {  // both operands as planes: KC / RC pairs, 64-wide tiles (LDS)
+        if constexpr (small_ok && decltype(N)::value == 64) f(A, B, N, IC<5>{}, R);
+        else return false;
       } else if constexpr (small_ok && decltype(R)::value == BM) {  // bf16 operands: KC / RC pairs
         f(A, B, N, IC<2>{}, R);
       } else {
@@ -2035,7 +2115,7 @@ bool glds_switch(int ma, int mb, int bnt, int prec, int bm, F&& f) {
     };
     if (bm == 64) {
       if constexpr (small_ok) {
-        if (bnt == 64 && prec != 2) return by_prec(IC<64>{}, IC<64>{});
+        if (bnt == 64 && prec != 2) return by_prec(IC<64>{}, IC<64>{});  // (prec 5: A planes of 64 rows)
       }
       return false;
     }

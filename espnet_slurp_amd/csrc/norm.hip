@@ -53,6 +53,56 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
+// The same LayerNorm with y written as bf16 planes (n = 3: the exact split, esp::split3_pair; n = 1:
+// bf16(y)) for the GEMMs that are its only readers (kernels.Planes).  A lane owns float4 quads
+// (D % 4 == 0); y values, mean and rstd are those of ln_fwd_kernel (same sums, same order per row:
+// the wave sums run over the same per-lane partials in a different lane assignment, so they can
+// differ in the last bit -- both are exact-order wave reductions of the same row).
+template <int PQ>
+__global__ __launch_bounds__(256) void ln_fwd_planes_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                            const float* __restrict__ b, uint16_t* __restrict__ y,
+                                                            long ldy, long ps, int n, float* __restrict__ mean_out,
+                                                            float* __restrict__ rstd_out, int M, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const int nq = D >> 2;
+  const float4* xr = reinterpret_cast<const float4*>(x + (long)row * D);
+  float4 v[PQ];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PQ; ++i) {
+    const int q = lane + 64 * i;
+    v[i] = q < nq ? xr[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  }
+  const float mean = esp::wave_sum(s) / (float)D;
+  float qs = 0.f;
+#pragma unroll
+  for (int i = 0; i < PQ; ++i) {
+    const int q = lane + 64 * i;
+    if (q < nq) {
+      const float a = v[i].x - mean, bb = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
+      qs += (a * a + bb * bb) + (c * c + d * d);
+    }
+  }
+  const float var = esp::wave_sum(qs) / (float)D;
+  const float rstd = 1.0f / sqrtf(var + eps);
+#pragma unroll
+  for (int i = 0; i < PQ; ++i) {
+    const int q = lane + 64 * i;
+    if (q >= nq) continue;
+    const float4 wq = reinterpret_cast<const float4*>(w)[q], bq = reinterpret_cast<const float4*>(b)[q];
+    esp::store_planes4(y, (long)row * ldy + 4 * q, ps, n, (v[i].x - mean) * rstd * wq.x + bq.x,
+                       (v[i].y - mean) * rstd * wq.y + bq.y, (v[i].z - mean) * rstd * wq.z + bq.z,
+                       (v[i].w - mean) * rstd * wq.w + bq.w);
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
 // dx (+)= rstd * (g - mean(g) - xhat*mean(g*xhat)), g = dy*w; partial dw/db per block.
 // A wave owns LN_RB consecutive rows per pass (their loads are all in flight before the first
 // reduction: row-level ILP), float4 along the row (D % 4 == 0); a block covers
@@ -604,6 +654,25 @@ __global__ void bn_swish_fwd4_kernel(const float* __restrict__ y, const float* _
   }
 }
 
+// the same, s written as bf16 planes (n = 3 exact split, 1 = bf16) for pointwise_conv2, its only
+// reader (kernels.Planes); row pitch ld (bf16 elements), plane stride ps
+__global__ void bn_swish_fwd4_planes_kernel(const float* __restrict__ y, const float* __restrict__ mean,
+                                            const float* __restrict__ rstd, const float* __restrict__ gamma,
+                                            const float* __restrict__ beta, uint16_t* __restrict__ s, long ld, long ps,
+                                            int n, int n4, int D) {
+  const int nq = D >> 2;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    const int r = i / nq, c = 4 * (i - r * nq);
+    const float4 v = reinterpret_cast<const float4*>(y)[i];
+    const float4 mu = *reinterpret_cast<const float4*>(mean + c), rs = *reinterpret_cast<const float4*>(rstd + c);
+    const float4 ga = *reinterpret_cast<const float4*>(gamma + c), be = *reinterpret_cast<const float4*>(beta + c);
+    const float zx = (v.x - mu.x) * rs.x * ga.x + be.x, zy = (v.y - mu.y) * rs.y * ga.y + be.y;
+    const float zz = (v.z - mu.z) * rs.z * ga.z + be.z, zw = (v.w - mu.w) * rs.w * ga.w + be.w;
+    esp::store_planes4(s, (long)r * ld + c, ps, n, zx * esp::fast_sigmoid(zx), zy * esp::fast_sigmoid(zy),
+                       zz * esp::fast_sigmoid(zz), zw * esp::fast_sigmoid(zw));
+  }
+}
+
 // s = swish(gamma*(y-mean)*rstd + beta)
 __global__ void bn_swish_fwd_kernel(const float* __restrict__ y, const float* __restrict__ mean,
                                     const float* __restrict__ rstd, const float* __restrict__ gamma,
@@ -731,6 +800,29 @@ ESP_API int esp_layernorm_fwd(const float* x, const float* w, const float* b, fl
   else if (per <= 8) hipLaunchKernelGGL(ln_fwd_kernel<8>, grid, dim3(256), 0, st, x, w, b, y, mean, rstd, M, D, eps);
   else hipLaunchKernelGGL(ln_fwd_kernel<32>, grid, dim3(256), 0, st, x, w, b, y, mean, rstd, M, D, eps);
   ESP_CHECK_LAUNCH("esp_layernorm_fwd");
+  return 0;
+}
+
+ESP_API int esp_layernorm_fwd_planes(const float* x, const float* w, const float* b, void* y, long ldy, long pstride,
+                                     int nplanes, float* mean, float* rstd, int M, int D, float eps, void* stream) {
+  ESP_ARG_CHECK(D <= MAXD && D % 4 == 0, "esp_layernorm_fwd_planes: D=%d must be a multiple of 4 and <= %d", D, MAXD);
+  ESP_ARG_CHECK((nplanes == 1 || nplanes == 3) && ldy >= D && ldy % 4 == 0 && (nplanes == 1 || pstride >= (long)M * ldy) &&
+                    ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 7) == 0 && ((uintptr_t)w & 15) == 0 &&
+                    ((uintptr_t)b & 15) == 0 && pstride % 4 == 0,
+                "esp_layernorm_fwd_planes: bad planes layout (nplanes %d, ldy %ld, pstride %ld) or alignment", nplanes,
+                ldy, pstride);
+  if (M <= 0) return 0;
+  dim3 grid((M + 3) / 4);
+  hipStream_t st = (hipStream_t)stream;
+  const int pq = (D / 4 + 63) / 64;
+  uint16_t* yp = (uint16_t*)y;
+  if (pq <= 1)
+    hipLaunchKernelGGL(ln_fwd_planes_kernel<1>, grid, dim3(256), 0, st, x, w, b, yp, ldy, pstride, nplanes, mean, rstd, M, D, eps);
+  else if (pq <= 2)
+    hipLaunchKernelGGL(ln_fwd_planes_kernel<2>, grid, dim3(256), 0, st, x, w, b, yp, ldy, pstride, nplanes, mean, rstd, M, D, eps);
+  else
+    hipLaunchKernelGGL(ln_fwd_planes_kernel<8>, grid, dim3(256), 0, st, x, w, b, yp, ldy, pstride, nplanes, mean, rstd, M, D, eps);
+  ESP_CHECK_LAUNCH("esp_layernorm_fwd_planes");
   return 0;
 }
 
@@ -865,9 +957,10 @@ ESP_API int esp_dwconv1d_wgrad(const float* dy, const float* x, float* dW, int B
 ESP_API long esp_bn_swish_fwd_workspace_bytes(int M, int D) {
   return M <= 0 || D <= 0 ? 0 : 8L * D * nchunks(M, rows_per_block(M));
 }
-ESP_API int esp_bn_swish_fwd(const float* y, const float* gamma, const float* beta, float* s, float* mean, float* rstd,
-                             float* run_mean, float* run_var, float momentum, float eps, int M, int D, double* work,
-                             long work_bytes, int T, const int* tvalid, void* stream) {
+static int bn_swish_fwd_impl(const float* y, const float* gamma, const float* beta, float* s, void* s_planes, long lds,
+                             long pstride, int nplanes, float* mean, float* rstd, float* run_mean, float* run_var,
+                             float momentum, float eps, int M, int D, double* work, long work_bytes, int T,
+                             const int* tvalid, void* stream) {
   ESP_ARG_CHECK(!tvalid || (T > 0 && M % T == 0), "esp_bn_swish_fwd: M must be a multiple of T with tvalid");
   const long need__ = esp_bn_swish_fwd_workspace_bytes(M, D);
   ESP_ARG_CHECK(work_bytes >= need__, "esp_bn_swish_fwd: workspace %ld B < %ld B required (esp_bn_swish_fwd_workspace_bytes)", work_bytes, need__);
@@ -881,14 +974,35 @@ ESP_API int esp_bn_swish_fwd(const float* y, const float* gamma, const float* be
   hipLaunchKernelGGL(bn_part_kernel, g1, dim3(256), 0, st, y, M, D, rpb, mean, 1, work, T, tvalid);
   hipLaunchKernelGGL(bn_finalize_kernel, bnf_grid(D), dim3(1024), 0, st, work, nb, D, M, 1, mean, rstd, run_mean,
                      run_var, momentum, eps, T, tvalid);
-  if (vec4_ok((long)M * D, D, {y, mean, rstd, gamma, beta, s}))
+  if (s_planes) {
+    hipLaunchKernelGGL(bn_swish_fwd4_planes_kernel, dim3(gridn((long)M * D / 4)), dim3(256), 0, st, y, mean, rstd,
+                       gamma, beta, (uint16_t*)s_planes, lds, pstride, nplanes, (int)((long)M * D / 4), D);
+  } else if (vec4_ok((long)M * D, D, {y, mean, rstd, gamma, beta, s})) {
     hipLaunchKernelGGL(bn_swish_fwd4_kernel, dim3(gridn((long)M * D / 4)), dim3(256), 0, st, y, mean, rstd, gamma,
                        beta, s, (int)((long)M * D / 4), D);
-  else
+  } else {
     hipLaunchKernelGGL(bn_swish_fwd_kernel, dim3(gridn((long)M * D)), dim3(256), 0, st, y, mean, rstd, gamma, beta,
                        s, (long)M * D, D);
+  }
   ESP_CHECK_LAUNCH("esp_bn_swish_fwd");
   return 0;
+}
+ESP_API int esp_bn_swish_fwd(const float* y, const float* gamma, const float* beta, float* s, float* mean, float* rstd,
+                             float* run_mean, float* run_var, float momentum, float eps, int M, int D, double* work,
+                             long work_bytes, int T, const int* tvalid, void* stream) {
+  return bn_swish_fwd_impl(y, gamma, beta, s, nullptr, 0, 0, 0, mean, rstd, run_mean, run_var, momentum, eps, M, D,
+                           work, work_bytes, T, tvalid, stream);
+}
+ESP_API int esp_bn_swish_fwd_planes(const float* y, const float* gamma, const float* beta, void* s_planes, long lds,
+                                    long pstride, int nplanes, float* mean, float* rstd, float* run_mean,
+                                    float* run_var, float momentum, float eps, int M, int D, double* work,
+                                    long work_bytes, int T, const int* tvalid, void* stream) {
+  ESP_ARG_CHECK(s_planes && (nplanes == 1 || nplanes == 3) && D % 4 == 0 && lds % 4 == 0 && lds >= D &&
+                    pstride % 4 == 0 && ((uintptr_t)s_planes & 7) == 0 &&
+                    vec4_ok((long)M * D, D, {y, mean, rstd, gamma, beta}),
+                "esp_bn_swish_fwd_planes: D, ld, pstride %% 4 == 0, aligned operands needed");
+  return bn_swish_fwd_impl(y, gamma, beta, nullptr, s_planes, lds, pstride, nplanes, mean, rstd, run_mean, run_var,
+                           momentum, eps, M, D, work, work_bytes, T, tvalid, stream);
 }
 
 // eval mode (BatchNorm1d with track_running_stats, convolution.py:56-79 under model.eval()):

@@ -221,7 +221,65 @@ class param_cast_scope:
 # Trainer's step; keyed like _W16, holding the fp32 source), else per GEMM.  ESP_BPLANES=0: off
 # (A/B measurements).
 _BPLANES = os.environ.get("ESP_BPLANES", "1") == "1"
+# producers of GEMM-only activations write them as Planes (ESP_XPLANES=0: fp32, A/B measurements)
+_XPLANES = os.environ.get("ESP_XPLANES", "1") == "1"
+_F32_PRODUCTS = [None]  # esp_f32_gemm_products() of the loaded build (set at first use)
 _WP = [None]
+
+
+class Planes:
+    """An fp32 matrix held as its bf16 split planes, the operand format of the planes GEMMs: n = 3
+    (esp_f32_to_planes: value = hi + mid + lo exactly, the fp32 path) or n = 1 (hi = bf16(value), round
+    to nearest even: the reduced-precision path's bf16 operand).  rows x cols, row pitch ld (bf16
+    elements, cols rounded up to 8), plane p at buf[p * ps], ps = rows * ld.  Producers write it in
+    place of the fp32 tensor when only GEMMs read the value (LayerNorm outputs, the FFN hidden state,
+    the attention context, the convolution module's BatchNorm + Swish output)."""
+    __slots__ = ("buf", "rows", "cols", "ld", "ps", "n")
+
+    def __init__(self, rows: int, cols: int, device, n: int = 3, buf=None):
+        self.rows, self.cols, self.n = rows, cols, n
+        self.ld = (cols + 7) // 8 * 8
+        self.ps = rows * self.ld
+        self.buf = torch.empty(n * self.ps, dtype=torch.bfloat16, device=device) if buf is None else buf
+
+    @property
+    def shape(self):
+        return (self.rows, self.cols)
+
+    @property
+    def device(self):
+        return self.buf.device
+
+    def data_ptr(self) -> int:
+        return self.buf.data_ptr()
+
+    def float(self) -> torch.Tensor:
+        """The fp32 values (hi + mid + lo, exact; tests and tools)."""
+        p = self.buf.view(self.n, self.rows, self.ld)[:, :, : self.cols].float()
+        return p.sum(0) if self.n == 3 else p[0]
+
+    @staticmethod
+    def of(x2d: torch.Tensor, n: int = 3) -> "Planes":
+        """Split a contiguous-row fp32 matrix (esp_f32_to_planes; n = 1: its bf16 cast)."""
+        rows, cols = x2d.shape
+        p = Planes(rows, cols, x2d.device, n)
+        if n == 3:
+            _native.call("esp_f32_to_planes", _p(x2d), _p(p.buf), rows, cols, x2d.stride(0), p.ld, p.ps, _st())
+        else:
+            _native.call("esp_f32_to_bf16", _p(x2d), _p(p.buf), rows, cols, x2d.stride(0), p.ld, 0, _st())
+        return p
+
+
+def planes_mode() -> int:
+    """Planes a producer writes for a GEMM-only tensor in the current compute mode: 3 (fp32 split
+    products), 1 (bf16 GEMM operands), 0 (write fp32: ESP_XPLANES=0 or an f32-MFMA build)."""
+    if not _XPLANES:
+        return 0
+    if _F32_PRODUCTS[0] is None:
+        _F32_PRODUCTS[0] = int(_native.load().esp_f32_gemm_products())
+    if _COMPUTE[0] == GEMM_BF16:
+        return 1 if _AMP_BF16_OPERANDS else 0
+    return 3 if _F32_PRODUCTS[0] == 6 else 0
 
 
 def planes(X, off: int, rows: int, cols: int, ld: int):
@@ -316,6 +374,10 @@ def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc
     like a parameter's, see planes())."""
     if R is not None and r_off is None:
         r_off = c_off
+    if isinstance(A, Planes) or isinstance(B, Planes) or isinstance(C, Planes):
+        return _gemm_planes(M, N, K, A, B, C, mode_a, lda, mode_b, ldb, ldc, a_off, b_off, c_off, bias, alpha,
+                            beta, R, r_off, act, aux, drop_p, seed, bwd_act, pre, rowsum, b_weight, batch, nb2, sa,
+                            sb, sc)
     if (_COMPUTE[0] == GEMM_BF16 and _AMP_BF16_OPERANDS and batch == 1 and mode_a in (KC, RC)
             and mode_b in (KC, RC) and ic_a is None and ic_b is None and M > 0 and N > 0):
         if _gemm_amp_operands(M, N, K, A, B, C, mode_a, lda, mode_b, ldb, ldc, a_off, b_off, c_off, bias, alpha,
@@ -361,6 +423,99 @@ def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc
         _PROF.append((2.0 * M * N * K * batch, ev0, ev1, key, extra))
 
 
+def _gemm_planes(M, N, K, A, B, C, mode_a, lda, mode_b, ldb, ldc, a_off, b_off, c_off, bias, alpha, beta, R, r_off,
+                 act, aux, drop_p, seed, bwd_act, pre, rowsum, b_weight, batch=1, nb2=1, sa=(0, 0), sb=(0, 0),
+                 sc=(0, 0)):
+    """gemm() with an operand given as Planes (KC / RC; unbatched planes operands) or C written as
+    Planes (fp32 mode: the plain and FFN w_1 epilogues): esp_gemm_f32_pl in the fp32 mode (the other
+    operand's planes from the step cache when it is a weight, else split here), the hi planes as bf16
+    operands in the reduced-precision mode (esp_gemm_bf16)."""
+    _DY16[0] = None
+    assert mode_a in (KC, RC) and mode_b in (KC, RC), (mode_a, mode_b)
+    for X, off in ((A, a_off), (B, b_off)):
+        if isinstance(X, Planes):
+            assert off == 0 and batch == 1, "a Planes operand is a whole (unbatched) matrix"
+    cp = C if isinstance(C, Planes) else None
+    if cp is not None:
+        assert _COMPUTE[0] != GEMM_BF16 and cp.n == 3 and R is None and rowsum is None
+        if not isinstance(A, Planes) and not isinstance(B, Planes) and not b_weight and not _is_param(
+                B.data_ptr() + b_off * 4, 4):
+            # fp32 operands, planes output (the attention context): esp_gemm_f32_pl without operand planes
+            ws = _ws(_GEMM_WS, "esp_gemm_f32", _GEMM_WS_BYTES, cp.device)
+            if _PROF is not None:
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev0.record()
+            _native.call("esp_gemm_f32_pl", mode_a, mode_b, M, N, K, batch, nb2, _p(A, a_off), lda, sa[0], sa[1],
+                         None, 0, 0, 0, 0, _p(B, b_off), ldb, sb[0], sb[1], None, 0, 0, 0, 0,
+                         _p(cp.buf, c_off), ldc, sc[0], sc[1], _p(bias), float(alpha), float(beta), None, act,
+                         _p(aux, c_off) if aux is not None else None, float(drop_p), seed & 0xFFFFFFFFFFFFFFFF,
+                         int(bwd_act), _p(pre, c_off) if pre is not None else None, None, cp.n, cp.ps, _p(ws),
+                         _GEMM_WS_BYTES, _st())
+            if _PROF is not None:
+                ev1.record()
+                extra = 4.0 * M * N * batch * (aux is not None) - 1.0 * M * N * batch  # 6-B planes out, not 4-B
+                _PROF.append((2.0 * M * N * K * batch, ev0, ev1, (mode_a, mode_b, M, N, K, batch), extra))
+            return
+    assert batch == 1, "planes operands: unbatched GEMMs"
+    if _COMPUTE[0] == GEMM_BF16:
+        def b16(X, off, rows, cols, ld, role=""):
+            if isinstance(X, Planes):
+                return X.buf, X.ld
+            return _bf16_copy(X, off, rows, cols, ld, role)
+        A16, la = b16(A, a_off, M, K, lda, "a_kc") if mode_a == KC else b16(A, a_off, K, M, lda)
+        B16, lb = b16(B, b_off, N, K, ldb) if mode_b == KC else b16(B, b_off, K, N, ldb, "b_rc")
+        ws = _ws(_GEMM_WS, "esp_gemm_bf16", _GEMM_WS_BYTES, C.device)
+        if _PROF is not None:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
+        _native.call("esp_gemm_bf16", mode_a, mode_b, M, N, K, 1, 1, _p(A16), la, 0, 0, _p(B16), lb, 0, 0,
+                     _p(C, c_off), ldc, 0, 0, _p(bias), float(alpha), float(beta), _p(R, r_off or 0), act,
+                     _p(aux, c_off) if aux is not None else None, float(drop_p), seed & 0xFFFFFFFFFFFFFFFF,
+                     int(bwd_act), _p(pre, c_off) if pre is not None else None, _p(rowsum), _p(ws), _GEMM_WS_BYTES,
+                     _st())
+        _guard_post("esp_gemm_bf16", ws, _GEMM_WS_BYTES)
+        if _PROF is not None:
+            ev1.record()
+            extra = 4.0 * M * N * ((R is not None) + (aux is not None) + (pre is not None))
+            _PROF.append((2.0 * M * N * K, ev0, ev1, (mode_a, mode_b, M, N, K, 1, "bf16"), extra))
+        return
+
+    def pl(X, off, rows, cols, ld, weight):
+        if isinstance(X, Planes):
+            assert X.n == 3 and (X.rows, X.cols) == (rows, cols), ((X.rows, X.cols, X.n), (rows, cols))
+            return None, 0, (X.buf, X.ld, X.ps)
+        if weight or _is_param(X.data_ptr() + off * 4, ((rows - 1) * ld + cols) * 4):
+            return X, off, planes(X, off, rows, cols, ld)
+        return X, off, None
+    ra, ca = (M, K) if mode_a == KC else (K, M)
+    rb, cb = (N, K) if mode_b == KC else (K, N)
+    Af, ao, ap = pl(A, a_off, ra, ca, lda, False)
+    Bf, bo, bq = pl(B, b_off, rb, cb, ldb, b_weight)
+    if bq is None:  # A given as planes: B's planes made here (the planes kernel needs both)
+        bq = planes(B, b_off, rb, cb, ldb)
+    ws = _ws(_GEMM_WS, "esp_gemm_f32", _GEMM_WS_BYTES, C.device)
+    if _PROF is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    _native.call("esp_gemm_f32_pl", mode_a, mode_b, M, N, K, 1, 1,
+                 _p(Af, ao) if Af is not None else None, lda if Af is not None else 0, 0, 0,
+                 _p(ap[0]) if ap else None, ap[1] if ap else 0, 0, 0, ap[2] if ap else 0,
+                 _p(Bf, bo) if Bf is not None else None, ldb if Bf is not None else 0, 0, 0,
+                 _p(bq[0]), bq[1], 0, 0, bq[2],
+                 _p(cp.buf if cp is not None else C, c_off), ldc, 0, 0, _p(bias), float(alpha), float(beta),
+                 _p(R, r_off or 0), act, _p(aux, c_off) if aux is not None else None, float(drop_p),
+                 seed & 0xFFFFFFFFFFFFFFFF, int(bwd_act), _p(pre, c_off) if pre is not None else None, _p(rowsum),
+                 cp.n if cp is not None else 0, cp.ps if cp is not None else 0, _p(ws), _GEMM_WS_BYTES, _st())
+    _guard_post("esp_gemm_f32", ws, _GEMM_WS_BYTES)
+    if _PROF is not None:
+        ev1.record()
+        extra = 4.0 * M * N * ((R is not None) + (aux is not None) + (pre is not None)) + (2.0 * M * N if cp is not None else 0.0)
+        _PROF.append((2.0 * M * N * K, ev0, ev1, (mode_a, mode_b, M, N, K, 1, "pl" if ap else "bp"), extra))
+
+
 def gemm_bf16(M: int, N: int, K: int, A16, B16, C, *, lda, ldb, ldc, c_off=0, bias=None, alpha=1.0, beta=0.0,
               R=None, act=ACT_NONE, aux=None, drop_p=0.0, seed=0, bwd_act=ACT_NONE, pre=None, mode_a=KC,
               mode_b=KC):
@@ -399,11 +554,12 @@ def ctypes_ptr(arr):
 
 def linear_fwd(x2d, W, b, out, *, act=ACT_NONE, aux=None, drop_p=0.0, seed=0, alpha=1.0, R=None, beta=1.0,
                out_off=0, ldo=None, b_weight=False):
-    """out = alpha*drop(act(x W^T + b)) (+ beta*R); x (M,K), W (N,K).  b_weight: W is a step-constant
-    weight that is not a parameter view (a re-laid copy): its split planes are cached like one."""
+    """out = alpha*drop(act(x W^T + b)) (+ beta*R); x (M,K) (fp32 or Planes), W (N,K).  b_weight: W is a
+    step-constant weight that is not a parameter view (a re-laid copy): its split planes are cached
+    like one."""
     M, K = x2d.shape
     N = W.shape[0]
-    gemm(M, N, K, x2d, W, out, mode_a=KC, lda=x2d.stride(0), mode_b=KC, ldb=W.stride(0),
+    gemm(M, N, K, x2d, W, out, mode_a=KC, lda=x2d.ld if isinstance(x2d, Planes) else x2d.stride(0), mode_b=KC, ldb=W.stride(0),
          ldc=ldo or N, c_off=out_off, bias=b, alpha=alpha, beta=beta if R is not None else 0.0, R=R,
          act=act, aux=aux, drop_p=drop_p, seed=seed, b_weight=b_weight)
     return out
@@ -429,11 +585,11 @@ def linear_bwd_data_act(dy, W, dx, pre, act, drop_p=0.0, seed=0, b_weight=False)
 
 
 def linear_bwd_weight(dy, x, dW, db=None):
-    """dW += dy^T x ; db += colsum(dy) (fused into the same GEMM pass over dy)."""
+    """dW += dy^T x ; db += colsum(dy) (fused into the same GEMM pass over dy); x fp32 or Planes."""
     M, N = dy.shape
     K = x.shape[1]
-    gemm(N, K, M, dy, x, dW, mode_a=RC, lda=dy.stride(0), mode_b=RC, ldb=x.stride(0), ldc=dW.stride(0),
-         R=dW, beta=1.0, rowsum=db, _keep_a16=True)
+    gemm(N, K, M, dy, x, dW, mode_a=RC, lda=dy.stride(0), mode_b=RC, ldb=x.ld if isinstance(x, Planes) else x.stride(0),
+         ldc=dW.stride(0), R=dW, beta=1.0, rowsum=db, _keep_a16=True)
 
 
 def colsum(x2d, out, accumulate=True, M=None, N=None, ld=None):
@@ -570,6 +726,12 @@ def layernorm_fwd(x2d, w, b, y, mean, rstd, eps=1e-12):
     _native.call("esp_layernorm_fwd", _p(x2d), _p(w), _p(b), _p(y), _p(mean), _p(rstd), M, D, float(eps), _st())
 
 
+def layernorm_fwd_planes(x2d, w, b, y: "Planes", mean, rstd, eps=1e-12):
+    M, D = x2d.shape
+    _native.call("esp_layernorm_fwd_planes", _p(x2d), _p(w), _p(b), _p(y.buf), y.ld, y.ps, y.n, _p(mean), _p(rstd),
+                 M, D, float(eps), _st())
+
+
 def layernorm_bwd(dy, x, w, mean, rstd, dx, dw, db, accumulate=False):
     M, D = x.shape
     n = _wsize("esp_layernorm_bwd", M, D)
@@ -603,11 +765,17 @@ def dwconv1d_wgrad(dy, x, dW, Bn, T, D, K, tvalid=None):
 
 
 def bn_swish_fwd(y, gamma, beta, s, mean, rstd, run_mean, run_var, momentum=0.1, eps=1e-5, T=0, tvalid=None):
+    """s: fp32 [M, D] or Planes (esp_bn_swish_fwd_planes)."""
     M, D = y.shape
     n = _wsize("esp_bn_swish_fwd", M, D)
     ws = _ws(WS, "esp_bn_swish_fwd", n, y.device)
-    _native.call("esp_bn_swish_fwd", _p(y), _p(gamma), _p(beta), _p(s), _p(mean), _p(rstd), _p(run_mean),
-                 _p(run_var), float(momentum), float(eps), M, D, _p(ws), n, int(T), _p(tvalid), _st())
+    if isinstance(s, Planes):
+        _native.call("esp_bn_swish_fwd_planes", _p(y), _p(gamma), _p(beta), _p(s.buf), s.ld, s.ps, s.n, _p(mean),
+                     _p(rstd), _p(run_mean), _p(run_var), float(momentum), float(eps), M, D, _p(ws), n, int(T),
+                     _p(tvalid), _st())
+    else:
+        _native.call("esp_bn_swish_fwd", _p(y), _p(gamma), _p(beta), _p(s), _p(mean), _p(rstd), _p(run_mean),
+                     _p(run_var), float(momentum), float(eps), M, D, _p(ws), n, int(T), _p(tvalid), _st())
     _guard_post("esp_bn_swish_fwd", ws, n)
 
 

@@ -87,6 +87,24 @@ int esp_gemm_f32_bp(int mode_a, int mode_b, int M, int N, int K, int batch, int 
                     float* aux, float drop_p, unsigned long long seed, int bwd_act, const float* pre, float* rowsum,
                     const int* im2col_a, float* work, long work_bytes, const void* b_planes, long ldbp, long sbp1,
                     long sbp2, long b_pstride, void* stream);
+/* esp_gemm_f32 with either operand, or both, also given as its three bf16 split planes (layout of
+ * esp_gemm_f32_bp's B planes; A planes: a_planes, ldap, sap1, sap2, a_pstride in bf16 elements, mode KC
+ * or RC, K % 8 == 0 for KC, M % 8 == 0 for RC).  Both as planes: no operand split in the k-loop (the
+ * same products, bit for bit; 64-wide tiles).  An operand whose planes do not qualify, or a launch
+ * with no planes kernel, takes its fp32 values (which may then not be NULL); A NULL fp32 operand with
+ * qualifying planes is allowed.  mode_a, mode_b: 0 (KC) or 1 (RC).
+ * c_nplanes 3 or 1: C is written as bf16 planes (the exact split / bf16) instead of fp32 -- C points at
+ * plane 0, plane p at C + p * c_pstride bf16 elements, ldc / sc1 / sc2 in bf16 elements (aux and pre
+ * share those offsets in fp32 elements) -- for the epilogues whose result only GEMMs read: plain
+ * (the attention context) and bias + activation + dropout + derivative (the FFN hidden state);
+ * N % 4 == 0, no residual, no row sums, never split-K.  0: fp32 C. */
+int esp_gemm_f32_pl(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2, const float* A, long lda,
+                    long sa1, long sa2, const void* a_planes, long ldap, long sap1, long sap2, long a_pstride,
+                    const float* B, long ldb, long sb1, long sb2, const void* b_planes, long ldbp, long sbp1,
+                    long sbp2, long b_pstride, float* C, long ldc, long sc1, long sc2, const float* bias,
+                    float alpha, float beta, const float* R, int act, float* aux, float drop_p,
+                    unsigned long long seed, int bwd_act, const float* pre, float* rowsum, int c_nplanes,
+                    long c_pstride, float* work, long work_bytes, void* stream);
 /* The three bf16 planes of a rows x cols fp32 matrix x (row pitch ldx): plane p at y + p * pstride
  * (bf16 elements, row pitch ldy), hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid), round to
  * nearest even with exact fp32 residuals, so x = hi + mid + lo for every finite x.  Columns
@@ -151,6 +169,11 @@ int esp_rng_advance(unsigned long long* key, void* stream);
 /* ---- normalisation (layer_norm.py:12-38; convolution.py:56-79) */
 int esp_layernorm_fwd(const float* x, const float* w, const float* b, float* y, float* mean,
                       float* rstd, int M, int D, float eps, void* stream);
+/* esp_layernorm_fwd with y written as bf16 planes for GEMM readers (kernels.Planes): nplanes 3 = the
+ * exact split hi + mid + lo (esp_f32_to_planes), 1 = bf16(y); plane p at y + p * pstride (bf16
+ * elements), row pitch ldy (>= D, % 4 == 0).  D % 4 == 0, x / w / b 16-B aligned, y 8-B aligned. */
+int esp_layernorm_fwd_planes(const float* x, const float* w, const float* b, void* y, long ldy, long pstride,
+                             int nplanes, float* mean, float* rstd, int M, int D, float eps, void* stream);
 int esp_layernorm_bwd(const float* dy, const float* x, const float* w, const float* mean,
                       const float* rstd, float* dx, int accumulate, float* dw, float* db, int M,
                       int D, float* work, long work_bytes, void* stream);
@@ -171,6 +194,13 @@ int esp_dwconv1d_wgrad(const float* dy, const float* x, float* dW, int Bn, int T
 int esp_bn_swish_fwd(const float* y, const float* gamma, const float* beta, float* s, float* mean,
                      float* rstd, float* run_mean, float* run_var, float momentum, float eps, int M,
                      int D, double* work, long work_bytes, int T, const int* tvalid, void* stream);
+/* esp_bn_swish_fwd with s written as bf16 planes for pointwise_conv2, its only reader (nplanes 3:
+ * the exact split, 1: bf16; plane p at s_planes + p * pstride bf16 elements, row pitch lds).
+ * D, lds, pstride % 4 == 0; 16-B aligned y / gamma / beta, 8-B aligned planes. */
+int esp_bn_swish_fwd_planes(const float* y, const float* gamma, const float* beta, void* s_planes, long lds,
+                            long pstride, int nplanes, float* mean, float* rstd, float* run_mean, float* run_var,
+                            float momentum, float eps, int M, int D, double* work, long work_bytes, int T,
+                            const int* tvalid, void* stream);
 /* eval mode: statistics from run_mean / run_var (mean / rstd written for inspection) */
 int esp_bn_swish_eval(const float* y, const float* gamma, const float* beta, float* s, const float* run_mean,
                       const float* run_var, float eps, int M, int D, float* mean, float* rstd, void* stream);

@@ -905,3 +905,141 @@ def test_guard_mode_canaries(dev, monkeypatch):
 def _native_ws(name, *dims):
     from espnet_slurp_amd import _native
     return _native.workspace_bytes(name, *dims)
+
+
+@pytest.mark.parametrize("shape", [(300, 264, 128), (1000, 1024, 96), (136, 64, 200), (6000, 256, 192)])
+@pytest.mark.parametrize("mb", [0, 1])
+def test_gemm_planes_both_operands_bit_exact(dev, shape, mb):
+    """A as kernels.Planes and B a weight (esp_gemm_f32_pl, both operands' planes from LDS: no split
+    in the k-loop) equals the in-register split bit for bit on unsplit launches (K < 256), with the
+    fused epilogues of the forward / input-gradient call sites, K tails (200) and ragged M / N."""
+    M, N, Kk = shape
+    A = _r(M, Kk, seed=61).to(dev)
+    B = (_r(N, Kk, seed=62) if mb == K.KC else _r(Kk, N, seed=62)).to(dev)
+    bias = _r(N, seed=63).to(dev)
+    R = _r(M, N, seed=64).to(dev)
+    pre = _r(M, N, seed=65).to(dev)
+    Ap = K.Planes.of(A)
+    assert torch.equal(Ap.float().cpu(), A.cpu())
+    cases = [dict()]
+    if mb == K.KC:
+        cases += [dict(bias=bias, act=K.ACT_SWISH | K.ACT_AUX_DERIV, aux="aux", drop_p=0.1, seed=7),
+                  dict(bias=bias, drop_p=0.1, seed=9, R=R, beta=1.0, alpha=0.5), dict(bias=bias)]
+    else:
+        cases += [dict(bwd_act=K.ACT_MUL, pre=pre), dict(R=R, beta=1.0)]
+    for kw in cases:
+        outs = []
+        for planes in (False, True):
+            C = torch.empty(M, N, device=dev)
+            aux = torch.empty(M, N, device=dev) if kw.get("aux") else None
+            k2 = dict(kw)
+            if aux is not None:
+                k2["aux"] = aux
+            X = Ap if planes else A
+            _with_bplanes(planes, lambda: K.gemm(M, N, Kk, X, B, C, mode_a=K.KC, lda=Ap.ld if planes else Kk,
+                                                 mode_b=mb, ldb=B.stride(0), ldc=N, b_weight=True, **k2))
+            outs.append((C, aux))
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0][0], outs[1][0]), (kw.keys(), (outs[0][0] - outs[1][0]).abs().max().item())
+        if outs[0][1] is not None:
+            assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("shape", [(256, 512, 192), (768, 256, 2000), (1024, 264, 47872 // 8)])
+def test_gemm_weight_gradient_planes(dev, shape):
+    """Weight gradient dW += dy^T x with x as Planes (RC x RC: B planes, A split) and the fused bias
+    gradient: equal to the fp32-x launch (bit for bit without split-K, else within 2e-7 of |dy||x|)."""
+    N, Kd, M = shape  # dW (N, Kd), rows M
+    dy = _r(M, N, seed=71).to(dev)
+    x = _r(M, Kd, seed=72).to(dev)
+    xp = K.Planes.of(x)
+    res = []
+    for planes in (False, True):
+        dW = torch.zeros(N, Kd, device=dev)
+        db = torch.zeros(N, device=dev)
+        _with_bplanes(planes, lambda: K.linear_bwd_weight(dy, xp if planes else x, dW, db))
+        res.append((dW.cpu().double(), db.cpu().double()))
+    torch.cuda.synchronize()
+    den = dy.abs().t().cpu().double() @ x.abs().cpu().double()
+    if M < 256:
+        assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    assert ((res[0][0] - res[1][0]).abs() / den).max().item() <= 2e-7
+    assert (res[0][1] - res[1][1]).abs().max().item() <= 1e-5 * math.sqrt(M)
+
+
+@pytest.mark.parametrize("MD", [(777, 256), (64, 512), (5, 80)])
+def test_layernorm_planes(dev, MD):
+    """esp_layernorm_fwd_planes: the planes hold y exactly (hi + mid + lo, hi = bf16(y)), y / mean /
+    rstd equal the fp32 LayerNorm kernel's within fp32 rounding (the row sums run in another lane
+    order), and the bf16 form (n = 1) is bf16(y)."""
+    M, D = MD
+    x = (_r(M, D, seed=81) * 3 + 1).to(dev)
+    w, b = _r(D, seed=82).to(dev), _r(D, seed=83).to(dev)
+    y = torch.empty(M, D, device=dev)
+    m0, r0 = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    K.layernorm_fwd(x, w, b, y, m0, r0)
+    yp = K.Planes(M, D, dev, 3)
+    m1, r1 = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    K.layernorm_fwd_planes(x, w, b, yp, m1, r1)
+    y1 = K.Planes(M, D, dev, 1)
+    K.layernorm_fwd_planes(x, w, b, y1, torch.empty(M, device=dev), torch.empty(M, device=dev))
+    torch.cuda.synchronize()
+    yf = yp.float()
+    assert (yf - y).abs().max().item() <= 4e-6 * max(1.0, y.abs().max().item())
+    assert torch.allclose(m1, m0, rtol=1e-6, atol=1e-6) and torch.allclose(r1, r0, rtol=1e-6, atol=0)
+    hi = yp.buf.view(3, M, yp.ld)[0, :, :D]
+    assert torch.equal(hi, yf.to(torch.bfloat16))
+    assert torch.equal(y1.buf.view(M, y1.ld)[:, :D], yf.to(torch.bfloat16))
+
+
+def test_gemm_planes_output_epilogues(dev):
+    """C written as planes (esp_gemm_f32_pl c_nplanes = 3): the FFN w_1 epilogue (bias + Swish / ReLU
+    + dropout, derivative to aux) with A and B as planes, and the batched attention context P.V
+    (fp32 operands, strided output): the planes hold exactly the fp32 epilogue's values (hi + mid + lo
+    == the fp32 C of the same launch) and aux is unchanged."""
+    M, N, Kk = 1000, 1024, 192  # K < 256: no split-K for the fp32-C launch either (a planes C never splits)
+    A = _r(M, Kk, seed=91).to(dev)
+    W = _r(N, Kk, seed=92, scale=0.1).to(dev)
+    bias = _r(N, seed=93).to(dev)
+    Ap = K.Planes.of(A)
+    for act, p in ((K.ACT_SWISH, 0.1), (K.ACT_RELU, 0.1), (K.ACT_SWISH, 0.0)):
+        outs = []
+        for pl in (False, True):
+            C = K.Planes(M, N, dev) if pl else torch.empty(M, N, device=dev)
+            aux = torch.empty(M, N, device=dev)
+            K.gemm(M, N, Kk, Ap, W, C, mode_a=K.KC, lda=Ap.ld, mode_b=K.KC, ldb=Kk, ldc=N, bias=bias,
+                   act=act | K.ACT_AUX_DERIV, aux=aux, drop_p=p, seed=5, b_weight=True)
+            outs.append((C.float() if pl else C, aux))
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1]), act
+    # P.V: z = 6 (head, utterance) pairs of T = 77 rows, d_k = 64, context rows strided into [B*T, D]
+    Bn, H, T, dk = 2, 3, 77, 64
+    D, Tp = H * dk, 80
+    P = _r(H * Bn * T * Tp, seed=94).to(dev)
+    V = _r(Bn * T, 3 * D, seed=95).to(dev)
+    outs = []
+    for pl in (False, True):
+        C = K.Planes(Bn * T, D, dev) if pl else torch.empty(Bn * T, D, device=dev)
+        K.gemm(T, dk, T, P, V, C, mode_a=K.KC, lda=Tp, mode_b=K.RC, ldb=3 * D, ldc=D, b_off=2 * D, batch=H * Bn,
+               nb2=Bn, sa=(Bn * T * Tp, T * Tp), sb=(dk, T * 3 * D), sc=(dk, T * D))
+        outs.append(C.float() if pl else C)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+
+
+def test_bn_swish_planes(dev):
+    """esp_bn_swish_fwd_planes: the same statistics (mean, rstd, running averages) as the fp32 kernel and
+    planes holding exactly its s values (hi + mid + lo == s)."""
+    M, D = 3000, 256
+    y = _r(M, D, seed=101).to(dev)
+    g, b = _r(D, seed=102).to(dev), _r(D, seed=103).to(dev)
+    outs = []
+    for pl in (False, True):
+        s = K.Planes(M, D, dev) if pl else torch.empty(M, D, device=dev)
+        mean, rstd = torch.empty(D, device=dev), torch.empty(D, device=dev)
+        rm, rv = torch.zeros(D, device=dev), torch.ones(D, device=dev)
+        K.bn_swish_fwd(y, g, b, s, mean, rstd, rm, rv)
+        outs.append((s.float() if pl else s, mean, rstd, rm, rv))
+    torch.cuda.synchronize()
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)

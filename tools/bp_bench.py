@@ -1,7 +1,7 @@
-"""B-planes GEMM (esp_gemm_f32_bp, PREC 3) vs the in-register split (PREC 0) on the weight-B
-shapes of the C2 step at B=128: forward (KC x KC) and input-gradient (KC x RC) linears and the
-conv2 forward.  Planes made once (param_cast_scope), as in the Trainer step.  Prints per shape
-the kernel time of both and the max |difference| (0 when no split-K)."""
+"""Planes GEMMs vs the in-register split (PREC 0) on the weight-B shapes of the C2 step at B=128:
+forward (KC x KC) and input-gradient (KC x RC) linears and the conv2 forward; B planes (PREC 3) and
+A + B planes (PREC 5, A as kernels.Planes).  Weight planes made once (param_cast_scope), as in the
+Trainer step.  Prints per shape the kernel time of each and the max |difference| (0 when no split-K)."""
 import os
 import sys
 
@@ -30,6 +30,8 @@ SHAPES = [  # (mode_a, mode_b, M, N, K, label)
 
 
 def run(ma, mb, m, n, k, reps=10):
+    """kernel ms of: the in-register split (fp32 A and B), B planes, A and B planes (A as kernels.Planes;
+    KC / RC A only); max |difference| of the planes results to the split one"""
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev).manual_seed(m + n + k)
     ic_a = None
@@ -43,22 +45,27 @@ def run(ma, mb, m, n, k, reps=10):
     B = torch.randn(n * k, device=dev, generator=g)
     ldb = k if mb == 0 else n
     out = {}
-    for bp in (False, True):
+    modes = ("split", "bp", "pl") if ma in (0, 1) else ("split", "bp")
+    for mode in modes:
         C = torch.empty(m * n, device=dev)
-        kw = dict(mode_a=ma, lda=lda, mode_b=mb, ldb=ldb, ldc=n, ic_a=ic_a, b_weight=bp)
+        Ax, la = A, lda
+        if mode == "pl":
+            Ax = K.Planes.of(A.view(m, k) if ma == 0 else A.view(k, m))
+            la = Ax.ld
+        kw = dict(mode_a=ma, lda=la, mode_b=mb, ldb=ldb, ldc=n, ic_a=ic_a, b_weight=mode != "split")
         with K.param_cast_scope():
             for _ in range(2):
-                K.gemm(m, n, k, A, B, C, **kw)
+                K.gemm(m, n, k, Ax, B, C, **kw)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(reps):
-                K.gemm(m, n, k, A, B, C, **kw)
+                K.gemm(m, n, k, Ax, B, C, **kw)
             e1.record()
             torch.cuda.synchronize()
-        out[bp] = (e0.elapsed_time(e1) / reps, C)
-    d = (out[True][1] - out[False][1]).abs().max().item()
-    return out[False][0], out[True][0], d
+        out[mode] = (e0.elapsed_time(e1) / reps, C)
+    d = max((out[x][1] - out["split"][1]).abs().max().item() for x in modes)
+    return {x: out[x][0] for x in modes}, d
 
 
 def one(i, bp, reps):
@@ -81,15 +88,16 @@ def one(i, bp, reps):
 def main():
     if len(sys.argv) > 1:
         return one(int(sys.argv[1]), sys.argv[2] == "1", int(sys.argv[3]) if len(sys.argv) > 3 else 5)
-    tot0 = tot1 = 0.0
+    tot = {}
     for ma, mb, m, n, k, label in SHAPES:
-        t0, t1, d = run(ma, mb, m, n, k)
+        t, d = run(ma, mb, m, n, k)
         fl = 2.0 * m * n * k
-        tot0 += t0
-        tot1 += t1
-        print(f"{label:12s} ({ma},{mb},{m},{n},{k})  split {1e3 * t0:8.1f} us {fl / t0 / 1e9:6.1f} TF/s   "
-              f"planes {1e3 * t1:8.1f} us {fl / t1 / 1e9:6.1f} TF/s   x{t0 / t1:5.2f}  maxdiff {d:.3g}", flush=True)
-    print(f"total split {tot0:.3f} ms planes {tot1:.3f} ms")
+        line = f"{label:12s} ({ma},{mb},{m},{n},{k})"
+        for x, ms in t.items():
+            tot[x] = tot.get(x, 0.0) + ms
+            line += f"  {x} {1e3 * ms:8.1f} us {fl / ms / 1e9:6.1f} TF/s"
+        print(line + f"  maxdiff {d:.3g}", flush=True)
+    print("total " + " ".join(f"{x} {v:.3f} ms" for x, v in tot.items()))
 
 
 if __name__ == "__main__":
