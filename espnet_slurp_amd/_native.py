@@ -40,6 +40,7 @@ SIGNATURES = {
     "esp_set_splitk_mode": [I],
     "esp_act_bwd": [P, P, P, L, I, F, U64, L, P],
     "esp_scale_dropout": [P, P, L, F, F, U64, P, F, P],
+    "esp_scale_dropout_planes": [P, P, L, L, I, F, F, U64, P],
     "esp_scale_by_dev": [P, L, P, P],
     "esp_embed_fwd": [P, P, P, P, I, I, I, F, F, U64, P],
     "esp_embed_bwd": [P, P, P, I, I, I, F, F, U64, P],

@@ -46,6 +46,12 @@ def empty(*shape, like: torch.Tensor):
     return torch.empty(*shape, dtype=torch.float32, device=like.device)
 
 
+def grad_buf(dout):
+    """The buffer of a branch gradient that only the branch's weight- and input-gradient GEMMs read:
+    kernels.Planes in the fp32 mode (the GEMMs then split nothing), else fp32 like dout."""
+    return K.grad_planes_like(dout) or torch.empty_like(dout)
+
+
 class Linear(nn.Module):
     """Parameter container with torch.nn.Linear's names/shapes/init (weight (out,in), bias)."""
 
@@ -139,10 +145,11 @@ class PositionwiseFeedForward(nn.Module):
 
     def bwd(self, c, dout):
         """dout: grad w.r.t. the residual output; returns grad w.r.t. x2d (new buffer)."""
-        dz = torch.empty_like(dout)
+        dz = grad_buf(dout)
         K.scale_dropout(dout, dz, alpha=c.alpha, drop_p=c.pr, seed=c.s2)
         K.linear_bwd_weight(dz, c.h, self.w_2.weight.grad, self.w_2.bias.grad)
-        dh = torch.empty_like(c.dact)
+        # dh feeds only w_1's weight- and input-gradient GEMMs: planes from the multiply epilogue
+        dh = grad_buf(c.dact)
         K.linear_bwd_data_act(dz, self.w_2.weight, dh, c.dact, K.ACT_MUL)
         return self.w_1.bwd(dh, c.x)
 
@@ -252,7 +259,7 @@ class RelPositionMultiHeadedAttention(nn.Module):
         B, T, P = c.B, c.T, c.P
         M, Z = B * T, H * B
         relpos = 2 if self.legacy else 1
-        dz = torch.empty_like(dout)
+        dz = grad_buf(dout)
         K.scale_dropout(dout, dz, drop_p=c.pr, seed=c.so)
         dctx = self.linear_out.bwd(dz, c.ctx)
         dqkv = empty(M, 3 * D, like=dout)
@@ -418,7 +425,7 @@ class MultiHeadedAttention(nn.Module):
         D = H * dk
         B, Tq, Tk = c.B, c.Tq, c.Tk
         Z = H * B
-        dz = torch.empty_like(dout)
+        dz = grad_buf(dout)
         K.scale_dropout(dout, dz, drop_p=c.pr, seed=c.so)
         dctx = self.linear_out.bwd(dz, c.ctx)
         if c.mem is None:
@@ -504,7 +511,7 @@ class ConvolutionModule(nn.Module):
 
     def bwd(self, c, dout):
         M, D = dout.shape
-        dz = torch.empty_like(dout)
+        dz = grad_buf(dout)
         K.scale_dropout(dout, dz, drop_p=c.pr, seed=c.so)
         w2 = self.pointwise_conv2.weight
         K.linear_bwd_weight(dz, c.s, w2.grad.view(D, D), self.pointwise_conv2.bias.grad)

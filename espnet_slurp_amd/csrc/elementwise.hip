@@ -93,6 +93,30 @@ __global__ void scale_drop4_kernel(const float* __restrict__ x, float* __restric
   }
 }
 
+// the same without a residual, y written as bf16 planes (n = 3 exact split, 1 = bf16) of a matrix whose
+// rows are whole planes rows (ld == cols): the backward's residual-branch gradient that only the
+// branch's weight- and input-gradient GEMMs read (kernels.Planes)
+__global__ void scale_drop4_planes_kernel(const float* __restrict__ x, uint16_t* __restrict__ y, long n4, long ps,
+                                          int np, float alpha, uint32_t thr, float scale, uint64_t seed,
+                                          const uint64_t* __restrict__ key) {
+  seed = esp::keyed(seed, key);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const float4 v4 = reinterpret_cast<const float4*>(x)[i];
+    float v[4] = {v4.x, v4.y, v4.z, v4.w};
+    bool kp[4] = {true, true, true, true};
+    if (thr) {
+      esp::keep_pair(seed, (uint64_t)(4 * i), thr, kp[0], kp[1]);
+      esp::keep_pair(seed, (uint64_t)(4 * i + 2), thr, kp[2], kp[3]);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (thr) v[e] = kp[e] ? v[e] * scale : 0.f;
+      v[e] *= alpha;
+    }
+    esp::store_planes4(y, 4 * i, ps, np, v[0], v[1], v[2], v[3]);
+  }
+}
+
 // encoder input of the blocks: x = drop(x * xscale); pos = drop(pos)  (embedding.py:228-244)
 // decoder: x = drop(E[tok] * xscale + pe[l])                            (embedding.py:81-94)
 __global__ void embed_fwd_kernel(const int64_t* __restrict__ tok, const float* __restrict__ E,
@@ -337,6 +361,20 @@ ESP_API int esp_scale_dropout(const float* x, float* y, long n, float alpha, flo
     hipLaunchKernelGGL(scale_drop_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, x, y, n, alpha, thr,
                        esp::drop_scale(thr), (uint64_t)seed, r, beta, esp::rng_key_ptr());
   ESP_CHECK_LAUNCH("esp_scale_dropout");
+  return 0;
+}
+
+ESP_API int esp_scale_dropout_planes(const float* x, void* y, long n, long pstride, int nplanes, float alpha,
+                                     float drop_p, unsigned long long seed, void* stream) {
+  ESP_ARG_CHECK(drop_p < 1.f, "dropout p must be < 1 (got %g)", (double)drop_p);
+  ESP_ARG_CHECK(n % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 7) == 0 && (nplanes == 1 || nplanes == 3) &&
+                    pstride % 4 == 0 && (nplanes == 1 || pstride >= n),
+                "esp_scale_dropout_planes: n, pstride %% 4 == 0, aligned x / y, nplanes 1 or 3");
+  const uint32_t thr = esp::drop_threshold(drop_p);
+  hipLaunchKernelGGL(scale_drop4_planes_kernel, dim3(grid_for(n / 4)), dim3(256), 0, (hipStream_t)stream, x,
+                     (uint16_t*)y, n / 4, pstride, nplanes, alpha, thr, esp::drop_scale(thr), (uint64_t)seed,
+                     esp::rng_key_ptr());
+  ESP_CHECK_LAUNCH("esp_scale_dropout_planes");
   return 0;
 }
 

@@ -168,6 +168,7 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
     if (kind < 0 || !g.wide) return false;
     if (kind == EPI_P0_PL && !(MA == KC && MB == RC)) return false;
     if ((kind == EPI_FFN_SWISH_PL || kind == EPI_FFN_RELU_PL) && !(MA == KC && MB == KC)) return false;
+    if (kind == EPI_BMUL_PL && !(MA == KC && MB == RC)) return false;
   }
   if (kind == EPI_SMB && !(MA == KC && MB == KC && g.bf16 == 0)) return false;
   if (!g.cpn && (((kind == EPI_BMUL || kind == EPI_RMASK) && !can_spec_bwd) || ((kind == EPI_P0 || kind == EPI_PR) && !can_pspec) ||

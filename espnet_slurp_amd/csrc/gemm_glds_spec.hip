@@ -33,6 +33,7 @@ bool glds_launch_spec(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hip
     } else if constexpr (MA == KC && MB == RC) {
       ESP_SPEC(EPI_BMUL)
       ESP_SPEC(EPI_RMASK)
+      ESP_SPEC(EPI_BMUL_PL)
     } else if constexpr (MA == I2CT_KC && MB == RC) {
       ESP_SPEC(EPI_RMASKMAP)
     }

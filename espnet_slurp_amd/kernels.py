@@ -565,11 +565,15 @@ def linear_fwd(x2d, W, b, out, *, act=ACT_NONE, aux=None, drop_p=0.0, seed=0, al
     return out
 
 
+def _ld(x):
+    return x.ld if isinstance(x, Planes) else x.stride(0)
+
+
 def linear_bwd_data(dy, W, dx, *, accumulate=False):
-    """dx (+)= dy W ; dy (M,N), W (N,K)."""
+    """dx (+)= dy W ; dy (M,N) fp32 or Planes, W (N,K)."""
     M, N = dy.shape
     K = W.shape[1]
-    gemm(M, K, N, dy, W, dx, mode_a=KC, lda=dy.stride(0), mode_b=RC, ldb=W.stride(0), ldc=dx.stride(0),
+    gemm(M, K, N, dy, W, dx, mode_a=KC, lda=_ld(dy), mode_b=RC, ldb=W.stride(0), ldc=dx.stride(0),
          R=dx if accumulate else None, beta=1.0)
     return dx
 
@@ -579,7 +583,7 @@ def linear_bwd_data_act(dy, W, dx, pre, act, drop_p=0.0, seed=0, b_weight=False)
     h = drop(act(pre)) (positionwise_feed_forward.py:32)."""
     M, N = dy.shape
     K = W.shape[1]
-    gemm(M, K, N, dy, W, dx, mode_a=KC, lda=dy.stride(0), mode_b=RC, ldb=W.stride(0), ldc=dx.stride(0),
+    gemm(M, K, N, dy, W, dx, mode_a=KC, lda=_ld(dy), mode_b=RC, ldb=W.stride(0), ldc=_ld(dx),
          bwd_act=act, pre=pre, drop_p=drop_p, seed=seed, b_weight=b_weight)
     return dx
 
@@ -588,8 +592,8 @@ def linear_bwd_weight(dy, x, dW, db=None):
     """dW += dy^T x ; db += colsum(dy) (fused into the same GEMM pass over dy); x fp32 or Planes."""
     M, N = dy.shape
     K = x.shape[1]
-    gemm(N, K, M, dy, x, dW, mode_a=RC, lda=dy.stride(0), mode_b=RC, ldb=x.ld if isinstance(x, Planes) else x.stride(0),
-         ldc=dW.stride(0), R=dW, beta=1.0, rowsum=db, _keep_a16=True)
+    gemm(N, K, M, dy, x, dW, mode_a=RC, lda=_ld(dy), mode_b=RC, ldb=_ld(x), ldc=dW.stride(0), R=dW, beta=1.0,
+         rowsum=db, _keep_a16=True)
 
 
 def colsum(x2d, out, accumulate=True, M=None, N=None, ld=None):
@@ -609,9 +613,24 @@ def act_bwd(dy, h, dx, act, drop_p=0.0, seed=0, idx_off=0):
 
 
 def scale_dropout(x, y, alpha=1.0, drop_p=0.0, seed=0, r=None, beta=1.0):
+    """y = alpha * drop(x) (+ beta * r); y fp32 or Planes (no residual; x contiguous rows)."""
+    if isinstance(y, Planes):
+        assert r is None and y.ld == y.cols and x.numel() == y.rows * y.cols
+        _native.call("esp_scale_dropout_planes", _p(x), _p(y.buf), x.numel(), y.ps, y.n, float(alpha), float(drop_p),
+                     seed, _st())
+        return y
     _native.call("esp_scale_dropout", _p(x), _p(y), x.numel(), float(alpha), float(drop_p), seed, _p(r),
                  float(beta), _st())
     return y
+
+
+def grad_planes_like(x2d):
+    """A backward gradient that only GEMMs read (a branch's weight- and input-gradient GEMMs), as Planes in
+    the fp32 mode (None otherwise: the caller keeps fp32)."""
+    M, D = x2d.shape
+    if planes_mode() == 3 and D % 8 == 0 and x2d.is_contiguous():
+        return Planes(M, D, x2d.device)
+    return None
 
 
 def scale_by_dev(x, s):

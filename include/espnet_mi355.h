@@ -96,7 +96,8 @@ int esp_gemm_f32_bp(int mode_a, int mode_b, int M, int N, int K, int batch, int 
  * c_nplanes 3 or 1: C is written as bf16 planes (the exact split / bf16) instead of fp32 -- C points at
  * plane 0, plane p at C + p * c_pstride bf16 elements, ldc / sc1 / sc2 in bf16 elements (aux and pre
  * share those offsets in fp32 elements) -- for the epilogues whose result only GEMMs read: plain
- * (the attention context) and bias + activation + dropout + derivative (the FFN hidden state);
+ * (the attention context), bias + activation + dropout + derivative (the FFN hidden state) and the
+ * backward multiply by pre (bwd_act ACT_MUL, no dropout / bias: the FFN hidden-state gradient);
  * N % 4 == 0, no residual, no row sums, never split-K.  0: fp32 C. */
 int esp_gemm_f32_pl(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2, const float* A, long lda,
                     long sa1, long sa2, const void* a_planes, long ldap, long sap1, long sap2, long a_pstride,
@@ -132,6 +133,11 @@ int esp_act_bwd(const float* dy, const float* h, float* dx, long n, int act, flo
                 unsigned long long seed, long idx_off, void* stream);
 int esp_scale_dropout(const float* x, float* y, long n, float alpha, float drop_p,
                       unsigned long long seed, const float* r, float beta, void* stream);
+/* y = alpha * drop(x) written as bf16 planes (nplanes 3 exact split, 1 bf16; plane p at y + p * pstride
+ * bf16 elements) of a matrix with ld == cols (n = rows * cols, % 4 == 0): the same masks as
+ * esp_scale_dropout for the same (drop_p, seed). */
+int esp_scale_dropout_planes(const float* x, void* y, long n, long pstride, int nplanes, float alpha, float drop_p,
+                             unsigned long long seed, void* stream);
 int esp_scale_by_dev(float* x, long n, const float* s, void* stream);
 /* decoder embedding + abs positional encoding (transformer_decoder.py:68-71, embedding.py:81-94) */
 int esp_embed_fwd(const long long* tok, const float* E, const float* pe, float* y, int nrows, int L,

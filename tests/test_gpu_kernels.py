@@ -1043,3 +1043,47 @@ def test_bn_swish_planes(dev):
     torch.cuda.synchronize()
     for a, c in zip(outs[0], outs[1]):
         assert torch.equal(a, c)
+
+
+def test_scale_dropout_planes_same_masks(dev):
+    """esp_scale_dropout_planes: the planes hold exactly esp_scale_dropout's values (same masks)."""
+    M, D = 1000, 256
+    x = _r(M, D, seed=111).to(dev)
+    y = torch.empty(M, D, device=dev)
+    K.scale_dropout(x, y, alpha=0.5, drop_p=0.1, seed=77)
+    yp = K.Planes(M, D, dev)
+    K.scale_dropout(x, yp, alpha=0.5, drop_p=0.1, seed=77)
+    torch.cuda.synchronize()
+    assert torch.equal(yp.float(), y)
+
+
+def test_ffn_backward_planes_matches_fp32(dev):
+    """The FFN backward with its branch gradients as planes (dz from the dropout backward, dh from the
+    derivative-multiply epilogue) gives the fp32 path's input and parameter gradients bit for bit where
+    no launch splits K, and within 2e-7 relative otherwise."""
+    from espnet_slurp_amd.blocks import PositionwiseFeedForward, Seeds
+    from espnet_slurp_amd.flat import FlatParams
+    torch.manual_seed(3)
+    res = []
+    for xplanes in (False, True):
+        prev = K._XPLANES
+        K._XPLANES = xplanes
+        try:
+            ff = PositionwiseFeedForward(256, 1024, 0.1, K.ACT_SWISH).to(dev)
+            torch.manual_seed(3)
+            for p in ff.parameters():
+                with torch.no_grad():
+                    p.copy_(torch.randn_like(p) * 0.05)
+            flat = FlatParams(ff, dev)
+            x = _r(2000, 256, seed=121).to(dev)
+            dout = _r(2000, 256, seed=122).to(dev)
+            with K.param_cast_scope():
+                xin = K.Planes.of(x) if xplanes else x
+                out, c = ff.fwd(xin, x, 0.5, 0.1, Seeds(5), True)
+                dx = ff.bwd(c, dout)
+            torch.cuda.synchronize()
+            res.append((out.clone(), dx.clone(), flat.grad.clone()))
+        finally:
+            K._XPLANES = prev
+    for a, b in zip(res[0], res[1]):
+        assert (a - b).abs().max().item() <= 2e-7 * max(1.0, a.abs().max().item()), (a - b).abs().max().item()
