@@ -59,6 +59,7 @@ SIGNATURES = {
     "esp_colsum": [P, I, I, L, P, I, P, L, P],
     "esp_glu_fwd": [P, P, L, I, P],
     "esp_glu_bwd": [P, P, P, L, I, P],
+    "esp_glu_bwd_planes": [P, P, P, L, I, L, I, P],
     "esp_dwconv1d": [P, P, P, P, I, I, I, I, I, P, P],
     "esp_dwconv1d_wgrad": [P, P, P, I, I, I, I, P, L, P, P],
     "esp_bn_swish_fwd": [P, P, P, P, P, P, P, P, F, F, I, I, P, L, I, P, P],

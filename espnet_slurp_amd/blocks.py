@@ -527,7 +527,8 @@ class ConvolutionModule(nn.Module):
         K.dwconv1d_wgrad(dy, c.g, dw.weight.grad, c.B, c.T, D, self.kernel_size, tvalid=c.tvalid)
         dg = ds  # reuse
         K.dwconv1d(dy, dw.weight, None, dg, c.B, c.T, D, self.kernel_size, flip=True, tvalid=c.tvalid)
-        du = empty(M, 2 * D, like=dout)
+        # du feeds only pointwise_conv1's weight- and input-gradient GEMMs
+        du = K.Planes(M, 2 * D, dout.device) if K.planes_mode() == 3 and D % 4 == 0 else empty(M, 2 * D, like=dout)
         K.glu_bwd(c.u, dg, du)
         w1 = self.pointwise_conv1.weight
         K.linear_bwd_weight(du, c.x, w1.grad.view(2 * D, D), self.pointwise_conv1.bias.grad)

@@ -513,6 +513,7 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
     const char* e = getenv("ESP_GEMM_ABL");
     if (e && (atoi(e) & 16)) g.wide = g.ragged4 = 0;
   }
+  g.drop_scale = 1.f;  // (the specialised dropout epilogues run unconditionally: p = 0 keeps every element at scale 1)
   if (drop_p > 0.f) {
     g.drop_thresh = esp::drop_threshold(drop_p);
     g.drop_scale = esp::drop_scale(g.drop_thresh);

@@ -329,6 +329,24 @@ __global__ void glu_bwd4_kernel(const float* __restrict__ u, const float* __rest
   }
 }
 
+// du written as bf16 planes (row pitch 2D, n = 3 exact split / 1 bf16) for pointwise_conv1's weight- and
+// input-gradient GEMMs, its only readers (kernels.Planes)
+__global__ void glu_bwd4_planes_kernel(const float* __restrict__ u, const float* __restrict__ dg,
+                                       uint16_t* __restrict__ du, long ps, int np, int rows, int D) {
+  const int nq = D >> 2, n = rows * nq;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int r = i / nq, c = 4 * (i - r * nq);
+    const float4 a = *reinterpret_cast<const float4*>(u + (long)r * 2 * D + c);
+    const float4 b = *reinterpret_cast<const float4*>(u + (long)r * 2 * D + D + c);
+    const float4 d = *reinterpret_cast<const float4*>(dg + (long)r * D + c);
+    const float sx = esp::fast_sigmoid(b.x), sy = esp::fast_sigmoid(b.y), sz = esp::fast_sigmoid(b.z),
+                sw = esp::fast_sigmoid(b.w);
+    esp::store_planes4(du, (long)r * 2 * D + c, ps, np, d.x * sx, d.y * sy, d.z * sz, d.w * sw);
+    esp::store_planes4(du, (long)r * 2 * D + D + c, ps, np, d.x * a.x * sx * (1.0f - sx), d.y * a.y * sy * (1.0f - sy),
+                       d.z * a.z * sz * (1.0f - sz), d.w * a.w * sw * (1.0f - sw));
+  }
+}
+
 __global__ void glu_bwd_kernel(const float* __restrict__ u, const float* __restrict__ dg, float* __restrict__ du,
                                long rows, int D) {
   const long n = rows * D;
@@ -889,6 +907,16 @@ ESP_API int esp_glu_fwd(const float* u, float* g, long rows, int D, void* stream
   return 0;
 }
 
+ESP_API int esp_glu_bwd_planes(const float* u, const float* dg, void* du, long pstride, int nplanes, long rows, int D,
+                               void* stream) {
+  ESP_ARG_CHECK((nplanes == 1 || nplanes == 3) && vec4_ok(rows * 2 * D, D, {u, dg}) && ((uintptr_t)du & 7) == 0 &&
+                    pstride % 4 == 0 && (nplanes == 1 || pstride >= rows * 2 * D),
+                "esp_glu_bwd_planes: D %% 4 == 0, aligned operands, nplanes 1 or 3");
+  hipLaunchKernelGGL(glu_bwd4_planes_kernel, dim3(gridn(rows * D / 4)), dim3(256), 0, (hipStream_t)stream, u, dg,
+                     (uint16_t*)du, pstride, nplanes, (int)rows, D);
+  ESP_CHECK_LAUNCH("esp_glu_bwd_planes");
+  return 0;
+}
 ESP_API int esp_glu_bwd(const float* u, const float* dg, float* du, long rows, int D, void* stream) {
   if (vec4_ok(rows * 2 * D, D, {u, dg, du}))
     hipLaunchKernelGGL(glu_bwd4_kernel, dim3(gridn(rows * D / 4)), dim3(256), 0, (hipStream_t)stream, u, dg, du,

@@ -766,7 +766,12 @@ def glu_fwd(u, g):
 
 
 def glu_bwd(u, dg, du):
+    """du: fp32 [rows, 2D] or Planes (esp_glu_bwd_planes)."""
     rows, D = dg.shape
+    if isinstance(du, Planes):
+        assert du.ld == 2 * D
+        _native.call("esp_glu_bwd_planes", _p(u), _p(dg), _p(du.buf), du.ps, du.n, rows, D, _st())
+        return
     _native.call("esp_glu_bwd", _p(u), _p(dg), _p(du), rows, D, _st())
 
 

@@ -142,15 +142,17 @@ class FlatGradReducer:
         hook.done = lambda: front[0] >= len(self.buckets)
         return hook
 
-    def broadcast_buffers(self, model):
+    def broadcast_buffers(self, model, async_op: bool = False):
         """DDP's broadcast_buffers (X7): rank 0's floating buffers (BatchNorm running stats) to
         every replica before the forward, as ONE broadcast of the flat buffer they are views
         of (flat.py).  Training-mode outputs do not read them, so this only keeps the
-        replicas' eval-mode state equal to rank 0's."""
+        replicas' eval-mode state equal to rank 0's.  async_op: returns the work handles."""
+        hs = []
         if self.flat.buffers:
-            dist.broadcast(self.flat.buf_flat, 0, group=self.group)
+            hs.append(dist.broadcast(self.flat.buf_flat, 0, group=self.group, async_op=async_op))
         for b in self.flat.other_buffers:
-            dist.broadcast(b, 0, group=self.group)
+            hs.append(dist.broadcast(b, 0, group=self.group, async_op=async_op))
+        return [h for h in hs if h is not None] if async_op else []
 
 
 def fused_stats_allreduce(stats: Dict[str, torch.Tensor], weight: torch.Tensor, group=None):

@@ -85,6 +85,9 @@ class Trainer:
         # DDP + graph: d loss of this replica = w_r / sum_r w / accum_grad, set on device between
         # the forward and the backward segments (the backward then yields pre-scaled gradients)
         self._scale = torch.ones(1, dtype=torch.float32, device=model.flat.flat.device)
+        # graph DP replays: this replica's batch weight and the all-reduced sum (see _dp_replay)
+        self._wloc = torch.ones(1, dtype=torch.float32, device=model.flat.flat.device)
+        self._wsum = torch.ones(1, dtype=torch.float32, device=model.flat.flat.device)
         self.reducer = (FlatGradReducer(model, model.flat, bucket_mb, hooks=not self.cuda_graph)
                         if self.distributed else None)
         self.iiter = 0          # micro-batches (trainer.py:502 iiter)
@@ -185,7 +188,11 @@ class Trainer:
         sig = (tuple(speech.shape), prep.T, prep.Umax, prep.L, prep.get("n_samples", 0), last,
                tuple((k, tuple(v.shape)) for k, v in sorted(prep.host.items())))
         e = self._graphs.pop(sig, None)
-        if self.distributed:  # DDP broadcast_buffers (X7), outside the graph (a collective)
+        if self.distributed and e is None:
+            # DDP broadcast_buffers (X7), outside the graph (a collective).  A replay broadcasts at the
+            # END of its step instead (_dp_replay), off the critical path: training-mode outputs never
+            # read the running statistics, nothing writes them between two steps, so every forward
+            # still starts from rank 0's buffers exactly as with DDP's broadcast before it.
             self.reducer.broadcast_buffers(model)
         if last:
             self.n_updates += 1
@@ -195,7 +202,7 @@ class Trainer:
             e.speech.copy_(speech, non_blocking=True)
             prep.copy_into(e.prep)
             if self.distributed:
-                self._dp_replay(e, last)
+                self._dp_replay(e, last, float(prep.host["weight"].view(-1)[0]))
             else:
                 e.graph.replay()
         self._graphs[sig] = e  # most recently used last
@@ -237,18 +244,39 @@ class Trainer:
         if self.options.accum_grad > 1:
             self._scale.mul_(1.0 / self.options.accum_grad)
 
-    def _dp_replay(self, e, last: bool):
+    def _dp_replay(self, e, last: bool, w_host: float):
+        # The critical path is forward graph -> backward segments (+ their bucket all-reduces):
+        #  * sum w: the batch weight is known on the host (espnet_model.prepare: weight = B, the
+        #    reference's force_gatherable(batch_size)), so its all-reduce runs beside the forward
+        #    replay, not between the forward and the first backward segment;
+        #  * the reported stats' recursive_average and DDP's buffer broadcast are launched after the
+        #    backward is queued and waited for at the end of the step (stream-ordered: the next step's
+        #    kernels run after them).
+        self._wloc.fill_(w_host)
+        self._wsum.copy_(self._wloc)
+        hw = dist.all_reduce(self._wsum, async_op=True)
         e.fwd.replay()
-        self._dp_scale(e.stats, e.weight)
+        hw.wait()
+        torch.div(self._wloc, self._wsum, out=self._scale)
+        if self.options.accum_grad > 1:
+            self._scale.mul_(1.0 / self.options.accum_grad)
         handles = []
         for g, buckets in e.segs:
             g.replay()
             if last and buckets:
                 handles += self.reducer.launch_sum(buckets)
+        keys = [k for k in e.stats if k != "grad_norm"]
+        vec = torch.cat([e.stats[k].view(-1)[:1].float() * self._wloc for k in keys] + [self._wloc])
+        tail = [dist.all_reduce(vec, async_op=True)] + self.reducer.broadcast_buffers(self.model, async_op=True)
         for h in handles:
             h.wait()
         if last:
             self._opt_tail()
+        for h in tail:
+            h.wait()
+        for i, k in enumerate(keys):
+            e.stats[k].view(-1)[:1].copy_(vec[i:i + 1] / vec[-1:])
+        self._last_weight = vec[-1:]
 
     def _dp_body(self, speech, prep):
         K.rng_advance(self._key)

@@ -187,6 +187,10 @@ int esp_colsum(const float* x, int M, int N, long ld, float* out, int accumulate
                long work_bytes, void* stream);
 int esp_glu_fwd(const float* u, float* g, long rows, int D, void* stream);
 int esp_glu_bwd(const float* u, const float* dg, float* du, long rows, int D, void* stream);
+/* esp_glu_bwd with du written as bf16 planes (nplanes 3 exact split, 1 bf16; row pitch 2D, plane p at
+ * du + p * pstride bf16 elements) for pointwise_conv1's gradient GEMMs; D % 4 == 0. */
+int esp_glu_bwd_planes(const float* u, const float* dg, void* du, long pstride, int nplanes, long rows, int D,
+                       void* stream);
 /* tvalid (device int, nullable): the batch is padded to T frames per utterance but only the
  * first *tvalid exist in the reference batch (length-bucketed HIP graphs).  The depthwise
  * convolution reads frames >= *tvalid as its zero padding and writes 0 there; BatchNorm
