@@ -177,9 +177,10 @@ def gemm_algorithmic_bytes(shapes) -> float:
             continue
         a = M * Kd * (4 / 9 if ma >= 2 else 1.0)
         b = N * Kd * (4 / 9 if mb >= 2 else 1.0)
-        # bf16-operand GEMMs read 2-byte A and B; B-planes GEMMs ("bp") read B as three bf16 planes
-        ea = 2.0 if key[6:] == ("bf16",) else 4.0
-        eb = 2.0 if key[6:] == ("bf16",) else 6.0 if key[6:] == ("bp",) else 4.0
+        # bf16-operand GEMMs read 2-byte A and B; B-planes GEMMs ("bp") read B as three bf16 planes,
+        # planes GEMMs ("pl") both operands
+        ea = 2.0 if key[6:] == ("bf16",) else 6.0 if key[6:] == ("pl",) else 4.0
+        eb = 2.0 if key[6:] == ("bf16",) else 6.0 if key[6:] in (("bp",), ("pl",)) else 4.0
         tot += n * batch * (ea * a + eb * b + 4.0 * M * N) + extra
     return tot
 

@@ -454,7 +454,7 @@ def _gemm_planes(M, N, K, A, B, C, mode_a, lda, mode_b, ldb, ldc, a_off, b_off, 
                          _GEMM_WS_BYTES, _st())
             if _PROF is not None:
                 ev1.record()
-                extra = 4.0 * M * N * batch * (aux is not None) - 1.0 * M * N * batch  # 6-B planes out, not 4-B
+                extra = 4.0 * M * N * batch * (aux is not None) + 2.0 * M * N * batch  # 6-B planes out, not 4-B
                 _PROF.append((2.0 * M * N * K * batch, ev0, ev1, (mode_a, mode_b, M, N, K, batch), extra))
             return
     assert batch == 1, "planes operands: unbatched GEMMs"
