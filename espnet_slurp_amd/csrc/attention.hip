@@ -775,6 +775,47 @@ __global__ __launch_bounds__(256) void relpos_attn_fwd_kernel(
 // blocks m <= g lie wholly below T (A rows q_v[i]), blocks m >= g+1 wholly at or above T (A rows
 // q_v[i+1], the shifted twin), so legacy selects the A operand per block and shares the ring.
 // LDS: ring rows of RW_PITCH floats (row groups r and r+4 of a 32-lane half 16 banks apart).
+// XS (the fp32 build's default, ESP_ATTN_XS=0: f32 MFMA): the ac and band products as bf16x6 split
+// products on v_mfma_f32_16x16x32_bf16 (the GEMM family's fp32 arithmetic, gemm_kernels.h): each
+// operand value v = hi + mid + lo exactly (three bf16), six products per pair, smallest first.  A
+// lane's 16 values of a row (d = 16 q4 + [0,16)) are the two k-halves of the 16x16x32 operand
+// (MFMA m takes d = 16 q4 + 8 m + [0, 8)); the output layout is the 16x16x4 one, so the ring,
+// softmax and stores are shared with the f32 form.
+typedef __attribute__((ext_vector_type(8))) __bf16 attn_bf16x8;
+struct Frag6 {
+  attn_bf16x8 v[3][2];  // [hi, mid, lo][k-half]
+};
+__device__ __forceinline__ void split_frag(const float (&f)[16], Frag6& o) {
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    uint32_t h[4], md[4], l[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) esp::split3_pair(f[8 * m + 2 * j], f[8 * m + 2 * j + 1], h[j], md[j], l[j]);
+    o.v[0][m] = __builtin_bit_cast(attn_bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
+    o.v[1][m] = __builtin_bit_cast(attn_bf16x8, make_uint4(md[0], md[1], md[2], md[3]));
+    o.v[2][m] = __builtin_bit_cast(attn_bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
+  }
+}
+__device__ __forceinline__ f32x4 mfma6(const Frag6& a, const Frag6& b, f32x4 c) {
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[1][m], b.v[1][m], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[2][m], b.v[0][m], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[0][m], b.v[2][m], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[1][m], b.v[0][m], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[0][m], b.v[1][m], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[0][m], b.v[0][m], c, 0, 0, 0);
+  }
+  return c;
+}
+
+#ifndef ESP_ATTN_XS_DEFAULT
+#if defined(ESP_F32_SPLIT) && ESP_F32_SPLIT == 0
+#define ESP_ATTN_XS_DEFAULT 0  // the f32-MFMA build (A/B runs)
+#else
+#define ESP_ATTN_XS_DEFAULT 1
+#endif
+#endif
 constexpr int RW_ROWS = 16, RW_PITCH = 37;
 constexpr int RW_SPITCH = 68;  // store-transpose rows: the two row groups of a ds_write_b32 half 16 banks apart
 // SPLIT = 2 (opt-in, ESP_ATTN_SPLIT=2): a row group's keys are shared by two waves of the block
@@ -782,8 +823,8 @@ constexpr int RW_SPITCH = 68;  // store-transpose rows: the two row groups of a 
 // 2); the row max and sum are combined through LDS with one block barrier each.  Measured at C2
 // B=128: 398 vs 395 us (327 vs 309 without dropout) — the kernel is not latency-bound but bound
 // by the SIMD's shared f32 MFMA / VALU issue, so the extra occupancy buys nothing.
-template <int NTA, bool P2, bool LEGACY, int SPLIT = 1>  // SPLIT * NTA >= ceil(T/16) key tiles
-__global__ __launch_bounds__(256, SPLIT == 2 ? 3 : 2) void relpos_attn_fwd16_kernel(
+template <int NTA, bool P2, bool LEGACY, int SPLIT = 1, bool XS = false>  // SPLIT * NTA >= ceil(T/16) key tiles
+__global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fwd16_kernel(
     const float* __restrict__ qu, const float* __restrict__ qv, const float* __restrict__ kmat, long ldk,
     const float* __restrict__ pm, long ldpm, int nb, float sqrt_dk, const int* __restrict__ klen,
     float* __restrict__ attn, float* __restrict__ pdrop, uint32_t thr, float dscale, uint64_t seed, int T, long lds,
@@ -827,7 +868,15 @@ __global__ __launch_bounds__(256, SPLIT == 2 ? 3 : 2) void relpos_attn_fwd16_ker
   float au[16], av[16], av2[16];
   ld16(qu + ((long)z * T + min(i0 + li, T - 1)) * RP_DK, au);
   ld16(qv + ((long)z * T + min(i0 + li, T - 1)) * RP_DK, av);
-  if (LEGACY) ld16(qv + ((long)z * T + min(i0 + 1 + li, T - 1)) * RP_DK, av2);
+  if (LEGACY && !XS) ld16(qv + ((long)z * T + min(i0 + 1 + li, T - 1)) * RP_DK, av2);
+  // XS: the query rows' split planes (once per wave).  Legacy: the band's A rows switch from q_v[i]
+  // to q_v[i+1] once, at block g+1, and never back, so xv is re-split from the shifted rows at that
+  // tile (one exposed load per wave) instead of holding both rows' planes
+  Frag6 xu, xv;
+  if constexpr (XS) {
+    split_frag(au, xu);
+    split_frag(av, xv);
+  }
   int kl = klen ? klen[b] : T;
   if (kl > T) kl = T;
 
@@ -836,7 +885,8 @@ __global__ __launch_bounds__(256, SPLIT == 2 ? 3 : 2) void relpos_attn_fwd16_ker
     for (int r = 0; r < 4; ++r) rg[(4 * q4 + r) * RW_PITCH + ((16 * m + li) & 31)] = s[r];
   };
   // fragments DEPTH tiles ahead: K(t) in kb[t % NB], band-block p rows P(m) in pb[m % NB]
-  constexpr int DEPTH = SPLIT == 2 ? 1 : 2, NB = DEPTH + 1;  // split: 3 waves per SIMD hide a tile less
+  // (split: 3 waves per SIMD hide a tile less; XS: the split planes of the current tile take the registers)
+  constexpr int DEPTH = SPLIT == 2 || XS ? 1 : 2, NB = DEPTH + 1;
   float kb[NB][16], pb[NB][16];  // indexed by the tile / block offset from t0
 #pragma unroll
   for (int d = 0; d < DEPTH; ++d) ld16(k_row(t0 + d), kb[d]);
@@ -845,9 +895,19 @@ __global__ __launch_bounds__(256, SPLIT == 2 ? 3 : 2) void relpos_attn_fwd16_ker
   {  // band block t0 (block 0 lies below T for every g: A rows q_v[i] in both variants)
     const bool shifted = LEGACY && t0 > g;
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (XS) {
+      Frag6 pf6;
+      split_frag(pb[0], pf6);
+      if (shifted) {  // (SPLIT 2: a second-half wave whose keys all lie past the switch)
+        ld16(qv + ((long)z * T + min(i0 + 1 + li, T - 1)) * RP_DK, av2);
+        split_frag(av2, xv);
+      }
+      s = mfma6(xv, pf6, s);
+    } else {
 #pragma unroll
-    for (int c = 0; c < 16; ++c)
-      s = __builtin_amdgcn_mfma_f32_16x16x4f32(shifted ? av2[c] : av[c], pb[0][c], s, 0, 0, 0);
+      for (int c = 0; c < 16; ++c)
+        s = __builtin_amdgcn_mfma_f32_16x16x4f32(shifted ? av2[c] : av[c], pb[0][c], s, 0, 0, 0);
+    }
     put_band(ring0, t0, s);
   }
 
@@ -864,10 +924,22 @@ __global__ __launch_bounds__(256, SPLIT == 2 ? 3 : 2) void relpos_attn_fwd16_ker
       const float(&pf)[16] = pb[(tt + 1) % NB];
       const bool shifted = LEGACY && t + 1 > g;  // legacy band block t+1 at/above table position T
       f32x4 a = {0.f, 0.f, 0.f, 0.f}, s = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (XS) {
+        Frag6 kf6, pf6;
+        split_frag(kf, kf6);
+        split_frag(pf, pf6);
+        if (LEGACY && t == g) {  // block t+1 = g+1: the first shifted band block
+          ld16(qv + ((long)z * T + min(i0 + 1 + li, T - 1)) * RP_DK, av2);
+          split_frag(av2, xv);
+        }
+        a = mfma6(xu, kf6, a);
+        s = mfma6(xv, pf6, s);
+      } else {
 #pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        a = __builtin_amdgcn_mfma_f32_16x16x4f32(au[c], kf[c], a, 0, 0, 0);
-        s = __builtin_amdgcn_mfma_f32_16x16x4f32(shifted ? av2[c] : av[c], pf[c], s, 0, 0, 0);
+        for (int c = 0; c < 16; ++c) {
+          a = __builtin_amdgcn_mfma_f32_16x16x4f32(au[c], kf[c], a, 0, 0, 0);
+          s = __builtin_amdgcn_mfma_f32_16x16x4f32(shifted ? av2[c] : av[c], pf[c], s, 0, 0, 0);
+        }
       }
       ld16(k_row(t + DEPTH), kb[(tt + DEPTH) % NB]);  // clamped rows: always safe to fetch
       ld16(p_row(t + 1 + DEPTH), pb[(tt + 1 + DEPTH) % NB]);
@@ -1220,6 +1292,41 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
   dim3 grid((unsigned)((T + (split ? 2 : 4) * RW_ROWS - 1) / ((split ? 2 : 4) * RW_ROWS)), (unsigned)(nb * H));
   hipStream_t st = (hipStream_t)stream;
   const bool p2 = sqrt_dk > 0.f && (__builtin_bit_cast(uint32_t, sqrt_dk) & 0x7fffffu) == 0;
+  static int xs_env = -1;  // ESP_ATTN_XS=0: the f32-MFMA products (A/B measurements)
+  if (xs_env < 0) xs_env = getenv("ESP_ATTN_XS") ? atoi(getenv("ESP_ATTN_XS")) : ESP_ATTN_XS_DEFAULT;
+  if (xs_env && !split) {
+#define ESP_RX3(N, P2_, L_)                                                                                            \
+  hipLaunchKernelGGL((relpos_attn_fwd16_kernel<N, P2_, L_, 1, true>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p,    \
+                     ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid)
+#define ESP_RX(N)                     \
+  do {                                \
+    if (relpos == 2) {                \
+      if (p2) ESP_RX3(N, true, true); \
+      else ESP_RX3(N, false, true);   \
+    } else {                          \
+      if (p2) ESP_RX3(N, true, false); \
+      else ESP_RX3(N, false, false);  \
+    }                                 \
+  } while (0)
+    if (nt <= 8) ESP_RX(8);
+    else if (nt <= 16) ESP_RX(16);
+    else if (relpos == 2) {
+      // legacy: the row-shift re-split leaves no registers for 24+ score tiles per wave; two waves
+      // share a row group's keys (SPLIT 2, half the score registers each)
+      grid.x = (unsigned)((T + 2 * RW_ROWS - 1) / (2 * RW_ROWS));
+      if (p2) hipLaunchKernelGGL((relpos_attn_fwd16_kernel<16, true, true, 2, true>), grid, dim3(256), 0, st, qu, qv,
+                                 kmat, ldk, p, ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds,
+                                 esp::rng_key_ptr(), tvalid);
+      else hipLaunchKernelGGL((relpos_attn_fwd16_kernel<16, false, true, 2, true>), grid, dim3(256), 0, st, qu, qv,
+                              kmat, ldk, p, ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds,
+                              esp::rng_key_ptr(), tvalid);
+    } else if (nt <= 24) ESP_RX(24);
+    else ESP_RX(32);
+#undef ESP_RX
+#undef ESP_RX3
+    ESP_CHECK_LAUNCH("esp_relpos_attn_probs");
+    return 0;
+  }
   if (split) {
 #define ESP_RS3(N, P2_, L_)                                                                                            \
   hipLaunchKernelGGL((relpos_attn_fwd16_kernel<N, P2_, L_, 2>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p, ldp_row, \
