@@ -134,7 +134,8 @@ class PositionwiseFeedForward(nn.Module):
         # dh/dv = keep * scale * act'(v): the backward epilogue is then a single multiply
         dact = empty(M, H, like=x2d)
         # h feeds only w_2 (forward and weight gradient): written as planes by the w_1 epilogue
-        h = K.Planes(M, H, x2d.device) if K.planes_mode() == 3 and H % 8 == 0 else empty(M, H, like=x2d)
+        npl = K.planes_mode() if H % 8 == 0 else 0
+        h = K.Planes(M, H, x2d.device, npl) if npl else empty(M, H, like=x2d)
         p_in = self.p if training else 0.0
         s1, s2 = seeds.next(), seeds.next()
         self.w_1.fwd(x2d, h, act=self.act | K.ACT_AUX_DERIV, aux=dact, drop_p=p_in, seed=s1)
@@ -242,8 +243,8 @@ class RelPositionMultiHeadedAttention(nn.Module):
         pv = pdrop if pdrop is not None else attn
         # ctx feeds only linear_out (forward and weight gradient): planes from the P.V epilogue (the
         # score-gradient epilogue, ESP_ATTN_DSCORES, reads it in fp32)
-        ctx_ = (K.Planes(M, D, x2d.device) if K.planes_mode() == 3 and D % 8 == 0 and not K.ATTN_DSCORES
-                else empty(M, D, like=x2d))
+        npl = K.planes_mode() if D % 8 == 0 and not K.ATTN_DSCORES else 0
+        ctx_ = K.Planes(M, D, x2d.device, npl) if npl else empty(M, D, like=x2d)
         K.gemm(T, dk, T, pv, qkv, ctx_, mode_a=K.KC, lda=Tp, mode_b=K.RC, ldb=3 * D, ldc=D, b_off=2 * D,
                batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * 3 * D), sc=(dk, T * D))
         out = empty(M, D, like=x2d)
@@ -409,7 +410,8 @@ class MultiHeadedAttention(nn.Module):
         pdrop = empty(Z * Tq * Tkp, like=xq) if pa > 0 else None
         K.attn_softmax_fwd(sc, None, 0, 0, math.sqrt(dk), klen, B, causal, sc, pdrop, pa, sa, Z, Tq, Tk, lds=Tkp)
         pv = pdrop if pdrop is not None else sc
-        ctx_ = K.Planes(B * Tq, D, xq.device) if K.planes_mode() == 3 and D % 8 == 0 else empty(B * Tq, D, like=xq)
+        npl = K.planes_mode() if D % 8 == 0 else 0
+        ctx_ = K.Planes(B * Tq, D, xq.device, npl) if npl else empty(B * Tq, D, like=xq)
         K.gemm(Tq, dk, Tk, pv, kvb, ctx_, mode_a=K.KC, lda=Tkp, mode_b=K.RC, ldb=kvld, ldc=D, b_off=voff,
                batch=Z, nb2=B, sa=(B * Tq * Tkp, Tq * Tkp), sb=(dk, Tk * kvld), sc=(dk, Tq * D))
         out = empty(B * Tq, D, like=xq)
@@ -528,7 +530,8 @@ class ConvolutionModule(nn.Module):
         dg = ds  # reuse
         K.dwconv1d(dy, dw.weight, None, dg, c.B, c.T, D, self.kernel_size, flip=True, tvalid=c.tvalid)
         # du feeds only pointwise_conv1's weight- and input-gradient GEMMs
-        du = K.Planes(M, 2 * D, dout.device) if K.planes_mode() == 3 and D % 4 == 0 else empty(M, 2 * D, like=dout)
+        npl = K.planes_mode() if D % 4 == 0 else 0
+        du = K.Planes(M, 2 * D, dout.device, npl) if npl else empty(M, 2 * D, like=dout)
         K.glu_bwd(c.u, dg, du)
         w1 = self.pointwise_conv1.weight
         K.linear_bwd_weight(du, c.x, w1.grad.view(2 * D, D), self.pointwise_conv1.bias.grad)

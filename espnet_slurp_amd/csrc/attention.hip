@@ -775,7 +775,7 @@ __global__ __launch_bounds__(256) void relpos_attn_fwd_kernel(
 // blocks m <= g lie wholly below T (A rows q_v[i]), blocks m >= g+1 wholly at or above T (A rows
 // q_v[i+1], the shifted twin), so legacy selects the A operand per block and shares the ring.
 // LDS: ring rows of RW_PITCH floats (row groups r and r+4 of a 32-lane half 16 banks apart).
-// XS (the fp32 build's default, ESP_ATTN_XS=0: f32 MFMA): the ac and band products as bf16x6 split
+// XS (ESP_ATTN_XS=1): the ac and band products as bf16x6 split
 // products on v_mfma_f32_16x16x32_bf16 (the GEMM family's fp32 arithmetic, gemm_kernels.h): each
 // operand value v = hi + mid + lo exactly (three bf16), six products per pair, smallest first.  A
 // lane's 16 values of a row (d = 16 q4 + [0,16)) are the two k-halves of the 16x16x32 operand
@@ -809,12 +809,10 @@ __device__ __forceinline__ f32x4 mfma6(const Frag6& a, const Frag6& b, f32x4 c) 
   return c;
 }
 
+// Off by default: measured at C2 B=128 (tools/attn_kernels_bench.py, one box) 441 vs 414 us latest,
+// 519 vs 420 legacy with one tile of prefetch -- the kernel is not bound by its MFMAs
 #ifndef ESP_ATTN_XS_DEFAULT
-#if defined(ESP_F32_SPLIT) && ESP_F32_SPLIT == 0
-#define ESP_ATTN_XS_DEFAULT 0  // the f32-MFMA build (A/B runs)
-#else
-#define ESP_ATTN_XS_DEFAULT 1
-#endif
+#define ESP_ATTN_XS_DEFAULT 0
 #endif
 constexpr int RW_ROWS = 16, RW_PITCH = 37;
 constexpr int RW_SPITCH = 68;  // store-transpose rows: the two row groups of a ds_write_b32 half 16 banks apart
@@ -885,8 +883,8 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
     for (int r = 0; r < 4; ++r) rg[(4 * q4 + r) * RW_PITCH + ((16 * m + li) & 31)] = s[r];
   };
   // fragments DEPTH tiles ahead: K(t) in kb[t % NB], band-block p rows P(m) in pb[m % NB]
-  // (split: 3 waves per SIMD hide a tile less; XS: the split planes of the current tile take the registers)
-  constexpr int DEPTH = SPLIT == 2 || XS ? 1 : 2, NB = DEPTH + 1;
+  // (split: 3 waves per SIMD hide a tile less)
+  constexpr int DEPTH = SPLIT == 2 ? 1 : 2, NB = DEPTH + 1;
   float kb[NB][16], pb[NB][16];  // indexed by the tile / block offset from t0
 #pragma unroll
   for (int d = 0; d < DEPTH; ++d) ld16(k_row(t0 + d), kb[d]);
@@ -1292,7 +1290,7 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
   dim3 grid((unsigned)((T + (split ? 2 : 4) * RW_ROWS - 1) / ((split ? 2 : 4) * RW_ROWS)), (unsigned)(nb * H));
   hipStream_t st = (hipStream_t)stream;
   const bool p2 = sqrt_dk > 0.f && (__builtin_bit_cast(uint32_t, sqrt_dk) & 0x7fffffu) == 0;
-  static int xs_env = -1;  // ESP_ATTN_XS=0: the f32-MFMA products (A/B measurements)
+  static int xs_env = -1;  // ESP_ATTN_XS=1: the split products (A/B measurements)
   if (xs_env < 0) xs_env = getenv("ESP_ATTN_XS") ? atoi(getenv("ESP_ATTN_XS")) : ESP_ATTN_XS_DEFAULT;
   if (xs_env && !split) {
 #define ESP_RX3(N, P2_, L_)                                                                                            \

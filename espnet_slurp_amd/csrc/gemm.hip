@@ -425,6 +425,25 @@ ESP_API int esp_gemm_bf16(int mode_a, int mode_b, int M, int N, int K, int batch
                   seed, bwd_act, pre, rowsum, nullptr, nullptr, work, work_bytes, stream, 2);
 }
 
+ESP_API int esp_gemm_bf16_pl(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2, const void* A, long lda,
+                             long sa1, long sa2, const void* B, long ldb, long sb1, long sb2, void* C, long ldc,
+                             long sc1, long sc2, const float* bias, float alpha, float beta, int act, float* aux,
+                             float drop_p, unsigned long long seed, int bwd_act, const float* pre, int c_nplanes,
+                             long c_pstride, float* work, long work_bytes, void* stream) {
+  ESP_ARG_CHECK((mode_a == KC || mode_a == RC) && (mode_b == KC || mode_b == RC),
+                "esp_gemm_bf16_pl: modes must be 0 (KC) or 1 (RC)");
+  ESP_ARG_CHECK(K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 && sa1 % 8 == 0 && sa2 % 8 == 0 && sb1 % 8 == 0 &&
+                    sb2 % 8 == 0 && aligned16(A) && aligned16(B),
+                "esp_gemm_bf16_pl: K, ld and strides must be multiples of 8 bf16 and A, B 16-B aligned");
+  ESP_ARG_CHECK((mode_a == KC || M % 8 == 0) && (mode_b == KC || N % 8 == 0),
+                "esp_gemm_bf16_pl: an RC operand's row count must be a multiple of 8 (M=%d N=%d)", M, N);
+  ESP_ARG_CHECK(c_nplanes == 1, "esp_gemm_bf16_pl: c_nplanes must be 1 (bf16 operands: a bf16 result)");
+  return gemm_run(mode_a, mode_b, M, N, K / 2, batch, nb2, (const float*)A, lda / 2, sa1 / 2, sa2 / 2,
+                  (const float*)B, ldb / 2, sb1 / 2, sb2 / 2, (float*)C, ldc, sc1, sc2, bias, alpha, beta, nullptr, act,
+                  aux, drop_p, seed, bwd_act, pre, nullptr, nullptr, nullptr, work, work_bytes, stream, 2, nullptr,
+                  nullptr, 0, 0, 0, 0, nullptr, 0, 0, 0, 0, c_nplanes, c_pstride);
+}
+
 // Rel-pos attention score gradient in one GEMM: dP = dctx V^T per (head, utterance) with the
 // softmax + attention-dropout + rel_shift adjoints in the epilogue (EPI_SMB):
 //   dS[i][j] = P[i][j] * (drop'(dP[i][j]) - dot[i]) / sqrt(d_k),  dot[i] = dctx_i . ctx_i

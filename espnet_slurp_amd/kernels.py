@@ -437,7 +437,7 @@ def _gemm_planes(M, N, K, A, B, C, mode_a, lda, mode_b, ldb, ldc, a_off, b_off, 
             assert off == 0 and batch == 1, "a Planes operand is a whole (unbatched) matrix"
     cp = C if isinstance(C, Planes) else None
     if cp is not None:
-        assert _COMPUTE[0] != GEMM_BF16 and cp.n == 3 and R is None and rowsum is None
+        assert cp.n == (1 if _COMPUTE[0] == GEMM_BF16 else 3) and R is None and rowsum is None, cp.n
         if not isinstance(A, Planes) and not isinstance(B, Planes) and not b_weight and not _is_param(
                 B.data_ptr() + b_off * 4, 4):
             # fp32 operands, planes output (the attention context): esp_gemm_f32_pl without operand planes
@@ -454,7 +454,7 @@ def _gemm_planes(M, N, K, A, B, C, mode_a, lda, mode_b, ldb, ldc, a_off, b_off, 
                          _GEMM_WS_BYTES, _st())
             if _PROF is not None:
                 ev1.record()
-                extra = 4.0 * M * N * batch * (aux is not None) + 2.0 * M * N * batch  # 6-B planes out, not 4-B
+                extra = 4.0 * M * N * batch * (aux is not None) + (2.0 if cp.n == 3 else -2.0) * M * N * batch  # 6-/2-B out
                 _PROF.append((2.0 * M * N * K * batch, ev0, ev1, (mode_a, mode_b, M, N, K, batch), extra))
             return
     assert batch == 1, "planes operands: unbatched GEMMs"
@@ -470,15 +470,23 @@ def _gemm_planes(M, N, K, A, B, C, mode_a, lda, mode_b, ldb, ldc, a_off, b_off, 
             ev0 = torch.cuda.Event(enable_timing=True)
             ev1 = torch.cuda.Event(enable_timing=True)
             ev0.record()
-        _native.call("esp_gemm_bf16", mode_a, mode_b, M, N, K, 1, 1, _p(A16), la, 0, 0, _p(B16), lb, 0, 0,
-                     _p(C, c_off), ldc, 0, 0, _p(bias), float(alpha), float(beta), _p(R, r_off or 0), act,
-                     _p(aux, c_off) if aux is not None else None, float(drop_p), seed & 0xFFFFFFFFFFFFFFFF,
-                     int(bwd_act), _p(pre, c_off) if pre is not None else None, _p(rowsum), _p(ws), _GEMM_WS_BYTES,
-                     _st())
+        if cp is not None:  # the bf16 result plane (the reduced-precision GEMM-only activations)
+            _native.call("esp_gemm_bf16_pl", mode_a, mode_b, M, N, K, 1, 1, _p(A16), la, 0, 0, _p(B16), lb, 0, 0,
+                         _p(cp.buf, c_off), ldc, 0, 0, _p(bias), float(alpha), float(beta), act,
+                         _p(aux, c_off) if aux is not None else None, float(drop_p), seed & 0xFFFFFFFFFFFFFFFF,
+                         int(bwd_act), _p(pre, c_off) if pre is not None else None, cp.n, cp.ps, _p(ws),
+                         _GEMM_WS_BYTES, _st())
+        else:
+            _native.call("esp_gemm_bf16", mode_a, mode_b, M, N, K, 1, 1, _p(A16), la, 0, 0, _p(B16), lb, 0, 0,
+                         _p(C, c_off), ldc, 0, 0, _p(bias), float(alpha), float(beta), _p(R, r_off or 0), act,
+                         _p(aux, c_off) if aux is not None else None, float(drop_p), seed & 0xFFFFFFFFFFFFFFFF,
+                         int(bwd_act), _p(pre, c_off) if pre is not None else None, _p(rowsum), _p(ws),
+                         _GEMM_WS_BYTES, _st())
         _guard_post("esp_gemm_bf16", ws, _GEMM_WS_BYTES)
         if _PROF is not None:
             ev1.record()
             extra = 4.0 * M * N * ((R is not None) + (aux is not None) + (pre is not None))
+            extra -= 2.0 * M * N if cp is not None else 0.0  # a 2-B result, not 4-B
             _PROF.append((2.0 * M * N * K, ev0, ev1, (mode_a, mode_b, M, N, K, 1, "bf16"), extra))
         return
 
@@ -626,10 +634,12 @@ def scale_dropout(x, y, alpha=1.0, drop_p=0.0, seed=0, r=None, beta=1.0):
 
 def grad_planes_like(x2d):
     """A backward gradient that only GEMMs read (a branch's weight- and input-gradient GEMMs), as Planes in
-    the fp32 mode (None otherwise: the caller keeps fp32)."""
+    the fp32 mode (n = 3) or their bf16 plane in the reduced-precision mode (n = 1: the bf16 value the GEMMs
+    would round it to), None otherwise (the caller keeps fp32)."""
     M, D = x2d.shape
-    if planes_mode() == 3 and D % 8 == 0 and x2d.is_contiguous():
-        return Planes(M, D, x2d.device)
+    n = planes_mode()
+    if n and D % 8 == 0 and x2d.is_contiguous():
+        return Planes(M, D, x2d.device, n)
     return None
 
 

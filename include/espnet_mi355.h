@@ -123,6 +123,14 @@ int esp_gemm_bf16(int mode_a, int mode_b, int M, int N, int K, int batch, int nb
                   long sc1, long sc2, const float* bias, float alpha, float beta, const float* R, int act,
                   float* aux, float drop_p, unsigned long long seed, int bwd_act, const float* pre, float* rowsum,
                   float* work, long work_bytes, void* stream);
+/* esp_gemm_bf16 with C written as its bf16 plane (c_nplanes 1: hi = bf16(C), the reduced-precision
+ * path's GEMM-only activations and gradients) under the rules of esp_gemm_f32_pl's c_nplanes: the
+ * plain, FFN w_1 and ACT_MUL epilogues, N % 4 == 0, no residual / row sums, never split-K. */
+int esp_gemm_bf16_pl(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2, const void* A, long lda,
+                     long sa1, long sa2, const void* B, long ldb, long sb1, long sb2, void* C, long ldc,
+                     long sc1, long sc2, const float* bias, float alpha, float beta, int act, float* aux,
+                     float drop_p, unsigned long long seed, int bwd_act, const float* pre, int c_nplanes,
+                     long c_pstride, float* work, long work_bytes, void* stream);
 /* y = bf16(x) (round to nearest even) for a rows x cols fp32 matrix (row pitch ldx); transpose:
  * y[c * ldy + r] (a cols x rows bf16 matrix), else y[r * ldy + c]. */
 int esp_f32_to_bf16(const float* x, void* y, long rows, int cols, long ldx, long ldy, int transpose,
