@@ -221,8 +221,12 @@ class param_cast_scope:
 # Trainer's step; keyed like _W16, holding the fp32 source), else per GEMM.  ESP_BPLANES=0: off
 # (A/B measurements).
 _BPLANES = os.environ.get("ESP_BPLANES", "1") == "1"
-# producers of GEMM-only activations write them as Planes (ESP_XPLANES=0: fp32, A/B measurements)
-_XPLANES = os.environ.get("ESP_XPLANES", "1") == "1"
+# producers of GEMM-only activations write them as Planes: by default in the bf16 mode only (n = 1, the
+# bf16 value its GEMMs round to: 805 vs 760 utt/s at C5 B=64); in the fp32 mode the consumers then
+# need both operands as planes (PREC 5, 64-wide tiles), measured slower than splitting A in registers
+# beside B's planes (PREC 3): 1222 vs 1333 utt/s at C2 B=128 (profiles/r04a_*).  ESP_XPLANES=1: both
+# modes, 0: neither (A/B measurements)
+_XPLANES = os.environ.get("ESP_XPLANES", "bf16")
 _F32_PRODUCTS = [None]  # esp_f32_gemm_products() of the loaded build (set at first use)
 _WP = [None]
 
@@ -273,13 +277,13 @@ class Planes:
 def planes_mode() -> int:
     """Planes a producer writes for a GEMM-only tensor in the current compute mode: 3 (fp32 split
     products), 1 (bf16 GEMM operands), 0 (write fp32: ESP_XPLANES=0 or an f32-MFMA build)."""
-    if not _XPLANES:
+    if not _XPLANES or _XPLANES == "0":
         return 0
     if _F32_PRODUCTS[0] is None:
         _F32_PRODUCTS[0] = int(_native.load().esp_f32_gemm_products())
     if _COMPUTE[0] == GEMM_BF16:
         return 1 if _AMP_BF16_OPERANDS else 0
-    return 3 if _F32_PRODUCTS[0] == 6 else 0
+    return 3 if _F32_PRODUCTS[0] == 6 and _XPLANES in ("1", True) else 0
 
 
 def planes(X, off: int, rows: int, cols: int, ld: int):
