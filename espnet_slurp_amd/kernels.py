@@ -440,10 +440,26 @@ def _gemm_planes(M, N, K, A, B, C, mode_a, lda, mode_b, ldb, ldc, a_off, b_off, 
         if isinstance(X, Planes):
             assert off == 0 and batch == 1, "a Planes operand is a whole (unbatched) matrix"
     cp = C if isinstance(C, Planes) else None
+    amp = _COMPUTE[0] == GEMM_BF16
+    if amp and not (K % 8 == 0 and (mode_a == KC or M % 8 == 0) and (mode_b == KC or N % 8 == 0)):
+        # shapes the bf16-operand kernel does not take (e.g. K = an odd token count): the fp32 operands of
+        # the planes (the bf16 values themselves) through the fp32-operand launch, which rounds them to the
+        # same bf16 in staging
+        if isinstance(A, Planes):
+            A, lda = A.float(), A.cols
+        if isinstance(B, Planes):
+            B, ldb = B.float(), B.cols
+        if cp is None:
+            return gemm(M, N, K, A, B, C, mode_a=mode_a, lda=lda, mode_b=mode_b, ldb=ldb, ldc=ldc, a_off=a_off,
+                        b_off=b_off, c_off=c_off, batch=batch, nb2=nb2, sa=sa, sb=sb, sc=sc, bias=bias, alpha=alpha,
+                        beta=beta, R=R, r_off=r_off, act=act, aux=aux, drop_p=drop_p, seed=seed, bwd_act=bwd_act,
+                        pre=pre, rowsum=rowsum)
+        b_weight = False  # (the fp32-operand planes-output launch below)
     if cp is not None:
-        assert cp.n == (1 if _COMPUTE[0] == GEMM_BF16 else 3) and R is None and rowsum is None, cp.n
-        if not isinstance(A, Planes) and not isinstance(B, Planes) and not b_weight and not _is_param(
-                B.data_ptr() + b_off * 4, 4):
+        assert cp.n == (1 if amp else 3) and R is None and rowsum is None, cp.n
+        if not isinstance(A, Planes) and not isinstance(B, Planes) and (
+                amp and not (K % 8 == 0 and (mode_a == KC or M % 8 == 0) and (mode_b == KC or N % 8 == 0))
+                or not b_weight and not _is_param(B.data_ptr() + b_off * 4, 4)):
             # fp32 operands, planes output (the attention context): esp_gemm_f32_pl without operand planes
             ws = _ws(_GEMM_WS, "esp_gemm_f32", _GEMM_WS_BYTES, cp.device)
             if _PROF is not None:
@@ -462,7 +478,7 @@ def _gemm_planes(M, N, K, A, B, C, mode_a, lda, mode_b, ldb, ldc, a_off, b_off, 
                 _PROF.append((2.0 * M * N * K * batch, ev0, ev1, (mode_a, mode_b, M, N, K, batch), extra))
             return
     assert batch == 1, "planes operands: unbatched GEMMs"
-    if _COMPUTE[0] == GEMM_BF16:
+    if amp:
         def b16(X, off, rows, cols, ld, role=""):
             if isinstance(X, Planes):
                 return X.buf, X.ld
