@@ -88,6 +88,7 @@ class Trainer:
         # graph DP replays: this replica's batch weight and the all-reduced sum (see _dp_replay)
         self._wloc = torch.ones(1, dtype=torch.float32, device=model.flat.flat.device)
         self._wsum = torch.ones(1, dtype=torch.float32, device=model.flat.flat.device)
+        self._bufs_synced = False  # graph DP: the one broadcast of rank 0's buffers before the first step
         self.reducer = (FlatGradReducer(model, model.flat, bucket_mb, hooks=not self.cuda_graph)
                         if self.distributed else None)
         self.iiter = 0          # micro-batches (trainer.py:502 iiter)
@@ -188,16 +189,20 @@ class Trainer:
         sig = (tuple(speech.shape), prep.T, prep.Umax, prep.L, prep.get("n_samples", 0), last,
                tuple((k, tuple(v.shape)) for k, v in sorted(prep.host.items())))
         e = self._graphs.pop(sig, None)
-        if self.distributed and e is None:
-            # DDP broadcast_buffers (X7), outside the graph (a collective).  A replay broadcasts at the
-            # END of its step instead (_dp_replay), off the critical path: training-mode outputs never
-            # read the running statistics, nothing writes them between two steps, so every forward
-            # still starts from rank 0's buffers exactly as with DDP's broadcast before it.
+        if self.distributed and not self._bufs_synced:
+            # DDP broadcast_buffers (X7), outside the graph (a collective): once before the first step,
+            # then at the END of every step (_dp_replay / _capture_dp), off the critical path --
+            # training-mode outputs never read the running statistics and nothing writes them between
+            # two steps, so every forward still starts from rank 0's buffers as with DDP's broadcast
+            # before it.  Capture and replay steps issue the same collectives in the same order (a
+            # rank may capture a new batch signature while another replays).
             self.reducer.broadcast_buffers(model)
+            self._bufs_synced = True
         if last:
             self.n_updates += 1
         if e is None:  # the capture call's eager warm-up IS this iteration's step
-            e = self._capture_dp(speech, prep, last) if self.distributed else self._capture(speech, prep, last)
+            e = (self._capture_dp(speech, prep, last, float(prep.host["weight"].view(-1)[0])) if self.distributed
+                 else self._capture(speech, prep, last))
         else:
             e.speech.copy_(speech, non_blocking=True)
             prep.copy_into(e.prep)
@@ -230,20 +235,12 @@ class Trainer:
 
     # ---------------------------------------------------------------- DDP + HIP graph
     # DDP semantics (trainer.py:594-608 + DDP's bucketed average, overlapped with backward):
-    #   replay forward graph -> stats all-reduce (recursive_average) and d loss_r = w_r / sum w
-    #   (/ accum_grad) on device -> replay the backward in segments; after each segment the
-    #   gradient buckets it completed are SUM-all-reduced asynchronously while the next segment
-    #   runs -> wait -> clip + Adam.  Pre-scaling by d loss makes the SUM the weighted average,
-    #   and accumulation over micro-batches is plain gradient accumulation (no_sync).
-    def _dp_scale(self, stats, weight):
-        avg, wsum = fused_stats_allreduce({k: v for k, v in stats.items() if k != "grad_norm"}, weight)
-        for k, v in avg.items():
-            stats[k].copy_(v)
-        self._last_weight = wsum
-        torch.div(weight.to(torch.float32).view(1), wsum, out=self._scale)
-        if self.options.accum_grad > 1:
-            self._scale.mul_(1.0 / self.options.accum_grad)
-
+    #   sum w all-reduce (beside the forward replay) -> d loss_r = w_r / sum w (/ accum_grad) on device
+    #   -> replay the backward in segments; after each segment the gradient buckets it completed are
+    #   SUM-all-reduced asynchronously while the next segment runs -> stats all-reduce
+    #   (recursive_average) and buffer broadcast launched -> wait -> clip + Adam.  Pre-scaling by
+    #   d loss makes the SUM the weighted average, and accumulation over micro-batches is plain
+    #   gradient accumulation (no_sync).
     def _dp_replay(self, e, last: bool, w_host: float):
         # The critical path is forward graph -> backward segments (+ their bucket all-reduces):
         #  * sum w: the batch weight is known on the host (espnet_model.prepare: weight = B, the
@@ -252,21 +249,16 @@ class Trainer:
         #  * the reported stats' recursive_average and DDP's buffer broadcast are launched after the
         #    backward is queued and waited for at the end of the step (stream-ordered: the next step's
         #    kernels run after them).
-        self._wloc.fill_(w_host)
-        self._wsum.copy_(self._wloc)
-        hw = dist.all_reduce(self._wsum, async_op=True)
+        hw = self._dp_wsum(w_host, async_op=True)
         e.fwd.replay()
         hw.wait()
-        torch.div(self._wloc, self._wsum, out=self._scale)
-        if self.options.accum_grad > 1:
-            self._scale.mul_(1.0 / self.options.accum_grad)
+        self._dp_set_scale()
         handles = []
         for g, buckets in e.segs:
             g.replay()
             if last and buckets:
                 handles += self.reducer.launch_sum(buckets)
-        keys = [k for k in e.stats if k != "grad_norm"]
-        vec = torch.cat([e.stats[k].view(-1)[:1].float() * self._wloc for k in keys] + [self._wloc])
+        keys, vec = self._stats_vec(e.stats)
         tail = [dist.all_reduce(vec, async_op=True)] + self.reducer.broadcast_buffers(self.model, async_op=True)
         for h in handles:
             h.wait()
@@ -274,8 +266,27 @@ class Trainer:
             self._opt_tail()
         for h in tail:
             h.wait()
+        self._stats_avg(e.stats, keys, vec)
+
+    def _dp_wsum(self, w_host: float, async_op: bool):
+        """sum_r w_r into self._wsum (this replica's w_r in self._wloc)."""
+        self._wloc.fill_(w_host)
+        self._wsum.copy_(self._wloc)
+        return dist.all_reduce(self._wsum, async_op=async_op)
+
+    def _dp_set_scale(self):
+        torch.div(self._wloc, self._wsum, out=self._scale)
+        if self.options.accum_grad > 1:
+            self._scale.mul_(1.0 / self.options.accum_grad)
+
+    def _stats_vec(self, stats):
+        """recursive_average's all-reduce operand: the stats weighted by w_r, then w_r."""
+        keys = [k for k in stats if k != "grad_norm"]
+        return keys, torch.cat([stats[k].view(-1)[:1].float() * self._wloc for k in keys] + [self._wloc])
+
+    def _stats_avg(self, stats, keys, vec):
         for i, k in enumerate(keys):
-            e.stats[k].view(-1)[:1].copy_(vec[i:i + 1] / vec[-1:])
+            stats[k].view(-1)[:1].copy_(vec[i:i + 1] / vec[-1:])
         self._last_weight = vec[-1:]
 
     def _dp_body(self, speech, prep):
@@ -285,7 +296,7 @@ class Trainer:
         stats["grad_norm"] = self._clip[0:1]
         return stats, weight, ctx
 
-    def _capture_dp(self, speech, prep, last: bool):
+    def _capture_dp(self, speech, prep, last: bool, w_host: float):
         dev = self.model.flat.flat.device
         if self._key is None:
             self._key = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).to(dev)
@@ -298,13 +309,20 @@ class Trainer:
             side = torch.cuda.Stream(device=dev)
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side):  # warm-up = this iteration's step (allocates workspaces)
+                # the collectives of a replay (_dp_replay), in its order: sum w, the gradient buckets,
+                # the stats, the buffer broadcast
+                self._dp_wsum(w_host, async_op=False)
                 stats, w, ctx = self._dp_body(e.speech, e.prep)
-                self._dp_scale(stats, w)
+                self._dp_set_scale()
                 model.backward_explicit(ctx, self._scale)
                 del ctx
                 if last:
                     self.reducer.allreduce_sum()
                     self._opt_tail()
+                keys, vec = self._stats_vec(stats)
+                dist.all_reduce(vec)
+                self._stats_avg(stats, keys, vec)
+                self.reducer.broadcast_buffers(model)
                 warm = {k: v.clone() for k, v in stats.items()}
             torch.cuda.current_stream(dev).wait_stream(side)
             torch.cuda.synchronize(dev)

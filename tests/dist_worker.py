@@ -93,6 +93,8 @@ def main_c2(out, mode, rank, world):
 
 
 def main():
+    import faulthandler
+    faulthandler.dump_traceback_later(90, exit=True)  # a hung rank prints every thread's stack and exits
     out, mode, accum = sys.argv[1], sys.argv[2], int(sys.argv[3])
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo", rank=rank, world_size=world)
