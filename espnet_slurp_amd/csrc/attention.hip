@@ -815,7 +815,10 @@ __device__ __forceinline__ f32x4 mfma6(const Frag6& a, const Frag6& b, f32x4 c) 
 #define ESP_ATTN_XS_DEFAULT 0
 #endif
 constexpr int RW_ROWS = 16, RW_PITCH = 37;
-constexpr int RW_SPITCH = 68;  // store-transpose rows: the two row groups of a ds_write_b32 half 16 banks apart
+// store-transpose rows: 64 floats, so the float4 read-back (ds_read_b128 lane groups of 16 lanes over
+// two rows, bank (a/4) mod 64) is conflict-free, with the column XOR-ed by 16 in rows 4..7 and 12..15
+// so the two row groups of a ds_write_b32 half land 16 banks apart too (68: the reads conflicted 2-way)
+constexpr int RW_SPITCH = 64;
 // SPLIT = 2 (opt-in, ESP_ATTN_SPLIT=2): a row group's keys are shared by two waves of the block
 // (tiles [0, NTA) and [NTA, 2 NTA)), half the score registers each (3 waves per SIMD instead of
 // 2); the row max and sum are combined through LDS with one block barrier each.  Measured at C2
@@ -826,13 +829,18 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
     const float* __restrict__ qu, const float* __restrict__ qv, const float* __restrict__ kmat, long ldk,
     const float* __restrict__ pm, long ldpm, int nb, float sqrt_dk, const int* __restrict__ klen,
     float* __restrict__ attn, float* __restrict__ pdrop, uint32_t thr, float dscale, uint64_t seed, int T, long lds,
-    const uint64_t* __restrict__ key, const int* __restrict__ tvalid) {
+    const uint64_t* __restrict__ key, const int* __restrict__ tvalid, int nrb, int Z) {
   __shared__ float ring[4][RW_ROWS * RW_PITCH];
   __shared__ __attribute__((aligned(16))) float stage[4][RW_ROWS * RW_SPITCH];
   __shared__ float xch[2][4][RW_ROWS];  // SPLIT 2: per-wave row max / row sum partials
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int z = blockIdx.y;
-  const int i0 = (SPLIT == 1 ? blockIdx.x * 4 + wave : blockIdx.x * 2 + (wave >> 1)) * RW_ROWS;
+  // XCD-aware block order (1-D grid, blocks dealt round-robin over the 8 XCDs): the nrb row blocks of
+  // one (head, utterance) z run on one XCD, so z's k rows and the head's p table are fetched into that
+  // XCD's L2 once instead of once per XCD
+  const int xcd = blockIdx.x & 7, jb = blockIdx.x >> 3, zq = jb / nrb;
+  const int z = zq * 8 + xcd, bx = jb - zq * nrb;
+  if (z >= Z) return;  // the whole block (nothing has synchronised yet)
+  const int i0 = (SPLIT == 1 ? bx * 4 + wave : bx * 2 + (wave >> 1)) * RW_ROWS;
   const int t0 = SPLIT == 1 ? 0 : (wave & 1) * NTA;  // first key tile of this wave
   if (SPLIT == 1 && i0 >= T) return;  // the whole wave: nothing below synchronises the block
   seed = esp::keyed(seed, key);
@@ -1038,7 +1046,7 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
   const bool even_T = (T & 1) == 0;  // uniform
   // every dropout index of the launch (z*T + i)*T + j below 2^32 (uniform): 32-bit hash inputs,
   // the same masks (keep_pair32)
-  const bool idx32 = (uint64_t)gridDim.y * (uint64_t)T * (uint64_t)T <= 0xffffffffull;
+  const bool idx32 = (uint64_t)Z * (uint64_t)T * (uint64_t)T <= 0xffffffffull;
   auto store_rows = [&](auto drop_c) {
     constexpr bool DROP = decltype(drop_c)::value;
 #pragma unroll
@@ -1047,12 +1055,12 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) stg[(4 * q4 + r) * RW_SPITCH + 16 * tt + li] = sc[t4 + tt][r] * inv[r];
+        for (int r = 0; r < 4; ++r) stg[(4 * q4 + r) * RW_SPITCH + ((16 * tt + li) ^ (16 * (q4 & 1)))] = sc[t4 + tt][r] * inv[r];
       asm volatile("" ::: "memory");
       const bool jok = 16 * (t0 + t4) + sc4 < T;
 #pragma unroll
       for (int ps = 0; ps < 4; ++ps) {
-        const float4 v = *reinterpret_cast<const float4*>(stg + (4 * ps + sr) * RW_SPITCH + sc4);
+        const float4 v = *reinterpret_cast<const float4*>(stg + (4 * ps + sr) * RW_SPITCH + (sc4 ^ (16 * (ps & 1))));
         if (rok[ps] && jok) {
           float* ar = abase[ps] + 16 * (t0 + t4);
           *reinterpret_cast<float4*>(ar) = v;
@@ -1287,7 +1295,9 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
   static int split_env = -1;  // ESP_ATTN_SPLIT=1|2: one wave per row group / two (key halves)
   if (split_env < 0) split_env = getenv("ESP_ATTN_SPLIT") ? atoi(getenv("ESP_ATTN_SPLIT")) : 1;
   const bool split = split_env == 2 && nt > 8 && nt <= 32;
-  dim3 grid((unsigned)((T + (split ? 2 : 4) * RW_ROWS - 1) / ((split ? 2 : 4) * RW_ROWS)), (unsigned)(nb * H));
+  const int Zn = nb * H;
+  int nrb = (T + (split ? 2 : 4) * RW_ROWS - 1) / ((split ? 2 : 4) * RW_ROWS);  // row blocks per z
+  dim3 grid((unsigned)(8 * ((Zn + 7) / 8) * nrb));  // XCD-aware order (see the kernel)
   hipStream_t st = (hipStream_t)stream;
   const bool p2 = sqrt_dk > 0.f && (__builtin_bit_cast(uint32_t, sqrt_dk) & 0x7fffffu) == 0;
   static int xs_env = -1;  // ESP_ATTN_XS=1: the split products (A/B measurements)
@@ -1295,7 +1305,7 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
   if (xs_env && !split) {
 #define ESP_RX3(N, P2_, L_)                                                                                            \
   hipLaunchKernelGGL((relpos_attn_fwd16_kernel<N, P2_, L_, 1, true>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p,    \
-                     ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid)
+                     ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid, nrb, Zn)
 #define ESP_RX(N)                     \
   do {                                \
     if (relpos == 2) {                \
@@ -1311,13 +1321,14 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
     else if (relpos == 2) {
       // legacy: the row-shift re-split leaves no registers for 24+ score tiles per wave; two waves
       // share a row group's keys (SPLIT 2, half the score registers each)
-      grid.x = (unsigned)((T + 2 * RW_ROWS - 1) / (2 * RW_ROWS));
+      nrb = (T + 2 * RW_ROWS - 1) / (2 * RW_ROWS);
+      grid.x = (unsigned)(8 * ((Zn + 7) / 8) * nrb);
       if (p2) hipLaunchKernelGGL((relpos_attn_fwd16_kernel<16, true, true, 2, true>), grid, dim3(256), 0, st, qu, qv,
                                  kmat, ldk, p, ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds,
-                                 esp::rng_key_ptr(), tvalid);
+                                 esp::rng_key_ptr(), tvalid, nrb, Zn);
       else hipLaunchKernelGGL((relpos_attn_fwd16_kernel<16, false, true, 2, true>), grid, dim3(256), 0, st, qu, qv,
                               kmat, ldk, p, ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds,
-                              esp::rng_key_ptr(), tvalid);
+                              esp::rng_key_ptr(), tvalid, nrb, Zn);
     } else if (nt <= 24) ESP_RX(24);
     else ESP_RX(32);
 #undef ESP_RX
@@ -1328,7 +1339,7 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
   if (split) {
 #define ESP_RS3(N, P2_, L_)                                                                                            \
   hipLaunchKernelGGL((relpos_attn_fwd16_kernel<N, P2_, L_, 2>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p, ldp_row, \
-                     nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid)
+                     nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid, nrb, Zn)
 #define ESP_RS(N)                     \
   do {                                \
     if (relpos == 2) {                \
@@ -1350,7 +1361,7 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
   }
 #define ESP_RW3(N, P2_, L_)                                                                                         \
   hipLaunchKernelGGL((relpos_attn_fwd16_kernel<N, P2_, L_>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p, ldp_row, \
-                     nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid)
+                     nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid, nrb, Zn)
 #define ESP_RW(N)                             \
   do {                                        \
     if (relpos == 2) {                        \
