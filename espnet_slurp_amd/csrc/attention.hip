@@ -775,35 +775,46 @@ __global__ __launch_bounds__(256) void relpos_attn_fwd_kernel(
 // blocks m <= g lie wholly below T (A rows q_v[i]), blocks m >= g+1 wholly at or above T (A rows
 // q_v[i+1], the shifted twin), so legacy selects the A operand per block and shares the ring.
 // LDS: ring rows of RW_PITCH floats (row groups r and r+4 of a 32-lane half 16 banks apart).
-// XS (ESP_ATTN_XS=1): the ac and band products as bf16x6 split
-// products on v_mfma_f32_16x16x32_bf16 (the GEMM family's fp32 arithmetic, gemm_kernels.h): each
-// operand value v = hi + mid + lo exactly (three bf16), six products per pair, smallest first.  A
-// lane's 16 values of a row (d = 16 q4 + [0,16)) are the two k-halves of the 16x16x32 operand
-// (MFMA m takes d = 16 q4 + 8 m + [0, 8)); the output layout is the 16x16x4 one, so the ring,
-// softmax and stores are shared with the f32 form.
+// XS = 6 (ESP_ATTN_XS=1): the ac and band products as bf16x6 split products on
+// v_mfma_f32_16x16x32_bf16 (the GEMM family's fp32 arithmetic, gemm_kernels.h): each operand value
+// v = hi + mid + lo exactly (three bf16), six products per pair, smallest first.  XS = 1 (the bf16
+// mode, esp_set_gemm_compute(1): every GEMM of the step on bf16 operands): hi.hi alone, i.e. torch
+// autocast's bf16 matmul of the RNE-rounded operands with fp32 accumulation.  A lane's 16 values of a
+// row (d = 16 q4 + [0,16)) are the two k-halves of the 16x16x32 operand (MFMA m takes
+// d = 16 q4 + 8 m + [0, 8)); the output layout is the 16x16x4 one, so the ring, softmax and stores
+// are shared with the f32 form (XS = 0).
 typedef __attribute__((ext_vector_type(8))) __bf16 attn_bf16x8;
 struct Frag6 {
-  attn_bf16x8 v[3][2];  // [hi, mid, lo][k-half]
+  attn_bf16x8 v[3][2];  // [hi, mid, lo][k-half] (XS = 1: hi only)
 };
+template <int NP>
 __device__ __forceinline__ void split_frag(const float (&f)[16], Frag6& o) {
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
     uint32_t h[4], md[4], l[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) esp::split3_pair(f[8 * m + 2 * j], f[8 * m + 2 * j + 1], h[j], md[j], l[j]);
+    for (int j = 0; j < 4; ++j) {
+      if constexpr (NP == 6) esp::split3_pair(f[8 * m + 2 * j], f[8 * m + 2 * j + 1], h[j], md[j], l[j]);
+      else h[j] = esp::bf16_pair(f[8 * m + 2 * j], f[8 * m + 2 * j + 1]);
+    }
     o.v[0][m] = __builtin_bit_cast(attn_bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
-    o.v[1][m] = __builtin_bit_cast(attn_bf16x8, make_uint4(md[0], md[1], md[2], md[3]));
-    o.v[2][m] = __builtin_bit_cast(attn_bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
+    if constexpr (NP == 6) {
+      o.v[1][m] = __builtin_bit_cast(attn_bf16x8, make_uint4(md[0], md[1], md[2], md[3]));
+      o.v[2][m] = __builtin_bit_cast(attn_bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
+    }
   }
 }
-__device__ __forceinline__ f32x4 mfma6(const Frag6& a, const Frag6& b, f32x4 c) {
+template <int NP>
+__device__ __forceinline__ f32x4 mfma_np(const Frag6& a, const Frag6& b, f32x4 c) {
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
-    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[1][m], b.v[1][m], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[2][m], b.v[0][m], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[0][m], b.v[2][m], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[1][m], b.v[0][m], c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[0][m], b.v[1][m], c, 0, 0, 0);
+    if constexpr (NP == 6) {
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[1][m], b.v[1][m], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[2][m], b.v[0][m], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[0][m], b.v[2][m], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[1][m], b.v[0][m], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[0][m], b.v[1][m], c, 0, 0, 0);
+    }
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[0][m], b.v[0][m], c, 0, 0, 0);
   }
   return c;
@@ -824,7 +835,7 @@ constexpr int RW_SPITCH = 64;
 // 2); the row max and sum are combined through LDS with one block barrier each.  Measured at C2
 // B=128: 398 vs 395 us (327 vs 309 without dropout) — the kernel is not latency-bound but bound
 // by the SIMD's shared f32 MFMA / VALU issue, so the extra occupancy buys nothing.
-template <int NTA, bool P2, bool LEGACY, int SPLIT = 1, bool XS = false>  // SPLIT * NTA >= ceil(T/16) key tiles
+template <int NTA, bool P2, bool LEGACY, int SPLIT = 1, int XS = 0>  // SPLIT * NTA >= ceil(T/16) key tiles
 __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fwd16_kernel(
     const float* __restrict__ qu, const float* __restrict__ qv, const float* __restrict__ kmat, long ldk,
     const float* __restrict__ pm, long ldpm, int nb, float sqrt_dk, const int* __restrict__ klen,
@@ -880,8 +891,8 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
   // tile (one exposed load per wave) instead of holding both rows' planes
   Frag6 xu, xv;
   if constexpr (XS) {
-    split_frag(au, xu);
-    split_frag(av, xv);
+    split_frag<XS>(au, xu);
+    split_frag<XS>(av, xv);
   }
   int kl = klen ? klen[b] : T;
   if (kl > T) kl = T;
@@ -903,12 +914,12 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
     if constexpr (XS) {
       Frag6 pf6;
-      split_frag(pb[0], pf6);
+      split_frag<XS>(pb[0], pf6);
       if (shifted) {  // (SPLIT 2: a second-half wave whose keys all lie past the switch)
         ld16(qv + ((long)z * T + min(i0 + 1 + li, T - 1)) * RP_DK, av2);
-        split_frag(av2, xv);
+        split_frag<XS>(av2, xv);
       }
-      s = mfma6(xv, pf6, s);
+      s = mfma_np<XS>(xv, pf6, s);
     } else {
 #pragma unroll
       for (int c = 0; c < 16; ++c)
@@ -932,14 +943,14 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
       f32x4 a = {0.f, 0.f, 0.f, 0.f}, s = {0.f, 0.f, 0.f, 0.f};
       if constexpr (XS) {
         Frag6 kf6, pf6;
-        split_frag(kf, kf6);
-        split_frag(pf, pf6);
+        split_frag<XS>(kf, kf6);
+        split_frag<XS>(pf, pf6);
         if (LEGACY && t == g) {  // block t+1 = g+1: the first shifted band block
           ld16(qv + ((long)z * T + min(i0 + 1 + li, T - 1)) * RP_DK, av2);
-          split_frag(av2, xv);
+          split_frag<XS>(av2, xv);
         }
-        a = mfma6(xu, kf6, a);
-        s = mfma6(xv, pf6, s);
+        a = mfma_np<XS>(xu, kf6, a);
+        s = mfma_np<XS>(xv, pf6, s);
       } else {
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
@@ -1302,10 +1313,17 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
   const bool p2 = sqrt_dk > 0.f && (__builtin_bit_cast(uint32_t, sqrt_dk) & 0x7fffffu) == 0;
   static int xs_env = -1;  // ESP_ATTN_XS=1: the split products (A/B measurements)
   if (xs_env < 0) xs_env = getenv("ESP_ATTN_XS") ? atoi(getenv("ESP_ATTN_XS")) : ESP_ATTN_XS_DEFAULT;
-  if (xs_env && !split) {
-#define ESP_RX3(N, P2_, L_)                                                                                            \
-  hipLaunchKernelGGL((relpos_attn_fwd16_kernel<N, P2_, L_, 1, true>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p,    \
+  // the bf16 mode computes the scores on bf16 operands like every other product of its step
+  const int np = xs_env ? 6 : (esp_get_gemm_compute() == 1 ? 1 : 0);
+  if (np && !split) {
+#define ESP_RX4(N, P2_, L_, NP_)                                                                                       \
+  hipLaunchKernelGGL((relpos_attn_fwd16_kernel<N, P2_, L_, 1, NP_>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p,     \
                      ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid, nrb, Zn)
+#define ESP_RX3(N, P2_, L_)              \
+  do {                                   \
+    if (np == 6) ESP_RX4(N, P2_, L_, 6); \
+    else ESP_RX4(N, P2_, L_, 1);         \
+  } while (0)
 #define ESP_RX(N)                     \
   do {                                \
     if (relpos == 2) {                \
@@ -1323,16 +1341,22 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
       // share a row group's keys (SPLIT 2, half the score registers each)
       nrb = (T + 2 * RW_ROWS - 1) / (2 * RW_ROWS);
       grid.x = (unsigned)(8 * ((Zn + 7) / 8) * nrb);
-      if (p2) hipLaunchKernelGGL((relpos_attn_fwd16_kernel<16, true, true, 2, true>), grid, dim3(256), 0, st, qu, qv,
-                                 kmat, ldk, p, ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds,
-                                 esp::rng_key_ptr(), tvalid, nrb, Zn);
-      else hipLaunchKernelGGL((relpos_attn_fwd16_kernel<16, false, true, 2, true>), grid, dim3(256), 0, st, qu, qv,
-                              kmat, ldk, p, ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds,
-                              esp::rng_key_ptr(), tvalid, nrb, Zn);
+#define ESP_RL(P2_, NP_)                                                                                               \
+  hipLaunchKernelGGL((relpos_attn_fwd16_kernel<16, P2_, true, 2, NP_>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p,   \
+                     ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid, nrb, Zn)
+      if (np == 6) {
+        if (p2) ESP_RL(true, 6);
+        else ESP_RL(false, 6);
+      } else {
+        if (p2) ESP_RL(true, 1);
+        else ESP_RL(false, 1);
+      }
+#undef ESP_RL
     } else if (nt <= 24) ESP_RX(24);
     else ESP_RX(32);
 #undef ESP_RX
 #undef ESP_RX3
+#undef ESP_RX4
     ESP_CHECK_LAUNCH("esp_relpos_attn_probs");
     return 0;
   }

@@ -595,7 +595,11 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
       const long t = ntiles(bn);
       // (B planes: only A is split, 3.7 split VALU per MFMA at either width)
       const double per = split_f32 && !bplanes && bn == 64 ? 1.5 : bn / 64;
-      if (split_f32 && work && t < target && K >= 2 * 128) return (double)t * per / 256.0;
+      // (bf16 operands, PREC 2: a weight gradient's split-K grid is priced by its total work too -- the
+      // 128-wide tiles halve its B re-reads, which bound the bf16 k-loop: C5 (1,1,2048,512,23936)
+      // 2.50 -> 2.03 ms, (1,1,512,2048,23936) 2.34 -> 1.79, r04 ESP_GEMM_BNT=128 A/B)
+      if ((split_f32 || (g.bf16 == 2 && mode_a == RC && mode_b == RC)) && work && t < target && K >= 2 * 128)
+        return (double)t * per / 256.0;
       double c = (double)((t + 255) / 256) * per;
       if (t < 2 * 256) c *= 1.3;
       return c;
