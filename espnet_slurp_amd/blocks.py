@@ -556,14 +556,22 @@ class Conv2dSubsampling(nn.Module):
         T1, F1 = (T - 3) // 2 + 1, (F - 3) // 2 + 1
         T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
         c0, c2 = self.conv[0], self.conv[2]
+        # the bf16 mode: conv1 also writes z1's bf16 copy, the conv2 GEMM's operand (z1 stays fp32 for the
+        # weight gradient's gather and the ReLU mask)
+        b16 = K.conv2_bf16_ok(D)
         z1 = empty(B * T1 * F1 * D, like=feats)
-        K.conv1_fwd(feats, c0.weight, c0.bias, z1, B, T, F, D)
+        z1_16 = torch.empty(B * T1 * F1 * D, dtype=torch.bfloat16, device=feats.device) if b16 else None
+        K.conv1_fwd(feats, c0.weight, c0.bias, z1, B, T, F, D, z16=z1_16)
         w2r = empty(D * 9 * D, like=feats)
         K.permute3(c2.weight, w2r, D, D, 9)
         z2 = empty(B * T2 * F2, D, like=feats)
         ic = (T1, F1, D, T2, F2)
-        K.gemm(B * T2 * F2, D, 9 * D, z1, w2r, z2, mode_a=K.I2C_KC, lda=0, mode_b=K.KC, ldb=9 * D, ldc=D,
-               bias=c2.bias, act=K.ACT_RELU, ic_a=ic, b_weight=True)
+        if b16:
+            K.conv2_fwd_bf16(z1_16, K.to_bf16(w2r, D, 9 * D, 9 * D), c2.bias, z2, B, T1, F1, D)
+            del z1_16
+        else:
+            K.gemm(B * T2 * F2, D, 9 * D, z1, w2r, z2, mode_a=K.I2C_KC, lda=0, mode_b=K.KC, ldb=9 * D, ldc=D,
+                   bias=c2.bias, act=K.ACT_RELU, ic_a=ic, b_weight=True)
         lin = self.out[0]
         wor = empty(D * F2 * D, like=feats)
         K.permute3(lin.weight, wor, D, D, F2)  # (n, c, f) -> (n, f, c)
@@ -599,7 +607,10 @@ class Conv2dSubsampling(nn.Module):
         # 4 implicit parity-class GEMMs with the ReLU mask in the epilogue (no 9x column buffer,
         # 8.4 GB at C2 B=128): 10.2 ms against 12.4 ms for column GEMM + col2im (kernels.py)
         if K.CONV2_IMPLICIT_DGRAD and D % 32 == 0:
-            K.conv2_dgrad(dz2p, c2.weight, c.z1, dz1, B, T1, F1, D)
+            # (the bf16 mode: dz2's bf16 copy is the class GEMMs' operand)
+            dz2_16 = K.to_bf16(dz2p, npix2, D, D) if K.conv2_bf16_ok(D) else None
+            K.conv2_dgrad(dz2p, c2.weight, c.z1, dz1, B, T1, F1, D, dz2_16=dz2_16)
+            del dz2_16
         else:
             dcol = empty(npix2, 9 * D, like=dx)
             K.gemm(npix2, 9 * D, D, dz2p, c.w2r, dcol, mode_a=K.KC, lda=D, mode_b=K.RC, ldb=9 * D, ldc=9 * D,

@@ -16,9 +16,13 @@ inline int gridn(long n) {
 // x (B,T,F) -> z (B,T1,F1,D).  A thread owns 4 output channels (weights + bias in registers,
 // loaded once) and strides over pixels; a wave covers 64 channel quads of one pixel, so the
 // 9-tap patch load is a broadcast and the store is 1 KB contiguous per wave.
+// z16 != nullptr (the bf16 mode): the output's bf16 copy too (RNE), the A operand of the bf16 conv2
+// forward (esp_conv2_fwd_bf16); z stays fp32 for the weight gradient's gather and the ReLU mask
+template <bool B16>
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict__ x, const float* __restrict__ W,
-                                                        const float* __restrict__ bias, float* __restrict__ z, int B,
-                                                        int T, int F, int T1, int F1, int D) {
+                                                        const float* __restrict__ bias, float* __restrict__ z,
+                                                        uint2* __restrict__ z16, int B, int T, int F, int T1, int F1,
+                                                        int D) {
   const int D4 = D / 4;
   const long tid = blockIdx.x * (long)blockDim.x + threadIdx.x;
   const long nthr = (long)gridDim.x * blockDim.x;  // multiple of D4 (host)
@@ -51,6 +55,7 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict_
       out[q] = fmaxf(a, 0.f);
     }
     *reinterpret_cast<float4*>(z + (long)p * D + o4 * 4) = make_float4(out[0], out[1], out[2], out[3]);
+    if constexpr (B16) z16[((long)p * D + o4 * 4) >> 2] = make_uint2(esp::bf16_pair(out[0], out[1]), esp::bf16_pair(out[2], out[3]));
   }
 }
 
@@ -185,8 +190,19 @@ __global__ void permute3_kernel(const float* __restrict__ in, float* __restrict_
 
 }  // namespace
 
+static int conv1_fwd_impl(const float* x, const float* W, const float* bias, float* z, void* z16, int B, int T, int F,
+                          int D, void* stream);
 ESP_API int esp_conv1_fwd(const float* x, const float* W, const float* bias, float* z, int B, int T, int F, int D,
                           void* stream) {
+  return conv1_fwd_impl(x, W, bias, z, nullptr, B, T, F, D, stream);
+}
+ESP_API int esp_conv1_fwd_bf16(const float* x, const float* W, const float* bias, float* z, void* z16, int B, int T,
+                               int F, int D, void* stream) {
+  ESP_ARG_CHECK(z16 && ((uintptr_t)z16 & 7) == 0, "esp_conv1_fwd_bf16: z16 must be 8-B aligned");
+  return conv1_fwd_impl(x, W, bias, z, z16, B, T, F, D, stream);
+}
+static int conv1_fwd_impl(const float* x, const float* W, const float* bias, float* z, void* z16, int B, int T, int F,
+                          int D, void* stream) {
   ESP_ARG_CHECK(D % 4 == 0, "esp_conv1_fwd: D %% 4 != 0");
   const int T1 = (T - 3) / 2 + 1, F1 = (F - 3) / 2 + 1;
   ESP_ARG_CHECK(256 % (D / 4) == 0, "esp_conv1_fwd: D/4 must divide 256");
@@ -194,8 +210,12 @@ ESP_API int esp_conv1_fwd(const float* x, const float* W, const float* bias, flo
   ESP_ARG_CHECK(npix < (1L << 32), "esp_conv1_fwd: %ld output pixels (32-bit index math)", npix);
   long nblk = (npix * (D / 4) + 255) / 256;
   if (nblk > 8192) nblk = 8192;  // ~16 pixels per thread at the C2 sizes: weights amortised
-  hipLaunchKernelGGL(conv1_fwd_kernel, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, x, W, bias, z, B, T,
-                     F, T1, F1, D);
+  if (z16)
+    hipLaunchKernelGGL(conv1_fwd_kernel<true>, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, x, W, bias, z,
+                       (uint2*)z16, B, T, F, T1, F1, D);
+  else
+    hipLaunchKernelGGL(conv1_fwd_kernel<false>, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, x, W, bias, z,
+                       nullptr, B, T, F, T1, F1, D);
   ESP_CHECK_LAUNCH("esp_conv1_fwd");
   return 0;
 }

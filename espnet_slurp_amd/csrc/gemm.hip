@@ -425,6 +425,21 @@ ESP_API int esp_gemm_bf16(int mode_a, int mode_b, int M, int N, int K, int batch
                   seed, bwd_act, pre, rowsum, nullptr, nullptr, work, work_bytes, stream, 2);
 }
 
+// The conv2 forward of the bf16 mode (subsampling.py:53-87 in NHWC): z2 = ReLU(im2col(z1) W^T + b)
+// with z1 and the (o, kt, kf, c)-laid weights in bf16 (z1_16 from esp_conv1_fwd_bf16, w16 row pitch
+// 9D), fp32 accumulate and output: the implicit-im2col GEMM on bf16 operands (PREC 2, the gather in
+// bf16-pair units).  D % 64 == 0.
+ESP_API int esp_conv2_fwd_bf16(const void* z1_16, const void* w16, const float* bias, float* z2, int B, int T1, int F1,
+                               int D, float* work, long work_bytes, void* stream) {
+  ESP_ARG_CHECK(B >= 1 && T1 >= 3 && F1 >= 3 && D % 64 == 0 && aligned16(z1_16) && aligned16(w16) && aligned16(z2),
+                "esp_conv2_fwd_bf16: bad sizes / alignment (D %% 64 == 0, 16-B aligned operands)");
+  const int T2 = (T1 - 3) / 2 + 1, F2 = (F1 - 3) / 2 + 1;
+  const int ic[5] = {T1, F1, D / 2, T2, F2};  // channel pairs
+  return gemm_run(I2C_KC, KC, B * T2 * F2, D, 9 * D / 2, 1, 1, (const float*)z1_16, 0, 0, 0, (const float*)w16,
+                  9 * D / 2, 0, 0, z2, D, 0, 0, bias, 1.f, 0.f, nullptr, ACT_RELU, nullptr, 0.f, 0, 0, nullptr, nullptr,
+                  ic, nullptr, work, work_bytes, stream, 2);
+}
+
 ESP_API int esp_gemm_bf16_pl(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2, const void* A, long lda,
                              long sa1, long sa2, const void* B, long ldb, long sb1, long sb2, void* C, long ldc,
                              long sc1, long sc2, const float* bias, float alpha, float beta, int act, float* aux,
@@ -722,8 +737,25 @@ __global__ void conv2_class_weights_kernel(const float* __restrict__ W, float* _
 // planes (the B-planes class GEMMs of the fp32 split build), 3 * 9 * D * D bf16
 // (esp_conv2_dgrad_workspace_bytes)
 ESP_API long esp_conv2_dgrad_workspace_bytes(int D) { return D <= 0 ? 0 : 4L * 9 * D * D + 6L * 9 * D * D; }
+static int conv2_dgrad_impl(const float* dz2, const void* dz2_16, const float* W, const float* z1, float* dz1, int B,
+                            int T1, int F1, int D, const float* zeros16, float* wc_work, long work_bytes,
+                            void* stream);
 ESP_API int esp_conv2_dgrad(const float* dz2, const float* W, const float* z1, float* dz1, int B, int T1, int F1,
                             int D, const float* zeros16, float* wc_work, long work_bytes, void* stream) {
+  return conv2_dgrad_impl(dz2, nullptr, W, z1, dz1, B, T1, F1, D, zeros16, wc_work, work_bytes, stream);
+}
+// the bf16 mode's form: dz2 as bf16 (dz2_16), the class weights cast to bf16 in the workspace, the class
+// GEMMs on bf16 operands (PREC 2, the tap gather in bf16-pair units); D % 64 == 0
+ESP_API int esp_conv2_dgrad_bf16(const void* dz2_16, const float* W, const float* z1, float* dz1, int B, int T1,
+                                 int F1, int D, const float* zeros16, float* wc_work, long work_bytes, void* stream) {
+  ESP_ARG_CHECK(D % 64 == 0, "esp_conv2_dgrad_bf16: D %% 64 == 0 needed");
+  return conv2_dgrad_impl(nullptr, dz2_16, W, z1, dz1, B, T1, F1, D, zeros16, wc_work, work_bytes, stream);
+}
+static int conv2_dgrad_impl(const float* dz2, const void* dz2_16, const float* W, const float* z1, float* dz1, int B,
+                            int T1, int F1, int D, const float* zeros16, float* wc_work, long work_bytes,
+                            void* stream) {
+  const bool b16 = dz2_16 != nullptr;
+  if (b16) dz2 = (const float*)dz2_16;  // bf16 pairs viewed as fp32 elements
   const int T2 = (T1 - 3) / 2 + 1, F2 = (F1 - 3) / 2 + 1;
   const long need__ = esp_conv2_dgrad_workspace_bytes(D);
   ESP_ARG_CHECK(work_bytes >= need__, "esp_conv2_dgrad: workspace %ld B < %ld B required (esp_conv2_dgrad_workspace_bytes)", work_bytes, need__);
@@ -733,10 +765,16 @@ ESP_API int esp_conv2_dgrad(const float* dz2, const float* W, const float* z1, f
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(conv2_class_weights_kernel, dim3(1024), dim3(256), 0, st, W, wc_work, D);
   ESP_CHECK_LAUNCH("esp_conv2_dgrad (weights)");
-  // fp32 compute on split products: the class weights as B planes (PREC 3, no B split in the k-loop)
-  const bool bp = g_compute == 0 && ESP_F32_SPLIT && variant() == 4;
+  // fp32 compute on split products: the class weights as B planes (PREC 3, no B split in the k-loop);
+  // the bf16 form: their bf16 copy (plane 0 of the same conversion: hi = RNE)
+  const bool bp = !b16 && g_compute == 0 && ESP_F32_SPLIT && variant() == 4;
   const long ps = 9L * D * D;
   __bf16* planes = reinterpret_cast<__bf16*>(wc_work + ps);
+  if (b16) {
+    hipLaunchKernelGGL(f32_to_planes_kernel, dim3((unsigned)std::min<long>((ps / 8 + 255) / 256, 8192)), dim3(256), 0,
+                       st, wc_work, (uint4*)planes, 9L * D, D, (long)D, (long)D, ps, 1);
+    ESP_CHECK_LAUNCH("esp_conv2_dgrad (bf16 weights)");
+  }
   if (bp) {
     hipLaunchKernelGGL(f32_to_planes_kernel, dim3((unsigned)std::min<long>((ps / 8 + 255) / 256, 8192)), dim3(256), 0,
                        st, wc_work, (uint4*)planes, 9L * D, D, (long)D, (long)D, ps, 1);
@@ -750,7 +788,7 @@ ESP_API int esp_conv2_dgrad(const float* dz2, const float* W, const float* z1, f
     GldsArgs t{};
     t.t_hw = make_fastdiv((uint32_t)(Ha * We));
     t.t_w = make_fastdiv((uint32_t)We);
-    t.t_T2 = T2; t.t_F2 = F2; t.t_C = D;
+    t.t_T2 = T2; t.t_F2 = F2; t.t_C = b16 ? D / 2 : D;  // (bf16: channel pairs)
     for (int ti = 0; ti < ntap; ++ti) {
       const int kt = ph ? 1 : 2 * (ti / nkf), kf = pw ? 1 : 2 * (ti % nkf);
       t.t_dt[ti] = (kt - ph) / 2;
@@ -758,7 +796,7 @@ ESP_API int esp_conv2_dgrad(const float* dz2, const float* W, const float* z1, f
     }
     t.t_zeros = zeros16;
     GemmArgs g{};
-    g.M = B * Ha * We; g.N = D; g.K = ntap * D; g.nb2 = 1;
+    g.M = B * Ha * We; g.N = D; g.K = b16 ? ntap * D / 2 : ntap * D; g.nb2 = 1;
     g.a = Operand{dz2, 0, 0, 0, 1, {}, 1};
     g.b = Operand{wc_work + (long)slot0[cls] * D * D, D, 0, 0, 1, {}, 1};
     g.c = dz1; g.ldc = D; g.alpha = 1.f; g.beta = 0.f;
@@ -768,6 +806,10 @@ ESP_API int esp_conv2_dgrad(const float* dz2, const float* W, const float* z1, f
       g.b = Operand{reinterpret_cast<const float*>(planes + (long)slot0[cls] * D * D), D, 0, 0, 1, {}, 1};
       g.b.ps = ps;
       g.bf16 = 3;
+    }
+    if (b16) {  // RC bf16: rows = D, ld in pairs
+      g.b = Operand{reinterpret_cast<const float*>(planes + (long)slot0[cls] * D * D), D / 2, 0, 0, 1, {}, 1};
+      g.bf16 = 2;
     }
     g.key = esp::rng_key_ptr();
     g.wide = 1;

@@ -2086,11 +2086,11 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
 
 // Map run-time (mode_a, mode_b, tile width, precision) onto compile-time constants for the mode
 // pairs the host issues; calls f(MA, MB, BNT, PREC) with std::integral_constant arguments.
-// false: no such instantiation (PREC 2 exists for KC x KC only).
+// false: no such instantiation.
 template <int V>
 using IC = std::integral_constant<int, V>;
 // bm = 64 (64 x 64 tiles) exists for bnt = 64, KC / RC operand pairs and prec 0 / 1 only;
-// prec 2 (bf16 operands) for the KC / RC pairs with 128-row tiles.
+// prec 2 (bf16 operands) for the KC / RC pairs and I2C_KC x KC / I2CT_KC x RC with 128-row tiles.
 template <class F>
 bool glds_switch(int ma, int mb, int bnt, int prec, int bm, F&& f) {
   auto tile = [&](auto A, auto B) {
@@ -2113,7 +2113,10 @@ bool glds_switch(int ma, int mb, int bnt, int prec, int bm, F&& f) {
       } else if (prec == 5) {  // both operands as planes: KC / RC pairs, 64-wide tiles (LDS)
         if constexpr (small_ok && decltype(N)::value == 64) f(A, B, N, IC<5>{}, R);
         else return false;
-      } else if constexpr (small_ok && decltype(R)::value == BM) {  // bf16 operands: KC / RC pairs
+      } else if constexpr ((small_ok || (MA_ == I2C_KC && MB_ == KC) || (MA_ == I2CT_KC && MB_ == RC)) &&
+                           decltype(R)::value == BM) {
+        // bf16 operands: KC / RC pairs, and the conv2 forward / input gradient (implicit-im2col A of
+        // bf16 pairs: the gathers run in pair units, C % 64 == 0)
         f(A, B, N, IC<2>{}, R);
       } else {
         return false;

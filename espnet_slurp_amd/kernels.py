@@ -1025,8 +1025,35 @@ def relshift_bwd(dS, dbd, relpos, Z, T, P, lds=None, ldp=None):
 
 
 # ----------------------------------------------------------------------------- subsampling
-def conv1_fwd(x, W, b, z, B, T, F, D):
+def conv1_fwd(x, W, b, z, B, T, F, D, z16=None):
+    """z16 (bf16, optional): the output's bf16 copy too (esp_conv1_fwd_bf16)."""
+    if z16 is not None:
+        _native.call("esp_conv1_fwd_bf16", _p(x), _p(W), _p(b), _p(z), _p(z16), B, T, F, D, _st())
+        return
     _native.call("esp_conv1_fwd", _p(x), _p(W), _p(b), _p(z), B, T, F, D, _st())
+
+
+def conv2_bf16_ok(D: int) -> bool:
+    """The bf16 mode runs the conv2 forward and input gradient on bf16 operands (esp_conv2_fwd_bf16 /
+    esp_conv2_dgrad_bf16) when D % 64 == 0."""
+    return _COMPUTE[0] == GEMM_BF16 and _AMP_BF16_OPERANDS and D % 64 == 0
+
+
+def conv2_fwd_bf16(z1_16, w16, bias, z2, B, T1, F1, D):
+    """z2 = ReLU(im2col(z1) W^T + b) on bf16 operands (esp_conv2_fwd_bf16)."""
+    ws = _ws(_GEMM_WS, "esp_gemm_bf16", _GEMM_WS_BYTES, z2.device)
+    if _PROF is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    _native.call("esp_conv2_fwd_bf16", _p(z1_16), _p(w16), _p(bias), _p(z2), B, T1, F1, D, _p(ws), _GEMM_WS_BYTES,
+                 _st())
+    _guard_post("esp_gemm_bf16", ws, _GEMM_WS_BYTES)
+    if _PROF is not None:
+        ev1.record()
+        T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
+        M = B * T2 * F2
+        _PROF.append((2.0 * M * D * 9 * D, ev0, ev1, (I2C_KC, KC, M, D, 9 * D, 1, "bf16"), 0.0))
 
 
 def col2im_relu(dcol, z1, dz1, B, T1, F1, D):
@@ -1141,8 +1168,9 @@ _ZEROS = {}
 CONV2_IMPLICIT_DGRAD = os.environ.get("ESP_CONV2_IMPLICIT_DGRAD", "1") == "1"
 
 
-def conv2_dgrad(dz2, W, z1, dz1, B, T1, F1, D):
-    """Conv2d(D, D, 3, 2) input gradient x conv1 ReLU mask as 4 implicit parity-class GEMMs."""
+def conv2_dgrad(dz2, W, z1, dz1, B, T1, F1, D, dz2_16=None):
+    """Conv2d(D, D, 3, 2) input gradient x conv1 ReLU mask as 4 implicit parity-class GEMMs; dz2_16 (the
+    bf16 mode): dz2 as bf16, the class GEMMs on bf16 operands (esp_conv2_dgrad_bf16)."""
     _f32(dz2, W, z1, dz1)
     key = str(dz2.device)
     if key not in _ZEROS:
@@ -1153,7 +1181,12 @@ def conv2_dgrad(dz2, W, z1, dz1, B, T1, F1, D):
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         ev0.record()
-    _native.call("esp_conv2_dgrad", _p(dz2), _p(W), _p(z1), _p(dz1), B, T1, F1, D, _p(_ZEROS[key]), _p(wc), n, _st())
+    if dz2_16 is not None:
+        _native.call("esp_conv2_dgrad_bf16", _p(dz2_16), _p(W), _p(z1), _p(dz1), B, T1, F1, D, _p(_ZEROS[key]), _p(wc),
+                     n, _st())
+    else:
+        _native.call("esp_conv2_dgrad", _p(dz2), _p(W), _p(z1), _p(dz1), B, T1, F1, D, _p(_ZEROS[key]), _p(wc), n,
+                     _st())
     _guard_post("esp_conv2_dgrad", wc, n)
     if _PROF is not None:  # the 4 class GEMMs as one family entry: A = dz2 (gathered), B = W, C = dz1 + ReLU mask read
         ev1.record()

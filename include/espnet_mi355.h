@@ -126,6 +126,15 @@ int esp_gemm_bf16(int mode_a, int mode_b, int M, int N, int K, int batch, int nb
 /* esp_gemm_bf16 with C written as its bf16 plane (c_nplanes 1: hi = bf16(C), the reduced-precision
  * path's GEMM-only activations and gradients) under the rules of esp_gemm_f32_pl's c_nplanes: the
  * plain, FFN w_1 and ACT_MUL epilogues, N % 4 == 0, no residual / row sums, never split-K. */
+/* The bf16 mode's conv2 forward (subsampling.py:53-87, NHWC): z2 = ReLU(im2col(z1_16) w16^T + bias) on
+ * bf16 operands (z1_16 from esp_conv1_fwd_bf16, w16 the (o, kt, kf, c)-laid weights in bf16, row pitch
+ * 9D), fp32 accumulate and output.  D % 64 == 0, 16-B aligned operands. */
+int esp_conv2_fwd_bf16(const void* z1_16, const void* w16, const float* bias, float* z2, int B, int T1, int F1, int D,
+                       float* work, long work_bytes, void* stream);
+/* esp_conv2_dgrad with dz2 in bf16 (the bf16 mode): the class GEMMs on bf16 operands (workspace as
+ * esp_conv2_dgrad's).  D % 64 == 0. */
+int esp_conv2_dgrad_bf16(const void* dz2_16, const float* W, const float* z1, float* dz1, int B, int T1, int F1, int D,
+                         const float* zeros16, float* wc_work, long work_bytes, void* stream);
 int esp_gemm_bf16_pl(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2, const void* A, long lda,
                      long sa1, long sa2, const void* B, long ldb, long sb1, long sb2, void* C, long ldc,
                      long sc1, long sc2, const float* bias, float alpha, float beta, int act, float* aux,
@@ -355,6 +364,9 @@ int esp_global_mvn(float* x, const int* lens, int B, int T, int F, const float* 
 /* ---- Conv2dSubsampling (subsampling.py:53-87), NHWC */
 int esp_conv1_fwd(const float* x, const float* W, const float* bias, float* z, int B, int T,
                   int F, int D, void* stream);
+/* esp_conv1_fwd writing z's bf16 copy (RNE) to z16 too (8-B aligned): the bf16 mode's conv2 operand. */
+int esp_conv1_fwd_bf16(const float* x, const float* W, const float* bias, float* z, void* z16, int B, int T, int F,
+                       int D, void* stream);
 /* conv2 input gradient as 4 implicit GEMMs (one per parity class of the conv1 output grid):
  * dz1 = relu'(z1) * conv_transpose(dz2, W), W = Conv2d(D,D,3,2).weight (o,c,kt,kf) as the
  * reference stores it; no 9x column buffer.  zeros16: >= 16 B of zeros (device); wc_work:

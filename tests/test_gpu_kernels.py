@@ -768,6 +768,44 @@ def test_conv2_dgrad_parity_classes_vs_column_path(dev, T1, F1):
     assert rel_err(got.cpu(), ref.cpu()) < 1e-5
 
 
+@pytest.mark.parametrize("T1,F1", [(31, 39), (9, 7)])
+def test_conv2_bf16_operands_match_staged_rounding(dev, T1, F1):
+    """The bf16 mode's conv2 forward (esp_conv2_fwd_bf16: implicit im2col over conv1's bf16 copy of z1,
+    bf16 weights, PREC 2) and input gradient (esp_conv2_dgrad_bf16: dz2 and the class weights in bf16)
+    against the same GEMMs on fp32 operands rounded to bf16 in LDS staging (PREC 1): the same bf16
+    products, fp32 accumulation-order differences only.  conv1's bf16 copy is bit-equal to torch's RNE."""
+    B, D = 3, 128
+    T, F = 2 * T1 + 1, 2 * F1 + 1
+    T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
+    g = torch.Generator().manual_seed(37)
+    x = torch.randn(B, T, F, generator=g).to(dev)
+    w0, b0 = (torch.randn(D, 1, 3, 3, generator=g) * 0.3).to(dev), (torch.randn(D, generator=g) * 0.1).to(dev)
+    W = (torch.randn(D, D, 3, 3, generator=g) * 0.05).to(dev)
+    bias = (torch.randn(D, generator=g) * 0.1).to(dev)
+    z1 = torch.empty(B * T1 * F1 * D, device=dev)
+    z16 = torch.empty(B * T1 * F1 * D, dtype=torch.bfloat16, device=dev)
+    K.conv1_fwd(x, w0, b0, z1, B, T, F, D, z16=z16)
+    w2r = torch.empty(D * 9 * D, device=dev)
+    K.permute3(W, w2r, D, D, 9)
+    ref = torch.empty(B * T2 * F2, D, device=dev)
+    got = torch.empty(B * T2 * F2, D, device=dev)
+    dz2 = torch.randn(B * T2 * F2, D, generator=g).to(dev)
+    dref = torch.empty(B * T1 * F1 * D, device=dev)
+    dgot = torch.full((B * T1 * F1 * D,), float("nan"), device=dev)
+    with K.gemm_compute("bf16"):
+        K.gemm(B * T2 * F2, D, 9 * D, z1, w2r, ref, mode_a=K.I2C_KC, lda=0, mode_b=K.KC, ldb=9 * D, ldc=D,
+               bias=bias, act=K.ACT_RELU, ic_a=(T1, F1, D, T2, F2))
+        assert K.conv2_bf16_ok(D)
+        K.conv2_fwd_bf16(z16, K.to_bf16(w2r, D, 9 * D, 9 * D), bias, got, B, T1, F1, D)
+        K.conv2_dgrad(dz2, W, z1, dref, B, T1, F1, D)
+        K.conv2_dgrad(dz2, W, z1, dgot, B, T1, F1, D, dz2_16=K.to_bf16(dz2, B * T2 * F2, D, D))
+    torch.cuda.synchronize()
+    assert torch.equal(z16.view(torch.int16), z1.bfloat16().view(torch.int16))
+    assert rel_err(got.cpu(), ref.cpu()) < 1e-5
+    assert not torch.isnan(dgot).any()
+    assert rel_err(dgot.cpu(), dref.cpu()) < 1e-5
+
+
 @pytest.mark.parametrize("M,D", [(11968, 512), (3000, 768), (47872, 256)])
 def test_bn_swish_large_rows_and_channels(dev, M, D):
     """BatchNorm + Swish statistics at the C4 / C5 shapes (B*T' = 32*374 rows, D = 512): the
