@@ -32,6 +32,7 @@ SIGNATURES = {
     "esp_conv2_fwd_bf16": [P, P, P, P, I, I, I, I, P, L, P],
     "esp_conv2_dgrad_bf16": [P, P, P, P, I, I, I, I, P, P, L, P],
     "esp_conv1_fwd_bf16": [P, P, P, P, P, I, I, I, I, P],
+    "esp_conv2_wgrad_bf16": [P, P, P, P, I, I, I, I, P, L, P],
     "esp_gemm_f32": [I, I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, L, P, F, F, P, I, P, F, U64, I, P, P,
                      P, P, P, L, P],
     "esp_gemm_f32_bp": [I, I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, L, P, F, F, P, I, P, F, U64, I, P, P,
@@ -118,7 +119,7 @@ _RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I, "esp_set_g
              "esp_get_gemm_compute": I, "esp_set_splitk_mode": I,
              "esp_f32_gemm_products": I}
 _RESTYPES.update({k: L for k in SIGNATURES if k.endswith("_workspace_bytes")})
-ABI_VERSION = 27  # bumped whenever a signature in include/espnet_mi355.h changes
+ABI_VERSION = 28  # bumped whenever a signature in include/espnet_mi355.h changes
 
 _lib = None
 

@@ -568,7 +568,8 @@ class Conv2dSubsampling(nn.Module):
         ic = (T1, F1, D, T2, F2)
         if b16:
             K.conv2_fwd_bf16(z1_16, K.to_bf16(w2r, D, 9 * D, 9 * D), c2.bias, z2, B, T1, F1, D)
-            del z1_16
+            if training and (B * T2 * F2) % 2:  # (the bf16 weight gradient takes an even pixel count)
+                z1_16 = None
         else:
             K.gemm(B * T2 * F2, D, 9 * D, z1, w2r, z2, mode_a=K.I2C_KC, lda=0, mode_b=K.KC, ldb=9 * D, ldc=D,
                    bias=c2.bias, act=K.ACT_RELU, ic_a=ic, b_weight=True)
@@ -580,8 +581,8 @@ class Conv2dSubsampling(nn.Module):
         sd = seeds.next()
         K.linear_fwd(z2.view(B * T2, F2 * D), wor.view(D, F2 * D), lin.bias, x, alpha=xscale, drop_p=pd, seed=sd,
                      b_weight=True)
-        return x, Ctx(feats=feats, z1=z1, w2r=w2r, z2=z2, wor=wor, pd=pd, sd=sd, xscale=xscale,
-                      B=B, T=T, F=F, T1=T1, F1=F1, T2=T2, F2=F2)
+        return x, Ctx(feats=feats, z1=z1, z1_16=z1_16 if training else None, w2r=w2r, z2=z2, wor=wor, pd=pd, sd=sd,
+                      xscale=xscale, B=B, T=T, F=F, T1=T1, F1=F1, T2=T2, F2=F2)
 
     def bwd(self, c, dx):
         D = self.odim
@@ -600,15 +601,18 @@ class Conv2dSubsampling(nn.Module):
         dz2p = dz2.view(npix2, D)
         ic = (T1, F1, D, T2, F2)
         dw2r = empty(D, 9 * D, like=dx)
-        K.gemm(D, 9 * D, npix2, dz2p, c.z1, dw2r, mode_a=K.RC, lda=D, mode_b=K.I2C_RC, ldb=0, ldc=9 * D, ic_b=ic,
-               rowsum=c2.bias.grad)
+        # the bf16 mode: dz2's bf16 copy is the operand of the weight- and input-gradient GEMMs
+        dz2_16 = K.to_bf16(dz2p, npix2, D, D) if K.conv2_bf16_ok(D) else None
+        if dz2_16 is not None and c.z1_16 is not None:
+            K.conv2_wgrad_bf16(dz2_16, c.z1_16, dw2r, c2.bias.grad, B, T1, F1, D)
+        else:
+            K.gemm(D, 9 * D, npix2, dz2p, c.z1, dw2r, mode_a=K.RC, lda=D, mode_b=K.I2C_RC, ldb=0, ldc=9 * D, ic_b=ic,
+                   rowsum=c2.bias.grad)
         K.permute3(dw2r, c2.weight.grad, D, 9, D, accumulate=True)  # (o, kk, c) -> (o, c, kk)
         dz1 = empty(B * T1 * F1 * D, like=dx)
         # 4 implicit parity-class GEMMs with the ReLU mask in the epilogue (no 9x column buffer,
         # 8.4 GB at C2 B=128): 10.2 ms against 12.4 ms for column GEMM + col2im (kernels.py)
         if K.CONV2_IMPLICIT_DGRAD and D % 32 == 0:
-            # (the bf16 mode: dz2's bf16 copy is the class GEMMs' operand)
-            dz2_16 = K.to_bf16(dz2p, npix2, D, D) if K.conv2_bf16_ok(D) else None
             K.conv2_dgrad(dz2p, c2.weight, c.z1, dz1, B, T1, F1, D, dz2_16=dz2_16)
             del dz2_16
         else:

@@ -160,7 +160,8 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
   if (MA == I2C_KC && 8L * g.a.ic.H * g.a.ic.W * g.a.ic.C >= (1L << 32)) return false;
   // implicit-im2col B: pixel offsets on 24-bit multiplies (i2c_pix_off24)
   if (MB == I2C_RC) {
-    const long rows = (long)g.K / ((long)g.b.ic.Ho * g.b.ic.Wo) * g.b.ic.H * g.b.ic.W;  // Bn * H * W
+    const long kpix = g.bf16 == 2 ? 2L * g.K : (long)g.K;  // (bf16: K counts pixel pairs)
+    const long rows = kpix / ((long)g.b.ic.Ho * g.b.ic.Wo) * g.b.ic.H * g.b.ic.W;  // Bn * H * W
     if (rows >= (1L << 24) || rows * g.b.ic.C >= (1L << 32)) return false;
   }
   int kind = g.splits > 1 ? EPI_PLAIN : epi_kind_spec(g);
@@ -438,6 +439,23 @@ ESP_API int esp_conv2_fwd_bf16(const void* z1_16, const void* w16, const float* 
   return gemm_run(I2C_KC, KC, B * T2 * F2, D, 9 * D / 2, 1, 1, (const float*)z1_16, 0, 0, 0, (const float*)w16,
                   9 * D / 2, 0, 0, z2, D, 0, 0, bias, 1.f, 0.f, nullptr, ACT_RELU, nullptr, 0.f, 0, 0, nullptr, nullptr,
                   ic, nullptr, work, work_bytes, stream, 2);
+}
+
+// The bf16 mode's conv2 weight gradient: dW2r (D x 9D, (o, kt, kf, c)) = dz2^T im2col(z1) and the bias
+// gradient db += sum over pixels of dz2, on bf16 operands (dz2_16 [pixels][D], z1_16 from
+// esp_conv1_fwd_bf16): RC x gathered-RC GEMM on bf16 pairs (PREC 2), K = pixels / 2 pairs (an even pixel
+// count), split K with the fixed-order reduction.  D % 64 == 0.
+ESP_API int esp_conv2_wgrad_bf16(const void* dz2_16, const void* z1_16, float* dw, float* db, int B, int T1, int F1,
+                                 int D, float* work, long work_bytes, void* stream) {
+  const int T2 = (T1 - 3) / 2 + 1, F2 = (F1 - 3) / 2 + 1;
+  const long npix = (long)B * T2 * F2;
+  ESP_ARG_CHECK(B >= 1 && T1 >= 3 && F1 >= 3 && D % 64 == 0 && npix % 2 == 0 && aligned16(dz2_16) &&
+                    aligned16(z1_16) && aligned16(dw),
+                "esp_conv2_wgrad_bf16: bad sizes / alignment (D %% 64 == 0, an even pixel count, 16-B aligned)");
+  const int ic[5] = {T1, F1, D, T2, F2};  // bf16 channels (the gather's offsets are halved in the kernel)
+  return gemm_run(RC, I2C_RC, D, 9 * D, (int)(npix / 2), 1, 1, (const float*)dz2_16, D / 2, 0, 0,
+                  (const float*)z1_16, 0, 0, 0, dw, 9 * D, 0, 0, nullptr, 1.f, 0.f, nullptr, 0, nullptr, 0.f, 0, 0,
+                  nullptr, db, nullptr, ic, work, work_bytes, stream, 2);
 }
 
 ESP_API int esp_gemm_bf16_pl(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2, const void* A, long lda,

@@ -1270,10 +1270,19 @@ __device__ __forceinline__ uint32_t i2c_pix_off24(const Im2col& ic, const FastDi
   return __umul24(__umul24(__umul24(bi, (uint32_t)ic.H) + 2 * ho, (uint32_t)ic.W) + 2 * wo, (uint32_t)ic.C);
 }
 
+// 16-byte chunk swizzle of a bf16 RC slab's k-row (see StageS)
+__device__ __forceinline__ int bf16_rc_swz(int rowb, int kr) {
+  return rowb == 256 ? (kr & 3) << 2 : ((kr >> 1) & 1) << 2;
+}
+
 // Per-lane source bookkeeping for one operand: NI wave-instructions per slab.
-template <int MODE, int ROWS, int NI>
+// B16 (PREC 2, bf16 pairs; I2C_RC: the bf16 conv2 weight gradient's gathered B): the slab is the bf16
+// RC image of StageS (64 pixel k-rows x ROWS bf16 columns, 16-B chunks of 8 channels XOR-swizzled by
+// k-row, bf16_rc_swz) and the im2col offsets are computed in bf16 elements (ic.C = bf16 channels)
+template <int MODE, int ROWS, int NI, bool B16 = false>
 struct Stage {
   static constexpr bool kKC = MODE == KC || MODE == I2C_KC || MODE == I2CT_KC;
+  static_assert(!B16 || MODE == I2C_RC || kKC, "Stage<B16>: bf16 pairs for the gathered operands only");
   const float* p[NI];  // per instruction: base incl. the slab-invariant part
   int q[NI];           // KC: k offset inside the slab (4*quad) ; RC: k-row inside the slab
   int ga[MODE == I2CT_KC ? NI : 1], ge[MODE == I2CT_KC ? NI : 1];  // I2CT: class-grid row / column
@@ -1298,6 +1307,13 @@ struct Stage {
           ge[i] = e;
           p[i] = base + (((long)bb * x->t_T2 + a) * x->t_F2 + e) * x->t_C;
         }
+      } else if constexpr (B16) {  // I2C_RC in bf16: chunk of 8 channel columns, pixel k-row kr
+        constexpr int QPR = ROWS / 8;  // 16-byte chunks per k-row
+        const int kr = slot / QPR, c = slot % QPR;
+        const int cs = c ^ bf16_rc_swz(ROWS * 2, kr);
+        const int gn = min(row0 + 8 * cs, (rows - 1) & ~7);  // first column of the chunk
+        q[i] = kr;
+        p[i] = base + (i2c_col_off(op.ic, fc, gn) >> 1);  // bf16 elements -> pairs
       } else {
         constexpr int QPR = ROWS / 4;  // quads per k-row
         const int kr = slot / QPR, rs = slot % QPR;
@@ -1338,6 +1354,9 @@ struct Stage {
           const bool in = a >= 0 && a < x->t_T2 && e >= 0 && e < x->t_F2;
           lds_dma16(in ? p[i] - ((long)dt * x->t_F2 + df) * x->t_C + o0 + q[i] : x->t_zeros, ldsw);
         }
+      } else if constexpr (B16) {  // pixel 2 k0 + kr (K counts pixel pairs)
+        const int pix = min(2 * k0 + q[i], 2 * K - 1);
+        lds_dma16(p[i] + (i2c_pix_off24(op.ic, fhw, fwo, (uint32_t)pix) >> 1), ldsw);
       } else {
         const int k = min(k0 + q[i], K - 1);
         if constexpr (MODE == RC) lds_dma16(p[i] + (long)k * op.ld, ldsw);
@@ -1374,9 +1393,6 @@ __device__ __forceinline__ uint32_t lds_addr(const float* p) {
 // bytes per k-row, the same 16 KB / 8 KB as every other slab), its 16-byte chunks XOR-swizzled
 // by k-row (bf16_rc_swz) for the transposing reads of frag_tr16.  K and k0 count pairs; an RC
 // k-row index is 2 * k + (0..63).  `rows` and `ld` of an RC operand: bf16 rows, ld in pairs.
-__device__ __forceinline__ int bf16_rc_swz(int rowb, int kr) {
-  return rowb == 256 ? (kr & 3) << 2 : ((kr >> 1) & 1) << 2;
-}
 
 template <int MODE, int ROWS, int NI, bool B16 = false>
 struct StageS {
@@ -1714,7 +1730,8 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
   using SAt = std::conditional_t<AP, StageP<MA, BMT>,
                                  std::conditional_t<SA_S, StageS<MA, BMT, NIA, PREC == 2>, Stage<MA, BMT, NIA>>>;
   using SBt = std::conditional_t<BP, StageP<MB, BNT>,
-                                 std::conditional_t<SB_S, StageS<MB, BNT, NIB, PREC == 2>, Stage<MB, BNT, NIB>>>;
+                                 std::conditional_t<SB_S, StageS<MB, BNT, NIB, PREC == 2>,
+                                                    Stage<MB, BNT, NIB, PREC == 2 && MB == I2C_RC>>>;
   SAt sa;
   SBt sb;
   auto init_ab = [&](const TileCoord& cc) {
@@ -1782,7 +1799,7 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          if constexpr (MB == RC) {
+          if constexpr (MB == RC || MB == I2C_RC) {
             frag_tr16<BNT>(cur + A_SZ, wn * TN * 32 + j * 32, lane, b4[j]);
           } else {
             float f[16];
@@ -2113,10 +2130,11 @@ bool glds_switch(int ma, int mb, int bnt, int prec, int bm, F&& f) {
       } else if (prec == 5) {  // both operands as planes: KC / RC pairs, 64-wide tiles (LDS)
         if constexpr (small_ok && decltype(N)::value == 64) f(A, B, N, IC<5>{}, R);
         else return false;
-      } else if constexpr ((small_ok || (MA_ == I2C_KC && MB_ == KC) || (MA_ == I2CT_KC && MB_ == RC)) &&
+      } else if constexpr ((small_ok || (MA_ == I2C_KC && MB_ == KC) || (MA_ == I2CT_KC && MB_ == RC) ||
+                            (MA_ == RC && MB_ == I2C_RC)) &&
                            decltype(R)::value == BM) {
         // bf16 operands: KC / RC pairs, and the conv2 forward / input gradient (implicit-im2col A of
-        // bf16 pairs: the gathers run in pair units, C % 64 == 0)
+        // bf16 pairs: the gathers run in pair units, C % 64 == 0) / weight gradient (gathered bf16 B)
         f(A, B, N, IC<2>{}, R);
       } else {
         return false;

@@ -1168,6 +1168,23 @@ _ZEROS = {}
 CONV2_IMPLICIT_DGRAD = os.environ.get("ESP_CONV2_IMPLICIT_DGRAD", "1") == "1"
 
 
+def conv2_wgrad_bf16(dz2_16, z1_16, dw, db, B, T1, F1, D):
+    """dw (D x 9D) = dz2^T im2col(z1), db += colsum(dz2), on bf16 operands (esp_conv2_wgrad_bf16)."""
+    ws = _ws(_GEMM_WS, "esp_gemm_bf16", _GEMM_WS_BYTES, dw.device)
+    if _PROF is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    _native.call("esp_conv2_wgrad_bf16", _p(dz2_16), _p(z1_16), _p(dw), _p(db), B, T1, F1, D, _p(ws), _GEMM_WS_BYTES,
+                 _st())
+    _guard_post("esp_gemm_bf16", ws, _GEMM_WS_BYTES)
+    if _PROF is not None:
+        ev1.record()
+        T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
+        npix = B * T2 * F2
+        _PROF.append((2.0 * D * 9 * D * npix, ev0, ev1, (RC, I2C_RC, D, 9 * D, npix, 1, "bf16"), 0.0))
+
+
 def conv2_dgrad(dz2, W, z1, dz1, B, T1, F1, D, dz2_16=None):
     """Conv2d(D, D, 3, 2) input gradient x conv1 ReLU mask as 4 implicit parity-class GEMMs; dz2_16 (the
     bf16 mode): dz2 as bf16, the class GEMMs on bf16 operands (esp_conv2_dgrad_bf16)."""

@@ -131,6 +131,11 @@ int esp_gemm_bf16(int mode_a, int mode_b, int M, int N, int K, int batch, int nb
  * 9D), fp32 accumulate and output.  D % 64 == 0, 16-B aligned operands. */
 int esp_conv2_fwd_bf16(const void* z1_16, const void* w16, const float* bias, float* z2, int B, int T1, int F1, int D,
                        float* work, long work_bytes, void* stream);
+/* The bf16 mode's conv2 weight gradient: dw (D x 9D, (o, kt, kf, c) order) = dz2^T im2col(z1) and
+ * db += column sums of dz2, on bf16 operands (dz2_16 [pixels][D], z1_16 from esp_conv1_fwd_bf16); an
+ * even pixel count, D % 64 == 0, 16-B aligned; `work` the split-K partials as esp_gemm_f32's. */
+int esp_conv2_wgrad_bf16(const void* dz2_16, const void* z1_16, float* dw, float* db, int B, int T1, int F1, int D,
+                         float* work, long work_bytes, void* stream);
 /* esp_conv2_dgrad with dz2 in bf16 (the bf16 mode): the class GEMMs on bf16 operands (workspace as
  * esp_conv2_dgrad's).  D % 64 == 0. */
 int esp_conv2_dgrad_bf16(const void* dz2_16, const float* W, const float* z1, float* dz1, int B, int T1, int F1, int D,

@@ -768,12 +768,14 @@ def test_conv2_dgrad_parity_classes_vs_column_path(dev, T1, F1):
     assert rel_err(got.cpu(), ref.cpu()) < 1e-5
 
 
-@pytest.mark.parametrize("T1,F1", [(31, 39), (9, 7)])
+@pytest.mark.parametrize("T1,F1", [(31, 39), (9, 7), (33, 40)])
 def test_conv2_bf16_operands_match_staged_rounding(dev, T1, F1):
     """The bf16 mode's conv2 forward (esp_conv2_fwd_bf16: implicit im2col over conv1's bf16 copy of z1,
     bf16 weights, PREC 2) and input gradient (esp_conv2_dgrad_bf16: dz2 and the class weights in bf16)
-    against the same GEMMs on fp32 operands rounded to bf16 in LDS staging (PREC 1): the same bf16
-    products, fp32 accumulation-order differences only.  conv1's bf16 copy is bit-equal to torch's RNE."""
+    and weight gradient (esp_conv2_wgrad_bf16: the gathered im2col B in the bf16 RC image, fused bias
+    gradient) against the same GEMMs on fp32 operands rounded to bf16 in LDS staging (PREC 1): the same
+    bf16 products, fp32 accumulation-order differences only.  conv1's bf16 copy is bit-equal to torch's
+    RNE."""
     B, D = 3, 128
     T, F = 2 * T1 + 1, 2 * F1 + 1
     T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
@@ -799,11 +801,22 @@ def test_conv2_bf16_operands_match_staged_rounding(dev, T1, F1):
         K.conv2_fwd_bf16(z16, K.to_bf16(w2r, D, 9 * D, 9 * D), bias, got, B, T1, F1, D)
         K.conv2_dgrad(dz2, W, z1, dref, B, T1, F1, D)
         K.conv2_dgrad(dz2, W, z1, dgot, B, T1, F1, D, dz2_16=K.to_bf16(dz2, B * T2 * F2, D, D))
+        # weight gradient + fused bias gradient (an even pixel count: B * T2 * F2)
+        npix = B * T2 * F2
+        if npix % 2 == 0:
+            wref, wgot = torch.empty(D, 9 * D, device=dev), torch.empty(D, 9 * D, device=dev)
+            bref, bgot = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
+            K.gemm(D, 9 * D, npix, dz2, z1, wref, mode_a=K.RC, lda=D, mode_b=K.I2C_RC, ldb=0, ldc=9 * D,
+                   ic_b=(T1, F1, D, T2, F2), rowsum=bref)
+            K.conv2_wgrad_bf16(K.to_bf16(dz2, npix, D, D), z16, wgot, bgot, B, T1, F1, D)
     torch.cuda.synchronize()
     assert torch.equal(z16.view(torch.int16), z1.bfloat16().view(torch.int16))
     assert rel_err(got.cpu(), ref.cpu()) < 1e-5
     assert not torch.isnan(dgot).any()
     assert rel_err(dgot.cpu(), dref.cpu()) < 1e-5
+    if npix % 2 == 0:
+        assert rel_err(wgot.cpu(), wref.cpu()) < 1e-5
+        assert rel_err(bgot.cpu(), bref.cpu()) < 1e-5
 
 
 @pytest.mark.parametrize("M,D", [(11968, 512), (3000, 768), (47872, 256)])
