@@ -768,7 +768,7 @@ __global__ __launch_bounds__(256) void relpos_attn_fwd_kernel(
 //   the band block goes to a per-wave 32-position LDS ring; the rel_shift read of tile t,
 //   bd_shift[ii][jj] = band[ii][jj - ii + 15] (offset from block t), touches blocks t and t+1.
 // The next tile's k / p fragments are fetched one tile ahead (64 B contiguous per lane, k order
-// permuted identically in both operands: lane quarter q supplies d = 16q + c at step c).
+// permuted identically in both operands: lane quarter q supplies d = 16 (c / 4) + 4 q + c % 4 at step c).
 // Legacy rel_shift (attention.py:145-165): j <= i reads band rows q_v[i]; j == i+1 is 0;
 // j >= i+2 reads q_v[i+1] . p[j-i-2].  In table positions k = j + T-1-i the first case is k < T,
 // the last k > T with p at k - T - 1, and band block m covers T-16-16g+16m + [0,16) (g = i0/16):
@@ -868,11 +868,15 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
   const float inv_sqrt_dk = 1.0f / sqrt_dk;
   float* ring0 = ring[wave];
 
+  // a lane's 16 values of a row: d = 16 u + 4 q4 + (0..3) for u = 0..3, so each of the four float4
+  // loads covers 64 contiguous bytes of a row across the lane quarter (16 rows x 64 B per instruction;
+  // d = 16 q4 + 0..15 touched 16 rows x 4 separate 16-B pieces).  Any d order serves the MFMAs as long
+  // as q, k and p share it (every operand is loaded here).
   auto ld16 = [&](const float* row, float (&f)[16]) {
-    const float4* r4 = reinterpret_cast<const float4*>(row + 16 * q4);
+    const float4* r4 = reinterpret_cast<const float4*>(row + 4 * q4);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const float4 v = r4[u];
+      const float4 v = r4[4 * u];
       f[4 * u] = v.x; f[4 * u + 1] = v.y; f[4 * u + 2] = v.z; f[4 * u + 3] = v.w;
     }
   };
@@ -937,6 +941,10 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
     // (a conditional tile makes the compiler merge its counts pessimistically: vmcnt(4) at every
     // tile, i.e. the prefetched fragments waited for one tile early)
     {
+      // the fragments DEPTH tiles ahead are requested first, into the buffers the previous tile
+      // released, so a fetch has DEPTH whole tiles of this wave's work to arrive
+      ld16(k_row(t + DEPTH), kb[(tt + DEPTH) % NB]);  // clamped rows: always safe to fetch
+      ld16(p_row(t + 1 + DEPTH), pb[(tt + 1 + DEPTH) % NB]);
       const float(&kf)[16] = kb[tt % NB];
       const float(&pf)[16] = pb[(tt + 1) % NB];
       const bool shifted = LEGACY && t + 1 > g;  // legacy band block t+1 at/above table position T
@@ -958,8 +966,6 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
           s = __builtin_amdgcn_mfma_f32_16x16x4f32(shifted ? av2[c] : av[c], pf[c], s, 0, 0, 0);
         }
       }
-      ld16(k_row(t + DEPTH), kb[(tt + DEPTH) % NB]);  // clamped rows: always safe to fetch
-      ld16(p_row(t + 1 + DEPTH), pb[(tt + 1 + DEPTH) % NB]);
       put_band(ring0, t + 1, s);
       asm volatile("" ::: "memory");  // ring writes before the shifted reads (LDS is in order per wave)
       const int j = t * 16 + li;
@@ -1102,6 +1108,10 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
       asm volatile("" ::: "memory");  // the reads above before the next chunk's writes
     }
   };
+  if (attn == nullptr) {  // diagnostic ablation (ESP_ATTN_ABL=1, timing only): no stores; keep the scores live
+    if (sc[0][0] == 12345.f) attn = pdrop;  // never taken with real data; stops the compiler dropping the work
+    else return;
+  }
   if (pdrop) store_rows(std::true_type{});
   else store_rows(std::false_type{});
 }
@@ -1315,6 +1325,9 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
   if (xs_env < 0) xs_env = getenv("ESP_ATTN_XS") ? atoi(getenv("ESP_ATTN_XS")) : ESP_ATTN_XS_DEFAULT;
   // the bf16 mode computes the scores on bf16 operands like every other product of its step
   const int np = xs_env ? 6 : (esp_get_gemm_compute() == 1 ? 1 : 0);
+  static int abl_env = -1;  // ESP_ATTN_ABL=1: no stores (diagnostic timing only; the output is garbage)
+  if (abl_env < 0) abl_env = getenv("ESP_ATTN_ABL") ? atoi(getenv("ESP_ATTN_ABL")) : 0;
+  if (abl_env == 1) attn = nullptr;
   if (np && !split) {
 #define ESP_RX4(N, P2_, L_, NP_)                                                                                       \
   hipLaunchKernelGGL((relpos_attn_fwd16_kernel<N, P2_, L_, 1, NP_>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p,     \
