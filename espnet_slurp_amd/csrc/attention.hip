@@ -840,7 +840,7 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
     const float* __restrict__ qu, const float* __restrict__ qv, const float* __restrict__ kmat, long ldk,
     const float* __restrict__ pm, long ldpm, int nb, float sqrt_dk, const int* __restrict__ klen,
     float* __restrict__ attn, float* __restrict__ pdrop, uint32_t thr, float dscale, uint64_t seed, int T, long lds,
-    const uint64_t* __restrict__ key, const int* __restrict__ tvalid, int nrb, int Z) {
+    const uint64_t* __restrict__ key, const int* __restrict__ tvalid, int nrb, int Z, int abl) {
   __shared__ float ring[4][RW_ROWS * RW_PITCH];
   __shared__ __attribute__((aligned(16))) float stage[4][RW_ROWS * RW_SPITCH];
   __shared__ float xch[2][4][RW_ROWS];  // SPLIT 2: per-wave row max / row sum partials
@@ -943,8 +943,10 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
     {
       // the fragments DEPTH tiles ahead are requested first, into the buffers the previous tile
       // released, so a fetch has DEPTH whole tiles of this wave's work to arrive
-      ld16(k_row(t + DEPTH), kb[(tt + DEPTH) % NB]);  // clamped rows: always safe to fetch
-      ld16(p_row(t + 1 + DEPTH), pb[(tt + 1 + DEPTH) % NB]);
+      if (!(abl & 4)) {  // (4: no per-tile fragment fetch -- stale fragments; diagnostic timing only)
+        ld16(k_row(t + DEPTH), kb[(tt + DEPTH) % NB]);  // clamped rows: always safe to fetch
+        ld16(p_row(t + 1 + DEPTH), pb[(tt + 1 + DEPTH) % NB]);
+      }
       const float(&kf)[16] = kb[tt % NB];
       const float(&pf)[16] = pb[(tt + 1) % NB];
       const bool shifted = LEGACY && t + 1 > g;  // legacy band block t+1 at/above table position T
@@ -966,7 +968,8 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
           s = __builtin_amdgcn_mfma_f32_16x16x4f32(shifted ? av2[c] : av[c], pf[c], s, 0, 0, 0);
         }
       }
-      put_band(ring0, t + 1, s);
+      if (!(abl & 2)) put_band(ring0, t + 1, s);
+      else if (s[0] == 12345.f) a[0] += 1.f;  // (diagnostic: no ring; keeps the band MFMAs live)
       asm volatile("" ::: "memory");  // ring writes before the shifted reads (LDS is in order per wave)
       const int j = t * 16 + li;
       // the four shifted band reads first, then their uses: one LDS round trip per tile (reads
@@ -975,7 +978,7 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int ii = 4 * q4 + r;
-        bdv[r] = ring0[ii * RW_PITCH + ((t * 16 + li - ii + 15) & 31)];
+        bdv[r] = (abl & 2) ? 0.f : ring0[ii * RW_PITCH + ((t * 16 + li - ii + 15) & 31)];
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -1327,11 +1330,11 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
   const int np = xs_env ? 6 : (esp_get_gemm_compute() == 1 ? 1 : 0);
   static int abl_env = -1;  // ESP_ATTN_ABL=1: no stores (diagnostic timing only; the output is garbage)
   if (abl_env < 0) abl_env = getenv("ESP_ATTN_ABL") ? atoi(getenv("ESP_ATTN_ABL")) : 0;
-  if (abl_env == 1) attn = nullptr;
+  if (abl_env & 1) attn = nullptr;  // (2: no rel_shift ring -- bd = 0; diagnostic timing only)
   if (np && !split) {
 #define ESP_RX4(N, P2_, L_, NP_)                                                                                       \
   hipLaunchKernelGGL((relpos_attn_fwd16_kernel<N, P2_, L_, 1, NP_>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p,     \
-                     ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid, nrb, Zn)
+                     ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid, nrb, Zn, abl_env)
 #define ESP_RX3(N, P2_, L_)              \
   do {                                   \
     if (np == 6) ESP_RX4(N, P2_, L_, 6); \
@@ -1356,7 +1359,7 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
       grid.x = (unsigned)(8 * ((Zn + 7) / 8) * nrb);
 #define ESP_RL(P2_, NP_)                                                                                               \
   hipLaunchKernelGGL((relpos_attn_fwd16_kernel<16, P2_, true, 2, NP_>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p,   \
-                     ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid, nrb, Zn)
+                     ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid, nrb, Zn, abl_env)
       if (np == 6) {
         if (p2) ESP_RL(true, 6);
         else ESP_RL(false, 6);
@@ -1376,7 +1379,7 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
   if (split) {
 #define ESP_RS3(N, P2_, L_)                                                                                            \
   hipLaunchKernelGGL((relpos_attn_fwd16_kernel<N, P2_, L_, 2>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p, ldp_row, \
-                     nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid, nrb, Zn)
+                     nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid, nrb, Zn, abl_env)
 #define ESP_RS(N)                     \
   do {                                \
     if (relpos == 2) {                \
@@ -1398,7 +1401,7 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
   }
 #define ESP_RW3(N, P2_, L_)                                                                                         \
   hipLaunchKernelGGL((relpos_attn_fwd16_kernel<N, P2_, L_>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p, ldp_row, \
-                     nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid, nrb, Zn)
+                     nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid, nrb, Zn, abl_env)
 #define ESP_RW(N)                             \
   do {                                        \
     if (relpos == 2) {                        \
