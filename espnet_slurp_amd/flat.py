@@ -7,7 +7,9 @@ buffers in a single launch each, and the data-parallel all-reduce works on large
 contiguous buckets of the flat gradient (train/distributed.py).  The parameter objects
 themselves are the reference's (same names, shapes and state_dict keys).
 
-Each slot starts at a multiple of 4 floats (16 B) so float4 accesses stay aligned.
+Each slot starts at a multiple of 8 floats (32 B): float4 accesses stay aligned, and a slot's
+element offset is a multiple of 8, so the per-step bf16 copy / bf16 split planes of the WHOLE flat
+buffer (kernels.flat_cast: one launch per step) hold every weight's copy at a 16-B aligned address.
 Attention projections are laid out q|k|v consecutively (weights, then biases) so that
 the fused QKV (and decoder KV) GEMMs read one (3D, D) weight view.
 """
@@ -23,6 +25,10 @@ from torch import nn
 
 def _align4(n: int) -> int:
     return (n + 3) // 4 * 4
+
+
+def _align8(n: int) -> int:
+    return (n + 7) // 8 * 8
 
 
 def ordered_parameters(model: nn.Module) -> List[Tuple[str, nn.Parameter]]:
@@ -53,7 +59,7 @@ class FlatParams:
         off = 0
         for _, p in self.params:
             self.slots[id(p)] = (off, p.numel())
-            off += _align4(p.numel())
+            off += _align8(p.numel())
         self.numel = off
         self.flat = torch.zeros(off, dtype=torch.float32, device=device)
         K.register_param_storage(self.flat)  # bf16 weight copies cached per training step (kernels)
@@ -92,7 +98,7 @@ class FlatParams:
         end = o0 + n0
         for p in plist[1:]:
             o, n = self.slots[id(p)]
-            assert o == _align4(end) and _align4(end) == end, "parameters are not adjacent"
+            assert o == _align8(end) and _align8(end) == end, "parameters are not adjacent"
             end = o + n
         return o0, end - o0
 

@@ -286,9 +286,57 @@ def planes_mode() -> int:
     return 3 if _F32_PRODUCTS[0] == 6 and _XPLANES in ("1", True) else 0
 
 
+# Inside param_cast_scope, a parameter's bf16 copy / split planes are views into ONE copy of the whole
+# flat parameter buffer made by one launch at its first use in the step (the FlatParams slots are
+# 8-float aligned, so every weight's copy starts 16-B aligned): 155 per-weight launches per C2 step
+# become one.  ESP_FLAT_CAST=0: per-weight copies (A/B measurements).
+_FLAT_CAST = os.environ.get("ESP_FLAT_CAST", "1") == "1"
+
+
+def _param_flat(ptr: int, nbytes: int):
+    """(flat tensor, its base address) of the registered parameter storage holding [ptr, ptr + nbytes)."""
+    for r, a, b in _PARAM_RANGES:
+        t = r()
+        if t is not None and a <= ptr and ptr + nbytes <= b:
+            return t, a
+    return None
+
+
+def _flat_view(kind: str, X, off: int, rows: int, cols: int, ld: int, wc):
+    """(copy, element offset, flat numel) of a parameter matrix in the step's whole-flat copy (kind
+    'bf16': esp_f32_to_bf16; 'planes': esp_f32_to_planes), or None when it does not qualify."""
+    if not _FLAT_CAST or wc is None or ld != cols or cols % 8:
+        return None
+    ptr = X.data_ptr() + off * 4
+    pf = _param_flat(ptr, ((rows - 1) * ld + cols) * 4)
+    if pf is None:
+        return None
+    flat, base = pf
+    e = (ptr - base) // 4
+    n = flat.numel()
+    if e % 8 or n % 8 or not flat.is_contiguous():
+        return None
+    key = ("flat", kind, base, n, torch.cuda.is_current_stream_capturing())
+    hit = wc.get(key)
+    if hit is None:
+        if kind == "bf16":
+            out = torch.empty(n, dtype=torch.bfloat16, device=flat.device)
+            _native.call("esp_f32_to_bf16", _p(flat), _p(out), 1, n, n, n, 0, _st())
+        else:
+            out = torch.empty(3 * n, dtype=torch.bfloat16, device=flat.device)
+            _native.call("esp_f32_to_planes", _p(flat), _p(out), 1, n, n, n, n, _st())
+        hit = (out, flat)
+        wc[key] = hit
+    return hit[0], e, n
+
+
 def planes(X, off: int, rows: int, cols: int, ld: int):
     """(planes, ldp, pstride): the three bf16 planes (esp_f32_to_planes) of the rows x cols fp32
     matrix at X[off] with row pitch ld; plane row pitch ldp = cols rounded up to 8."""
+    fv = _flat_view("planes", X, off, rows, cols, ld, _WP[0])
+    if fv is not None:  # (a parameter: a view into the step's planes of the whole flat buffer)
+        buf, e, n = fv
+        return buf[e:], cols, n
     key = (X.data_ptr() + off * 4, rows, cols, ld, torch.cuda.is_current_stream_capturing())
     wc = _WP[0]
     if wc is not None:
@@ -326,6 +374,10 @@ def _bf16_copy(X, off: int, rows: int, cols: int, ld: int, role: str = "") -> to
         # the graph: entries are per capture state
         ckey = key + (torch.cuda.is_current_stream_capturing(),)
         param = _is_param(key[0], ((rows - 1) * ld + cols) * 4)
+        if param:
+            fv = _flat_view("bf16", X, off, rows, cols, ld, wc)
+            if fv is not None:  # (a view into the step's bf16 copy of the whole flat buffer)
+                return fv[0][fv[1]:], cols
         if param or role == "b_rc":
             hit = wc.get(ckey)
             if hit is not None:

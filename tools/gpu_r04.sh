@@ -2,8 +2,8 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 bash gpurun_steps.sh \
-  "timeout -k 10 120 python -u tools/attn_kernels_bench.py 128 --only probs > gpurun_out/attn_a0.log 2>&1" \
-  "ESP_ATTN_ABL=1 timeout -k 10 120 python -u tools/attn_kernels_bench.py 128 --only probs > gpurun_out/attn_a1.log 2>&1" \
-  "ESP_ATTN_ABL=5 timeout -k 10 120 python -u tools/attn_kernels_bench.py 128 --only probs > gpurun_out/attn_a5.log 2>&1" \
-  "ESP_ATTN_ABL=4 timeout -k 10 120 python -u tools/attn_kernels_bench.py 128 --only probs > gpurun_out/attn_a4.log 2>&1" \
-  "ESP_ATTN_XS=1 ESP_ATTN_ABL=5 timeout -k 10 120 python -u tools/attn_kernels_bench.py 128 --only probs > gpurun_out/attn_a5xs.log 2>&1"
+  "timeout -k 10 900 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_model.py tests/test_gpu_fullsize.py tests/test_gpu_bf16.py tests/test_gpu_graph.py tests/test_gpu_trainer.py -x -q --timeout 170 --timeout-method thread > gpurun_out/pytest_flat.log 2>&1" \
+  "timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/b_flat1.log 2>&1" \
+  "ESP_FLAT_CAST=0 timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/b_flat0.log 2>&1" \
+  "timeout -k 10 300 python -u bench.py --config c5 --batch 64 --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/b5_flat1.log 2>&1" \
+  "ESP_FLAT_CAST=0 timeout -k 10 300 python -u bench.py --config c5 --batch 64 --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/b5_flat0.log 2>&1"
