@@ -215,6 +215,9 @@ def test_flat_parameters_views_and_qkv_adjacency():
     assert torch.equal(w[:64], att.linear_q.weight) and torch.equal(w[128:], att.linear_v.weight)
     m.load_state_dict(O.deterministic_params(small_cfg("latest"), 1))
     assert torch.equal(f.view(att.linear_k.weight), att.linear_k.weight)
+    # every slot starts 8-float aligned (the whole-flat bf16 copy / planes keep each weight 16-B
+    # aligned, kernels._flat_view) and the flat length is a multiple of 8
+    assert all(o % 8 == 0 for o, _ in f.slots.values()) and f.numel % 8 == 0
 
 
 def test_subsampled_lengths_and_sos_eos():
