@@ -205,44 +205,55 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
   }
 }
 
-// out[c] (+)= sum_{p<nb} part[p*stride + c]   for c < N.  Block = 64 columns x 16 row
-// groups (1024 threads); each group sums rows g, g+16, ...; groups combined in fixed order.
+// out[c] (+)= sum_{p<nb} part[p*stride + c]   for c < N.  Block = 16 columns x 64 row groups (1024
+// threads, grid N / 16: 4x the blocks of a 64-column block, each thread a quarter of the rows); a
+// group sums rows g, g+64, ... into four interleaved accumulators (four loads in flight), combined in
+// fixed order, then the 64 groups in fixed order (deterministic).  These are ~10-us latency-bound
+// launches (80 + 48 per C2 step): with 64-column blocks a thread walked nb/16 dependent loads.
+constexpr int FC_COLS = 16, FC_GROUPS = 64;
+template <typename T>
+__device__ __forceinline__ T fc_sum_rows(const T* __restrict__ part, int nb, long stride, int c, int g) {
+  T s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  int p = g;
+  for (; p + 3 * FC_GROUPS < nb; p += 4 * FC_GROUPS) {
+    s0 += part[(long)p * stride + c];
+    s1 += part[(long)(p + FC_GROUPS) * stride + c];
+    s2 += part[(long)(p + 2 * FC_GROUPS) * stride + c];
+    s3 += part[(long)(p + 3 * FC_GROUPS) * stride + c];
+  }
+  for (; p < nb; p += FC_GROUPS) s0 += part[(long)p * stride + c];
+  return (s0 + s1) + (s2 + s3);
+}
+template <typename T>
+__device__ __forceinline__ T fc_block_sum(T s, int cl, int g, T (&sh)[FC_GROUPS][FC_COLS]) {
+  sh[g][cl] = s;
+  __syncthreads();
+  T t = 0;
+  if (g == 0)
+    for (int k = 0; k < FC_GROUPS; ++k) t += sh[k][cl];
+  return t;
+}
+
 template <typename T>
 __global__ __launch_bounds__(1024) void finalize_cols_kernel(const T* __restrict__ part, int nb, long stride, int N,
                                                              float* __restrict__ out, int accumulate) {
-  __shared__ T sh[16][64];
-  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  T s = 0;
-  if (c < N) {
-#pragma unroll 4
-    for (int p = g; p < nb; p += 16) s += part[(long)p * stride + c];
-  }
-  sh[g][cl] = s;
-  __syncthreads();
-  if (g == 0 && c < N) {
-    T t = 0;
-    for (int k = 0; k < 16; ++k) t += sh[k][cl];
-    out[c] = accumulate ? out[c] + (float)t : (float)t;
-  }
+  __shared__ T sh[FC_GROUPS][FC_COLS];
+  const int cl = threadIdx.x % FC_COLS, g = threadIdx.x / FC_COLS;
+  const int c = blockIdx.x * FC_COLS + cl;
+  const T s = c < N ? fc_sum_rows(part, nb, stride, c, g) : (T)0;
+  const T t = fc_block_sum(s, cl, g, sh);
+  if (g == 0 && c < N) out[c] = accumulate ? out[c] + (float)t : (float)t;
 }
 
 // the same over 2*D columns of [nb][2D] partials, accumulated into out0 (c < D) / out1 (c >= D)
 __global__ __launch_bounds__(1024) void finalize_cols2_kernel(const float* __restrict__ part, int nb, long stride, int D,
                                                               float* __restrict__ out0, float* __restrict__ out1) {
-  __shared__ float sh[16][64];
-  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
-  float s = 0.f;
-  if (c < 2 * D) {
-#pragma unroll 4
-    for (int p = g; p < nb; p += 16) s += part[(long)p * stride + c];
-  }
-  sh[g][cl] = s;
-  __syncthreads();
+  __shared__ float sh[FC_GROUPS][FC_COLS];
+  const int cl = threadIdx.x % FC_COLS, g = threadIdx.x / FC_COLS;
+  const int c = blockIdx.x * FC_COLS + cl;
+  const float s = c < 2 * D ? fc_sum_rows(part, nb, stride, c, g) : 0.f;
+  const float t = fc_block_sum(s, cl, g, sh);
   if (g == 0 && c < 2 * D) {
-    float t = 0.f;
-    for (int k = 0; k < 16; ++k) t += sh[k][cl];
     if (c < D) out0[c] += t;
     else out1[c - D] += t;
   }
@@ -802,7 +813,7 @@ inline int rows_per_block(int M) {
   int r = (M + BN_CHUNKS - 1) / BN_CHUNKS;
   return r < 8 ? 8 : r;
 }
-inline dim3 fin_grid(int N) { return dim3((N + 63) / 64); }
+inline dim3 fin_grid(int N) { return dim3((N + FC_COLS - 1) / FC_COLS); }
 inline dim3 bnf_grid(int D) { return dim3((D + BNF_COLS - 1) / BNF_COLS); }
 
 }  // namespace
