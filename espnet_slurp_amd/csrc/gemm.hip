@@ -181,7 +181,7 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
   GldsArgs x{};
   if (MA == I2CT_KC) x = *tconv;  // the transposed-conv gather parameters
   x.ntx = (g.N + BNT - 1) / BNT;
-  const int bm = g.bm == 64 ? 64 : BM;
+  const int bm = g.bm == 64 || g.bm == 256 ? g.bm : BM;
   x.nty = (g.M + bm - 1) / bm;
   if (MA == I2C_KC) {
     x.c_a = make_fastdiv(g.a.ic.C);
@@ -650,6 +650,11 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
     // gathered-B re-reads and split-K refills the chip (8.39 vs 9.22 ms at C2 B=128,
     // tools/gemm_bench.py with ESP_GEMM_BNT; the K ~ 48k linear weight gradients keep 128x64)
     if (mode_b == I2C_RC && work && K >= 65536) g.bnt = 128;
+    // 256 x 128 tiles for the bf16-operand GEMMs (ESP_GEMM_BM256=1, A/B measurements): twice the
+    // MFMA work per staged byte of the 128 x 128 tile, whose k-loop is load-bound at bf16 rates
+    static int bm256 = -1;
+    if (bm256 < 0) bm256 = getenv("ESP_GEMM_BM256") ? atoi(getenv("ESP_GEMM_BM256")) : 0;
+    if (bm256 && g.bf16 == 2 && g.bnt == 128 && mode_a <= RC && mode_b <= RC && !smb && M >= 4096) g.bm = 256;
     static int force_bnt = -1;  // ESP_GEMM_BNT=64|128: tile width override (diagnostics)
     if (force_bnt < 0) force_bnt = getenv("ESP_GEMM_BNT") ? atoi(getenv("ESP_GEMM_BNT")) : 0;
     if ((force_bnt == 64 || force_bnt == 128) && N > 64 && g.bf16 != 5) g.bnt = force_bnt;
@@ -661,7 +666,7 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
       const long by_k = K / 128;  // keep >= 8 slabs of BK per split
       if (sp > by_k) sp = by_k;
       // in-kernel combine (LDS-DMA kernel): partials on whole tiles + tickets in the last 64 KB
-      const int bmt = g.bm == 64 ? 64 : BM;
+      const int bmt = g.bm == 64 || g.bm == 256 ? g.bm : BM;
       const long mp = (long)(M + bmt - 1) / bmt * bmt, np = g.bnt ? (long)(N + g.bnt - 1) / g.bnt * g.bnt : N;
       // opt-in (ESP_SPLITK_INKERNEL=1): measured slower at C2 B=128 -- the last-arriving unit of a
       // tile sums all of its splits alone (64 splits x 32 KB behind 8 tiles for the d x d weight

@@ -1645,7 +1645,8 @@ constexpr int glds_lds_bytes(int BNT, int BMT, int PREC) {
 }
 template <int BNT, int EPI, int BMT = BM, int PREC = 0>
 constexpr int glds_occupancy() {
-  constexpr int by_regs = BMT == 64 ? 4 : (BNT == 64 && (EPI == EPI_PLAIN || EPI >= EPI_BIAS)) ? 3 : 2;
+  // (256 x 128 bf16 tiles: 96 KB of LDS, one block -- one wave per SIMD -- per CU)
+  constexpr int by_regs = BMT == 256 ? 1 : BMT == 64 ? 4 : (BNT == 64 && (EPI == EPI_PLAIN || EPI >= EPI_BIAS)) ? 3 : 2;
   constexpr int by_lds = 163840 / glds_lds_bytes(BNT, BMT, PREC);
   return by_regs < by_lds ? by_regs : by_lds;
 }
@@ -1687,7 +1688,8 @@ __device__ __forceinline__ void split3_bf16(const float* v, bf16x8& hi, bf16x8& 
 template <int MA, int MB, int BNT, bool RS, int EPI, int PREC = 0, int BMT = BM>
 __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void gemm_glds_kernel(GemmArgs g, GldsArgs x) {
   constexpr int WN = BMT == 64 ? 2 : BNT / 64, WM = 4 / WN, TM = BMT / (WM * 32), TN = BNT / (WN * 32);
-  static_assert(BMT == 128 || BNT == 64, "64-row tiles are 64 wide");
+  static_assert(BMT == 128 || (BMT == 64 && BNT == 64) || (BMT == 256 && BNT == 128 && PREC == 2),
+                "64-row tiles are 64 wide; 256-row tiles: 128 wide, bf16 operands");
   static_assert(PREC < 3 || MB == KC || MB == RC, "B planes: KC / RC operands");
   static_assert(PREC != 5 || MA == KC || MA == RC, "A planes: KC / RC operands");
   constexpr bool BP = PREC >= 3;                 // B as three bf16 planes (StageP)
@@ -2147,6 +2149,15 @@ bool glds_switch(int ma, int mb, int bnt, int prec, int bm, F&& f) {
       }
       return false;
     }
+    if (bm == 256) {  // 256 x 128 tiles: bf16 operands (PREC 2), KC / RC pairs
+      if constexpr (small_ok) {
+        if (bnt == 128 && prec == 2) {
+          f(A, B, IC<128>{}, IC<2>{}, IC<256>{});
+          return true;
+        }
+      }
+      return false;
+    }
     return bnt == 64 ? by_prec(IC<64>{}, IC<BM>{}) : by_prec(IC<128>{}, IC<BM>{});
   };
   switch (ma * 8 + mb) {
@@ -2178,8 +2189,8 @@ bool glds_launch_pspec(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hi
                        const GldsArgs& x);
 // resident blocks per CU of a launch (host side)
 inline int glds_occupancy_rt(int bnt, int epi, int bm, int prec) {
-  const int by_regs = bm == 64 ? 4 : (bnt == 64 && (epi == EPI_PLAIN || epi >= EPI_BIAS)) ? 3 : 2;
-  const int by_lds = 163840 / glds_lds_bytes(bnt, bm == 64 ? 64 : BM, prec);
+  const int by_regs = bm == 256 ? 1 : bm == 64 ? 4 : (bnt == 64 && (epi == EPI_PLAIN || epi >= EPI_BIAS)) ? 3 : 2;
+  const int by_lds = 163840 / glds_lds_bytes(bnt, bm == 64 || bm == 256 ? bm : BM, prec);
   return std::min(by_regs, by_lds);
 }
 
