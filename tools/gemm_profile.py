@@ -17,6 +17,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--config", choices=sorted(bench.PRESETS), default="c2")
+    ap.add_argument("--order", default=None,
+                    help="write the profiled step's GEMM launches in launch order (flops + shape key per line) "
+                         "for tools/gemm_shapes_trace.py")
     a = ap.parse_args()
     d, heads, ff, layers, amp = bench.PRESETS[a.config]
     args = argparse.Namespace(d=d, heads=heads, ff=ff, layers=layers, vocab=600, rel_pos="latest", batch=a.batch)
@@ -29,6 +32,7 @@ def main():
     tr.train_one_step(batch)
     torch.cuda.synchronize()
     K.profile_gemm_start()
+    launches = K._PROF  # (the list profile_gemm_stop consumes; entries in launch order)
     t0 = torch.cuda.Event(enable_timing=True)
     t1 = torch.cuda.Event(enable_timing=True)
     t0.record()
@@ -36,6 +40,10 @@ def main():
     t1.record()
     flops, ms, n, shapes = K.profile_gemm_stop(by_shape=True)
     step_ms = t0.elapsed_time(t1)
+    if a.order:
+        with open(a.order, "w") as f:
+            for fl, ev0, ev1, key, _extra in launches:
+                f.write(f"{fl:.0f}\t{ev0.elapsed_time(ev1):.6f}\t{key!r}\n")
     print(f"step {step_ms:.1f} ms, gemm {ms:.1f} ms in {n} launches, {flops / ms / 1e9:.1f} TFLOP/s")
     rows = sorted(shapes.items(), key=lambda kv: -kv[1][1])
     for key, (cnt, t, f, _extra) in rows[:40]:
