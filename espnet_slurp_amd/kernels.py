@@ -433,7 +433,7 @@ def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc
     if isinstance(A, Planes) or isinstance(B, Planes) or isinstance(C, Planes):
         return _gemm_planes(M, N, K, A, B, C, mode_a, lda, mode_b, ldb, ldc, a_off, b_off, c_off, bias, alpha,
                             beta, R, r_off, act, aux, drop_p, seed, bwd_act, pre, rowsum, b_weight, batch, nb2, sa,
-                            sb, sc)
+                            sb, sc, keep_a=_keep_a16)
     if (_COMPUTE[0] == GEMM_BF16 and _AMP_BF16_OPERANDS and batch == 1 and mode_a in (KC, RC)
             and mode_b in (KC, RC) and ic_a is None and ic_b is None and M > 0 and N > 0):
         if _gemm_amp_operands(M, N, K, A, B, C, mode_a, lda, mode_b, ldb, ldc, a_off, b_off, c_off, bias, alpha,
@@ -479,13 +479,21 @@ def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc
         _PROF.append((2.0 * M * N * K * batch, ev0, ev1, key, extra))
 
 
+# ESP_PLANES_DY_MEMO=0: the planes path casts a weight gradient's dy again for the input gradient
+# (A/B measurements)
+_PLANES_DY_MEMO = os.environ.get("ESP_PLANES_DY_MEMO", "1") == "1"
+
+
 def _gemm_planes(M, N, K, A, B, C, mode_a, lda, mode_b, ldb, ldc, a_off, b_off, c_off, bias, alpha, beta, R, r_off,
                  act, aux, drop_p, seed, bwd_act, pre, rowsum, b_weight, batch=1, nb2=1, sa=(0, 0), sb=(0, 0),
-                 sc=(0, 0)):
+                 sc=(0, 0), keep_a=False):
     """gemm() with an operand given as Planes (KC / RC; unbatched planes operands) or C written as
     Planes (fp32 mode: the plain and FFN w_1 epilogues): esp_gemm_f32_pl in the fp32 mode (the other
     operand's planes from the step cache when it is a weight, else split here), the hi planes as bf16
-    operands in the reduced-precision mode (esp_gemm_bf16)."""
+    operands in the reduced-precision mode (esp_gemm_bf16).  keep_a: a weight gradient's fp32 dy, whose
+    bf16 copy is handed to the input-gradient GEMM that follows (_DY16), as in _gemm_amp_operands -- the
+    fused q / k / v projections' dqkv beside their LayerNorm output's planes were cast twice."""
+    memo = _DY16[0]
     _DY16[0] = None
     assert mode_a in (KC, RC) and mode_b in (KC, RC), (mode_a, mode_b)
     for X, off in ((A, a_off), (B, b_off)):
@@ -531,12 +539,16 @@ def _gemm_planes(M, N, K, A, B, C, mode_a, lda, mode_b, ldb, ldc, a_off, b_off, 
             return
     assert batch == 1, "planes operands: unbatched GEMMs"
     if amp:
-        def b16(X, off, rows, cols, ld, role=""):
+        def b16(X, off, rows, cols, ld, role="", m=None):
             if isinstance(X, Planes):
                 return X.buf, X.ld
+            _DY16[0] = m  # (A only: _bf16_copy hands the memo's copy over when it names this region)
             return _bf16_copy(X, off, rows, cols, ld, role)
-        A16, la = b16(A, a_off, M, K, lda, "a_kc") if mode_a == KC else b16(A, a_off, K, M, lda)
+        A16, la = b16(A, a_off, M, K, lda, "a_kc", memo) if mode_a == KC else b16(A, a_off, K, M, lda, "", memo)
         B16, lb = b16(B, b_off, N, K, ldb) if mode_b == KC else b16(B, b_off, K, N, ldb, "b_rc")
+        _DY16[0] = None
+        if keep_a and _PLANES_DY_MEMO and not isinstance(A, Planes):  # (holding A, as _gemm_amp_operands)
+            _DY16[0] = ((A.data_ptr() + a_off * 4, K, M, lda), A16, la, A)
         ws = _ws(_GEMM_WS, "esp_gemm_bf16", _GEMM_WS_BYTES, C.device)
         if _PROF is not None:
             ev0 = torch.cuda.Event(enable_timing=True)
