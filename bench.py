@@ -207,8 +207,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     # B per GPU ("tune; report B"): measured at C2 64 -> 848, 96 -> 875, 128 -> 906,
-    # 192 -> 917, 256 -> 932 utt/s (profiles/r01g_batch_sweep.txt); 128 keeps the 8-GPU global batch at 1024
-    ap.add_argument("--batch", type=int, default=128, help="utterances per GPU")
+    # 192 -> 917, 256 -> 932 utt/s in round 1 (profiles/r01g_batch_sweep.txt); at the round-4 HEAD on one
+    # box 128 -> 1299, 192 -> 1297, 256 -> 1342 (profiles/r04i_batch_sweep.txt).  256 (8-GPU global
+    # batch 2048); tests/test_gpu_bench_shape.py checks B=128 against the oracle and B=256 against B=128
+    ap.add_argument("--batch", type=int, default=256, help="utterances per GPU")
     ap.add_argument("--d", type=int, default=256)
     ap.add_argument("--heads", type=int, default=4)
     ap.add_argument("--ff", type=int, default=1024)

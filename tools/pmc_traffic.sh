@@ -7,5 +7,5 @@ rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
 bash gpurun_steps.sh \
  "timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run -- python3 bench.py --eager --steps 1 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/pmc_fetch.log 2>&1" \
  "timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run -- python3 bench.py --eager --steps 1 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/pmc_write.log 2>&1" || exit $?
-python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write ${META:-128 C2 256,12,0} > gpurun_out/gemm_traffic${TAG:+_$TAG}.json 2>&1
+python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write ${META:-256 C2 256,12,0} > gpurun_out/gemm_traffic${TAG:+_$TAG}.json 2>&1
 rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
