@@ -131,6 +131,16 @@ int splitk_mode() {
   return g_splitk;
 }
 
+// smallest K a split-K split keeps (ESP_SPLITK_MINK, A/B measurements; 128 before round 4's end)
+long g_splitk_mink = -1;
+long splitk_mink() {
+  if (g_splitk_mink < 0) {
+    const char* e = getenv("ESP_SPLITK_MINK");
+    g_splitk_mink = e && atol(e) >= 32 ? atol(e) : 256;
+  }
+  return g_splitk_mink;
+}
+
 // ESP_GEMM_VARIANT != 4 forces the register-staged fallback kernel (diagnostics)
 int g_variant = -1;
 int variant() {
@@ -631,7 +641,7 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
       // (bf16 operands, PREC 2: a weight gradient's split-K grid is priced by its total work too -- the
       // 128-wide tiles halve its B re-reads, which bound the bf16 k-loop: C5 (1,1,2048,512,23936)
       // 2.50 -> 2.03 ms, (1,1,512,2048,23936) 2.34 -> 1.79, r04 ESP_GEMM_BNT=128 A/B)
-      if ((split_f32 || (g.bf16 == 2 && mode_a == RC && mode_b == RC)) && work && t < target && K >= 2 * 128)
+      if ((split_f32 || (g.bf16 == 2 && mode_a == RC && mode_b == RC)) && work && t < target && K >= 2 * (t >= 64 ? splitk_mink() : 128))
         return (double)t * per / 256.0;
       double c = (double)((t + 255) / 256) * per;
       if (t < 2 * 256) c *= 1.3;
@@ -661,9 +671,15 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
   }
   {
     const long tiles = ntiles(g.bnt ? g.bnt : BN, g.bm);
-    if (work && tiles < target && K >= 2 * 128) {
+    // each split keeps >= splitk_mink() of K on grids of >= 64 tiles: the reduction launch (~8-10 us)
+    // outweighs halving a K = 256 k-loop (the decoder's M = 5248 shapes: 24.8 -> 17.5 and 12.6 us,
+    // profiles/r04j_ vs r04l_gemm_shapes_trace_b128.txt); a grid of a few tiles (the d x d weight
+    // gradients over K = 747 / 5248 rows: 8 tiles) needs the splits to fill the chip (19.7 -> 31 us
+    // and 21 -> 26 us with 256), so it keeps 128
+    const long mink = tiles >= 64 ? splitk_mink() : 128;
+    if (work && tiles < target && K >= 2 * mink) {
       long sp = (target + tiles - 1) / tiles;
-      const long by_k = K / 128;  // keep >= 8 slabs of BK per split
+      const long by_k = K / mink;
       if (sp > by_k) sp = by_k;
       // in-kernel combine (LDS-DMA kernel): partials on whole tiles + tickets in the last 64 KB
       const int bmt = g.bm == 64 || g.bm == 256 ? g.bm : BM;
