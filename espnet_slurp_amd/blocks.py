@@ -46,6 +46,11 @@ def empty(*shape, like: torch.Tensor):
     return torch.empty(*shape, dtype=torch.float32, device=like.device)
 
 
+def _bpl(pl):
+    """gemm(b_planes=...) of a kernels.Planes (n = 3) holding B's whole source matrix, or None."""
+    return (pl.buf, pl.ld, pl.ps) if pl is not None else None
+
+
 def grad_buf(dout):
     """The buffer of a branch gradient that only the branch's weight- and input-gradient GEMMs read:
     kernels.Planes in the fp32 mode (the GEMMs then split nothing), else fp32 like dout."""
@@ -245,14 +250,20 @@ class RelPositionMultiHeadedAttention(nn.Module):
         # score-gradient epilogue, ESP_ATTN_DSCORES, reads it in fp32)
         npl = K.planes_mode() if D % 8 == 0 and not K.ATTN_DSCORES else 0
         ctx_ = K.Planes(M, D, x2d.device, npl) if npl else empty(M, D, like=x2d)
+        # qkv and p as split planes for the batched contractions that take them as B (ESP_ATTN_BPLANES)
+        qkv_pl = p_pl = None
+        if K.attn_bplanes_ok(D):
+            qkv_pl, p_pl = K.Planes.of(qkv), K.Planes.of(p)
         K.gemm(T, dk, T, pv, qkv, ctx_, mode_a=K.KC, lda=Tp, mode_b=K.RC, ldb=3 * D, ldc=D, b_off=2 * D,
-               batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * 3 * D), sc=(dk, T * D))
+               batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * 3 * D), sc=(dk, T * D),
+               b_planes=_bpl(qkv_pl))
         out = empty(M, D, like=x2d)
         pr = p_res if training else 0.0
         so = seeds.next()
         self.linear_out.fwd(ctx_, out, drop_p=pr, seed=so, R=resid, beta=1.0)
         return out, Ctx(x=x2d, qkv=qkv, p=p, pos=pos_emb, q_u=q_u, q_v=q_v, attn=attn, pv=pv, ctx=ctx_,
-                        flash=False, pa=pa, sa=sa, pr=pr, so=so, B=B, T=T, P=P, tvalid=tv)
+                        flash=False, pa=pa, sa=sa, pr=pr, so=so, B=B, T=T, P=P, tvalid=tv, qkv_pl=qkv_pl,
+                        p_pl=p_pl)
 
     def bwd(self, c, dout):
         H, dk = self.h, self.d_k
@@ -285,7 +296,8 @@ class RelPositionMultiHeadedAttention(nn.Module):
                               v_off=2 * D)
         else:  # dP = dctx v^T  (into a (Z,T,T) buffer)
             K.gemm(T, T, dk, dctx, c.qkv, dS, mode_a=K.KC, lda=D, mode_b=K.KC, ldb=3 * D, ldc=Tp, b_off=2 * D,
-                   batch=Z, nb2=B, sa=(dk, T * D), sb=(dk, T * 3 * D), sc=(B * T * Tp, T * Tp))
+                   batch=Z, nb2=B, sa=(dk, T * D), sb=(dk, T * 3 * D), sc=(B * T * Tp, T * Tp),
+                   b_planes=_bpl(c.qkv_pl))
         # dV = pv^T dctx -> dqkv[:, 2D:3D]
         K.gemm(T, dk, T, c.pv, dctx, dqkv, mode_a=K.RC, lda=Tp, mode_b=K.RC, ldb=D, ldc=3 * D, c_off=2 * D,
                batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * D), sc=(dk, T * 3 * D))
@@ -296,7 +308,8 @@ class RelPositionMultiHeadedAttention(nn.Module):
                                       tvalid=c.tvalid)
         # dq_u = dS k -> dqkv[:, 0:D]
         K.gemm(T, dk, T, dS, c.qkv, dqkv, mode_a=K.KC, lda=Tp, mode_b=K.RC, ldb=3 * D, ldc=3 * D, b_off=D,
-               batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * 3 * D), sc=(dk, T * 3 * D))
+               batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * 3 * D), sc=(dk, T * 3 * D),
+               b_planes=_bpl(c.qkv_pl))
         # dk = dS^T q_u -> dqkv[:, D:2D]
         K.gemm(T, dk, T, dS, c.q_u, dqkv, mode_a=K.RC, lda=Tp, mode_b=K.RC, ldb=dk, ldc=3 * D, c_off=D,
                batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(B * T * dk, T * dk), sc=(dk, T * 3 * D))
@@ -304,7 +317,7 @@ class RelPositionMultiHeadedAttention(nn.Module):
         # dq_v = dbd p -> tmp
         tmp = empty(M, D, like=dout)
         K.gemm(T, dk, P, dbd, c.p, tmp, mode_a=K.KC, lda=Pp, mode_b=K.RC, ldb=D, ldc=D,
-               batch=Z, nb2=B, sa=(B * T * Pp, T * Pp), sb=(dk, 0), sc=(dk, T * D))
+               batch=Z, nb2=B, sa=(B * T * Pp, T * Pp), sb=(dk, 0), sc=(dk, T * D), b_planes=_bpl(c.p_pl))
         K.colsum(tmp, self.pos_bias_v.grad.view(-1), accumulate=True)
         K.add2d(tmp, D, dqkv, 3 * D, M, D)
         # dp[:, h] = sum_b dbd[h,b]^T q_v[h,b]   (K = B*T)

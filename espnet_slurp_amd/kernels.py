@@ -423,7 +423,7 @@ def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc
          a_off=0, b_off=0, c_off=0, batch=1, nb2=1, sa=(0, 0), sb=(0, 0), sc=(0, 0),
          bias=None, alpha=1.0, beta=0.0, R=None, r_off=None, act=ACT_NONE, aux=None,
          drop_p=0.0, seed=0, ic_a: Optional[Sequence[int]] = None, ic_b: Optional[Sequence[int]] = None,
-         bwd_act=ACT_NONE, pre=None, rowsum=None, _keep_a16=False, b_weight=False):
+         bwd_act=ACT_NONE, pre=None, rowsum=None, _keep_a16=False, b_weight=False, b_planes=None):
     """C[z](m,n) = alpha*epi(sum_k A(m,k)B(k,n) + bias) + beta*R (see gemm.hip).
     bwd_act/pre: epilogue drop'(.)*act'(pre) (FFN backward); rowsum: += sum_k A(m,k) (bias grad).
     b_weight: B is a weight-like operand, constant for the step (its split planes may be cached
@@ -443,12 +443,19 @@ def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc
     ws = _ws(_GEMM_WS, "esp_gemm_f32", _GEMM_WS_BYTES, C.device)
     ica = (_native.I * 5)(*ic_a) if ic_a is not None else None
     icb = (_native.I * 5)(*ic_b) if ic_b is not None else None
-    bp = None
+    bp = None  # (planes pointer, plane row pitch, batch strides, plane stride)
     if (_BPLANES and _COMPUTE[0] == 0 and batch == 1 and mode_b in (KC, RC) and mode_a in (KC, RC, I2C_KC)
             and ic_b is None and M > 0 and N > 0 and K > 0):
         rows, cols = (N, K) if mode_b == KC else (K, N)
         if b_weight or _is_param(B.data_ptr() + b_off * 4, ((rows - 1) * ldb + cols) * 4):
-            bp = planes(B, b_off, rows, cols, ldb)
+            buf, ldp, ps = planes(B, b_off, rows, cols, ldb)
+            bp = (_p(buf), ldp, 0, 0, ps)
+    if (b_planes is not None and bp is None and _COMPUTE[0] == 0 and mode_b in (KC, RC) and mode_a in (KC, RC)
+            and ic_a is None and ic_b is None and M > 0 and N > 0 and K > 0):
+        # planes of B's whole source matrix, same element layout (ld): b_off and the batch strides carry over
+        buf, ldp, ps = b_planes
+        assert ldp == ldb, (ldp, ldb)
+        bp = (_p(buf, b_off), ldp, sb[0], sb[1], ps)
     if _PROF is not None:
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
@@ -460,7 +467,7 @@ def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc
                      _p(R, r_off or 0), act, _p(aux, c_off) if aux is not None else None,
                      float(drop_p), seed & 0xFFFFFFFFFFFFFFFF,
                      int(bwd_act), _p(pre, c_off) if pre is not None else None, _p(rowsum),
-                     ctypes_ptr(ica), _p(ws), _GEMM_WS_BYTES, _p(bp[0]), bp[1], 0, 0, bp[2], _st())
+                     ctypes_ptr(ica), _p(ws), _GEMM_WS_BYTES, bp[0], bp[1], bp[2], bp[3], bp[4], _st())
     else:
         _native.call("esp_gemm_f32", mode_a, mode_b, M, N, K, batch, nb2,
                      _p(A, a_off), lda, sa[0], sa[1], _p(B, b_off), ldb, sb[0], sb[1],
@@ -1032,6 +1039,20 @@ ATTN_FWD32 = os.environ.get("ESP_ATTN_FWD32", "0") == "1"
 # at C2 B=128 it is 412 + 73 us per layer against 59 + 266 (the epilogue's rel_shift scatter is one
 # scalar store per element; the row-wise pass writes each shifted bd row contiguously)
 ATTN_DSCORES = os.environ.get("ESP_ATTN_DSCORES", "0") == "1"
+# ESP_ATTN_BPLANES=1: the fp32 batched attention contractions whose B is qkv or the projected position
+# table (P.V, dP = dctx v^T, dS.k, dbd.p) take B as split planes made once per layer (PREC 3: only A
+# split in the k-loop) instead of splitting both operands in registers (PREC 0).  Opt-in: the
+# contractions gain 7-11 % but the two splits per layer cost more (C2 B=256 1337-1339 vs 1345-1351
+# utt/s, profiles/r04m_attn_bplanes_ab.txt) -- it pays once the qkv projection writes the planes itself
+ATTN_BPLANES = os.environ.get("ESP_ATTN_BPLANES", "0") == "1"
+
+
+def attn_bplanes_ok(D: int) -> bool:
+    if not ATTN_BPLANES or _COMPUTE[0] != 0 or D % 8:
+        return False
+    if _F32_PRODUCTS[0] is None:
+        _F32_PRODUCTS[0] = int(_native.load().esp_f32_gemm_products())
+    return _F32_PRODUCTS[0] == 6
 
 
 def relpos_attn_bwd(dctx, ldd, vmat, ldv, attn, dS, dbd, ldp, nb, H, sqrt_dk, drop_p, seed, T, lds, v_off=0):
