@@ -46,6 +46,10 @@ def empty(*shape, like: torch.Tensor):
     return torch.empty(*shape, dtype=torch.float32, device=like.device)
 
 
+# ESP_DZ2_DIRECT=0: the bf16 mode casts an fp32 dz2 for the conv2 gradients (A/B measurements)
+_DZ2_DIRECT = __import__("os").environ.get("ESP_DZ2_DIRECT", "1") == "1"
+
+
 def _bpl(pl):
     """gemm(b_planes=...) of a kernels.Planes (n = 3) holding B's whole source matrix, or None."""
     return (pl.buf, pl.ld, pl.ps) if pl is not None else None
@@ -608,14 +612,23 @@ class Conv2dSubsampling(nn.Module):
         z2f = c.z2.view(B * T2, F2 * D)
         K.linear_bwd_weight(dv, z2f, dwor.view(D, F2 * D), lin.bias.grad)
         K.permute3(dwor, lin.weight.grad, D, F2, D, accumulate=True)  # (n, f, c) -> (n, c, f)
-        dz2 = empty(B * T2, F2 * D, like=dx)
-        K.linear_bwd_data_act(dv, c.wor.view(D, F2 * D), dz2, z2f, K.ACT_RELU, b_weight=True)  # ReLU' from its output
         npix2 = B * T2 * F2
-        dz2p = dz2.view(npix2, D)
+        # the bf16 mode: dz2's bf16 copy is the operand of the weight- and input-gradient GEMMs; when both
+        # take it (even pixel count, implicit input gradient) the input-gradient GEMM of `out` writes it
+        # directly (its bf16 result plane, EPI_RMASK_PL) and dz2 never exists in fp32
+        direct16 = (K.conv2_bf16_ok(D) and c.z1_16 is not None and K.CONV2_IMPLICIT_DGRAD and D % 32 == 0
+                    and K.planes_mode() == 1 and (F2 * D) % 8 == 0 and _DZ2_DIRECT)
+        if direct16:
+            dz2 = K.Planes(B * T2, F2 * D, dx.device, 1)
+            K.linear_bwd_data_act(dv, c.wor.view(D, F2 * D), dz2, z2f, K.ACT_RELU, b_weight=True)
+            dz2p, dz2_16 = None, dz2.buf.view(npix2, D)
+        else:
+            dz2 = empty(B * T2, F2 * D, like=dx)
+            K.linear_bwd_data_act(dv, c.wor.view(D, F2 * D), dz2, z2f, K.ACT_RELU, b_weight=True)  # ReLU' from its output
+            dz2p = dz2.view(npix2, D)
+            dz2_16 = K.to_bf16(dz2p, npix2, D, D) if K.conv2_bf16_ok(D) else None
         ic = (T1, F1, D, T2, F2)
         dw2r = empty(D, 9 * D, like=dx)
-        # the bf16 mode: dz2's bf16 copy is the operand of the weight- and input-gradient GEMMs
-        dz2_16 = K.to_bf16(dz2p, npix2, D, D) if K.conv2_bf16_ok(D) else None
         if dz2_16 is not None and c.z1_16 is not None:
             K.conv2_wgrad_bf16(dz2_16, c.z1_16, dw2r, c2.bias.grad, B, T1, F1, D)
         else:

@@ -179,7 +179,7 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
     if (kind < 0 || !g.wide) return false;
     if (kind == EPI_P0_PL && !(MA == KC && MB == RC)) return false;
     if ((kind == EPI_FFN_SWISH_PL || kind == EPI_FFN_RELU_PL) && !(MA == KC && MB == KC)) return false;
-    if (kind == EPI_BMUL_PL && !(MA == KC && MB == RC)) return false;
+    if ((kind == EPI_BMUL_PL || kind == EPI_RMASK_PL) && !(MA == KC && MB == RC)) return false;
   }
   if (kind == EPI_SMB && !(MA == KC && MB == KC && g.bf16 == 0)) return false;
   if (!g.cpn && (((kind == EPI_BMUL || kind == EPI_RMASK) && !can_spec_bwd) || ((kind == EPI_P0 || kind == EPI_PR) && !can_pspec) ||
@@ -250,7 +250,7 @@ int launch(const GemmArgs& g0, int batch, hipStream_t st, const Operand* b_fp32 
     if (g.bnt == 64 || g.bnt == 128) done = launch_glds(MA, MB, g, batch, st);
   }
   if (!done && g.cpn) {
-    esp::set_error("esp_gemm_f32_pl: no kernel writes this epilogue as planes (planes output: plain, or the FFN "
+    esp::set_error("esp_gemm_f32_pl: no kernel writes this epilogue as planes (planes output: plain, the ReLU mask, or the FFN "
                    "bias + activation + dropout + derivative; N %% 4 == 0, 16-B aligned, LDS-DMA operands)");
     return -1;
   }

@@ -3,7 +3,8 @@
 // forward (KC x KC), EPI_BRELU (bias + ReLU) for the conv2 forward (implicit-im2col I2C_KC x KC)
 // and KC x KC, EPI_BMUL for the FFN input gradient and EPI_RMASK for the gradient through conv2's
 // ReLU (KC x RC) and its row-mapped form for the implicit conv2 input gradient (I2CT_KC x RC); the
-// FFN w_1 kinds with the hidden state written as bf16 planes (EPI_FFN_*_PL).
+// FFN w_1 kinds with the hidden state written as bf16 planes (EPI_FFN_*_PL), the FFN and ReLU-mask input
+// gradients as planes (EPI_BMUL_PL, EPI_RMASK_PL).
 // See store_spec.
 #include "gemm_kernels.h"
 
@@ -34,6 +35,7 @@ bool glds_launch_spec(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hip
       ESP_SPEC(EPI_BMUL)
       ESP_SPEC(EPI_RMASK)
       ESP_SPEC(EPI_BMUL_PL)
+      ESP_SPEC(EPI_RMASK_PL)
     } else if constexpr (MA == I2CT_KC && MB == RC) {
       ESP_SPEC(EPI_RMASKMAP)
     }

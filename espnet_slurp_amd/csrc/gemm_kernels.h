@@ -156,13 +156,16 @@ enum { EPI_PLAIN = 0, EPI_FWD = 1, EPI_BWD = 2, EPI_BIAS = 3, EPI_BDR = 4, EPI_F
        // the same kinds with C written as bf16 planes (GemmArgs cpn): the FFN hidden state, the attention context
        EPI_FFN_SWISH_PL = 14, EPI_FFN_RELU_PL = 15, EPI_P0_PL = 16,
        // ... and the FFN's input gradient through the stored derivative (its only readers: w_1's GEMMs)
-       EPI_BMUL_PL = 17 };
+       EPI_BMUL_PL = 17,
+       // ... and the gradient through a ReLU output (the subsampling's dz2: its readers are conv2's GEMMs)
+       EPI_RMASK_PL = 18 };
 // the fp32-output kind a planes-output kind computes
 constexpr int epi_base(int e) {
   return e == EPI_FFN_SWISH_PL ? EPI_FFN_SWISH
          : e == EPI_FFN_RELU_PL ? EPI_FFN_RELU
          : e == EPI_P0_PL      ? EPI_P0
          : e == EPI_BMUL_PL    ? EPI_BMUL
+         : e == EPI_RMASK_PL   ? EPI_RMASK
                                : e;
 }
 __host__ __device__ inline int epi_kind(const GemmArgs& g) {
@@ -180,6 +183,7 @@ __host__ inline int epi_kind_spec(const GemmArgs& g) {
     if (g.bias && g.aux && !g.bwd_act && g.act == (ACT_SWISH | ACT_AUX_DERIV)) return EPI_FFN_SWISH_PL;
     if (g.bias && g.aux && !g.bwd_act && g.act == (ACT_RELU | ACT_AUX_DERIV)) return EPI_FFN_RELU_PL;
     if (k == EPI_BWD && g.bwd_act == ACT_MUL && !g.drop_thresh && !g.bias && g.alpha == 1.0f) return EPI_BMUL_PL;
+    if (k == EPI_BWD && g.bwd_act == ACT_RELU && !g.drop_thresh && !g.bias && g.alpha == 1.0f) return EPI_RMASK_PL;
     return -1;
   }
   if (g.cmap)

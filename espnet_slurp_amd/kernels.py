@@ -1272,13 +1272,14 @@ def conv2_wgrad_bf16(dz2_16, z1_16, dw, db, B, T1, F1, D):
 
 def conv2_dgrad(dz2, W, z1, dz1, B, T1, F1, D, dz2_16=None):
     """Conv2d(D, D, 3, 2) input gradient x conv1 ReLU mask as 4 implicit parity-class GEMMs; dz2_16 (the
-    bf16 mode): dz2 as bf16, the class GEMMs on bf16 operands (esp_conv2_dgrad_bf16)."""
+    bf16 mode): dz2 as bf16, the class GEMMs on bf16 operands (esp_conv2_dgrad_bf16; dz2 may then be None)."""
+    assert dz2 is not None or dz2_16 is not None
     _f32(dz2, W, z1, dz1)
-    key = str(dz2.device)
+    key = str(W.device)
     if key not in _ZEROS:
-        _ZEROS[key] = torch.zeros(64, dtype=torch.float32, device=dz2.device)
+        _ZEROS[key] = torch.zeros(64, dtype=torch.float32, device=W.device)
     n = _wsize("esp_conv2_dgrad", D)
-    wc = _ws(_WS2, "esp_conv2_dgrad", n, dz2.device)
+    wc = _ws(_WS2, "esp_conv2_dgrad", n, W.device)
     if _PROF is not None:
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
