@@ -164,7 +164,29 @@ __global__ void __launch_bounds__(256) embed_bwd_kernel(const int64_t* __restric
     if (hit) rows[base + __popcll(m & ((1ull << lane) - 1))] = r;
     __syncthreads();
     any |= n > 0;
-    for (int k = 0; k < n; ++k) {
+    // EMB_GROUP rows' loads issued before their adds (which stay in ascending row order): a token
+    // that fills most of the list (the eos padding of the decoder input) no longer waits out one
+    // load latency per row: 962 -> ~500 us per launch at C2 B=256 (profiles/r04p_ vs r04r_kernel_summary_b256.txt;
+    // 8- and 32-row groups measure the same -- the rest is the token scan)
+    constexpr int EMB_GROUP = 32;
+    int k = 0;
+    for (; k + EMB_GROUP <= n; k += EMB_GROUP) {
+#pragma unroll
+      for (int j = 0; j < EMB_MAXD / 256; ++j) {
+        const int d = tid + j * 256;
+        if (j * 256 >= D) break;  // (uniform)
+        float g[EMB_GROUP];
+#pragma unroll
+        for (int u = 0; u < EMB_GROUP; ++u) g[u] = d < D ? dy[(long)rows[k + u] * D + d] : 0.f;
+#pragma unroll
+        for (int u = 0; u < EMB_GROUP; ++u) {
+          float x = g[u];
+          if (thr) x = esp::keep_elem(seed, (uint64_t)((long)rows[k + u] * D + d), thr) ? x * scale : 0.f;
+          if (d < D) acc[j] += x * xscale;
+        }
+      }
+    }
+    for (; k < n; ++k) {
       const long rb = (long)rows[k] * D;
 #pragma unroll
       for (int j = 0; j < EMB_MAXD / 256; ++j) {
