@@ -2,7 +2,9 @@
 """Benchmark: utterances/sec of the full ESPnet2 Conformer CTC/attention training step.
 
     python bench.py [--gpus N --steps K --warmup W --batch B]
-    (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+    (N>1: either launched by the caller, python -m torch.distributed.run --nproc-per-node N ...
+    bench.py --gpus N ..., or started plainly: bench.py then launches the N ranks itself, one
+    process per GPU over RCCL, as espnet2/tasks/abs_task.py:1049-1070 spawns its DDP workers)
 
 Workload (BASELINE.json configs[1]): 80-dim fbank x 1500 frames,
 Conformer encoder d=256, 4 heads, FF 1024, 12 blocks (macaron, rel-pos latest, cnn k=31),
@@ -201,6 +203,31 @@ def measured_gemm_traffic(args) -> dict:
     return {}
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_launch(argv, gpus, env, port=None):
+    """How this invocation runs (decided before anything touches the GPU).  Returns None to run the
+    bench in this process (a single GPU, or one rank of a launcher that set WORLD_SIZE), or the
+    command that starts `gpus` ranks on this node -- torch.distributed.run, one process per GPU,
+    rendezvous on 127.0.0.1 -- whose exit status this process then returns.  A launcher whose
+    WORLD_SIZE differs from --gpus is an error (the line would report the wrong n_gpus)."""
+    world = env.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} but the launcher's WORLD_SIZE is {world}")
+        return None
+    if gpus <= 1:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port or free_port()}",
+            os.path.abspath(__file__)] + list(argv)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -228,6 +255,17 @@ def main():
     ap.add_argument("--config", choices=sorted(PRESETS), default=None,
                     help="BASELINE.json config preset (overrides --d/--heads/--ff/--layers; c5 implies --amp)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    cmd = rank_launch(sys.argv[1:], args.gpus, os.environ)
+    if cmd is not None:
+        # the N ranks as child processes (this process has not touched the GPU: counting devices
+        # does not initialise it on this image)
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but {have} GPU(s) visible")
+        import subprocess
+        sys.exit(subprocess.run(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")).returncode)
     if args.config:
         args.d, args.heads, args.ff, args.layers, amp = PRESETS[args.config]
         args.amp = args.amp or amp

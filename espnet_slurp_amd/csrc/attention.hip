@@ -775,72 +775,47 @@ __global__ __launch_bounds__(256) void relpos_attn_fwd_kernel(
 // blocks m <= g lie wholly below T (A rows q_v[i]), blocks m >= g+1 wholly at or above T (A rows
 // q_v[i+1], the shifted twin), so legacy selects the A operand per block and shares the ring.
 // LDS: ring rows of RW_PITCH floats (row groups r and r+4 of a 32-lane half 16 banks apart).
-// XS = 6 (ESP_ATTN_XS=1): the ac and band products as bf16x6 split products on
-// v_mfma_f32_16x16x32_bf16 (the GEMM family's fp32 arithmetic, gemm_kernels.h): each operand value
-// v = hi + mid + lo exactly (three bf16), six products per pair, smallest first.  XS = 1 (the bf16
-// mode, esp_set_gemm_compute(1): every GEMM of the step on bf16 operands): hi.hi alone, i.e. torch
-// autocast's bf16 matmul of the RNE-rounded operands with fp32 accumulation.  A lane's 16 values of a
-// row (d = 16 q4 + [0,16)) are the two k-halves of the 16x16x32 operand (MFMA m takes
-// d = 16 q4 + 8 m + [0, 8)); the output layout is the 16x16x4 one, so the ring, softmax and stores
-// are shared with the f32 form (XS = 0).
+// XS = 1 (the bf16 mode, esp_set_gemm_compute(1): every product of that step on bf16 operands): the ac
+// and band products on v_mfma_f32_16x16x32_bf16 of the RNE-rounded operands with fp32 accumulation
+// (torch autocast's bf16 matmul).  A lane's 16 values of a row (d = 16 q4 + [0,16)) are the two
+// k-halves of the 16x16x32 operand (MFMA m takes d = 16 q4 + 8 m + [0, 8)); the output layout is the
+// 16x16x4 one, so the ring, softmax and stores are shared with the f32 form (XS = 0).  (A bf16x6
+// split-product form of the fp32 scores was measured slower, 441 vs 414 us at C2 B=128 -- the kernel
+// is not bound by its MFMAs, DESIGN 3.4 -- and removed in round 5.)
 typedef __attribute__((ext_vector_type(8))) __bf16 attn_bf16x8;
-struct Frag6 {
-  attn_bf16x8 v[3][2];  // [hi, mid, lo][k-half] (XS = 1: hi only)
+struct Frag16 {
+  attn_bf16x8 v[2];  // [k-half]
 };
-template <int NP>
-__device__ __forceinline__ void split_frag(const float (&f)[16], Frag6& o) {
+__device__ __forceinline__ void split_frag(const float (&f)[16], Frag16& o) {
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
-    uint32_t h[4], md[4], l[4];
+    uint32_t h[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if constexpr (NP == 6) esp::split3_pair(f[8 * m + 2 * j], f[8 * m + 2 * j + 1], h[j], md[j], l[j]);
-      else h[j] = esp::bf16_pair(f[8 * m + 2 * j], f[8 * m + 2 * j + 1]);
-    }
-    o.v[0][m] = __builtin_bit_cast(attn_bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
-    if constexpr (NP == 6) {
-      o.v[1][m] = __builtin_bit_cast(attn_bf16x8, make_uint4(md[0], md[1], md[2], md[3]));
-      o.v[2][m] = __builtin_bit_cast(attn_bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
-    }
+    for (int j = 0; j < 4; ++j) h[j] = esp::bf16_pair(f[8 * m + 2 * j], f[8 * m + 2 * j + 1]);
+    o.v[m] = __builtin_bit_cast(attn_bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
   }
 }
-template <int NP>
-__device__ __forceinline__ f32x4 mfma_np(const Frag6& a, const Frag6& b, f32x4 c) {
+__device__ __forceinline__ f32x4 mfma_np(const Frag16& a, const Frag16& b, f32x4 c) {
 #pragma unroll
-  for (int m = 0; m < 2; ++m) {
-    if constexpr (NP == 6) {
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[1][m], b.v[1][m], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[2][m], b.v[0][m], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[0][m], b.v[2][m], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[1][m], b.v[0][m], c, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[0][m], b.v[1][m], c, 0, 0, 0);
-    }
-    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[0][m], b.v[0][m], c, 0, 0, 0);
-  }
+  for (int m = 0; m < 2; ++m) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[m], b.v[m], c, 0, 0, 0);
   return c;
 }
 
-// Off by default: measured at C2 B=128 (tools/attn_kernels_bench.py, one box) 441 vs 414 us latest,
-// 519 vs 420 legacy with one tile of prefetch -- the kernel is not bound by its MFMAs
-#ifndef ESP_ATTN_XS_DEFAULT
-#define ESP_ATTN_XS_DEFAULT 0
-#endif
 constexpr int RW_ROWS = 16, RW_PITCH = 37;
 // store-transpose rows: 64 floats, so the float4 read-back (ds_read_b128 lane groups of 16 lanes over
 // two rows, bank (a/4) mod 64) is conflict-free, with the column XOR-ed by 16 in rows 4..7 and 12..15
 // so the two row groups of a ds_write_b32 half land 16 banks apart too (68: the reads conflicted 2-way)
 constexpr int RW_SPITCH = 64;
-// SPLIT = 2 (opt-in, ESP_ATTN_SPLIT=2): a row group's keys are shared by two waves of the block
-// (tiles [0, NTA) and [NTA, 2 NTA)), half the score registers each (3 waves per SIMD instead of
-// 2); the row max and sum are combined through LDS with one block barrier each.  Measured at C2
-// B=128: 398 vs 395 us (327 vs 309 without dropout) — the kernel is not latency-bound but bound
-// by the SIMD's shared f32 MFMA / VALU issue, so the extra occupancy buys nothing.
+// SPLIT = 2 (the bf16 mode's legacy rel_shift past 16 key tiles): a row group's keys are shared by
+// two waves of the block (tiles [0, NTA) and [NTA, 2 NTA)), half the score registers each; the row
+// max and sum are combined through LDS with one block barrier each.  (As an fp32 option it measured
+// 398 vs 395 us at C2 B=128 and was removed in round 5.)
 template <int NTA, bool P2, bool LEGACY, int SPLIT = 1, int XS = 0>  // SPLIT * NTA >= ceil(T/16) key tiles
-__global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fwd16_kernel(
+__global__ __launch_bounds__(256, 2) void relpos_attn_fwd16_kernel(
     const float* __restrict__ qu, const float* __restrict__ qv, const float* __restrict__ kmat, long ldk,
     const float* __restrict__ pm, long ldpm, int nb, float sqrt_dk, const int* __restrict__ klen,
     float* __restrict__ attn, float* __restrict__ pdrop, uint32_t thr, float dscale, uint64_t seed, int T, long lds,
-    const uint64_t* __restrict__ key, const int* __restrict__ tvalid, int nrb, int Z, int abl) {
+    const uint64_t* __restrict__ key, const int* __restrict__ tvalid, int nrb, int Z) {
   __shared__ float ring[4][RW_ROWS * RW_PITCH];
   __shared__ __attribute__((aligned(16))) float stage[4][RW_ROWS * RW_SPITCH];
   __shared__ float xch[2][4][RW_ROWS];  // SPLIT 2: per-wave row max / row sum partials
@@ -857,7 +832,6 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
   seed = esp::keyed(seed, key);
   const int head = z / nb, b = z - head * nb;
   const int li = lane & 15, q4 = lane >> 4;
-  const int nt = (T + 15) >> 4;
   const int g = i0 >> 4;
   // legacy rel_shift length: the reference batch's T' (tvalid) when the batch is padded to a
   // length bucket -- its table positions j + T'-1-i depend on T' (the latest ones, i - j, do not);
@@ -893,10 +867,10 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
   // XS: the query rows' split planes (once per wave).  Legacy: the band's A rows switch from q_v[i]
   // to q_v[i+1] once, at block g+1, and never back, so xv is re-split from the shifted rows at that
   // tile (one exposed load per wave) instead of holding both rows' planes
-  Frag6 xu, xv;
+  Frag16 xu, xv;
   if constexpr (XS) {
-    split_frag<XS>(au, xu);
-    split_frag<XS>(av, xv);
+    split_frag(au, xu);
+    split_frag(av, xv);
   }
   int kl = klen ? klen[b] : T;
   if (kl > T) kl = T;
@@ -917,13 +891,13 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
     const bool shifted = LEGACY && t0 > g;
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
     if constexpr (XS) {
-      Frag6 pf6;
-      split_frag<XS>(pb[0], pf6);
+      Frag16 pf6;
+      split_frag(pb[0], pf6);
       if (shifted) {  // (SPLIT 2: a second-half wave whose keys all lie past the switch)
         ld16(qv + ((long)z * T + min(i0 + 1 + li, T - 1)) * RP_DK, av2);
-        split_frag<XS>(av2, xv);
+        split_frag(av2, xv);
       }
-      s = mfma_np<XS>(xv, pf6, s);
+      s = mfma_np(xv, pf6, s);
     } else {
 #pragma unroll
       for (int c = 0; c < 16; ++c)
@@ -943,24 +917,22 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
     {
       // the fragments DEPTH tiles ahead are requested first, into the buffers the previous tile
       // released, so a fetch has DEPTH whole tiles of this wave's work to arrive
-      if (!(abl & 4)) {  // (4: no per-tile fragment fetch -- stale fragments; diagnostic timing only)
-        ld16(k_row(t + DEPTH), kb[(tt + DEPTH) % NB]);  // clamped rows: always safe to fetch
-        ld16(p_row(t + 1 + DEPTH), pb[(tt + 1 + DEPTH) % NB]);
-      }
+      ld16(k_row(t + DEPTH), kb[(tt + DEPTH) % NB]);  // clamped rows: always safe to fetch
+      ld16(p_row(t + 1 + DEPTH), pb[(tt + 1 + DEPTH) % NB]);
       const float(&kf)[16] = kb[tt % NB];
       const float(&pf)[16] = pb[(tt + 1) % NB];
       const bool shifted = LEGACY && t + 1 > g;  // legacy band block t+1 at/above table position T
       f32x4 a = {0.f, 0.f, 0.f, 0.f}, s = {0.f, 0.f, 0.f, 0.f};
       if constexpr (XS) {
-        Frag6 kf6, pf6;
-        split_frag<XS>(kf, kf6);
-        split_frag<XS>(pf, pf6);
+        Frag16 kf6, pf6;
+        split_frag(kf, kf6);
+        split_frag(pf, pf6);
         if (LEGACY && t == g) {  // block t+1 = g+1: the first shifted band block
           ld16(qv + ((long)z * T + min(i0 + 1 + li, T - 1)) * RP_DK, av2);
-          split_frag<XS>(av2, xv);
+          split_frag(av2, xv);
         }
-        a = mfma_np<XS>(xu, kf6, a);
-        s = mfma_np<XS>(xv, pf6, s);
+        a = mfma_np(xu, kf6, a);
+        s = mfma_np(xv, pf6, s);
       } else {
 #pragma unroll
         for (int c = 0; c < 16; ++c) {
@@ -968,8 +940,7 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
           s = __builtin_amdgcn_mfma_f32_16x16x4f32(shifted ? av2[c] : av[c], pf[c], s, 0, 0, 0);
         }
       }
-      if (!(abl & 2)) put_band(ring0, t + 1, s);
-      else if (s[0] == 12345.f) a[0] += 1.f;  // (diagnostic: no ring; keeps the band MFMAs live)
+      put_band(ring0, t + 1, s);
       asm volatile("" ::: "memory");  // ring writes before the shifted reads (LDS is in order per wave)
       const int j = t * 16 + li;
       // the four shifted band reads first, then their uses: one LDS round trip per tile (reads
@@ -978,7 +949,7 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int ii = 4 * q4 + r;
-        bdv[r] = (abl & 2) ? 0.f : ring0[ii * RW_PITCH + ((t * 16 + li - ii + 15) & 31)];
+        bdv[r] = ring0[ii * RW_PITCH + ((t * 16 + li - ii + 15) & 31)];
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -1111,10 +1082,6 @@ __global__ __launch_bounds__(256, SPLIT == 2 && !XS ? 3 : 2) void relpos_attn_fw
       asm volatile("" ::: "memory");  // the reads above before the next chunk's writes
     }
   };
-  if (attn == nullptr) {  // diagnostic ablation (ESP_ATTN_ABL=1, timing only): no stores; keep the scores live
-    if (sc[0][0] == 12345.f) attn = pdrop;  // never taken with real data; stops the compiler dropping the work
-    else return;
-  }
   if (pdrop) store_rows(std::true_type{});
   else store_rows(std::false_type{});
 }
@@ -1316,92 +1283,52 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
   if (!thr) pdrop = nullptr;
   const float ds = esp::drop_scale(thr);
   const int nt = (T + 15) / 16;
-  static int split_env = -1;  // ESP_ATTN_SPLIT=1|2: one wave per row group / two (key halves)
-  if (split_env < 0) split_env = getenv("ESP_ATTN_SPLIT") ? atoi(getenv("ESP_ATTN_SPLIT")) : 1;
-  const bool split = split_env == 2 && nt > 8 && nt <= 32;
   const int Zn = nb * H;
-  int nrb = (T + (split ? 2 : 4) * RW_ROWS - 1) / ((split ? 2 : 4) * RW_ROWS);  // row blocks per z
+  int nrb = (T + 4 * RW_ROWS - 1) / (4 * RW_ROWS);  // row blocks per z (4 waves x 16 rows)
   dim3 grid((unsigned)(8 * ((Zn + 7) / 8) * nrb));  // XCD-aware order (see the kernel)
   hipStream_t st = (hipStream_t)stream;
   const bool p2 = sqrt_dk > 0.f && (__builtin_bit_cast(uint32_t, sqrt_dk) & 0x7fffffu) == 0;
-  static int xs_env = -1;  // ESP_ATTN_XS=1: the split products (A/B measurements)
-  if (xs_env < 0) xs_env = getenv("ESP_ATTN_XS") ? atoi(getenv("ESP_ATTN_XS")) : ESP_ATTN_XS_DEFAULT;
   // the bf16 mode computes the scores on bf16 operands like every other product of its step
-  const int np = xs_env ? 6 : (esp_get_gemm_compute() == 1 ? 1 : 0);
-  static int abl_env = -1;  // ESP_ATTN_ABL=1: no stores (diagnostic timing only; the output is garbage)
-  if (abl_env < 0) abl_env = getenv("ESP_ATTN_ABL") ? atoi(getenv("ESP_ATTN_ABL")) : 0;
-  if (abl_env & 1) attn = nullptr;  // (2: no rel_shift ring -- bd = 0; diagnostic timing only)
-  if (np && !split) {
-#define ESP_RX4(N, P2_, L_, NP_)                                                                                       \
-  hipLaunchKernelGGL((relpos_attn_fwd16_kernel<N, P2_, L_, 1, NP_>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p,     \
-                     ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid, nrb, Zn, abl_env)
-#define ESP_RX3(N, P2_, L_)              \
-  do {                                   \
-    if (np == 6) ESP_RX4(N, P2_, L_, 6); \
-    else ESP_RX4(N, P2_, L_, 1);         \
+  if (esp_get_gemm_compute() == 1) {
+#define ESP_RX(N, P2_, L_)                                                                                         \
+  hipLaunchKernelGGL((relpos_attn_fwd16_kernel<N, P2_, L_, 1, 1>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p, \
+                     ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(),   \
+                     tvalid, nrb, Zn)
+#define ESP_RXN(N)                      \
+  do {                                  \
+    if (relpos == 2) {                  \
+      if (p2) ESP_RX(N, true, true);    \
+      else ESP_RX(N, false, true);      \
+    } else {                            \
+      if (p2) ESP_RX(N, true, false);   \
+      else ESP_RX(N, false, false);     \
+    }                                   \
   } while (0)
-#define ESP_RX(N)                     \
-  do {                                \
-    if (relpos == 2) {                \
-      if (p2) ESP_RX3(N, true, true); \
-      else ESP_RX3(N, false, true);   \
-    } else {                          \
-      if (p2) ESP_RX3(N, true, false); \
-      else ESP_RX3(N, false, false);  \
-    }                                 \
-  } while (0)
-    if (nt <= 8) ESP_RX(8);
-    else if (nt <= 16) ESP_RX(16);
+    if (nt <= 8) ESP_RXN(8);
+    else if (nt <= 16) ESP_RXN(16);
     else if (relpos == 2) {
       // legacy: the row-shift re-split leaves no registers for 24+ score tiles per wave; two waves
       // share a row group's keys (SPLIT 2, half the score registers each)
       nrb = (T + 2 * RW_ROWS - 1) / (2 * RW_ROWS);
       grid.x = (unsigned)(8 * ((Zn + 7) / 8) * nrb);
-#define ESP_RL(P2_, NP_)                                                                                               \
-  hipLaunchKernelGGL((relpos_attn_fwd16_kernel<16, P2_, true, 2, NP_>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p,   \
-                     ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid, nrb, Zn, abl_env)
-      if (np == 6) {
-        if (p2) ESP_RL(true, 6);
-        else ESP_RL(false, 6);
-      } else {
-        if (p2) ESP_RL(true, 1);
-        else ESP_RL(false, 1);
-      }
-#undef ESP_RL
-    } else if (nt <= 24) ESP_RX(24);
-    else ESP_RX(32);
+      if (p2)
+        hipLaunchKernelGGL((relpos_attn_fwd16_kernel<16, true, true, 2, 1>), grid, dim3(256), 0, st, qu, qv, kmat, ldk,
+                           p, ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds,
+                           esp::rng_key_ptr(), tvalid, nrb, Zn);
+      else
+        hipLaunchKernelGGL((relpos_attn_fwd16_kernel<16, false, true, 2, 1>), grid, dim3(256), 0, st, qu, qv, kmat, ldk,
+                           p, ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds,
+                           esp::rng_key_ptr(), tvalid, nrb, Zn);
+    } else if (nt <= 24) ESP_RXN(24);
+    else ESP_RXN(32);
+#undef ESP_RXN
 #undef ESP_RX
-#undef ESP_RX3
-#undef ESP_RX4
-    ESP_CHECK_LAUNCH("esp_relpos_attn_probs");
-    return 0;
-  }
-  if (split) {
-#define ESP_RS3(N, P2_, L_)                                                                                            \
-  hipLaunchKernelGGL((relpos_attn_fwd16_kernel<N, P2_, L_, 2>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p, ldp_row, \
-                     nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid, nrb, Zn, abl_env)
-#define ESP_RS(N)                     \
-  do {                                \
-    if (relpos == 2) {                \
-      if (p2) ESP_RS3(N, true, true); \
-      else ESP_RS3(N, false, true);   \
-    } else {                          \
-      if (p2) ESP_RS3(N, true, false); \
-      else ESP_RS3(N, false, false);  \
-    }                                 \
-  } while (0)
-    const int half = (nt + 1) / 2;
-    if (half <= 8) ESP_RS(8);
-    else if (half <= 12) ESP_RS(12);
-    else ESP_RS(16);
-#undef ESP_RS
-#undef ESP_RS3
     ESP_CHECK_LAUNCH("esp_relpos_attn_probs");
     return 0;
   }
 #define ESP_RW3(N, P2_, L_)                                                                                         \
   hipLaunchKernelGGL((relpos_attn_fwd16_kernel<N, P2_, L_>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p, ldp_row, \
-                     nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid, nrb, Zn, abl_env)
+                     nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), tvalid, nrb, Zn)
 #define ESP_RW(N)                             \
   do {                                        \
     if (relpos == 2) {                        \

@@ -107,49 +107,32 @@ __global__ void rowsum_rc_kernel(const float* __restrict__ p, long ld, int M, in
   out[r] += s;
 }
 
-// resident blocks of the persistent LDS-DMA kernel: 2 per CU (64 KB LDS each);
-// ESP_GEMM_PERSIST=0 launches one block per tile instead
-long g_persist = -1;
+// resident blocks of the persistent LDS-DMA kernel: per_cu per CU (64 KB LDS each)
+long g_cus = -1;
 long persist_blocks(int per_cu) {
-  if (g_persist < 0) {
-    const char* e = getenv("ESP_GEMM_PERSIST");
+  if (g_cus < 0) {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess)
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-    g_persist = (e && atoi(e) == 0) ? 0 : cus;
+    g_cus = cus;
   }
-  return g_persist ? (long)per_cu * g_persist : (1L << 40);
+  return (long)per_cu * g_cus;
 }
 
 int g_compute = 0;  // 0: fp32 MFMA (exact f32 fma chain), 1: bf16-input MFMA with fp32 accumulate
 
-// split-K combine: 0 the reduction launch (default), 1 in-kernel (last-arriving unit per tile);
-// esp_set_splitk_mode, initialised from ESP_SPLITK_INKERNEL
-int g_splitk = -1;
-int splitk_mode() {
-  if (g_splitk < 0) g_splitk = (getenv("ESP_SPLITK_INKERNEL") && atoi(getenv("ESP_SPLITK_INKERNEL")) == 1) ? 1 : 0;
-  return g_splitk;
-}
+// split-K combine: 0 the reduction launch (default), 1 in-kernel (last-arriving unit per tile;
+// measured slower, kept for esp_set_splitk_mode and its parity test)
+int g_splitk = 0;
+int splitk_mode() { return g_splitk; }
 
-// smallest K a split-K split keeps (ESP_SPLITK_MINK, A/B measurements; 128 before round 4's end)
-long g_splitk_mink = -1;
-long splitk_mink() {
-  if (g_splitk_mink < 0) {
-    const char* e = getenv("ESP_SPLITK_MINK");
-    g_splitk_mink = e && atol(e) >= 32 ? atol(e) : 256;
-  }
-  return g_splitk_mink;
-}
+// smallest K a split-K split keeps on grids of >= 64 tiles (128 before round 4's end)
+constexpr long kSplitkMinK = 256;
+long splitk_mink() { return kSplitkMinK; }
 
-// ESP_GEMM_VARIANT != 4 forces the register-staged fallback kernel (diagnostics)
-int g_variant = -1;
-int variant() {
-  if (g_variant < 0) {
-    const char* e = getenv("ESP_GEMM_VARIANT");
-    g_variant = e ? atoi(e) : 4;
-  }
-  return g_variant;
-}
+// work units split-K aims for: two resident blocks on each of 256 CUs (256 / 384 / 768 measured within
+// +-0.5 %, profiles/r03i_abc_splitk_target.txt)
+constexpr long kSplitkTarget = 2 * 256;
 
 // Launch the LDS-DMA kernel with the epilogue kind compiled in (each kind is its own kernel,
 // so the plain GEMMs carry none of the fused epilogues' registers; the instantiations live in
@@ -191,7 +174,7 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
   GldsArgs x{};
   if (MA == I2CT_KC) x = *tconv;  // the transposed-conv gather parameters
   x.ntx = (g.N + BNT - 1) / BNT;
-  const int bm = g.bm == 64 || g.bm == 256 ? g.bm : BM;
+  const int bm = g.bm == 64 ? g.bm : BM;
   x.nty = (g.M + bm - 1) / bm;
   if (MA == I2C_KC) {
     x.c_a = make_fastdiv(g.a.ic.C);
@@ -204,11 +187,6 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
     x.wo_b = make_fastdiv(g.b.ic.Wo);
   }
   x.ntiles = (int)((long)x.ntx * x.nty * batch * g.splits);
-  {
-    static int abl = -1;
-    if (abl < 0) abl = getenv("ESP_GEMM_ABL") ? atoi(getenv("ESP_GEMM_ABL")) : 0;
-    x.abl = abl;
-  }
   const bool rs = can_rs && g.rowsum;
   if (rs) kind = EPI_PLAIN;
   const dim3 grid((unsigned)std::min<long>(x.ntiles, persist_blocks(glds_occupancy_rt(BNT, kind, bm, g.bf16))));
@@ -571,10 +549,6 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
            (!work || aligned16(work));
   g.ragged4 = !g.wide && N % 4 != 0 && ldc % 4 == 0 && sc1 % 4 == 0 && sc2 % 4 == 0 && aligned16(C) &&
               (!R || aligned16(R)) && !aux && !pre && !bias;
-  {
-    const char* e = getenv("ESP_GEMM_ABL");
-    if (e && (atoi(e) & 16)) g.wide = g.ragged4 = 0;
-  }
   g.drop_scale = 1.f;  // (the specialised dropout epilogues run unconditionally: p = 0 keeps every element at scale 1)
   if (drop_p > 0.f) {
     g.drop_thresh = esp::drop_threshold(drop_p);
@@ -588,8 +562,7 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
   g.batch = batch;
   g.splits = 1;
   g.kchunk = K;
-  static long target = -1;  // work units split-K aims for (ESP_SPLITK_TARGET: measurements)
-  if (target < 0) target = getenv("ESP_SPLITK_TARGET") ? atol(getenv("ESP_SPLITK_TARGET")) : 2 * 256;
+  const long target = kSplitkTarget;
   auto ntiles = [&](int bn, int bm = BM) { return (long)((N + bn - 1) / bn) * ((M + bm - 1) / bm) * batch; };
   g.bnt = 0;
   g.bm = BM;
@@ -605,7 +578,7 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
            (mode == KC ? (K % 8 == 0 && ld >= K && 128L * ld * 2 < (1L << 32))
                        : (rows % 8 == 0 && ld >= rows && 32L * ld * 2 + 2L * rows < (1L << 32)));
   };
-  const bool split_ok = prec_in < 0 && g.bf16 == 0 && ESP_F32_SPLIT && variant() == 4 && K > 0;
+  const bool split_ok = prec_in < 0 && g.bf16 == 0 && ESP_F32_SPLIT && K > 0;
   if (split_ok && mode_b <= RC && planes_ok(b_planes, ldbp, sbp1, sbp2, bps, mode_b, N) &&
       (((mode_a == KC || mode_a == I2C_KC) && mode_b == KC) || ((mode_a == KC || mode_a == RC) && mode_b == RC) ||
        (a_planes && mode_a <= RC))) {
@@ -627,7 +600,7 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
     return -1;
   }
   const bool bplanes = g.bf16 >= 3;
-  if (variant() == 4 && g.a.glds && g.b.glds && K > 0) {
+  if (g.a.glds && g.b.glds && K > 0) {
     // per-CU time model: ceil(tiles / CUs) tiles of bn/64 units each, x1.3 when the grid
     // leaves CUs with a single resident block (one wave per SIMD); ties keep 128 (intensity)
     // fp32 on split products (ESP_F32_SPLIT): a 64-wide tile costs ~3/4 of a 128-wide one (its
@@ -650,7 +623,7 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
     g.bnt = (N <= 64 || g.bf16 == 5 || cost(64) < cost(128)) ? 64 : 128;
     // 64 x 64 tiles for grids that 128-row tiles leave under-filled (decoder M ~ 5k tokens, the
     // 41-query source attention): one work unit per tile, x1.15 for the halved operand reuse
-    if (g.bnt == 64 && mode_a <= RC && mode_b <= RC && g.bf16 != 2 && !smb && !getenv("ESP_GEMM_NO_BM64")) {
+    if (g.bnt == 64 && mode_a <= RC && mode_b <= RC && g.bf16 != 2 && !smb) {
       const long t = ntiles(64, 64);
       double c = (double)((t + 255) / 256) * 1.15;
       if (t < 2 * 256) c *= 1.3;
@@ -660,14 +633,8 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
     // gathered-B re-reads and split-K refills the chip (8.39 vs 9.22 ms at C2 B=128,
     // tools/gemm_bench.py with ESP_GEMM_BNT; the K ~ 48k linear weight gradients keep 128x64)
     if (mode_b == I2C_RC && work && K >= 65536) g.bnt = 128;
-    // 256 x 128 tiles for the bf16-operand GEMMs (ESP_GEMM_BM256=1, A/B measurements): twice the
-    // MFMA work per staged byte of the 128 x 128 tile, whose k-loop is load-bound at bf16 rates
-    static int bm256 = -1;
-    if (bm256 < 0) bm256 = getenv("ESP_GEMM_BM256") ? atoi(getenv("ESP_GEMM_BM256")) : 0;
-    if (bm256 && g.bf16 == 2 && g.bnt == 128 && mode_a <= RC && mode_b <= RC && !smb && M >= 4096) g.bm = 256;
-    static int force_bnt = -1;  // ESP_GEMM_BNT=64|128: tile width override (diagnostics)
-    if (force_bnt < 0) force_bnt = getenv("ESP_GEMM_BNT") ? atoi(getenv("ESP_GEMM_BNT")) : 0;
-    if ((force_bnt == 64 || force_bnt == 128) && N > 64 && g.bf16 != 5) g.bnt = force_bnt;
+    // (256 x 128 bf16 tiles -- one block, one wave per SIMD, per CU -- measured slower, C5 B=64 860.3 vs
+    // 889.3 utt/s, and were removed in round 5)
   }
   {
     const long tiles = ntiles(g.bnt ? g.bnt : BN, g.bm);
@@ -682,7 +649,7 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
       const long by_k = K / mink;
       if (sp > by_k) sp = by_k;
       // in-kernel combine (LDS-DMA kernel): partials on whole tiles + tickets in the last 64 KB
-      const int bmt = g.bm == 64 || g.bm == 256 ? g.bm : BM;
+      const int bmt = g.bm == 64 ? g.bm : BM;
       const long mp = (long)(M + bmt - 1) / bmt * bmt, np = g.bnt ? (long)(N + g.bnt - 1) / g.bnt * g.bnt : N;
       // opt-in (ESP_SPLITK_INKERNEL=1): measured slower at C2 B=128 -- the last-arriving unit of a
       // tile sums all of its splits alone (64 splits x 32 KB behind 8 tiles for the d x d weight
@@ -696,7 +663,7 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
       // CU balance: with ceil(tiles*sp / 256) tile-rounds on the busiest CU, 72 tiles x 8 splits
       // (conv2 weight gradient) leave a third of the chip idle in the last round; take the
       // smallest sp up to 4x the target-derived one whose last round is >= 95 % full.
-      if (sp >= 2 && !getenv("ESP_SPLITK_NOBALANCE")) {
+      if (sp >= 2) {
         // score the split count that is actually launched: the chunk is rounded up to BK, so
         // ceil(K / chunk) can be smaller than the candidate
         auto launched = [&](long s) {
@@ -806,7 +773,7 @@ static int conv2_dgrad_impl(const float* dz2, const void* dz2_16, const float* W
   ESP_CHECK_LAUNCH("esp_conv2_dgrad (weights)");
   // fp32 compute on split products: the class weights as B planes (PREC 3, no B split in the k-loop);
   // the bf16 form: their bf16 copy (plane 0 of the same conversion: hi = RNE)
-  const bool bp = !b16 && g_compute == 0 && ESP_F32_SPLIT && variant() == 4;
+  const bool bp = !b16 && g_compute == 0 && ESP_F32_SPLIT;
   const long ps = 9L * D * D;
   __bf16* planes = reinterpret_cast<__bf16*>(wc_work + ps);
   if (b16) {
@@ -852,12 +819,8 @@ static int conv2_dgrad_impl(const float* dz2, const void* dz2_16, const float* W
     }
     g.key = esp::rng_key_ptr();
     g.wide = 1;
-    static int dgrad_bnt = -1;  // ESP_CONV2_DGRAD_BNT=64|128 (measurements)
-    if (dgrad_bnt < 0) {
-      const char* e = getenv("ESP_CONV2_DGRAD_BNT");
-      dgrad_bnt = (e && atoi(e) == 64) ? 64 : 128;
-    }
-    g.batch = 1; g.splits = 1; g.kchunk = g.K; g.bnt = D % dgrad_bnt == 0 ? dgrad_bnt : 64; g.bm = BM;
+    // 128-wide tiles (64-wide measured 6.95 -> 8.69 ms per step, profiles/r04g_gemm_shapes_b128_gs_dg64.txt)
+    g.batch = 1; g.splits = 1; g.kchunk = g.K; g.bnt = D % 128 == 0 ? 128 : 64; g.bm = BM;
     g.cmap = 1;
     g.cm_hw = t.t_hw; g.cm_w = t.t_w;
     g.cm_T1 = T1; g.cm_F1 = F1; g.cm_ph = ph; g.cm_pw = pw;

@@ -1222,11 +1222,15 @@ struct GldsArgs {
   int t_T2, t_F2, t_C;
   int t_dt[4], t_df[4];
   const float* t_zeros;  // >= 16 zero bytes: the DMA source of lanes outside the grid
-  int abl;             // diagnostic ablation bits (ESP_GEMM_ABL, timing only): 1 no DMA after the
-                       // first slab, 2 no epilogue stores, 4 no k-loop barrier / waits, 16 dword
-                       // (not float4) epilogue stores, 32 non-temporal epilogue stores, 64 the
-                       // float4 (transposed) epilogue instead of the column epilogue (store_cols)
 };
+// Diagnostic ablation bits, compile time only (a separate build, e.g. make VARIANT=_abl
+// EXTRA=-DESP_GEMM_ABL_BITS=1; timing only, the outputs are wrong): 1 no DMA after the first slab,
+// 2 no epilogue stores, 4 no k-loop barrier / waits, 32 non-temporal epilogue stores, 64 the float4
+// (transposed) epilogue instead of the column epilogue (store_cols).  The product build has none.
+#ifndef ESP_GEMM_ABL_BITS
+#define ESP_GEMM_ABL_BITS 0
+#endif
+constexpr int kGemmAbl = ESP_GEMM_ABL_BITS;
 
 constexpr int GL_BK = 32;
 
@@ -2036,7 +2040,7 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
       }
     };
     auto finish_slab = [&]() {
-      if (!(x.abl & 4)) {
+      if (!(kGemmAbl & 4)) {
         wait_vm0();     // this wave's DMA of the next slab has landed
         wait_lgkm0();   // this wave's reads of this slab are done
         raw_barrier();  // -> everyone's: next slab readable, this buffer free for the one after
@@ -2047,7 +2051,7 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
     for (int kt = 0; kt + 1 < c.nk; ++kt) {  // all but the last slab: slab kt+1 streams in
       const int k1 = c.kbeg + (kt + 1) * GL_BK;
       float* nxt = smem + (buf ^ 1) * BUF;  // last read before the previous barrier
-      if (!(x.abl & 1)) issue_ab(k1, nxt);
+      if (!(kGemmAbl & 1)) issue_ab(k1, nxt);
       compute(smem + buf * BUF, GL_BK);
       finish_slab();
     }
@@ -2079,11 +2083,11 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
       float* Wz = g.work + ((long)c.split * g.batch + c.z) * ((long)g.sk_mp * g.sk_np);
       store_cols<EPI_P0, TM, TN, true, 16>(g, 0, g.sk_np, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, lane, acc, Wz);
       splitk_combine<BMT, BNT>(g, c.z, c.m0 / BMT, c.tn, x.ntx, x.nty, reinterpret_cast<int*>(smem + 2 * BUF));
-    } else if (!(x.abl & 2)) {
+    } else if (!(kGemmAbl & 2)) {
       float* W = g.splits > 1 ? g.work + ((long)c.split * g.batch + c.z) * (long)g.M * g.N : nullptr;
       if constexpr (EPI >= EPI_BIAS) {  // specialised kinds: never split-K, always wide
         const int mr0 = c.m0 + wm * TM * 32, nc0 = c.n0 + wn * TN * 32;
-        if (col_epi_ok<EPI>() && !(x.abl & 64) && mr0 + TM * 32 <= g.M && nc0 + TN * 32 <= g.N) {
+        if (col_epi_ok<EPI>() && !(kGemmAbl & 64) && mr0 + TM * 32 <= g.M && nc0 + TN * 32 <= g.N) {
           const long cb = c_base(g, c.z);
           if (g.alpha == 1.0f) store_cols<EPI, TM, TN, true>(g, cb, g.ldc, mr0, nc0, lane, acc, g.c);
           else store_cols<EPI, TM, TN, false>(g, cb, g.ldc, mr0, nc0, lane, acc, g.c);
@@ -2091,10 +2095,10 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
           store_spec_tiles<EPI, TM, TN>(g, c.z, mr0, nc0, lane, acc);
         }
       } else if (g.wide) {
-        if (W && !(x.abl & 64) && c.m0 + wm * TM * 32 + TM * 32 <= g.M && c.n0 + wn * TN * 32 + TN * 32 <= g.N)
+        if (W && !(kGemmAbl & 64) && c.m0 + wm * TM * 32 + TM * 32 <= g.M && c.n0 + wn * TN * 32 + TN * 32 <= g.N)
           store_cols<EPI_P0, TM, TN, true>(g, 0, g.N, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, lane, acc, W);
         else if (W) store_partials_wide<TM, TN>(g, W, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, lane, acc);
-        else store_tiles_wide<EPI, TM, TN>(g, c.z, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, lane, acc, (x.abl & 32) != 0);
+        else store_tiles_wide<EPI, TM, TN>(g, c.z, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, lane, acc, (kGemmAbl & 32) != 0);
       } else {
         if (W) store_partials<TM, TN>(g, W, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, h, l32, acc);
         else store_tiles<EPI, TM, TN>(g, c.z, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, h, l32, acc);
@@ -2150,15 +2154,6 @@ bool glds_switch(int ma, int mb, int bnt, int prec, int bm, F&& f) {
     if (bm == 64) {
       if constexpr (small_ok) {
         if (bnt == 64 && prec != 2) return by_prec(IC<64>{}, IC<64>{});  // (prec 5: A planes of 64 rows)
-      }
-      return false;
-    }
-    if (bm == 256) {  // 256 x 128 tiles: bf16 operands (PREC 2), KC / RC pairs
-      if constexpr (small_ok) {
-        if (bnt == 128 && prec == 2) {
-          f(A, B, IC<128>{}, IC<2>{}, IC<256>{});
-          return true;
-        }
       }
       return false;
     }

@@ -174,10 +174,10 @@ def profile_gemm_stop(by_shape: bool = False):
 # round-to-nearest-even cast of each operand; the batched attention contractions and the conv2
 # implicit-im2col GEMMs keep fp32 operands rounded to bf16 in LDS staging (PREC 1).  Same
 # numerics either way: bf16-rounded operands, fp32 accumulate and epilogue.
-# ESP_AMP_BF16_OPERANDS=0 keeps every GEMM on PREC 1 (A/B measurements).
-_AMP_BF16_OPERANDS = os.environ.get("ESP_AMP_BF16_OPERANDS", "1") == "1"
+# _AMP_BF16_OPERANDS = False keeps every GEMM on PREC 1 (A/B measurements).
+_AMP_BF16_OPERANDS = True
 # a Linear input's forward bf16 copy is kept for its weight gradient (_bf16_copy roles)
-_KEEP_X16 = os.environ.get("ESP_KEEP_X16", "1") == "1"
+_KEEP_X16 = True
 _COMPUTE = [0]  # mirror of esp_get_gemm_compute (set_gemm_compute)
 
 
@@ -218,15 +218,15 @@ class param_cast_scope:
 # fp32 GEMMs whose B operand is a weight take B as its three bf16 split planes (esp_gemm_f32_bp,
 # gemm_kernels.h PREC 3): the same split products as the in-register split, bit for bit, with only A
 # split in the k-loop.  A weight's planes are made once per step inside param_cast_scope (the
-# Trainer's step; keyed like _W16, holding the fp32 source), else per GEMM.  ESP_BPLANES=0: off
+# Trainer's step; keyed like _W16, holding the fp32 source), else per GEMM.  _BPLANES = False: off
 # (A/B measurements).
-_BPLANES = os.environ.get("ESP_BPLANES", "1") == "1"
+_BPLANES = True
 # producers of GEMM-only activations write them as Planes: by default in the bf16 mode only (n = 1, the
 # bf16 value its GEMMs round to: 805 vs 760 utt/s at C5 B=64); in the fp32 mode the consumers then
 # need both operands as planes (PREC 5, 64-wide tiles), measured slower than splitting A in registers
-# beside B's planes (PREC 3): 1222 vs 1333 utt/s at C2 B=128 (profiles/r04a_*).  ESP_XPLANES=1: both
-# modes, 0: neither (A/B measurements)
-_XPLANES = os.environ.get("ESP_XPLANES", "bf16")
+# beside B's planes (PREC 3): 1222 vs 1333 utt/s at C2 B=128 (profiles/r04a_*).  _XPLANES = True: both
+# modes, False: neither (tests/test_gpu_kernels.py sets both)
+_XPLANES = "bf16"
 _F32_PRODUCTS = [None]  # esp_f32_gemm_products() of the loaded build (set at first use)
 _WP = [None]
 
@@ -276,7 +276,7 @@ class Planes:
 
 def planes_mode() -> int:
     """Planes a producer writes for a GEMM-only tensor in the current compute mode: 3 (fp32 split
-    products), 1 (bf16 GEMM operands), 0 (write fp32: ESP_XPLANES=0 or an f32-MFMA build)."""
+    products), 1 (bf16 GEMM operands), 0 (write fp32: _XPLANES False or an f32-MFMA build)."""
     if not _XPLANES or _XPLANES == "0":
         return 0
     if _F32_PRODUCTS[0] is None:
@@ -289,8 +289,8 @@ def planes_mode() -> int:
 # Inside param_cast_scope, a parameter's bf16 copy / split planes are views into ONE copy of the whole
 # flat parameter buffer made by one launch at its first use in the step (the FlatParams slots are
 # 8-float aligned, so every weight's copy starts 16-B aligned): 155 per-weight launches per C2 step
-# become one.  ESP_FLAT_CAST=0: per-weight copies (A/B measurements).
-_FLAT_CAST = os.environ.get("ESP_FLAT_CAST", "1") == "1"
+# become one.  _FLAT_CAST = False: per-weight copies (A/B measurements).
+_FLAT_CAST = True
 
 
 def _param_flat(ptr: int, nbytes: int):
@@ -486,9 +486,9 @@ def gemm(M: int, N: int, K: int, A, B, C, *, mode_a=KC, lda, mode_b=KC, ldb, ldc
         _PROF.append((2.0 * M * N * K * batch, ev0, ev1, key, extra))
 
 
-# ESP_PLANES_DY_MEMO=0: the planes path casts a weight gradient's dy again for the input gradient
+# _PLANES_DY_MEMO = False: the planes path casts a weight gradient's dy again for the input gradient
 # (A/B measurements)
-_PLANES_DY_MEMO = os.environ.get("ESP_PLANES_DY_MEMO", "1") == "1"
+_PLANES_DY_MEMO = True
 
 
 def _gemm_planes(M, N, K, A, B, C, mode_a, lda, mode_b, ldb, ldc, a_off, b_off, c_off, bias, alpha, beta, R, r_off,
@@ -1030,21 +1030,21 @@ def attn_softmax_bwd_relpos(attn, dP, dS, dbd, ldp, drop_p, seed, sqrt_dk, rows,
                  seed, float(sqrt_dk), rows, T, lds, _p(tvalid), _st())
 
 
-FUSED_ATTN_BWD = os.environ.get("ESP_FUSED_ATTN_BWD", "0") == "1"
-# ESP_ATTN_FWD32=1: the 32-row-block fused forward (relpos_attn_fwd_kernel, latest only) instead of
+FUSED_ATTN_BWD = False
+# ATTN_FWD32 = True: the 32-row-block fused forward (relpos_attn_fwd_kernel, latest only) instead of
 # the 16-row-wave kernel (esp_relpos_attn_probs); kept for A/B measurements
-ATTN_FWD32 = os.environ.get("ESP_ATTN_FWD32", "0") == "1"
-# ESP_ATTN_DSCORES=1: the softmax / rel_shift adjoints in the dP GEMM's epilogue (esp_attn_dscores,
+ATTN_FWD32 = False
+# ATTN_DSCORES = True: the softmax / rel_shift adjoints in the dP GEMM's epilogue (esp_attn_dscores,
 # FlashAttention-2's row dot) instead of the dP GEMM + the row-wise adjoint pass.  Opt-in: measured
 # at C2 B=128 it is 412 + 73 us per layer against 59 + 266 (the epilogue's rel_shift scatter is one
 # scalar store per element; the row-wise pass writes each shifted bd row contiguously)
-ATTN_DSCORES = os.environ.get("ESP_ATTN_DSCORES", "0") == "1"
-# ESP_ATTN_BPLANES=1: the fp32 batched attention contractions whose B is qkv or the projected position
+ATTN_DSCORES = False
+# ATTN_BPLANES = True: the fp32 batched attention contractions whose B is qkv or the projected position
 # table (P.V, dP = dctx v^T, dS.k, dbd.p) take B as split planes made once per layer (PREC 3: only A
 # split in the k-loop) instead of splitting both operands in registers (PREC 0).  Opt-in: the
 # contractions gain 7-11 % but the two splits per layer cost more (C2 B=256 1337-1339 vs 1345-1351
 # utt/s, profiles/r04m_attn_bplanes_ab.txt) -- it pays once the qkv projection writes the planes itself
-ATTN_BPLANES = os.environ.get("ESP_ATTN_BPLANES", "0") == "1"
+ATTN_BPLANES = False
 
 
 def attn_bplanes_ok(D: int) -> bool:
@@ -1063,11 +1063,11 @@ def relpos_attn_bwd(dctx, ldd, vmat, ldv, attn, dS, dbd, ldp, nb, H, sqrt_dk, dr
 
 
 # Flash-style rel-pos attention (csrc/flash_relpos.hip), d_k = 64, T <= 512, latest and legacy.
-# Opt-in (ESP_FLASH_ATTN=1): in fp32 at T' = 374 the recompute it trades for the (Z,T,T)
+# Opt-in (FLASH_ATTN = True): in fp32 at T' = 374 the recompute it trades for the (Z,T,T)
 # probability traffic costs about what that traffic did (fp32 MFMA is 157 TF against 8 TB/s:
 # 32 flop per P byte at d_k = 64), and measured per layer at C2 B=128 (tools/flash_bench.py):
 # forward 0.84 vs 0.99 ms (flash wins), backward 2.10 vs 1.79 ms (materialised wins) -> off.
-FLASH_ATTN = os.environ.get("ESP_FLASH_ATTN", "0") == "1"
+FLASH_ATTN = False
 _DP_WS = _Workspace()
 
 
@@ -1248,9 +1248,9 @@ def global_mvn(x, lens_i32, mean, std, norm_means=True, norm_vars=True):
 _ZEROS = {}
 # conv2 input gradient as 4 implicit parity-class GEMMs with the ReLU mask in a specialised
 # row-mapped epilogue (EPI_RMASKMAP, 128-wide tiles): 10.2 ms vs 12.4 ms for the column GEMM +
-# col2im at C2 B=128 (tools/conv2_dgrad_bench.py), bench 1067 vs 1050 utt/s.  ESP_CONV2_IMPLICIT_DGRAD=0:
+# col2im at C2 B=128 (tools/conv2_dgrad_bench.py), bench 1067 vs 1050 utt/s.  CONV2_IMPLICIT_DGRAD = False:
 # the column path.
-CONV2_IMPLICIT_DGRAD = os.environ.get("ESP_CONV2_IMPLICIT_DGRAD", "1") == "1"
+CONV2_IMPLICIT_DGRAD = True
 
 
 def conv2_wgrad_bf16(dz2_16, z1_16, dw, db, B, T1, F1, D):

@@ -313,6 +313,12 @@ class Trainer:
                 # the stats, the buffer broadcast
                 self._dp_wsum(w_host, async_op=False)
                 stats, w, ctx = self._dp_body(e.speech, e.prep)
+                # the replay takes the batch weight from the host (prepare()'s copy) for sum w, the loss
+                # prescale and the stats average, where the eager path uses the device weight: they must
+                # agree (one sync per capture)
+                wd = float(w.view(-1)[0].item())
+                if wd != w_host:
+                    raise RuntimeError(f"graph DDP: device batch weight {wd} != host weight {w_host}")
                 self._dp_set_scale()
                 model.backward_explicit(ctx, self._scale)
                 del ctx
@@ -488,7 +494,11 @@ class Trainer:
         for _, batch in self._stop_aligned(iterator):
             if self.options.no_forward_run:
                 continue
-            _, stats, weight = self.model(**batch)
+            # one cast of the flat parameters per batch (param_cast_scope) instead of one planes copy per
+            # weight per GEMM; a scope per batch, so no batch's activation copies outlive it.  fp32 like
+            # the reference, whose validation runs outside autocast (trainer.py:724-772)
+            with K.gemm_compute("fp32"), K.param_cast_scope():
+                _, stats, weight = self.model(**batch)
             stats = {k: v for k, v in stats.items() if v is not None}
             if self.distributed:
                 stats, weight = fused_stats_allreduce(stats, weight)

@@ -141,9 +141,13 @@ class FlipProbe:
     from z2 ([B*T2*F2, D], post-ReLU), decoder layer l from its FFN's dh/dv (dact: keep * scale *
     (v > 0), rows b * L + position).  Use around the forward: `with FlipProbe(model) as fp: ...`."""
 
-    def __init__(self, model):
+    def __init__(self, model, copies=1):
         self.model = model
         self.ctx = {}
+        # copies > 1: the batch is the fixture's utterances repeated `copies` times (utterance-mean
+        # losses: each copy carries 1/copies of every per-utterance contribution), so a site's
+        # decision is the mean of its copies' decisions -- (mean - s64) x c is the exact correction
+        self.copies = copies
 
     def __enter__(self):
         from espnet_slurp_amd import blocks
@@ -167,6 +171,17 @@ class FlipProbe:
         self._b.Conv2dSubsampling.fwd, self._b.PositionwiseFeedForward.fwd = self._sub, self._ffn
 
     def decisions(self, site: str, idx: np.ndarray) -> np.ndarray:
+        if self.copies == 1:
+            return self._decisions(site, idx)
+        nb = self.ctx["conv"].B // self.copies
+        out = np.zeros(len(idx), dtype=np.float64)
+        for k in range(self.copies):
+            ik = idx.copy()
+            ik[:, 0] += k * nb  # the utterance index of copy k
+            out += self._decisions(site, ik)
+        return out / self.copies
+
+    def _decisions(self, site: str, idx: np.ndarray) -> np.ndarray:
         c = self.ctx["conv"]
         ix = torch.from_numpy(idx).to(c.z1.device)
         if site == "conv1":
@@ -239,4 +254,6 @@ def loss_gate(got, g, key="loss", slack=0.0):
     """|build - ref64| <= max(1e-4, 2 |ref32 - ref64|) (+ slack)."""
     l64, l32 = float(g[f"{key}_f64"]), float(g[f"{key}_f32"])
     tol = max(1e-4, 2 * abs(l32 - l64)) + slack
+    print(f"LOSS_GATE {key} err={abs(got - l64):.3e} e_ref={abs(l32 - l64):.3e} ulp32={float(np.spacing(np.float32(l64))):.3e} "
+          f"tol={tol:.3e} got={got!r} l64={l64!r}")
     return abs(got - l64) <= tol, (key, got, l64, tol)

@@ -680,6 +680,37 @@ def test_embed_bwd_many_rows(dev):
     assert (out.cpu().double() - ref).abs().max().item() < 1e-4
 
 
+def test_embed_bwd_grouped_rows_with_dropout_bit_exact(dev):
+    """The grouped-load path of embed_bwd_kernel (EMB_GROUP = 32 matching rows of a 256-row chunk
+    loaded before their adds): one token fills ~90 % of the rows (the decoder's eos padding), D not a
+    multiple of 256, dropout on.  Reference: dy dropped by esp_scale_dropout (the same element
+    indices r * D + d, so the same masks), then per vocab row an fp32 sum in ascending row order --
+    bit-equal, since the kernel's adds stay in that order (xscale a power of two: x * xscale exact)."""
+    nrows, V, D, p, seed = 1000, 40, 320, 0.1, 1234
+    g = torch.Generator().manual_seed(47)
+    tok = torch.randint(0, V - 3, (nrows,), generator=g)
+    tok[torch.rand(nrows, generator=g) < 0.9] = 7
+    dy = _r(nrows, D, seed=48)
+    dE0 = _r(V, D, seed=49)
+    dyd = torch.empty(nrows, D, device=dev)
+    K.scale_dropout(dy.to(dev), dyd, 1.0, p, seed)
+    y = (dyd.cpu().numpy() * np.float32(16.0)).astype(np.float32)
+    ref = dE0.numpy().copy()
+    tk = tok.numpy()
+    for v in range(V):
+        rows = np.nonzero(tk == v)[0]
+        if len(rows) == 0:
+            continue
+        acc = np.zeros(D, dtype=np.float32)
+        for r in rows:
+            acc = (acc + y[r]).astype(np.float32)
+        ref[v] = (ref[v] + acc).astype(np.float32)
+    out = dE0.to(dev)
+    K.embed_bwd(tok.to(dev), dy.to(dev), out, 16.0, p, seed)
+    got = out.cpu().numpy()
+    assert (tk == 7).sum() > 800 and np.array_equal(got, ref), np.abs(got - ref).max()
+
+
 def test_specaug_time_warp_unequal_lengths(dev):
     """Per-utterance branch of TimeWarp.forward (time_warp.py:76-86): each x[b, :len_b] is warped
     with its own (center, warped), the result zero-padded (pad_list(ys, 0.0)); an utterance too
