@@ -157,7 +157,7 @@ def test_two_rank_c2_shape_ddp_step(dev, tmp_path, mode):
     assert not bad, bad
     for r in res:
         for st in r["stats"]:
-            for key, slack in (("loss", 0.0), ("loss_att", 0.0), ("loss_ctc", 2e-4)):
+            for key, slack in (("loss", 0.0), ("loss_att", 0.0), ("loss_ctc", 0.0)):
                 ok, info = loss_gate(st[key], g, key, slack)
                 assert ok, info
             assert abs(st["acc"] - float(g["acc_f64"])) < 1e-6

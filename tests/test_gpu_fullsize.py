@@ -30,7 +30,7 @@ def test_fullsize_c2_train_step_grads(dev, rel):
     loss.backward()
     torch.cuda.synchronize()
     for key, got, slack in (("loss", loss.item(), 0.0), ("loss_att", stats["loss_att"].item(), 0.0),
-                            ("loss_ctc", stats["loss_ctc"].item(), 2e-4)):
+                            ("loss_ctc", stats["loss_ctc"].item(), 0.0)):
         ok, info = loss_gate(got, g, key, slack)
         assert ok, info
     assert abs(stats["acc"].item() - float(g["acc_f64"])) < 1e-6
@@ -59,7 +59,7 @@ def test_fullsize_c4_train_step_grads(dev):
     loss.backward()
     torch.cuda.synchronize()
     for key, got, slack in (("loss", loss.item(), 0.0), ("loss_att", stats["loss_att"].item(), 0.0),
-                            ("loss_ctc", stats["loss_ctc"].item(), 2e-4)):
+                            ("loss_ctc", stats["loss_ctc"].item(), 0.0)):
         ok, info = loss_gate(got, g, key, slack)
         assert ok, info
     assert abs(stats["acc"].item() - float(g["acc_f64"])) < 1e-6
@@ -78,7 +78,7 @@ def test_fullsize_c4_forward_loss(dev):
         loss, stats, _ = model(speech.to(dev), slen, text, tlen)
     ok, info = loss_gate(loss.item(), g)
     assert ok, info
-    ok, info = loss_gate(stats["loss_ctc"].item(), g, "loss_ctc", 2e-4)
+    ok, info = loss_gate(stats["loss_ctc"].item(), g, "loss_ctc")
     assert ok, info
 
 
@@ -108,7 +108,7 @@ def test_fullsize_c5_train_step_grads(dev):
     g = golden("fullsize_c5_grad_latest")
     model, loss, stats, fp = _c5_step(dev, g, False)
     for key, got, slack in (("loss", loss, 0.0), ("loss_att", stats["loss_att"].item(), 0.0),
-                            ("loss_ctc", stats["loss_ctc"].item(), 2e-4)):
+                            ("loss_ctc", stats["loss_ctc"].item(), 0.0)):
         ok, info = loss_gate(got, g, key, slack)
         assert ok, info
     assert abs(stats["acc"].item() - float(g["acc_f64"])) < 1e-6

@@ -55,7 +55,7 @@ def test_slurp_yaml_eval_step_matches_reference(dev):
         hs, _ = model.encode(speech.to(dev), slen)
         frames = model.ctc.argmax(hs).cpu().numpy()
     for key, got, slack in (("loss", loss.item(), 0.0), ("loss_att", stats["loss_att"].item(), 0.0),
-                            ("loss_ctc", stats["loss_ctc"].item(), 2e-4)):
+                            ("loss_ctc", stats["loss_ctc"].item(), 0.0)):
         ok, info = loss_gate(got, g, key, slack)
         assert ok, info
     # greedy CTC frames: >= 99.9 % agreement (ties), error rates on top of them
@@ -79,7 +79,7 @@ def test_slurp_yaml_train_step_grads(dev):
     loss.backward()
     torch.cuda.synchronize()
     for key, got, slack in (("loss", loss.item(), 0.0), ("loss_att", stats["loss_att"].item(), 0.0),
-                            ("loss_ctc", stats["loss_ctc"].item(), 2e-4)):
+                            ("loss_ctc", stats["loss_ctc"].item(), 0.0)):
         ok, info = loss_gate(got, g, key, slack)
         assert ok, info
     bad = grad_gate(model, g, flips=fp)
