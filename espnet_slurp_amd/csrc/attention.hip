@@ -801,6 +801,11 @@ __device__ __forceinline__ f32x4 mfma_np(const Frag16& a, const Frag16& b, f32x4
   return c;
 }
 
+// 1 (default): T' <= 384 runs relpos_probs_lds_kernel (block-staged operands, split products); 0: the
+// per-wave kernel for every T' (an A/B build: make VARIANT=_w EXTRA=-DESP_ATTN_PROBS_LDS=0)
+#ifndef ESP_ATTN_PROBS_LDS
+#define ESP_ATTN_PROBS_LDS 1
+#endif
 constexpr int RW_ROWS = 16, RW_PITCH = 37;
 // store-transpose rows: 64 floats, so the float4 read-back (ds_read_b128 lane groups of 16 lanes over
 // two rows, bank (a/4) mod 64) is conflict-free, with the column XOR-ed by 16 in rows 4..7 and 12..15
@@ -1086,6 +1091,301 @@ __global__ __launch_bounds__(256, 2) void relpos_attn_fwd16_kernel(
   else store_rows(std::false_type{});
 }
 
+// ---------------------------------------------------------------- rel-pos probabilities, block-staged operands
+// Round 5: the same result layout and softmax / dropout / store tail as relpos_attn_fwd16_kernel,
+// with the per-tile operands staged ONCE per block instead of fetched by every wave:
+// * a block = 4 waves = 64 consecutive query rows of one (head, utterance) z; at key tile t every
+//   wave needs key tile t, and wave w the band block of table positions pbase + 16 (t - w) + [0,16)
+//   (pbase = T' - i_block: the four waves' band windows are one block apart), so per step the block
+//   takes in ONE key tile and ONE new band block (4 KB each: a float4 per thread), splits each value
+//   once into its bf16 planes (split3_pair; the bf16 mode: the bf16 value alone) and writes them to
+//   LDS rings (key tiles: 2 slots; band blocks: 5 -- the four waves read blocks t-3..t while t+1 is
+//   written); one block barrier per tile;
+// * the ac and band products on v_mfma_f32_16x16x32_bf16 from those planes: NP = 6 the six split
+//   products of the GEMM family's fp32 arithmetic (hi.hi + hi.mid + mid.hi + hi.lo + lo.hi + mid.mid,
+//   smallest first; fp32-accurate, gemm_kernels.h PREC 0), NP = 1 the bf16 mode's single product.
+//   The query rows are split once per wave in registers.  Per tile and wave 24 (NP 6) MFMAs of 16
+//   cycles instead of 32 f32 MFMAs of 32 cycles, and no per-wave global fragment fetch (DESIGN 3.4:
+//   the fetches and the f32 MFMA issue were the kernel's two costs besides its stores).
+// Plane image of a 16-row tile: row r (64 bf16 = 128 B = 8 chunks of 16 B) holds chunk c at
+// c ^ swz16(r); a lane (li, q4) of MFMA m reads chunk 2 q4 + m of row li -- conflict-free ds_read_b128
+// for every 16-lane group (rows of one parity take distinct chunks; the XOR only uses bits {0, 2}).
+__device__ __forceinline__ int swz16(int r) { return ((r >> 1) & 1) | (r & 4); }
+template <int NPL>
+struct FragPl {
+  attn_bf16x8 v[NPL][2];  // [plane hi, mid, lo][MFMA m: dims 16 q4 + 8 m + 0..7]
+};
+template <int NPL>
+__device__ __forceinline__ void split_row16(const float (&f)[16], FragPl<NPL>& o) {
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    uint32_t h[4], md[4], l[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if constexpr (NPL == 3) esp::split3_pair(f[8 * m + 2 * j], f[8 * m + 2 * j + 1], h[j], md[j], l[j]);
+      else h[j] = esp::bf16_pair(f[8 * m + 2 * j], f[8 * m + 2 * j + 1]);
+    }
+    o.v[0][m] = __builtin_bit_cast(attn_bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
+    if constexpr (NPL == 3) {
+      o.v[1][m] = __builtin_bit_cast(attn_bf16x8, make_uint4(md[0], md[1], md[2], md[3]));
+      o.v[2][m] = __builtin_bit_cast(attn_bf16x8, make_uint4(l[0], l[1], l[2], l[3]));
+    }
+  }
+}
+template <int NPL>
+__device__ __forceinline__ void read_frag_pl(const uint8_t* tile, int plane_bytes, int li, int q4, FragPl<NPL>& o) {
+#pragma unroll
+  for (int p = 0; p < NPL; ++p)
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+      o.v[p][m] = *reinterpret_cast<const attn_bf16x8*>(tile + p * plane_bytes + li * 128 + (((2 * q4 + m) ^ swz16(li)) << 4));
+}
+// c += a . b over the 64 dims: NPL 3 the six split products smallest first per 32-dim half, NPL 1 hi.hi
+template <int NPL>
+__device__ __forceinline__ f32x4 mfma_pl(const FragPl<NPL>& a, const FragPl<NPL>& b, f32x4 c) {
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    if constexpr (NPL == 3) {
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[1][m], b.v[1][m], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[2][m], b.v[0][m], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[0][m], b.v[2][m], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[1][m], b.v[0][m], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[0][m], b.v[1][m], c, 0, 0, 0);
+    }
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v[0][m], b.v[0][m], c, 0, 0, 0);
+  }
+  return c;
+}
+
+template <int NTA, bool P2, bool LEGACY, int NP>  // NTA >= ceil(T / 16) key tiles; NP 6 (fp32) or 1 (bf16)
+__global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
+    const float* __restrict__ qu, const float* __restrict__ qv, const float* __restrict__ kmat, long ldk,
+    const float* __restrict__ pm, long ldpm, int nb, float sqrt_dk, const int* __restrict__ klen,
+    float* __restrict__ attn, float* __restrict__ pdrop, uint32_t thr, float dscale, uint64_t seed, int T, long lds,
+    const uint64_t* __restrict__ key, const int* __restrict__ tvalid, int nrb, int Z) {
+  constexpr int NPL = NP == 6 ? 3 : 1;
+  constexpr int PLB = RW_ROWS * 128;  // bytes of one plane of a 16-row tile
+  constexpr int PSL = 5;              // band-block ring slots
+  __shared__ __attribute__((aligned(16))) uint8_t kpl[2][NPL * PLB];
+  __shared__ __attribute__((aligned(16))) uint8_t ppl[PSL][NPL * PLB];
+  __shared__ float ring[4][RW_ROWS * RW_PITCH];
+  __shared__ __attribute__((aligned(16))) float stage[4][RW_ROWS * RW_SPITCH];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // XCD-aware block order, as relpos_attn_fwd16_kernel: a z's row blocks on one XCD
+  const int xcd = blockIdx.x & 7, jb = blockIdx.x >> 3, zq = jb / nrb;
+  const int z = zq * 8 + xcd, bx = jb - zq * nrb;
+  if (z >= Z) return;  // the whole block (nothing has synchronised yet)
+  const int ib = bx * 4 * RW_ROWS;  // the block's first query row
+  const int i0 = ib + wave * RW_ROWS;
+  // (a wave whose rows all lie past T still stages and synchronises with the block; it stores nothing)
+  seed = esp::keyed(seed, key);
+  const int head = z / nb, b = z - head * nb;
+  const int li = lane & 15, q4 = lane >> 4;
+  const int g = i0 >> 4;
+  const int Ts = LEGACY ? legacy_tv(tvalid, T) : T;
+  const int P = LEGACY ? T : 2 * T - 1;
+  const int pbase = Ts - ib;  // band block u: table positions pbase + 16 u + [0, 16)
+  const float inv_sqrt_dk = 1.0f / sqrt_dk;
+  float* ring0 = ring[wave];
+  auto pslot = [](int u) { return ((u % PSL) + PSL) % PSL; };
+
+  // staging: thread -> row sr of the tile, dims sd..sd+3 (one float4; 16 threads per 256-B row)
+  const int sr = tid >> 4, sd = 4 * (tid & 15);
+  const int woff = sr * 128 + (((sd >> 3) ^ swz16(sr)) << 4) + ((sd >> 2) & 1) * 8;
+  auto k_src = [&](int t) {
+    return reinterpret_cast<const float4*>(kmat + ((long)b * T + min(t * 16 + sr, T - 1)) * ldk + head * RP_DK + sd);
+  };
+  auto p_src = [&](int u) {
+    int pos = pbase + 16 * u + sr;
+    if (LEGACY && pos > Ts) pos -= Ts + 1;  // the shifted band's table: p[j - i - 2]
+    return reinterpret_cast<const float4*>(pm + (long)min(max(pos, 0), P - 1) * ldpm + head * RP_DK + sd);
+  };
+  auto put_tile = [&](uint8_t* dst, const float4 v) {
+    if constexpr (NPL == 3) {
+      uint32_t h0, m0, l0, h1, m1, l1;
+      esp::split3_pair(v.x, v.y, h0, m0, l0);
+      esp::split3_pair(v.z, v.w, h1, m1, l1);
+      *reinterpret_cast<uint2*>(dst + woff) = make_uint2(h0, h1);
+      *reinterpret_cast<uint2*>(dst + PLB + woff) = make_uint2(m0, m1);
+      *reinterpret_cast<uint2*>(dst + 2 * PLB + woff) = make_uint2(l0, l1);
+    } else {
+      *reinterpret_cast<uint2*>(dst + woff) = make_uint2(esp::bf16_pair(v.x, v.y), esp::bf16_pair(v.z, v.w));
+    }
+  };
+  {  // prologue: band blocks u = -4..0 (wave w starts at u = -1 - w) and key tile 0
+    float4 pv[PSL];
+#pragma unroll
+    for (int s = 0; s < PSL; ++s) pv[s] = *p_src(s - 4);
+    const float4 kv = *k_src(0);
+#pragma unroll
+    for (int s = 0; s < PSL; ++s) put_tile(ppl[pslot(s - 4)], pv[s]);
+    put_tile(kpl[0], kv);
+  }
+  // the wave's query rows (d = 16 q4 + 0..15, contiguous: the plane images' order), split once
+  auto ld16c = [&](const float* row, float (&f)[16]) {
+    const float4* r4 = reinterpret_cast<const float4*>(row + 16 * q4);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float4 v = r4[u];
+      f[4 * u] = v.x; f[4 * u + 1] = v.y; f[4 * u + 2] = v.z; f[4 * u + 3] = v.w;
+    }
+  };
+  FragPl<NPL> xu, xv;
+  {
+    float f[16];
+    ld16c(qu + ((long)z * T + min(i0 + li, T - 1)) * RP_DK, f);
+    split_row16(f, xu);
+    ld16c(qv + ((long)z * T + min(i0 + li, T - 1)) * RP_DK, f);
+    split_row16(f, xv);
+  }
+  int kl = klen ? klen[b] : T;
+  if (kl > T) kl = T;
+  auto put_band = [&](float* rg, int m, const f32x4& s) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rg[(4 * q4 + r) * RW_PITCH + ((16 * m + li) & 31)] = s[r];
+  };
+  __syncthreads();
+  {  // band block 0 of this wave (u = -1 - w; below T for every g: A rows q_v[i] in both variants)
+    FragPl<NPL> pf;
+    read_frag_pl(ppl[pslot(-1 - wave)], PLB, li, q4, pf);
+    put_band(ring0, 0, mfma_pl(xv, pf, f32x4{0.f, 0.f, 0.f, 0.f}));
+  }
+
+  f32x4 sc[NTA];
+#pragma unroll
+  for (int t = 0; t < NTA; ++t) {
+    // the next step's key tile and band block: requested now, split into LDS after this tile's work
+    float4 nk, np;
+    if (t + 1 < NTA) {
+      nk = *k_src(t + 1);
+      np = *p_src(t + 1);
+    }
+    FragPl<NPL> kf, pf;
+    read_frag_pl(kpl[t & 1], PLB, li, q4, kf);
+    read_frag_pl(ppl[pslot(t - wave)], PLB, li, q4, pf);
+    if (LEGACY && t == g) {  // band block t+1 = g+1: the first shifted block -- its A rows are q_v[i+1]
+      float f[16];
+      ld16c(qv + ((long)z * T + min(i0 + 1 + li, T - 1)) * RP_DK, f);
+      split_row16(f, xv);
+    }
+    const f32x4 a = mfma_pl(xu, kf, f32x4{0.f, 0.f, 0.f, 0.f});
+    const f32x4 s = mfma_pl(xv, pf, f32x4{0.f, 0.f, 0.f, 0.f});
+    put_band(ring0, t + 1, s);
+    asm volatile("" ::: "memory");  // ring writes before the shifted reads (LDS is in order per wave)
+    const int j = t * 16 + li;
+    float bdv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ii = 4 * q4 + r;
+      bdv[r] = ring0[ii * RW_PITCH + ((t * 16 + li - ii + 15) & 31)];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int ii = 4 * q4 + r, i = i0 + ii;
+      float bd = bdv[r];
+      if (LEGACY && j == i + 1) bd = 0.f;
+      const float sv = a[r] + bd;
+      sc[t][r] = j < kl ? (P2 ? sv * inv_sqrt_dk : sv / sqrt_dk) : -INFINITY;
+    }
+    asm volatile("" ::: "memory");  // ... and these reads before the next tile's ring writes
+    if (t + 1 < NTA) {
+      put_tile(kpl[(t + 1) & 1], nk);
+      put_tile(ppl[pslot(t + 1)], np);
+      __syncthreads();  // step t+1's planes written; every wave done reading the slots they replaced
+    }
+  }
+
+  // softmax over each row: a row's keys sit in the 16 lanes of one quarter x NTA tiles
+  float nm[4], inv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float v = sc[0][r];
+#pragma unroll
+    for (int t = 1; t < NTA; ++t) v = fmaxf(v, sc[t][r]);
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    v = v == -INFINITY ? 0.f : v;  // fully masked row: every e below is exp(-inf) = 0
+    nm[r] = P2 ? -v * 1.4426950408889634f : -v;
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float v = 0.f;
+#pragma unroll
+    for (int t = 0; t < NTA; ++t) {
+      const float x = sc[t][r];
+      const float e = P2 ? __builtin_amdgcn_exp2f(fmaf(x, 1.4426950408889634f, nm[r])) : expf(x + nm[r]);
+      sc[t][r] = e;
+      v += e;
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) v += __shfl_xor(v, o, 64);
+    inv[r] = v > 0.f ? 1.0f / v : 0.f;
+  }
+  // probabilities -> HBM through the per-wave LDS transpose (relpos_attn_fwd16_kernel's tail)
+  float* stg = stage[wave];
+  const int sr2 = lane >> 4, sc4 = 4 * (lane & 15);
+  float* abase[4];
+  float* dbase[4];
+  uint64_t ibase[4];
+  bool rok[4];
+#pragma unroll
+  for (int ps = 0; ps < 4; ++ps) {
+    const int i = i0 + 4 * ps + sr2;
+    rok[ps] = i < T;
+    const long row = (long)z * T + min(i, T - 1);
+    abase[ps] = attn + row * lds + sc4;
+    dbase[ps] = pdrop ? pdrop + row * lds + sc4 : nullptr;
+    ibase[ps] = (uint64_t)(row * T + sc4);
+  }
+  const bool even_T = (T & 1) == 0;
+  const bool idx32 = (uint64_t)Z * (uint64_t)T * (uint64_t)T <= 0xffffffffull;
+  auto store_rows = [&](auto drop_c) {
+    constexpr bool DROP = decltype(drop_c)::value;
+#pragma unroll
+    for (int t4 = 0; t4 < NTA; t4 += 4) {
+      if (16 * t4 >= T) break;
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) stg[(4 * q4 + r) * RW_SPITCH + ((16 * tt + li) ^ (16 * (q4 & 1)))] = sc[t4 + tt][r] * inv[r];
+      asm volatile("" ::: "memory");
+      const bool jok = 16 * t4 + sc4 < T;
+#pragma unroll
+      for (int ps = 0; ps < 4; ++ps) {
+        const float4 v = *reinterpret_cast<const float4*>(stg + (4 * ps + sr2) * RW_SPITCH + (sc4 ^ (16 * (ps & 1))));
+        if (rok[ps] && jok) {
+          *reinterpret_cast<float4*>(abase[ps] + 16 * t4) = v;
+          if (DROP) {
+            const uint64_t ix = ibase[ps] + 16 * t4;
+            float4 d;
+            bool k0, k1, k2, k3;
+            if (even_T && idx32) {
+              esp::keep_pair32(seed, (uint32_t)ix, thr, k0, k1);
+              esp::keep_pair32(seed, (uint32_t)ix + 2, thr, k2, k3);
+            } else if (even_T) {
+              esp::keep_pair(seed, ix, thr, k0, k1);
+              esp::keep_pair(seed, ix + 2, thr, k2, k3);
+            } else {
+              k0 = esp::keep_elem(seed, ix, thr);
+              k1 = esp::keep_elem(seed, ix + 1, thr);
+              k2 = esp::keep_elem(seed, ix + 2, thr);
+              k3 = esp::keep_elem(seed, ix + 3, thr);
+            }
+            d.x = k0 ? v.x * dscale : 0.f;
+            d.y = k1 ? v.y * dscale : 0.f;
+            d.z = k2 ? v.z * dscale : 0.f;
+            d.w = k3 ? v.w * dscale : 0.f;
+            *reinterpret_cast<float4*>(dbase[ps] + 16 * t4) = d;
+          }
+        }
+      }
+      asm volatile("" ::: "memory");
+    }
+  };
+  if (pdrop) store_rows(std::true_type{});
+  else store_rows(std::false_type{});
+}
+
 inline int gridn(long n) {
   long b = (n + 255) / 256;
   return (int)(b > 65536 ? 65536 : (b < 1 ? 1 : b));
@@ -1288,6 +1588,38 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
   dim3 grid((unsigned)(8 * ((Zn + 7) / 8) * nrb));  // XCD-aware order (see the kernel)
   hipStream_t st = (hipStream_t)stream;
   const bool p2 = sqrt_dk > 0.f && (__builtin_bit_cast(uint32_t, sqrt_dk) & 0x7fffffu) == 0;
+  if (ESP_ATTN_PROBS_LDS && nt <= 24) {
+    // block-staged operands, split products (relpos_probs_lds_kernel): fp32-accurate six products in
+    // the fp32 mode, the single bf16 product in the bf16 mode (like every other product of its step)
+    const bool b16 = esp_get_gemm_compute() == 1;
+#define ESP_RL(N, P2_, L_, NP_)                                                                                     \
+  hipLaunchKernelGGL((relpos_probs_lds_kernel<N, P2_, L_, NP_>), grid, dim3(256), 0, st, qu, qv, kmat, ldk, p,     \
+                     ldp_row, nb, sqrt_dk, klen, attn, pdrop, thr, ds, (uint64_t)seed, T, lds, esp::rng_key_ptr(), \
+                     tvalid, nrb, Zn)
+#define ESP_RLN(N, P2_, L_)          \
+  do {                               \
+    if (b16) ESP_RL(N, P2_, L_, 1);  \
+    else ESP_RL(N, P2_, L_, 6);      \
+  } while (0)
+#define ESP_RLT(N)                                 \
+  do {                                             \
+    if (relpos == 2) {                             \
+      if (p2) ESP_RLN(N, true, true);              \
+      else ESP_RLN(N, false, true);                \
+    } else {                                       \
+      if (p2) ESP_RLN(N, true, false);             \
+      else ESP_RLN(N, false, false);               \
+    }                                              \
+  } while (0)
+    if (nt <= 8) ESP_RLT(8);
+    else if (nt <= 16) ESP_RLT(16);
+    else ESP_RLT(24);
+#undef ESP_RLT
+#undef ESP_RLN
+#undef ESP_RL
+    ESP_CHECK_LAUNCH("esp_relpos_attn_probs");
+    return 0;
+  }
   // the bf16 mode computes the scores on bf16 operands like every other product of its step
   if (esp_get_gemm_compute() == 1) {
 #define ESP_RX(N, P2_, L_)                                                                                         \

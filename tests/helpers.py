@@ -251,9 +251,17 @@ def grad_gate(model, g, skip_rel=1e-6, flips=None):
 
 
 def loss_gate(got, g, key="loss", slack=0.0):
-    """|build - ref64| <= max(1e-4, 2 |ref32 - ref64|) (+ slack)."""
+    """|build - ref64| <= max(1e-4, 2 |ref32 - ref64|) (+ slack) on the loss.
+    The component losses (loss_ctc ~ 1.6e3-1.9e3, loss_att) are gated the same way with one more floor:
+    one fp32 ulp of the value (1.22e-4 at loss_ctc's magnitude).  An fp32 number of that size is a
+    multiple of its ulp, so an atol below one ulp demands the correctly rounded result, which no fp32
+    pipeline promises -- the reference's own fp32 loss_ctc is off by 5.6e-6 .. 7.4e-4 (0.05 .. 6 ulp)
+    across the committed fixtures; a 1-ulp difference is a rounding-order difference, not a defect.
+    The total loss (~700, ulp 6.1e-5) keeps the plain max(1e-4, 2 e_ref)."""
     l64, l32 = float(g[f"{key}_f64"]), float(g[f"{key}_f32"])
     tol = max(1e-4, 2 * abs(l32 - l64)) + slack
+    if key != "loss":
+        tol = max(tol, float(np.spacing(np.float32(abs(l64)))))
     print(f"LOSS_GATE {key} err={abs(got - l64):.3e} e_ref={abs(l32 - l64):.3e} ulp32={float(np.spacing(np.float32(l64))):.3e} "
           f"tol={tol:.3e} got={got!r} l64={l64!r}")
     return abs(got - l64) <= tol, (key, got, l64, tol)
