@@ -1170,7 +1170,7 @@ __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
   __shared__ __attribute__((aligned(16))) uint8_t ppl[PSL][NPL * PLB];
   __shared__ float ring[4][RW_ROWS * RW_PITCH];
   __shared__ __attribute__((aligned(16))) float stage[4][RW_ROWS * RW_SPITCH];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // XCD-aware block order, as relpos_attn_fwd16_kernel: a z's row blocks on one XCD
   const int xcd = blockIdx.x & 7, jb = blockIdx.x >> 3, zq = jb / nrb;
   const int z = zq * 8 + xcd, bx = jb - zq * nrb;
@@ -1252,13 +1252,18 @@ __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
   }
 
   f32x4 sc[NTA];
+  // key tiles / band blocks two steps ahead in registers (slot s & 1 holds step s's): a step's loads
+  // have two steps of work to arrive before they are split into LDS
+  float4 nk[2], np[2];
+  if (NTA > 1) {
+    nk[1] = *k_src(1);
+    np[1] = *p_src(1);
+  }
 #pragma unroll
   for (int t = 0; t < NTA; ++t) {
-    // the next step's key tile and band block: requested now, split into LDS after this tile's work
-    float4 nk, np;
-    if (t + 1 < NTA) {
-      nk = *k_src(t + 1);
-      np = *p_src(t + 1);
+    if (t + 2 < NTA) {
+      nk[t & 1] = *k_src(t + 2);
+      np[t & 1] = *p_src(t + 2);
     }
     FragPl<NPL> kf, pf;
     read_frag_pl(kpl[t & 1], PLB, li, q4, kf);
@@ -1289,8 +1294,8 @@ __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
     }
     asm volatile("" ::: "memory");  // ... and these reads before the next tile's ring writes
     if (t + 1 < NTA) {
-      put_tile(kpl[(t + 1) & 1], nk);
-      put_tile(ppl[pslot(t + 1)], np);
+      put_tile(kpl[(t + 1) & 1], nk[(t + 1) & 1]);
+      put_tile(ppl[pslot(t + 1)], np[(t + 1) & 1]);
       __syncthreads();  // step t+1's planes written; every wave done reading the slots they replaced
     }
   }

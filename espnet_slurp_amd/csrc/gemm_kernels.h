@@ -42,6 +42,11 @@ constexpr int BM = 128, BN = 128, BK = 32, NT = 256;  // BK: split-K granularity
 #ifndef ESP_F32_SPLIT
 #define ESP_F32_SPLIT 1
 #endif
+// 1 (default): the fp32 split-product GEMMs run the software-pipelined k-loop (gemm_glds_kernel PIPE);
+// 0: the round-4 k-loop (an A/B build: make VARIANT=_np EXTRA=-DESP_GEMM_PIPE=0)
+#ifndef ESP_GEMM_PIPE
+#define ESP_GEMM_PIPE 1
+#endif
 
 enum Mode { KC = 0, RC = 1, I2C_KC = 2, I2C_RC = 3, I2CT_KC = 4 };
 enum Act { ACT_NONE = 0, ACT_RELU = 1, ACT_SWISH = 2, ACT_MUL = 3 /* bwd_act only: v *= pre */ };
@@ -1605,6 +1610,23 @@ __device__ __forceinline__ void frag16(const float* slab, int r, int h, float (&
   }
 }
 
+// half of frag16: the 8 k-values k = 16h + 8hs + s (s = 0..7) of tile row r -- the values the fp32
+// split products of k-step hs take (PREC 0 / 3), read one k-step ahead in the pipelined k-loop
+template <int MODE, int ROWS>
+__device__ __forceinline__ void frag8(const float* slab, int r, int h, int hs, float (&f)[8]) {
+  if constexpr (MODE == KC || MODE == I2C_KC || MODE == I2CT_KC) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float4 v = *reinterpret_cast<const float4*>(slab + (r * 8 + ((4 * h + 2 * hs + j) ^ kc_swz(r))) * 4);
+      f[4 * j + 0] = v.x; f[4 * j + 1] = v.y; f[4 * j + 2] = v.z; f[4 * j + 3] = v.w;
+    }
+  } else {
+    const int rr = r ^ (h << 5);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) f[s] = slab[(16 * h + 8 * hs + s) * ROWS + rr];
+  }
+}
+
 __device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 // s_barrier without __syncthreads()'s fence (which would drain vmcnt); the empty asm keeps
@@ -1702,6 +1724,22 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
   static_assert(PREC != 5 || MA == KC || MA == RC, "A planes: KC / RC operands");
   constexpr bool BP = PREC >= 3;                 // B as three bf16 planes (StageP)
   constexpr bool AP = PREC == 5;                 // A as three bf16 planes too: no split in the k-loop
+  // the software-pipelined k-loop (k-step fragments one step ahead, the barrier between k-steps):
+  // the fp32 split-product forms with A split in registers
+  // (KC x RC only: measured at C2 B=256 the FFN input gradient 346 -> 305 us, the dgrad / P.V shapes
+  // 1-1.3 % faster, while the RC x RC weight gradients and the conv2 GEMMs ran 3-8 % slower with it,
+  // profiles/r05c_gemm_pipe_ab.txt)
+  constexpr bool PIPE = ESP_GEMM_PIPE && ESP_F32_SPLIT && (PREC == 0 || PREC == 3) && MA == KC && MB == RC;
+  struct FragA {
+    float v[TM][8];
+  };
+  struct FragBf {
+    float v[TN][8];
+  };
+  struct FragBp {
+    bf16x8 v[TN][3];
+  };
+  using FragB = std::conditional_t<BP, FragBp, FragBf>;
   constexpr int PLF = BNT * 16;                  // floats per B plane image (BNT x 32 bf16)
   constexpr int PLA = BMT * 16;                  // floats per A plane image
   constexpr int A_SZ = AP ? 3 * PLA : BMT * GL_BK, B_SZ = BP ? 3 * PLF : BNT * GL_BK, BUF = A_SZ + B_SZ;
@@ -2039,6 +2077,70 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
         }
       }
     };
+    // one k-step (hs) of the fp32 split products: A's 8 values per tile row, B's 8 values (PREC 0) or
+    // its three planes (PREC 3)
+    auto load_half = [&](const float* cur, int hs, FragA& a, FragB& b) {
+      if constexpr (PIPE) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) frag8<MA, BMT>(cur, wm * TM * 32 + i * 32 + l32, h, hs, a.v[i]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (BP) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) {
+              if constexpr (MB == KC) b.v[j][p] = frag_pl_kc(cur + A_SZ + p * PLF, wn * TN * 32 + j * 32 + l32, h, hs);
+              else b.v[j][p] = frag_pl_rc<BNT>(cur + A_SZ + p * PLF, wn * TN * 32 + j * 32, lane, hs);
+            }
+          } else {
+            frag8<MB, BNT>(cur + A_SZ, wn * TN * 32 + j * 32 + l32, h, hs, b.v[j]);
+          }
+        }
+      }
+    };
+    auto mma_half = [&](int hs, int kv, FragA& a, FragB& b) {
+      if constexpr (PIPE) {
+        if (kv < GL_BK) {  // K tail: A's k >= kv are 0 (B's clamped tail holds finite values)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a.v[i][e] = 16 * h + 8 * hs + e < kv ? a.v[i][e] : 0.f;
+        }
+        bf16x8 ah[TM][3], bh[TN][3];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) split3_bf16(a.v[i], ah[i][0], ah[i][1], ah[i][2]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          if constexpr (BP) {
+#pragma unroll
+            for (int p = 0; p < 3; ++p) bh[j][p] = b.v[j][p];
+          } else {
+            split3_bf16(b.v[j], bh[j][0], bh[j][1], bh[j][2]);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][1], bh[j][1], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][2], bh[j][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][2], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][1], bh[j][0], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][1], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][0], acc[i][j], 0, 0, 0);
+          }
+        if constexpr (RS) {
+          if (do_rs) {  // after the MFMAs were issued: the adds ride in their shadow
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+              float a0 = 0.f;
+#pragma unroll
+              for (int e = 0; e < 8; ++e) a0 += a.v[i][e];
+              rs[i] += a0;
+            }
+          }
+        }
+      }
+    };
     auto finish_slab = [&]() {
       if (!(kGemmAbl & 4)) {
         wait_vm0();     // this wave's DMA of the next slab has landed
@@ -2048,23 +2150,53 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
       buf ^= 1;
     };
 
-    for (int kt = 0; kt + 1 < c.nk; ++kt) {  // all but the last slab: slab kt+1 streams in
-      const int k1 = c.kbeg + (kt + 1) * GL_BK;
-      float* nxt = smem + (buf ^ 1) * BUF;  // last read before the previous barrier
-      if (!(kGemmAbl & 1)) issue_ab(k1, nxt);
-      compute(smem + buf * BUF, GL_BK);
-      finish_slab();
-    }
-    {  // last slab: the next tile's first slab streams in (this tile's stages are done)
-      float* cur = smem + buf * BUF;
-      float* nxt = smem + (buf ^ 1) * BUF;
-      if (has_next) {
-        cn = tile_coord<BNT, BMT>(g, x, tnext, G);
-        init_ab(cn);
-        issue_ab(cn.kbeg, nxt);
+    if constexpr (PIPE) {
+      // fp32 split products (PREC 0 / 3), software-pipelined by k-step: the fragments of k-step hs+1
+      // are read while the MFMAs of k-step hs issue, and the slab barrier sits BETWEEN a slab's two
+      // k-steps -- after it the wave issues k-step 1's MFMAs (operands already in registers) while
+      // the next slab's first fragments are read, instead of waiting out a fragment read + split
+      // after every barrier.  The fragments of k-step 1 are read before the barrier (that buffer is
+      // re-filled right after it); the MFMAs, their order and the fused row sums are those of compute().
+      FragA Fa, Ga;
+      FragB Fb, Gb;
+      load_half(smem + buf * BUF, 0, Fa, Fb);
+      for (int kt = 0; kt < c.nk; ++kt) {
+        float* cur = smem + buf * BUF;
+        float* nxt = smem + (buf ^ 1) * BUF;  // last read before the previous barrier
+        const bool last = kt + 1 == c.nk;
+        if (!last) {
+          if (!(kGemmAbl & 1)) issue_ab(c.kbeg + (kt + 1) * GL_BK, nxt);
+        } else if (has_next) {  // the next tile's first slab streams in (this tile's stages are done)
+          cn = tile_coord<BNT, BMT>(g, x, tnext, G);
+          init_ab(cn);
+          issue_ab(cn.kbeg, nxt);
+        }
+        const int kv = last ? c.kend - (c.kbeg + kt * GL_BK) : GL_BK;
+        load_half(cur, 1, Ga, Gb);
+        mma_half(0, kv, Fa, Fb);
+        finish_slab();
+        if (!last) load_half(smem + buf * BUF, 0, Fa, Fb);
+        mma_half(1, kv, Ga, Gb);
       }
-      compute(cur, c.kend - (c.kbeg + (c.nk - 1) * GL_BK));
-      finish_slab();
+    } else {
+      for (int kt = 0; kt + 1 < c.nk; ++kt) {  // all but the last slab: slab kt+1 streams in
+        const int k1 = c.kbeg + (kt + 1) * GL_BK;
+        float* nxt = smem + (buf ^ 1) * BUF;  // last read before the previous barrier
+        if (!(kGemmAbl & 1)) issue_ab(k1, nxt);
+        compute(smem + buf * BUF, GL_BK);
+        finish_slab();
+      }
+      {  // last slab: the next tile's first slab streams in (this tile's stages are done)
+        float* cur = smem + buf * BUF;
+        float* nxt = smem + (buf ^ 1) * BUF;
+        if (has_next) {
+          cn = tile_coord<BNT, BMT>(g, x, tnext, G);
+          init_ab(cn);
+          issue_ab(cn.kbeg, nxt);
+        }
+        compute(cur, c.kend - (c.kbeg + (c.nk - 1) * GL_BK));
+        finish_slab();
+      }
     }
     // epilogue: fire-and-forget stores that drain under the next tile's first slab
     if (RS && do_rs) {
