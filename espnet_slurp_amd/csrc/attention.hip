@@ -806,6 +806,10 @@ __device__ __forceinline__ f32x4 mfma_np(const Frag16& a, const Frag16& b, f32x4
 #ifndef ESP_ATTN_PROBS_LDS
 #define ESP_ATTN_PROBS_LDS 1
 #endif
+// staging steps in flight in relpos_probs_lds_kernel (2: 573 us per C2 B=256 launch, 1: 639)
+#ifndef ESP_ATTN_PREFETCH
+#define ESP_ATTN_PREFETCH 3
+#endif
 constexpr int RW_ROWS = 16, RW_PITCH = 37;
 // store-transpose rows: 64 floats, so the float4 read-back (ds_read_b128 lane groups of 16 lanes over
 // two rows, bank (a/4) mod 64) is conflict-free, with the column XOR-ed by 16 in rows 4..7 and 12..15
@@ -1252,18 +1256,21 @@ __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
   }
 
   f32x4 sc[NTA];
-  // key tiles / band blocks two steps ahead in registers (slot s & 1 holds step s's): a step's loads
-  // have two steps of work to arrive before they are split into LDS
-  float4 nk[2], np[2];
-  if (NTA > 1) {
-    nk[1] = *k_src(1);
-    np[1] = *p_src(1);
-  }
+  // key tiles / band blocks PF steps ahead in registers (slot s % PF holds step s's): a step's loads
+  // have PF steps of work to arrive before they are split into LDS
+  constexpr int PF = ESP_ATTN_PREFETCH;
+  float4 nk[PF], np[PF];
+#pragma unroll
+  for (int s = 1; s < PF; ++s)
+    if (s < NTA) {
+      nk[s % PF] = *k_src(s);
+      np[s % PF] = *p_src(s);
+    }
 #pragma unroll
   for (int t = 0; t < NTA; ++t) {
-    if (t + 2 < NTA) {
-      nk[t & 1] = *k_src(t + 2);
-      np[t & 1] = *p_src(t + 2);
+    if (t + PF < NTA) {
+      nk[t % PF] = *k_src(t + PF);
+      np[t % PF] = *p_src(t + PF);
     }
     FragPl<NPL> kf, pf;
     read_frag_pl(kpl[t & 1], PLB, li, q4, kf);
@@ -1294,8 +1301,8 @@ __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
     }
     asm volatile("" ::: "memory");  // ... and these reads before the next tile's ring writes
     if (t + 1 < NTA) {
-      put_tile(kpl[(t + 1) & 1], nk[(t + 1) & 1]);
-      put_tile(ppl[pslot(t + 1)], np[(t + 1) & 1]);
+      put_tile(kpl[(t + 1) & 1], nk[(t + 1) % PF]);
+      put_tile(ppl[pslot(t + 1)], np[(t + 1) % PF]);
       __syncthreads();  // step t+1's planes written; every wave done reading the slots they replaced
     }
   }
