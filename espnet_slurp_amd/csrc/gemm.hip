@@ -133,6 +133,12 @@ long splitk_mink() { return kSplitkMinK; }
 // work units split-K aims for: two resident blocks on each of 256 CUs (256 / 384 / 768 measured within
 // +-0.5 %, profiles/r03i_abc_splitk_target.txt)
 constexpr long kSplitkTarget = 2 * 256;
+// most splits of one GEMM: 128, so the 4-tile d x d weight gradients (256 x 256 over K = B*T') reach
+// the two resident blocks per CU (64 left them at one: 99 TF/s, profiles/r04l_gemm_shapes_trace_b128.txt)
+constexpr long kMaxSplits = 128;
+#ifndef ESP_GEMM_TILE_TIE
+#define ESP_GEMM_TILE_TIE 1.0
+#endif
 
 // Launch the LDS-DMA kernel with the epilogue kind compiled in (each kind is its own kernel,
 // so the plain GEMMs carry none of the fused epilogues' registers; the instantiations live in
@@ -620,7 +626,12 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
       if (t < 2 * 256) c *= 1.3;
       return c;
     };
-    g.bnt = (N <= 64 || g.bf16 == 5 || cost(64) < cost(128)) ? 64 : 128;
+    // (ESP_GEMM_TILE_TIE < 1: a 64-wide tile must win by that factor -- A/B builds of the near-ties)
+    g.bnt = (N <= 64 || g.bf16 == 5 || cost(64) < ESP_GEMM_TILE_TIE * cost(128)) ? 64 : 128;
+    // the conv2 forward (implicit-im2col A gathered from the conv1 map, K = 9 D): 128-wide tiles halve the
+    // gathered-A re-reads -- 13.79 -> 11.97 ms per C2 B=256 step (the cost model's near-tie picked 64;
+    // profiles/r05f_conv2_fwd_width_ab.txt)
+    if (mode_a == I2C_KC && N % 128 == 0) g.bnt = 128;
     // 64 x 64 tiles for grids that 128-row tiles leave under-filled (decoder M ~ 5k tokens, the
     // 41-query source attention): one work unit per tile, x1.15 for the halved operand reuse
     if (g.bnt == 64 && mode_a <= RC && mode_b <= RC && g.bf16 != 2 && !smb) {
@@ -633,6 +644,7 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
     // gathered-B re-reads and split-K refills the chip (8.39 vs 9.22 ms at C2 B=128,
     // tools/gemm_bench.py with ESP_GEMM_BNT; the K ~ 48k linear weight gradients keep 128x64)
     if (mode_b == I2C_RC && work && K >= 65536) g.bnt = 128;
+
     // (256 x 128 bf16 tiles -- one block, one wave per SIMD, per CU -- measured slower, C5 B=64 860.3 vs
     // 889.3 utt/s, and were removed in round 5)
   }
@@ -659,7 +671,7 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
       const long part = inkernel ? mp * np : (long)M * N;
       const long cap = (work_bytes - (inkernel ? ESP_GEMM_TICKET_BYTES : 0)) / (4L * (part * batch + (rowsum ? M : 0)));
       if (sp > cap) sp = cap;
-      if (sp > 64) sp = 64;
+      if (sp > kMaxSplits) sp = kMaxSplits;
       // CU balance: with ceil(tiles*sp / 256) tile-rounds on the busiest CU, 72 tiles x 8 splits
       // (conv2 weight gradient) leave a third of the chip idle in the last round; take the
       // smallest sp up to 4x the target-derived one whose last round is >= 95 % full.
@@ -671,7 +683,7 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
           return (K + chunk - 1) / chunk;
         };
         auto imb = [&](long s) { const long t = tiles * s; return (double)((t + 255) / 256 * 256) / (double)t; };
-        const long hi = std::min(std::min(by_k, cap), std::min<long>(64, 4 * sp));
+        const long hi = std::min(std::min(by_k, cap), std::min<long>(kMaxSplits, 4 * sp));
         long best = launched(sp);
         for (long s = sp; s <= hi; ++s) {
           const long e = launched(s);
