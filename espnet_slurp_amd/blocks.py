@@ -46,13 +46,8 @@ def empty(*shape, like: torch.Tensor):
     return torch.empty(*shape, dtype=torch.float32, device=like.device)
 
 
-# ESP_DZ2_DIRECT=0: the bf16 mode casts an fp32 dz2 for the conv2 gradients (A/B measurements)
-_DZ2_DIRECT = __import__("os").environ.get("ESP_DZ2_DIRECT", "1") == "1"
-
-
-def _bpl(pl):
-    """gemm(b_planes=...) of a kernels.Planes (n = 3) holding B's whole source matrix, or None."""
-    return (pl.buf, pl.ld, pl.ps) if pl is not None else None
+# False: the bf16 mode casts an fp32 dz2 for the conv2 gradients (an A/B constant, r04o: +0.6 % with it)
+_DZ2_DIRECT = True
 
 
 def grad_buf(dout):
@@ -254,20 +249,14 @@ class RelPositionMultiHeadedAttention(nn.Module):
         # score-gradient epilogue, ESP_ATTN_DSCORES, reads it in fp32)
         npl = K.planes_mode() if D % 8 == 0 and not K.ATTN_DSCORES else 0
         ctx_ = K.Planes(M, D, x2d.device, npl) if npl else empty(M, D, like=x2d)
-        # qkv and p as split planes for the batched contractions that take them as B (ESP_ATTN_BPLANES)
-        qkv_pl = p_pl = None
-        if K.attn_bplanes_ok(D):
-            qkv_pl, p_pl = K.Planes.of(qkv), K.Planes.of(p)
         K.gemm(T, dk, T, pv, qkv, ctx_, mode_a=K.KC, lda=Tp, mode_b=K.RC, ldb=3 * D, ldc=D, b_off=2 * D,
-               batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * 3 * D), sc=(dk, T * D),
-               b_planes=_bpl(qkv_pl))
+               batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * 3 * D), sc=(dk, T * D))
         out = empty(M, D, like=x2d)
         pr = p_res if training else 0.0
         so = seeds.next()
         self.linear_out.fwd(ctx_, out, drop_p=pr, seed=so, R=resid, beta=1.0)
         return out, Ctx(x=x2d, qkv=qkv, p=p, pos=pos_emb, q_u=q_u, q_v=q_v, attn=attn, pv=pv, ctx=ctx_,
-                        flash=False, pa=pa, sa=sa, pr=pr, so=so, B=B, T=T, P=P, tvalid=tv, qkv_pl=qkv_pl,
-                        p_pl=p_pl)
+                        flash=False, pa=pa, sa=sa, pr=pr, so=so, B=B, T=T, P=P, tvalid=tv)
 
     def bwd(self, c, dout):
         H, dk = self.h, self.d_k
@@ -300,8 +289,7 @@ class RelPositionMultiHeadedAttention(nn.Module):
                               v_off=2 * D)
         else:  # dP = dctx v^T  (into a (Z,T,T) buffer)
             K.gemm(T, T, dk, dctx, c.qkv, dS, mode_a=K.KC, lda=D, mode_b=K.KC, ldb=3 * D, ldc=Tp, b_off=2 * D,
-                   batch=Z, nb2=B, sa=(dk, T * D), sb=(dk, T * 3 * D), sc=(B * T * Tp, T * Tp),
-                   b_planes=_bpl(c.qkv_pl))
+                   batch=Z, nb2=B, sa=(dk, T * D), sb=(dk, T * 3 * D), sc=(B * T * Tp, T * Tp))
         # dV = pv^T dctx -> dqkv[:, 2D:3D]
         K.gemm(T, dk, T, c.pv, dctx, dqkv, mode_a=K.RC, lda=Tp, mode_b=K.RC, ldb=D, ldc=3 * D, c_off=2 * D,
                batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * D), sc=(dk, T * 3 * D))
@@ -312,8 +300,7 @@ class RelPositionMultiHeadedAttention(nn.Module):
                                       tvalid=c.tvalid)
         # dq_u = dS k -> dqkv[:, 0:D]
         K.gemm(T, dk, T, dS, c.qkv, dqkv, mode_a=K.KC, lda=Tp, mode_b=K.RC, ldb=3 * D, ldc=3 * D, b_off=D,
-               batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * 3 * D), sc=(dk, T * 3 * D),
-               b_planes=_bpl(c.qkv_pl))
+               batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * 3 * D), sc=(dk, T * 3 * D))
         # dk = dS^T q_u -> dqkv[:, D:2D]
         K.gemm(T, dk, T, dS, c.q_u, dqkv, mode_a=K.RC, lda=Tp, mode_b=K.RC, ldb=dk, ldc=3 * D, c_off=D,
                batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(B * T * dk, T * dk), sc=(dk, T * 3 * D))
@@ -321,7 +308,7 @@ class RelPositionMultiHeadedAttention(nn.Module):
         # dq_v = dbd p -> tmp
         tmp = empty(M, D, like=dout)
         K.gemm(T, dk, P, dbd, c.p, tmp, mode_a=K.KC, lda=Pp, mode_b=K.RC, ldb=D, ldc=D,
-               batch=Z, nb2=B, sa=(B * T * Pp, T * Pp), sb=(dk, 0), sc=(dk, T * D), b_planes=_bpl(c.p_pl))
+               batch=Z, nb2=B, sa=(B * T * Pp, T * Pp), sb=(dk, 0), sc=(dk, T * D))
         K.colsum(tmp, self.pos_bias_v.grad.view(-1), accumulate=True)
         K.add2d(tmp, D, dqkv, 3 * D, M, D)
         # dp[:, h] = sum_b dbd[h,b]^T q_v[h,b]   (K = B*T)

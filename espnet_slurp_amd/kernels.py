@@ -1039,22 +1039,6 @@ ATTN_FWD32 = False
 # at C2 B=128 it is 412 + 73 us per layer against 59 + 266 (the epilogue's rel_shift scatter is one
 # scalar store per element; the row-wise pass writes each shifted bd row contiguously)
 ATTN_DSCORES = False
-# ATTN_BPLANES = True: the fp32 batched attention contractions whose B is qkv or the projected position
-# table (P.V, dP = dctx v^T, dS.k, dbd.p) take B as split planes made once per layer (PREC 3: only A
-# split in the k-loop) instead of splitting both operands in registers (PREC 0).  Opt-in: the
-# contractions gain 7-11 % but the two splits per layer cost more (C2 B=256 1337-1339 vs 1345-1351
-# utt/s, profiles/r04m_attn_bplanes_ab.txt) -- it pays once the qkv projection writes the planes itself
-ATTN_BPLANES = False
-
-
-def attn_bplanes_ok(D: int) -> bool:
-    if not ATTN_BPLANES or _COMPUTE[0] != 0 or D % 8:
-        return False
-    if _F32_PRODUCTS[0] is None:
-        _F32_PRODUCTS[0] = int(_native.load().esp_f32_gemm_products())
-    return _F32_PRODUCTS[0] == 6
-
-
 def relpos_attn_bwd(dctx, ldd, vmat, ldv, attn, dS, dbd, ldp, nb, H, sqrt_dk, drop_p, seed, T, lds, v_off=0):
     """Fused latest rel-pos attention backward: dP = dctx V^T (MFMA), dropout/softmax/rel_shift adjoints."""
     _f32(dctx, vmat, attn, dS, dbd)
