@@ -61,6 +61,7 @@ SIGNATURES = {
     "esp_rng_advance": [P, P],
     "esp_layernorm_fwd": [P, P, P, P, P, P, I, I, F, P],
     "esp_layernorm_fwd_planes": [P, P, P, P, L, L, I, P, P, I, I, F, P],
+    "esp_layernorm_fwd_dual": [P, P, P, P, P, L, L, I, P, P, I, I, F, P],
     "esp_layernorm_bwd": [P, P, P, P, P, P, I, P, P, I, I, P, L, P],
     "esp_colsum": [P, I, I, L, P, I, P, L, P],
     "esp_glu_fwd": [P, P, L, I, P],
@@ -84,6 +85,7 @@ SIGNATURES = {
     "esp_attn_bwd_prep": [P, L, P, L, I, I, I, I, P, P, L, I, P],
     "esp_attn_dscores": [P, L, P, L, P, P, P, P, L, I, I, I, I, F, F, U64, I, L, P],
     "esp_attn_softmax_bwd_relpos": [P, P, P, P, L, I, F, U64, F, L, I, L, P, P],
+    "esp_attn_softmax_bwd_relpos_band": [P, P, P, P, L, F, U64, F, L, I, L, P],
     "esp_relpos_attn_bwd": [P, L, P, L, P, P, P, L, I, I, F, F, U64, I, L, P],
     "esp_relpos_flash_fwd": [P, P, P, L, P, L, P, L, I, I, I, F, P, P, L, P, F, U64, I, P],
     "esp_relpos_flash_bwd": [P, P, P, L, P, L, P, L, I, I, I, F, P, P, P, L, P, F, U64, I, P, L, P, P, L, P, P, P],
@@ -119,7 +121,7 @@ _RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I, "esp_set_g
              "esp_get_gemm_compute": I, "esp_set_splitk_mode": I,
              "esp_f32_gemm_products": I}
 _RESTYPES.update({k: L for k in SIGNATURES if k.endswith("_workspace_bytes")})
-ABI_VERSION = 28  # bumped whenever a signature in include/espnet_mi355.h changes
+ABI_VERSION = 29  # bumped whenever a signature in include/espnet_mi355.h changes
 
 _lib = None
 

@@ -103,6 +103,11 @@ class LayerNorm(nn.Module):
         if n:
             y = K.Planes(M, D, x2d.device, n)
             K.layernorm_fwd_planes(x2d, self.weight, self.bias, y, mean, rstd, self.eps)
+        elif gemm_only and D % 8 == 0 and K.wgrad_xplanes_ok():
+            # fp32 y for the Linear's forward beside the weight planes, and y's split planes for its weight
+            # gradient (B planes: no B split in that RC x RC GEMM's k-loop)
+            y = empty(M, D, like=x2d)
+            K.layernorm_fwd_dual(x2d, self.weight, self.bias, y, mean, rstd, self.eps)
         else:
             y = empty(M, D, like=x2d)
             K.layernorm_fwd(x2d, self.weight, self.bias, y, mean, rstd, self.eps)
@@ -272,11 +277,13 @@ class RelPositionMultiHeadedAttention(nn.Module):
             return self._bwd_flash(c, dctx, dqkv)
         Tp, Pp = K.pitch(T), K.pitch(P)
         dS = empty(Z * T * Tp, like=dout)
-        dbd = empty(Z * T * Pp, like=dout)
         # the fused dP + softmax/rel_shift adjoint kernel measures slower than the K=64 GEMM + the
         # row-wise adjoint pass at C2 (198 vs 157 us per layer): opt-in until it is reworked
         fused = not self.legacy and K.relpos_fused_ok(T, dk) and K.FUSED_ATTN_BWD
         dscores = not fused and K.ATTN_DSCORES
+        # latest rel_shift, row-wise adjoint: dbd in the kept zeroed buffer, only its band written
+        band = None if (self.legacy or fused or dscores or Tp % 4) else K.relpos_band_buffer(Z, T, Pp, dout.device)
+        dbd = band if band is not None else empty(Z * T * Pp, like=dout)
         if dscores:
             # dS = P (drop'(dP) - dot) / sqrt(dk) and its rel_shift adjoint in the dP GEMM's epilogue,
             # dot_i = dctx_i . ctx_i (= sum_j P_drop dP): no dP tensor, no row-wise pass
@@ -295,6 +302,8 @@ class RelPositionMultiHeadedAttention(nn.Module):
                batch=Z, nb2=B, sa=(B * T * Tp, T * Tp), sb=(dk, T * D), sc=(dk, T * 3 * D))
         if fused or dscores:
             pass
+        elif band is not None:
+            K.attn_softmax_bwd_relpos_band(c.attn, dS, dS, dbd, Pp, c.pa, c.sa, math.sqrt(dk), Z * T, T, Tp)
         else:  # softmax + rel_shift adjoints in one pass (latest and legacy)
             K.attn_softmax_bwd_relpos(c.attn, dS, dS, dbd, Pp, c.pa, c.sa, math.sqrt(dk), Z * T, T, Tp, relpos=relpos,
                                       tvalid=c.tvalid)

@@ -274,6 +274,8 @@ __global__ __launch_bounds__(256) void softmax_bwd_relpos_kernel(const float* __
 // (the pitch's padding columns get 0), and hands its 4 values through a per-wave LDS row so the
 // rel_shift-adjoint dbd stores stay one contiguous 256-B run per instruction (j = lane + 64e).
 // P2: sqrt(d_k) a power of two -> exact multiply by 1/sqrt(d_k).
+// REL 1 latest, 2 legacy, 3 latest writing only the dbd band (row i: columns T-1-i .. 2T-2-i) into a
+// buffer whose other elements are already zero (esp_attn_softmax_bwd_relpos_band: half the dbd bytes)
 template <int Q, int REL, bool P2>  // Q quads per lane: 256*Q >= T
 __global__ __launch_bounds__(256) void softmax_bwd_relpos4_kernel(const float* __restrict__ attn, const float* dP,
                                                                   float* dS, float* __restrict__ dbd, long ldp,
@@ -337,7 +339,7 @@ __global__ __launch_bounds__(256) void softmax_bwd_relpos4_kernel(const float* _
   asm volatile("" ::: "memory");  // wave-private LDS row: in-order within the wave
   float* br = dbd + row * ldp;
   const int Ts = REL == 2 ? legacy_tv(tvalid, T) : T;  // the rel_shift's length (see the scalar kernel)
-  const bool live = REL == 1 || i < Ts;
+  const bool live = REL != 2 || i < Ts;
   const int sh = Ts - 1 - i;
   if (live) {
 #pragma unroll
@@ -345,15 +347,15 @@ __global__ __launch_bounds__(256) void softmax_bwd_relpos4_kernel(const float* _
       const int j = lane + 64 * e;
       if (j < T) {
         const float v = st[j];
-        if (REL == 1 || j <= i) br[j + sh] = v;
+        if (REL != 2 || j <= i) br[j + sh] = v;
         else if (j >= i + 2 && j < Ts) br[ldp + j - i - 2] = v;  // row i+1 of the same z (i + 1 < Ts here)
       }
     }
   }
-  if (REL == 1) {
+  if constexpr (REL == 1) {
     for (int k = lane; k < sh; k += 64) br[k] = 0.f;
     for (int k = sh + T + lane; k < 2 * T - 1; k += 64) br[k] = 0.f;
-  } else {
+  } else if constexpr (REL == 2) {
     if (!live) {
       for (int k = lane; k < T; k += 64) br[k] = 0.f;
     } else {
@@ -1698,6 +1700,38 @@ ESP_API int esp_relpos_attn_probs(const float* qu, const float* qv, const float*
 }
 
 // softmax backward + latest rel_shift adjoint in one pass (see softmax_bwd_relpos_kernel)
+// latest rel_shift, dbd written only on its band: dbd's other elements must already be 0 (a buffer kept
+// for this use, zeroed once: the kernel never writes outside the band)
+ESP_API int esp_attn_softmax_bwd_relpos_band(const float* attn, const float* dP, float* dS, float* dbd, long ldp,
+                                             float drop_p, unsigned long long seed, float sqrt_dk, long rows, int T,
+                                             long lds, void* stream) {
+  ESP_ARG_CHECK(T >= 1 && T <= 1024 && lds >= T && lds % 4 == 0 && ldp >= 2 * T - 1 && rows % T == 0,
+                "esp_attn_softmax_bwd_relpos_band: bad sizes");
+  ESP_ARG_CHECK(((uintptr_t)attn & 15) == 0 && ((uintptr_t)dP & 15) == 0 && ((uintptr_t)dS & 15) == 0,
+                "esp_attn_softmax_bwd_relpos_band: attn / dP / dS must be 16-B aligned");
+  ESP_ARG_CHECK(drop_p < 1.f, "dropout p must be < 1 (got %g)", (double)drop_p);
+  const uint32_t thr = esp::drop_threshold(drop_p);
+  const float ds = esp::drop_scale(thr);
+  dim3 grid((unsigned)((rows + 3) / 4));
+  hipStream_t st = (hipStream_t)stream;
+  const bool p2 = sqrt_dk > 0.f && (__builtin_bit_cast(uint32_t, sqrt_dk) & 0x7fffffu) == 0;
+#define ESP_SBB(Q)                                                                                                 \
+  do {                                                                                                             \
+    if (p2)                                                                                                        \
+      hipLaunchKernelGGL((softmax_bwd_relpos4_kernel<Q, 3, true>), grid, dim3(256), 0, st, attn, dP, dS, dbd, ldp,  \
+                         thr, ds, (uint64_t)seed, sqrt_dk, rows, T, lds, esp::rng_key_ptr(), nullptr);             \
+    else                                                                                                           \
+      hipLaunchKernelGGL((softmax_bwd_relpos4_kernel<Q, 3, false>), grid, dim3(256), 0, st, attn, dP, dS, dbd, ldp, \
+                         thr, ds, (uint64_t)seed, sqrt_dk, rows, T, lds, esp::rng_key_ptr(), nullptr);             \
+  } while (0)
+  if (T <= 256) ESP_SBB(1);
+  else if (T <= 512) ESP_SBB(2);
+  else ESP_SBB(4);
+#undef ESP_SBB
+  ESP_CHECK_LAUNCH("esp_attn_softmax_bwd_relpos_band");
+  return 0;
+}
+
 ESP_API int esp_attn_softmax_bwd_relpos(const float* attn, const float* dP, float* dS, float* dbd, long ldp,
                                         int relpos, float drop_p, unsigned long long seed, float sqrt_dk, long rows,
                                         int T, long lds, const int* tvalid, void* stream) {

@@ -612,7 +612,10 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
     // fp32 on split products (ESP_F32_SPLIT): a 64-wide tile costs ~3/4 of a 128-wide one (its
     // waves split 1.5x the operand values per MFMA), and a grid that split-K will refill is
     // priced by its total work (the K ~ 48k weight gradients: 3.8 vs 4.9 ms on 128-wide tiles)
-    const bool split_f32 = ESP_F32_SPLIT && g.bf16 == 0;
+    // (B planes, PREC 3, are the same split-product arithmetic: a weight gradient on X planes is priced
+    // like its PREC 0 form -- priced per tile instead, its split-K grid took 64-wide tiles, 12.6 ms for what
+    // 128-wide tiles do in ~11, profiles/r05j_*)
+    const bool split_f32 = ESP_F32_SPLIT && (g.bf16 == 0 || g.bf16 == 3);
     auto cost = [&](int bn) {
       const long t = ntiles(bn);
       // (B planes: only A is split, 3.7 split VALU per MFMA at either width)

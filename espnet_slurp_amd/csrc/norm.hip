@@ -62,7 +62,8 @@ template <int PQ>
 __global__ __launch_bounds__(256) void ln_fwd_planes_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                             const float* __restrict__ b, uint16_t* __restrict__ y,
                                                             long ldy, long ps, int n, float* __restrict__ mean_out,
-                                                            float* __restrict__ rstd_out, int M, int D, float eps) {
+                                                            float* __restrict__ rstd_out, int M, int D, float eps,
+                                                            float* __restrict__ yf) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
@@ -93,9 +94,10 @@ __global__ __launch_bounds__(256) void ln_fwd_planes_kernel(const float* __restr
     const int q = lane + 64 * i;
     if (q >= nq) continue;
     const float4 wq = reinterpret_cast<const float4*>(w)[q], bq = reinterpret_cast<const float4*>(b)[q];
-    esp::store_planes4(y, (long)row * ldy + 4 * q, ps, n, (v[i].x - mean) * rstd * wq.x + bq.x,
-                       (v[i].y - mean) * rstd * wq.y + bq.y, (v[i].z - mean) * rstd * wq.z + bq.z,
-                       (v[i].w - mean) * rstd * wq.w + bq.w);
+    const float4 o = make_float4((v[i].x - mean) * rstd * wq.x + bq.x, (v[i].y - mean) * rstd * wq.y + bq.y,
+                                 (v[i].z - mean) * rstd * wq.z + bq.z, (v[i].w - mean) * rstd * wq.w + bq.w);
+    esp::store_planes4(y, (long)row * ldy + 4 * q, ps, n, o.x, o.y, o.z, o.w);
+    if (yf) reinterpret_cast<float4*>(yf + (long)row * D)[q] = o;  // (esp_layernorm_fwd_dual: y in fp32 too)
   }
   if (lane == 0) {
     mean_out[row] = mean;
@@ -832,13 +834,14 @@ ESP_API int esp_layernorm_fwd(const float* x, const float* w, const float* b, fl
   return 0;
 }
 
-ESP_API int esp_layernorm_fwd_planes(const float* x, const float* w, const float* b, void* y, long ldy, long pstride,
-                                     int nplanes, float* mean, float* rstd, int M, int D, float eps, void* stream) {
+static int layernorm_fwd_planes_impl(const float* x, const float* w, const float* b, void* y, long ldy, long pstride,
+                                     int nplanes, float* mean, float* rstd, int M, int D, float eps, float* yf,
+                                     void* stream) {
   ESP_ARG_CHECK(D <= MAXD && D % 4 == 0, "esp_layernorm_fwd_planes: D=%d must be a multiple of 4 and <= %d", D, MAXD);
   ESP_ARG_CHECK((nplanes == 1 || nplanes == 3) && ldy >= D && ldy % 4 == 0 && (nplanes == 1 || pstride >= (long)M * ldy) &&
                     ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 7) == 0 && ((uintptr_t)w & 15) == 0 &&
                     ((uintptr_t)b & 15) == 0 && pstride % 4 == 0,
-                "esp_layernorm_fwd_planes: bad planes layout (nplanes %d, ldy %ld, pstride %ld) or alignment", nplanes,
+                "esp_layernorm_fwd_planes/_dual: bad planes layout (nplanes %d, ldy %ld, pstride %ld) or alignment", nplanes,
                 ldy, pstride);
   if (M <= 0) return 0;
   dim3 grid((M + 3) / 4);
@@ -846,16 +849,30 @@ ESP_API int esp_layernorm_fwd_planes(const float* x, const float* w, const float
   const int pq = (D / 4 + 63) / 64;
   uint16_t* yp = (uint16_t*)y;
   if (pq <= 1)
-    hipLaunchKernelGGL(ln_fwd_planes_kernel<1>, grid, dim3(256), 0, st, x, w, b, yp, ldy, pstride, nplanes, mean, rstd, M, D, eps);
+    hipLaunchKernelGGL(ln_fwd_planes_kernel<1>, grid, dim3(256), 0, st, x, w, b, yp, ldy, pstride, nplanes, mean, rstd, M, D, eps, yf);
   else if (pq <= 2)
-    hipLaunchKernelGGL(ln_fwd_planes_kernel<2>, grid, dim3(256), 0, st, x, w, b, yp, ldy, pstride, nplanes, mean, rstd, M, D, eps);
+    hipLaunchKernelGGL(ln_fwd_planes_kernel<2>, grid, dim3(256), 0, st, x, w, b, yp, ldy, pstride, nplanes, mean, rstd, M, D, eps, yf);
   else
-    hipLaunchKernelGGL(ln_fwd_planes_kernel<8>, grid, dim3(256), 0, st, x, w, b, yp, ldy, pstride, nplanes, mean, rstd, M, D, eps);
+    hipLaunchKernelGGL(ln_fwd_planes_kernel<8>, grid, dim3(256), 0, st, x, w, b, yp, ldy, pstride, nplanes, mean, rstd, M, D, eps, yf);
   ESP_CHECK_LAUNCH("esp_layernorm_fwd_planes");
   return 0;
 }
 
 // workspace: 2*D*ceil(M/32) floats (esp_layernorm_bwd_workspace_bytes).  dw/db are accumulated (+=).
+ESP_API int esp_layernorm_fwd_planes(const float* x, const float* w, const float* b, void* y, long ldy, long pstride,
+                                     int nplanes, float* mean, float* rstd, int M, int D, float eps, void* stream) {
+  return layernorm_fwd_planes_impl(x, w, b, y, ldy, pstride, nplanes, mean, rstd, M, D, eps, nullptr, stream);
+}
+
+// y in fp32 (row pitch D) AND as planes: the LayerNorm outputs that feed a Linear forward (fp32 A, weight
+// planes B) and its weight gradient (B = the planes: no split of B in that GEMM's k-loop)
+ESP_API int esp_layernorm_fwd_dual(const float* x, const float* w, const float* b, float* yf, void* y, long ldy,
+                                   long pstride, int nplanes, float* mean, float* rstd, int M, int D, float eps,
+                                   void* stream) {
+  ESP_ARG_CHECK(yf && ((uintptr_t)yf & 15) == 0, "esp_layernorm_fwd_dual: y (fp32) must be 16-B aligned");
+  return layernorm_fwd_planes_impl(x, w, b, y, ldy, pstride, nplanes, mean, rstd, M, D, eps, yf, stream);
+}
+
 ESP_API long esp_layernorm_bwd_workspace_bytes(int M, int D) {
   return M <= 0 || D <= 0 ? 0 : 4L * 2 * D * ((M + LN_BWD_ROWS - 1) / LN_BWD_ROWS);
 }

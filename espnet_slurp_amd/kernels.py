@@ -688,11 +688,48 @@ def linear_bwd_data_act(dy, W, dx, pre, act, drop_p=0.0, seed=0, b_weight=False)
 
 
 def linear_bwd_weight(dy, x, dW, db=None):
-    """dW += dy^T x ; db += colsum(dy) (fused into the same GEMM pass over dy); x fp32 or Planes."""
+    """dW += dy^T x ; db += colsum(dy) (fused into the same GEMM pass over dy); x fp32 or Planes.  An fp32 x
+    that carries its split planes (`twin_planes`: a LayerNorm output written by esp_layernorm_fwd_dual) is
+    taken as B planes (PREC 3: only dy is split in the k-loop)."""
     M, N = dy.shape
     K = x.shape[1]
+    tw = twin_planes(x) if _COMPUTE[0] == 0 else None
     gemm(N, K, M, dy, x, dW, mode_a=RC, lda=_ld(dy), mode_b=RC, ldb=_ld(x), ldc=dW.stride(0), R=dW, beta=1.0,
-         rowsum=db, _keep_a16=True)
+         rowsum=db, _keep_a16=True, b_planes=None if tw is None else (tw.buf, tw.ld, tw.ps))
+
+
+# fp32 tensors that also carry their three split planes (an attribute of the tensor object, so it lives
+# exactly as long as the tensor the backward keeps): the fp32 mode's LayerNorm outputs that feed Linears
+# (forward: fp32 A beside the weight planes; weight gradient: these planes as B, PREC 3).  Measured neutral
+# at C2 B=256 (profiles/r05k_wgrad_xplanes_ab.txt: 66 weight gradients 176 -> 174 us on PREC 3, the dual
+# LayerNorm 33 -> 47 us), so off: the RC x RC k-loop is not bound by B's split alone (its dy operand still
+# splits in registers from ds_read_b32 fragments).  The path stays tested
+# (test_layernorm_dual_and_weight_gradient_on_twin_planes) for A-side planes.
+WGRAD_XPLANES = False
+
+
+def wgrad_xplanes_ok() -> bool:
+    """The fp32 mode of a split-product build (the planes are the B operand of a PREC 3 weight gradient)."""
+    if not WGRAD_XPLANES or _COMPUTE[0] != 0:
+        return False
+    if _F32_PRODUCTS[0] is None:
+        _F32_PRODUCTS[0] = int(_native.load().esp_f32_gemm_products())
+    return _F32_PRODUCTS[0] == 6
+
+
+def twin_planes(x):
+    pl = getattr(x, "_esp_planes", None)
+    return pl if pl is not None and pl.rows == x.shape[0] and pl.cols == x.shape[1] else None
+
+
+def layernorm_fwd_dual(x2d, w, b, y, mean, rstd, eps=1e-12):
+    """esp_layernorm_fwd_dual: y (fp32) and its split planes, attached to y (twin_planes)."""
+    M, D = x2d.shape
+    pl = Planes(M, D, x2d.device, 3)
+    _native.call("esp_layernorm_fwd_dual", _p(x2d), _p(w), _p(b), _p(y), _p(pl.buf), pl.ld, pl.ps, 3, _p(mean),
+                 _p(rstd), M, D, float(eps), _st())
+    y._esp_planes = pl
+    return y
 
 
 def colsum(x2d, out, accumulate=True, M=None, N=None, ld=None):
@@ -1028,6 +1065,32 @@ def attn_softmax_bwd_relpos(attn, dP, dS, dbd, ldp, drop_p, seed, sqrt_dk, rows,
     (writes dS and dbd); tvalid: legacy length-bucket T' (device int32)."""
     _native.call("esp_attn_softmax_bwd_relpos", _p(attn), _p(dP), _p(dS), _p(dbd), ldp, int(relpos), float(drop_p),
                  seed, float(sqrt_dk), rows, T, lds, _p(tvalid), _st())
+
+
+def attn_softmax_bwd_relpos_band(attn, dP, dS, dbd, ldp, drop_p, seed, sqrt_dk, rows, T, lds):
+    """The latest-rel_shift adjoint writing only dbd's band (esp_attn_softmax_bwd_relpos_band); dbd must be
+    a relpos_band_buffer (zero outside the band)."""
+    _native.call("esp_attn_softmax_bwd_relpos_band", _p(attn), _p(dP), _p(dS), _p(dbd), ldp, float(drop_p), seed,
+                 float(sqrt_dk), rows, T, lds, _st())
+
+
+# dbd buffers of the latest rel_shift adjoint, kept per (device, Z, T, pitch) and zeroed once: the band
+# kernel writes each row's T band columns only, so the rest stays 0 for every layer and step (half the
+# adjoint's dbd bytes).  Made outside graph capture only (a buffer made inside would live in the graph's
+# pool); a few shapes at most (length buckets), beyond that the full-row kernel.
+_DBD_BUFS = {}
+_DBD_MAX_SHAPES = 4
+
+
+def relpos_band_buffer(Z, T, Pp, device):
+    key = (str(device), Z, T, Pp)
+    buf = _DBD_BUFS.get(key)
+    if buf is None:
+        if len(_DBD_BUFS) >= _DBD_MAX_SHAPES or torch.cuda.is_current_stream_capturing():
+            return None
+        buf = torch.zeros(Z * T * Pp, dtype=torch.float32, device=device)
+        _DBD_BUFS[key] = buf
+    return buf
 
 
 FUSED_ATTN_BWD = False

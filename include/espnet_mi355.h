@@ -202,6 +202,12 @@ int esp_layernorm_fwd(const float* x, const float* w, const float* b, float* y, 
  * elements), row pitch ldy (>= D, % 4 == 0).  D % 4 == 0, x / w / b 16-B aligned, y 8-B aligned. */
 int esp_layernorm_fwd_planes(const float* x, const float* w, const float* b, void* y, long ldy, long pstride,
                              int nplanes, float* mean, float* rstd, int M, int D, float eps, void* stream);
+/* ABI 29: y written in fp32 (yf, row pitch D, 16-B aligned) AND as planes (as esp_layernorm_fwd_planes):
+ * the fp32 mode's LayerNorm outputs that feed a Linear's forward (fp32 A) and its weight gradient (the
+ * planes as B, gemm_kernels.h PREC 3).  Replaces the same LayerNorm as esp_layernorm_fwd (layer_norm.py:12-38). */
+int esp_layernorm_fwd_dual(const float* x, const float* w, const float* b, float* yf, void* y, long ldy,
+                           long pstride, int nplanes, float* mean, float* rstd, int M, int D, float eps,
+                           void* stream);
 int esp_layernorm_bwd(const float* dy, const float* x, const float* w, const float* mean,
                       const float* rstd, float* dx, int accumulate, float* dw, float* db, int M,
                       int D, float* work, long work_bytes, void* stream);
@@ -267,6 +273,12 @@ int esp_relshift_bwd(const float* dS, long lds, float* dbd, long ldp, int relpos
 int esp_attn_softmax_bwd_relpos(const float* attn, const float* dP, float* dS, float* dbd, long ldp,
                                 int relpos, float drop_p, unsigned long long seed, float sqrt_dk,
                                 long rows, int T, long lds, const int* tvalid, void* stream);
+/* ABI 29: the latest form (P = 2T-1) writing only row i's band of dbd, columns T-1-i .. 2T-2-i, into a
+ * buffer whose other elements are already 0 (kept and zeroed once by the caller: nothing else writes it);
+ * half the dbd bytes of esp_attn_softmax_bwd_relpos.  lds % 4 == 0, attn / dP / dS 16-B aligned. */
+int esp_attn_softmax_bwd_relpos_band(const float* attn, const float* dP, float* dS, float* dbd, long ldp,
+                                     float drop_p, unsigned long long seed, float sqrt_dk, long rows, int T,
+                                     long lds, void* stream);
 /* Fused latest rel-pos attention backward: dP = dctx V^T on the MFMA per 32-row block, attention
  * dropout adjoint, softmax adjoint, rel_shift adjoint -> dS (pitch lds) and dbd (pitch ldp).
  * dctx rows at dctx + (b*T+i)*ldd + 64h, V rows at vmat + (b*T+j)*ldv + 64h; d_k = 64, T <= 512. */

@@ -1077,6 +1077,62 @@ def test_layernorm_planes(dev, MD):
     assert torch.equal(y1.buf.view(M, y1.ld)[:, :D], yf.to(torch.bfloat16))
 
 
+def test_layernorm_dual_and_weight_gradient_on_twin_planes(dev):
+    """esp_layernorm_fwd_dual (round 5): its fp32 y equals the planes' value exactly (hi + mid + lo == y,
+    the same kernel writes both), y / mean / rstd equal esp_layernorm_fwd_planes' bit for bit; and the
+    weight gradient that takes y's attached planes as B (PREC 3: only dy split in the k-loop) equals the
+    one that splits fp32 y in registers, bit for bit (same split, same products, same order), fused bias
+    gradient included, at an RC x RC shape with split-K (K = 12000 rows)."""
+    M, D, N = 12000, 256, 768
+    x = (_r(M, D, seed=84) * 3 + 1).to(dev)
+    w, b = _r(D, seed=85).to(dev), _r(D, seed=86).to(dev)
+    yp = K.Planes(M, D, dev, 3)
+    m0, r0 = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    K.layernorm_fwd_planes(x, w, b, yp, m0, r0)
+    y = torch.empty(M, D, device=dev)
+    m1, r1 = torch.empty(M, device=dev), torch.empty(M, device=dev)
+    K.layernorm_fwd_dual(x, w, b, y, m1, r1)
+    tw = K.twin_planes(y)
+    assert tw is not None and tw.n == 3
+    assert torch.equal(tw.float(), y) and torch.equal(tw.buf, yp.buf)
+    assert torch.equal(m1, m0) and torch.equal(r1, r0)
+    dy = _r(M, N, seed=87).to(dev)
+    res = []
+    for twin in (False, True):
+        yy = y if twin else y.clone()  # (a clone carries no planes)
+        assert (K.twin_planes(yy) is not None) == twin
+        dW = torch.zeros(N, D, device=dev)
+        db = torch.zeros(N, device=dev)
+        K.linear_bwd_weight(dy, yy, dW, db)
+        res.append((dW, db))
+    torch.cuda.synchronize()
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    ref = dy.double().t() @ y.double()
+    assert (res[1][0].double() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+
+
+def test_softmax_bwd_relpos_band_matches_full_rows(dev):
+    """esp_attn_softmax_bwd_relpos_band (round 5): into a kept buffer that is zero outside the rel_shift
+    band, two successive launches on different inputs give dS and the whole dbd (band AND the zeros) of the
+    full-row kernel, bit for bit -- the band kernel never writes outside the band and overwrites all of it.
+    Dropout on, T' = 374 (pitch 376 / 748), latest rel_shift."""
+    Z, T, pa, seed = 24, 374, 0.1, 99
+    Tp, Pp = K.pitch(T), K.pitch(2 * T - 1)
+    band = K.relpos_band_buffer(Z, T, Pp, dev)
+    assert band is not None and band.abs().max().item() == 0.0
+    for rep in range(2):
+        attn = torch.softmax(_r(Z * T, Tp, seed=100 + rep), dim=1).to(dev).reshape(-1)
+        dP = _r(Z * T * Tp, seed=110 + rep).to(dev)
+        dS0, dS1 = torch.empty_like(dP), torch.empty_like(dP)
+        full = torch.full((Z * T * Pp,), float("nan"), device=dev)
+        K.attn_softmax_bwd_relpos(attn, dP, dS0, full, Pp, pa, seed, 8.0, Z * T, T, Tp, relpos=1)
+        K.attn_softmax_bwd_relpos_band(attn, dP, dS1, band, Pp, pa, seed, 8.0, Z * T, T, Tp)
+        torch.cuda.synchronize()
+        cols = slice(0, 2 * T - 1)
+        assert torch.equal(dS0.view(Z * T, Tp)[:, :T], dS1.view(Z * T, Tp)[:, :T])
+        assert torch.equal(full.view(Z * T, Pp)[:, cols], band.view(Z * T, Pp)[:, cols])
+
+
 def test_gemm_planes_output_epilogues(dev):
     """C written as planes (esp_gemm_f32_pl c_nplanes = 3): the FFN w_1 epilogue (bias + Swish / ReLU
     + dropout, derivative to aux) with A and B as planes, and the batched attention context P.V

@@ -1,0 +1,13 @@
+#!/bin/bash
+# round 5: weight gradients on LayerNorm twin planes with 128-wide tiles (cost model fix) + band-only dbd:
+# parity, bench A/B (twin planes on / off), kernel summary
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+rm -rf gpurun_out/prof_k
+bash gpurun_steps.sh \
+  "timeout -k 10 700 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_model.py tests/test_gpu_bench_shape.py tests/test_gpu_fullsize.py tests/test_gpu_blocks.py tests/test_gpu_graph.py tests/test_gpu_buckets.py -v -s --maxfail 10 --timeout 350 --timeout-method thread > gpurun_out/r05k_pytest.log 2>&1; rc=\$?; [ \$rc -le 1 ]" \
+  "timeout -k 10 400 python -u bench.py --no-cpu-baseline --feed-steps 0 > gpurun_out/r05k_bench.log 2>&1" \
+  "timeout -k 10 400 python -u tools/bench_with.py kernels.WGRAD_XPLANES=0 -- --no-cpu-baseline --feed-steps 0 > gpurun_out/r05k_bench_off.log 2>&1" \
+  "timeout -k 10 400 python -u bench.py --no-cpu-baseline --feed-steps 0 > gpurun_out/r05k_bench2.log 2>&1" \
+  "timeout -k 10 400 python -u tools/bench_with.py kernels.WGRAD_XPLANES=0 -- --no-cpu-baseline --feed-steps 0 > gpurun_out/r05k_bench_off2.log 2>&1" \
+  "timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_k -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --feed-steps 0 > gpurun_out/prof_k.log 2>&1"
