@@ -86,6 +86,7 @@ SIGNATURES = {
     "esp_attn_dscores": [P, L, P, L, P, P, P, P, L, I, I, I, I, F, F, U64, I, L, P],
     "esp_attn_softmax_bwd_relpos": [P, P, P, P, L, I, F, U64, F, L, I, L, P, P],
     "esp_attn_softmax_bwd_relpos_band": [P, P, P, P, L, F, U64, F, L, I, L, P],
+    "esp_relpos_dqv": [P, L, P, L, P, L, I, I, I, P, L, P],
     "esp_relpos_attn_bwd": [P, L, P, L, P, P, P, L, I, I, F, F, U64, I, L, P],
     "esp_relpos_flash_fwd": [P, P, P, L, P, L, P, L, I, I, I, F, P, P, L, P, F, U64, I, P],
     "esp_relpos_flash_bwd": [P, P, P, L, P, L, P, L, I, I, I, F, P, P, P, L, P, F, U64, I, P, L, P, P, L, P, P, P],

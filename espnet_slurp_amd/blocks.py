@@ -316,8 +316,11 @@ class RelPositionMultiHeadedAttention(nn.Module):
         K.colsum(dqkv, self.pos_bias_u.grad.view(-1), accumulate=True, M=M, N=D, ld=3 * D)
         # dq_v = dbd p -> tmp
         tmp = empty(M, D, like=dout)
-        K.gemm(T, dk, P, dbd, c.p, tmp, mode_a=K.KC, lda=Pp, mode_b=K.RC, ldb=D, ldc=D,
-               batch=Z, nb2=B, sa=(B * T * Pp, T * Pp), sb=(dk, 0), sc=(dk, T * D))
+        if not self.legacy and dk == 64:  # the band of each row tile only (dbd is 0 outside it)
+            K.relpos_dqv(dbd, Pp, c.p, D, tmp, D, B, H, T)
+        else:
+            K.gemm(T, dk, P, dbd, c.p, tmp, mode_a=K.KC, lda=Pp, mode_b=K.RC, ldb=D, ldc=D,
+                   batch=Z, nb2=B, sa=(B * T * Pp, T * Pp), sb=(dk, 0), sc=(dk, T * D))
         K.colsum(tmp, self.pos_bias_v.grad.view(-1), accumulate=True)
         K.add2d(tmp, D, dqkv, 3 * D, M, D)
         # dp[:, h] = sum_b dbd[h,b]^T q_v[h,b]   (K = B*T)

@@ -310,7 +310,7 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
                     const int* im2col_a, const int* im2col_b, float* work, long work_bytes, void* stream,
                     int prec_in, const GemmArgs* smb = nullptr, const void* b_planes = nullptr, long ldbp = 0,
                     long sbp1 = 0, long sbp2 = 0, long bps = 0, const void* a_planes = nullptr, long ldap = 0,
-                    long sap1 = 0, long sap2 = 0, long aps = 0, int cpn = 0, long cps = 0);
+                    long sap1 = 0, long sap2 = 0, long aps = 0, int cpn = 0, long cps = 0, const int* band = nullptr);
 
 ESP_API int esp_gemm_f32(int mode_a, int mode_b, int M, int N, int K, int batch, int nb2,
                          const float* A, long lda, long sa1, long sa2,
@@ -503,7 +503,8 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
                     float drop_p, unsigned long long seed, int bwd_act, const float* pre, float* rowsum,
                     const int* im2col_a, const int* im2col_b, float* work, long work_bytes, void* stream,
                     int prec_in, const GemmArgs* smb, const void* b_planes, long ldbp, long sbp1, long sbp2,
-                    long bps, const void* a_planes, long ldap, long sap1, long sap2, long aps, int cpn, long cps) {
+                    long bps, const void* a_planes, long ldap, long sap1, long sap2, long aps, int cpn, long cps,
+                    const int* band) {
   ESP_ARG_CHECK(M >= 0 && N >= 0 && K >= 0 && batch >= 1 && nb2 >= 1 && batch % nb2 == 0,
                 "esp_gemm_f32: bad sizes M=%d N=%d K=%d batch=%d nb2=%d", M, N, K, batch, nb2);
   ESP_ARG_CHECK(mode_a >= 0 && mode_a <= 3 && mode_b >= 0 && mode_b <= 3, "esp_gemm_f32: bad mode");
@@ -544,6 +545,10 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
   }
   g.cpn = cpn;
   g.cps = cps;
+  if (band) {
+    g.band_c0 = band[0];
+    g.band_w = band[1];
+  }
   if (cpn) {  // planes output: 8-B quads per plane (C is plane 0, bf16)
     ESP_ARG_CHECK((cpn == 1 || cpn == 3) && N % 4 == 0 && ldc % 4 == 0 && cps % 4 == 0 && ((uintptr_t)C & 7) == 0 &&
                       !R && !rowsum && (cpn == 1 || cps >= (long)M * ldc || batch > 1),
@@ -727,6 +732,24 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
   }
 }
 
+
+// Rel-pos attention (latest rel_shift), the q_v gradient through the band scores:
+//   dq_v[z](i, :) = sum_k dbd[z](i, k) p[k, 64 h : 64 h + 64],  z = h * nb + b
+// (attention.py:240-263 backward; the dbd.p contraction of RelPositionMultiHeadedAttention.bwd).  Row i of
+// dbd is zero outside its rel_shift band, columns T-1-i .. 2T-2-i (esp_attn_softmax_bwd_relpos_band / the
+// full-row kernel), so each 128-row tile's k-loop runs over its rows' band union only: T + 127 of the
+// 2T - 1 columns.  dbd (Z, T) rows of pitch ldp (>= 2T-1, % 4 == 0); p (2T-1, H*64) pitch ldpm; out rows
+// (b*T + i) pitch ldo, head h at column 64 h.  d_k = 64.
+ESP_API int esp_relpos_dqv(const float* dbd, long ldp, const float* p, long ldpm, float* out, long ldo, int nb, int H,
+                           int T, float* work, long work_bytes, void* stream) {
+  ESP_ARG_CHECK(T >= 1 && nb >= 1 && H >= 1 && ldp >= 2 * T - 1 && ldp % 4 == 0 && ldpm >= 64L * H && ldo >= 64L * H,
+                "esp_relpos_dqv: bad sizes T=%d ldp=%ld ldpm=%ld ldo=%ld", T, ldp, ldpm, ldo);
+  const int band[2] = {T - 1, T};
+  const int P = 2 * T - 1;
+  return gemm_run(KC, RC, T, 64, P, nb * H, nb, dbd, ldp, (long)nb * T * ldp, (long)T * ldp, p, ldpm, 64, 0, out, ldo,
+                  64, (long)T * ldo, nullptr, 1.f, 0.f, nullptr, 0, nullptr, 0.f, 0, 0, nullptr, nullptr, nullptr,
+                  nullptr, work, work_bytes, stream, -1, nullptr, nullptr, 0, 0, 0, 0, nullptr, 0, 0, 0, 0, 0, 0, band);
+}
 
 // ============================================================================ conv2 input gradient
 // Conv2d(D, D, 3, stride 2) input gradient as 4 implicit GEMMs, one per parity class (ph, pw)

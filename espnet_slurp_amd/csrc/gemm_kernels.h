@@ -140,6 +140,9 @@ struct GemmArgs {
   // at c + p * cps; cpn = 3 (exact split) or 1 (bf16)
   int cpn;
   long cps;
+  // banded A (KC; esp_relpos_dqv): row m of A is zero outside columns [band_c0 - m, band_c0 - m + band_w),
+  // so a row tile's k-loop runs only over its rows' union (LDS-DMA kernel; band_w = 0: the whole K)
+  int band_c0, band_w;
 };
 
 __device__ __forceinline__ long row_off(const GemmArgs& g, int m) {
@@ -1659,6 +1662,13 @@ __device__ __forceinline__ TileCoord tile_coord(const GemmArgs& g, const GldsArg
   c.split = zz - c.z * g.splits;
   c.kbeg = c.split * g.kchunk;
   c.kend = min(g.K, c.kbeg + g.kchunk);
+  if (g.band_w) {  // the row tile's band union, slab-aligned below (the rows' zeros outside cost nothing)
+    const int m0 = tm * BMT;
+    const int lo = max(0, g.band_c0 - (m0 + BMT - 1)) / GL_BK * GL_BK;
+    const int hi = min(g.K, g.band_c0 - m0 + g.band_w);
+    c.kbeg = max(c.kbeg, lo);
+    c.kend = max(c.kbeg + 1, min(c.kend, hi));  // (never empty: a slab of zeros at worst)
+  }
   c.nk = (c.kend - c.kbeg + GL_BK - 1) / GL_BK;  // >= 1: the host routes K == 0 elsewhere
   c.m0 = tm * BMT;
   c.n0 = c.tn * BNT;
@@ -1713,6 +1723,36 @@ __device__ __forceinline__ void split3_bf16(const float* v, bf16x8& hi, bf16x8& 
   hi = __builtin_bit_cast(bf16x8, make_uint4(H[0], H[1], H[2], H[3]));
   mid = __builtin_bit_cast(bf16x8, make_uint4(Md[0], Md[1], Md[2], Md[3]));
   lo = __builtin_bit_cast(bf16x8, make_uint4(L[0], L[1], L[2], L[3]));
+}
+
+
+// The six split products of every (i, j) tile pair (smallest first: mid.mid, lo.hi, hi.lo, mid.hi, hi.mid,
+// hi.hi).  ESP_GEMM_MFMA_ORDER 0: each pair's six MFMAs back to back (one accumulator chain at a time);
+// 1: product-major, the TM x TN independent accumulators interleaved -- each accumulator receives the same
+// products in the same order either way (bit-identical results)
+#ifndef ESP_GEMM_MFMA_ORDER
+#define ESP_GEMM_MFMA_ORDER 0
+#endif
+template <int TM, int TN>
+__device__ __forceinline__ void mma6(f32x16 (&acc)[TM][TN], const bf16x8 (&ah)[TM][3], const bf16x8 (&bh)[TN][3]) {
+  constexpr int PA[6] = {1, 2, 0, 1, 0, 0}, PB[6] = {1, 0, 2, 0, 1, 0};
+  if constexpr (ESP_GEMM_MFMA_ORDER == 1) {
+#pragma unroll
+    for (int p = 0; p < 6; ++p)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][PA[p]], bh[j][PB[p]], acc[i][j], 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int p = 0; p < 6; ++p)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][PA[p]], bh[j][PB[p]], acc[i][j], 0, 0, 0);
+  }
 }
 
 template <int MA, int MB, int BNT, bool RS, int EPI, int PREC = 0, int BMT = BM>
@@ -1926,17 +1966,7 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
 #pragma unroll
                   for (int p = 0; p < 3; ++p) ah[i][p][e] = (__bf16)0.0f;
           }
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][1], bh[j][1], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][2], bh[j][0], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][2], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][1], bh[j][0], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][1], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][0], acc[i][j], 0, 0, 0);
-            }
+          mma6<TM, TN>(acc, ah, bh);
           if constexpr (RS) {  // fused bias gradient: the fp32 A values are hi + mid + lo exactly
             if (do_rs) {
 #pragma unroll
@@ -1977,17 +2007,7 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
             }
 #pragma unroll
           for (int i = 0; i < TM; ++i) split3_bf16(&af[i][8 * hs], ah[i][0], ah[i][1], ah[i][2]);
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][1], bh[j][1], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][2], bh[j][0], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][2], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][1], bh[j][0], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][1], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][0], acc[i][j], 0, 0, 0);
-            }
+          mma6<TM, TN>(acc, ah, bh);
         }
         if constexpr (RS) {
           if (do_rs) {
@@ -2044,17 +2064,7 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
           for (int i = 0; i < TM; ++i) split3_bf16(&af[i][8 * hs], ah[i][0], ah[i][1], ah[i][2]);
 #pragma unroll
           for (int j = 0; j < TN; ++j) split3_bf16(&bf[j][8 * hs], bh[j][0], bh[j][1], bh[j][2]);
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][1], bh[j][1], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][2], bh[j][0], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][2], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][1], bh[j][0], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][1], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][0], acc[i][j], 0, 0, 0);
-            }
+          mma6<TM, TN>(acc, ah, bh);
         }
       } else {
 #pragma unroll
@@ -2117,17 +2127,7 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
             split3_bf16(b.v[j], bh[j][0], bh[j][1], bh[j][2]);
           }
         }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][1], bh[j][1], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][2], bh[j][0], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][2], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][1], bh[j][0], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][1], acc[i][j], 0, 0, 0);
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][0], bh[j][0], acc[i][j], 0, 0, 0);
-          }
+        mma6<TM, TN>(acc, ah, bh);
         if constexpr (RS) {
           if (do_rs) {  // after the MFMAs were issued: the adds ride in their shadow
 #pragma unroll

@@ -1074,6 +1074,20 @@ def attn_softmax_bwd_relpos_band(attn, dP, dS, dbd, ldp, drop_p, seed, sqrt_dk, 
                  float(sqrt_dk), rows, T, lds, _st())
 
 
+def relpos_dqv(dbd, ldp, p, ldpm, out, ldo, nb, H, T):
+    """dq_v[z] = dbd[z] . p_h over each row tile's rel_shift band (esp_relpos_dqv; latest, d_k = 64)."""
+    ws = _ws(_GEMM_WS, "esp_gemm_f32", _GEMM_WS_BYTES, out.device)
+    if _PROF is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
+    _native.call("esp_relpos_dqv", _p(dbd), ldp, _p(p), ldpm, _p(out), ldo, nb, H, T, _p(ws), _GEMM_WS_BYTES, _st())
+    _guard_post("esp_gemm_f32", ws, _GEMM_WS_BYTES)
+    if _PROF is not None:  # algorithmic work: the band only (T x T of the 2T-1 columns per row)
+        ev1.record()
+        _PROF.append((2.0 * T * 64 * T * nb * H, ev0, ev1, (KC, RC, T, 64, T, nb * H, "band"), 0.0))
+
+
 # dbd buffers of the latest rel_shift adjoint, kept per (device, Z, T, pitch) and zeroed once: the band
 # kernel writes each row's T band columns only, so the rest stays 0 for every layer and step (half the
 # adjoint's dbd bytes).  Made outside graph capture only (a buffer made inside would live in the graph's

@@ -273,6 +273,12 @@ int esp_relshift_bwd(const float* dS, long lds, float* dbd, long ldp, int relpos
 int esp_attn_softmax_bwd_relpos(const float* attn, const float* dP, float* dS, float* dbd, long ldp,
                                 int relpos, float drop_p, unsigned long long seed, float sqrt_dk,
                                 long rows, int T, long lds, const int* tvalid, void* stream);
+/* ABI 29: the latest rel_shift's q_v gradient through the band scores, dq_v[z] = dbd[z] . p_h (z = h*nb + b):
+ * the dbd.p contraction with each 128-row tile's k-loop over its rows' band union only (row i of dbd is 0
+ * outside columns T-1-i .. 2T-2-i).  dbd (nb*H*T rows, pitch ldp >= 2T-1, % 4 == 0), p (2T-1 rows, pitch
+ * ldpm, head h at column 64 h), out rows b*T + i (pitch ldo, head h at column 64 h); d_k = 64. */
+int esp_relpos_dqv(const float* dbd, long ldp, const float* p, long ldpm, float* out, long ldo, int nb, int H,
+                   int T, float* work, long work_bytes, void* stream);
 /* ABI 29: the latest form (P = 2T-1) writing only row i's band of dbd, columns T-1-i .. 2T-2-i, into a
  * buffer whose other elements are already 0 (kept and zeroed once by the caller: nothing else writes it);
  * half the dbd bytes of esp_attn_softmax_bwd_relpos.  lds % 4 == 0, attn / dP / dS 16-B aligned. */

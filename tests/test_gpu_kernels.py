@@ -1133,6 +1133,33 @@ def test_softmax_bwd_relpos_band_matches_full_rows(dev):
         assert torch.equal(full.view(Z * T, Pp)[:, cols], band.view(Z * T, Pp)[:, cols])
 
 
+def test_relpos_dqv_band_matches_dense_gemm(dev):
+    """esp_relpos_dqv (round 5): each 128-row tile's k-loop over its rows' rel_shift band only equals the
+    dense dbd.p GEMM over all 2T-1 columns bit for bit (the skipped slabs hold zeros; the kept slabs are the
+    dense GEMM's, same order), and the fp64 product.  B=48, H=4 (576 tiles: no split-K), T' = 374."""
+    B, H, T, dk = 48, 4, 374, 64
+    Z, D, P = B * H, H * dk, 2 * T - 1
+    Pp = K.pitch(P)
+    g = torch.Generator().manual_seed(5)
+    dbd = torch.zeros(Z * T, Pp)
+    vals = torch.randn(Z * T, T, generator=g)
+    i = torch.arange(T).repeat(Z)
+    cols = (T - 1 - i)[:, None] + torch.arange(T)[None, :]
+    dbd.scatter_(1, cols, vals)
+    p = torch.randn(P, D, generator=g) * 0.1
+    dbd, p = dbd.to(dev).reshape(-1), p.to(dev)
+    out0 = torch.empty(B * T, D, device=dev)
+    out1 = torch.empty(B * T, D, device=dev)
+    K.gemm(T, dk, P, dbd, p, out0, mode_a=K.KC, lda=Pp, mode_b=K.RC, ldb=D, ldc=D,
+           batch=Z, nb2=B, sa=(B * T * Pp, T * Pp), sb=(dk, 0), sc=(dk, T * D))
+    K.relpos_dqv(dbd, Pp, p, D, out1, D, B, H, T)
+    torch.cuda.synchronize()
+    assert torch.equal(out0, out1)
+    d = dbd.view(H, B, T, Pp)[..., :P].double().cpu()
+    ref = torch.einsum("hbik,khd->bihd", d, p.double().cpu().view(P, H, dk)).reshape(B * T, D)
+    assert (out1.double().cpu() - ref).abs().max().item() <= 1e-5 * ref.abs().max().item()
+
+
 def test_gemm_planes_output_epilogues(dev):
     """C written as planes (esp_gemm_f32_pl c_nplanes = 3): the FFN w_1 epilogue (bias + Swish / ReLU
     + dropout, derivative to aux) with A and B as planes, and the batched attention context P.V

@@ -1,6 +1,7 @@
 """One GEMM shape, repeated (for rocprofv3 --pmc passes and quick timings):
-    python tools/gemm_one.py mode_a mode_b M N K [reps] [--rowsum]
-fp32 operands (the default fp32 split-product path; weights are not parameters here, so PREC 0)."""
+    python tools/gemm_one.py mode_a mode_b M N K [reps] [--rowsum] [--bw]
+fp32 operands (the default fp32 split-product path; PREC 0, or with --bw B taken as a weight: its split
+planes made per call, PREC 3)."""
 import os
 import sys
 
@@ -22,7 +23,9 @@ def main():
     rs = torch.zeros(M, device=dev) if "--rowsum" in sys.argv else None
     lda = Kk if ma == K.KC else M
     ldb = Kk if mb == K.KC else N
-    fn = lambda: K.gemm(M, N, Kk, A, B, C, mode_a=ma, lda=lda, mode_b=mb, ldb=ldb, ldc=N, rowsum=rs)  # noqa: E731
+    bw = "--bw" in sys.argv
+    fn = lambda: K.gemm(M, N, Kk, A, B, C, mode_a=ma, lda=lda, mode_b=mb, ldb=ldb, ldc=N, rowsum=rs,  # noqa: E731
+                        b_weight=bw)
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
