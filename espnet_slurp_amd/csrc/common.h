@@ -105,15 +105,39 @@ __device__ __forceinline__ float fast_sigmoid(float v) {
 // values taken back from the packed bits.  The GEMMs' in-register split (gemm_kernels.h
 // split3_bf16) and every producer of planes (esp_f32_to_planes, LayerNorm, GEMM epilogues) use this,
 // so a planes operand holds exactly the values the in-register split would form.
+// ESP_SPLIT_DOT 1 (default): each residual is one v_dot2c_f32_bf16, r = v + (-1) * bf16part, which
+// takes the part straight from the packed pair (no unpack): 7 VALU per pair instead of 11 (the split is
+// the in-register GEMMs' VALU bound: 11 VALU per pair ~ the MFMA time of the six products,
+// profiles/r05m_*).  The residual is exactly representable, so it is exact under any rounding of the
+// dot's sum; 0: the unpack + v_sub form.
+#ifndef ESP_SPLIT_DOT
+#define ESP_SPLIT_DOT 1
+#endif
 __device__ __forceinline__ void split3_pair(float a, float b, uint32_t& hi, uint32_t& mid, uint32_t& lo) {
   typedef __attribute__((ext_vector_type(2))) float f2;
   typedef __attribute__((ext_vector_type(2))) __bf16 b2;
-  const uint32_t hp = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){a, b}, b2));
-  const float ra = a - __uint_as_float(hp << 16), rb = b - __uint_as_float(hp & 0xffff0000u);
-  const uint32_t mp = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){ra, rb}, b2));
-  const float sa = ra - __uint_as_float(mp << 16), sb = rb - __uint_as_float(mp & 0xffff0000u);
-  hi = hp;
-  mid = mp;
+  const b2 hp = __builtin_convertvector((f2){a, b}, b2);
+#if ESP_SPLIT_DOT
+  // the (-1, 0) / (0, -1) bf16 pairs from SGPRs: as an inline constant the assembler encodes (-1, 0) as
+  // the fp32 -1.0, which the hardware reads as the pair (0, -1)
+  uint32_t na, nb;
+  asm("s_mov_b32 %0, 0xbf80" : "=s"(na));
+  asm("s_mov_b32 %0, 0xbf800000" : "=s"(nb));
+  const b2 NA = __builtin_bit_cast(b2, na), NB = __builtin_bit_cast(b2, nb);
+  const float ra = __builtin_amdgcn_fdot2_f32_bf16(hp, NA, a, false);
+  const float rb = __builtin_amdgcn_fdot2_f32_bf16(hp, NB, b, false);
+  const b2 mp = __builtin_convertvector((f2){ra, rb}, b2);
+  const float sa = __builtin_amdgcn_fdot2_f32_bf16(mp, NA, ra, false);
+  const float sb = __builtin_amdgcn_fdot2_f32_bf16(mp, NB, rb, false);
+#else
+  const uint32_t hu = __builtin_bit_cast(uint32_t, hp);
+  const float ra = a - __uint_as_float(hu << 16), rb = b - __uint_as_float(hu & 0xffff0000u);
+  const b2 mp = __builtin_convertvector((f2){ra, rb}, b2);
+  const uint32_t mu = __builtin_bit_cast(uint32_t, mp);
+  const float sa = ra - __uint_as_float(mu << 16), sb = rb - __uint_as_float(mu & 0xffff0000u);
+#endif
+  hi = __builtin_bit_cast(uint32_t, hp);
+  mid = __builtin_bit_cast(uint32_t, mp);
   lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){sa, sb}, b2));
 }
 // bf16x2 (round to nearest even) of a pair: the n = 1 "planes" (the reduced-precision operand)

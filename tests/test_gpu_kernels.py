@@ -131,9 +131,13 @@ def _with_bplanes(on, fn):
 
 
 def test_f32_to_planes_exact_split(dev):
-    """esp_f32_to_planes: hi + mid + lo == x exactly (fp64 sum) for finite x over 40 binades,
-    hi == bf16(x) (round to nearest even, torch's cast), zeroed pitch padding."""
-    x = (_r(37, 203, seed=5) * torch.exp2(torch.randint(-20, 20, (37, 203), generator=torch.Generator().manual_seed(6)).float()))
+    """esp_f32_to_planes: hi + mid + lo == x exactly (fp64 sum) for normal x over 200 binades, and each
+    part is the round-to-nearest-even bf16 of the exact residual: hi == bf16(x), mid == bf16(x - hi),
+    lo == bf16(x - hi - mid) (torch's casts on the CPU; the residuals are exact fp32 differences) -- the
+    definition the in-register split (split3_pair, ESP_SPLIT_DOT) must meet bit for bit.  Zeroed pitch
+    padding."""
+    x = (_r(37, 203, seed=5) * torch.exp2(torch.randint(-100, 100, (37, 203), generator=torch.Generator().manual_seed(6)).float()))
+    x[0, :4] = torch.tensor([0.0, -0.0, 1.0 + 2.0 ** -23, -(1.0 + 2.0 ** -8 + 2.0 ** -16)])
     xd = x.to(dev)
     pl, ldp, ps = K.planes(xd, 0, 37, 203, 203)
     torch.cuda.synchronize()
@@ -141,7 +145,12 @@ def test_f32_to_planes_exact_split(dev):
     p = pl.cpu().view(3, 37, 208)
     s = p[0, :, :203].double() + p[1, :, :203].double() + p[2, :, :203].double()
     assert torch.equal(s, x.double())
-    assert torch.equal(p[0, :, :203], x.to(torch.bfloat16))
+    hi = x.to(torch.bfloat16)
+    r1 = x - hi.float()
+    mid = r1.to(torch.bfloat16)
+    lo = (r1 - mid.float()).to(torch.bfloat16)
+    for got, want in ((p[0, :, :203], hi), (p[1, :, :203], mid), (p[2, :, :203], lo)):
+        assert torch.equal(got.view(torch.int16), want.view(torch.int16))
     assert not p[:, :, 203:].float().any()
 
 

@@ -1,7 +1,7 @@
 """One GEMM shape, repeated (for rocprofv3 --pmc passes and quick timings):
     python tools/gemm_one.py mode_a mode_b M N K [reps] [--rowsum] [--bw]
 fp32 operands (the default fp32 split-product path; PREC 0, or with --bw B taken as a weight: its split
-planes made per call, PREC 3)."""
+planes made per call, PREC 3; --pl: both operands given as split planes made once, PREC 5)."""
 import os
 import sys
 
@@ -24,6 +24,9 @@ def main():
     lda = Kk if ma == K.KC else M
     ldb = Kk if mb == K.KC else N
     bw = "--bw" in sys.argv
+    if "--pl" in sys.argv:
+        A = K.Planes.of(A.view(M, Kk) if ma == K.KC else A.view(Kk, M))
+        B = K.Planes.of(B.view(N, Kk) if mb == K.KC else B.view(Kk, N))
     fn = lambda: K.gemm(M, N, Kk, A, B, C, mode_a=ma, lda=lda, mode_b=mb, ldb=ldb, ldc=N, rowsum=rs,  # noqa: E731
                         b_weight=bw)
     for _ in range(3):
