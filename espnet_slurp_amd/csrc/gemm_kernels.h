@@ -1718,8 +1718,13 @@ constexpr int glds_occupancy() {
 // profiles/r03i_abc_split_code.txt)
 __device__ __forceinline__ void split3_bf16(const float* v, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
   uint32_t H[4], Md[4], L[4];
+  if constexpr ((kGemmAbl & 128) != 0) {  // diagnostic: hi only (mid = lo = hi), wrong results
 #pragma unroll
-  for (int p = 0; p < 4; ++p) esp::split3_pair(v[2 * p], v[2 * p + 1], H[p], Md[p], L[p]);
+    for (int p = 0; p < 4; ++p) H[p] = Md[p] = L[p] = esp::bf16_pair(v[2 * p], v[2 * p + 1]);
+  } else {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) esp::split3_pair(v[2 * p], v[2 * p + 1], H[p], Md[p], L[p]);
+  }
   hi = __builtin_bit_cast(bf16x8, make_uint4(H[0], H[1], H[2], H[3]));
   mid = __builtin_bit_cast(bf16x8, make_uint4(Md[0], Md[1], Md[2], Md[3]));
   lo = __builtin_bit_cast(bf16x8, make_uint4(L[0], L[1], L[2], L[3]));
@@ -1730,6 +1735,10 @@ __device__ __forceinline__ void split3_bf16(const float* v, bf16x8& hi, bf16x8& 
 // hi.hi).  ESP_GEMM_MFMA_ORDER 0: each pair's six MFMAs back to back (one accumulator chain at a time);
 // 1: product-major, the TM x TN independent accumulators interleaved -- each accumulator receives the same
 // products in the same order either way (bit-identical results)
+// diagnostic scheduling hint (iglp_opt strategy in the k-loop bodies; -1: none)
+#ifndef ESP_GEMM_IGLP
+#define ESP_GEMM_IGLP -1
+#endif
 #ifndef ESP_GEMM_MFMA_ORDER
 #define ESP_GEMM_MFMA_ORDER 0
 #endif
@@ -1871,6 +1880,9 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
     // k >= kv values are zeroed in registers (B's staged tail holds finite clamped elements), so
     // no LDS zero pass and no extra barrier
     auto compute = [&](const float* cur, int kv) {
+#if ESP_GEMM_IGLP >= 0
+      __builtin_amdgcn_iglp_opt(ESP_GEMM_IGLP);
+#endif
       if constexpr (PREC == 2) {
         // fragments as 4 chunks of 8 bf16 per tile (k = 32h + 8t + 0..7 for chunk t)
         float4 a4[TM][4], b4[TN][4];
@@ -2108,6 +2120,9 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
       }
     };
     auto mma_half = [&](int hs, int kv, FragA& a, FragB& b) {
+#if ESP_GEMM_IGLP >= 0
+      __builtin_amdgcn_iglp_opt(ESP_GEMM_IGLP);
+#endif
       if constexpr (PIPE) {
         if (kv < GL_BK) {  // K tail: A's k >= kv are 0 (B's clamped tail holds finite values)
 #pragma unroll
