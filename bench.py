@@ -441,12 +441,16 @@ def main():
             # the second kernel the round-1 verdict named: rel-pos attention probabilities
             # (algorithmic ac + bd work, 4 T'^2 d_k per head and utterance, no padded tiles; P and
             # its dropout copy written once)
+            # peak: the MFMA form the kernel issues -- bf16 operands on the bf16 MFMA in the bf16 mode (the
+            # bf16 dense peak), six split products per fp32 product otherwise (the split ceiling, as the GEMMs)
             "attention_roofline": None if not attn_launches else {
-                "kernel": "relpos_attn_fwd16_kernel (esp_relpos_attn_probs), HIP events on the same eager replay",
+                "kernel": "relpos_probs_lds_kernel (esp_relpos_attn_probs), HIP events on the same eager replay",
                 "flops_per_launch": round(attn_flops / attn_launches),
                 "launches": attn_launches, "avg_launch_us": round(1e3 * attn_ms / attn_launches, 2),
-                "achieved": round(attn_flops / (attn_ms * 1e-3) / 1e12, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(attn_flops / (attn_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
+                "achieved": round(attn_flops / (attn_ms * 1e-3) / 1e12, 2), "peak": peak,
+                "unit": "TFLOP/s", "frac": round(attn_flops / (attn_ms * 1e-3) / 1e12 / peak, 4),
+                "f32_mfma_peak_frac": None if args.amp else round(
+                    attn_flops / (attn_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4),
                 "write_GBps": round(attn_bytes / (attn_ms * 1e-3) / 1e9, 1)},
             "step_roofline": {"train_gflop_per_utt": round(train / 1e9, 2),
                               "achieved_tflops": round(value / world * train / 1e12, 2),
