@@ -180,7 +180,7 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
   GldsArgs x{};
   if (MA == I2CT_KC) x = *tconv;  // the transposed-conv gather parameters
   x.ntx = (g.N + BNT - 1) / BNT;
-  const int bm = g.bm == 64 ? g.bm : BM;
+  const int bm = g.bm == 64 || g.bm == 256 ? g.bm : BM;
   x.nty = (g.M + bm - 1) / bm;
   if (MA == I2C_KC) {
     x.c_a = make_fastdiv(g.a.ic.C);
@@ -657,6 +657,14 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
 
     // (256 x 128 bf16 tiles -- one block, one wave per SIMD, per CU -- measured slower, C5 B=64 860.3 vs
     // 889.3 utt/s, and were removed in round 5)
+#if ESP_GEMM_WIDE
+    // 256 x 128 tiles of 8 waves (two per SIMD in one block per CU, a 3-slab ring where it fits): the 32-bit
+    // staging offsets of 256 KC rows / a 256-pixel run within <= 2 maps
+    if (g.bnt == 128 && g.bm == BM && (g.bf16 == 0 || g.bf16 == 1 || g.bf16 == 3) && !smb && M >= 256 &&
+        mode_b != I2C_RC && (mode_a != KC || 256L * g.a.ld * 4 < (1L << 32)) &&
+        (mode_a != I2C_KC || (long)g.a.ic.Ho * g.a.ic.Wo >= 256))
+      g.bm = 256;
+#endif
   }
   {
     const long tiles = ntiles(g.bnt ? g.bnt : BN, g.bm);
@@ -671,12 +679,12 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
       const long by_k = K / mink;
       if (sp > by_k) sp = by_k;
       // in-kernel combine (LDS-DMA kernel): partials on whole tiles + tickets in the last 64 KB
-      const int bmt = g.bm == 64 ? g.bm : BM;
+      const int bmt = g.bm == 64 || g.bm == 256 ? g.bm : BM;
       const long mp = (long)(M + bmt - 1) / bmt * bmt, np = g.bnt ? (long)(N + g.bnt - 1) / g.bnt * g.bnt : N;
       // opt-in (ESP_SPLITK_INKERNEL=1): measured slower at C2 B=128 -- the last-arriving unit of a
       // tile sums all of its splits alone (64 splits x 32 KB behind 8 tiles for the d x d weight
       // gradients: 222 vs 68 us), where the separate reduction spreads them over the chip
-      const bool inkernel = splitk_mode() == 1 && g.bnt && !bplanes && tiles <= ESP_GEMM_TICKETS &&
+      const bool inkernel = splitk_mode() == 1 && g.bnt && !bplanes && g.bm != 256 && tiles <= ESP_GEMM_TICKETS &&
                             work_bytes > ESP_GEMM_TICKET_BYTES;
       const long part = inkernel ? mp * np : (long)M * N;
       const long cap = (work_bytes - (inkernel ? ESP_GEMM_TICKET_BYTES : 0)) / (4L * (part * batch + (rowsum ? M : 0)));

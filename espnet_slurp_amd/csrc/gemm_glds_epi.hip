@@ -15,13 +15,13 @@ bool glds_launch_epi(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hipS
     constexpr bool can_bwd = (MA == KC || MA == I2CT_KC) && MB == RC;
     if constexpr (can_fwd) {
       if (epi == EPI_FWD) {
-        hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_FWD, BF, BMT>), grid, dim3(NT), 0, st, g, x);
+        hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_FWD, BF, BMT>), grid, dim3(glds_threads(BMT)), 0, st, g, x);
         ok = true;
       }
     }
     if constexpr (can_bwd) {
       if (epi == EPI_BWD) {
-        hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_BWD, BF, BMT>), grid, dim3(NT), 0, st, g, x);
+        hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_BWD, BF, BMT>), grid, dim3(glds_threads(BMT)), 0, st, g, x);
         ok = true;
       }
     }

@@ -12,11 +12,11 @@ bool glds_launch_plain(int ma, int mb, int bnt, int prec, bool rs, dim3 grid, hi
     constexpr int BF = decltype(F)::value, BMT = decltype(R)::value;
     if constexpr (MA == RC) {
       if (rs) {
-        hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, true, EPI_PLAIN, BF, BMT>), grid, dim3(NT), 0, st, g, x);
+        hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, true, EPI_PLAIN, BF, BMT>), grid, dim3(glds_threads(BMT)), 0, st, g, x);
         return;
       }
     }
-    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_PLAIN, BF, BMT>), grid, dim3(NT), 0, st, g, x);
+    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_PLAIN, BF, BMT>), grid, dim3(glds_threads(BMT)), 0, st, g, x);
   });
 }
 

@@ -14,19 +14,19 @@ bool glds_launch_pspec(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hi
     constexpr int BF = decltype(F)::value, BMT = decltype(R)::value;
     if constexpr ((MA == KC || MA == RC) && (MB == KC || MB == RC)) {
       if (epi == EPI_P0) {
-        hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_P0, BF, BMT>), grid, dim3(NT), 0, st, g, x);
+        hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_P0, BF, BMT>), grid, dim3(glds_threads(BMT)), 0, st, g, x);
         ok = true;
       } else if (epi == EPI_PR) {
-        hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_PR, BF, BMT>), grid, dim3(NT), 0, st, g, x);
+        hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_PR, BF, BMT>), grid, dim3(glds_threads(BMT)), 0, st, g, x);
         ok = true;
       } else if constexpr (MA == KC && MB == RC && BF <= 1) {  // the attention context as planes (P.V)
         if (epi == EPI_P0_PL) {
-          hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_P0_PL, BF, BMT>), grid, dim3(NT), 0, st, g, x);
+          hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_P0_PL, BF, BMT>), grid, dim3(glds_threads(BMT)), 0, st, g, x);
           ok = true;
         }
       } else if constexpr (MA == KC && MB == KC && BF == 0) {
         if (epi == EPI_SMB) {
-          hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_SMB, BF, BMT>), grid, dim3(NT), 0, st, g, x);
+          hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, EPI_SMB, BF, BMT>), grid, dim3(glds_threads(BMT)), 0, st, g, x);
           ok = true;
         }
       }

@@ -18,7 +18,7 @@ bool glds_launch_spec(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hip
     constexpr int BF = decltype(F)::value, BMT = decltype(R)::value;
 #define ESP_SPEC(K)                                                                                   \
   if (epi == K) {                                                                                     \
-    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, K, BF, BMT>), grid, dim3(NT), 0, st, g, x); \
+    hipLaunchKernelGGL((gemm_glds_kernel<MA, MB, BNT, false, K, BF, BMT>), grid, dim3(glds_threads(BMT)), 0, st, g, x); \
     ok = true;                                                                                        \
   }
     if constexpr (MA == KC && MB == KC) {

@@ -1241,6 +1241,17 @@ struct GldsArgs {
 constexpr int kGemmAbl = ESP_GEMM_ABL_BITS;
 
 constexpr int GL_BK = 32;
+// LDS slab ring depth of the LDS-DMA kernel: 2 (double buffer: slab k+1 in flight while k is read, every
+// slab waits vmcnt(0)); 3: slabs k+1 and k+2 in flight across tile boundaries, a counted vmcnt leaves the
+// newer one in flight at the slab barrier (1.5x the LDS: one 128x128 block per CU)
+#ifndef ESP_GEMM_WIDE
+#define ESP_GEMM_WIDE 0
+#endif
+#ifndef ESP_GEMM_STAGES
+#define ESP_GEMM_STAGES 2
+#endif
+constexpr int GL_ST = ESP_GEMM_STAGES;
+static_assert(GL_ST == 2 || GL_ST == 3, "ESP_GEMM_STAGES: 2 or 3");
 
 // K-contiguous slab image: row r (128 B = 8 quads) holds global quad q at position q ^ kc_swz(r).
 // A ds_read_b128 of frag16 serves 16-lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32)
@@ -1295,8 +1306,9 @@ __device__ __forceinline__ int bf16_rc_swz(int rowb, int kr) {
 // B16 (PREC 2, bf16 pairs; I2C_RC: the bf16 conv2 weight gradient's gathered B): the slab is the bf16
 // RC image of StageS (64 pixel k-rows x ROWS bf16 columns, 16-B chunks of 8 channels XOR-swizzled by
 // k-row, bf16_rc_swz) and the im2col offsets are computed in bf16 elements (ic.C = bf16 channels)
-template <int MODE, int ROWS, int NI, bool B16 = false>
+template <int MODE, int ROWS, int NI, bool B16 = false, int NW = 4>
 struct Stage {
+  static constexpr int kNI = NI;  // DMA instructions per slab issue (per wave)
   static constexpr bool kKC = MODE == KC || MODE == I2C_KC || MODE == I2CT_KC;
   static_assert(!B16 || MODE == I2C_RC || kKC, "Stage<B16>: bf16 pairs for the gathered operands only");
   const float* p[NI];  // per instruction: base incl. the slab-invariant part
@@ -1307,7 +1319,7 @@ struct Stage {
                                        int lane, const GldsArgs* x = nullptr) {
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int slot = (i * 4 + wave) * 64 + lane;
+      const int slot = (i * NW + wave) * 64 + lane;
       if constexpr (kKC) {
         const int r = slot >> 3, qs = slot & 7;
         const int qq = qs ^ kc_swz(r);
@@ -1358,7 +1370,7 @@ struct Stage {
     }
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      float* ldsw = dst + (i * 4 + wave) * 256;
+      float* ldsw = dst + (i * NW + wave) * 256;
       if constexpr (kKC) {
         const int k = min(k0 + q[i], (K - 1) & ~3);
         if constexpr (MODE == KC) lds_dma16(p[i] + k, ldsw);
@@ -1410,8 +1422,9 @@ __device__ __forceinline__ uint32_t lds_addr(const float* p) {
 // by k-row (bf16_rc_swz) for the transposing reads of frag_tr16.  K and k0 count pairs; an RC
 // k-row index is 2 * k + (0..63).  `rows` and `ld` of an RC operand: bf16 rows, ld in pairs.
 
-template <int MODE, int ROWS, int NI, bool B16 = false>
+template <int MODE, int ROWS, int NI, bool B16 = false, int NW = 4>
 struct StageS {
+  static constexpr int kNI = NI;
   static constexpr bool kKC = MODE == KC || MODE == I2C_KC;
   static constexpr bool kT16 = B16 && MODE == RC;  // transposed-read bf16 image
   const float* base;
@@ -1433,7 +1446,7 @@ struct StageS {
     }
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int slot = (i * 4 + wave) * 64 + lane;
+      const int slot = (i * NW + wave) * 64 + lane;
       if constexpr (kKC) {
         const int r = slot >> 3, qq = (slot & 7) ^ kc_swz(r);
         const int gr = min(row0 + r, rows - 1);
@@ -1469,7 +1482,7 @@ struct StageS {
     }
     if (MODE == I2C_KC || k0 + GL_BK <= K) {
 #pragma unroll
-      for (int i = 0; i < NI; ++i) lds_dma16_s(sb, off[i], dst + (i * 4 + wave) * 1024);
+      for (int i = 0; i < NI; ++i) lds_dma16_s(sb, off[i], dst + (i * NW + wave) * 1024);
     } else {
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
@@ -1477,7 +1490,7 @@ struct StageS {
         if constexpr (MODE == KC) o -= 4u * (uint32_t)max(0, q[i] - (((K - 1) & ~3) - k0));
         else if constexpr (kT16) o -= 4u * (uint32_t)ld * (uint32_t)max(0, q[i] - (2 * (K - k0) - 1));
         else o -= 4u * (uint32_t)ld * (uint32_t)max(0, q[i] - (K - 1 - k0));
-        lds_dma16_s(sb, o, dst + (i * 4 + wave) * 1024);
+        lds_dma16_s(sb, o, dst + (i * NW + wave) * 1024);
       }
     }
   }
@@ -1526,10 +1539,11 @@ __device__ __forceinline__ void frag_tr16(const float* slab, int rbase, int lane
 // Host: K % 8 == 0 (KC), N % 8 == 0 (RC), 16-B aligned planes, ld / strides / ps % 8 == 0.
 __device__ __forceinline__ int pl_kc_swz(int r) { return (r >> 2) & 3; }
 
-template <int MODE, int ROWS>
+template <int MODE, int ROWS, int NW = 4>
 struct StageP {
   static constexpr int PLB = ROWS * 64;           // bytes of one plane's slab image
-  static constexpr int NI = PLB / 1024 / 4;       // wave instructions per plane per wave
+  static constexpr int NI = PLB / 1024 / NW;      // wave instructions per plane per wave
+  static constexpr int kNI = 3 * NI;
   const char* base;  // plane 0 at the tile's first row / k-row kb (bytes)
   long ld, psb;      // ld in bf16 elements, plane stride in bytes
   int kb;
@@ -1544,7 +1558,7 @@ struct StageP {
     base = reinterpret_cast<const char*>(MODE == KC ? zb + (long)row0 * op.ld + kbeg : zb + (long)kbeg * op.ld);
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int slot = (i * 4 + wave) * 64 + lane;
+      const int slot = (i * NW + wave) * 64 + lane;
       if constexpr (MODE == KC) {
         const int r = slot >> 2, gc = (slot & 3) ^ pl_kc_swz(r);
         const int gr = min(row0 + r, rows - 1);
@@ -1571,7 +1585,7 @@ struct StageP {
           if constexpr (MODE == KC) o -= 2u * (uint32_t)max(0, q[i] - (K - 8 - k0));
           else o -= 2u * (uint32_t)ld * (uint32_t)max(0, q[i] - (K - 1 - k0));
         }
-        lds_dma16_s(reinterpret_cast<const float*>(sb + p * psb), o, dst + p * PLB + (i * 4 + wave) * 1024);
+        lds_dma16_s(reinterpret_cast<const float*>(sb + p * psb), o, dst + p * PLB + (i * NW + wave) * 1024);
       }
   }
 };
@@ -1632,6 +1646,11 @@ __device__ __forceinline__ void frag8(const float* slab, int r, int h, int hs, f
 
 __device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+template <int N>
+__device__ __forceinline__ void wait_vm_n() {
+  static_assert(N >= 0 && N < 64, "vmcnt: 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 // s_barrier without __syncthreads()'s fence (which would drain vmcnt); the empty asm keeps
 // the compiler from moving LDS accesses across it
 __device__ __forceinline__ void raw_barrier() {
@@ -1680,12 +1699,24 @@ __device__ __forceinline__ TileCoord tile_coord(const GemmArgs& g, const GldsArg
 // PREC 3 (B as three bf16 planes: 1.5x the B slab bytes) is also bounded by LDS: 128x128 tiles use
 // exactly 80 KB (two per CU), 128x64 56 KB (two), 64x64 40 KB (four); PREC 5 (both operands as
 // planes): 128x64 72 KB (two), 64x64 48 KB (three)
+// 256 x 128 tiles (ESP_GEMM_WIDE builds): 8 waves (two per SIMD in one block per CU), each wave the 64 x 64
+// of a 128 x 128 tile's wave; a 3-slab ring where 3 slabs fit the LDS
+constexpr int glds_threads(int BMT) { return BMT == 256 ? 512 : NT; }
+constexpr int glds_stage_bytes(int BNT, int BMT, int PREC) {
+  return 4 * ((PREC == 5 ? 48 * BMT : BMT * GL_BK) + (PREC >= 3 ? 48 * BNT : BNT * GL_BK));
+}
+#ifndef ESP_GEMM_WIDE_STAGES
+#define ESP_GEMM_WIDE_STAGES 3
+#endif
+constexpr int glds_stages(int BNT, int BMT, int PREC) {
+  return BMT == 256 ? (ESP_GEMM_WIDE_STAGES == 3 && 3 * glds_stage_bytes(BNT, BMT, PREC) + 16 <= 163840 ? 3 : 2) : GL_ST;
+}
 constexpr int glds_lds_bytes(int BNT, int BMT, int PREC) {
-  return 2 * 4 * ((PREC == 5 ? 48 * BMT : BMT * GL_BK) + (PREC >= 3 ? 48 * BNT : BNT * GL_BK)) + (PREC >= 3 ? 0 : 16);
+  return glds_stages(BNT, BMT, PREC) * glds_stage_bytes(BNT, BMT, PREC) + (PREC >= 3 ? 0 : 16);
 }
 template <int BNT, int EPI, int BMT = BM, int PREC = 0>
 constexpr int glds_occupancy() {
-  // (256 x 128 bf16 tiles: 96 KB of LDS, one block -- one wave per SIMD -- per CU)
+  // (256 x 128 tiles: 8 waves in one block per CU)
   constexpr int by_regs = BMT == 256 ? 1 : BMT == 64 ? 4 : (BNT == 64 && (EPI == EPI_PLAIN || EPI >= EPI_BIAS)) ? 3 : 2;
   constexpr int by_lds = 163840 / glds_lds_bytes(BNT, BMT, PREC);
   return by_regs < by_lds ? by_regs : by_lds;
@@ -1765,10 +1796,11 @@ __device__ __forceinline__ void mma6(f32x16 (&acc)[TM][TN], const bf16x8 (&ah)[T
 }
 
 template <int MA, int MB, int BNT, bool RS, int EPI, int PREC = 0, int BMT = BM>
-__global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void gemm_glds_kernel(GemmArgs g, GldsArgs x) {
-  constexpr int WN = BMT == 64 ? 2 : BNT / 64, WM = 4 / WN, TM = BMT / (WM * 32), TN = BNT / (WN * 32);
-  static_assert(BMT == 128 || (BMT == 64 && BNT == 64) || (BMT == 256 && BNT == 128 && PREC == 2),
-                "64-row tiles are 64 wide; 256-row tiles: 128 wide, bf16 operands");
+__global__ __launch_bounds__(glds_threads(BMT), (glds_occupancy<BNT, EPI, BMT, PREC>())) void gemm_glds_kernel(GemmArgs g, GldsArgs x) {
+  constexpr int NTK = glds_threads(BMT), NW = NTK / 64, ST = glds_stages(BNT, BMT, PREC);
+  constexpr int WN = BMT == 64 ? 2 : BNT / 64, WM = NW / WN, TM = BMT / (WM * 32), TN = BNT / (WN * 32);
+  static_assert(BMT == 128 || (BMT == 64 && BNT == 64) || (BMT == 256 && BNT == 128 && PREC != 5),
+                "64-row tiles are 64 wide; 256-row tiles: 128 wide");
   static_assert(PREC < 3 || MB == KC || MB == RC, "B planes: KC / RC operands");
   static_assert(PREC != 5 || MA == KC || MA == RC, "A planes: KC / RC operands");
   constexpr bool BP = PREC >= 3;                 // B as three bf16 planes (StageP)
@@ -1792,10 +1824,10 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
   constexpr int PLF = BNT * 16;                  // floats per B plane image (BNT x 32 bf16)
   constexpr int PLA = BMT * 16;                  // floats per A plane image
   constexpr int A_SZ = AP ? 3 * PLA : BMT * GL_BK, B_SZ = BP ? 3 * PLF : BNT * GL_BK, BUF = A_SZ + B_SZ;
-  constexpr int NIA = A_SZ / 4 / NT, NIB = B_SZ / 4 / NT;
+  constexpr int NIA = A_SZ / 4 / NTK, NIB = B_SZ / 4 / NTK;
   // + the split-K combine flag (the in-kernel combine is never used with B planes: their 128x128
   // tiles need exactly 80 KB for two blocks per CU)
-  __shared__ __attribute__((aligned(16))) float smem[2 * BUF + (BP ? 0 : 4)];
+  __shared__ __attribute__((aligned(16))) float smem[ST * BUF + (BP ? 0 : 4)];
 
   const int G = gridDim.x;
   int t = blockIdx.x;
@@ -1824,11 +1856,11 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
   // scalar-base staging (StageS) for KC / RC / implicit-im2col A; the gathered operands keep
   // per-lane 64-bit addresses (Stage); B planes: StageP
   constexpr bool SA_S = MA == KC || MA == RC || MA == I2C_KC, SB_S = MB == KC || MB == RC;
-  using SAt = std::conditional_t<AP, StageP<MA, BMT>,
-                                 std::conditional_t<SA_S, StageS<MA, BMT, NIA, PREC == 2>, Stage<MA, BMT, NIA>>>;
-  using SBt = std::conditional_t<BP, StageP<MB, BNT>,
-                                 std::conditional_t<SB_S, StageS<MB, BNT, NIB, PREC == 2>,
-                                                    Stage<MB, BNT, NIB, PREC == 2 && MB == I2C_RC>>>;
+  using SAt = std::conditional_t<AP, StageP<MA, BMT, NW>,
+                                 std::conditional_t<SA_S, StageS<MA, BMT, NIA, PREC == 2, NW>, Stage<MA, BMT, NIA, false, NW>>>;
+  using SBt = std::conditional_t<BP, StageP<MB, BNT, NW>,
+                                 std::conditional_t<SB_S, StageS<MB, BNT, NIB, PREC == 2, NW>,
+                                                    Stage<MB, BNT, NIB, PREC == 2 && MB == I2C_RC, NW>>>;
   SAt sa;
   SBt sb;
   auto init_ab = [&](const TileCoord& cc) {
@@ -1852,8 +1884,44 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
 
   TileCoord c = tile_coord<BNT, BMT>(g, x, t, G);
   init_ab(c);
-  issue_ab(c.kbeg, smem);
-  wait_vm0();
+  // GL_ST == 3: the DMA cursor (tile dtile, slab dkt of dc) runs two slabs ahead of the k-loop, across
+  // tile boundaries; each issue is NSLAB DMA instructions per wave
+  constexpr int NSLAB = SAt::kNI + SBt::kNI;
+  TileCoord dc = c;
+  int dkt = 0, dtile = t, slot = 0;
+  bool dmore = true;
+  auto dma_issue = [&](float* dst) -> bool {
+    if (!dmore) return false;
+    issue_ab(dc.kbeg + dkt * GL_BK, dst);
+    if (++dkt == dc.nk) {
+      dtile += G;
+      if (dtile < x.ntiles) {
+        dc = tile_coord<BNT, BMT>(g, x, dtile, G);
+        init_ab(dc);
+        dkt = 0;
+      } else {
+        dmore = false;
+      }
+    }
+    return true;
+  };
+  // the slab ring advance: this wave's DMA of the next slab landed (the one after it may stay in flight),
+  // this wave's reads of this slab done, then everyone's
+  auto finish3 = [&](bool ahead) {
+    if (ahead) wait_vm_n<NSLAB>();
+    else wait_vm0();
+    wait_lgkm0();
+    raw_barrier();
+    slot = slot == ST - 1 ? 0 : slot + 1;
+  };
+  if constexpr (ST == 3) {
+    dma_issue(smem);
+    if (dma_issue(smem + BUF)) wait_vm_n<NSLAB>();
+    else wait_vm0();
+  } else {
+    issue_ab(c.kbeg, smem);
+    wait_vm0();
+  }
   raw_barrier();
   int buf = 0;
 
@@ -2165,7 +2233,32 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
       buf ^= 1;
     };
 
-    if constexpr (PIPE) {
+    if constexpr (ST == 3) {
+      // the 3-slab ring: slab kt + 2 (of this or a later tile) is issued as slab kt is read
+      if constexpr (PIPE) {
+        FragA Fa, Ga;
+        FragB Fb, Gb;
+        load_half(smem + slot * BUF, 0, Fa, Fb);
+        for (int kt = 0; kt < c.nk; ++kt) {
+          const bool ahead = dma_issue(smem + (slot == 0 ? 2 : slot - 1) * BUF);
+          const bool last = kt + 1 == c.nk;
+          const int kv = last ? c.kend - (c.kbeg + kt * GL_BK) : GL_BK;
+          load_half(smem + slot * BUF, 1, Ga, Gb);
+          mma_half(0, kv, Fa, Fb);
+          finish3(ahead);
+          if (!last) load_half(smem + slot * BUF, 0, Fa, Fb);
+          mma_half(1, kv, Ga, Gb);
+        }
+      } else {
+        for (int kt = 0; kt < c.nk; ++kt) {
+          const bool ahead = dma_issue(smem + (slot == 0 ? 2 : slot - 1) * BUF);
+          const int kv = kt + 1 == c.nk ? c.kend - (c.kbeg + kt * GL_BK) : GL_BK;
+          compute(smem + slot * BUF, kv);
+          finish3(ahead);
+        }
+      }
+      if (has_next) cn = tile_coord<BNT, BMT>(g, x, tnext, G);
+    } else if constexpr (PIPE) {
       // fp32 split products (PREC 0 / 3), software-pipelined by k-step: the fragments of k-step hs+1
       // are read while the MFMAs of k-step hs issue, and the slab barrier sits BETWEEN a slab's two
       // k-steps -- after it the wave issues k-step 1's MFMAs (operands already in registers) while
@@ -2229,7 +2322,7 @@ __global__ __launch_bounds__(NT, (glds_occupancy<BNT, EPI, BMT, PREC>())) void g
     if (!BP && g.tickets) {  // in-kernel split-K: write-through partial tile, ticket, last unit combines
       float* Wz = g.work + ((long)c.split * g.batch + c.z) * ((long)g.sk_mp * g.sk_np);
       store_cols<EPI_P0, TM, TN, true, 16>(g, 0, g.sk_np, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, lane, acc, Wz);
-      splitk_combine<BMT, BNT>(g, c.z, c.m0 / BMT, c.tn, x.ntx, x.nty, reinterpret_cast<int*>(smem + 2 * BUF));
+      splitk_combine<BMT, BNT>(g, c.z, c.m0 / BMT, c.tn, x.ntx, x.nty, reinterpret_cast<int*>(smem + ST * BUF));
     } else if (!(kGemmAbl & 2)) {
       float* W = g.splits > 1 ? g.work + ((long)c.split * g.batch + c.z) * (long)g.M * g.N : nullptr;
       if constexpr (EPI >= EPI_BIAS) {  // specialised kinds: never split-K, always wide
@@ -2304,6 +2397,14 @@ bool glds_switch(int ma, int mb, int bnt, int prec, int bm, F&& f) {
       }
       return false;
     }
+#if ESP_GEMM_WIDE
+    if (bm == 256) {  // 256 x 128 tiles, 8 waves: fp32 operands (PREC 0 / 1) and B planes (PREC 3)
+      if constexpr (MA_ != RC || MB_ != I2C_RC) {
+        if (bnt == 128 && (prec == 0 || prec == 1 || prec == 3)) return by_prec(IC<128>{}, IC<256>{});
+      }
+      return false;
+    }
+#endif
     return bnt == 64 ? by_prec(IC<64>{}, IC<BM>{}) : by_prec(IC<128>{}, IC<BM>{});
   };
   switch (ma * 8 + mb) {

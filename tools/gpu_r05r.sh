@@ -1,0 +1,12 @@
+#!/bin/bash
+# round 5: 3-slab LDS ring (ESP_GEMM_STAGES=3, libespnet_mi355_w.so) vs the double buffer: GEMM parity
+# under the variant, GEMM timings, bench A/B
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+T=gpurun_out/r05r_gemm.txt
+rm -f $T
+bash gpurun_steps.sh \
+  "ESP_LIB_VARIANT=_w timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_blocks.py tests/test_gpu_bench_shape.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r05r_pytest_w.log 2>&1" \
+  "for v in '' _w; do for s in '1 1 1024 256 95744 20 --rowsum' '1 1 256 256 95744 20 --rowsum' '0 1 95744 256 1024 20 --bw' '0 0 95744 1024 256 20 --bw' '0 0 95744 1024 256 20'; do ESP_LIB_VARIANT=\$v timeout -k 10 60 python -u tools/gemm_one.py \$s >> $T 2>&1 || exit 1; echo \"  [\$v] \$s\" >> $T; done; done" \
+  "timeout -k 10 400 python -u bench.py --no-cpu-baseline --feed-steps 0 > gpurun_out/r05r_bench.log 2>&1" \
+  "ESP_LIB_VARIANT=_w timeout -k 10 400 python -u bench.py --no-cpu-baseline --feed-steps 0 > gpurun_out/r05r_bench_w.log 2>&1"
