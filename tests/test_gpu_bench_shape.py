@@ -88,23 +88,27 @@ def test_bench_shape_graph_replay_matches_eager(dev):
     assert torch.allclose(fe, fg, rtol=0, atol=1e-6)
 
 
-def test_bench_shape_b256_step_vs_oracle(dev):
-    """B=256 (bench.py's default batch since round 4) gated against the oracle fixture itself, with
+@pytest.mark.parametrize("copies", [2, 3])
+def test_bench_shape_b256_step_vs_oracle(dev, copies):
+    """B=256 (bench.py's default batch) and B=384 (+1-2 %, the largest that fits with the HIP graph,
+    profiles/r05v_batch_sweep.txt) gated against the oracle fixture itself, with
     the same gates as the B=128 step above: the batch is the fixture's 128 utterances twice over, and
     with utterance-mean losses (ctc.py reduction sum / B, label_smoothing_loss.py:63 normalize by
     batch) and BatchNorm statistics of a duplicated batch equal to the original's, the exact loss and
     gradients of that batch ARE the fixture's fp64 values.  The ReLU decisions within rounding of 0
     (flipfix.py) are read from both copies (FlipProbe(copies=2): each copy carries half of a site's
-    contribution).  This is the bench's own shape: the conv1 output holds 1.91e9 elements (int32
-    index range) and every grid, split-K count and persistent-grid wrap is the bench's."""
+    contribution).  This is the bench's own shape: the conv1 output holds 1.91e9 (B=256) / 2.87e9 (B=384:
+    past the int32 range) elements and every grid, split-K count and persistent-grid wrap is the bench's
+    (three copies: the same argument with each copy carrying a third)."""
     g = golden("bench_c2_b128")
     cfg = _cfg()
     model = build_model(cfg, dev)
     load_seeded(model, cfg, int(g["seed"]))
     model.train()
     speech, slen, text, tlen = _batch(g, dev)
-    with FlipProbe(model, copies=2) as fp:
-        loss, stats, _ = model(speech.repeat(2, 1, 1), slen.repeat(2), text.clone().repeat(2, 1), tlen.repeat(2))
+    with FlipProbe(model, copies=copies) as fp:
+        loss, stats, _ = model(speech.repeat(copies, 1, 1), slen.repeat(copies), text.clone().repeat(copies, 1),
+                               tlen.repeat(copies))
     loss.backward()
     torch.cuda.synchronize()
     assert torch.isfinite(loss).item()
