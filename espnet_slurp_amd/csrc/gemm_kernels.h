@@ -2382,7 +2382,7 @@ bool glds_switch(int ma, int mb, int bnt, int prec, int bm, F&& f) {
         else return false;
       } else if constexpr ((small_ok || (MA_ == I2C_KC && MB_ == KC) || (MA_ == I2CT_KC && MB_ == RC) ||
                             (MA_ == RC && MB_ == I2C_RC)) &&
-                           decltype(R)::value == BM) {
+                           (decltype(R)::value == BM || (ESP_GEMM_WIDE && decltype(R)::value == 256))) {
         // bf16 operands: KC / RC pairs, and the conv2 forward / input gradient (implicit-im2col A of
         // bf16 pairs: the gathers run in pair units, C % 64 == 0) / weight gradient (gathered bf16 B)
         f(A, B, N, IC<2>{}, R);
@@ -2398,9 +2398,9 @@ bool glds_switch(int ma, int mb, int bnt, int prec, int bm, F&& f) {
       return false;
     }
 #if ESP_GEMM_WIDE
-    if (bm == 256) {  // 256 x 128 tiles, 8 waves: fp32 operands (PREC 0 / 1) and B planes (PREC 3)
+    if (bm == 256) {  // 256 x 128 tiles, 8 waves: fp32 operands (PREC 0 / 1), B planes (PREC 3), bf16 (PREC 2)
       if constexpr (MA_ != RC || MB_ != I2C_RC) {
-        if (bnt == 128 && (prec == 0 || prec == 1 || prec == 3)) return by_prec(IC<128>{}, IC<256>{});
+        if (bnt == 128 && prec != 5) return by_prec(IC<128>{}, IC<256>{});
       }
       return false;
     }
