@@ -1096,6 +1096,11 @@ _DBD_BUFS = {}
 _DBD_MAX_SHAPES = 4
 
 
+def release_relpos_band_buffers():
+    """Drop the kept dbd buffers (tests; a process that changes its batch shapes for good)."""
+    _DBD_BUFS.clear()
+
+
 def relpos_band_buffer(Z, T, Pp, device):
     key = (str(device), Z, T, Pp)
     buf = _DBD_BUFS.get(key)
