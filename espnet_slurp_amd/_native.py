@@ -53,9 +53,11 @@ SIGNATURES = {
     "esp_specaug": [P, P, I, I, I, P, P, P, I, P, I, P],
     "esp_utterance_mvn": [P, I, I, I, P, P],
     "esp_grad_norm": [P, L, F, P, L, P, P],
-    "esp_adam": [P, P, P, P, L, P, F, F, F, F, F, I, P],
-    "esp_opt_hyper": [P, ctypes.c_double, ctypes.c_double, F, F, P, P],
-    "esp_adam_dev": [P, P, P, P, L, P, P, F, F, F, F, P],
+    "esp_adam": [P, P, P, P, L, P, F, ctypes.c_double, ctypes.c_double, F, F, I, P],
+    "esp_opt_hyper": [P, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, P, P],
+    "esp_adam_dev": [P, P, P, P, L, P, P, ctypes.c_double, ctypes.c_double, F, F, P],
+    "esp_adam_amsgrad": [P, P, P, P, P, L, P, F, ctypes.c_double, ctypes.c_double, F, F, I, P],
+    "esp_adam_dev_amsgrad": [P, P, P, P, P, L, P, P, ctypes.c_double, ctypes.c_double, F, F, P],
     "esp_opt_advance": [P, P, P],
     "esp_set_rng_key": [P],
     "esp_rng_advance": [P, P],
@@ -122,7 +124,7 @@ _RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I, "esp_set_g
              "esp_get_gemm_compute": I, "esp_set_splitk_mode": I,
              "esp_f32_gemm_products": I}
 _RESTYPES.update({k: L for k in SIGNATURES if k.endswith("_workspace_bytes")})
-ABI_VERSION = 29  # bumped whenever a signature in include/espnet_mi355.h changes
+ABI_VERSION = 30  # bumped whenever a signature in include/espnet_mi355.h changes
 
 _lib = None
 

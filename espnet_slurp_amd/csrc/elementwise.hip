@@ -20,7 +20,7 @@ void set_error(const char* fmt, ...) {
 }  // namespace esp
 
 ESP_API const char* esp_last_error(void) { return esp::g_err; }
-ESP_API int esp_abi_version(void) { return 29; }
+ESP_API int esp_abi_version(void) { return 30; }
 ESP_API int esp_set_rng_key(const unsigned long long* key) {
   esp::g_rng_key = (const uint64_t*)key;
   return 0;
@@ -332,13 +332,15 @@ __global__ void norm_finalize_kernel(const double* __restrict__ part, int nb, fl
   }
 }
 
-// torch.optim.Adam (non-amsgrad, L2 weight_decay added to the gradient), step `t`
-// (1-based), applied to the flat buffers; grad is first multiplied by the clip coefficient.
-// Skips entirely when the finite flag is 0 (trainer.py:651-667).
+// torch.optim.Adam (L2 weight_decay added to the gradient), step `t` (1-based), applied to the flat
+// buffers; grad is first multiplied by the clip coefficient.  Skips entirely when the finite flag is 0
+// (trainer.py:651-667).  AMS (amsgrad=True): the denominator takes the running maximum of exp_avg_sq,
+// kept in vmax (torch: max_exp_avg_sqs = maximum(max_exp_avg_sqs, exp_avg_sq)).
+template <bool AMS>
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                            float* __restrict__ v, long n, const float* __restrict__ clip, float lr,
-                            float b1, float b2, float eps, float wd, float bc1, float bc2_sqrt,
-                            const float* __restrict__ hyper) {
+                            float* __restrict__ v, float* __restrict__ vmax, long n, const float* __restrict__ clip,
+                            float lr, float omb1, float b2, float omb2, float eps, float wd, float bc1,
+                            float bc2_sqrt, const float* __restrict__ hyper) {
   if (clip[2] == 0.f) return;
   if (hyper) {  // device-resident step hyper-parameters (HIP-graph replay): {lr, bc1, sqrt(bc2)}
     lr = hyper[0];
@@ -351,11 +353,16 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
     const float pi = p[i];
     if (wd != 0.f) gi += wd * pi;
     const float m0 = m[i];
-    const float mi = m0 + (1.f - b1) * (gi - m0);  // torch: exp_avg.lerp_(grad, 1-beta1)
-    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    const float mi = m0 + omb1 * (gi - m0);  // torch: exp_avg.lerp_(grad, 1-beta1)
+    const float vi = b2 * v[i] + omb2 * gi * gi;  // exp_avg_sq.mul_(beta2).addcmul_(grad, grad, 1-beta2)
     m[i] = mi;
     v[i] = vi;
-    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    float vd = vi;
+    if constexpr (AMS) {
+      vd = fmaxf(vmax[i], vi);
+      vmax[i] = vd;
+    }
+    const float denom = sqrtf(vd) / bc2_sqrt + eps;
     p[i] = pi - (lr / bc1) * (mi / denom);
   }
 }
@@ -460,28 +467,39 @@ ESP_API int esp_grad_norm(const float* g, long n, float max_norm, double* work, 
   return 0;
 }
 
-ESP_API int esp_adam(float* p, const float* g, float* m, float* v, long n, const float* clip, float lr, float b1,
-                     float b2, float eps, float wd, int step, void* stream) {
+ESP_API int esp_adam(float* p, const float* g, float* m, float* v, long n, const float* clip, float lr, double b1,
+                     double b2, float eps, float wd, int step, void* stream) {
   ESP_ARG_CHECK(step >= 1, "esp_adam: step must be >= 1");
-  const float bc1 = (float)(1.0 - pow((double)b1, (double)step));  // python-float math, as torch
-  const float bc2 = (float)(1.0 - pow((double)b2, (double)step));
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, clip, lr,
-                     b1, b2, eps, wd, bc1, sqrtf(bc2), nullptr);
+  const float bc1 = (float)(1.0 - pow(b1, (double)step));  // python-float math, as torch
+  const float bc2s = (float)sqrt(1.0 - pow(b2, (double)step));  // torch: (1 - beta2 ** step) ** 0.5
+  hipLaunchKernelGGL(adam_kernel<false>, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, nullptr,
+                     n, clip, lr, (float)(1.0 - b1), (float)b2, (float)(1.0 - b2), eps, wd, bc1, bc2s, nullptr);
   ESP_CHECK_LAUNCH("esp_adam");
+  return 0;
+}
+
+ESP_API int esp_adam_amsgrad(float* p, const float* g, float* m, float* v, float* vmax, long n, const float* clip,
+                             float lr, double b1, double b2, float eps, float wd, int step, void* stream) {
+  ESP_ARG_CHECK(step >= 1 && vmax, "esp_adam_amsgrad: step must be >= 1 and vmax non-NULL");
+  const float bc1 = (float)(1.0 - pow(b1, (double)step));
+  const float bc2s = (float)sqrt(1.0 - pow(b2, (double)step));  // torch: (1 - beta2 ** step) ** 0.5
+  hipLaunchKernelGGL(adam_kernel<true>, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, vmax, n,
+                     clip, lr, (float)(1.0 - b1), (float)b2, (float)(1.0 - b2), eps, wd, bc1, bc2s, nullptr);
+  ESP_CHECK_LAUNCH("esp_adam_amsgrad");
   return 0;
 }
 
 // ---- device-resident optimizer bookkeeping, so a whole training step can be one HIP graph.
 // state[0] = Adam steps applied so far, state[1] = WarmupLR steps taken (scheduler.last_epoch).
 namespace {
-__global__ void opt_hyper_kernel(const double* __restrict__ state, double base_lr, double warmup, float b1, float b2,
+__global__ void opt_hyper_kernel(const double* __restrict__ state, double base_lr, double warmup, double b1, double b2,
                                  float* __restrict__ hyper) {
   const double t = state[0] + 1.0, s = state[1] + 1.0;
   double lr = base_lr;
   if (warmup > 0.0) lr = base_lr * sqrt(warmup) * fmin(1.0 / sqrt(s), s * pow(warmup, -1.5));
   hyper[0] = (float)lr;
-  hyper[1] = (float)(1.0 - pow((double)b1, t));
-  hyper[2] = sqrtf((float)(1.0 - pow((double)b2, t)));
+  hyper[1] = (float)(1.0 - pow(b1, t));
+  hyper[2] = (float)sqrt(1.0 - pow(b2, t));  // torch: bias_correction2_sqrt = (1 - beta2 ** step) ** 0.5
 }
 __global__ void opt_advance_kernel(double* __restrict__ state, const float* __restrict__ clip) {
   if (clip[2] != 0.f) {
@@ -497,7 +515,7 @@ __global__ void rng_advance_kernel(unsigned long long* __restrict__ key) {
 }
 }  // namespace
 
-ESP_API int esp_opt_hyper(const double* state, double base_lr, double warmup, float b1, float b2, float* hyper,
+ESP_API int esp_opt_hyper(const double* state, double base_lr, double warmup, double b1, double b2, float* hyper,
                           void* stream) {
   hipLaunchKernelGGL(opt_hyper_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, state, base_lr, warmup, b1, b2, hyper);
   ESP_CHECK_LAUNCH("esp_opt_hyper");
@@ -505,10 +523,19 @@ ESP_API int esp_opt_hyper(const double* state, double base_lr, double warmup, fl
 }
 
 ESP_API int esp_adam_dev(float* p, const float* g, float* m, float* v, long n, const float* clip, const float* hyper,
-                         float b1, float b2, float eps, float wd, void* stream) {
-  hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, n, clip, 0.f, b1,
-                     b2, eps, wd, 1.f, 1.f, hyper);
+                         double b1, double b2, float eps, float wd, void* stream) {
+  hipLaunchKernelGGL(adam_kernel<false>, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, nullptr,
+                     n, clip, 0.f, (float)(1.0 - b1), (float)b2, (float)(1.0 - b2), eps, wd, 1.f, 1.f, hyper);
   ESP_CHECK_LAUNCH("esp_adam_dev");
+  return 0;
+}
+
+ESP_API int esp_adam_dev_amsgrad(float* p, const float* g, float* m, float* v, float* vmax, long n, const float* clip,
+                                 const float* hyper, double b1, double b2, float eps, float wd, void* stream) {
+  ESP_ARG_CHECK(vmax != nullptr, "esp_adam_dev_amsgrad: vmax is NULL");
+  hipLaunchKernelGGL(adam_kernel<true>, dim3(grid_for(n, 4)), dim3(256), 0, (hipStream_t)stream, p, g, m, v, vmax, n,
+                     clip, 0.f, (float)(1.0 - b1), (float)b2, (float)(1.0 - b2), eps, wd, 1.f, 1.f, hyper);
+  ESP_CHECK_LAUNCH("esp_adam_dev_amsgrad");
   return 0;
 }
 

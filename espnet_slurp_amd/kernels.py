@@ -810,6 +810,16 @@ def adam(p, g, m, v, clip3, lr, b1, b2, eps, wd, step):
                  float(eps), float(wd), int(step), _st())
 
 
+def adam_amsgrad(p, g, m, v, vmax, clip3, lr, b1, b2, eps, wd, step):
+    _native.call("esp_adam_amsgrad", _p(p), _p(g), _p(m), _p(v), _p(vmax), p.numel(), _p(clip3), float(lr), float(b1),
+                 float(b2), float(eps), float(wd), int(step), _st())
+
+
+def adam_dev_amsgrad(p, g, m, v, vmax, clip3, hyper3, b1, b2, eps, wd):
+    _native.call("esp_adam_dev_amsgrad", _p(p), _p(g), _p(m), _p(v), _p(vmax), p.numel(), _p(clip3), _p(hyper3),
+                 float(b1), float(b2), float(eps), float(wd), _st())
+
+
 def opt_hyper(state_f64, base_lr, warmup, b1, b2, hyper3):
     _native.call("esp_opt_hyper", _p(state_f64), float(base_lr), float(warmup), float(b1), float(b2), _p(hyper3),
                  _st())

@@ -21,27 +21,71 @@ def clip_grad_norm_(flat: FlatParams, max_norm: float, out: torch.Tensor = None)
 
 
 class FusedAdam(torch.optim.Optimizer):
+    """torch.optim.Adam over the flat parameter buffer.  One param group (the espnet2 default,
+    abs_task.py:856-880 builds Adam(model.parameters(), **optim_conf)) is one launch over the whole
+    buffer; several groups (each its own lr / betas / eps / weight_decay / amsgrad, as torch) are one
+    launch per run of a group's parameters that lie next to each other in the flat buffer.
+    amsgrad=True keeps max_exp_avg_sq in a third flat buffer."""
+
     def __init__(self, params, flat: FlatParams, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.0, amsgrad: bool = False):
-        if amsgrad:
-            raise NotImplementedError("amsgrad")
-        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
-        if len(self.param_groups) != 1:
-            raise NotImplementedError("FusedAdam: one param group (the espnet2 default)")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=amsgrad))
         self.flat = flat
         self.exp_avg = torch.zeros_like(flat.flat)
         self.exp_avg_sq = torch.zeros_like(flat.flat)
+        self.max_exp_avg_sq = (torch.zeros_like(flat.flat) if any(g["amsgrad"] for g in self.param_groups)
+                               else None)
         self.n_steps = 0
         self._ones = torch.tensor([1.0, 1.0, 1.0], device=flat.flat.device)
+        self._ranges = self.group_ranges()
+
+    def group_ranges(self):
+        """Per param group, the (offset, length) runs of the flat buffer its launches cover: the whole
+        buffer for a single group holding every flat parameter, else the group's parameters in flat
+        order, merged while no parameter of another group lies between them (alignment padding inside
+        a run holds zeros, which Adam leaves at zero)."""
+        slots = self.flat.slots
+        for g in self.param_groups:
+            for p in g["params"]:
+                if id(p) not in slots:
+                    raise ValueError("FusedAdam: a parameter outside the flat buffer")
+        if len(self.param_groups) == 1 and len(self.param_groups[0]["params"]) == len(slots):
+            return [[(0, self.flat.flat.numel())]]
+        owner = {id(p): gi for gi, g in enumerate(self.param_groups) for p in g["params"]}
+        order = sorted(slots.items(), key=lambda kv: kv[1][0])  # every flat parameter, by offset
+        out = [[] for _ in self.param_groups]
+        prev = None  # (group, run start) of the run being extended
+        for pid, (o, k) in order:
+            gi = owner.get(pid)
+            if gi is None:
+                prev = None
+                continue
+            if prev is not None and prev[0] == gi:
+                start = out[gi][-1][0]
+                out[gi][-1] = (start, o + k - start)
+            else:
+                out[gi].append((o, k))
+            prev = (gi, o)
+        return out
+
+    def _bufs(self, o, k):
+        f = self.flat
+        vm = self.max_exp_avg_sq[o:o + k] if self.max_exp_avg_sq is not None else None
+        return f.flat[o:o + k], f.grad[o:o + k], self.exp_avg[o:o + k], self.exp_avg_sq[o:o + k], vm
 
     @torch.no_grad()
     def step(self, closure=None, clip: torch.Tensor = None):
         """clip: the 3-vector of clip_grad_norm_ (coefficient + finite flag); None = no clipping."""
-        g = self.param_groups[0]
         self.n_steps += 1
-        b1, b2 = g["betas"]
-        K.adam(self.flat.flat, self.flat.grad, self.exp_avg, self.exp_avg_sq, clip if clip is not None else self._ones,
-               g["lr"], b1, b2, g["eps"], g["weight_decay"], self.n_steps)
+        c = clip if clip is not None else self._ones
+        for g, runs in zip(self.param_groups, self._ranges):
+            b1, b2 = g["betas"]
+            for o, k in runs:
+                p, gr, m, v, vm = self._bufs(o, k)
+                if g["amsgrad"]:
+                    K.adam_amsgrad(p, gr, m, v, vm, c, g["lr"], b1, b2, g["eps"], g["weight_decay"], self.n_steps)
+                else:
+                    K.adam(p, gr, m, v, c, g["lr"], b1, b2, g["eps"], g["weight_decay"], self.n_steps)
         return None
 
     # ---------------------------------------------------------- device-resident bookkeeping
@@ -53,20 +97,27 @@ class FusedAdam(torch.optim.Optimizer):
             last = float(scheduler.last_epoch) if scheduler is not None else 0.0
             self._dstate = torch.tensor([float(self.n_steps), last], dtype=torch.float64, device=dev)
             self._hyper = torch.empty(3, dtype=torch.float32, device=dev)
+            self._hyper_g = [self._hyper] + [torch.empty(3, dtype=torch.float32, device=dev)
+                                             for _ in self.param_groups[1:]]
         return self._dstate
 
     def step_device(self, clip: torch.Tensor, scheduler=None):
         """Adam step whose lr / bias corrections come from the device state (WarmupLR formula
         on device): capturable in a HIP graph.  Counts the step (and the scheduler step) on
         device only when the gradient norm was finite."""
-        g = self.param_groups[0]
-        b1, b2 = g["betas"]
         st = self.device_state(scheduler)
         warmup = float(getattr(scheduler, "warmup_steps", 0.0) or 0.0)
-        base = scheduler.base_lrs[0] if scheduler is not None else g["lr"]
-        K.opt_hyper(st, base, warmup, b1, b2, self._hyper)
-        K.adam_dev(self.flat.flat, self.flat.grad, self.exp_avg, self.exp_avg_sq, clip, self._hyper, b1, b2, g["eps"],
-                   g["weight_decay"])
+        for gi, (g, runs) in enumerate(zip(self.param_groups, self._ranges)):
+            b1, b2 = g["betas"]
+            base = scheduler.base_lrs[gi] if scheduler is not None else g["lr"]
+            hyper = self._hyper if gi == 0 else self._hyper_g[gi]
+            K.opt_hyper(st, base, warmup, b1, b2, hyper)
+            for o, k in runs:
+                p, gr, m, v, vm = self._bufs(o, k)
+                if g["amsgrad"]:
+                    K.adam_dev_amsgrad(p, gr, m, v, vm, clip, hyper, b1, b2, g["eps"], g["weight_decay"])
+                else:
+                    K.adam_dev(p, gr, m, v, clip, hyper, b1, b2, g["eps"], g["weight_decay"])
         K.opt_advance(st, clip)
 
     def sync_from_device(self, scheduler=None):
@@ -84,56 +135,69 @@ class FusedAdam(torch.optim.Optimizer):
         self.flat.zero_grad()
 
     # ---------------------------------------------------------- checkpoint interop
-    def _adam_group(self) -> dict:
-        """param_groups[0] as torch.optim.Adam would hold it (every Adam default key of this
-        torch version, with this optimizer's hyper-parameters)."""
-        g = self.param_groups[0]
+    @staticmethod
+    def _adam_group(g) -> dict:
+        """A param group as torch.optim.Adam would hold it (every Adam default key of this torch
+        version, with the group's hyper-parameters)."""
         ref = torch.optim.Adam([torch.nn.Parameter(torch.zeros(1))], lr=g["lr"], betas=g["betas"], eps=g["eps"],
-                               weight_decay=g["weight_decay"])
+                               weight_decay=g["weight_decay"], amsgrad=g["amsgrad"])
         return dict(ref.param_groups[0])
 
     def state_dict(self):
         """torch.optim.Adam.state_dict() format — what the reference's checkpoint.pth holds under
-        "optimizers" (trainer.py:340-352, abs_task.py:78-79): per parameter (keyed by its index
-        in param_groups[0]["params"]) {"step": float32 scalar, "exp_avg", "exp_avg_sq"} with the
-        parameter's shape, copied out of the flat moment buffers.  Graph mode keeps the step
-        count on device: it is read from there.  The group's lr is the host value — call
-        Trainer.sync_host_state() first (train_one_epoch does)."""
-        g = self.param_groups[0]
+        "optimizers" (trainer.py:340-352, abs_task.py:78-79): per parameter (keyed by its index,
+        numbered across the param groups in order) {"step": float32 scalar, "exp_avg", "exp_avg_sq"
+        (+ "max_exp_avg_sq" in an amsgrad group)} with the parameter's shape, copied out of the flat
+        moment buffers.  Graph mode keeps the step count on device: it is read from there.  The
+        groups' lr are the host values — call Trainer.sync_host_state() first (train_one_epoch does)."""
         n = int(self._dstate[0].item()) if getattr(self, "_dstate", None) is not None else self.n_steps
-        state = {}
-        if n > 0:
-            for i, p in enumerate(g["params"]):
-                o, k = self.flat.slots[id(p)]
-                state[i] = {"step": torch.tensor(float(n), dtype=torch.float32),
-                            "exp_avg": self.exp_avg[o:o + k].view(p.shape).clone(),
-                            "exp_avg_sq": self.exp_avg_sq[o:o + k].view(p.shape).clone()}
-        group = self._adam_group()
-        group["params"] = list(range(len(g["params"])))
-        if "initial_lr" in g:  # added by the LR scheduler (torch _LRScheduler.__init__)
-            group["initial_lr"] = g["initial_lr"]
-        return {"state": state, "param_groups": [group]}
+        state, groups, idx = {}, [], 0
+        for g in self.param_groups:
+            ids = []
+            for p in g["params"]:
+                if n > 0:
+                    o, k = self.flat.slots[id(p)]
+                    st = {"step": torch.tensor(float(n), dtype=torch.float32),
+                          "exp_avg": self.exp_avg[o:o + k].view(p.shape).clone(),
+                          "exp_avg_sq": self.exp_avg_sq[o:o + k].view(p.shape).clone()}
+                    if g["amsgrad"]:
+                        st["max_exp_avg_sq"] = self.max_exp_avg_sq[o:o + k].view(p.shape).clone()
+                    state[idx] = st
+                ids.append(idx)
+                idx += 1
+            group = self._adam_group(g)
+            group["params"] = ids
+            if "initial_lr" in g:  # added by the LR scheduler (torch _LRScheduler.__init__)
+                group["initial_lr"] = g["initial_lr"]
+            groups.append(group)
+        return {"state": state, "param_groups": groups}
 
     @torch.no_grad()
     def load_state_dict(self, state_dict):
         """Load a torch.optim.Adam state_dict (the reference's checkpoint, or ours): the moments
         are copied into the flat buffers in place (a captured HIP graph keeps pointing at them),
-        the step count into the host and device counters.  FusedAdam keeps ONE step count: a
-        checkpoint whose parameters have different Adam step counts is refused."""
+        the step count into the host and device counters.  The groups must match this optimizer's
+        in number and size (torch's rule); a group's amsgrad setting is taken from the checkpoint.
+        FusedAdam keeps ONE step count: a checkpoint whose parameters have different Adam step
+        counts is refused."""
         saved_groups = state_dict["param_groups"]
-        g = self.param_groups[0]
-        if len(saved_groups) != 1 or len(saved_groups[0]["params"]) != len(g["params"]):
+        if len(saved_groups) != len(self.param_groups) or any(
+                len(sg["params"]) != len(g["params"]) for sg, g in zip(saved_groups, self.param_groups)):
             raise ValueError("loaded state dict has a different number of parameter groups / parameters")
-        sg = saved_groups[0]
-        if sg.get("amsgrad", False):
-            raise NotImplementedError("amsgrad")
-        for key in ("lr", "betas", "eps", "weight_decay"):
-            g[key] = tuple(sg[key]) if key == "betas" else sg[key]
-        if "initial_lr" in sg:  # set by the LR scheduler at construction
-            g["initial_lr"] = sg["initial_lr"]
-        index = dict(zip(sg["params"], g["params"]))
+        index = {}
+        for sg, g in zip(saved_groups, self.param_groups):
+            for key in ("lr", "betas", "eps", "weight_decay"):
+                g[key] = tuple(sg[key]) if key == "betas" else sg[key]
+            g["amsgrad"] = bool(sg.get("amsgrad", False))
+            if "initial_lr" in sg:  # set by the LR scheduler at construction
+                g["initial_lr"] = sg["initial_lr"]
+            index.update(zip(sg["params"], g["params"]))
+        if any(g["amsgrad"] for g in self.param_groups) and self.max_exp_avg_sq is None:
+            self.max_exp_avg_sq = torch.zeros_like(self.flat.flat)
         self.exp_avg.zero_()
         self.exp_avg_sq.zero_()
+        if self.max_exp_avg_sq is not None:
+            self.max_exp_avg_sq.zero_()
         steps = set()
         for i, st in state_dict["state"].items():
             p = index[int(i)]
@@ -142,6 +206,8 @@ class FusedAdam(torch.optim.Optimizer):
                 raise ValueError(f"state of parameter {i}: {tuple(st['exp_avg'].shape)} != {tuple(p.shape)}")
             self.exp_avg[o:o + k].copy_(st["exp_avg"].reshape(-1))
             self.exp_avg_sq[o:o + k].copy_(st["exp_avg_sq"].reshape(-1))
+            if "max_exp_avg_sq" in st:
+                self.max_exp_avg_sq[o:o + k].copy_(st["max_exp_avg_sq"].reshape(-1))
             steps.add(int(float(st["step"])))
         if len(steps) > 1:
             raise ValueError(f"parameters have different Adam step counts {sorted(steps)}")

@@ -177,17 +177,25 @@ int esp_utterance_mvn(float* x, int B, int T, int F, const int* lens, void* stre
 int esp_grad_norm(const float* g, long n, float max_norm, double* work, long work_bytes, float* out3,
                   void* stream);
 int esp_adam(float* p, const float* g, float* m, float* v, long n, const float* clip3, float lr,
-             float b1, float b2, float eps, float wd, int step, void* stream);
+             double b1, double b2, float eps, float wd, int step, void* stream);
 /* Device-resident optimizer bookkeeping (a whole training step as one HIP graph):
  * state (2 doubles) = {Adam steps applied, WarmupLR steps taken}.  esp_opt_hyper writes the
  * next step's {lr, 1-b1^t, sqrt(1-b2^t)} (warmuplr.py:43-50, torch Adam) to hyper (3 floats);
  * esp_adam_dev reads them; esp_opt_advance counts the step only if clip3[2] (finite) != 0,
  * which is exactly when trainer.py:651-686 steps the optimizer and the scheduler. */
-int esp_opt_hyper(const double* state, double base_lr, double warmup, float b1, float b2, float* hyper,
+int esp_opt_hyper(const double* state, double base_lr, double warmup, double b1, double b2, float* hyper,
                   void* stream);
 int esp_adam_dev(float* p, const float* g, float* m, float* v, long n, const float* clip3,
-                 const float* hyper, float b1, float b2, float eps, float wd, void* stream);
+                 const float* hyper, double b1, double b2, float eps, float wd, void* stream);
 int esp_opt_advance(double* state, const float* clip3, void* stream);
+/* ABI 30: torch.optim.Adam(amsgrad=True) (the optim_conf key abs_task.py:856-880 passes through): as
+ * esp_adam / esp_adam_dev, the denominator on vmax = max(vmax, exp_avg_sq), kept in place (n floats).
+ * ABI 30 also passes beta1 / beta2 of every Adam entry as double: 1 - beta and the bias corrections are
+ * formed in double as torch forms them from python floats (fp32 1 - 0.999f is 1.3e-5 off 0.001). */
+int esp_adam_amsgrad(float* p, const float* g, float* m, float* v, float* vmax, long n, const float* clip3,
+                     float lr, double b1, double b2, float eps, float wd, int step, void* stream);
+int esp_adam_dev_amsgrad(float* p, const float* g, float* m, float* v, float* vmax, long n, const float* clip3,
+                         const float* hyper, double b1, double b2, float eps, float wd, void* stream);
 /* Dropout key: every dropout kernel XORs its seed with *key when set (NULL: off).  The key
  * lives in device memory so a replayed HIP graph draws fresh masks; esp_rng_advance mixes it
  * (splitmix64) on device. */
