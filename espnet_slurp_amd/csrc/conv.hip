@@ -18,15 +18,20 @@ inline int gridn(long n) {
 // 9-tap patch load is a broadcast and the store is 1 KB contiguous per wave.
 // z16 != nullptr (the bf16 mode): the output's bf16 copy too (RNE), the A operand of the bf16 conv2
 // forward (esp_conv2_fwd_bf16); z stays fp32 for the weight gradient's gather and the ReLU mask
+#ifndef ESP_CONV1_NT
+#define ESP_CONV1_NT 1
+#endif
 template <bool B16>
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict__ x, const float* __restrict__ W,
                                                         const float* __restrict__ bias, float* __restrict__ z,
                                                         uint2* __restrict__ z16, int B, int T, int F, int T1, int F1,
-                                                        int D) {
-  const int D4 = D / 4;
-  const long tid = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  const long nthr = (long)gridDim.x * blockDim.x;  // multiple of D4 (host)
-  const int o4 = (int)(tid % D4);
+                                                        int D, unsigned chunk) {
+  // block b owns output pixels [b * chunk, (b + 1) * chunk); per step its 256 threads cover PS = 256 / (D/4)
+  // consecutive pixels x all D channels (PS KB of contiguous float4 stores).  The pixel's (b, t1, f1) is
+  // decomposed once and then advanced by PS (one row wrap per step at most when PS < F1) -- the per-pixel
+  // integer divisions of a grid-stride loop were ~half of the kernel's VALU
+  const int D4 = D / 4, PS = 256 / D4;
+  const int o4 = threadIdx.x % D4, tp = threadIdx.x / D4;
   float w[4][9], bb[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -35,12 +40,15 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict_
     for (int k = 0; k < 9; ++k) w[q][k] = W[(o4 * 4 + q) * 9 + k];
   }
   const unsigned npix = (unsigned)B * T1 * F1;  // < 2^32 (host check): 32-bit index math
-  for (unsigned p = (unsigned)(tid / D4); p < npix; p += (unsigned)(nthr / D4)) {
-    const unsigned r = p / (unsigned)F1;
-    const int f1 = (int)(p - r * (unsigned)F1);
-    const int b = (int)(r / (unsigned)T1);
-    const int t1 = (int)(r - (unsigned)b * T1);
-    const float* xp = x + ((long)b * T + 2 * t1) * F + 2 * f1;
+  const unsigned c0 = blockIdx.x * chunk, c1 = min(npix, c0 + chunk);
+  unsigned p = c0 + tp;
+  if (p >= c1) return;
+  const unsigned r0 = p / (unsigned)F1;
+  int f1 = (int)(p - r0 * (unsigned)F1);
+  int bi = (int)(r0 / (unsigned)T1);
+  int t1 = (int)(r0 - (unsigned)bi * T1);
+  for (; p < c1; p += PS) {
+    const float* xp = x + ((long)bi * T + 2 * t1) * F + 2 * f1;
     float patch[9];
 #pragma unroll
     for (int kt = 0; kt < 3; ++kt)
@@ -54,8 +62,22 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict_
       for (int k = 0; k < 9; ++k) a += w[q][k] * patch[k];
       out[q] = fmaxf(a, 0.f);
     }
+#if ESP_CONV1_NT  // non-temporal stores of the 7.7 GB map: 2109 -> 1453 us at C2 B=256 (profiles/r05ac_conv1_nt_ab.txt)
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v ov = {out[0], out[1], out[2], out[3]};
+    __builtin_nontemporal_store(ov, reinterpret_cast<f4v*>(z + (long)p * D + o4 * 4));
+#else
     *reinterpret_cast<float4*>(z + (long)p * D + o4 * 4) = make_float4(out[0], out[1], out[2], out[3]);
+#endif
     if constexpr (B16) z16[((long)p * D + o4 * 4) >> 2] = make_uint2(esp::bf16_pair(out[0], out[1]), esp::bf16_pair(out[2], out[3]));
+    f1 += PS;
+    while (f1 >= F1) {  // (once at most when PS < F1, the C2 / C5 shapes)
+      f1 -= F1;
+      if (++t1 == T1) {
+        t1 = 0;
+        ++bi;
+      }
+    }
   }
 }
 
@@ -208,14 +230,16 @@ static int conv1_fwd_impl(const float* x, const float* W, const float* bias, flo
   ESP_ARG_CHECK(256 % (D / 4) == 0, "esp_conv1_fwd: D/4 must divide 256");
   const long npix = (long)B * T1 * F1;
   ESP_ARG_CHECK(npix < (1L << 32), "esp_conv1_fwd: %ld output pixels (32-bit index math)", npix);
-  long nblk = (npix * (D / 4) + 255) / 256;
+  const long ps = 256 / (D / 4);
+  long nblk = (npix + ps - 1) / ps;
   if (nblk > 8192) nblk = 8192;  // ~16 pixels per thread at the C2 sizes: weights amortised
+  const unsigned chunk = (unsigned)((npix + nblk - 1) / nblk);
   if (z16)
     hipLaunchKernelGGL(conv1_fwd_kernel<true>, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, x, W, bias, z,
-                       (uint2*)z16, B, T, F, T1, F1, D);
+                       (uint2*)z16, B, T, F, T1, F1, D, chunk);
   else
     hipLaunchKernelGGL(conv1_fwd_kernel<false>, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, x, W, bias, z,
-                       nullptr, B, T, F, T1, F1, D);
+                       nullptr, B, T, F, T1, F1, D, chunk);
   ESP_CHECK_LAUNCH("esp_conv1_fwd");
   return 0;
 }
