@@ -982,10 +982,14 @@ def add2d(x, ldx, y, ldy, M, N, x_off=0, y_off=0):
     _native.call("esp_add2d", _p(x, x_off), ldx, _p(y, y_off), ldy, M, N, _st())
 
 
+# row pitch granularity of score-like buffers (floats)
+SCORE_ALIGN = 4
+
+
 def pitch(n: int) -> int:
-    """Row pitch of score-like buffers: a multiple of 4 floats, so every row is 16-B aligned
-    and the GEMMs reading them take the LDS-DMA path."""
-    return (n + 3) & ~3
+    """Row pitch of score-like buffers: a multiple of SCORE_ALIGN (>= 4) floats, so every row is 16-B
+    aligned and the GEMMs reading them take the LDS-DMA path."""
+    return (n + SCORE_ALIGN - 1) // SCORE_ALIGN * SCORE_ALIGN
 
 
 def attn_softmax_fwd(ac, bd, relpos, P, sqrt_dk, klen_i32, nb, causal, attn, pdrop, drop_p, seed, Z, Tq, Tk,
