@@ -213,9 +213,9 @@ class RelPositionMultiHeadedAttention(nn.Module):
         pa = self.p if training else 0.0
         sa = seeds.next()
         tv = tvalid if self.legacy else None
-        if tv is not None and (K.flash_ok(T, dk) or K.ATTN_DSCORES):
-            raise NotImplementedError("legacy rel_pos with length buckets: not with ESP_FLASH_ATTN / ESP_ATTN_DSCORES")
-        if K.flash_ok(T, dk):
+        # a legacy length-bucketed batch (rel_shift at T' = *tvalid) takes the materialised kernels, which read
+        # T' on device; the opt-in flash / score-gradient forms stay for every other batch
+        if K.flash_ok(T, dk) and tv is None:
             # scores, softmax, dropout and P.V in one kernel: only ctx and 2 floats per row to HBM
             ctx_ = empty(M, D, like=x2d)
             stats = empty(Z * T * 2, like=x2d)
@@ -280,7 +280,7 @@ class RelPositionMultiHeadedAttention(nn.Module):
         # the fused dP + softmax/rel_shift adjoint kernel measures slower than the K=64 GEMM + the
         # row-wise adjoint pass at C2 (198 vs 157 us per layer): opt-in until it is reworked
         fused = not self.legacy and K.relpos_fused_ok(T, dk) and K.FUSED_ATTN_BWD
-        dscores = not fused and K.ATTN_DSCORES
+        dscores = not fused and K.ATTN_DSCORES and c.tvalid is None  # (legacy + length bucket: the row-wise pass)
         # latest rel_shift, row-wise adjoint: dbd in the kept zeroed buffer, only its band written
         band = None if (self.legacy or fused or dscores or Tp % 4) else K.relpos_band_buffer(Z, T, Pp, dout.device)
         dbd = band if band is not None else empty(Z * T * Pp, like=dout)
