@@ -671,6 +671,12 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
         mode_b != I2C_RC && (mode_a != KC || 256L * g.a.ld * 4 < (1L << 32)) &&
         (mode_a != I2C_KC || (long)g.a.ic.Ho * g.a.ic.Wo >= 256))
       g.bm = 256;
+#elif ESP_GEMM_WIDE_KCRC
+    // the KC x RC GEMMs on B planes (linear input gradients, P0 / FFN w_2 shapes): 256 x 128 tiles of 8 waves
+    // on a 2-slab ring, 3-7 % faster per kernel at C2 B=256 (the other pairs measured slower, r05am)
+    if (g.bnt == 128 && g.bm == BM && g.bf16 == 3 && mode_a == KC && mode_b == RC && !smb && M >= 256 &&
+        256L * g.a.ld * 4 < (1L << 32))
+      g.bm = 256;
 #endif
   }
   {

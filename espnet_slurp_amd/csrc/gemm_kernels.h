@@ -1247,6 +1247,11 @@ constexpr int GL_BK = 32;
 #ifndef ESP_GEMM_WIDE
 #define ESP_GEMM_WIDE 0
 #endif
+// 256 x 128 tiles of 8 waves for the KC x RC GEMMs on B planes only (the pairs they speed up: the linear
+// input gradients / P0 / FFN w_2 shapes 3-7 %, profiles/r05am_*)
+#ifndef ESP_GEMM_WIDE_KCRC
+#define ESP_GEMM_WIDE_KCRC 1
+#endif
 #ifndef ESP_GEMM_STAGES
 #define ESP_GEMM_STAGES 2
 #endif
@@ -2397,14 +2402,13 @@ bool glds_switch(int ma, int mb, int bnt, int prec, int bm, F&& f) {
       }
       return false;
     }
-#if ESP_GEMM_WIDE
-    if (bm == 256) {  // 256 x 128 tiles, 8 waves: fp32 operands (PREC 0 / 1), B planes (PREC 3), bf16 (PREC 2)
-      if constexpr (MA_ != RC || MB_ != I2C_RC) {
-        if (bnt == 128 && prec != 5) return by_prec(IC<128>{}, IC<256>{});
+    if (bm == 256) {  // 256 x 128 tiles, 8 waves: KC x RC on B planes (default build, ESP_GEMM_WIDE_KCRC); every
+                      // fp32 / B-planes / bf16-operand pair in an ESP_GEMM_WIDE build
+      if constexpr ((ESP_GEMM_WIDE && (MA_ != RC || MB_ != I2C_RC)) || (ESP_GEMM_WIDE_KCRC && MA_ == KC && MB_ == RC)) {
+        if (bnt == 128 && (ESP_GEMM_WIDE ? prec != 5 : prec == 3)) return by_prec(IC<128>{}, IC<256>{});
       }
       return false;
     }
-#endif
     return bnt == 64 ? by_prec(IC<64>{}, IC<BM>{}) : by_prec(IC<128>{}, IC<BM>{});
   };
   switch (ma * 8 + mb) {
