@@ -1256,6 +1256,11 @@ __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
     read_frag_pl(ppl[pslot(-1 - wave)], PLB, li, q4, pf);
     put_band(ring0, 0, mfma_pl(xv, pf, f32x4{0.f, 0.f, 0.f, 0.f}));
   }
+  // wave 3 read block -4 here, whose slot (pslot(-4) == pslot(1)) step 0 refills with block 1: every
+  // wave's prologue read completes before any wave's step-0 ring write (without this barrier a wave
+  // that ran ahead could overwrite it while wave 3 still read it -- rare, order-dependent bd errors on
+  // the block's last 16 rows at key tile 0)
+  __syncthreads();
 
   f32x4 sc[NTA];
   // key tiles / band blocks PF steps ahead in registers (slot s % PF holds step s's): a step's loads
