@@ -106,6 +106,7 @@ SIGNATURES = {
     "esp_reduce_losses": [P, I, I, P, P, I, F, F, P, P],
     "esp_argmax": [P, P, L, I, P],
     "esp_ctc_forced_align": [P, I, I, P, I, I, P, P, P],
+    "esp_ctc_forced_align_batch": [P, I, I, I, P, P, I, P, I, P, P, P],
     "esp_ctc_prefix_init": [P, I, I, I, P, P],
     "esp_ctc_prefix_score": [P, I, I, P, P, I, P, I, I, I, I, P, P, P],
     # workspace-size queries (host arithmetic; return bytes)
@@ -124,7 +125,7 @@ _RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I, "esp_set_g
              "esp_get_gemm_compute": I, "esp_set_splitk_mode": I,
              "esp_f32_gemm_products": I}
 _RESTYPES.update({k: L for k in SIGNATURES if k.endswith("_workspace_bytes")})
-ABI_VERSION = 30  # bumped whenever a signature in include/espnet_mi355.h changes
+ABI_VERSION = 31  # bumped whenever a signature in include/espnet_mi355.h changes
 
 _lib = None
 

@@ -80,3 +80,9 @@ class CTC(nn.Module):
         """espnet1 CTC.forced_align semantics (espnet/nets/pytorch_backend/ctc.py:185-249)."""
         lpz = self.log_softmax(h if h.dim() == 3 else h[None])[0].contiguous()
         return K.ctc_forced_align(lpz, y.to(lpz.device).long().contiguous(), blank_id)
+
+    def forced_align_batch(self, hs_pad, hlens, ys_pad, ys_lens, blank_id=0):
+        """forced_align of every utterance of a padded batch in one launch (each row as the per-utterance
+        call on hs_pad[b, :hlens[b]] and ys_pad[b, :ys_lens[b]]); (B, T) int64, -1 past hlens[b]."""
+        lpz = self.log_softmax(hs_pad)
+        return K.ctc_forced_align_batch(lpz, hlens, ys_pad, ys_lens, blank_id)

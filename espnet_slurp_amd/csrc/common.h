@@ -101,7 +101,10 @@ __device__ __forceinline__ float fast_sigmoid(float v) {
 // ---------------------------------------------------------------- fp32 -> bf16 split planes
 // v = hi + mid + lo exactly (finite v): hi = bf16(v), mid = bf16(v - hi), lo = bf16(v - hi - mid),
 // round to nearest even, both residuals exact fp32 differences.  One element pair per call, each part
-// packed as bf16x2 (element a in the low half): one v_cvt_pk_bf16_f32 per part, the parts' fp32
+// packed as bf16x2 (element a in the low half).  Defined for finite a, b only: with ESP_SPLIT_DOT the
+// residual is a dot over the packed pair, so an inf / NaN partner (or |b| rounding to a bf16 inf) makes the
+// finite element's residual NaN (0 * inf); non-finite operands give a non-finite GEMM output either way,
+// and the Trainer skips such a step (its finite check), so only non-finite results meet non-finite ones: one v_cvt_pk_bf16_f32 per part, the parts' fp32
 // values taken back from the packed bits.  The GEMMs' in-register split (gemm_kernels.h
 // split3_bf16) and every producer of planes (esp_f32_to_planes, LayerNorm, GEMM epilogues) use this,
 // so a planes operand holds exactly the values the in-register split would form.

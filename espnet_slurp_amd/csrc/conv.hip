@@ -40,7 +40,8 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict_
     for (int k = 0; k < 9; ++k) w[q][k] = W[(o4 * 4 + q) * 9 + k];
   }
   const unsigned npix = (unsigned)B * T1 * F1;  // < 2^32 (host check): 32-bit index math
-  const unsigned c0 = blockIdx.x * chunk, c1 = min(npix, c0 + chunk);
+  // c1 in 64 bits: c0 + chunk can pass 2^32 in the last block when npix is near it
+  const unsigned c0 = blockIdx.x * chunk, c1 = (unsigned)min((unsigned long)npix, (unsigned long)c0 + chunk);
   unsigned p = c0 + tp;
   if (p >= c1) return;
   const unsigned r0 = p / (unsigned)F1;

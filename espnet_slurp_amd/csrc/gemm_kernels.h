@@ -1690,8 +1690,16 @@ __device__ __forceinline__ TileCoord tile_coord(const GemmArgs& g, const GldsArg
     const int m0 = tm * BMT;
     const int lo = max(0, g.band_c0 - (m0 + BMT - 1)) / GL_BK * GL_BK;
     const int hi = min(g.K, g.band_c0 - m0 + g.band_w);
-    c.kbeg = max(c.kbeg, lo);
-    c.kend = max(c.kbeg + 1, min(c.kend, hi));  // (never empty: a slab of zeros at worst)
+    const int kb = max(c.kbeg, lo), ke = min(c.kend, hi);
+    if (kb < ke) {
+      c.kbeg = kb;
+      c.kend = ke;
+    } else {
+      // a split-K chunk wholly below lo or at/above hi: its own first column, which is zero in
+      // every row of the tile (lo and hi bound the union of the rows' bands), so the unit adds
+      // exactly nothing.  (Not lo: the split that owns lo computes that column already.)
+      c.kend = c.kbeg + 1;
+    }
   }
   c.nk = (c.kend - c.kbeg + GL_BK - 1) / GL_BK;  // >= 1: the host routes K == 0 elsewhere
   c.m0 = tm * BMT;

@@ -300,14 +300,16 @@ __global__ void argmax_kernel(const float* __restrict__ x, int64_t* __restrict__
   if (lane == 0) out[row] = am == 0x7fffffff ? 0 : am;
 }
 
-// espnet1 forced_align, one block per sequence. lpz (T,V) fp32; y (U); out (T) labels;
-// path: (T, S) int32 workspace
-__global__ __launch_bounds__(1024) void forced_align_kernel(const float* __restrict__ lpz, int T, int V,
-                                                            const int64_t* __restrict__ y, int U, int blank,
-                                                            int* __restrict__ path, int64_t* __restrict__ out) {
+// espnet1 forced_align (ctc.py:185-249), one block per sequence. lpz (T,V) fp32; y (U); out (T) labels;
+// path: (T, S) int32 workspace.  The reference's quirks are kept: candidate s-1 of state 0 is Python's
+// index -1 (the last state; a back-pointer -1 decodes to the last label, the blank), every step's sum is
+// an fp32 add stored in a float64 table (log-zero -1e11 included), and ties keep the first candidate
+// (np.argmax: stay, then s-1, then s-2; the final pair prefers S-1).
+__device__ __forceinline__ void forced_align_body(const float* __restrict__ lpz, int T, int V,
+                                                  const int64_t* __restrict__ y, int U, int blank,
+                                                  int* __restrict__ path, int64_t* __restrict__ out, double (*dl)[1025],
+                                                  int* lab) {
   const int S = 2 * U + 1;
-  __shared__ double dl[2][1025];
-  __shared__ int lab[1025];
   for (int s = threadIdx.x; s < S; s += blockDim.x) lab[s] = (s & 1) ? (int)y[s >> 1] : blank;
   __syncthreads();
   for (int s = threadIdx.x; s < S; s += blockDim.x) {
@@ -345,6 +347,36 @@ __global__ __launch_bounds__(1024) void forced_align_kernel(const float* __restr
       out[t] = lab[st < 0 ? st + S : st];
     }
   }
+}
+
+__global__ __launch_bounds__(1024) void forced_align_kernel(const float* __restrict__ lpz, int T, int V,
+                                                            const int64_t* __restrict__ y, int U, int blank,
+                                                            int* __restrict__ path, int64_t* __restrict__ out) {
+  __shared__ double dl[2][1025];
+  __shared__ int lab[1025];
+  forced_align_body(lpz, T, V, y, U, blank, path, out, dl, lab);
+}
+
+// a batch: block b aligns utterance b (its own T_b = tlen[b] frames of lpz[b], its own U_b = ulen[b] labels
+// of row b of y) exactly as one forced_align call on that utterance would; frames t >= T_b of out row b
+// are -1.  path: B x T x (2 Umax + 1) int32.
+__global__ __launch_bounds__(1024) void forced_align_batch_kernel(const float* __restrict__ lpz, int T, int V,
+                                                                  const int* __restrict__ tlen,
+                                                                  const int64_t* __restrict__ y, int Umax,
+                                                                  const int* __restrict__ ulen, int blank,
+                                                                  int* __restrict__ path, int64_t* __restrict__ out) {
+  __shared__ double dl[2][1025];
+  __shared__ int lab[1025];
+  const int b = blockIdx.x;
+  const int Tb = min(max(tlen[b], 0), T), Ub = min(max(ulen[b], 0), Umax);
+  int64_t* ob = out + (long)b * T;
+  for (int t = Tb + threadIdx.x; t < T; t += blockDim.x) ob[t] = -1;
+  if (Tb < 1 || Ub < 1) {  // nothing to align (the reference needs T >= 1 and a non-empty y)
+    for (int t = threadIdx.x; t < Tb; t += blockDim.x) ob[t] = -1;
+    return;
+  }
+  forced_align_body(lpz + (long)b * T * V, Tb, V, y + (long)b * Umax, Ub, blank,
+                    path + (long)b * T * (2 * Umax + 1), ob, dl, lab);
 }
 
 }  // namespace
@@ -411,6 +443,17 @@ ESP_API int esp_ctc_forced_align(const float* lpz, int T, int V, const long long
   hipLaunchKernelGGL(forced_align_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, lpz, T, V, (const int64_t*)y, U,
                      blank, path, (int64_t*)out);
   ESP_CHECK_LAUNCH("esp_ctc_forced_align");
+  return 0;
+}
+
+ESP_API int esp_ctc_forced_align_batch(const float* lpz, int B, int T, int V, const int* tlen, const long long* y,
+                                       int Umax, const int* ulen, int blank, int* path, long long* out, void* stream) {
+  ESP_ARG_CHECK(2 * Umax + 1 <= 1024 && Umax >= 1 && T >= 1 && B >= 0 && V >= 1,
+                "esp_ctc_forced_align_batch: bad sizes B=%d T=%d V=%d Umax=%d", B, T, V, Umax);
+  if (B == 0) return 0;
+  hipLaunchKernelGGL(forced_align_batch_kernel, dim3(B), dim3(1024), 0, (hipStream_t)stream, lpz, T, V, tlen,
+                     (const int64_t*)y, Umax, ulen, blank, path, (int64_t*)out);
+  ESP_CHECK_LAUNCH("esp_ctc_forced_align_batch");
   return 0;
 }
 

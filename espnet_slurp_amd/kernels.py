@@ -1105,9 +1105,15 @@ def relpos_dqv(dbd, ldp, p, ldpm, out, ldo, nb, H, T):
 # dbd buffers of the latest rel_shift adjoint, kept per (device, Z, T, pitch) and zeroed once: the band
 # kernel writes each row's T band columns only, so the rest stays 0 for every layer and step (half the
 # adjoint's dbd bytes).  Made outside graph capture only (a buffer made inside would live in the graph's
-# pool); a few shapes at most (length buckets), beyond that the full-row kernel.
+# pool); a few shapes at most (length buckets), beyond that the full-row kernel.  One buffer cannot serve
+# two shapes: graphs of different length buckets replay interleaved, and each writes its own band pattern,
+# which is out-of-band garbage in the other's layout -- so the buffers are per shape, and bounded by a
+# byte cap per device (at C2 B=256 one buffer is 1.15 GB: three shapes fit the cap), not by count alone.
+# Nothing frees a buffer while the process runs (a captured graph holds its address);
+# release_relpos_band_buffers() does, for tests and for a caller that has dropped its graphs.
 _DBD_BUFS = {}
 _DBD_MAX_SHAPES = 4
+_DBD_MAX_BYTES = 4 << 30
 
 
 def release_relpos_band_buffers():
@@ -1120,6 +1126,9 @@ def relpos_band_buffer(Z, T, Pp, device):
     buf = _DBD_BUFS.get(key)
     if buf is None:
         if len(_DBD_BUFS) >= _DBD_MAX_SHAPES or torch.cuda.is_current_stream_capturing():
+            return None
+        held = sum(b.numel() * 4 for k, b in _DBD_BUFS.items() if k[0] == str(device))
+        if held + Z * T * Pp * 4 > _DBD_MAX_BYTES:
             return None
         buf = torch.zeros(Z * T * Pp, dtype=torch.float32, device=device)
         _DBD_BUFS[key] = buf
@@ -1279,6 +1288,26 @@ def ctc_forced_align(lpz, y, blank=0):
     path = torch.empty(T * (2 * U + 1), dtype=torch.int32, device=lpz.device)
     out = torch.empty(T, dtype=torch.int64, device=lpz.device)
     _native.call("esp_ctc_forced_align", _p(lpz), T, V, _p(y), U, blank, _p(path), _p(out), _st())
+    return out
+
+
+def ctc_forced_align_batch(lpz, tlen, y, ulen, blank=0):
+    """forced_align of every utterance of a batch in one launch: lpz (B, T, V) fp32 log-probs, tlen (B,) frames,
+    y (B, Umax) labels, ulen (B,) label counts -> (B, T) int64, -1 past each utterance's frames."""
+    B, T, V = lpz.shape
+    Umax = y.shape[1]
+    dev = lpz.device
+    lpz = lpz.contiguous()
+    _f32(lpz)
+    y = y.to(dev).long().contiguous()
+    tl = torch.as_tensor(tlen).to(device=dev, dtype=torch.int32).contiguous()
+    ul = torch.as_tensor(ulen).to(device=dev, dtype=torch.int32).contiguous()
+    if tl.numel() != B or ul.numel() != B or y.shape[0] != B:
+        raise ValueError(f"ctc_forced_align_batch: B={B}, tlen {tl.numel()}, ulen {ul.numel()}, y {tuple(y.shape)}")
+    path = torch.empty(B * T * (2 * Umax + 1), dtype=torch.int32, device=dev)
+    out = torch.empty(B, T, dtype=torch.int64, device=dev)
+    _native.call("esp_ctc_forced_align_batch", _p(lpz), B, T, V, _p(tl), _p(y), Umax, _p(ul), blank, _p(path),
+                 _p(out), _st())
     return out
 
 

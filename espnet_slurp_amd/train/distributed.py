@@ -5,7 +5,10 @@ cut from the flat gradient buffer (flat.py) in backward-completion order: as the
 backward finishes a module (decoder layer, encoder block, ...) the module's slice is marked
 ready; a bucket whose slice is complete is all-reduced asynchronously, overlapping the
 remaining backward kernels (RCCL orders itself after the work already on the stream).
-Gradients are averaged (ReduceOp.AVG on RCCL; SUM + scale on gloo) exactly like DDP.
+Gradients are averaged as SUM + a 1/world scale on device, on every backend (round 6: RCCL's
+ReduceOp.AVG had only ever run at world 1, while the world-2 tests took the gloo SUM branch -- now the
+tested code IS the RCCL code; for world a power of two the scale is exact, so the result is DDP's
+average bit for bit given the same summation order).
 The per-step scalar statistics (X4/X5) travel in one small fused all-reduce.
 BatchNorm statistics stay per-replica (no SyncBN), as in the reference; rank 0's BN
 buffers are broadcast at each forward when `broadcast_buffers` (DDP default, X7).
@@ -70,8 +73,7 @@ class FlatGradReducer:
         while self.next_launch < len(self.buckets) and self.ready[self.next_launch] == self.bucket_count[self.next_launch]:
             s, e = self.buckets[self.next_launch]
             t = self.flat.grad[s:e]
-            op = dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM
-            self.handles[self.next_launch] = dist.all_reduce(t, op=op, group=self.group, async_op=True)
+            self.handles[self.next_launch] = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
             self.next_launch += 1
 
     def module_done(self, module):
@@ -91,11 +93,13 @@ class FlatGradReducer:
         self._launch_ready()
         for h in self.handles.values():
             h.wait()
-        if self.backend != "nccl":
-            if self.flat.grad.is_cuda:
-                K.scale_dropout(self.flat.grad, self.flat.grad, alpha=1.0 / self.world)
-            else:  # gloo on host tensors (the CPU multi-process tests)
-                self.flat.grad.mul_(1.0 / self.world)
+        # the average: the same SUM + scale whatever the backend (the world-2 gloo tests run this code)
+        if self.world == 1:
+            pass
+        elif self.flat.grad.is_cuda:
+            K.scale_dropout(self.flat.grad, self.flat.grad, alpha=1.0 / self.world)
+        else:  # host tensors (the CPU multi-process tests)
+            self.flat.grad.mul_(1.0 / self.world)
         self._reset()
 
     def allreduce_sum(self):

@@ -431,6 +431,13 @@ int esp_reduce_losses(const double* nll, int B, int zero_inf, const double* row_
 int esp_argmax(const float* x, long long* out, long rows, int V, void* stream);
 int esp_ctc_forced_align(const float* lpz, int T, int V, const long long* y, int U, int blank,
                          int* path, long long* out, void* stream);
+/* ABI 31: forced_align over a batch (replaces a loop of espnet/nets/pytorch_backend/ctc.py:185-249
+ * CTC.forced_align calls, one per utterance): lpz (B, T, V) fp32 log-probs, utterance b uses its first
+ * tlen[b] frames and the first ulen[b] labels of row b of y (B, Umax) int64 (tlen / ulen: device int32);
+ * out (B, T) int64 labels, -1 past tlen[b] (and for an utterance with no frames or labels);
+ * path: B * T * (2 Umax + 1) int32 workspace.  Each row equals esp_ctc_forced_align on that utterance. */
+int esp_ctc_forced_align_batch(const float* lpz, int B, int T, int V, const int* tlen, const long long* y,
+                               int Umax, const int* ulen, int blank, int* path, long long* out, void* stream);
 
 /* ---- beam-search CTC prefix scoring (espnet/nets/ctc_prefix_score.py:279-359 CTCPrefixScore,
  *      espnet/nets/scorers/ctc.py CTCPrefixScorer; inference)

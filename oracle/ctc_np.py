@@ -95,7 +95,7 @@ def ctc_argmax_np(logits):
     return np.argmax(np.asarray(logits), axis=-1)
 
 
-def forced_align_np(lpz, y, blank_id=0):
+def forced_align_np(lpz, y, blank_id=0, return_states=False):
     """espnet1 CTC.forced_align (ctc.py:185-249); lpz (T,V) fp32 log-probs, y (U,) int."""
     lpz = np.asarray(lpz, dtype=np.float32)
     y = np.asarray(y, dtype=np.int64)
@@ -122,7 +122,9 @@ def forced_align_np(lpz, y, blank_id=0):
     seq[-1] = [S - 1, S - 2][int(np.argmax(cands))]
     for t in range(T - 2, -1, -1):
         seq[t] = state_path[t + 1, seq[t + 1]]
-    return [int(lab[s]) for s in seq]
+    labels = [int(lab[s]) for s in seq]
+    # return_states: also the state index per frame as the reference holds it (-1 = the s = 0 wrap)
+    return (labels, seq.tolist()) if return_states else labels
 
 
 LOGZERO = np.float32(-10000000000.0)

@@ -27,6 +27,10 @@ Fixture keys, per gated tensor n and site s (conv1, conv2, dec<l>):
   flip/<n>/<s>/s32  int8 [k]       the reference's fp32 decision
   flip/<n>/<s>/c    float64 [k, S] contribution of an "on" decision to the S slice elements
   gs_f32c/<n>                      the fp32 slice with its own flips corrected to the fp64 decisions
+  flip/<n>/<s>/cp   float64 [k, 8] (round 6) the contribution to the 8 fingerprint projections (fingerprint.py),
+                                   formed over every element of the tensor; fp_f32c/<n> the fp32 projections
+                                   corrected like gs_f32c.  (Row-norm fingerprints are not flip-corrected:
+                                   the gate skips them on these tensors, whose projections it corrects.)
 """
 import numpy as np
 import torch
@@ -169,22 +173,38 @@ def _near(pre64, pre32, factor=4.0):
     return (pre64.abs() < tau).nonzero(), tau
 
 
-def flip_records(r64: Records, r32: Records, slice_idx, out: dict, gs32: dict, log=print, prefix="", corr=None):
+def flip_records(r64: Records, r32: Records, slice_idx, out: dict, gs32: dict, log=print, prefix="", corr=None,
+                 shapes=None, corr_fp=None):
     """Compute the flip records of module docstring from the fp64 / fp32 Records of one fixture and
     write them (and the corrected fp32 slices gs_f32c/<n>) into `out`.  slice_idx(name) -> the
     fixture's slice element indices; gs32[name] -> the fp32 slice values.  prefix: site-name prefix
     (one forward of several whose gradients add, e.g. "r0:" per data-parallel rank); corr: a dict
-    that accumulates the fp32 corrections over such calls (gs_f32c written from the running sum)."""
+    that accumulates the fp32 corrections over such calls (gs_f32c written from the running sum).
+    shapes: {name: numel} of the gated tensors -- when given, each site's contribution is also formed for
+    EVERY element of the tensor and projected on the fingerprint vectors (fingerprint.py): "cp" [k, 8], and
+    fp_f32c/<n> = the fp32 projections with the fp32 run's flips corrected (corr_fp accumulates like corr)."""
+    import fingerprint as FP
     corr = {} if corr is None else corr
+    corr_fp = {} if corr_fp is None else corr_fp
+    sg = {}
 
-    def add(name, site, idx, s64, s32, c):
+    def allidx(name):
+        return np.arange(shapes[name], dtype=np.int64) if shapes else None
+
+    def add(name, site, idx, s64, s32, c, cfull=None):
         site = prefix + site
         out[f"flip/{name}/{site}/idx"] = idx.numpy().astype(np.int64)
         out[f"flip/{name}/{site}/s64"] = s64.numpy().astype(np.int8)
         out[f"flip/{name}/{site}/s32"] = s32.numpy().astype(np.int8)
         out[f"flip/{name}/{site}/c"] = c.numpy().astype(np.float64)
-        d = (s32.double() - s64.double())[:, None] * c  # fp32's flips relative to fp64
-        corr[name] = corr.get(name, 0.0) + d.sum(0)
+        ds = (s32.double() - s64.double())[:, None]  # fp32's flips relative to fp64
+        corr[name] = corr.get(name, 0.0) + (ds * c).sum(0)
+        if cfull is not None:
+            if name not in sg:
+                sg[name] = FP.signs(name, shapes[name])
+            cp = cfull @ sg[name].T  # [k, N_PROJ]
+            out[f"flip/{name}/{site}/cp"] = cp.numpy().astype(np.float64)
+            corr_fp[name] = corr_fp.get(name, 0.0) + (ds * cp).sum(0)
 
     if r64.conv:
         c64, c32 = r64.conv, r32.conv
@@ -193,20 +213,46 @@ def flip_records(r64: Records, r32: Records, slice_idx, out: dict, gs32: dict, l
         g1 = c64["out1_grad"].double()
         g2 = c64["out2_grad"].double()
         W2 = c64["W2"].double()                    # [O, C, 3, 3]
+
+        def conv1_contrib(b, c, t1, f1, gg, iw, ib):
+            wc, wi, wj = iw // 9, (iw % 9) // 3, iw % 3  # weight [C, 1, 3, 3] flat
+            xw = x[b[:, None], 2 * t1[:, None] + wi[None], 2 * f1[:, None] + wj[None]]  # [k, S]
+            cw = torch.where(c[:, None] == wc[None], gg[:, None] * xw, torch.zeros_like(xw))
+            cb = torch.where(c[:, None] == ib[None], gg[:, None].expand(-1, len(ib)),
+                             torch.zeros(len(b), len(ib), dtype=torch.float64))
+            return cw, cb
+
+        def conv2_contrib(b, o, t2, f2, gg, iw, ib):
+            wc, wi, wj = iw // 9, (iw % 9) // 3, iw % 3
+            cw = torch.zeros(len(b), len(iw), dtype=torch.float64)
+            cb = torch.zeros(len(b), len(ib), dtype=torch.float64)
+            for kt in range(3):
+                for kf in range(3):
+                    tt, ff = 2 * t2 + kt, 2 * f2 + kf
+                    # weight elements (c', i, j)
+                    m = (pre1[b[:, None], wc[None], tt[:, None], ff[:, None]] > 0).double()
+                    wv = W2[o[:, None], wc[None], kt, kf]
+                    xv = x[b[:, None], 2 * tt[:, None] + wi[None], 2 * ff[:, None] + wj[None]]
+                    cw += gg[:, None] * wv * m * xv
+                    mb = (pre1[b[:, None], ib[None], tt[:, None], ff[:, None]] > 0).double()
+                    cb += gg[:, None] * W2[o[:, None], ib[None], kt, kf] * mb
+            return cw, cb
+
         iw = torch.from_numpy(slice_idx(CONV_TENSORS[0]))
         ib = torch.from_numpy(slice_idx(CONV_TENSORS[1]))
-        wc, wi, wj = iw // 9, (iw % 9) // 3, iw % 3  # weight [C, 1, 3, 3] flat
         # conv1 flips
         near, tau1 = _near(c64["pre1"], c32["pre1"])
         b, c, t1, f1 = near.unbind(1) if len(near) else (torch.zeros(0, dtype=torch.long),) * 4
         gg = g1[b, c, t1, f1]
         s64 = c64["pre1"][b, c, t1, f1] > 0
         s32 = c32["pre1"][b, c, t1, f1] > 0
-        xw = x[b[:, None], 2 * t1[:, None] + wi[None], 2 * f1[:, None] + wj[None]]  # [k, S]
-        cw = torch.where(c[:, None] == wc[None], gg[:, None] * xw, torch.zeros_like(xw))
-        cb = torch.where(c[:, None] == ib[None], gg[:, None].expand(-1, len(ib)), torch.zeros(len(b), len(ib), dtype=torch.float64))
-        add(CONV_TENSORS[0], "conv1", near, s64, s32, cw)
-        add(CONV_TENSORS[1], "conv1", near, s64, s32, cb)
+        cw, cb = conv1_contrib(b, c, t1, f1, gg, iw, ib)
+        fw = fb = None
+        if shapes:
+            fw, fb = conv1_contrib(b, c, t1, f1, gg, torch.from_numpy(allidx(CONV_TENSORS[0])),
+                                   torch.from_numpy(allidx(CONV_TENSORS[1])))
+        add(CONV_TENSORS[0], "conv1", near, s64, s32, cw, fw)
+        add(CONV_TENSORS[1], "conv1", near, s64, s32, cb, fb)
         log(f"conv1: tau {tau1:.3g}, {len(b)} decisions, {(s64 != s32).sum().item()} flipped in fp32")
         # conv2 flips: through relu1's fp64 mask into conv.0
         near, tau2 = _near(c64["pre2"], c32["pre2"])
@@ -214,20 +260,13 @@ def flip_records(r64: Records, r32: Records, slice_idx, out: dict, gs32: dict, l
         gg = g2[b, o, t2, f2]
         s64 = c64["pre2"][b, o, t2, f2] > 0
         s32 = c32["pre2"][b, o, t2, f2] > 0
-        cw = torch.zeros(len(b), len(iw), dtype=torch.float64)
-        cb = torch.zeros(len(b), len(ib), dtype=torch.float64)
-        for kt in range(3):
-            for kf in range(3):
-                tt, ff = 2 * t2 + kt, 2 * f2 + kf
-                # weight slice elements (c', i, j)
-                m = (pre1[b[:, None], wc[None], tt[:, None], ff[:, None]] > 0).double()
-                wv = W2[o[:, None], wc[None], kt, kf]
-                xv = x[b[:, None], 2 * tt[:, None] + wi[None], 2 * ff[:, None] + wj[None]]
-                cw += gg[:, None] * wv * m * xv
-                mb = (pre1[b[:, None], ib[None], tt[:, None], ff[:, None]] > 0).double()
-                cb += gg[:, None] * W2[o[:, None], ib[None], kt, kf] * mb
-        add(CONV_TENSORS[0], "conv2", near, s64, s32, cw)
-        add(CONV_TENSORS[1], "conv2", near, s64, s32, cb)
+        cw, cb = conv2_contrib(b, o, t2, f2, gg, iw, ib)
+        fw = fb = None
+        if shapes:
+            fw, fb = conv2_contrib(b, o, t2, f2, gg, torch.from_numpy(allidx(CONV_TENSORS[0])),
+                                   torch.from_numpy(allidx(CONV_TENSORS[1])))
+        add(CONV_TENSORS[0], "conv2", near, s64, s32, cw, fw)
+        add(CONV_TENSORS[1], "conv2", near, s64, s32, cb, fb)
         log(f"conv2: tau {tau2:.3g}, {len(b)} decisions, {(s64 != s32).sum().item()} flipped in fp32")
     for l, d64 in sorted(r64.dec.items()):
         d32 = r32.dec[l]
@@ -240,13 +279,19 @@ def flip_records(r64: Records, r32: Records, slice_idx, out: dict, gs32: dict, l
         W1 = d64["W1"].double()
         y = d64["y"].double()
         gam, bet = d64["gamma"].double(), d64["beta"].double()
-        for name in (lay + ".norm3.weight", lay + ".norm3.bias"):
-            ci = torch.from_numpy(slice_idx(name))
+
+        def dec_contrib(name, ci):
             c = g[:, None] * W1[u[:, None], ci[None]]
             if name.endswith("weight"):
                 xhat = (y[b[:, None], p[:, None], ci[None]] - bet[ci][None]) / gam[ci][None]
                 c = c * xhat
-            add(name, f"dec{l}", near, s64, s32, c)
+            return c
+        for name in (lay + ".norm3.weight", lay + ".norm3.bias"):
+            c = dec_contrib(name, torch.from_numpy(slice_idx(name)))
+            cf = dec_contrib(name, torch.from_numpy(allidx(name))) if shapes else None
+            add(name, f"dec{l}", near, s64, s32, c, cf)
         log(f"{lay}: tau {tau:.3g}, {len(b)} decisions, {(s64 != s32).sum().item()} flipped in fp32")
     for name, d in corr.items():
         out[f"gs_f32c/{name}"] = np.asarray(gs32[name], dtype=np.float64) - d.numpy()
+    for name, d in corr_fp.items():
+        out[f"fp_f32c/{name}"] = np.asarray(out[f"fp_f32/{name}"], dtype=np.float64) - d.numpy()

@@ -9,14 +9,17 @@ cannot produce this fixture here: at B=128 its fp32 autograd graph needs ~75 GB 
 one ~130 GB, over this container's 64 GB; the oracle runs on the GPU box's host (16 threads,
 ~4 min, ~130 GB peak), which is where this script is meant to run.  The oracle is pinned to
 the reference at this exact model shape (tests/golden/fullsize_c2_grad_{latest,legacy}.npz,
-B=2: the generator asserts oracle == reference); what B=128 adds is the batch-coupled part
+B=2: since round 6 their generator, make_golden.fullsize_train_fixture, runs the oracle's fp64 step on the
+same inputs and asserts its loss and EVERY parameter gradient equal the reference's fp64 ones to fp64
+rounding before writing; until round 5 it checked nothing of the kind); what B=128 adds is the batch-coupled part
 (BatchNorm statistics over B*T' = 47,872 frames, the 1/B loss normalisation) and, on the GPU
 side, every shape-dependent code path of the bench (split-K counts, persistent-grid wrap,
 implicit-im2col index ranges, attention grids with z = 512).
 
 Stored: the seed, lengths and target lengths (the inputs are regenerated from the seed by
 O.synthetic_batch), loss / loss_ctc / loss_att / acc, and per parameter the gradient L2
-norm, max |g| and a fixed slice of elements, for both precisions, plus the ReLU flip records of
+norm, max |g|, a fixed slice of elements and the whole-tensor fingerprint (fingerprint.py: 8 fp64
+projections, per-row norms), for both precisions, plus the ReLU flip records of
 conv.0 and the decoder norm3 slices (flipfix.py) (the format of make_golden.fullsize_train_fixture,
 read by tests/helpers.grad_gate / loss_gate).
 Test infrastructure only: never imported by the product.
@@ -37,6 +40,7 @@ sys.path.insert(0, ROOT)
 from oracle import espnet_cpu as O  # noqa: E402
 
 sys.path.insert(0, HERE)
+import fingerprint as FP  # noqa: E402
 import flipfix  # noqa: E402
 
 B, T, V, SEED = 128, 1500, 600, 71
@@ -66,7 +70,7 @@ def slice_indices(name: str, numel: int) -> np.ndarray:
     return idx.astype(np.int64)
 
 
-def run(dt, tag, out, recs):
+def run(dt, tag, out, recs, rows, shapes):
     cfg = bench_cfg()
     lens, ulens = bench_lengths()
     P = {k: v.requires_grad_(v.is_floating_point() and "running" not in k)
@@ -93,6 +97,8 @@ def run(dt, tag, out, recs):
         out[f"gmax_{tag}/{n}"] = np.float64(g.abs().max().item())
         out[f"gidx/{n}"] = idx
         out[f"gs_{tag}/{n}"] = g[torch.from_numpy(idx)].numpy()
+        FP.summarize(n, p.grad.detach(), tag, out, rows)
+        shapes[n] = g.numel()
 
 
 def main():
@@ -101,13 +107,16 @@ def main():
     print(f"bench fixture: B={B} T={T} on {n} threads", flush=True)
     out = {}
     recs = {}
-    run(torch.float32, "f32", out, recs)
+    rows = {}
+    shapes = {}
+    run(torch.float32, "f32", out, recs, rows, shapes)
     gc.collect()
-    run(torch.float64, "f64", out, recs)
+    run(torch.float64, "f64", out, recs, rows, shapes)
     gc.collect()
+    FP.finish_rows(out, rows)
     gs32 = {k[len("gs_f32/"):]: v for k, v in out.items() if k.startswith("gs_f32/")}
     flipfix.flip_records(recs["f64"], recs["f32"], lambda n: out["gidx/" + n], out, gs32,
-                         log=lambda m: print(m, flush=True))
+                         log=lambda m: print(m, flush=True), shapes=shapes)
     del recs
     gc.collect()
     lens, ulens = bench_lengths()

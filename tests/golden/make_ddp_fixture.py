@@ -10,7 +10,7 @@ utterances (T up to 1500) sharded 3 / 2, per-rank loss weighted by its batch siz
 loss = sum_r w_r loss_r / sum_r w (what DDP's average of world * w_r / sum w * loss_r yields), one
 backward over both replicas -> the averaged gradient.  fp32 AND fp64; stored in the format of
 make_golden.fullsize_train_fixture (loss and stats as recursive_average's weighted means,
-per-tensor gradient norms and slices) plus each rank's ReLU flip records ("r0:", "r1:" site
+per-tensor gradient norms, slices and fingerprints) plus each rank's ReLU flip records ("r0:", "r1:" site
 prefixes, flipfix.py).  Read by tests/test_gpu_distributed.py::test_two_rank_c2_shape_ddp_step.
 Test infrastructure only.
 """
@@ -24,6 +24,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 import make_golden as G  # noqa: E402  (sets up the reference import)
+import fingerprint as FP  # noqa: E402
 import flipfix  # noqa: E402
 from oracle import espnet_cpu as O  # noqa: E402
 
@@ -47,6 +48,7 @@ def main():
     cfg = G.c2_cfg("latest")
     out = {}
     recs = {}
+    rows = {}
     for dt, tag in ((torch.float32, "f32"), (torch.float64, "f64")):
         t0 = time.time()
         models, losses, ws, stats = [], [], [], {}
@@ -72,17 +74,20 @@ def main():
         # the averaged gradient: one replica's parameters receive their own rank's share; sum them
         for (n, p0), (_, p1) in zip(models[0].named_parameters(), models[1].named_parameters()):
             p0.grad = p0.grad + p1.grad
-        G.grad_summary(models[0], tag, out)
+        G.grad_summary(models[0], tag, out, rows)
+        shapes = {n: p.numel() for n, p in models[0].named_parameters()}
         out[f"loss_{tag}"] = np.float64(total.item())
         for k, v in stats.items():
             out[f"{k}_{tag}"] = np.float64(v / wsum)
         print(f"ddp {tag}: loss {total.item():.8f} ({time.time() - t0:.1f} s)", flush=True)
         del models, losses, total
+    FP.finish_rows(out, rows)
     gs32 = {k[len("gs_f32/"):]: v for k, v in out.items() if k.startswith("gs_f32/")}
-    corr = {}
+    corr, corr_fp = {}, {}
     for r in range(WORLD):
         flipfix.flip_records(recs[("f64", r)], recs[("f32", r)], lambda n: out["gidx/" + n], out, gs32,
-                             log=lambda m: print(f"rank {r}: {m}", flush=True), prefix=f"r{r}:", corr=corr)
+                             log=lambda m: print(f"rank {r}: {m}", flush=True), prefix=f"r{r}:", corr=corr,
+                             shapes=shapes, corr_fp=corr_fp)
     out.update(lens=np.array(LENS), ulens=np.array(ULENS), seed=np.int64(SEED), world=np.int64(WORLD))
     path = os.path.join(HERE, "ddp_c2.npz")
     np.savez_compressed(path, **out)

@@ -201,6 +201,63 @@ def align_fixture():
     np.savez_compressed(os.path.join(HERE, "align.npz"), **cases)
 
 
+def align_c2_fixture():
+    """forced_align / argmax at the C2 workload shape (VERDICT r5 'next' 1a): T' = 374 frames, V = 600,
+    U in {20, 40}, through the reference's own espnet1 CTC (ctc_lo = identity, so h is the logits).
+    Cases: 0 trained-like (a monotone label path dominates), 1 / 2 random logits (U = 40 / 20), where
+    the s = 0 candidate s-1 = Python's index -1 (the last state) wins on some frames of the returned
+    path, 3 logits quantised to {0, 1, 2} (exact fp32 ties in lpz, the path sums and argmax), 4 all-zero
+    logits (every path sum ties), 5 runs of repeated labels.  The generator asserts the oracle equals the
+    reference on every case and records how many frames of each alignment came through the wrap."""
+    rng = np.random.Generator(np.random.PCG64(374))
+    T, V = 374, 600
+    ctc1 = CTC1(odim=V, eprojs=V, dropout_rate=0.0)
+    with torch.no_grad():
+        ctc1.ctc_lo.weight.copy_(torch.eye(V))
+        ctc1.ctc_lo.bias.zero_()
+    cases = {}
+    wraps = []
+    specs = [(40, "peaked"), (40, "random"), (20, "random"), (40, "quant"), (40, "zeros"), (40, "repeats")]
+    for ci, (U, kind) in enumerate(specs):
+        y = rng.integers(1, V - 1, size=U).astype(np.int64)
+        if kind == "repeats":
+            y[5:9] = y[4]
+            y[20:22] = y[19]
+        if kind == "peaked":
+            h = rng.standard_normal((T, V)).astype(np.float32)
+            pos = np.sort(rng.choice(np.arange(1, T - 1), size=U, replace=False))
+            h[:, 0] += 4.0
+            for u, p in enumerate(pos):
+                h[p, y[u]] += 8.0
+        elif kind in ("random", "repeats"):
+            h = (2.0 * rng.standard_normal((T, V))).astype(np.float32)
+        elif kind == "quant":
+            h = rng.integers(0, 3, size=(T, V)).astype(np.float32)
+        else:
+            h = np.zeros((T, V), dtype=np.float32)
+        with torch.no_grad():
+            ali = ctc1.forced_align(torch.from_numpy(h)[None], torch.from_numpy(y), blank_id=0)
+            lpz = ctc1.log_softmax(torch.from_numpy(h)[None])[0].numpy()
+        ali = np.array([int(a) for a in ali], dtype=np.int64)
+        mine, states = ctc_np.forced_align_np(lpz, y, return_states=True)
+        assert (np.array(mine) == ali).all(), (ci, kind)
+        wraps.append(int(sum(1 for s_ in states if s_ < 0)))
+        cases[f"lpz{ci}"] = lpz
+        cases[f"y{ci}"] = y
+        cases[f"ali{ci}"] = ali
+        # argmax (ctc.py:119-127 is torch.argmax over the logits): on lpz for every case, and on the logits
+        # themselves where they hold exact ties (kept small: the integer / zero logits compress to nothing)
+        cases[f"argmax{ci}"] = torch.argmax(torch.from_numpy(lpz), dim=-1).numpy()
+        if kind in ("quant", "zeros"):
+            cases[f"h{ci}"] = h
+            cases[f"argmax_h{ci}"] = torch.argmax(torch.from_numpy(h), dim=-1).numpy()
+    cases["wrap_frames"] = np.array(wraps, dtype=np.int64)
+    cases["kinds"] = np.array([k for _, k in specs])
+    print("align_c2: ok; frames through the s=0 wrap per case", wraps)
+    assert any(w > 0 for w in wraps), "no case exercises the s=0 wrap"
+    np.savez_compressed(os.path.join(HERE, "align_c2.npz"), **cases)
+
+
 def specaug_fixture():
     B, T, F_ = 2, 100, 80
     rng = np.random.Generator(np.random.PCG64(5))
@@ -309,8 +366,10 @@ def slice_indices(name: str, numel: int) -> np.ndarray:
     return idx.astype(np.int64)
 
 
-def grad_summary(model, tag: str, out: dict):
-    """Per-tensor gradient L2 norm (fp64), max |g| and a fixed slice of elements."""
+def grad_summary(model, tag: str, out: dict, rows=None):
+    """Per-tensor gradient L2 norm (fp64), max |g|, a fixed slice of elements and (rows: a dict kept across
+    the fp32 and fp64 runs, fingerprint.finish_rows after both) the whole-tensor fingerprint."""
+    import fingerprint as FP
     for n, p in model.named_parameters():
         g = p.grad.detach().double().reshape(-1)
         idx = slice_indices(n, g.numel())
@@ -318,19 +377,44 @@ def grad_summary(model, tag: str, out: dict):
         out[f"gmax_{tag}/{n}"] = np.float64(g.abs().max().item())
         out[f"gidx/{n}"] = idx
         out[f"gs_{tag}/{n}"] = g[torch.from_numpy(idx)].numpy()
+        if rows is not None:
+            FP.summarize(n, p.grad.detach(), tag, out, rows)
+
+
+def oracle_vs_reference(cfg, seed, speech, slen, text, tlen, ref_loss, ref_grads, name, log=print):
+    """VERDICT r5 'next' 1d: the oracle restatement (oracle/espnet_cpu.py) run in fp64 on the fixture's own
+    inputs and parameters must equal the reference's fp64 step -- the loss and EVERY parameter gradient
+    (max |g_oracle - g_ref| relative to the largest gradient element of the model) -- to fp64 rounding, so
+    the oracle-generated fixtures at other batch sizes (make_bench_fixture.py) rest on a pinned oracle."""
+    P = {k: v.clone().requires_grad_(v.is_floating_point() and "running" not in k)
+         for k, v in O.deterministic_params(cfg, seed, torch.float64).items()}
+    oloss, _, _ = O.asr_forward(P, speech.to(torch.float64), slen, text, tlen, cfg, bn_state={})
+    oloss.backward()
+    scale = max(float(g.abs().max()) for g in ref_grads.values())
+    dl = abs(oloss.item() - ref_loss) / max(1.0, abs(ref_loss))
+    worst = max((float((P[n].grad - g).abs().max()) / scale, n) for n, g in ref_grads.items())
+    log(f"{name}: oracle vs reference fp64: |dloss| {dl:.2e} relative, worst gradient {worst[0]:.2e} ({worst[1]})")
+    assert dl < 1e-10, dl
+    assert worst[0] < 1e-9, worst
+    return dl, worst[0]
 
 
 def fullsize_train_fixture(name: str, cfg, B=2, T=1500, lens=(1500, 1337), ulens=(40, 27), seed=42,
-                           with_grads=True, build=None, train=True):
+                           with_grads=True, build=None, train=True, oracle_check=True):
     """Full-size fp32 AND fp64 reference step (SURVEY.md §8(d) gate judged against fp64): loss,
-    loss_ctc / loss_att / acc and, with_grads, every parameter's gradient norm and a fixed
-    slice of its elements.  train=False runs the reference in eval mode (validation step:
-    no dropout, no SpecAug, BatchNorm from its running statistics)."""
+    loss_ctc / loss_att / acc and, with_grads, every parameter's gradient norm, a fixed
+    slice of its elements and its whole-tensor fingerprint (fingerprint.py).  train=False runs the
+    reference in eval mode (validation step: no dropout, no SpecAug, BatchNorm from its running
+    statistics).  With grads and oracle_check, the oracle's fp64 step is asserted equal to the
+    reference's (loss and every gradient, oracle_vs_reference) before the fixture is written."""
     import time as _t
     import flipfix
+    import fingerprint as FP
     build = build or (lambda: build_reference(cfg))
     out = {}
     recs = {}
+    rows = {}
+    shapes = {}
     F_ = cfg.enc.input_size
     for dt, tag in ((torch.float32, "f32"), (torch.float64, "f64")):
         t0 = _t.time()
@@ -344,7 +428,11 @@ def fullsize_train_fixture(name: str, cfg, B=2, T=1500, lens=(1500, 1337), ulens
                 loss, stats, _ = model(speech.to(dt), slen, text, tlen)
             loss.backward()
             recs[tag] = probe.rec.detach()
-            grad_summary(model, tag, out)
+            grad_summary(model, tag, out, rows)
+            shapes = {n: p.numel() for n, p in model.named_parameters()}
+            if tag == "f64" and oracle_check and train:
+                ref_grads = {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+                ref_loss = loss.item()
         else:
             with torch.no_grad():
                 loss, stats, _ = model(speech.to(dt), slen, text, tlen)
@@ -359,9 +447,19 @@ def fullsize_train_fixture(name: str, cfg, B=2, T=1500, lens=(1500, 1337), ulens
         print(f"{name} {tag}: loss {loss.item():.6f} ({_t.time() - t0:.1f} s)", flush=True)
         del model
     if with_grads:
+        FP.finish_rows(out, rows)
         gs32 = {k[len("gs_f32/"):]: v for k, v in out.items() if k.startswith("gs_f32/")}
         flipfix.flip_records(recs["f64"], recs["f32"], lambda n: out["gidx/" + n], out, gs32,
-                             log=lambda m: print(f"{name}: {m}", flush=True))
+                             log=lambda m: print(f"{name}: {m}", flush=True), shapes=shapes)
+        del recs
+        if oracle_check and train:
+            speech, slen, text, tlen = O.synthetic_batch(B, T, F_, cfg.vocab_size, list(lens), list(ulens), seed + 1)
+            t0 = _t.time()
+            dl, dg = oracle_vs_reference(cfg, seed, speech, slen, text, tlen, ref_loss, ref_grads, name,
+                                         log=lambda m: print(m, flush=True))
+            print(f"{name}: oracle check {_t.time() - t0:.1f} s", flush=True)
+            out["oracle_ref64_dloss"] = np.float64(dl)
+            out["oracle_ref64_dgrad"] = np.float64(dg)
     out.update(lens=np.array(lens), ulens=np.array(ulens), seed=np.int64(seed), B=np.int64(B), T=np.int64(T))
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
 
@@ -681,38 +779,49 @@ def trainrun_fixture():
     from espnet2.train.trainer import TrainerOptions as RefOptions
 
     class Factory(AbsIterFactory):
-        def __init__(self, spec):
-            self.spec = spec
+        def __init__(self, spec, dtype):
+            self.spec, self.dtype = spec, dtype
 
         def build_iter(self, epoch, shuffle=None):
-            return trainrun_batches(self.spec, epoch)
+            return [(ids, dict(b, speech=b["speech"].to(self.dtype))) for ids, b in trainrun_batches(self.spec, epoch)]
 
     cfg = small_cfg("latest")
-    model = build_reference(cfg)
-    load_params(model, cfg, 21)
-    opt = torch.optim.Adam(model.parameters(), lr=0.002, betas=(0.9, 0.98), eps=1e-9, weight_decay=1e-6)
-    sch = WarmupLR(opt, warmup_steps=10)
-    with tempfile.TemporaryDirectory() as td:
-        o = RefOptions(ngpu=0, resume=True, use_amp=False, train_dtype="float32", grad_noise=False, accum_grad=1,
-                       grad_clip=5.0, grad_clip_type=2.0, log_interval=None, no_forward_run=False,
-                       use_matplotlib=False, use_tensorboard=False, use_wandb=False, output_dir=td,
-                       sharded_ddp=False, unused_parameters=False, wandb_model_log_interval=-1,
-                       create_graph_in_tensorboard=False, **TRAINRUN_OPTS)
-        RefTrainer.run(model=model, optimizers=[opt], schedulers=[sch], train_iter_factory=Factory(TRAINRUN_TRAIN),
-                       valid_iter_factory=Factory(TRAINRUN_VALID), plot_attention_iter_factory=None,
-                       trainer_options=o, distributed_option=DistributedOption(distributed=False, ngpu=0))
-        out = Path(td)
-        from espnet_slurp_amd.train.checkpoint import safe_load
-        rep = safe_load(out / "checkpoint.pth")["reporter"]
-        values = {}
-        for e, per in rep["stats"].items():
-            values[str(e)] = {ph: {k: float(v) for k, v in d.items() if k in ("loss", "loss_att", "loss_ctc", "acc",
-                                                                                "optim0_lr0")}
-                              for ph, d in per.items() if ph in ("train", "valid")}
-        files = sorted(p.name for p in out.iterdir())
-        links = {p.name: str(p.readlink()) for p in out.iterdir() if p.is_symlink()}
-    meta = {"values": values, "files": files, "links": links, "seed": 21, "opts": TRAINRUN_OPTS,
+    runs = {}
+    # the same run in fp32 (the fixture) and in fp64 (round 6: the bar the GPU's values are gated against,
+    # with the fp32 run's own distance to it as the allowance -- the rule of every other gate)
+    for dt, tag in ((torch.float32, "f32"), (torch.float64, "f64")):
+        model = build_reference(cfg).to(dt)
+        load_params(model, cfg, 21, dt)
+        opt = torch.optim.Adam(model.parameters(), lr=0.002, betas=(0.9, 0.98), eps=1e-9, weight_decay=1e-6)
+        sch = WarmupLR(opt, warmup_steps=10)
+        with tempfile.TemporaryDirectory() as td:
+            o = RefOptions(ngpu=0, resume=True, use_amp=False, train_dtype=str(dt).split(".")[1], grad_noise=False,
+                           accum_grad=1, grad_clip=5.0, grad_clip_type=2.0, log_interval=None, no_forward_run=False,
+                           use_matplotlib=False, use_tensorboard=False, use_wandb=False, output_dir=td,
+                           sharded_ddp=False, unused_parameters=False, wandb_model_log_interval=-1,
+                           create_graph_in_tensorboard=False, **TRAINRUN_OPTS)
+            RefTrainer.run(model=model, optimizers=[opt], schedulers=[sch],
+                           train_iter_factory=Factory(TRAINRUN_TRAIN, dt), valid_iter_factory=Factory(TRAINRUN_VALID, dt),
+                           plot_attention_iter_factory=None, trainer_options=o,
+                           distributed_option=DistributedOption(distributed=False, ngpu=0))
+            out = Path(td)
+            from espnet_slurp_amd.train.checkpoint import safe_load
+            rep = safe_load(out / "checkpoint.pth")["reporter"]
+            values = {}
+            for e, per in rep["stats"].items():
+                values[str(e)] = {ph: {k: float(v) for k, v in d.items() if k in ("loss", "loss_att", "loss_ctc",
+                                                                                    "acc", "optim0_lr0")}
+                                  for ph, d in per.items() if ph in ("train", "valid")}
+            runs[tag] = (values, sorted(p.name for p in out.iterdir()),
+                         {p.name: str(p.readlink()) for p in out.iterdir() if p.is_symlink()})
+    values, files, links = runs["f32"]
+    assert runs["f64"][1] == files and runs["f64"][2] == links, (runs["f64"][1:], files, links)
+    meta = {"values": values, "values_f64": runs["f64"][0], "files": files, "links": links, "seed": 21,
+            "opts": TRAINRUN_OPTS,
             "adam": {"lr": 0.002, "betas": [0.9, 0.98], "eps": 1e-9, "weight_decay": 1e-6}, "warmup_steps": 10}
+    for e, per in values.items():
+        for ph, vals in per.items():
+            print(e, ph, {k: f"{abs(v - runs['f64'][0][e][ph][k]):.2e}" for k, v in vals.items()})
     with open(os.path.join(HERE, "trainrun_ref.json"), "w") as f:
         json.dump(meta, f, indent=1)
     print("trainrun:", files, links)
@@ -729,6 +838,8 @@ if __name__ == "__main__":
         ctc_fixture()
     if "align" in which:
         align_fixture()
+    if "align_c2" in which:
+        align_c2_fixture()
     if "specaug" in which:
         specaug_fixture()
     if "small" in which:

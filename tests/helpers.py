@@ -247,6 +247,46 @@ def grad_gate(model, g, skip_rel=1e-6, flips=None):
         er = float(np.abs(s32 - g["gs_f64/" + n]).max()) / gm
         if es > max(1e-4, 2 * er):
             bad.append((n, "slice", es, er))
+        bad += fingerprint_gate(n, p.grad, g, gn64, flips)
+    return bad
+
+
+def fingerprint_gate(n, grad, g, gn64, flips=None):
+    """The whole-tensor fingerprint of a full-size fixture (tests/golden/fingerprint.py, round 6): the 8 fp64
+    projections on fixed +-1 vectors, relative to the fp64 norm, and for rank >= 2 tensors every row's L2 norm,
+    relative to the largest fp64 row norm -- each within max(1e-4, 2 e_ref), e_ref the reference fp32 run's own
+    error.  Projections of the ReLU-flip tensors are corrected like their slices (flip/<n>/<site>/cp, exact:
+    a projection is linear); their row norms are not gated (not linear; the corrected projections cover
+    them).  Fixtures written before round 6 carry no fingerprint: nothing is checked then."""
+    if "fp_f64/" + n not in g:
+        return []
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import fingerprint as FP
+    bad = []
+    p64 = g["fp_f64/" + n].astype(np.float64)
+    pg = FP.projections(n, grad).cpu().numpy()
+    pre = f"flip/{n}/"
+    sites = sorted({k[len(pre):].split("/")[0] for k in g if k.startswith(pre)})
+    for site in sites:
+        idx = g[f"{pre}{site}/idx"]
+        if len(idx) == 0 or f"{pre}{site}/cp" not in g:
+            continue
+        assert flips is not None, f"{n}: the fixture holds ReLU flip records, pass flips=FlipProbe(...)"
+        sg = flips.decisions(site, idx).astype(np.float64)
+        pg = pg - ((sg - g[f"{pre}{site}/s64"].astype(np.float64))[:, None] * g[f"{pre}{site}/cp"]).sum(0)
+    p32 = g["fp_f32c/" + n] if "fp_f32c/" + n in g else g["fp_f32/" + n]
+    ep = float(np.abs(pg - p64).max()) / gn64
+    er = float(np.abs(p32 - p64).max()) / gn64
+    if ep > max(1e-4, 2 * er):
+        bad.append((n, "projection", ep, er))
+    if "rn_f64/" + n in g and not sites:
+        r64 = g["rn_f64/" + n].astype(np.float64)
+        rg = FP.row_norms(grad).cpu().numpy()
+        er = float(g["rn_eref/" + n])
+        en = float(np.abs(rg - r64).max()) / max(float(r64.max()), 1e-300)
+        if en > max(1e-4, 2 * er):
+            bad.append((n, "rows", en, er, int(np.abs(rg - r64).argmax())))
     return bad
 
 

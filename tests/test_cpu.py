@@ -113,6 +113,20 @@ def test_forced_align_numpy_oracle_bit_exact():
         assert np.array_equal(ctc_np.ctc_argmax_np(g[f"h{ci}"]), g[f"argmax{ci}"])
 
 
+def test_forced_align_numpy_oracle_bit_exact_c2_shape():
+    """The oracle against the reference's forced_align at the workload shape (align_c2.npz: T' = 374,
+    V = 600, U = 20 / 40; random, tied and trained-like logits, the s = 0 wrap on several frames)."""
+    g = golden("align_c2")
+    assert int(g["wrap_frames"].max()) > 0
+    for ci in range(len(g["kinds"])):
+        ali, st = ctc_np.forced_align_np(g[f"lpz{ci}"], g[f"y{ci}"], return_states=True)
+        assert np.array_equal(np.array(ali), g[f"ali{ci}"]), ci
+        assert sum(1 for s in st if s < 0) == int(g["wrap_frames"][ci])
+        assert np.array_equal(ctc_np.ctc_argmax_np(g[f"lpz{ci}"]), g[f"argmax{ci}"])
+        if f"h{ci}" in g:
+            assert np.array_equal(ctc_np.ctc_argmax_np(g[f"h{ci}"]), g[f"argmax_h{ci}"])
+
+
 def test_specaug_oracle_vs_reference():
     g = golden("specaug")
     x = torch.from_numpy(g["x"])

@@ -55,16 +55,36 @@ def _trainer(dev, out, graph, max_epoch=None, dropout=None):
     return Trainer(model, opt, sch, opts, cuda_graph=graph), ref
 
 
-@pytest.mark.parametrize("graph", [False, True])
-def test_trainer_run_matches_reference(dev, tmp_path, graph):
-    tr, ref = _trainer(dev, tmp_path, graph)
-    rep = tr.run(_Factory(TRAIN, dev), _Factory(VALID, dev))
+def _gate(rep, ref, tag):
+    """Every reporter value of the 3-epoch run against the reference's fp64 run of the same Trainer.run
+    (trainrun_ref.json "values_f64", make_golden.py trainrun): within max(1e-4, 2 |ref32 - ref64|) -- the
+    loss gate of every other test; the reference's own fp32 run is 1.5e-7 .. 1.2e-4 off fp64 over the 9
+    updates -- and acc exactly (both reference runs agree to the last bit: no argmax decision is near a tie;
+    1e-6 covers the fp32 / fp64 representation of the same fraction).  The learning rate is host arithmetic
+    (1e-9).  Every error is logged (TRAINRUN_GATE lines)."""
+    fails = []
     for e, per in ref["values"].items():
         for ph, vals in per.items():
             for k, v in vals.items():
                 got = rep.get_value(ph, k, epoch=int(e))
-                tol = 1e-9 if k.startswith("optim") else (2e-3 if k == "acc" else 2e-4 * max(1.0, abs(v)))
-                assert abs(got - v) <= tol, (e, ph, k, got, v)
+                v64 = ref["values_f64"][e][ph][k]
+                if k.startswith("optim"):
+                    tol = 1e-9
+                elif k == "acc":
+                    tol = 1e-6
+                else:
+                    tol = max(1e-4, 2 * abs(v - v64))
+                print(f"TRAINRUN_GATE {tag} e{e} {ph} {k} err={abs(got - v64):.3e} e_ref={abs(v - v64):.3e} tol={tol:.3e}")
+                if abs(got - v64) > tol:
+                    fails.append((e, ph, k, got, v64, tol))
+    assert not fails, fails
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_trainer_run_matches_reference(dev, tmp_path, graph):
+    tr, ref = _trainer(dev, tmp_path, graph)
+    rep = tr.run(_Factory(TRAIN, dev), _Factory(VALID, dev))
+    _gate(rep, ref, f"run graph={graph}")
     files = sorted(p.name for p in tmp_path.iterdir())
     assert files == ref["files"], (files, ref["files"])
     links = {p.name: str(p.readlink()) for p in tmp_path.iterdir() if p.is_symlink()}
@@ -89,12 +109,7 @@ def test_trainer_run_resume(dev, tmp_path, graph):
     tr2, _ = _trainer(dev, tmp_path, graph)
     rep = tr2.run(_Factory(TRAIN, dev), _Factory(VALID, dev))
     assert rep.get_epoch() == 3
-    for e, per in ref["values"].items():
-        for ph, vals in per.items():
-            for k, v in vals.items():
-                got = rep.get_value(ph, k, epoch=int(e))
-                tol = 1e-9 if k.startswith("optim") else (2e-3 if k == "acc" else 2e-4 * max(1.0, abs(v)))
-                assert abs(got - v) <= tol, (e, ph, k, got, v)
+    _gate(rep, ref, f"resume graph={graph}")
     assert sorted(p.name for p in tmp_path.iterdir()) == ref["files"]
 
 
