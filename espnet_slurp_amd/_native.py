@@ -100,6 +100,8 @@ SIGNATURES = {
     "esp_col2im_relu": [P, P, P, I, I, I, I, P],
     "esp_conv1_wgrad": [P, P, P, P, I, I, I, I, P, L, P],
     "esp_permute3": [P, P, I, I, I, I, P],
+    "esp_im2col_nhwc": [P, P, I, I, I, I, I, I, P],
+    "esp_col2im_relu_nhwc": [P, P, P, I, I, I, I, I, I, P],
     "esp_log_softmax": [P, P, L, I, P],
     "esp_ctc_loss": [P, P, I, P, P, I, I, I, I, F, I, P, P, P, L, P],
     "esp_label_smoothing": [P, P, L, I, I, F, F, P, P, P, P],

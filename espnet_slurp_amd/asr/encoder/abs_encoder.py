@@ -31,14 +31,20 @@ class TooShortUttError(Exception):
         self.limit = limit
 
 
-def subsampled_lengths(ilens_cpu: torch.Tensor, T: int) -> torch.Tensor:
-    """Valid-frame counts of `mask[:, :, :-2:2][:, :, :-2:2]` (subsampling.py:87): frame i
-    survives the first stage iff i even, i < T-2, i < len; and so on.  Not the conv
-    output-size formula."""
+# second-stage (cut, stride) of the mask slicing per input_layer: conv2d `[:, :, :-2:2]` (subsampling.py:87),
+# conv2d6 `[:, :, :-4:3]` (subsampling.py:146); the first stage is `[:, :, :-2:2]` for both
+_MASK_STAGE2 = {"conv2d": (2, 2), "conv2d6": (4, 3)}
+
+
+def subsampled_lengths(ilens_cpu: torch.Tensor, T: int, input_layer: str = "conv2d") -> torch.Tensor:
+    """Valid-frame counts of `mask[:, :, :-2:2][:, :, :-c:s]` (subsampling.py:87 / :146): frame i
+    survives the first stage iff i even, i < T-2, i < len; the second iff j % s == 0, j < T1 - c,
+    j < len1.  Not the conv output-size formula."""
+    cut, st = _MASK_STAGE2[input_layer]
     lens = ilens_cpu.long().clamp(max=T)
     T1 = len(range(0, T - 2, 2))
     l1 = torch.clamp((lens + 1) // 2, max=T1)
-    l2 = torch.clamp((l1 + 1) // 2, max=len(range(0, T1 - 2, 2)))
+    l2 = torch.clamp((l1 + st - 1) // st, max=len(range(0, T1 - cut, st)))
     return l2
 
 

@@ -15,7 +15,7 @@ import torch
 from torch import nn
 
 from ... import kernels as K
-from ...blocks import (ConvolutionModule, Conv2dSubsampling, Ctx, LayerNorm, PositionwiseFeedForward,
+from ...blocks import (ConvolutionModule, Ctx, make_subsampling, LayerNorm, PositionwiseFeedForward,
                        RelPositionMultiHeadedAttention, Seeds, empty)
 from .abs_encoder import (AbsEncoder, EncoderFn, TooShortUttError, draw_seed, lengths_to_device, pos_table,
                           subsampled_lengths)
@@ -119,7 +119,7 @@ class ConformerEncoder(AbsEncoder):
         else:
             raise ValueError("unknown rel_pos_type: " + rel_pos_type)
         unsupported = []
-        if input_layer != "conv2d":
+        if input_layer not in ("conv2d", "conv2d6"):
             unsupported.append(f"input_layer={input_layer}")
         if not normalize_before or concat_after:
             unsupported.append("normalize_before=False/concat_after=True")
@@ -138,7 +138,7 @@ class ConformerEncoder(AbsEncoder):
         if unsupported:
             raise NotImplementedError("espnet_slurp_amd ConformerEncoder: unsupported " + ", ".join(unsupported))
         self.legacy = pos_enc_layer_type == "legacy_rel_pos"
-        self.embed = Conv2dSubsampling(input_size, output_size)
+        self.embed = make_subsampling(input_layer, input_size, output_size)
         self.encoders = nn.ModuleList([
             EncoderLayer(
                 output_size,
@@ -173,12 +173,13 @@ class ConformerEncoder(AbsEncoder):
         padding and BatchNorm statistics, and the legacy rel_shift is taken at T'; every other op
         is per frame or masked by klen)."""
         B, T, _ = feats.shape
-        if T < 7:
+        lim = self.embed.min_frames  # check_short_utt (subsampling.py:31-39)
+        if T < lim:
             raise TooShortUttError(
-                f"has {T} frames and is too short for subsampling (it needs more than 7 frames), return empty results",
-                T, 7)
+                f"has {T} frames and is too short for subsampling (it needs more than {lim} frames), return empty results",
+                T, lim)
         D = self._output_size
-        olens = subsampled_lengths(ilens_cpu, T)
+        olens = subsampled_lengths(ilens_cpu, T, self.embed.input_layer)
         if klen is None:
             klen = lengths_to_device(olens, feats.device)
         x, c_emb = self.embed.fwd(feats, math.sqrt(D), self.positional_dropout_rate, seeds, training)
@@ -217,7 +218,7 @@ class ConformerEncoder(AbsEncoder):
         assert self.flat is not None, "call espnet_slurp_amd.flatten_model(model) before running"
         ilens_cpu = ilens.detach().cpu()
         feats = xs_pad.contiguous().float()
-        olens = subsampled_lengths(ilens_cpu, feats.shape[1])
+        olens = subsampled_lengths(ilens_cpu, feats.shape[1], self.embed.input_layer)
         hs = self.forward_prepared(feats, ilens_cpu, lengths_to_device(olens, feats.device), draw_seed())
         return hs, K.h2d(olens, xs_pad.device), None
 
@@ -233,4 +234,4 @@ class ConformerEncoder(AbsEncoder):
 
     def output_lengths(self, ilens_cpu: torch.Tensor, T: int) -> torch.Tensor:
         """Valid output frames per utterance (host, no device round trip)."""
-        return subsampled_lengths(ilens_cpu, T)
+        return subsampled_lengths(ilens_cpu, T, self.embed.input_layer)

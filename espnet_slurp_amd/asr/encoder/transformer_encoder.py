@@ -11,7 +11,7 @@ import torch
 from torch import nn
 
 from ... import kernels as K
-from ...blocks import Conv2dSubsampling, Ctx, LayerNorm, MultiHeadedAttention, PositionwiseFeedForward, Seeds
+from ...blocks import Ctx, make_subsampling, LayerNorm, MultiHeadedAttention, PositionwiseFeedForward, Seeds
 from .abs_encoder import (AbsEncoder, EncoderFn, TooShortUttError, draw_seed, lengths_to_device, pos_table,
                           subsampled_lengths)
 
@@ -48,11 +48,11 @@ class TransformerEncoder(AbsEncoder):
                  positionwise_conv_kernel_size: int = 1, padding_idx: int = -1, interctc_layer_idx: List[int] = [],
                  interctc_use_conditioning: bool = False):
         super().__init__()
-        if input_layer != "conv2d" or not normalize_before or concat_after or positionwise_layer_type != "linear" \
+        if input_layer not in ("conv2d", "conv2d6") or not normalize_before or concat_after or positionwise_layer_type != "linear" \
                 or interctc_layer_idx or interctc_use_conditioning:
-            raise NotImplementedError("espnet_slurp_amd TransformerEncoder supports the conv2d/pre-LN/linear-FFN form")
+            raise NotImplementedError("espnet_slurp_amd TransformerEncoder supports the conv2d / conv2d6, pre-LN, linear-FFN form")
         self._output_size = output_size
-        self.embed = Conv2dSubsampling(input_size, output_size)
+        self.embed = make_subsampling(input_layer, input_size, output_size)
         self.encoders = nn.ModuleList([
             TransformerEncoderLayer(output_size,
                                     MultiHeadedAttention(attention_heads, output_size, attention_dropout_rate),
@@ -73,10 +73,11 @@ class TransformerEncoder(AbsEncoder):
     def run_forward(self, feats, ilens_cpu, seeds: Seeds, training: bool, klen=None, tvalid=None):
         # tvalid (length buckets) needs no handling here: every op is per frame or masked by klen
         B, T, _ = feats.shape
-        if T < 7:
-            raise TooShortUttError(f"has {T} frames and is too short for subsampling", T, 7)
+        lim = self.embed.min_frames  # check_short_utt (subsampling.py:31-39)
+        if T < lim:
+            raise TooShortUttError(f"has {T} frames and is too short for subsampling", T, lim)
         D = self._output_size
-        olens = subsampled_lengths(ilens_cpu, T)
+        olens = subsampled_lengths(ilens_cpu, T, self.embed.input_layer)
         if klen is None:
             klen = lengths_to_device(olens, feats.device)
         # embed: linear -> x*sqrt(D) + pe -> dropout.  The linear's epilogue gives x*sqrt(D);
@@ -121,7 +122,7 @@ class TransformerEncoder(AbsEncoder):
         assert self.flat is not None, "call espnet_slurp_amd.flatten_model(model) before running"
         ilens_cpu = ilens.detach().cpu()
         feats = xs_pad.contiguous().float()
-        olens = subsampled_lengths(ilens_cpu, feats.shape[1])
+        olens = subsampled_lengths(ilens_cpu, feats.shape[1], self.embed.input_layer)
         hs = self.forward_prepared(feats, ilens_cpu, lengths_to_device(olens, feats.device), draw_seed())
         return hs, K.h2d(olens, xs_pad.device), None
 
@@ -137,4 +138,4 @@ class TransformerEncoder(AbsEncoder):
 
     def output_lengths(self, ilens_cpu: torch.Tensor, T: int) -> torch.Tensor:
         """Valid output frames per utterance (host, no device round trip)."""
-        return subsampled_lengths(ilens_cpu, T)
+        return subsampled_lengths(ilens_cpu, T, self.embed.input_layer)

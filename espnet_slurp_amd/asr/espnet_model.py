@@ -245,7 +245,7 @@ class ESPnetASRModel(AbsESPnetModel):
                 n_samples = self.frontend.samples_for_frames(T)
                 assert n_samples <= T_in, (n_samples, T_in)
             # valid frames after Conv2dSubsampling of the batch's own padded length
-            host["tvalid"] = torch.tensor([((T_true - 1) // 2 - 1) // 2], dtype=torch.int32)
+            host["tvalid"] = torch.tensor([self.encoder.embed.out_frames(T_true)], dtype=torch.int32)
         if u_bucket is not None and u_bucket > text_cpu.shape[1]:
             pad = torch.full((B, int(u_bucket) - text_cpu.shape[1]), self.ignore_id, dtype=text_cpu.dtype)
             text_cpu = torch.cat([text_cpu, pad], 1)

@@ -559,12 +559,22 @@ class ConvolutionModule(nn.Module):
 class Conv2dSubsampling(nn.Module):
     """subsampling.py:42-87 in NHWC; returns x*sqrt(D) (+ dropout), before the rel-pos table."""
 
+    input_layer = "conv2d"
+    k2, s2 = 3, 2  # the second convolution's kernel / stride
+    min_frames = 7  # check_short_utt (subsampling.py:31-39)
+
     def __init__(self, idim: int, odim: int):
         super().__init__()
-        self.conv = nn.Sequential(nn.Conv2d(1, odim, 3, 2), nn.ReLU(), nn.Conv2d(odim, odim, 3, 2), nn.ReLU())
-        self.f2 = ((idim - 1) // 2 - 1) // 2
+        self.conv = nn.Sequential(nn.Conv2d(1, odim, 3, 2), nn.ReLU(), nn.Conv2d(odim, odim, self.k2, self.s2),
+                                  nn.ReLU())
+        self.f2 = self.out_frames(idim)
         self.out = nn.Sequential(Linear(odim * self.f2, odim))
         self.odim = odim
+
+    @classmethod
+    def out_frames(cls, T: int) -> int:
+        """Output length of the two convolutions for T input frames (or bins)."""
+        return ((T - 3) // 2 + 1 - cls.k2) // cls.s2 + 1
 
     def fwd(self, feats, xscale, p_drop, seeds: Seeds, training: bool):
         B, T, F = feats.shape
@@ -647,3 +657,82 @@ class Conv2dSubsampling(nn.Module):
             K.col2im_relu(dcol, c.z1, dz1, B, T1, F1, D)
             del dcol
         K.conv1_wgrad(c.feats, dz1, c0.weight.grad.view(D, 9), c0.bias.grad, B, c.T, c.F, D)
+
+
+class Conv2dSubsampling6(Conv2dSubsampling):
+    """input_layer "conv2d6" (subsampling.py:101-146): Conv2d(1, D, 3, 2) + ReLU, Conv2d(D, D, 5, 3) + ReLU,
+    Linear(D * F2, D), F2 = ((idim - 1) // 2 - 2) // 3.  conv1 and the output Linear are the conv2d kernels;
+    the 5 x 5 / stride 3 convolution runs on explicit NHWC columns (esp_im2col_nhwc: 25 D per output pixel,
+    kept for the weight gradient) as one KC x KC GEMM with the bias + ReLU epilogue, its weight gradient an
+    RC x RC GEMM with the fused bias gradient, its input gradient a KC x RC GEMM into columns and the
+    ReLU-masked column adjoint (esp_col2im_relu_nhwc).  The LibriSpeech-960 Conformer recipe
+    (egs2/librispeech/asr1/conf/tuning/train_asr_conformer.yaml) uses it; the SLURP recipe does not, so this
+    is not the bench path."""
+
+    input_layer = "conv2d6"
+    k2, s2 = 5, 3
+    min_frames = 11
+
+    def fwd(self, feats, xscale, p_drop, seeds: Seeds, training: bool):
+        B, T, F = feats.shape
+        D = self.odim
+        k, st = self.k2, self.s2
+        T1, F1 = (T - 3) // 2 + 1, (F - 3) // 2 + 1
+        T2, F2 = (T1 - k) // st + 1, (F1 - k) // st + 1
+        c0, c2 = self.conv[0], self.conv[2]
+        z1 = empty(B * T1 * F1 * D, like=feats)
+        K.conv1_fwd(feats, c0.weight, c0.bias, z1, B, T, F, D)
+        npix2, KK = B * T2 * F2, k * k * D
+        col = empty(npix2, KK, like=feats)
+        K.im2col_nhwc(z1, col, B, T1, F1, D, k, st)
+        w2r = empty(D * k * k * D, like=feats)
+        K.permute3(c2.weight, w2r, D, D, k * k)  # (o, c, kt, kf) -> (o, kt, kf, c)
+        z2 = empty(npix2, D, like=feats)
+        K.gemm(npix2, D, KK, col, w2r, z2, mode_a=K.KC, lda=KK, mode_b=K.KC, ldb=KK, ldc=D, bias=c2.bias,
+               act=K.ACT_RELU, b_weight=True)
+        lin = self.out[0]
+        wor = empty(D * F2 * D, like=feats)
+        K.permute3(lin.weight, wor, D, D, F2)  # (n, c, f) -> (n, f, c)
+        x = empty(B * T2, D, like=feats)
+        pd = p_drop if training else 0.0
+        sd = seeds.next()
+        K.linear_fwd(z2.view(B * T2, F2 * D), wor.view(D, F2 * D), lin.bias, x, alpha=xscale, drop_p=pd, seed=sd,
+                     b_weight=True)
+        return x, Ctx(feats=feats, z1=z1, col=col if training else None, w2r=w2r, z2=z2, wor=wor, pd=pd, sd=sd,
+                      xscale=xscale, B=B, T=T, F=F, T1=T1, F1=F1, T2=T2, F2=F2)
+
+    def bwd(self, c, dx):
+        D = self.odim
+        k, st = self.k2, self.s2
+        B, T2, F2, T1, F1 = c.B, c.T2, c.F2, c.T1, c.F1
+        c0, c2 = self.conv[0], self.conv[2]
+        lin = self.out[0]
+        dv = torch.empty_like(dx)
+        K.scale_dropout(dx, dv, alpha=c.xscale, drop_p=c.pd, seed=c.sd)
+        dwor = torch.zeros(D * F2 * D, dtype=torch.float32, device=dx.device)
+        z2f = c.z2.view(B * T2, F2 * D)
+        K.linear_bwd_weight(dv, z2f, dwor.view(D, F2 * D), lin.bias.grad)
+        K.permute3(dwor, lin.weight.grad, D, F2, D, accumulate=True)  # (n, f, c) -> (n, c, f)
+        npix2, KK = B * T2 * F2, k * k * D
+        dz2 = empty(B * T2, F2 * D, like=dx)
+        K.linear_bwd_data_act(dv, c.wor.view(D, F2 * D), dz2, z2f, K.ACT_RELU, b_weight=True)  # ReLU' from its output
+        dz2p = dz2.view(npix2, D)
+        dw2r = empty(D, KK, like=dx)
+        K.gemm(D, KK, npix2, dz2p, c.col, dw2r, mode_a=K.RC, lda=D, mode_b=K.RC, ldb=KK, ldc=KK,
+               rowsum=c2.bias.grad)
+        K.permute3(dw2r, c2.weight.grad, D, k * k, D, accumulate=True)  # (o, kk, c) -> (o, c, kk)
+        c.col = None
+        dcol = empty(npix2, KK, like=dx)
+        K.gemm(npix2, KK, D, dz2p, c.w2r, dcol, mode_a=K.KC, lda=D, mode_b=K.RC, ldb=KK, ldc=KK, b_weight=True)
+        dz1 = empty(B * T1 * F1 * D, like=dx)
+        K.col2im_relu_nhwc(dcol, c.z1, dz1, B, T1, F1, D, k, st)
+        del dcol
+        K.conv1_wgrad(c.feats, dz1, c0.weight.grad.view(D, 9), c0.bias.grad, B, c.T, c.F, D)
+
+
+def make_subsampling(input_layer: str, idim: int, odim: int) -> Conv2dSubsampling:
+    """The encoders' input_layer choice (conformer_encoder.py:173-222 / transformer_encoder.py:97-140)."""
+    cls = {"conv2d": Conv2dSubsampling, "conv2d6": Conv2dSubsampling6}.get(input_layer)
+    if cls is None:
+        raise NotImplementedError(f"input_layer={input_layer}: conv2d and conv2d6 are built")
+    return cls(idim, odim)

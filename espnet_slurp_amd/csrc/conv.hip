@@ -122,6 +122,71 @@ __global__ void col2im_relu_kernel(const float* __restrict__ dcol, const float* 
   }
 }
 
+// Conv2dSubsampling6's second convolution (Conv2d(D, D, 5, 3), subsampling.py:101-146) on explicit columns:
+// generic (k, s) NHWC im2col and its ReLU-masked col2im gather.  Column layout (kt, kf, c): row p =
+// (b, t2, f2) holds x[b, s t2 + kt, s f2 + kf, c] at (kt k + kf) C + c -- the (o, kt, kf, c) weight image
+// (esp_permute3) makes the convolution one KC x KC GEMM.  float4 over C, one thread per (pixel, tap, c4).
+__global__ void im2col_nhwc_kernel(const float* __restrict__ x, float* __restrict__ col, int B, int T1, int F1,
+                                   int C, int T2, int F2, int k, int s) {
+  const int C4 = C / 4, KK = k * k;
+  const long n = (long)B * T2 * F2 * KK * C4;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c4 = (int)(i % C4);
+    long q = i / C4;
+    const int tap = (int)(q % KK);
+    const long p = q / KK;
+    const int f2 = (int)(p % F2);
+    const long r = p / F2;
+    const int t2 = (int)(r % T2);
+    const int b = (int)(r / T2);
+    const int kt = tap / k, kf = tap - kt * k;
+    const float4 v = *reinterpret_cast<const float4*>(
+        x + (((long)b * T1 + s * t2 + kt) * F1 + s * f2 + kf) * C + c4 * 4);
+    *reinterpret_cast<float4*>(col + p * ((long)KK * C) + (long)tap * C + c4 * 4) = v;
+  }
+}
+
+// dx[b,t1,f1,c] = (z>0) * sum over the taps (kt, kf) that reach (t1, f1) -- (t1 - kt) % s == 0 and
+// (t1 - kt) / s < T2, likewise f -- of dcol[(b,t2,f2)][(kt k + kf) C + c], kt and kf ascending
+__global__ void col2im_relu_nhwc_kernel(const float* __restrict__ dcol, const float* __restrict__ z,
+                                        float* __restrict__ dx, int B, int T1, int F1, int C, int T2, int F2, int k,
+                                        int s) {
+  const int C4 = C / 4;
+  const long n = (long)B * T1 * F1 * C4;
+  const long rowc = (long)k * k * C;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c4 = (int)(i % C4);
+    long p = i / C4;
+    const int f1 = (int)(p % F1);
+    p /= F1;
+    const int t1 = (int)(p % T1);
+    const int b = (int)(p / T1);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int kt = 0; kt < k; ++kt) {
+      const int tt = t1 - kt;
+      if (tt < 0 || tt % s) continue;
+      const int t2 = tt / s;
+      if (t2 >= T2) continue;
+      for (int kf = 0; kf < k; ++kf) {
+        const int ff = f1 - kf;
+        if (ff < 0 || ff % s) continue;
+        const int f2 = ff / s;
+        if (f2 >= F2) continue;
+        const float4 v = *reinterpret_cast<const float4*>(
+            dcol + (((long)b * T2 + t2) * F2 + f2) * rowc + (long)(kt * k + kf) * C + c4 * 4);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+      }
+    }
+    const long o = (((long)b * T1 + t1) * F1 + f1) * C + c4 * 4;
+    const float4 zz = *reinterpret_cast<const float4*>(z + o);
+    acc.x = zz.x > 0.f ? acc.x : 0.f;
+    acc.y = zz.y > 0.f ? acc.y : 0.f;
+    acc.z = zz.z > 0.f ? acc.z : 0.f;
+    acc.w = zz.w > 0.f ? acc.w : 0.f;
+    *reinterpret_cast<float4*>(dx + o) = acc;
+  }
+}
+
 // conv1 weight/bias gradient partials: block = chunk of pixels, thread = channel; the 9-tap
 // patches of a sub-chunk are staged in LDS (3 x float4 per pixel, broadcast reads), the dz rows
 // are read 4 pixels ahead.  Partials are stored output-major part[(o*10+k)*nb + block] so the
@@ -242,6 +307,31 @@ static int conv1_fwd_impl(const float* x, const float* W, const float* bias, flo
     hipLaunchKernelGGL(conv1_fwd_kernel<false>, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, x, W, bias, z,
                        nullptr, B, T, F, T1, F1, D, chunk);
   ESP_CHECK_LAUNCH("esp_conv1_fwd");
+  return 0;
+}
+
+ESP_API int esp_im2col_nhwc(const float* x, float* col, int B, int T1, int F1, int C, int k, int s, void* stream) {
+  ESP_ARG_CHECK(C % 4 == 0 && k >= 1 && s >= 1 && T1 >= k && F1 >= k && B >= 0,
+                "esp_im2col_nhwc: bad shape B=%d T1=%d F1=%d C=%d k=%d s=%d", B, T1, F1, C, k, s);
+  const int T2 = (T1 - k) / s + 1, F2 = (F1 - k) / s + 1;
+  const long n = (long)B * T2 * F2 * k * k * (C / 4);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(im2col_nhwc_kernel, dim3(gridn(n)), dim3(256), 0, (hipStream_t)stream, x, col, B, T1, F1, C, T2,
+                     F2, k, s);
+  ESP_CHECK_LAUNCH("esp_im2col_nhwc");
+  return 0;
+}
+
+ESP_API int esp_col2im_relu_nhwc(const float* dcol, const float* z, float* dx, int B, int T1, int F1, int C, int k,
+                                 int s, void* stream) {
+  ESP_ARG_CHECK(C % 4 == 0 && k >= 1 && s >= 1 && T1 >= k && F1 >= k && B >= 0,
+                "esp_col2im_relu_nhwc: bad shape B=%d T1=%d F1=%d C=%d k=%d s=%d", B, T1, F1, C, k, s);
+  const int T2 = (T1 - k) / s + 1, F2 = (F1 - k) / s + 1;
+  const long n = (long)B * T1 * F1 * (C / 4);
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(col2im_relu_nhwc_kernel, dim3(gridn(n)), dim3(256), 0, (hipStream_t)stream, dcol, z, dx, B, T1,
+                     F1, C, T2, F2, k, s);
+  ESP_CHECK_LAUNCH("esp_col2im_relu_nhwc");
   return 0;
 }
 

@@ -1234,6 +1234,18 @@ def col2im_relu(dcol, z1, dz1, B, T1, F1, D):
     _native.call("esp_col2im_relu", _p(dcol), _p(z1), _p(dz1), B, T1, F1, D, _st())
 
 
+def im2col_nhwc(x, col, B, T1, F1, C, k, s):
+    """NHWC [B, T1, F1, C] -> columns [B*T2*F2, k*k*C], (kt, kf, c) per row (esp_im2col_nhwc)."""
+    _f32(x, col)
+    _native.call("esp_im2col_nhwc", _p(x), _p(col), B, T1, F1, C, k, s, _st())
+
+
+def col2im_relu_nhwc(dcol, z, dx, B, T1, F1, C, k, s):
+    """dx = relu'(z) * the adjoint of im2col_nhwc applied to dcol (esp_col2im_relu_nhwc)."""
+    _f32(dcol, z, dx)
+    _native.call("esp_col2im_relu_nhwc", _p(dcol), _p(z), _p(dx), B, T1, F1, C, k, s, _st())
+
+
 def conv1_wgrad(x, dz1, dW, db, B, T, F, D):
     n = _wsize("esp_conv1_wgrad", B, T, F, D)
     ws = _ws(WS, "esp_conv1_wgrad", n, x.device)

@@ -408,6 +408,14 @@ int esp_col2im_relu(const float* dcol, const float* z1, float* dz1, int B, int T
                     void* stream);
 int esp_conv1_wgrad(const float* x, const float* dz1, float* dW, float* db, int B, int T, int F,
                     int D, float* work, long work_bytes, void* stream);
+/* ABI 31: input_layer "conv2d6" (espnet/nets/pytorch_backend/transformer/subsampling.py:101-146
+ * Conv2dSubsampling6: its second Conv2d(D, D, 5, 3)) on explicit columns.  NHWC x [B, T1, F1, C] ->
+ * col [B*T2*F2, k*k*C] with row p = (b, t2, f2), column (kt*k + kf)*C + c, T2 = (T1-k)/s + 1,
+ * F2 = (F1-k)/s + 1 (a KC x KC GEMM with the (o, kt, kf, c) weight is then the convolution);
+ * col2im_relu_nhwc: dx = relu'(z) * the column adjoint (taps summed kt, kf ascending).  C % 4 == 0. */
+int esp_im2col_nhwc(const float* x, float* col, int B, int T1, int F1, int C, int k, int s, void* stream);
+int esp_col2im_relu_nhwc(const float* dcol, const float* z, float* dx, int B, int T1, int F1, int C, int k,
+                         int s, void* stream);
 int esp_permute3(const float* in, float* out, int O, int Bd, int Ad, int accumulate, void* stream);
 
 /* ---- losses (ctc.py:39-97, label_smoothing_loss.py:41-63, nets_utils.py:299-320,

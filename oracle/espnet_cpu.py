@@ -42,6 +42,7 @@ class EncCfg:
     use_cnn_module: bool = True
     cnn_module_kernel: int = 31
     max_pos_emb_len: int = 5000
+    input_layer: str = "conv2d"      # conv2d | conv2d6 (Conv2dSubsampling6, subsampling.py:101-146)
 
 
 @dataclass
@@ -90,10 +91,11 @@ def subsequent_mask(n: int) -> torch.Tensor:
     return torch.tril(torch.ones(n, n, dtype=torch.bool))
 
 
-def subsampled_lengths(lengths: torch.Tensor, T: int) -> torch.Tensor:
-    """Length of `mask[:, :, :-2:2][:, :, :-2:2]` (subsampling.py:87) as counts."""
+def subsampled_lengths(lengths: torch.Tensor, T: int, input_layer: str = "conv2d") -> torch.Tensor:
+    """Length of `mask[:, :, :-2:2][:, :, :-2:2]` (subsampling.py:87; conv2d6: `[:, :, :-2:2][:, :, :-4:3]`,
+    :146) as counts."""
     m = ~make_pad_mask(lengths, T)
-    m = m[:, :-2:2][:, :-2:2]
+    m = m[:, :-2:2][:, :-2:2] if input_layer == "conv2d" else m[:, :-2:2][:, :-4:3]
     return m.sum(1)
 
 
@@ -152,14 +154,18 @@ def dropout(x, p: float, training: bool = True):
     return F.dropout(x, p, training) if (p > 0 and training) else x
 
 
-def conv2d_subsampling(P: Params, pre: str, x, mask):
-    """Conv2dSubsampling.forward, subsampling.py:53-87 (returns pre-pos-enc features)."""
+def conv2d_subsampling(P: Params, pre: str, x, mask, input_layer: str = "conv2d"):
+    """Conv2dSubsampling.forward, subsampling.py:53-87 (returns pre-pos-enc features); input_layer
+    "conv2d6": Conv2dSubsampling6.forward, subsampling.py:101-146 (second conv 5 x 5, stride 3)."""
     x = x.unsqueeze(1)
     x = F.relu(F.conv2d(x, P[pre + ".conv.0.weight"], P[pre + ".conv.0.bias"], stride=2))
-    x = F.relu(F.conv2d(x, P[pre + ".conv.2.weight"], P[pre + ".conv.2.bias"], stride=2))
+    s2 = 2 if input_layer == "conv2d" else 3
+    x = F.relu(F.conv2d(x, P[pre + ".conv.2.weight"], P[pre + ".conv.2.bias"], stride=s2))
     b, c, t, f = x.size()
     x = linear(P, pre + ".out.0", x.transpose(1, 2).contiguous().view(b, t, c * f))
-    return x, mask[:, :, :-2:2][:, :, :-2:2]
+    if input_layer == "conv2d":
+        return x, mask[:, :, :-2:2][:, :, :-2:2]
+    return x, mask[:, :, :-2:2][:, :, :-4:3]
 
 
 def rel_shift_latest(x):
@@ -283,10 +289,11 @@ def transformer_enc_layer(P, pre, x, mask, cfg: EncCfg, training=True):
 def encoder(P, feats, lens, cfg: EncCfg, bn_state=None, training=True):
     """ConformerEncoder.forward (conformer_encoder.py:292-368) / TransformerEncoder.forward."""
     T = feats.size(1)
-    if T < 7:
-        raise ValueError("TooShortUttError: needs more than 7 frames")
+    lim = 7 if cfg.input_layer == "conv2d" else 11  # check_short_utt, subsampling.py:31-39
+    if T < lim:
+        raise ValueError(f"TooShortUttError: needs more than {lim} frames")
     masks = (~make_pad_mask(lens, T))[:, None, :]
-    x, masks = conv2d_subsampling(P, "encoder.embed", feats, masks)
+    x, masks = conv2d_subsampling(P, "encoder.embed", feats, masks, cfg.input_layer)
     Tp = x.size(1)
     D = cfg.output_size
     if cfg.kind == "conformer":
@@ -463,7 +470,7 @@ def param_shapes(cfg: ModelCfg) -> Dict[str, Tuple[int, ...]]:
     """state_dict keys/shapes of the reference model, trainable + BN buffers."""
     e, V = cfg.enc, cfg.vocab_size
     D, FF, H = e.output_size, e.linear_units, e.attention_heads
-    F2 = ((e.input_size - 1) // 2 - 1) // 2
+    F2 = ((e.input_size - 1) // 2 - 1) // 2 if e.input_layer == "conv2d" else ((e.input_size - 1) // 2 - 2) // 3
     s: Dict[str, Tuple[int, ...]] = {}
 
     def lin(pre, i, o, bias=True):
@@ -477,7 +484,8 @@ def param_shapes(cfg: ModelCfg) -> Dict[str, Tuple[int, ...]]:
 
     s["encoder.embed.conv.0.weight"] = (D, 1, 3, 3)
     s["encoder.embed.conv.0.bias"] = (D,)
-    s["encoder.embed.conv.2.weight"] = (D, D, 3, 3)
+    k2 = 3 if e.input_layer == "conv2d" else 5
+    s["encoder.embed.conv.2.weight"] = (D, D, k2, k2)
     s["encoder.embed.conv.2.bias"] = (D,)
     lin("encoder.embed.out.0", D * F2, D)
     for i in range(e.num_blocks):

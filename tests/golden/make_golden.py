@@ -54,7 +54,7 @@ def build_reference(cfg: O.ModelCfg):
             input_size=e.input_size, output_size=e.output_size, attention_heads=e.attention_heads,
             linear_units=e.linear_units, num_blocks=e.num_blocks, dropout_rate=e.dropout_rate,
             positional_dropout_rate=e.positional_dropout_rate,
-            attention_dropout_rate=e.attention_dropout_rate, input_layer="conv2d",
+            attention_dropout_rate=e.attention_dropout_rate, input_layer=e.input_layer,
             normalize_before=True, macaron_style=e.macaron_style, rel_pos_type=e.rel_pos_type,
             pos_enc_layer_type="rel_pos", selfattention_layer_type="rel_selfattn",
             activation_type="swish", use_cnn_module=e.use_cnn_module,
@@ -845,6 +845,10 @@ if __name__ == "__main__":
     if "small" in which:
         model_fixture("model_small_latest", small_cfg("latest"), 3, 120, [120, 97, 64], [9, 5, 7], 1)
         model_fixture("model_small_legacy", small_cfg("legacy"), 3, 120, [120, 97, 64], [9, 5, 7], 2)
+    if "conv2d6" in which:  # input_layer conv2d6 (Conv2dSubsampling6, the LibriSpeech Conformer recipe's)
+        cfg = small_cfg("latest")
+        cfg.enc.input_layer = "conv2d6"
+        model_fixture("model_small_conv2d6", cfg, 3, 120, [120, 97, 64], [9, 5, 7], 6)
     if "lnorm" in which:  # length_normalized_loss=True (LabelSmoothingLoss normalize_length)
         cfg = small_cfg("latest")
         cfg.length_normalized_loss = True

@@ -50,11 +50,11 @@ def build_model(cfg: O.ModelCfg, device, specaug=None, dropout=None, frontend=No
                                linear_units=e.linear_units, num_blocks=e.num_blocks, dropout_rate=p,
                                positional_dropout_rate=p, attention_dropout_rate=p, macaron_style=e.macaron_style,
                                rel_pos_type=e.rel_pos_type, use_cnn_module=e.use_cnn_module,
-                               cnn_module_kernel=e.cnn_module_kernel)
+                               cnn_module_kernel=e.cnn_module_kernel, input_layer=e.input_layer)
     else:
         enc = TransformerEncoder(input_size=e.input_size, output_size=e.output_size, attention_heads=e.attention_heads,
                                  linear_units=e.linear_units, num_blocks=e.num_blocks, dropout_rate=p,
-                                 positional_dropout_rate=p, attention_dropout_rate=p)
+                                 positional_dropout_rate=p, attention_dropout_rate=p, input_layer=e.input_layer)
     dec = None
     if cfg.dec is not None and cfg.ctc_weight != 1.0:
         d = cfg.dec

@@ -242,6 +242,13 @@ def test_subsampled_lengths_and_sos_eos():
         lens = lens[lens <= T]
         ref = O.subsampled_lengths(lens, T)
         assert torch.equal(subsampled_lengths(lens, T), ref), T
+    for T in (11, 12, 13, 17, 64, 120, 1499, 1500):  # conv2d6: mask[:, :, :-2:2][:, :, :-4:3]
+        lens = torch.tensor(sorted({T, max(1, T - 1), max(1, T // 2), 11, 7, 1, 2, 3, 5}))
+        lens = lens[lens <= T]
+        ref = O.subsampled_lengths(lens, T, "conv2d6")
+        assert torch.equal(subsampled_lengths(lens, T, "conv2d6"), ref), T
+        from espnet_slurp_amd.blocks import Conv2dSubsampling6
+        assert Conv2dSubsampling6.out_frames(T) == int(ref.max()), T  # lens holds T: the full length
     ys = torch.tensor([[5, 6, 7, -1], [8, -1, -1, -1], [1, 2, 3, 4]])
     yi, yo, yl = add_sos_eos(ys, torch.tensor([3, 1, 4]), 9, 9, -1)
     ri, ro = O.add_sos_eos(ys, 9, 9, -1)
