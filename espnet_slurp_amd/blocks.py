@@ -282,7 +282,7 @@ class RelPositionMultiHeadedAttention(nn.Module):
         fused = not self.legacy and K.relpos_fused_ok(T, dk) and K.FUSED_ATTN_BWD
         dscores = not fused and K.ATTN_DSCORES and c.tvalid is None  # (legacy + length bucket: the row-wise pass)
         # latest rel_shift, row-wise adjoint: dbd in the kept zeroed buffer, only its band written
-        band = None if (self.legacy or fused or dscores or Tp % 4) else K.relpos_band_buffer(Z, T, Pp, dout.device)
+        band = None if (self.legacy or fused or dscores or Tp % 4 or T > 1024) else K.relpos_band_buffer(Z, T, Pp, dout.device)
         dbd = band if band is not None else empty(Z * T * Pp, like=dout)
         if dscores:
             # dS = P (drop'(dP) - dot) / sqrt(dk) and its rel_shift adjoint in the dP GEMM's epilogue,

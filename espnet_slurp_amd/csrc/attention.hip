@@ -269,6 +269,117 @@ __global__ __launch_bounds__(256) void softmax_bwd_relpos_kernel(const float* __
   }
 }
 
+// Rows longer than the register-resident kernels hold (Tk > 1024: utterances past ~41 s at 40 ms frames):
+// the same arithmetic in passes over the row -- max, sum of exp(s - max), then the normalised write --
+// with the score (ac + the rel_shift of bd, masks) recomputed from HBM on each pass, so the values equal
+// softmax_fwd_kernel's (same expf arguments, same wave reductions; only the summation grouping per lane
+// differs).  One wave per row, any length.
+__device__ __forceinline__ float softmax_score(const float* acr, const float* bdz, int relpos, int i, int j, int Tq,
+                                               int Ts, long ldp, int kl, int causal, float sqrt_dk) {
+  if (j >= kl || (causal && j > i)) return -INFINITY;
+  float a = acr[j];
+  if (relpos == 1) {
+    a += bdz[(long)i * ldp + (j + Tq - 1 - i)];
+  } else if (relpos == 2 && i < Ts) {
+    if (j <= i) a += bdz[(long)i * ldp + (j + Ts - 1 - i)];
+    else if (j > i + 1) a += bdz[(long)(i + 1) * ldp + (j - i - 2)];
+  }
+  return a / sqrt_dk;
+}
+__global__ __launch_bounds__(256) void softmax_fwd_loop_kernel(const float* ac, const float* __restrict__ bd,
+                                                               int relpos, int P, float sqrt_dk,
+                                                               const int* __restrict__ klen, int nb, int causal,
+                                                               float* attn, float* __restrict__ pdrop, uint32_t thr,
+                                                               float dscale, uint64_t seed, int Z, int Tq, int Tk,
+                                                               long lds, long ldp, const uint64_t* __restrict__ key,
+                                                               const int* __restrict__ tvalid) {
+  seed = esp::keyed(seed, key);
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (long)Z * Tq) return;
+  const int i = (int)(row % Tq);
+  const int Ts = relpos == 2 && tvalid ? min(max(*tvalid, 1), Tq) : Tq;
+  const int z = (int)(row / Tq);
+  const int b = z % nb;
+  int kl = klen ? klen[b] : Tk;
+  if (kl > Tk) kl = Tk;
+  const float* acr = ac + row * lds;
+  const float* bdz = bd ? bd + (long)z * Tq * ldp : nullptr;
+  float mx = -INFINITY;
+  for (int j = lane; j < Tk; j += 64) mx = fmaxf(mx, softmax_score(acr, bdz, relpos, i, j, Tq, Ts, ldp, kl, causal, sqrt_dk));
+  mx = esp::wave_max(mx);
+  float sum = 0.f;
+  for (int j = lane; j < Tk; j += 64) {
+    const float v = softmax_score(acr, bdz, relpos, i, j, Tq, Ts, ldp, kl, causal, sqrt_dk);
+    sum += v == -INFINITY ? 0.f : expf(v - mx);
+  }
+  sum = esp::wave_sum(sum);
+  const float inv = sum > 0.f ? 1.0f / sum : 0.f;
+  float* ar = attn + row * lds;
+  float* pr = pdrop ? pdrop + row * lds : nullptr;
+  for (int j = lane; j < Tk; j += 64) {
+    const float v = softmax_score(acr, bdz, relpos, i, j, Tq, Ts, ldp, kl, causal, sqrt_dk);
+    const float p = (v == -INFINITY ? 0.f : expf(v - mx)) * inv;
+    ar[j] = p;  // (ac may alias attn: element j was read above by this lane only)
+    if (pr) pr[j] = esp::keep_elem(seed, (uint64_t)(row * Tk + j), thr) ? p * dscale : 0.f;
+  }
+}
+
+// softmax backward (REL 0), + the latest (1) / legacy (2) rel_shift adjoint, for rows of any length: the
+// dot pass, then the dS (and dbd) pass -- softmax_bwd_kernel / softmax_bwd_relpos_kernel's arithmetic
+template <int REL>
+__global__ __launch_bounds__(256) void softmax_bwd_loop_kernel(const float* __restrict__ attn, const float* dP,
+                                                               float* dS, float* __restrict__ dbd, long ldp,
+                                                               uint32_t thr, float dscale, uint64_t seed,
+                                                               float sqrt_dk, long rows, int T, long lds,
+                                                               const uint64_t* __restrict__ key,
+                                                               const int* __restrict__ tvalid) {
+  seed = esp::keyed(seed, key);
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* ar = attn + row * lds;
+  const float* gr = dP + row * lds;
+  auto gval = [&](int j) {
+    float gv = gr[j];
+    if (thr) gv = esp::keep_elem(seed, (uint64_t)(row * T + j), thr) ? gv * dscale : 0.f;
+    return gv;
+  };
+  float dot = 0.f;
+  for (int j = lane; j < T; j += 64) dot += ar[j] * gval(j);
+  dot = esp::wave_sum(dot);
+  float* sr = dS + row * lds;
+  if constexpr (REL == 0) {
+    for (int j = lane; j < T; j += 64) sr[j] = ar[j] * (gval(j) - dot) / sqrt_dk;
+    return;
+  } else {
+    const int i = (int)(row % T);
+    float* br = dbd + row * ldp;
+    const int Ts = REL == 2 ? legacy_tv(tvalid, T) : T;
+    const bool live = REL == 1 || i < Ts;
+    const int sh = Ts - 1 - i;
+    for (int j = lane; j < T; j += 64) {
+      const float v = ar[j] * (gval(j) - dot) / sqrt_dk;
+      sr[j] = v;
+      if (!live) continue;
+      if (REL == 1 || j <= i) br[j + sh] = v;
+      else if (j >= i + 2 && j < Ts) br[ldp + j - i - 2] = v;
+    }
+    if (REL == 1) {
+      for (int k = lane; k < sh; k += 64) br[k] = 0.f;
+      for (int k = sh + T + lane; k < 2 * T - 1; k += 64) br[k] = 0.f;
+    } else {
+      if (!live) {
+        for (int k = lane; k < T; k += 64) br[k] = 0.f;
+      } else {
+        if (i == 0)
+          for (int k = lane; k < sh; k += 64) br[k] = 0.f;
+        for (int k = Ts + lane; k < T; k += 64) br[k] = 0.f;
+      }
+    }
+  }
+}
+
 // float4 form of softmax_bwd_relpos_kernel (lds % 4 == 0, 16-B aligned rows): lane L loads the
 // quads 4L + 256q of P and dP (1 KB per wave instruction instead of 256 B), writes dS as float4
 // (the pitch's padding columns get 0), and hands its 4 values through a per-wave LDS row so the
@@ -1455,7 +1566,7 @@ ESP_API int esp_add2d(const float* x, long ldx, float* y, long ldy, int M, int N
 ESP_API int esp_attn_softmax_fwd(const float* ac, const float* bd, int relpos, int P, float sqrt_dk, const int* klen,
                                  int nb, int causal, float* attn, float* pdrop, float drop_p, unsigned long long seed,
                                  int Z, int Tq, int Tk, long lds, long ldp, const int* tvalid, void* stream) {
-  ESP_ARG_CHECK(Tk <= 1024, "esp_attn_softmax_fwd: Tk=%d > 1024", Tk);
+  ESP_ARG_CHECK(Tk >= 1, "esp_attn_softmax_fwd: Tk=%d", Tk);
   ESP_ARG_CHECK(relpos == 0 || (Tq == Tk && bd), "esp_attn_softmax_fwd: rel-pos needs Tq==Tk and bd");
   ESP_ARG_CHECK(relpos != 1 || P == 2 * Tq - 1, "esp_attn_softmax_fwd: latest rel-pos needs P=2T-1");
   ESP_ARG_CHECK(relpos != 2 || P == Tq, "esp_attn_softmax_fwd: legacy rel-pos needs P=T");
@@ -1474,7 +1585,10 @@ ESP_API int esp_attn_softmax_fwd(const float* ac, const float* bd, int relpos, i
   else if (Tk <= 128) ESP_SM(2);
   else if (Tk <= 256) ESP_SM(4);
   else if (Tk <= 512) ESP_SM(8);
-  else ESP_SM(16);
+  else if (Tk <= 1024) ESP_SM(16);
+  else
+    hipLaunchKernelGGL(softmax_fwd_loop_kernel, grid, dim3(256), 0, st, ac, bd, relpos, P, sqrt_dk, klen, nb, causal,
+                       attn, pdrop, thr, ds, (uint64_t)seed, Z, Tq, Tk, lds, ldp, esp::rng_key_ptr(), tvalid);
 #undef ESP_SM
   ESP_CHECK_LAUNCH("esp_attn_softmax_fwd");
   return 0;
@@ -1482,7 +1596,7 @@ ESP_API int esp_attn_softmax_fwd(const float* ac, const float* bd, int relpos, i
 
 ESP_API int esp_attn_softmax_bwd(const float* attn, const float* dP, float* dS, float drop_p, unsigned long long seed,
                                  float sqrt_dk, long rows, int Tk, long lds, void* stream) {
-  ESP_ARG_CHECK(Tk <= 1024, "esp_attn_softmax_bwd: Tk too large");
+  ESP_ARG_CHECK(Tk >= 1, "esp_attn_softmax_bwd: Tk=%d", Tk);
   ESP_ARG_CHECK(lds >= Tk, "esp_attn_softmax_bwd: pitch < Tk");
   ESP_ARG_CHECK(drop_p < 1.f, "dropout p must be < 1 (got %g)", (double)drop_p);
   const uint32_t thr = esp::drop_threshold(drop_p);
@@ -1495,7 +1609,10 @@ ESP_API int esp_attn_softmax_bwd(const float* attn, const float* dP, float* dS, 
   else if (Tk <= 128) ESP_SB(2);
   else if (Tk <= 256) ESP_SB(4);
   else if (Tk <= 512) ESP_SB(8);
-  else ESP_SB(16);
+  else if (Tk <= 1024) ESP_SB(16);
+  else
+    hipLaunchKernelGGL(softmax_bwd_loop_kernel<0>, grid, dim3(256), 0, st, attn, dP, dS, nullptr, 0L, thr, ds,
+                       (uint64_t)seed, sqrt_dk, rows, Tk, lds, esp::rng_key_ptr(), nullptr);
 #undef ESP_SB
   ESP_CHECK_LAUNCH("esp_attn_softmax_bwd");
   return 0;
@@ -1741,7 +1858,7 @@ ESP_API int esp_attn_softmax_bwd_relpos(const float* attn, const float* dP, floa
                                         int relpos, float drop_p, unsigned long long seed, float sqrt_dk, long rows,
                                         int T, long lds, const int* tvalid, void* stream) {
   ESP_ARG_CHECK(relpos == 1 || relpos == 2, "esp_attn_softmax_bwd_relpos: relpos must be 1 or 2");
-  ESP_ARG_CHECK(T >= 1 && T <= 1024 && lds >= T && ldp >= (relpos == 1 ? 2 * T - 1 : T) && rows % T == 0,
+  ESP_ARG_CHECK(T >= 1 && lds >= T && ldp >= (relpos == 1 ? 2 * T - 1 : T) && rows % T == 0,
                 "esp_attn_softmax_bwd_relpos: bad sizes");
   ESP_ARG_CHECK(drop_p < 1.f, "dropout p must be < 1 (got %g)", (double)drop_p);
   const uint32_t thr = esp::drop_threshold(drop_p);
@@ -1786,7 +1903,13 @@ ESP_API int esp_attn_softmax_bwd_relpos(const float* attn, const float* dP, floa
   else if (T <= 128) ESP_SBR(2);
   else if (T <= 256) ESP_SBR(4);
   else if (T <= 512) ESP_SBR(8);
-  else ESP_SBR(16);
+  else if (T <= 1024) ESP_SBR(16);
+  else if (relpos == 1)
+    hipLaunchKernelGGL(softmax_bwd_loop_kernel<1>, grid, dim3(256), 0, st, attn, dP, dS, dbd, ldp, thr, ds,
+                       (uint64_t)seed, sqrt_dk, rows, T, lds, esp::rng_key_ptr(), tvalid);
+  else
+    hipLaunchKernelGGL(softmax_bwd_loop_kernel<2>, grid, dim3(256), 0, st, attn, dP, dS, dbd, ldp, thr, ds,
+                       (uint64_t)seed, sqrt_dk, rows, T, lds, esp::rng_key_ptr(), tvalid);
 #undef ESP_SBR
   ESP_CHECK_LAUNCH("esp_attn_softmax_bwd_relpos");
   return 0;

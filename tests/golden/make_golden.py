@@ -521,6 +521,14 @@ def c2_cfg(rel_pos_type):
                       dec=O.DecCfg(attention_heads=4, linear_units=2048, num_blocks=6))
 
 
+def long_cfg(rel_pos_type):
+    """The long-utterance fixtures' model: C2's layer shapes (d = 256, H = 4, d_k = 64, FF 1024), 2 encoder and
+    2 decoder blocks (tests/helpers.long_cfg)."""
+    return O.ModelCfg(vocab_size=600, enc=O.EncCfg(output_size=256, attention_heads=4, linear_units=1024,
+                                                   num_blocks=2, rel_pos_type=rel_pos_type),
+                      dec=O.DecCfg(attention_heads=4, linear_units=1024, num_blocks=2))
+
+
 SLURP_YAML = "egs2/slurp/asr1/conf/tuning/train_asr_conformer.yaml"
 
 
@@ -845,6 +853,12 @@ if __name__ == "__main__":
     if "small" in which:
         model_fixture("model_small_latest", small_cfg("latest"), 3, 120, [120, 97, 64], [9, 5, 7], 1)
         model_fixture("model_small_legacy", small_cfg("legacy"), 3, 120, [120, 97, 64], [9, 5, 7], 2)
+    if "long" in which:  # long utterances (VERDICT r5 'missing' 1): T' = 875 latest / legacy, T' = 1100 latest,
+        # d_k = 64 (the rel-pos kernels' head size), 2 encoder / 2 decoder blocks
+        for name, rel, T, lens in (("long_t875_latest", "latest", 3503, (3503, 3000)),
+                                   ("long_t875_legacy", "legacy", 3503, (3503, 3000)),
+                                   ("long_t1100_latest", "latest", 4403, (4403, 3803))):
+            fullsize_train_fixture(name, long_cfg(rel), B=2, T=T, lens=lens, ulens=(60, 45), seed=91)
     if "conv2d6" in which:  # input_layer conv2d6 (Conv2dSubsampling6, the LibriSpeech Conformer recipe's)
         cfg = small_cfg("latest")
         cfg.enc.input_layer = "conv2d6"
