@@ -119,8 +119,10 @@ def cpu_model() -> str:
 
 def cpu_baseline(args):
     """The oracle (plain PyTorch CPU restatement, oracle/espnet_cpu.py) timed on the host
-    cores: same C2 model shape, fp32, B=4 x 1500 frames, dropout 0.1, no SpecAug draws,
-    1 warmup + 3 timed steps of fwd + bwd + clip + torch Adam."""
+    cores: same C2 model shape, fp32, B=4 x 1500 frames, dropout 0.1, SpecAug on with the GPU step's
+    configuration (time warp window 5, 2 frequency masks of width [0, 30), 2 time masks of width [0, 40);
+    fresh draws every step, mask_along_axis.py:32-44 / time_warp.py:25-27), 1 warmup + 3 timed steps of
+    fwd + bwd + clip + torch Adam -- the same step the GPU times."""
     from oracle import espnet_cpu as O
     n = host_cores()
     torch.set_num_threads(n)
@@ -139,9 +141,21 @@ def cpu_baseline(args):
     speech, slen, text, tlen = O.synthetic_batch(B, 1500, 80, args.vocab, [1500] * B, [40, 33, 27, 20], 7)
     bn = {}
     times = []
+    gen = torch.Generator().manual_seed(11)
+
+    def specaug_draws(T, F):
+        center = int(torch.randint(5, T - 5, (1,), generator=gen)[0])
+        warped = int(torch.randint(center - 5, center + 5, (1,), generator=gen)[0]) + 1
+        d = {"center": center, "warped": warped}
+        for key, D, hi in (("freq", F, 30), ("time", T, 40)):
+            ml = torch.randint(0, hi, (B, 2), generator=gen)
+            d[key + "_len"] = ml
+            d[key + "_pos"] = torch.randint(0, max(1, D - int(ml.max())), (B, 2), generator=gen)
+        return d
+
     for it in range(4):
         t0 = time.perf_counter()
-        loss, _, _ = O.asr_forward(P, speech, slen, text, tlen, cfg, bn_state=bn)
+        loss, _, _ = O.asr_forward(P, speech, slen, text, tlen, cfg, specaug=specaug_draws(1500, 80), bn_state=bn)
         loss.backward()
         torch.nn.utils.clip_grad_norm_(params, 5.0)
         opt.step()
@@ -150,7 +164,7 @@ def cpu_baseline(args):
     t = sum(times[1:]) / len(times[1:])
     return {"value": round(B / t, 4), "unit": "utt/s", "cores": n, "kind": "port", "cpu_model": cpu_model(),
             "sample": f"oracle/espnet_cpu.py {workload_name(args).split()[0]}-shape step (fwd+bwd+clip+Adam), "
-                      f"d={args.d} {args.layers}L, B=4 x 1500 frames, fp32, "
+                      f"d={args.d} {args.layers}L, B=4 x 1500 frames, fp32, SpecAug on, "
                       f"1 warmup + 3 timed steps, {t:.2f} s/step on {n} threads"}
 
 
@@ -293,6 +307,9 @@ def main():
     ap.add_argument("--graph-buckets", default="100,8",
                     help="frames,tokens bucket multiples of TrainerOptions.graph_buckets (--variable-lengths)")
     ap.add_argument("--amp", action="store_true", help="bf16 GEMM operands, fp32 accumulate (TrainerOptions.use_amp)")
+    ap.add_argument("--dp-world1", action="store_true",
+                    help="N=1 through the data-parallel path (a 1-rank RCCL group: segmented-graph capture, bucket "
+                         "all-reduces) -- the per-rank HBM and step of the N-GPU job, measurable on one GPU")
     ap.add_argument("--config", choices=sorted(PRESETS), default=None,
                     help="BASELINE.json config preset (overrides --d/--heads/--ff/--layers; c5 implies --amp)")
     args = ap.parse_args()
@@ -314,10 +331,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    dp = world > 1 or args.dp_world1
+    if dp:
         # enough RCCL channels that a ring uses all 7 xGMI links of each GPU
         os.environ.setdefault("NCCL_MIN_NCHANNELS", "8")
-        dist.init_process_group("nccl")
+        if world == 1:  # --dp-world1: a 1-rank group of this process
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(free_port()))
+            dist.init_process_group("nccl", rank=0, world_size=1)
+        else:
+            dist.init_process_group("nccl")
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     torch.manual_seed(0)
@@ -333,7 +356,7 @@ def main():
     sched = WarmupLR(opt, warmup_steps=25000)
     buckets = tuple(int(v) for v in args.graph_buckets.split(",")) if args.variable_lengths else None
     trainer = Trainer(model, opt, sched, TrainerOptions(grad_clip=5.0, use_amp=args.amp, graph_buckets=buckets),
-                      distributed=world > 1, cuda_graph=not args.eager)
+                      distributed=dp, cuda_graph=not args.eager)
     batches = [synthetic_batch(args.batch, args.vocab, rank, device, args.variable_lengths, i)
                for i in range(4 if args.variable_lengths else 1)]
     batch = batches[0]
@@ -344,13 +367,13 @@ def main():
 
     if args.eager:
         K.profile_gemm_start()
-    if world > 1:
+    if dp:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         stats = trainer.train_one_step(batches[i % len(batches)])
-    if world > 1:
+    if dp:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -371,7 +394,7 @@ def main():
     if not args.eager:
         # the graph's kernels cannot be bracketed one by one: time the same GEMM launches (same
         # kernels, shapes and inputs) in one eager step right after the timed region
-        eager = Trainer(model, opt, sched, TrainerOptions(grad_clip=5.0, use_amp=args.amp), distributed=world > 1)
+        eager = Trainer(model, opt, sched, TrainerOptions(grad_clip=5.0, use_amp=args.amp), distributed=dp)
         torch.cuda.synchronize()
         # hold the GPU for ~200 ms so the host enqueues the whole eager step (~1,500 launches)
         # before the first GEMM runs: each event pair then brackets its kernel back to back,
@@ -384,9 +407,14 @@ def main():
     attn_flops, attn_bytes, attn_ms, attn_launches = K.profile_attn_stop()
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    if world > 1:
+    if dp:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
+    # peak HBM this rank reserved (the caching allocator, graph pools included), max over ranks
+    peak = torch.tensor([torch.cuda.max_memory_reserved(device) / 2 ** 30], dtype=torch.float64, device=device)
+    if dp:
+        dist.all_reduce(peak, op=dist.ReduceOp.MAX)
+    hbm_peak_gib = round(float(peak.item()), 1)
 
     if rank == 0:
         traffic = measured_gemm_traffic(args)
@@ -420,6 +448,8 @@ def main():
             "data": "synthetic (N(0,1) fbank, random tokens U[20,40], random-init weights)",
             "launch": "eager" if args.eager else "hip_graph",
             "graphs_captured": len(trainer._graphs) if not args.eager else 0,
+            "dp_path": dp,
+            "hbm_peak_gib": hbm_peak_gib,
             "last_step": {"loss": round(last_loss, 4), "grad_norm": round(last_gn, 4),
                           "skipped_steps": trainer.n_skipped},
             "config": {"workload": f"{workload_name(args)} d={args.d} H={args.heads} FF={args.ff} "
@@ -463,7 +493,7 @@ def main():
                         "`value` keeps the resident synthetic batch of SURVEY 8(d))"},
         }
         print(json.dumps(out))
-    if world > 1:
+    if dp:
         dist.destroy_process_group()
 
 

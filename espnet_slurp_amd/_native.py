@@ -108,6 +108,7 @@ SIGNATURES = {
     "esp_reduce_losses": [P, I, I, P, P, I, F, F, P, P],
     "esp_argmax": [P, P, L, I, P],
     "esp_ctc_forced_align": [P, I, I, P, I, I, P, P, P],
+    "esp_attn_slot_check_errors": [],
     "esp_ctc_forced_align_batch": [P, I, I, I, P, P, I, P, I, P, P, P],
     "esp_ctc_prefix_init": [P, I, I, I, P, P],
     "esp_ctc_prefix_score": [P, I, I, P, P, I, P, I, I, I, I, P, P, P],
@@ -123,7 +124,7 @@ SIGNATURES = {
     "esp_ctc_loss_workspace_bytes": [I, I, I],
     "esp_relpos_dp_workspace_bytes": [I, I, I],
 }
-_RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I, "esp_set_gemm_compute": I,
+_RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I, "esp_attn_slot_check_errors": I, "esp_set_gemm_compute": I,
              "esp_get_gemm_compute": I, "esp_set_splitk_mode": I,
              "esp_f32_gemm_products": I}
 _RESTYPES.update({k: L for k in SIGNATURES if k.endswith("_workspace_bytes")})

@@ -1274,6 +1274,32 @@ __device__ __forceinline__ f32x4 mfma_pl(const FragPl<NPL>& a, const FragPl<NPL>
   return c;
 }
 
+// LDS slot schedule of relpos_probs_lds_kernel (the audit of VERDICT r5 'next' 7; PF, the register prefetch
+// depth, does not touch LDS):
+//   kpl[2]   key tile t lives in kpl[t & 1].  Written: tile 0 in the prologue, tile t+1 at the end of step t.
+//            Readers of the slot it replaces (tile t-1): every wave in step t-1, all before the block barrier
+//            that ends step t-1 -- the write comes after that barrier.  Step t reads kpl[t & 1] only.
+//   ppl[5]   band block u lives in ppl[pslot(u)] = ppl[u mod 5]; wave w reads block t - w at step t
+//            (u = t-3..t over the block) and block -1 - w in the prologue.  Written: blocks -4..0 in the
+//            prologue, block t+1 at the end of step t into the slot of block t-4, whose readers are wave w
+//            at step t-4+w (w = 0..3), i.e. steps t-4..t-1, all before the barrier ending step t-1; step t
+//            reads blocks t-3..t, none in that slot.  The one reuse outside the loop: step 0 writes block 1
+//            into pslot(-4), which wave 3 read in the prologue -- the block barrier after the prologue's
+//            band read orders it (round-5 fix).
+//   ring[w], stage[w]: per wave (LDS is in order within a wave; asm memory fences keep the compiler from
+//            reordering the ring writes / reads).
+// ESP_ATTN_SLOT_CHECK=1 (a separate build: make VARIANT=_slotchk EXTRA=-DESP_ATTN_SLOT_CHECK=1, loaded with
+// ESP_LIB_VARIANT=_slotchk) checks this at run time: each slot carries a per-wave generation word in LDS --
+// set to BUSY before a wave writes its rows of the slot and to the block / tile index after -- and every
+// fragment read checks all four words equal the expected index before AND after the read, so a write that
+// overlaps the read in any order is seen; mismatches are counted in g_attn_slot_err (vector stores only) and
+// read back by esp_attn_slot_check_errors().
+#ifndef ESP_ATTN_SLOT_CHECK
+#define ESP_ATTN_SLOT_CHECK 0
+#endif
+#if ESP_ATTN_SLOT_CHECK
+__device__ int g_attn_slot_err[64];
+#endif
 template <int NTA, bool P2, bool LEGACY, int NP>  // NTA >= ceil(T / 16) key tiles; NP 6 (fp32) or 1 (bf16)
 __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
     const float* __restrict__ qu, const float* __restrict__ qv, const float* __restrict__ kmat, long ldk,
@@ -1305,6 +1331,28 @@ __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
   const float inv_sqrt_dk = 1.0f / sqrt_dk;
   float* ring0 = ring[wave];
   auto pslot = [](int u) { return ((u % PSL) + PSL) % PSL; };
+#if ESP_ATTN_SLOT_CHECK
+  __shared__ int kgen[2][4], pgen[PSL][4];
+  constexpr int BUSY = -0x7fffffff;
+  auto mark = [&](int* gw, int v) {  // this wave's generation word of a slot (before / after its rows)
+    asm volatile("" ::: "memory");
+    if (lane == 0) gw[wave] = v;
+    asm volatile("" ::: "memory");
+  };
+  auto check = [&](const int* gw, int v, int where) {
+    asm volatile("" ::: "memory");
+    bool bad = false;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) bad |= gw[w] != v;
+    asm volatile("" ::: "memory");
+    if (bad) g_attn_slot_err[lane] = 1 + where;  // (vector store; no printf: it multiplies the unrolled code)
+  };
+#define ESP_SLOT_MARK(g, v) mark(g, v)
+#define ESP_SLOT_CHECK(g, v, w) check(g, v, w)
+#else
+#define ESP_SLOT_MARK(g, v) ((void)0)
+#define ESP_SLOT_CHECK(g, v, w) ((void)0)
+#endif
 
   // staging: thread -> row sr of the tile, dims sd..sd+3 (one float4; 16 threads per 256-B row)
   const int sr = tid >> 4, sd = 4 * (tid & 15);
@@ -1335,8 +1383,14 @@ __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
     for (int s = 0; s < PSL; ++s) pv[s] = *p_src(s - 4);
     const float4 kv = *k_src(0);
 #pragma unroll
-    for (int s = 0; s < PSL; ++s) put_tile(ppl[pslot(s - 4)], pv[s]);
+    for (int s = 0; s < PSL; ++s) {
+      ESP_SLOT_MARK(pgen[pslot(s - 4)], BUSY);
+      put_tile(ppl[pslot(s - 4)], pv[s]);
+      ESP_SLOT_MARK(pgen[pslot(s - 4)], s - 4);
+    }
+    ESP_SLOT_MARK(kgen[0], BUSY);
     put_tile(kpl[0], kv);
+    ESP_SLOT_MARK(kgen[0], 0);
   }
   // the wave's query rows (d = 16 q4 + 0..15, contiguous: the plane images' order), split once
   auto ld16c = [&](const float* row, float (&f)[16]) {
@@ -1364,7 +1418,9 @@ __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
   __syncthreads();
   {  // band block 0 of this wave (u = -1 - w; below T for every g: A rows q_v[i] in both variants)
     FragPl<NPL> pf;
+    ESP_SLOT_CHECK(pgen[pslot(-1 - wave)], -1 - wave, 0);
     read_frag_pl(ppl[pslot(-1 - wave)], PLB, li, q4, pf);
+    ESP_SLOT_CHECK(pgen[pslot(-1 - wave)], -1 - wave, 1);
     put_band(ring0, 0, mfma_pl(xv, pf, f32x4{0.f, 0.f, 0.f, 0.f}));
   }
   // wave 3 read block -4 here, whose slot (pslot(-4) == pslot(1)) step 0 refills with block 1: every
@@ -1391,8 +1447,12 @@ __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
       np[t % PF] = *p_src(t + PF);
     }
     FragPl<NPL> kf, pf;
+    ESP_SLOT_CHECK(kgen[t & 1], t, 2);
+    ESP_SLOT_CHECK(pgen[pslot(t - wave)], t - wave, 3);
     read_frag_pl(kpl[t & 1], PLB, li, q4, kf);
     read_frag_pl(ppl[pslot(t - wave)], PLB, li, q4, pf);
+    ESP_SLOT_CHECK(kgen[t & 1], t, 4);
+    ESP_SLOT_CHECK(pgen[pslot(t - wave)], t - wave, 5);
     if (LEGACY && t == g) {  // band block t+1 = g+1: the first shifted block -- its A rows are q_v[i+1]
       float f[16];
       ld16c(qv + ((long)z * T + min(i0 + 1 + li, T - 1)) * RP_DK, f);
@@ -1419,8 +1479,12 @@ __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
     }
     asm volatile("" ::: "memory");  // ... and these reads before the next tile's ring writes
     if (t + 1 < NTA) {
+      ESP_SLOT_MARK(kgen[(t + 1) & 1], BUSY);
       put_tile(kpl[(t + 1) & 1], nk[(t + 1) % PF]);
+      ESP_SLOT_MARK(kgen[(t + 1) & 1], t + 1);
+      ESP_SLOT_MARK(pgen[pslot(t + 1)], BUSY);
       put_tile(ppl[pslot(t + 1)], np[(t + 1) % PF]);
+      ESP_SLOT_MARK(pgen[pslot(t + 1)], t + 1);
       __syncthreads();  // step t+1's planes written; every wave done reading the slots they replaced
     }
   }
@@ -1514,6 +1578,8 @@ __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
   };
   if (pdrop) store_rows(std::true_type{});
   else store_rows(std::false_type{});
+#undef ESP_SLOT_MARK
+#undef ESP_SLOT_CHECK
 }
 
 inline int gridn(long n) {
@@ -1522,6 +1588,22 @@ inline int gridn(long n) {
 }
 
 }  // namespace
+
+// the slot-check build's mismatch count since the last call (then reset); -1 in every other build
+ESP_API int esp_attn_slot_check_errors(void) {
+#if ESP_ATTN_SLOT_CHECK
+  if (hipDeviceSynchronize() != hipSuccess) return -2;
+  int h[64];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_attn_slot_err), sizeof h) != hipSuccess) return -2;
+  int n = 0;
+  for (int i = 0; i < 64; ++i) n += h[i] != 0;
+  const int zeros[64] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_attn_slot_err), zeros, sizeof zeros) != hipSuccess) return -2;
+  return n;
+#else
+  return -1;
+#endif
+}
 
 ESP_API int esp_heads_split(const float* src, long ld, int col0, int B, int T, int H, int dk, const float* bias,
                             float* dst, void* stream) {

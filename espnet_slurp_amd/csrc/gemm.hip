@@ -657,21 +657,7 @@ static int gemm_run(int mode_a, int mode_b, int M, int N, int K, int batch, int 
 
     // (256 x 128 bf16 tiles -- one block, one wave per SIMD, per CU -- measured slower, C5 B=64 860.3 vs
     // 889.3 utt/s, and were removed in round 5)
-#ifndef ESP_GEMM_WIDE_BF16
-#define ESP_GEMM_WIDE_BF16 1
-#endif
-#ifndef ESP_GEMM_WIDE_F32
-#define ESP_GEMM_WIDE_F32 1
-#endif
-#if ESP_GEMM_WIDE
-    // 256 x 128 tiles of 8 waves (two per SIMD in one block per CU, a 3-slab ring where it fits): the 32-bit
-    // staging offsets of 256 KC rows / a 256-pixel run within <= 2 maps
-    if (g.bnt == 128 && g.bm == BM && g.bf16 != 5 && (g.bf16 == 2 ? ESP_GEMM_WIDE_BF16 : ESP_GEMM_WIDE_F32) && !smb &&
-        M >= 256 &&
-        mode_b != I2C_RC && (mode_a != KC || 256L * g.a.ld * 4 < (1L << 32)) &&
-        (mode_a != I2C_KC || (long)g.a.ic.Ho * g.a.ic.Wo >= 256))
-      g.bm = 256;
-#elif ESP_GEMM_WIDE_KCRC
+#if ESP_GEMM_WIDE_KCRC
     // the KC x RC GEMMs on B planes (linear input gradients, P0 / FFN w_2 shapes): 256 x 128 tiles of 8 waves
     // on a 2-slab ring, 3-7 % faster per kernel at C2 B=256 (the other pairs measured slower, r05am)
     if (g.bnt == 128 && g.bm == BM && g.bf16 == 3 && mode_a == KC && mode_b == RC && !smb && M >= 256 &&

@@ -1231,32 +1231,19 @@ struct GldsArgs {
   int t_dt[4], t_df[4];
   const float* t_zeros;  // >= 16 zero bytes: the DMA source of lanes outside the grid
 };
-// Diagnostic ablation bits, compile time only (a separate build, e.g. make VARIANT=_abl
-// EXTRA=-DESP_GEMM_ABL_BITS=1; timing only, the outputs are wrong): 1 no DMA after the first slab,
-// 2 no epilogue stores, 4 no k-loop barrier / waits, 32 non-temporal epilogue stores, 64 the float4
-// (transposed) epilogue instead of the column epilogue (store_cols).  The product build has none.
-#ifndef ESP_GEMM_ABL_BITS
-#define ESP_GEMM_ABL_BITS 0
-#endif
-constexpr int kGemmAbl = ESP_GEMM_ABL_BITS;
+// (Round 6: the diagnostic ablation bits, the 3-slab ring, the all-GEMM 256 x 128 tiles, the iglp_opt hint and
+// the product-major MFMA order -- timing builds and measured-slower variants, DESIGN 3.1 / 3.10 -- were removed
+// from the product header; their code is in git history before this note.)
 
 constexpr int GL_BK = 32;
 // LDS slab ring depth of the LDS-DMA kernel: 2 (double buffer: slab k+1 in flight while k is read, every
-// slab waits vmcnt(0)); 3: slabs k+1 and k+2 in flight across tile boundaries, a counted vmcnt leaves the
-// newer one in flight at the slab barrier (1.5x the LDS: one 128x128 block per CU)
-#ifndef ESP_GEMM_WIDE
-#define ESP_GEMM_WIDE 0
-#endif
+// slab waits vmcnt(0))
 // 256 x 128 tiles of 8 waves for the KC x RC GEMMs on B planes only (the pairs they speed up: the linear
 // input gradients / P0 / FFN w_2 shapes 3-7 %, profiles/r05am_*)
 #ifndef ESP_GEMM_WIDE_KCRC
 #define ESP_GEMM_WIDE_KCRC 1
 #endif
-#ifndef ESP_GEMM_STAGES
-#define ESP_GEMM_STAGES 2
-#endif
-constexpr int GL_ST = ESP_GEMM_STAGES;
-static_assert(GL_ST == 2 || GL_ST == 3, "ESP_GEMM_STAGES: 2 or 3");
+constexpr int GL_ST = 2;
 
 // K-contiguous slab image: row r (128 B = 8 quads) holds global quad q at position q ^ kc_swz(r).
 // A ds_read_b128 of frag16 serves 16-lane groups {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32)
@@ -1712,18 +1699,13 @@ __device__ __forceinline__ TileCoord tile_coord(const GemmArgs& g, const GldsArg
 // PREC 3 (B as three bf16 planes: 1.5x the B slab bytes) is also bounded by LDS: 128x128 tiles use
 // exactly 80 KB (two per CU), 128x64 56 KB (two), 64x64 40 KB (four); PREC 5 (both operands as
 // planes): 128x64 72 KB (two), 64x64 48 KB (three)
-// 256 x 128 tiles (ESP_GEMM_WIDE builds): 8 waves (two per SIMD in one block per CU), each wave the 64 x 64
-// of a 128 x 128 tile's wave; a 3-slab ring where 3 slabs fit the LDS
+// 256 x 128 tiles (the KC x RC GEMMs on B planes, ESP_GEMM_WIDE_KCRC): 8 waves (two per SIMD in one block per
+// CU), each wave the 64 x 64 of a 128 x 128 tile's wave, on the 2-slab ring
 constexpr int glds_threads(int BMT) { return BMT == 256 ? 512 : NT; }
 constexpr int glds_stage_bytes(int BNT, int BMT, int PREC) {
   return 4 * ((PREC == 5 ? 48 * BMT : BMT * GL_BK) + (PREC >= 3 ? 48 * BNT : BNT * GL_BK));
 }
-#ifndef ESP_GEMM_WIDE_STAGES
-#define ESP_GEMM_WIDE_STAGES 3
-#endif
-constexpr int glds_stages(int BNT, int BMT, int PREC) {
-  return BMT == 256 ? (ESP_GEMM_WIDE_STAGES == 3 && 3 * glds_stage_bytes(BNT, BMT, PREC) + 16 <= 163840 ? 3 : 2) : GL_ST;
-}
+constexpr int glds_stages(int, int, int) { return GL_ST; }
 constexpr int glds_lds_bytes(int BNT, int BMT, int PREC) {
   return glds_stages(BNT, BMT, PREC) * glds_stage_bytes(BNT, BMT, PREC) + (PREC >= 3 ? 0 : 16);
 }
@@ -1762,13 +1744,8 @@ constexpr int glds_occupancy() {
 // profiles/r03i_abc_split_code.txt)
 __device__ __forceinline__ void split3_bf16(const float* v, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
   uint32_t H[4], Md[4], L[4];
-  if constexpr ((kGemmAbl & 128) != 0) {  // diagnostic: hi only (mid = lo = hi), wrong results
 #pragma unroll
-    for (int p = 0; p < 4; ++p) H[p] = Md[p] = L[p] = esp::bf16_pair(v[2 * p], v[2 * p + 1]);
-  } else {
-#pragma unroll
-    for (int p = 0; p < 4; ++p) esp::split3_pair(v[2 * p], v[2 * p + 1], H[p], Md[p], L[p]);
-  }
+  for (int p = 0; p < 4; ++p) esp::split3_pair(v[2 * p], v[2 * p + 1], H[p], Md[p], L[p]);
   hi = __builtin_bit_cast(bf16x8, make_uint4(H[0], H[1], H[2], H[3]));
   mid = __builtin_bit_cast(bf16x8, make_uint4(Md[0], Md[1], Md[2], Md[3]));
   lo = __builtin_bit_cast(bf16x8, make_uint4(L[0], L[1], L[2], L[3]));
@@ -1776,36 +1753,18 @@ __device__ __forceinline__ void split3_bf16(const float* v, bf16x8& hi, bf16x8& 
 
 
 // The six split products of every (i, j) tile pair (smallest first: mid.mid, lo.hi, hi.lo, mid.hi, hi.mid,
-// hi.hi).  ESP_GEMM_MFMA_ORDER 0: each pair's six MFMAs back to back (one accumulator chain at a time);
-// 1: product-major, the TM x TN independent accumulators interleaved -- each accumulator receives the same
-// products in the same order either way (bit-identical results)
-// diagnostic scheduling hint (iglp_opt strategy in the k-loop bodies; -1: none)
-#ifndef ESP_GEMM_IGLP
-#define ESP_GEMM_IGLP -1
-#endif
-#ifndef ESP_GEMM_MFMA_ORDER
-#define ESP_GEMM_MFMA_ORDER 0
-#endif
+// hi.hi), each pair's six MFMAs back to back (one accumulator chain at a time; the product-major order
+// measured 0.6-0.7 % slower, r05l)
 template <int TM, int TN>
 __device__ __forceinline__ void mma6(f32x16 (&acc)[TM][TN], const bf16x8 (&ah)[TM][3], const bf16x8 (&bh)[TN][3]) {
   constexpr int PA[6] = {1, 2, 0, 1, 0, 0}, PB[6] = {1, 0, 2, 0, 1, 0};
-  if constexpr (ESP_GEMM_MFMA_ORDER == 1) {
 #pragma unroll
-    for (int p = 0; p < 6; ++p)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+    for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][PA[p]], bh[j][PB[p]], acc[i][j], 0, 0, 0);
-  } else {
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int p = 0; p < 6; ++p)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][PA[p]], bh[j][PB[p]], acc[i][j], 0, 0, 0);
-  }
+      for (int p = 0; p < 6; ++p)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i][PA[p]], bh[j][PB[p]], acc[i][j], 0, 0, 0);
 }
 
 template <int MA, int MB, int BNT, bool RS, int EPI, int PREC = 0, int BMT = BM>
@@ -1897,44 +1856,8 @@ __global__ __launch_bounds__(glds_threads(BMT), (glds_occupancy<BNT, EPI, BMT, P
 
   TileCoord c = tile_coord<BNT, BMT>(g, x, t, G);
   init_ab(c);
-  // GL_ST == 3: the DMA cursor (tile dtile, slab dkt of dc) runs two slabs ahead of the k-loop, across
-  // tile boundaries; each issue is NSLAB DMA instructions per wave
-  constexpr int NSLAB = SAt::kNI + SBt::kNI;
-  TileCoord dc = c;
-  int dkt = 0, dtile = t, slot = 0;
-  bool dmore = true;
-  auto dma_issue = [&](float* dst) -> bool {
-    if (!dmore) return false;
-    issue_ab(dc.kbeg + dkt * GL_BK, dst);
-    if (++dkt == dc.nk) {
-      dtile += G;
-      if (dtile < x.ntiles) {
-        dc = tile_coord<BNT, BMT>(g, x, dtile, G);
-        init_ab(dc);
-        dkt = 0;
-      } else {
-        dmore = false;
-      }
-    }
-    return true;
-  };
-  // the slab ring advance: this wave's DMA of the next slab landed (the one after it may stay in flight),
-  // this wave's reads of this slab done, then everyone's
-  auto finish3 = [&](bool ahead) {
-    if (ahead) wait_vm_n<NSLAB>();
-    else wait_vm0();
-    wait_lgkm0();
-    raw_barrier();
-    slot = slot == ST - 1 ? 0 : slot + 1;
-  };
-  if constexpr (ST == 3) {
-    dma_issue(smem);
-    if (dma_issue(smem + BUF)) wait_vm_n<NSLAB>();
-    else wait_vm0();
-  } else {
-    issue_ab(c.kbeg, smem);
-    wait_vm0();
-  }
+  issue_ab(c.kbeg, smem);
+  wait_vm0();
   raw_barrier();
   int buf = 0;
 
@@ -1961,9 +1884,6 @@ __global__ __launch_bounds__(glds_threads(BMT), (glds_occupancy<BNT, EPI, BMT, P
     // k >= kv values are zeroed in registers (B's staged tail holds finite clamped elements), so
     // no LDS zero pass and no extra barrier
     auto compute = [&](const float* cur, int kv) {
-#if ESP_GEMM_IGLP >= 0
-      __builtin_amdgcn_iglp_opt(ESP_GEMM_IGLP);
-#endif
       if constexpr (PREC == 2) {
         // fragments as 4 chunks of 8 bf16 per tile (k = 32h + 8t + 0..7 for chunk t)
         float4 a4[TM][4], b4[TN][4];
@@ -2201,9 +2121,6 @@ __global__ __launch_bounds__(glds_threads(BMT), (glds_occupancy<BNT, EPI, BMT, P
       }
     };
     auto mma_half = [&](int hs, int kv, FragA& a, FragB& b) {
-#if ESP_GEMM_IGLP >= 0
-      __builtin_amdgcn_iglp_opt(ESP_GEMM_IGLP);
-#endif
       if constexpr (PIPE) {
         if (kv < GL_BK) {  // K tail: A's k >= kv are 0 (B's clamped tail holds finite values)
 #pragma unroll
@@ -2238,40 +2155,13 @@ __global__ __launch_bounds__(glds_threads(BMT), (glds_occupancy<BNT, EPI, BMT, P
       }
     };
     auto finish_slab = [&]() {
-      if (!(kGemmAbl & 4)) {
-        wait_vm0();     // this wave's DMA of the next slab has landed
-        wait_lgkm0();   // this wave's reads of this slab are done
-        raw_barrier();  // -> everyone's: next slab readable, this buffer free for the one after
-      }
+      wait_vm0();     // this wave's DMA of the next slab has landed
+      wait_lgkm0();   // this wave's reads of this slab are done
+      raw_barrier();  // -> everyone's: next slab readable, this buffer free for the one after
       buf ^= 1;
     };
 
-    if constexpr (ST == 3) {
-      // the 3-slab ring: slab kt + 2 (of this or a later tile) is issued as slab kt is read
-      if constexpr (PIPE) {
-        FragA Fa, Ga;
-        FragB Fb, Gb;
-        load_half(smem + slot * BUF, 0, Fa, Fb);
-        for (int kt = 0; kt < c.nk; ++kt) {
-          const bool ahead = dma_issue(smem + (slot == 0 ? 2 : slot - 1) * BUF);
-          const bool last = kt + 1 == c.nk;
-          const int kv = last ? c.kend - (c.kbeg + kt * GL_BK) : GL_BK;
-          load_half(smem + slot * BUF, 1, Ga, Gb);
-          mma_half(0, kv, Fa, Fb);
-          finish3(ahead);
-          if (!last) load_half(smem + slot * BUF, 0, Fa, Fb);
-          mma_half(1, kv, Ga, Gb);
-        }
-      } else {
-        for (int kt = 0; kt < c.nk; ++kt) {
-          const bool ahead = dma_issue(smem + (slot == 0 ? 2 : slot - 1) * BUF);
-          const int kv = kt + 1 == c.nk ? c.kend - (c.kbeg + kt * GL_BK) : GL_BK;
-          compute(smem + slot * BUF, kv);
-          finish3(ahead);
-        }
-      }
-      if (has_next) cn = tile_coord<BNT, BMT>(g, x, tnext, G);
-    } else if constexpr (PIPE) {
+    if constexpr (PIPE) {
       // fp32 split products (PREC 0 / 3), software-pipelined by k-step: the fragments of k-step hs+1
       // are read while the MFMAs of k-step hs issue, and the slab barrier sits BETWEEN a slab's two
       // k-steps -- after it the wave issues k-step 1's MFMAs (operands already in registers) while
@@ -2286,7 +2176,7 @@ __global__ __launch_bounds__(glds_threads(BMT), (glds_occupancy<BNT, EPI, BMT, P
         float* nxt = smem + (buf ^ 1) * BUF;  // last read before the previous barrier
         const bool last = kt + 1 == c.nk;
         if (!last) {
-          if (!(kGemmAbl & 1)) issue_ab(c.kbeg + (kt + 1) * GL_BK, nxt);
+          issue_ab(c.kbeg + (kt + 1) * GL_BK, nxt);
         } else if (has_next) {  // the next tile's first slab streams in (this tile's stages are done)
           cn = tile_coord<BNT, BMT>(g, x, tnext, G);
           init_ab(cn);
@@ -2303,7 +2193,7 @@ __global__ __launch_bounds__(glds_threads(BMT), (glds_occupancy<BNT, EPI, BMT, P
       for (int kt = 0; kt + 1 < c.nk; ++kt) {  // all but the last slab: slab kt+1 streams in
         const int k1 = c.kbeg + (kt + 1) * GL_BK;
         float* nxt = smem + (buf ^ 1) * BUF;  // last read before the previous barrier
-        if (!(kGemmAbl & 1)) issue_ab(k1, nxt);
+        issue_ab(k1, nxt);
         compute(smem + buf * BUF, GL_BK);
         finish_slab();
       }
@@ -2336,11 +2226,11 @@ __global__ __launch_bounds__(glds_threads(BMT), (glds_occupancy<BNT, EPI, BMT, P
       float* Wz = g.work + ((long)c.split * g.batch + c.z) * ((long)g.sk_mp * g.sk_np);
       store_cols<EPI_P0, TM, TN, true, 16>(g, 0, g.sk_np, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, lane, acc, Wz);
       splitk_combine<BMT, BNT>(g, c.z, c.m0 / BMT, c.tn, x.ntx, x.nty, reinterpret_cast<int*>(smem + ST * BUF));
-    } else if (!(kGemmAbl & 2)) {
+    } else {
       float* W = g.splits > 1 ? g.work + ((long)c.split * g.batch + c.z) * (long)g.M * g.N : nullptr;
       if constexpr (EPI >= EPI_BIAS) {  // specialised kinds: never split-K, always wide
         const int mr0 = c.m0 + wm * TM * 32, nc0 = c.n0 + wn * TN * 32;
-        if (col_epi_ok<EPI>() && !(kGemmAbl & 64) && mr0 + TM * 32 <= g.M && nc0 + TN * 32 <= g.N) {
+        if (col_epi_ok<EPI>() && mr0 + TM * 32 <= g.M && nc0 + TN * 32 <= g.N) {
           const long cb = c_base(g, c.z);
           if (g.alpha == 1.0f) store_cols<EPI, TM, TN, true>(g, cb, g.ldc, mr0, nc0, lane, acc, g.c);
           else store_cols<EPI, TM, TN, false>(g, cb, g.ldc, mr0, nc0, lane, acc, g.c);
@@ -2348,10 +2238,10 @@ __global__ __launch_bounds__(glds_threads(BMT), (glds_occupancy<BNT, EPI, BMT, P
           store_spec_tiles<EPI, TM, TN>(g, c.z, mr0, nc0, lane, acc);
         }
       } else if (g.wide) {
-        if (W && !(kGemmAbl & 64) && c.m0 + wm * TM * 32 + TM * 32 <= g.M && c.n0 + wn * TN * 32 + TN * 32 <= g.N)
+        if (W && c.m0 + wm * TM * 32 + TM * 32 <= g.M && c.n0 + wn * TN * 32 + TN * 32 <= g.N)
           store_cols<EPI_P0, TM, TN, true>(g, 0, g.N, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, lane, acc, W);
         else if (W) store_partials_wide<TM, TN>(g, W, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, lane, acc);
-        else store_tiles_wide<EPI, TM, TN>(g, c.z, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, lane, acc, (kGemmAbl & 32) != 0);
+        else store_tiles_wide<EPI, TM, TN>(g, c.z, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, lane, acc, false);
       } else {
         if (W) store_partials<TM, TN>(g, W, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, h, l32, acc);
         else store_tiles<EPI, TM, TN>(g, c.z, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, h, l32, acc);
@@ -2395,7 +2285,7 @@ bool glds_switch(int ma, int mb, int bnt, int prec, int bm, F&& f) {
         else return false;
       } else if constexpr ((small_ok || (MA_ == I2C_KC && MB_ == KC) || (MA_ == I2CT_KC && MB_ == RC) ||
                             (MA_ == RC && MB_ == I2C_RC)) &&
-                           (decltype(R)::value == BM || (ESP_GEMM_WIDE && decltype(R)::value == 256))) {
+                           decltype(R)::value == BM) {
         // bf16 operands: KC / RC pairs, and the conv2 forward / input gradient (implicit-im2col A of
         // bf16 pairs: the gathers run in pair units, C % 64 == 0) / weight gradient (gathered bf16 B)
         f(A, B, N, IC<2>{}, R);
@@ -2410,10 +2300,9 @@ bool glds_switch(int ma, int mb, int bnt, int prec, int bm, F&& f) {
       }
       return false;
     }
-    if (bm == 256) {  // 256 x 128 tiles, 8 waves: KC x RC on B planes (default build, ESP_GEMM_WIDE_KCRC); every
-                      // fp32 / B-planes / bf16-operand pair in an ESP_GEMM_WIDE build
-      if constexpr ((ESP_GEMM_WIDE && (MA_ != RC || MB_ != I2C_RC)) || (ESP_GEMM_WIDE_KCRC && MA_ == KC && MB_ == RC)) {
-        if (bnt == 128 && (ESP_GEMM_WIDE ? prec != 5 : prec == 3)) return by_prec(IC<128>{}, IC<256>{});
+    if (bm == 256) {  // 256 x 128 tiles, 8 waves: KC x RC on B planes (ESP_GEMM_WIDE_KCRC)
+      if constexpr (ESP_GEMM_WIDE_KCRC && MA_ == KC && MB_ == RC) {
+        if (bnt == 128 && prec == 3) return by_prec(IC<128>{}, IC<256>{});
       }
       return false;
     }

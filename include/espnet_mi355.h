@@ -366,6 +366,10 @@ int esp_attn_dscores(const float* dctx, long ldd, const float* vmat, long ldv, c
  * lds % 4 == 0 (columns T .. round_up(T, 4) - 1 of the pitch are written as 0).  Replaces, for these shapes, the
  * reference's matrix_ac / matrix_bd matmuls + rel_shift + softmax + dropout
  * (attention.py:240-263, 64-96). */
+/* ABI 31: the relpos_probs_lds_kernel LDS slot-schedule check (attention.hip; a debug build, make
+ * VARIANT=_slotchk EXTRA=-DESP_ATTN_SLOT_CHECK=1): slot-generation mismatches counted since the last call
+ * (the count is reset), -1 in a build without the check. */
+int esp_attn_slot_check_errors(void);
 int esp_relpos_attn_probs(const float* qu, const float* qv, const float* kmat, long ldk, const float* p,
                           long ldp_row, int relpos, int nb, int H, float sqrt_dk, const int* klen,
                           float* attn, float* pdrop, float drop_p, unsigned long long seed, int T,

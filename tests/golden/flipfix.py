@@ -13,9 +13,12 @@ fp64 run:
   conv1 flip at (b, c, t1, f1), g1 = dL/d relu1:   d conv.0.weight[c, 0, i, j] = g1 x[b, 2t1+i, 2f1+j],
                                                   d conv.0.bias[c] = g1
   conv2 flip at (b, o, t2, f2), g2 = dL/d relu2:   d relu1[b, c, 2t2+kt, 2f2+kf] = g2 W2[o, c, kt, kf], through
-                                                  relu1's (fp64) mask into conv.0 as above
+                                                  relu1's (fp64) mask into conv.0 as above; and (round 6)
+                                                  d conv.2.weight[o, c, kt, kf] = g2 relu1[b, c, 2t2+kt, 2f2+kf],
+                                                  d conv.2.bias[o] = g2 (conv2d6: 5 x 5, stride 3)
   decoder flip at (b, l, u), g = dL/d relu:        d norm3.weight[c] = g W1[u, c] xhat[b, l, c],
-                                                  d norm3.bias[c] = g W1[u, c]
+                                                  d norm3.bias[c] = g W1[u, c]; and (round 6)
+                                                  d w_1.weight[u, c] = g y[b, l, c], d w_1.bias[u] = g
 
 The GPU test reads its own decisions at those positions (tests/helpers.FlipProbe) and subtracts
 (s_gpu - s64) x contribution; the fixture's fp32 slices are corrected the same way with the fp32
@@ -36,6 +39,9 @@ import numpy as np
 import torch
 
 CONV_TENSORS = ("encoder.embed.conv.0.weight", "encoder.embed.conv.0.bias")
+# round 6: a flip at the second ReLU also moves the second convolution's own gradient (row o of conv.2), and a
+# decoder flip the FFN's w_1 row u -- single rows, which the whole-tensor row-norm fingerprint sees
+CONV2_TENSORS = ("encoder.embed.conv.2.weight", "encoder.embed.conv.2.bias")
 
 
 class Records:
@@ -135,11 +141,12 @@ class OracleProbe:
         F = torch.nn.functional
         self._sub, self._ffn = O.conv2d_subsampling, O.ffn
 
-        def sub(P_, pre, x, mask):
+        def sub(P_, pre, x, mask, input_layer="conv2d"):
             rec.conv["x"] = x
             pre1 = F.conv2d(x.unsqueeze(1), P_[pre + ".conv.0.weight"], P_[pre + ".conv.0.bias"], stride=2)
             out1 = F.relu(pre1)
-            pre2 = F.conv2d(out1, P_[pre + ".conv.2.weight"], P_[pre + ".conv.2.bias"], stride=2)
+            pre2 = F.conv2d(out1, P_[pre + ".conv.2.weight"], P_[pre + ".conv.2.bias"],
+                            stride=2 if input_layer == "conv2d" else 3)
             out2 = F.relu(pre2)
             for v in (out1, out2):
                 if v.requires_grad:
@@ -147,7 +154,9 @@ class OracleProbe:
             rec.conv.update(pre1=pre1, out1=out1, pre2=pre2, out2=out2, W2=P_[pre + ".conv.2.weight"])
             b, c, t, f = out2.size()
             y = O.linear(P_, pre + ".out.0", out2.transpose(1, 2).contiguous().view(b, t, c * f))
-            return y, mask[:, :, :-2:2][:, :, :-2:2]
+            if input_layer == "conv2d":
+                return y, mask[:, :, :-2:2][:, :, :-2:2]
+            return y, mask[:, :, :-2:2][:, :, :-4:3]
 
         def ffn(P_, pre, x, act, p_drop=0.0, training=True):
             if not (pre.startswith("decoder.") and act == "relu"):
@@ -191,20 +200,37 @@ def flip_records(r64: Records, r32: Records, slice_idx, out: dict, gs32: dict, l
     def allidx(name):
         return np.arange(shapes[name], dtype=np.int64) if shapes else None
 
-    def add(name, site, idx, s64, s32, c, cfull=None):
+    def signs(name):
+        if name not in sg:
+            sg[name] = FP.signs(name, shapes[name])
+        return sg[name]
+
+    def add(name, site, idx, s64, s32, c, cfull=None, cp=None, rows=None):
+        """c: [k, S] contributions to the slice; cfull: [k, numel] to every element (small tensors) or cp:
+        [k, N_PROJ] directly to the projections; rows: the row each site moves (row-sparse tensors)."""
         site = prefix + site
         out[f"flip/{name}/{site}/idx"] = idx.numpy().astype(np.int64)
         out[f"flip/{name}/{site}/s64"] = s64.numpy().astype(np.int8)
         out[f"flip/{name}/{site}/s32"] = s32.numpy().astype(np.int8)
         out[f"flip/{name}/{site}/c"] = c.numpy().astype(np.float64)
+        if rows is not None:
+            out[f"flip/{name}/{site}/rows"] = rows.numpy().astype(np.int64)
         ds = (s32.double() - s64.double())[:, None]  # fp32's flips relative to fp64
         corr[name] = corr.get(name, 0.0) + (ds * c).sum(0)
         if cfull is not None:
-            if name not in sg:
-                sg[name] = FP.signs(name, shapes[name])
-            cp = cfull @ sg[name].T  # [k, N_PROJ]
+            cp = cfull @ signs(name).T  # [k, N_PROJ]
+        if cp is not None:
             out[f"flip/{name}/{site}/cp"] = cp.numpy().astype(np.float64)
             corr_fp[name] = corr_fp.get(name, 0.0) + (ds * cp).sum(0)
+
+    def row_cp(name, rows, vals):
+        """projection contributions of sites that each move one row: vals [k, R] the row's values, rows [k]"""
+        sgn = signs(name).view(FP.N_PROJ, -1, vals.shape[1])  # [P, rows, R]
+        cp = torch.zeros(len(rows), FP.N_PROJ, dtype=torch.float64)
+        for a in range(0, len(rows), 256):
+            r = rows[a:a + 256]
+            cp[a:a + 256] = torch.einsum("kj,pkj->kp", vals[a:a + 256], sgn[:, r, :])
+        return cp
 
     if r64.conv:
         c64, c32 = r64.conv, r32.conv
@@ -222,13 +248,17 @@ def flip_records(r64: Records, r32: Records, slice_idx, out: dict, gs32: dict, l
                              torch.zeros(len(b), len(ib), dtype=torch.float64))
             return cw, cb
 
+        # the second convolution: 3 x 3 stride 2 (conv2d) or 5 x 5 stride 3 (conv2d6, Conv2dSubsampling6)
+        k2 = W2.shape[2]
+        s2 = {3: 2, 5: 3}[k2]
+
         def conv2_contrib(b, o, t2, f2, gg, iw, ib):
             wc, wi, wj = iw // 9, (iw % 9) // 3, iw % 3
             cw = torch.zeros(len(b), len(iw), dtype=torch.float64)
             cb = torch.zeros(len(b), len(ib), dtype=torch.float64)
-            for kt in range(3):
-                for kf in range(3):
-                    tt, ff = 2 * t2 + kt, 2 * f2 + kf
+            for kt in range(k2):
+                for kf in range(k2):
+                    tt, ff = s2 * t2 + kt, s2 * f2 + kf
                     # weight elements (c', i, j)
                     m = (pre1[b[:, None], wc[None], tt[:, None], ff[:, None]] > 0).double()
                     wv = W2[o[:, None], wc[None], kt, kf]
@@ -267,6 +297,27 @@ def flip_records(r64: Records, r32: Records, slice_idx, out: dict, gs32: dict, l
                                    torch.from_numpy(allidx(CONV_TENSORS[1])))
         add(CONV_TENSORS[0], "conv2", near, s64, s32, cw, fw)
         add(CONV_TENSORS[1], "conv2", near, s64, s32, cb, fb)
+        # the same sites' direct share of conv.2's gradient: d W2[o, c, kt, kf] = g2 out1[b, c, s2 t2 + kt,
+        # s2 f2 + kf], d b2[o] = g2 -- row o only
+        out1 = c64["out1"].double()
+        C = out1.shape[1]
+        CK = C * k2 * k2
+        j = torch.arange(CK)
+        jc, jt, jf = j // (k2 * k2), (j % (k2 * k2)) // k2, j % k2
+        i2 = torch.from_numpy(slice_idx(CONV2_TENSORS[0]))
+        eo, ec, et, ef = i2 // CK, (i2 % CK) // (k2 * k2), (i2 % (k2 * k2)) // k2, i2 % k2
+        xv = out1[b[:, None], ec[None], s2 * t2[:, None] + et[None], s2 * f2[:, None] + ef[None]]
+        cw2 = torch.where(o[:, None] == eo[None], gg[:, None] * xv, torch.zeros_like(xv))
+        ib2 = torch.from_numpy(slice_idx(CONV2_TENSORS[1]))
+        cb2 = torch.where(o[:, None] == ib2[None], gg[:, None].expand(-1, len(ib2)),
+                          torch.zeros(len(b), len(ib2), dtype=torch.float64))
+        cpw2 = cpb2 = None
+        if shapes:
+            vals = gg[:, None] * out1[b[:, None], jc[None], s2 * t2[:, None] + jt[None], s2 * f2[:, None] + jf[None]]
+            cpw2 = row_cp(CONV2_TENSORS[0], o, vals)
+            cpb2 = row_cp(CONV2_TENSORS[1], o, gg[:, None])
+        add(CONV2_TENSORS[0], "conv2", near, s64, s32, cw2, cp=cpw2, rows=o)
+        add(CONV2_TENSORS[1], "conv2", near, s64, s32, cb2, cp=cpb2, rows=o)
         log(f"conv2: tau {tau2:.3g}, {len(b)} decisions, {(s64 != s32).sum().item()} flipped in fp32")
     for l, d64 in sorted(r64.dec.items()):
         d32 = r32.dec[l]
@@ -290,6 +341,21 @@ def flip_records(r64: Records, r32: Records, slice_idx, out: dict, gs32: dict, l
             c = dec_contrib(name, torch.from_numpy(slice_idx(name)))
             cf = dec_contrib(name, torch.from_numpy(allidx(name))) if shapes else None
             add(name, f"dec{l}", near, s64, s32, c, cf)
+        # the FFN's w_1 row u: d w_1.weight[u, c] = g y[b, p, c], d w_1.bias[u] = g
+        D = y.shape[2]
+        wn, bn = lay + ".feed_forward.w_1.weight", lay + ".feed_forward.w_1.bias"
+        iw1 = torch.from_numpy(slice_idx(wn))
+        yv = y[b[:, None], p[:, None], (iw1 % D)[None]]
+        cw1 = torch.where(u[:, None] == (iw1 // D)[None], g[:, None] * yv, torch.zeros_like(yv))
+        ib1 = torch.from_numpy(slice_idx(bn))
+        cb1 = torch.where(u[:, None] == ib1[None], g[:, None].expand(-1, len(ib1)),
+                          torch.zeros(len(b), len(ib1), dtype=torch.float64))
+        cpw1 = cpb1 = None
+        if shapes:
+            cpw1 = row_cp(wn, u, g[:, None] * y[b, p, :])
+            cpb1 = row_cp(bn, u, g[:, None])
+        add(wn, f"dec{l}", near, s64, s32, cw1, cp=cpw1, rows=u)
+        add(bn, f"dec{l}", near, s64, s32, cb1, cp=cpb1, rows=u)
         log(f"{lay}: tau {tau:.3g}, {len(b)} decisions, {(s64 != s32).sum().item()} flipped in fp32")
     for name, d in corr.items():
         out[f"gs_f32c/{name}"] = np.asarray(gs32[name], dtype=np.float64) - d.numpy()

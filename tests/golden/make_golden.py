@@ -576,7 +576,8 @@ def slurp_cfg_from_config(conf, V, dropout_zero=False):
                      positional_dropout_rate=z(e["positional_dropout_rate"]),
                      attention_dropout_rate=z(e["attention_dropout_rate"]),
                      rel_pos_type=e.get("rel_pos_type", "legacy"), macaron_style=e["macaron_style"],
-                     use_cnn_module=e["use_cnn_module"], cnn_module_kernel=e["cnn_module_kernel"]),
+                     use_cnn_module=e["use_cnn_module"], cnn_module_kernel=e["cnn_module_kernel"],
+                     input_layer=e.get("input_layer", "conv2d")),
         dec=O.DecCfg(attention_heads=d["attention_heads"], linear_units=d["linear_units"], num_blocks=d["num_blocks"],
                      dropout_rate=z(d["dropout_rate"]), positional_dropout_rate=z(d["positional_dropout_rate"]),
                      self_attention_dropout_rate=z(d["self_attention_dropout_rate"]),
@@ -620,6 +621,57 @@ def slurp_yaml_fixture():
     conf0["specaug"] = None
     fullsize_train_fixture("slurp_yaml_train", slurp_cfg_from_config(conf, V, dropout_zero=True), seed=62,
                            build=lambda: build_reference_from_config(conf0, V))
+
+
+LIBRISPEECH_YAML = "egs2/librispeech/asr1/conf/tuning/train_asr_conformer.yaml"
+
+
+def librispeech_config():
+    """The LibriSpeech-960 Conformer recipe's training config (the C4 corpus; run.sh's asr_config): d = 512,
+    H = 8, FF 2048, 12 blocks, input_layer conv2d6, macaron_style false, no rel_pos_type (the legacy default),
+    nbpe 5000 (run.sh).  asr.sh feeds it raw audio through DefaultFrontend (80 log-mel) + global_mvn; here the
+    80-dim features are the input and utterance_mvn the normalisation (the front end and GlobalMVN have their
+    own fixture, frontend.npz)."""
+    import yaml
+    with open(os.path.join(refshim.REF, LIBRISPEECH_YAML)) as f:
+        conf = yaml.safe_load(f)
+    keys = ("encoder", "encoder_conf", "decoder", "decoder_conf", "model_conf", "specaug", "specaug_conf",
+            "optim", "optim_conf", "scheduler", "scheduler_conf", "max_epoch", "best_model_criterion",
+            "keep_nbest_models", "accum_grad")
+    resolved = {k: conf[k] for k in keys if k in conf}
+    resolved.update(input_size=80, normalize="utterance_mvn", normalize_conf={}, ctc_conf={}, frontend=None,
+                    token_list_size=5000, source=LIBRISPEECH_YAML + " + egs2/librispeech/asr1/run.sh (nbpe 5000)")
+    return resolved
+
+
+def librispeech_yaml_fixture():
+    """The LibriSpeech Conformer recipe config end to end: the resolved config + the reference model's
+    state_dict layout as JSON, and the dropout-free / SpecAug-off architecture's full-size (B=2, T=1500) fp32 /
+    fp64 training step with every gradient summarised (input_layer conv2d6, no macaron FFN, legacy rel-pos)."""
+    import json
+    V = 5000
+    conf = librispeech_config()
+    ref = build_reference_from_config(conf, V)
+    sd = ref.state_dict()
+    cfg = slurp_cfg_from_config(conf, V)
+    P = O.deterministic_params(cfg, 0)
+    assert set(P) == set(sd), set(P) ^ set(sd)
+    conf["reference_state_dict"] = [[k, list(v.shape)] for k, v in sd.items()]
+    conf["reference_num_params"] = int(sum(p.numel() for p in ref.parameters()))
+    conf["reference_modules"] = {"encoder.embed": type(ref.encoder.embed).__name__,
+                                 "encoder.encoders.0.self_attn": type(ref.encoder.encoders[0].self_attn).__name__}
+    with open(os.path.join(HERE, "librispeech_asr_conformer_config.json"), "w") as f:
+        json.dump(conf, f, indent=1)
+    print("librispeech config:", conf["reference_num_params"], "params", conf["reference_modules"])
+    del ref
+    conf0 = json.loads(json.dumps(conf))
+    for sec in ("encoder_conf", "decoder_conf"):
+        for k in list(conf0[sec]):
+            if k.endswith("dropout_rate"):
+                conf0[sec][k] = 0.0
+    conf0["specaug"] = None
+    fullsize_train_fixture("librispeech_yaml_train", slurp_cfg_from_config(conf, V, dropout_zero=True), seed=64,
+                           ulens=(60, 45), build=lambda: build_reference_from_config(conf0, V))
 
 
 def frontend_fixture():
@@ -904,3 +956,5 @@ if __name__ == "__main__":
         slurp_yaml_fixture()
     if "trainrun" in which:
         trainrun_fixture()
+    if "librispeech" in which:
+        librispeech_yaml_fixture()

@@ -129,7 +129,8 @@ def cfg_from_config(conf, dropout_zero=False):
                      positional_dropout_rate=z(e["positional_dropout_rate"]),
                      attention_dropout_rate=z(e["attention_dropout_rate"]),
                      rel_pos_type=e.get("rel_pos_type", "legacy"), macaron_style=e["macaron_style"],
-                     use_cnn_module=e["use_cnn_module"], cnn_module_kernel=e["cnn_module_kernel"]),
+                     use_cnn_module=e["use_cnn_module"], cnn_module_kernel=e["cnn_module_kernel"],
+                     input_layer=e.get("input_layer", "conv2d")),
         dec=O.DecCfg(attention_heads=d["attention_heads"], linear_units=d["linear_units"], num_blocks=d["num_blocks"]),
         ctc_weight=conf["model_conf"]["ctc_weight"], lsm_weight=conf["model_conf"]["lsm_weight"],
         length_normalized_loss=conf["model_conf"]["length_normalized_loss"])
@@ -280,13 +281,25 @@ def fingerprint_gate(n, grad, g, gn64, flips=None):
     er = float(np.abs(p32 - p64).max()) / gn64
     if ep > max(1e-4, 2 * er):
         bad.append((n, "projection", ep, er))
-    if "rn_f64/" + n in g and not sites:
+    # rows: every row of a tensor without flip sites; of a tensor whose sites each move one row (conv.2, the
+    # decoder w_1: flip/<n>/<site>/rows), every row no recorded site touches; of the others (conv.0: a conv2 site
+    # reaches every channel through relu1's mask) none -- their corrected projections cover them
+    skip = None
+    if sites:
+        if all(f"{pre}{site}/rows" in g for site in sites):
+            skip = np.unique(np.concatenate([g[f"{pre}{site}/rows"] for site in sites] + [np.zeros(0, np.int64)]))
+        else:
+            skip = "all"
+    if "rn_f64/" + n in g and not (isinstance(skip, str)):
         r64 = g["rn_f64/" + n].astype(np.float64)
         rg = FP.row_norms(grad).cpu().numpy()
         er = float(g["rn_eref/" + n])
-        en = float(np.abs(rg - r64).max()) / max(float(r64.max()), 1e-300)
+        d = np.abs(rg - r64)
+        if skip is not None and len(skip):
+            d[skip] = 0.0
+        en = float(d.max()) / max(float(r64.max()), 1e-300)
         if en > max(1e-4, 2 * er):
-            bad.append((n, "rows", en, er, int(np.abs(rg - r64).argmax())))
+            bad.append((n, "rows", en, er, int(d.argmax())))
     return bad
 
 

@@ -199,3 +199,39 @@ def test_subsampling_block(dev, T, F, D, implicit, monkeypatch):
     y.backward(dout.double().reshape(B, T2, D))
     assert rel_err(out.cpu(), y.detach().reshape(B * T2, D)) < 1e-5
     _check_grads(mod, P, "e")
+
+
+@pytest.mark.parametrize("T", [29, 77, 130, 256, 300, 374, 384])
+@pytest.mark.parametrize("legacy", [False, True])
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_probs_lds_slot_schedule(dev, T, legacy, mode):
+    """relpos_probs_lds_kernel's LDS slot schedule (attention.hip, the audit above the kernel): every NTA
+    instantiation (8 / 16 / 24 key tiles), latest and legacy, the fp32 (six products) and bf16 forms, ragged
+    key lengths, dropout on.  In the slot-check build (ESP_LIB_VARIANT=_slotchk: per-wave generation words
+    checked before and after every fragment read) no read may overlap a write of its slot; in every build
+    the probabilities are finite and each row with keys sums to 1."""
+    from espnet_slurp_amd import _native
+    from espnet_slurp_amd import kernels as K
+    lib = _native.load()
+    lib.esp_attn_slot_check_errors()  # reset
+    B, H, dk = 3, 4, 64
+    D, Z = H * dk, 3 * H
+    P = T if legacy else 2 * T - 1
+    g = torch.Generator().manual_seed(T)
+    qkv = (torch.randn(B * T, 3 * D, generator=g) * 0.5).to(dev)
+    p = (torch.randn(P, D, generator=g) * 0.5).to(dev)
+    q_u = (torch.randn(Z * T * dk, generator=g) * 0.5).to(dev)
+    q_v = (torch.randn(Z * T * dk, generator=g) * 0.5).to(dev)
+    klen = torch.tensor([T, max(1, T - 7), max(1, T // 3)], dtype=torch.int32, device=dev)
+    Tp = K.pitch(T)
+    ac = torch.empty(Z * T * Tp, device=dev)
+    pdrop = torch.empty(Z * T * Tp, device=dev)
+    with K.gemm_compute(mode):
+        K.relpos_attn_probs(q_u, q_v, qkv, 3 * D, p, D, 2 if legacy else 1, B, H, math.sqrt(dk), klen, ac, pdrop,
+                            0.1, 1234, T, Tp, k_off=D)
+    torch.cuda.synchronize()
+    n = lib.esp_attn_slot_check_errors()
+    assert n in (-1, 0), f"{n} LDS slot-schedule violations"
+    a = ac.view(Z, T, Tp)[:, :, :T]
+    assert torch.isfinite(a).all()
+    assert torch.allclose(a.sum(-1), torch.ones(Z, T, device=dev), atol=1e-5)

@@ -55,13 +55,27 @@ def _trainer(dev, out, graph, max_epoch=None, dropout=None):
     return Trainer(model, opt, sch, opts, cuda_graph=graph), ref
 
 
-def _gate(rep, ref, tag):
+# Validation values only: the eval-mode BatchNorm reads its running mean, which tracks the depthwise
+# convolution's bias -- a parameter whose exact gradient is 0 (training-mode BatchNorm removes it), so its
+# computed gradient is rounding noise (~1e-17 in fp64, far larger in any fp32 pipeline), and Adam (eps 1e-9)
+# turns noise of 1e-9 or more into updates of order lr whose sign is the noise's.  The run with those gradients
+# set to their exact value 0 (test_trainer_run_exact_zero_grads) meets the plain gate on every value, so this
+# allowance is that noise's effect and nothing else; 5e-4 covers the largest validation difference measured
+# (3.1e-4 on loss_ctc ~ 22, r06a_pytest_gpu.log TRAINRUN_GATE lines).
+VALID_NOISE = 5e-4
+# parameters whose exact gradient is 0: the depthwise convolution's bias before training-mode BatchNorm and the
+# attention key biases (softmax is invariant to a per-row shift)
+_EXACT_ZERO = ("conv_module.depthwise_conv.bias", "linear_k.bias")
+
+
+def _gate(rep, ref, tag, valid_noise=0.0):
     """Every reporter value of the 3-epoch run against the reference's fp64 run of the same Trainer.run
     (trainrun_ref.json "values_f64", make_golden.py trainrun): within max(1e-4, 2 |ref32 - ref64|) -- the
     loss gate of every other test; the reference's own fp32 run is 1.5e-7 .. 1.2e-4 off fp64 over the 9
-    updates -- and acc exactly (both reference runs agree to the last bit: no argmax decision is near a tie;
-    1e-6 covers the fp32 / fp64 representation of the same fraction).  The learning rate is host arithmetic
-    (1e-9).  Every error is logged (TRAINRUN_GATE lines)."""
+    updates -- (+ valid_noise on the validation values, VALID_NOISE above) and acc exactly (both reference
+    runs agree to the last bit: no argmax decision is near a tie; 1e-6 covers the fp32 / fp64 representation
+    of the same fraction).  The learning rate is host arithmetic (1e-9).  Every error is logged
+    (TRAINRUN_GATE lines)."""
     fails = []
     for e, per in ref["values"].items():
         for ph, vals in per.items():
@@ -73,7 +87,7 @@ def _gate(rep, ref, tag):
                 elif k == "acc":
                     tol = 1e-6
                 else:
-                    tol = max(1e-4, 2 * abs(v - v64))
+                    tol = max(1e-4, 2 * abs(v - v64)) + (valid_noise if ph == "valid" else 0.0)
                 print(f"TRAINRUN_GATE {tag} e{e} {ph} {k} err={abs(got - v64):.3e} e_ref={abs(v - v64):.3e} tol={tol:.3e}")
                 if abs(got - v64) > tol:
                     fails.append((e, ph, k, got, v64, tol))
@@ -84,7 +98,7 @@ def _gate(rep, ref, tag):
 def test_trainer_run_matches_reference(dev, tmp_path, graph):
     tr, ref = _trainer(dev, tmp_path, graph)
     rep = tr.run(_Factory(TRAIN, dev), _Factory(VALID, dev))
-    _gate(rep, ref, f"run graph={graph}")
+    _gate(rep, ref, f"run graph={graph}", valid_noise=VALID_NOISE)
     files = sorted(p.name for p in tmp_path.iterdir())
     assert files == ref["files"], (files, ref["files"])
     links = {p.name: str(p.readlink()) for p in tmp_path.iterdir() if p.is_symlink()}
@@ -101,6 +115,26 @@ def test_trainer_run_matches_reference(dev, tmp_path, graph):
 
 
 @pytest.mark.parametrize("graph", [False, True])
+def test_trainer_run_exact_zero_grads(dev, tmp_path, graph, monkeypatch):
+    """The same run with the gradients that are exactly 0 in exact arithmetic (_EXACT_ZERO) set to 0 before
+    each clip + Adam (what the fp64 reference computes to ~1e-17): every value, validation included, within the
+    plain gate -- the evidence that VALID_NOISE is rounding noise on those parameters, amplified by Adam."""
+    from espnet_slurp_amd.train import trainer as T
+    tr, ref = _trainer(dev, tmp_path, graph)
+    views = [p.grad for n, p in tr.model.named_parameters() if n.endswith(_EXACT_ZERO)]
+    assert len(views) >= 4, len(views)
+    clip = T.clip_grad_norm_
+
+    def clip_exact(flat, max_norm, out):
+        for g in views:  # views into the flat gradient: device ops, captured into the graph step as well
+            g.zero_()
+        return clip(flat, max_norm, out)
+    monkeypatch.setattr(T, "clip_grad_norm_", clip_exact)
+    rep = tr.run(_Factory(TRAIN, dev), _Factory(VALID, dev))
+    _gate(rep, ref, f"exact-zero graph={graph}")
+
+
+@pytest.mark.parametrize("graph", [False, True])
 def test_trainer_run_resume(dev, tmp_path, graph):
     """Stop after 2 epochs, resume from checkpoint.pth in a fresh trainer for the 3rd
     (trainer.py:196-210): the same reporter values and files as one 3-epoch run."""
@@ -109,7 +143,7 @@ def test_trainer_run_resume(dev, tmp_path, graph):
     tr2, _ = _trainer(dev, tmp_path, graph)
     rep = tr2.run(_Factory(TRAIN, dev), _Factory(VALID, dev))
     assert rep.get_epoch() == 3
-    _gate(rep, ref, f"resume graph={graph}")
+    _gate(rep, ref, f"resume graph={graph}", valid_noise=VALID_NOISE)
     assert sorted(p.name for p in tmp_path.iterdir()) == ref["files"]
 
 
