@@ -109,8 +109,9 @@ class EncoderFn(torch.autograd.Function):
     flat gradient buffer (flat.py) and returns no input gradient (fbank needs none)."""
 
     @staticmethod
-    def forward(ctx, feats, anchor, enc, ilens_cpu, seed, grad_hook, klen=None, tvalid=None):
-        hs, olens, saved = enc.run_forward(feats, ilens_cpu, Seeds(seed), enc.training, klen=klen, tvalid=tvalid)
+    def forward(ctx, feats, anchor, enc, ilens_cpu, seed, grad_hook, klen=None, tvalid=None, inter=None):
+        kw = {} if inter is None else {"inter": inter}
+        hs, olens, saved = enc.run_forward(feats, ilens_cpu, Seeds(seed), enc.training, klen=klen, tvalid=tvalid, **kw)
         ctx.enc = enc
         ctx.saved = saved
         ctx.grad_hook = grad_hook
@@ -121,4 +122,4 @@ class EncoderFn(torch.autograd.Function):
     def backward(ctx, dhs):
         ctx.enc.run_backward(ctx.saved, dhs.contiguous(), ctx.grad_hook)
         ctx.saved = None
-        return None, None, None, None, None, None, None, None
+        return None, None, None, None, None, None, None, None, None

@@ -130,8 +130,8 @@ class ConformerEncoder(AbsEncoder):
             unsupported.append(f"{pos_enc_layer_type}/{selfattention_layer_type}")
         if activation_type != "swish":
             unsupported.append(f"activation_type={activation_type}")
-        if zero_triu or interctc_layer_idx or interctc_use_conditioning or layer_drop_rate:
-            unsupported.append("zero_triu/interctc/layer_drop")
+        if zero_triu or interctc_use_conditioning or layer_drop_rate:
+            unsupported.append("zero_triu/interctc_use_conditioning/layer_drop")
         sdr = stochastic_depth_rate if isinstance(stochastic_depth_rate, list) else [stochastic_depth_rate]
         if any(r != 0.0 for r in sdr):
             unsupported.append("stochastic_depth_rate")
@@ -153,7 +153,9 @@ class ConformerEncoder(AbsEncoder):
         self.dropout_rate = dropout_rate
         self.positional_dropout_rate = positional_dropout_rate
         self.max_pos_emb_len = max_pos_emb_len
-        self.interctc_layer_idx = interctc_layer_idx
+        if len(interctc_layer_idx) > 0:  # conformer_encoder.py:283-285
+            assert 0 < min(interctc_layer_idx) and max(interctc_layer_idx) < num_blocks
+        self.interctc_layer_idx = list(interctc_layer_idx)
         self.interctc_use_conditioning = interctc_use_conditioning
         self.flat = None
         self._seed_counter = 0
@@ -167,11 +169,15 @@ class ConformerEncoder(AbsEncoder):
             l.self_attn.flat = flat
 
     # ---------------------------------------------------------------- explicit passes
-    def run_forward(self, feats, ilens_cpu, seeds: Seeds, training: bool, klen=None, tvalid=None):
+    def run_forward(self, feats, ilens_cpu, seeds: Seeds, training: bool, klen=None, tvalid=None, inter=None):
         """tvalid: optional device int32 (1,) = the reference batch's T' when feats are padded
         to a length bucket (frames beyond are excluded from the convolution module's depthwise
         padding and BatchNorm statistics, and the legacy rel_shift is taken at T'; every other op
-        is per frame or masked by klen)."""
+        is per frame or masked by klen).
+        inter: the model's intermediate-CTC request (ESPnetASRModel._inter_request) -- after each block in
+        interctc_layer_idx the block output is normalised by after_norm (conformer_encoder.py:333-341) and its
+        CTC loss and loss gradient are formed right here, like the heads' CTC (fused into the forward); the
+        backward adds the gradient into the residual stream at that block (run_backward)."""
         B, T, _ = feats.shape
         lim = self.embed.min_frames  # check_short_utt (subsampling.py:31-39)
         if T < lim:
@@ -193,22 +199,48 @@ class ConformerEncoder(AbsEncoder):
         else:
             pos = tab
         ctxs = []
-        for layer in self.encoders:
+        inters = []
+        for li, layer in enumerate(self.encoders):
             x, c = layer.fwd(x, pos, klen, B, T2, seeds, training, tvalid=tvalid)
             ctxs.append(c)
+            if inter is not None and li + 1 in self.interctc_layer_idx:
+                inters.append(self._interctc_fwd(li + 1, x, B, T2, inter))
         hs, c_after = self.after_norm.fwd(x)
-        return hs.view(B, T2, D), olens, Ctx(emb=c_emb, layers=ctxs, after=c_after)
+        return hs.view(B, T2, D), olens, Ctx(emb=c_emb, layers=ctxs, after=c_after, inter=inters)
+
+    def _interctc_fwd(self, idx, x, B, T2, inter):
+        """One intermediate CTC branch: after_norm(x), its CTC nll (B,) and d(weighted loss)/d logits."""
+        y, c_ln = self.after_norm.fwd(x)
+        ctc = inter["ctc"]
+        nll, grad, _ = ctc.loss_and_grad(y, B, T2, inter["hlens"], inter["ys"], inter["tlens"], inter["Umax"],
+                                         inter["gscale"], want_grad=inter["want_grad"])
+        inter["nll"].append((idx, nll))
+        if grad is not None:
+            inter["grads"].append(grad)
+        return Ctx(idx=idx, y=y, c_ln=c_ln, grad=grad, ctc=ctc)
 
     def run_backward(self, saved, dhs, grad_hook=None):
         B, T2, D = dhs.shape
         d = self.after_norm.bwd_new(saved.after, dhs.view(B * T2, D))
-        if grad_hook is not None:
+        inter = {c.idx: c for c in (saved.get("inter") or []) if c.grad is not None}
+        # after_norm (and ctc_lo) receive more gradient from the intermediate branches below: their
+        # module-done hooks (the DP bucket launches) wait until the last branch is done
+        if grad_hook is not None and not inter:
             grad_hook(self.after_norm)
         for i in range(len(self.encoders) - 1, -1, -1):
+            ic = inter.get(i + 1)
+            if ic is not None:  # the intermediate branch read block i's output: its gradient joins d there
+                dy = torch.empty_like(ic.y)
+                ic.ctc.backward_from_logits(ic.grad, ic.y, dy)
+                self.after_norm.bwd(ic.c_ln, dy, d)
             d = self.encoders[i].bwd(saved.layers[i], d)
             saved.layers[i] = None
             if grad_hook is not None:
                 grad_hook(self.encoders[i])
+        if grad_hook is not None and inter:
+            grad_hook(self.after_norm)
+            grad_hook(next(iter(inter.values())).ctc)
+        saved.inter = None
         self.embed.bwd(saved.emb, d)
         if grad_hook is not None:
             grad_hook(self.embed)
@@ -223,14 +255,16 @@ class ConformerEncoder(AbsEncoder):
         return hs, K.h2d(olens, xs_pad.device), None
 
     def forward_prepared(self, feats: torch.Tensor, ilens_cpu: torch.Tensor, klen: torch.Tensor, seed: int,
-                         tvalid: torch.Tensor = None):
+                         tvalid: torch.Tensor = None, inter=None):
         """Encoder output hs (B, T', D) from device-resident inputs only (klen: int32 output
-        lengths on device): no host->device traffic, so it can be captured in a HIP graph."""
+        lengths on device): no host->device traffic, so it can be captured in a HIP graph.
+        inter: the model's intermediate-CTC request (run_forward)."""
         anchor = self.after_norm.weight
         hook = getattr(self, "_grad_hook", None)
         if torch.is_grad_enabled() and anchor.requires_grad:
-            return EncoderFn.apply(feats, anchor, self, ilens_cpu, seed, hook, klen, tvalid)
-        return self.run_forward(feats, ilens_cpu, Seeds(seed), self.training, klen=klen, tvalid=tvalid)[0]
+            return EncoderFn.apply(feats, anchor, self, ilens_cpu, seed, hook, klen, tvalid, inter)
+        return self.run_forward(feats, ilens_cpu, Seeds(seed), self.training, klen=klen, tvalid=tvalid,
+                                inter=inter)[0]
 
     def output_lengths(self, ilens_cpu: torch.Tensor, T: int) -> torch.Tensor:
         """Valid output frames per utterance (host, no device round trip)."""

@@ -102,8 +102,9 @@ class ESPnetASRModel(AbsESPnetModel):
             raise NotImplementedError("pre-/post-encoder/transducer are not on the hot path")
         if frontend is not None and not hasattr(frontend, "apply_prepared"):
             raise NotImplementedError("frontend: only the native DefaultFrontend (frontend: default)")
-        if interctc_weight != 0.0 or lang_token_id != -1:
-            raise NotImplementedError("interctc / lang_token_id")
+        if lang_token_id != -1:
+            raise NotImplementedError("lang_token_id")
+        assert 0.0 <= interctc_weight < 1.0, interctc_weight  # espnet_model.py:71
         self.blank_id = token_list.index(sym_blank)
         self.sos = token_list.index(sym_sos) if sym_sos in token_list else vocab_size - 1
         self.eos = token_list.index(sym_eos) if sym_eos in token_list else vocab_size - 1
@@ -141,6 +142,22 @@ class ESPnetASRModel(AbsESPnetModel):
         return self.flat
 
     # ------------------------------------------------------------------ heads
+    def _inter_request(self, prep: "Prepared", want_grad: bool):
+        """Intermediate CTC (espnet_model.py:222-245, conformer_encoder.py:333-350): the request the encoder
+        fills in its forward -- the shared CTC module, the targets, and the gradient scale of each branch,
+        ctc_weight * interctc_weight / (n_layers * B) (loss = ctc_weight ((1 - w) loss_ctc + w mean_l
+        loss_interctc_l) + (1 - ctc_weight) loss_att).  None when the model has no intermediate branch."""
+        idx = getattr(self.encoder, "interctc_layer_idx", None)
+        if self.interctc_weight == 0.0 or not idx or self.ctc is None:
+            prep["inter"] = None
+            return None
+        d = prep.dev
+        inter = dict(ctc=self.ctc, hlens=d["hlens"], ys=d["ys"], tlens=d["tlens"], Umax=prep.Umax,
+                     gscale=self.ctc_weight * self.interctc_weight / (len(idx) * prep.B), want_grad=want_grad,
+                     nll=[], grads=[], stats={})
+        prep["inter"] = inter
+        return inter
+
     def _heads_forward(self, hs, prep: "Prepared", seeds: Seeds, want_grad: bool):
         B, T, D = hs.shape
         dev = hs.device
@@ -149,10 +166,25 @@ class ESPnetASRModel(AbsESPnetModel):
         hlens_i32 = d["hlens"]
         state = {"hs2d": hs2d, "B": B, "T": T}
         nll = grad_ctc = None
+        inter = prep.get("inter")
+        w_ic = self.interctc_weight if inter else 0.0
         if self.ctc is not None:
             nll, grad_ctc, _ = self.ctc.loss_and_grad(hs2d, B, T, hlens_i32, d["ys"], d["tlens"], prep.Umax,
-                                                      self.ctc_weight / B, want_grad=want_grad)
+                                                      self.ctc_weight * (1.0 - w_ic) / B, want_grad=want_grad)
             state["grad_ctc"] = grad_ctc
+        nll_main = nll
+        if inter:
+            # loss_ctc of the loss = (1 - w) loss_ctc + w mean_l loss_interctc_l, each utterance's inf zeroed in
+            # its own CTC first (zero_infinity, ctc.py:44-45); the reported loss_ctc stays the main branch's
+            zi = self.ctc.zero_infinity
+            z = (lambda v: torch.where(torch.isinf(v), torch.zeros_like(v), v)) if zi else (lambda v: v)
+            comb = z(nll) * (1.0 - w_ic)
+            for idx, nl in inter["nll"]:
+                comb = comb + z(nl) * (w_ic / len(inter["nll"]))
+                inter["stats"][f"loss_interctc_layer{idx}"] = (z(nl).sum() / B).float().view(1)
+            state["loss_ctc_main"] = (z(nll).sum() / B).float().view(1)
+            state["inter"] = inter
+            nll = comb
         row_loss = row_stat = None
         R = 0
         # length_normalized_loss: the denominator is this batch's target count, taken on device
@@ -177,6 +209,8 @@ class ESPnetASRModel(AbsESPnetModel):
                         denom, self.ctc_weight, out4)
         if ln and self.decoder is not None:
             state["inv_denom"] = out4[4:5]
+        if inter:  # out4[0] (the stats' loss_ctc): the main branch's, the loss out4[3] already has the mix
+            out4[0:1].copy_(state["loss_ctc_main"])
         return out4, state
 
     def _heads_backward(self, state, g_loss, hook=None):
@@ -187,7 +221,11 @@ class ESPnetASRModel(AbsESPnetModel):
             g = state["grad_ctc"]
             K.scale_by_dev(g, g_loss)
             self.ctc.backward_from_logits(g, hs2d, dhs)
-            if hook is not None:
+            inter = state.get("inter")
+            if inter:  # the intermediate branches' loss gradients, applied in the encoder backward (which hooks ctc)
+                for gi in inter["grads"]:
+                    K.scale_by_dev(gi, g_loss)
+            elif hook is not None:
                 hook(self.ctc)
         if self.decoder is not None:
             g = state["grad_att"]
@@ -279,7 +317,10 @@ class ESPnetASRModel(AbsESPnetModel):
             feats = self.specaug.apply_prepared(feats, d["lens"], draws)
         if self.normalize is not None:
             feats = self.normalize.apply_prepared(feats, d["lens"])
-        encoder_out = self.encoder.forward_prepared(feats, prep.sl_cpu, d["hlens"], prep.enc_seed, d.get("tvalid"))
+        grad_on = torch.is_grad_enabled() and next(iter(self.parameters())).requires_grad
+        inter = self._inter_request(prep, grad_on)
+        encoder_out = self.encoder.forward_prepared(feats, prep.sl_cpu, d["hlens"], prep.enc_seed, d.get("tvalid"),
+                                                    **({"inter": inter} if inter else {}))
         anchor = next(p for p in (self.ctc or self.decoder).parameters())
         if torch.is_grad_enabled() and anchor.requires_grad:
             loss, others = HeadsFn.apply(encoder_out, anchor, self, prep, prep.heads_seed)
@@ -294,6 +335,8 @@ class ESPnetASRModel(AbsESPnetModel):
             cer=None, wer=None,
             loss=loss.detach(),
         )
+        if inter:
+            stats.update({k: v.detach() for k, v in inter["stats"].items()})
         if not self.training and self.error_calculator is not None:
             stats.update(self._error_rates(encoder_out, prep))
         return loss, stats, d["weight"]
@@ -315,8 +358,9 @@ class ESPnetASRModel(AbsESPnetModel):
             if self.normalize is not None:
                 feats = self.normalize.apply_prepared(feats, d["lens"])
             enc = self.encoder
+            inter = self._inter_request(prep, True)
             hs, _olens, saved = enc.run_forward(feats, prep.sl_cpu, Seeds(prep.enc_seed), enc.training, klen=d["hlens"],
-                                                tvalid=d.get("tvalid"))
+                                                tvalid=d.get("tvalid"), **({"inter": inter} if inter else {}))
             out4, state = self._heads_forward(hs, prep, Seeds(prep.heads_seed), True)
         loss, others = out4[3:4], out4[0:3]
         stats = dict(
@@ -327,6 +371,8 @@ class ESPnetASRModel(AbsESPnetModel):
             cer=None, wer=None,
             loss=loss,
         )
+        if inter:
+            stats.update(inter["stats"])
         return loss, stats, d["weight"], (saved, state)
 
     def backward_explicit(self, ctx, g_loss: torch.Tensor, hook=None):

@@ -43,6 +43,7 @@ class EncCfg:
     cnn_module_kernel: int = 31
     max_pos_emb_len: int = 5000
     input_layer: str = "conv2d"      # conv2d | conv2d6 (Conv2dSubsampling6, subsampling.py:101-146)
+    interctc_layer_idx: Tuple[int, ...] = ()  # intermediate CTC layers (conformer_encoder.py:283-285,333-350)
 
 
 @dataclass
@@ -62,6 +63,7 @@ class ModelCfg:
     enc: EncCfg = field(default_factory=EncCfg)
     dec: Optional[DecCfg] = field(default_factory=DecCfg)
     ctc_weight: float = 0.3
+    interctc_weight: float = 0.0     # espnet_model.py:54,222-245
     lsm_weight: float = 0.1
     ignore_id: int = -1
     length_normalized_loss: bool = False
@@ -305,8 +307,14 @@ def encoder(P, feats, lens, cfg: EncCfg, bn_state=None, training=True):
         pos = pos.to(x.dtype)
         x = dropout(x, cfg.positional_dropout_rate, training)
         pos = dropout(pos, cfg.positional_dropout_rate, training)
+        inter = []
         for i in range(cfg.num_blocks):
             x = conformer_layer(P, f"encoder.encoders.{i}", x, pos, masks, cfg, bn_state, training)
+            if i + 1 in cfg.interctc_layer_idx:  # intermediate outputs are also normalised (:337-341)
+                inter.append((i + 1, layer_norm(P, "encoder.after_norm", x)))
+        if inter:
+            x = layer_norm(P, "encoder.after_norm", x)
+            return (x, inter), masks.squeeze(1).sum(1)
     else:
         x = x * math.sqrt(D) + abs_pos_table(Tp, D).to(x.dtype)
         x = dropout(x, cfg.positional_dropout_rate, training)
@@ -442,11 +450,21 @@ def asr_forward(P: Params, speech, speech_lengths, text, text_lengths, cfg: Mode
             feats = mask_along_axis_fixed(feats, specaug["time_pos"], specaug["time_len"], 1)
     feats = utterance_mvn(feats, lens)
     hs, hlens = encoder(P, feats, lens, cfg.enc, bn_state, training)
+    inter = None
+    if isinstance(hs, tuple):
+        hs, inter = hs
     stats = {}
     loss_ctc = loss_att = acc = None
     if cfg.ctc_weight != 0.0:
         loss_ctc = ctc_loss(P, hs, hlens, text, text_lengths, cfg.blank_id)
         stats["loss_ctc"] = loss_ctc.detach()
+    if cfg.interctc_weight != 0.0 and inter:  # espnet_model.py:222-245
+        loss_ic = 0.0
+        for idx, h in inter:
+            l_ic = ctc_loss(P, h, hlens, text, text_lengths, cfg.blank_id)
+            stats[f"loss_interctc_layer{idx}"] = l_ic.detach()
+            loss_ic = loss_ic + l_ic
+        loss_ctc = (1 - cfg.interctc_weight) * loss_ctc + cfg.interctc_weight * (loss_ic / len(inter))
     if cfg.ctc_weight != 1.0:
         ys_in, ys_out = add_sos_eos(text, cfg.sos, cfg.eos, cfg.ignore_id)
         dec_out = decoder(P, hs, hlens, ys_in, text_lengths + 1, cfg.dec, training)

@@ -58,7 +58,7 @@ def build_reference(cfg: O.ModelCfg):
             normalize_before=True, macaron_style=e.macaron_style, rel_pos_type=e.rel_pos_type,
             pos_enc_layer_type="rel_pos", selfattention_layer_type="rel_selfattn",
             activation_type="swish", use_cnn_module=e.use_cnn_module,
-            cnn_module_kernel=e.cnn_module_kernel)
+            cnn_module_kernel=e.cnn_module_kernel, interctc_layer_idx=list(e.interctc_layer_idx))
     else:
         enc = TransformerEncoder(
             input_size=e.input_size, output_size=e.output_size, attention_heads=e.attention_heads,
@@ -79,7 +79,7 @@ def build_reference(cfg: O.ModelCfg):
         vocab_size=cfg.vocab_size, token_list=token_list(cfg.vocab_size), frontend=None,
         specaug=None, normalize=UtteranceMVN(), preencoder=None, encoder=enc, postencoder=None,
         decoder=dec, ctc=ctc, joint_network=None, ctc_weight=cfg.ctc_weight,
-        lsm_weight=cfg.lsm_weight, length_normalized_loss=cfg.length_normalized_loss,
+        interctc_weight=cfg.interctc_weight, lsm_weight=cfg.lsm_weight, length_normalized_loss=cfg.length_normalized_loss,
         report_cer=False, report_wer=False)
     return model
 
@@ -113,7 +113,7 @@ def model_fixture(name, cfg, B, T, lens, ulens, seed, with_grads=True, dtype=tor
     loss.backward()
     out = dict(speech=speech.float().numpy(), speech_lengths=slen.numpy(), text=text.numpy(),
                text_lengths=tlen.numpy(), seed=np.int64(seed), loss=np.float64(loss.item()))
-    for k in ("loss_ctc", "loss_att"):
+    for k in ["loss_ctc", "loss_att"] + [k for k in stats if k.startswith("loss_interctc_layer")]:
         if stats.get(k) is not None:
             out[k] = np.float64(stats[k].item())
     if stats.get("acc") is not None:
@@ -911,6 +911,11 @@ if __name__ == "__main__":
                                    ("long_t875_legacy", "legacy", 3503, (3503, 3000)),
                                    ("long_t1100_latest", "latest", 4403, (4403, 3803))):
             fullsize_train_fixture(name, long_cfg(rel), B=2, T=T, lens=lens, ulens=(60, 45), seed=91)
+    if "interctc" in which:  # intermediate CTC (conformer_encoder.py:283-285,333-350; espnet_model.py:222-245)
+        cfg = small_cfg("latest", blocks=3)
+        cfg.enc.interctc_layer_idx = (1, 2)
+        cfg.interctc_weight = 0.3
+        model_fixture("model_small_interctc", cfg, 3, 120, [120, 97, 64], [9, 5, 7], 8)
     if "conv2d6" in which:  # input_layer conv2d6 (Conv2dSubsampling6, the LibriSpeech Conformer recipe's)
         cfg = small_cfg("latest")
         cfg.enc.input_layer = "conv2d6"

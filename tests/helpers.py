@@ -50,7 +50,8 @@ def build_model(cfg: O.ModelCfg, device, specaug=None, dropout=None, frontend=No
                                linear_units=e.linear_units, num_blocks=e.num_blocks, dropout_rate=p,
                                positional_dropout_rate=p, attention_dropout_rate=p, macaron_style=e.macaron_style,
                                rel_pos_type=e.rel_pos_type, use_cnn_module=e.use_cnn_module,
-                               cnn_module_kernel=e.cnn_module_kernel, input_layer=e.input_layer)
+                               cnn_module_kernel=e.cnn_module_kernel, input_layer=e.input_layer,
+                               interctc_layer_idx=list(e.interctc_layer_idx))
     else:
         enc = TransformerEncoder(input_size=e.input_size, output_size=e.output_size, attention_heads=e.attention_heads,
                                  linear_units=e.linear_units, num_blocks=e.num_blocks, dropout_rate=p,
@@ -66,7 +67,7 @@ def build_model(cfg: O.ModelCfg, device, specaug=None, dropout=None, frontend=No
     m = ESPnetASRModel(vocab_size=cfg.vocab_size, token_list=token_list(cfg.vocab_size), frontend=frontend,
                        specaug=specaug, normalize=UtteranceMVN(), preencoder=None, encoder=enc, postencoder=None,
                        decoder=dec, ctc=ctc, joint_network=None, ctc_weight=cfg.ctc_weight,
-                       lsm_weight=cfg.lsm_weight, length_normalized_loss=cfg.length_normalized_loss,
+                       interctc_weight=cfg.interctc_weight, lsm_weight=cfg.lsm_weight, length_normalized_loss=cfg.length_normalized_loss,
                        report_cer=False, report_wer=False)
     m = m.to(device)
     m.flatten()

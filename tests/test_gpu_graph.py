@@ -12,12 +12,15 @@ from tests.helpers import build_model, load_seeded, small_cfg
 pytestmark = pytest.mark.gpu
 
 
-def _trainer(dev, graph, dropout=0.0, seed=11, accum=1, lnorm=False):
+def _trainer(dev, graph, dropout=0.0, seed=11, accum=1, lnorm=False, interctc=False):
     from espnet_slurp_amd.optimizers.fused_adam import FusedAdam
     from espnet_slurp_amd.schedulers.warmup_lr import WarmupLR
     from espnet_slurp_amd.train.trainer import Trainer, TrainerOptions
-    cfg = small_cfg("latest")
+    cfg = small_cfg("latest", blocks=3 if interctc else 2)
     cfg.length_normalized_loss = lnorm
+    if interctc:
+        cfg.enc.interctc_layer_idx = (1, 2)
+        cfg.interctc_weight = 0.3
     model = build_model(cfg, dev, dropout=dropout)
     load_seeded(model, cfg, seed)
     model.train()
@@ -197,3 +200,34 @@ def test_skipped_steps_counted_in_graph_mode(dev):
         assert o.n_steps == 1
         assert t.train_one_epoch([(None, bad)]) is True
         assert t.train_one_epoch([(None, _copy(b))]) is False
+
+
+@pytest.mark.parametrize("dp", [False, True])
+def test_graph_interctc_matches_eager(dev, dp):
+    """Intermediate CTC (ConformerEncoder interctc_layer_idx, interctc_weight) under the HIP graph, plain and
+    through the data-parallel segmented capture on a 1-rank RCCL group (the module-done hooks of ctc /
+    after_norm wait for the intermediate branches): losses, the per-layer loss_interctc stats and the
+    parameters after 3 steps equal the eager steps'."""
+    import torch.distributed as dist
+    if dp:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29573")
+        dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        te, me, _, _ = _trainer(dev, False, interctc=True)
+        tg, mg, _, _ = _trainer(dev, True, interctc=True)
+        if dp:
+            from espnet_slurp_amd.train.trainer import Trainer
+            tg = Trainer(mg, tg.optimizer, tg.scheduler, tg.options, distributed=True, cuda_graph=True)
+        for _ in range(3):
+            se = te.train_one_step(_batch(dev))
+            sg = tg.train_one_step(_batch(dev))
+            for k in ("loss", "loss_ctc", "loss_interctc_layer1", "loss_interctc_layer2"):
+                a, b = se[k].item(), sg[k].item()
+                assert abs(a - b) <= (1e-5 if dp else 1e-6) * max(1.0, abs(a)), (k, a, b)
+        te.resolve_pending()
+        tg.sync_host_state()
+        assert torch.allclose(me.flat.flat, mg.flat.flat, rtol=0, atol=1e-5 if dp else 1e-6)
+    finally:
+        if dp:
+            dist.destroy_process_group()
