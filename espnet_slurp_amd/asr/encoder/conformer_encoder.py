@@ -130,8 +130,8 @@ class ConformerEncoder(AbsEncoder):
             unsupported.append(f"{pos_enc_layer_type}/{selfattention_layer_type}")
         if activation_type != "swish":
             unsupported.append(f"activation_type={activation_type}")
-        if zero_triu or interctc_use_conditioning or layer_drop_rate:
-            unsupported.append("zero_triu/interctc_use_conditioning/layer_drop")
+        if zero_triu or layer_drop_rate:
+            unsupported.append("zero_triu/layer_drop")
         sdr = stochastic_depth_rate if isinstance(stochastic_depth_rate, list) else [stochastic_depth_rate]
         if any(r != 0.0 for r in sdr):
             unsupported.append("stochastic_depth_rate")
@@ -156,6 +156,9 @@ class ConformerEncoder(AbsEncoder):
         if len(interctc_layer_idx) > 0:  # conformer_encoder.py:283-285
             assert 0 < min(interctc_layer_idx) and max(interctc_layer_idx) < num_blocks
         self.interctc_layer_idx = list(interctc_layer_idx)
+        # self-conditioning (conformer_encoder.py:286-287, 343-350): the model creates conditioning_layer =
+        # Linear(vocab, D) (espnet_model.py:96-101) and passes the CTC module to the forward
+        self.conditioning_layer = None
         self.interctc_use_conditioning = interctc_use_conditioning
         self.flat = None
         self._seed_counter = 0
@@ -204,25 +207,39 @@ class ConformerEncoder(AbsEncoder):
             x, c = layer.fwd(x, pos, klen, B, T2, seeds, training, tvalid=tvalid)
             ctxs.append(c)
             if inter is not None and li + 1 in self.interctc_layer_idx:
-                inters.append(self._interctc_fwd(li + 1, x, B, T2, inter))
+                x, ic = self._interctc_fwd(li + 1, x, B, T2, inter)
+                inters.append(ic)
         hs, c_after = self.after_norm.fwd(x)
         return hs.view(B, T2, D), olens, Ctx(emb=c_emb, layers=ctxs, after=c_after, inter=inters)
 
     def _interctc_fwd(self, idx, x, B, T2, inter):
-        """One intermediate CTC branch: after_norm(x), its CTC nll (B,) and d(weighted loss)/d logits."""
+        """One intermediate branch: y = after_norm(x), its CTC nll (B,) and d(weighted loss)/d logits (when the
+        model weights the branch), and with self-conditioning the new residual stream x + conditioning_layer(
+        softmax(ctc_lo(y))) (conformer_encoder.py:343-350).  Returns (x, branch context)."""
         y, c_ln = self.after_norm.fwd(x)
         ctc = inter["ctc"]
-        nll, grad, _ = ctc.loss_and_grad(y, B, T2, inter["hlens"], inter["ys"], inter["tlens"], inter["Umax"],
-                                         inter["gscale"], want_grad=inter["want_grad"])
-        inter["nll"].append((idx, nll))
-        if grad is not None:
-            inter["grads"].append(grad)
-        return Ctx(idx=idx, y=y, c_ln=c_ln, grad=grad, ctc=ctc)
+        nll = grad = lp = None
+        if inter["weighted"]:
+            nll, grad, lp = ctc.loss_and_grad(y, B, T2, inter["hlens"], inter["ys"], inter["tlens"], inter["Umax"],
+                                              inter["gscale"], want_grad=inter["want_grad"])
+            inter["nll"].append((idx, nll))
+            if grad is not None:
+                inter["grads"].append(grad)
+        prob = None
+        if self.conditioning_layer is not None:
+            if lp is None:
+                logits = ctc.logits(y)
+                lp = torch.empty_like(logits)
+                K.log_softmax(logits, lp, logits.shape[0], logits.shape[1])
+            prob = torch.exp(lp)  # ctc.softmax (ctc.py:100-108): exp of the log-softmax rows
+            x = self.conditioning_layer.fwd(prob, R=x, beta=1.0)  # x + W p + b
+        return x, Ctx(idx=idx, y=y, c_ln=c_ln, grad=grad, ctc=ctc, prob=prob,
+                      live=grad is not None or (prob is not None and inter["want_grad"]))
 
     def run_backward(self, saved, dhs, grad_hook=None):
         B, T2, D = dhs.shape
         d = self.after_norm.bwd_new(saved.after, dhs.view(B * T2, D))
-        inter = {c.idx: c for c in (saved.get("inter") or []) if c.grad is not None}
+        inter = {c.idx: c for c in (saved.get("inter") or []) if c.live}
         # after_norm (and ctc_lo) receive more gradient from the intermediate branches below: their
         # module-done hooks (the DP bucket launches) wait until the last branch is done
         if grad_hook is not None and not inter:
@@ -230,8 +247,19 @@ class ConformerEncoder(AbsEncoder):
         for i in range(len(self.encoders) - 1, -1, -1):
             ic = inter.get(i + 1)
             if ic is not None:  # the intermediate branch read block i's output: its gradient joins d there
+                if ic.prob is not None:
+                    # self-conditioning: d (x + W p + b) / d p = W^T d -> softmax adjoint into the logits (+ the
+                    # branch's CTC loss gradient), d x keeps d itself (the identity path)
+                    rows, V = ic.prob.shape
+                    dp = self.conditioning_layer.bwd(d, ic.prob)
+                    dl = torch.empty_like(dp)
+                    K.attn_softmax_bwd(ic.prob, dp, dl, 0.0, 0, 1.0, rows, V)
+                    if ic.grad is not None:
+                        dl.add_(ic.grad)
+                else:
+                    dl = ic.grad
                 dy = torch.empty_like(ic.y)
-                ic.ctc.backward_from_logits(ic.grad, ic.y, dy)
+                ic.ctc.backward_from_logits(dl, ic.y, dy)
                 self.after_norm.bwd(ic.c_ln, dy, d)
             d = self.encoders[i].bwd(saved.layers[i], d)
             saved.layers[i] = None
@@ -240,6 +268,8 @@ class ConformerEncoder(AbsEncoder):
         if grad_hook is not None and inter:
             grad_hook(self.after_norm)
             grad_hook(next(iter(inter.values())).ctc)
+            if self.conditioning_layer is not None:
+                grad_hook(self.conditioning_layer)
         saved.inter = None
         self.embed.bwd(saved.emb, d)
         if grad_hook is not None:

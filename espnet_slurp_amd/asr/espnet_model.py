@@ -16,7 +16,7 @@ import torch
 from torch import nn
 
 from .. import kernels as K
-from ..blocks import Seeds, empty
+from ..blocks import Linear, Seeds, empty
 from ..flat import FlatParams
 from .encoder.abs_encoder import draw_seed
 from .error_calculator import ErrorCalculator
@@ -119,6 +119,8 @@ class ESPnetASRModel(AbsESPnetModel):
         self.preencoder = preencoder
         self.postencoder = postencoder
         self.encoder = encoder
+        if getattr(encoder, "interctc_use_conditioning", False):  # espnet_model.py:96-101
+            encoder.conditioning_layer = Linear(vocab_size, encoder.output_size())
         self.decoder = None if ctc_weight == 1.0 else decoder
         self.ctc = None if ctc_weight == 0.0 else ctc
         self.lsm_weight = lsm_weight
@@ -148,13 +150,14 @@ class ESPnetASRModel(AbsESPnetModel):
         ctc_weight * interctc_weight / (n_layers * B) (loss = ctc_weight ((1 - w) loss_ctc + w mean_l
         loss_interctc_l) + (1 - ctc_weight) loss_att).  None when the model has no intermediate branch."""
         idx = getattr(self.encoder, "interctc_layer_idx", None)
-        if self.interctc_weight == 0.0 or not idx or self.ctc is None:
+        cond = getattr(self.encoder, "conditioning_layer", None) is not None
+        if not idx or self.ctc is None or (self.interctc_weight == 0.0 and not cond):
             prep["inter"] = None
             return None
         d = prep.dev
         inter = dict(ctc=self.ctc, hlens=d["hlens"], ys=d["ys"], tlens=d["tlens"], Umax=prep.Umax,
                      gscale=self.ctc_weight * self.interctc_weight / (len(idx) * prep.B), want_grad=want_grad,
-                     nll=[], grads=[], stats={})
+                     weighted=self.interctc_weight != 0.0, nll=[], grads=[], stats={})
         prep["inter"] = inter
         return inter
 
@@ -167,6 +170,11 @@ class ESPnetASRModel(AbsESPnetModel):
         state = {"hs2d": hs2d, "B": B, "T": T}
         nll = grad_ctc = None
         inter = prep.get("inter")
+        # (the encoder's intermediate branches also add ctc_lo gradient in its backward: the ctc module-done
+        # hook waits for them, _heads_backward)
+        state["inter_any"] = inter is not None
+        if inter is not None and not inter["weighted"]:  # self-conditioning only: no intermediate loss
+            inter = None
         w_ic = self.interctc_weight if inter else 0.0
         if self.ctc is not None:
             nll, grad_ctc, _ = self.ctc.loss_and_grad(hs2d, B, T, hlens_i32, d["ys"], d["tlens"], prep.Umax,
@@ -225,7 +233,7 @@ class ESPnetASRModel(AbsESPnetModel):
             if inter:  # the intermediate branches' loss gradients, applied in the encoder backward (which hooks ctc)
                 for gi in inter["grads"]:
                     K.scale_by_dev(gi, g_loss)
-            elif hook is not None:
+            if hook is not None and not state.get("inter_any"):
                 hook(self.ctc)
         if self.decoder is not None:
             g = state["grad_att"]

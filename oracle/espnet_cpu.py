@@ -44,6 +44,7 @@ class EncCfg:
     max_pos_emb_len: int = 5000
     input_layer: str = "conv2d"      # conv2d | conv2d6 (Conv2dSubsampling6, subsampling.py:101-146)
     interctc_layer_idx: Tuple[int, ...] = ()  # intermediate CTC layers (conformer_encoder.py:283-285,333-350)
+    interctc_use_conditioning: bool = False   # self-conditioning (conformer_encoder.py:343-350)
 
 
 @dataclass
@@ -311,7 +312,10 @@ def encoder(P, feats, lens, cfg: EncCfg, bn_state=None, training=True):
         for i in range(cfg.num_blocks):
             x = conformer_layer(P, f"encoder.encoders.{i}", x, pos, masks, cfg, bn_state, training)
             if i + 1 in cfg.interctc_layer_idx:  # intermediate outputs are also normalised (:337-341)
-                inter.append((i + 1, layer_norm(P, "encoder.after_norm", x)))
+                h = layer_norm(P, "encoder.after_norm", x)
+                inter.append((i + 1, h))
+                if cfg.interctc_use_conditioning:  # x + conditioning_layer(ctc.softmax(h)) (:343-350)
+                    x = x + linear(P, "encoder.conditioning_layer", torch.softmax(linear(P, "ctc.ctc_lo", h), dim=-1))
         if inter:
             x = layer_norm(P, "encoder.after_norm", x)
             return (x, inter), masks.squeeze(1).sum(1)
@@ -506,6 +510,8 @@ def param_shapes(cfg: ModelCfg) -> Dict[str, Tuple[int, ...]]:
     s["encoder.embed.conv.2.weight"] = (D, D, k2, k2)
     s["encoder.embed.conv.2.bias"] = (D,)
     lin("encoder.embed.out.0", D * F2, D)
+    if e.interctc_use_conditioning:  # espnet_model.py:96-101 (registered on the encoder, after its layers)
+        lin("encoder.conditioning_layer", V, D)
     for i in range(e.num_blocks):
         p = f"encoder.encoders.{i}"
         for n in ("q", "k", "v", "out"):

@@ -58,7 +58,8 @@ def build_reference(cfg: O.ModelCfg):
             normalize_before=True, macaron_style=e.macaron_style, rel_pos_type=e.rel_pos_type,
             pos_enc_layer_type="rel_pos", selfattention_layer_type="rel_selfattn",
             activation_type="swish", use_cnn_module=e.use_cnn_module,
-            cnn_module_kernel=e.cnn_module_kernel, interctc_layer_idx=list(e.interctc_layer_idx))
+            cnn_module_kernel=e.cnn_module_kernel, interctc_layer_idx=list(e.interctc_layer_idx),
+            interctc_use_conditioning=e.interctc_use_conditioning)
     else:
         enc = TransformerEncoder(
             input_size=e.input_size, output_size=e.output_size, attention_heads=e.attention_heads,
@@ -916,6 +917,8 @@ if __name__ == "__main__":
         cfg.enc.interctc_layer_idx = (1, 2)
         cfg.interctc_weight = 0.3
         model_fixture("model_small_interctc", cfg, 3, 120, [120, 97, 64], [9, 5, 7], 8)
+        cfg.enc.interctc_use_conditioning = True  # + self-conditioning (conformer_encoder.py:343-350)
+        model_fixture("model_small_interctc_cond", cfg, 3, 120, [120, 97, 64], [9, 5, 7], 9)
     if "conv2d6" in which:  # input_layer conv2d6 (Conv2dSubsampling6, the LibriSpeech Conformer recipe's)
         cfg = small_cfg("latest")
         cfg.enc.input_layer = "conv2d6"

@@ -51,7 +51,8 @@ def build_model(cfg: O.ModelCfg, device, specaug=None, dropout=None, frontend=No
                                positional_dropout_rate=p, attention_dropout_rate=p, macaron_style=e.macaron_style,
                                rel_pos_type=e.rel_pos_type, use_cnn_module=e.use_cnn_module,
                                cnn_module_kernel=e.cnn_module_kernel, input_layer=e.input_layer,
-                               interctc_layer_idx=list(e.interctc_layer_idx))
+                               interctc_layer_idx=list(e.interctc_layer_idx),
+                               interctc_use_conditioning=e.interctc_use_conditioning)
     else:
         enc = TransformerEncoder(input_size=e.input_size, output_size=e.output_size, attention_heads=e.attention_heads,
                                  linear_units=e.linear_units, num_blocks=e.num_blocks, dropout_rate=p,

@@ -12,7 +12,7 @@ from tests.helpers import build_model, load_seeded, small_cfg
 pytestmark = pytest.mark.gpu
 
 
-def _trainer(dev, graph, dropout=0.0, seed=11, accum=1, lnorm=False, interctc=False):
+def _trainer(dev, graph, dropout=0.0, seed=11, accum=1, lnorm=False, interctc=False, cond=False):
     from espnet_slurp_amd.optimizers.fused_adam import FusedAdam
     from espnet_slurp_amd.schedulers.warmup_lr import WarmupLR
     from espnet_slurp_amd.train.trainer import Trainer, TrainerOptions
@@ -21,6 +21,7 @@ def _trainer(dev, graph, dropout=0.0, seed=11, accum=1, lnorm=False, interctc=Fa
     if interctc:
         cfg.enc.interctc_layer_idx = (1, 2)
         cfg.interctc_weight = 0.3
+        cfg.enc.interctc_use_conditioning = cond
     model = build_model(cfg, dev, dropout=dropout)
     load_seeded(model, cfg, seed)
     model.train()
@@ -202,8 +203,8 @@ def test_skipped_steps_counted_in_graph_mode(dev):
         assert t.train_one_epoch([(None, _copy(b))]) is False
 
 
-@pytest.mark.parametrize("dp", [False, True])
-def test_graph_interctc_matches_eager(dev, dp):
+@pytest.mark.parametrize("dp,cond", [(False, False), (True, False), (False, True), (True, True)])
+def test_graph_interctc_matches_eager(dev, dp, cond):
     """Intermediate CTC (ConformerEncoder interctc_layer_idx, interctc_weight) under the HIP graph, plain and
     through the data-parallel segmented capture on a 1-rank RCCL group (the module-done hooks of ctc /
     after_norm wait for the intermediate branches): losses, the per-layer loss_interctc stats and the
@@ -214,8 +215,8 @@ def test_graph_interctc_matches_eager(dev, dp):
         os.environ.setdefault("MASTER_PORT", "29573")
         dist.init_process_group("nccl", rank=0, world_size=1)
     try:
-        te, me, _, _ = _trainer(dev, False, interctc=True)
-        tg, mg, _, _ = _trainer(dev, True, interctc=True)
+        te, me, _, _ = _trainer(dev, False, interctc=True, cond=cond)
+        tg, mg, _, _ = _trainer(dev, True, interctc=True, cond=cond)
         if dp:
             from espnet_slurp_amd.train.trainer import Trainer
             tg = Trainer(mg, tg.optimizer, tg.scheduler, tg.options, distributed=True, cuda_graph=True)
