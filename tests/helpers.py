@@ -156,12 +156,19 @@ class FlipProbe:
         from espnet_slurp_amd import blocks
         self._b = blocks
         self._sub, self._ffn = blocks.Conv2dSubsampling.fwd, blocks.PositionwiseFeedForward.fwd
+        self._sub6 = blocks.Conv2dSubsampling6.fwd
         probe = self
 
         def sub(mod, *a, **k):
             x, c = probe._sub(mod, *a, **k)
             probe.ctx["conv"] = c
             return x, c
+
+        def sub6(mod, *a, **k):  # conv2d6 (its own fwd): the same z1 / z2 decisions
+            x, c = probe._sub6(mod, *a, **k)
+            probe.ctx["conv"] = c
+            return x, c
+        blocks.Conv2dSubsampling6.fwd = sub6
 
         def ffn(mod, *a, **k):
             out, c = probe._ffn(mod, *a, **k)
@@ -172,6 +179,7 @@ class FlipProbe:
 
     def __exit__(self, *exc):
         self._b.Conv2dSubsampling.fwd, self._b.PositionwiseFeedForward.fwd = self._sub, self._ffn
+        self._b.Conv2dSubsampling6.fwd = self._sub6
 
     def decisions(self, site: str, idx: np.ndarray) -> np.ndarray:
         if self.copies == 1:

@@ -5,6 +5,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 rm -rf gpurun_out/prof_b
 bash gpurun_steps.sh \
+  "timeout -k 10 600 python -u -m pytest tests/test_librispeech_config.py tests/test_gpu_model.py tests/test_gpu_graph.py -m gpu -v -s -rf --timeout 300 --timeout-method thread > gpurun_out/r06b_pytest_new.log 2>&1" \
+  "timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/r06b_smoke.log 2>&1" \
   "timeout -k 10 400 python -u bench.py > gpurun_out/r06b_bench.log 2>&1" \
   "timeout -k 10 300 python -u bench.py --rel-pos legacy --no-cpu-baseline --feed-steps 0 > gpurun_out/r06b_bench_legacy.log 2>&1" \
   "timeout -k 10 300 python -u bench.py --dp-world1 --no-cpu-baseline --feed-steps 0 --steps 10 > gpurun_out/r06b_bench_dp_b256.log 2>&1" \
