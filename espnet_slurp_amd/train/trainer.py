@@ -330,8 +330,15 @@ class Trainer:
                 self._stats_avg(stats, keys, vec)
                 self.reducer.broadcast_buffers(model)
                 warm = {k: v.clone() for k, v in stats.items()}
+                del stats, w
             torch.cuda.current_stream(dev).wait_stream(side)
             torch.cuda.synchronize(dev)
+            # release the warm-up step's cached blocks before the capture allocates the graph pool, as
+            # torch.cuda.graph does on entry for the single-GPU capture: without it the DP step reserved the
+            # warm-up's activations AND the pool's (230 vs 155 GiB at C2 B=256, r06b_bench_dp_b256.log)
+            import gc
+            gc.collect()
+            torch.cuda.empty_cache()
             pool = torch.cuda.graph_pool_handle()
             cap = torch.cuda.Stream(device=dev)
             segs = []
