@@ -97,6 +97,8 @@ SIGNATURES = {
     "esp_global_mvn": [P, P, I, I, I, P, P, I, I, P],
     "esp_conv2_dgrad": [P, P, P, P, I, I, I, I, P, P, L, P],
     "esp_conv1_fwd": [P, P, P, P, I, I, I, I, P],
+    "esp_conv1_fwd_bits": [P, P, P, P, P, P, I, I, I, I, P],
+    "esp_conv2_dgrad_bits": [P, P, P, P, P, I, I, I, I, P, P, L, P],
     "esp_col2im_relu": [P, P, P, I, I, I, I, P],
     "esp_conv1_wgrad": [P, P, P, P, I, I, I, I, P, L, P],
     "esp_permute3": [P, P, I, I, I, I, P],
@@ -128,7 +130,7 @@ _RESTYPES = {"esp_last_error": ctypes.c_char_p, "esp_abi_version": I, "esp_attn_
              "esp_get_gemm_compute": I, "esp_set_splitk_mode": I,
              "esp_f32_gemm_products": I}
 _RESTYPES.update({k: L for k in SIGNATURES if k.endswith("_workspace_bytes")})
-ABI_VERSION = 31  # bumped whenever a signature in include/espnet_mi355.h changes
+ABI_VERSION = 32  # bumped whenever a signature in include/espnet_mi355.h changes
 
 _lib = None
 

@@ -587,7 +587,10 @@ class Conv2dSubsampling(nn.Module):
         b16 = K.conv2_bf16_ok(D)
         z1 = empty(B * T1 * F1 * D, like=feats)
         z1_16 = torch.empty(B * T1 * F1 * D, dtype=torch.bfloat16, device=feats.device) if b16 else None
-        K.conv1_fwd(feats, c0.weight, c0.bias, z1, B, T, F, D, z16=z1_16)
+        # training: the ReLU mask also as a packed bit map, the input gradient's mask operand (1/32 of z1's bytes)
+        z1bits = (torch.empty(B * T1 * F1 * D // 32, dtype=torch.int32, device=feats.device)
+                  if training and K.CONV2_DGRAD_BITS and K.CONV2_IMPLICIT_DGRAD and D % 32 == 0 else None)
+        K.conv1_fwd(feats, c0.weight, c0.bias, z1, B, T, F, D, z16=z1_16, zbits=z1bits)
         w2r = empty(D * 9 * D, like=feats)
         K.permute3(c2.weight, w2r, D, D, 9)
         z2 = empty(B * T2 * F2, D, like=feats)
@@ -607,8 +610,8 @@ class Conv2dSubsampling(nn.Module):
         sd = seeds.next()
         K.linear_fwd(z2.view(B * T2, F2 * D), wor.view(D, F2 * D), lin.bias, x, alpha=xscale, drop_p=pd, seed=sd,
                      b_weight=True)
-        return x, Ctx(feats=feats, z1=z1, z1_16=z1_16 if training else None, w2r=w2r, z2=z2, wor=wor, pd=pd, sd=sd,
-                      xscale=xscale, B=B, T=T, F=F, T1=T1, F1=F1, T2=T2, F2=F2)
+        return x, Ctx(feats=feats, z1=z1, z1_16=z1_16 if training else None, z1bits=z1bits, w2r=w2r, z2=z2, wor=wor,
+                      pd=pd, sd=sd, xscale=xscale, B=B, T=T, F=F, T1=T1, F1=F1, T2=T2, F2=F2)
 
     def bwd(self, c, dx):
         D = self.odim
@@ -648,7 +651,7 @@ class Conv2dSubsampling(nn.Module):
         # 4 implicit parity-class GEMMs with the ReLU mask in the epilogue (no 9x column buffer,
         # 8.4 GB at C2 B=128): 10.2 ms against 12.4 ms for column GEMM + col2im (kernels.py)
         if K.CONV2_IMPLICIT_DGRAD and D % 32 == 0:
-            K.conv2_dgrad(dz2p, c2.weight, c.z1, dz1, B, T1, F1, D, dz2_16=dz2_16)
+            K.conv2_dgrad(dz2p, c2.weight, c.z1, dz1, B, T1, F1, D, dz2_16=dz2_16, z1bits=c.get("z1bits"))
             del dz2_16
         else:
             dcol = empty(npix2, 9 * D, like=dx)

@@ -923,6 +923,15 @@ __device__ __forceinline__ f32x4 mfma_np(const Frag16& a, const Frag16& b, f32x4
 #ifndef ESP_ATTN_PREFETCH
 #define ESP_ATTN_PREFETCH 3
 #endif
+#ifndef ESP_ATTN_PREFETCH_LEGACY
+#define ESP_ATTN_PREFETCH_LEGACY ESP_ATTN_PREFETCH
+#endif
+// legacy rel_shift in relpos_probs_lds_kernel: how band blocks past the diagonal get the shifted A rows
+// q_v[i+1] (split once into LDS in the prologue): 1 a second register fragment and a per-step select, 2 the
+// fragment re-read from LDS every step and selected at step g
+#ifndef ESP_ATTN_LEGACY_SEL
+#define ESP_ATTN_LEGACY_SEL 1
+#endif
 constexpr int RW_ROWS = 16, RW_PITCH = 37;
 // store-transpose rows: 64 floats, so the float4 read-back (ds_read_b128 lane groups of 16 lanes over
 // two rows, bank (a/4) mod 64) is conflict-free, with the column XOR-ed by 16 in rows 4..7 and 12..15
@@ -1312,7 +1321,10 @@ __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
   __shared__ __attribute__((aligned(16))) uint8_t kpl[2][NPL * PLB];
   __shared__ __attribute__((aligned(16))) uint8_t ppl[PSL][NPL * PLB];
   __shared__ float ring[4][RW_ROWS * RW_PITCH];
-  __shared__ __attribute__((aligned(16))) float stage[4][RW_ROWS * RW_SPITCH];
+  // per wave: the store transpose after the loop; legacy: before it, the plane image of the wave's shifted
+  // rows q_v[i+1] (split once in the prologue, read at step g -- a split inside the unrolled loop spilled)
+  constexpr int STG = LEGACY && NPL * PLB / 4 > RW_ROWS * RW_SPITCH ? NPL * PLB / 4 : RW_ROWS * RW_SPITCH;
+  __shared__ __attribute__((aligned(16))) float stage[4][STG];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // XCD-aware block order, as relpos_attn_fwd16_kernel: a z's row blocks on one XCD
   const int xcd = blockIdx.x & 7, jb = blockIdx.x >> 3, zq = jb / nrb;
@@ -1391,6 +1403,14 @@ __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
     ESP_SLOT_MARK(kgen[0], BUSY);
     put_tile(kpl[0], kv);
     ESP_SLOT_MARK(kgen[0], 0);
+    if constexpr (LEGACY) {  // wave w's shifted rows q_v[ib + 16 w + 1 + r] as a plane image in stage[w]
+      float4 sv[4];
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+        sv[w] = *reinterpret_cast<const float4*>(qv + ((long)z * T + min(ib + 16 * w + 1 + sr, T - 1)) * RP_DK + sd);
+#pragma unroll
+      for (int w = 0; w < 4; ++w) put_tile(reinterpret_cast<uint8_t*>(stage[w]), sv[w]);
+    }
   }
   // the wave's query rows (d = 16 q4 + 0..15, contiguous: the plane images' order), split once
   auto ld16c = [&](const float* row, float (&f)[16]) {
@@ -1429,10 +1449,13 @@ __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
   // the block's last 16 rows at key tile 0)
   __syncthreads();
 
+  FragPl<NPL> xv2;  // legacy (ESP_ATTN_LEGACY_SEL 1): the shifted rows' fragment, from the stage image
+  if constexpr (LEGACY && ESP_ATTN_LEGACY_SEL == 1)
+    read_frag_pl(reinterpret_cast<const uint8_t*>(stage[wave]), PLB, li, q4, xv2);
   f32x4 sc[NTA];
   // key tiles / band blocks PF steps ahead in registers (slot s % PF holds step s's): a step's loads
   // have PF steps of work to arrive before they are split into LDS
-  constexpr int PF = ESP_ATTN_PREFETCH;
+  constexpr int PF = LEGACY ? ESP_ATTN_PREFETCH_LEGACY : ESP_ATTN_PREFETCH;
   float4 nk[PF], np[PF];
 #pragma unroll
   for (int s = 1; s < PF; ++s)
@@ -1442,6 +1465,17 @@ __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
     }
 #pragma unroll
   for (int t = 0; t < NTA; ++t) {
+#if ESP_ATTN_LEGACY_SEL == 2
+    if constexpr (LEGACY) {  // the shifted fragment re-read every step, selected from step g on
+      FragPl<NPL> nv;
+      read_frag_pl(reinterpret_cast<const uint8_t*>(stage[wave]), PLB, li, q4, nv);
+      const bool sw = t == g;
+#pragma unroll
+      for (int p_ = 0; p_ < NPL; ++p_)
+#pragma unroll
+        for (int m_ = 0; m_ < 2; ++m_) xv.v[p_][m_] = sw ? nv.v[p_][m_] : xv.v[p_][m_];
+    }
+#endif
     if (t + PF < NTA) {
       nk[t % PF] = *k_src(t + PF);
       np[t % PF] = *p_src(t + PF);
@@ -1453,13 +1487,21 @@ __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
     read_frag_pl(ppl[pslot(t - wave)], PLB, li, q4, pf);
     ESP_SLOT_CHECK(kgen[t & 1], t, 4);
     ESP_SLOT_CHECK(pgen[pslot(t - wave)], t - wave, 5);
-    if (LEGACY && t == g) {  // band block t+1 = g+1: the first shifted block -- its A rows are q_v[i+1]
-      float f[16];
-      ld16c(qv + ((long)z * T + min(i0 + 1 + li, T - 1)) * RP_DK, f);
-      split_row16(f, xv);
-    }
     const f32x4 a = mfma_pl(xu, kf, f32x4{0.f, 0.f, 0.f, 0.f});
-    const f32x4 s = mfma_pl(xv, pf, f32x4{0.f, 0.f, 0.f, 0.f});
+    f32x4 s;
+    if constexpr (LEGACY && ESP_ATTN_LEGACY_SEL == 1) {
+      // band blocks t+1 >= g+1 (the shifted part) take the A rows q_v[i+1]: a per-step select, branch-free
+      // (a branch at t == g in the unrolled loop split it into 24 scheduling regions: 42 VGPRs spilled)
+      FragPl<NPL> xa;
+      const bool sw = t >= g;
+#pragma unroll
+      for (int p_ = 0; p_ < NPL; ++p_)
+#pragma unroll
+        for (int m_ = 0; m_ < 2; ++m_) xa.v[p_][m_] = sw ? xv2.v[p_][m_] : xv.v[p_][m_];
+      s = mfma_pl(xa, pf, f32x4{0.f, 0.f, 0.f, 0.f});
+    } else {
+      s = mfma_pl(xv, pf, f32x4{0.f, 0.f, 0.f, 0.f});
+    }
     put_band(ring0, t + 1, s);
     asm volatile("" ::: "memory");  // ring writes before the shifted reads (LDS is in order per wave)
     const int j = t * 16 + li;

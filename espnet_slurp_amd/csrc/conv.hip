@@ -21,11 +21,13 @@ inline int gridn(long n) {
 #ifndef ESP_CONV1_NT
 #define ESP_CONV1_NT 1
 #endif
+// zbits != nullptr: the ReLU mask as a packed bit map too, bit c % 32 of word p * D/32 + c / 32 = (z[p][c] > 0)
+// (D % 32 == 0): the conv2 input gradient's mask read (esp_conv2_dgrad_bits), 1/32 of the fp32 map's bytes
 template <bool B16>
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict__ x, const float* __restrict__ W,
                                                         const float* __restrict__ bias, float* __restrict__ z,
-                                                        uint2* __restrict__ z16, int B, int T, int F, int T1, int F1,
-                                                        int D, unsigned chunk) {
+                                                        uint2* __restrict__ z16, uint32_t* __restrict__ zbits, int B,
+                                                        int T, int F, int T1, int F1, int D, unsigned chunk) {
   // block b owns output pixels [b * chunk, (b + 1) * chunk); per step its 256 threads cover PS = 256 / (D/4)
   // consecutive pixels x all D channels (PS KB of contiguous float4 stores).  The pixel's (b, t1, f1) is
   // decomposed once and then advanced by PS (one row wrap per step at most when PS < F1) -- the per-pixel
@@ -71,6 +73,15 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict_
     *reinterpret_cast<float4*>(z + (long)p * D + o4 * 4) = make_float4(out[0], out[1], out[2], out[3]);
 #endif
     if constexpr (B16) z16[((long)p * D + o4 * 4) >> 2] = make_uint2(esp::bf16_pair(out[0], out[1]), esp::bf16_pair(out[2], out[3]));
+    if (zbits) {  // (uniform) 8 lanes (o4 & ~7 .. +7, one pixel: D4 % 8 == 0) OR their nibbles into one word
+      uint32_t v = ((out[0] > 0.f ? 1u : 0u) | (out[1] > 0.f ? 2u : 0u) | (out[2] > 0.f ? 4u : 0u) |
+                    (out[3] > 0.f ? 8u : 0u)) << (4 * (o4 & 7));
+      // DPP, no LDS round trip: quad_perm [1,0,3,2], [2,3,0,1], then row_half_mirror (lane i <-> 7 - i)
+      v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+      v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+      v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);
+      if ((o4 & 7) == 0) zbits[(long)p * (D >> 5) + (o4 >> 3)] = v;
+    }
     f1 += PS;
     while (f1 >= F1) {  // (once at most when PS < F1, the C2 / C5 shapes)
       f1 -= F1;
@@ -278,19 +289,26 @@ __global__ void permute3_kernel(const float* __restrict__ in, float* __restrict_
 
 }  // namespace
 
-static int conv1_fwd_impl(const float* x, const float* W, const float* bias, float* z, void* z16, int B, int T, int F,
-                          int D, void* stream);
+static int conv1_fwd_impl(const float* x, const float* W, const float* bias, float* z, void* z16, unsigned* zbits, int B,
+                          int T, int F, int D, void* stream);
 ESP_API int esp_conv1_fwd(const float* x, const float* W, const float* bias, float* z, int B, int T, int F, int D,
                           void* stream) {
-  return conv1_fwd_impl(x, W, bias, z, nullptr, B, T, F, D, stream);
+  return conv1_fwd_impl(x, W, bias, z, nullptr, nullptr, B, T, F, D, stream);
 }
 ESP_API int esp_conv1_fwd_bf16(const float* x, const float* W, const float* bias, float* z, void* z16, int B, int T,
                                int F, int D, void* stream) {
   ESP_ARG_CHECK(z16 && ((uintptr_t)z16 & 7) == 0, "esp_conv1_fwd_bf16: z16 must be 8-B aligned");
-  return conv1_fwd_impl(x, W, bias, z, z16, B, T, F, D, stream);
+  return conv1_fwd_impl(x, W, bias, z, z16, nullptr, B, T, F, D, stream);
 }
-static int conv1_fwd_impl(const float* x, const float* W, const float* bias, float* z, void* z16, int B, int T, int F,
-                          int D, void* stream) {
+ESP_API int esp_conv1_fwd_bits(const float* x, const float* W, const float* bias, float* z, void* z16, unsigned* zbits,
+                               int B, int T, int F, int D, void* stream) {
+  ESP_ARG_CHECK(!z16 || ((uintptr_t)z16 & 7) == 0, "esp_conv1_fwd_bits: z16 must be 8-B aligned");
+  ESP_ARG_CHECK(zbits && ((uintptr_t)zbits & 3) == 0 && D % 32 == 0,
+                "esp_conv1_fwd_bits: zbits (4-B aligned) and D %% 32 == 0 needed");
+  return conv1_fwd_impl(x, W, bias, z, z16, zbits, B, T, F, D, stream);
+}
+static int conv1_fwd_impl(const float* x, const float* W, const float* bias, float* z, void* z16, unsigned* zbits, int B,
+                          int T, int F, int D, void* stream) {
   ESP_ARG_CHECK(D % 4 == 0, "esp_conv1_fwd: D %% 4 != 0");
   const int T1 = (T - 3) / 2 + 1, F1 = (F - 3) / 2 + 1;
   ESP_ARG_CHECK(256 % (D / 4) == 0, "esp_conv1_fwd: D/4 must divide 256");
@@ -302,10 +320,10 @@ static int conv1_fwd_impl(const float* x, const float* W, const float* bias, flo
   const unsigned chunk = (unsigned)((npix + nblk - 1) / nblk);
   if (z16)
     hipLaunchKernelGGL(conv1_fwd_kernel<true>, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, x, W, bias, z,
-                       (uint2*)z16, B, T, F, T1, F1, D, chunk);
+                       (uint2*)z16, (uint32_t*)zbits, B, T, F, T1, F1, D, chunk);
   else
     hipLaunchKernelGGL(conv1_fwd_kernel<false>, dim3((unsigned)nblk), dim3(256), 0, (hipStream_t)stream, x, W, bias, z,
-                       nullptr, B, T, F, T1, F1, D, chunk);
+                       nullptr, (uint32_t*)zbits, B, T, F, T1, F1, D, chunk);
   ESP_CHECK_LAUNCH("esp_conv1_fwd");
   return 0;
 }

@@ -20,7 +20,7 @@ void set_error(const char* fmt, ...) {
 }  // namespace esp
 
 ESP_API const char* esp_last_error(void) { return esp::g_err; }
-ESP_API int esp_abi_version(void) { return 31; }
+ESP_API int esp_abi_version(void) { return 32; }
 ESP_API int esp_set_rng_key(const unsigned long long* key) {
   esp::g_rng_key = (const uint64_t*)key;
   return 0;

@@ -790,30 +790,41 @@ __global__ void conv2_class_weights_kernel(const float* __restrict__ W, float* _
 // planes (the B-planes class GEMMs of the fp32 split build), 3 * 9 * D * D bf16
 // (esp_conv2_dgrad_workspace_bytes)
 ESP_API long esp_conv2_dgrad_workspace_bytes(int D) { return D <= 0 ? 0 : 4L * 9 * D * D + 6L * 9 * D * D; }
-static int conv2_dgrad_impl(const float* dz2, const void* dz2_16, const float* W, const float* z1, float* dz1, int B,
-                            int T1, int F1, int D, const float* zeros16, float* wc_work, long work_bytes,
-                            void* stream);
+static int conv2_dgrad_impl(const float* dz2, const void* dz2_16, const float* W, const float* z1,
+                            const unsigned* z1bits, float* dz1, int B, int T1, int F1, int D, const float* zeros16,
+                            float* wc_work, long work_bytes, void* stream);
 ESP_API int esp_conv2_dgrad(const float* dz2, const float* W, const float* z1, float* dz1, int B, int T1, int F1,
                             int D, const float* zeros16, float* wc_work, long work_bytes, void* stream) {
-  return conv2_dgrad_impl(dz2, nullptr, W, z1, dz1, B, T1, F1, D, zeros16, wc_work, work_bytes, stream);
+  return conv2_dgrad_impl(dz2, nullptr, W, z1, nullptr, dz1, B, T1, F1, D, zeros16, wc_work, work_bytes, stream);
+}
+// the conv1 ReLU mask from esp_conv1_fwd_bits' packed bit map (D/32 words per pixel) instead of the fp32 map:
+// the epilogue reads 1/32 of the bytes; dz2 fp32 (dz2) or bf16 (dz2_16, the bf16 mode, D % 64 == 0), one of them
+ESP_API int esp_conv2_dgrad_bits(const float* dz2, const void* dz2_16, const float* W, const unsigned* z1bits,
+                                 float* dz1, int B, int T1, int F1, int D, const float* zeros16, float* wc_work,
+                                 long work_bytes, void* stream) {
+  ESP_ARG_CHECK(z1bits && ((uintptr_t)z1bits & 3) == 0 && (dz2 == nullptr) != (dz2_16 == nullptr) &&
+                    (!dz2_16 || D % 64 == 0),
+                "esp_conv2_dgrad_bits: z1bits (4-B aligned) and exactly one of dz2 / dz2_16 (D %% 64 == 0) needed");
+  return conv2_dgrad_impl(dz2, dz2_16, W, nullptr, z1bits, dz1, B, T1, F1, D, zeros16, wc_work, work_bytes, stream);
 }
 // the bf16 mode's form: dz2 as bf16 (dz2_16), the class weights cast to bf16 in the workspace, the class
 // GEMMs on bf16 operands (PREC 2, the tap gather in bf16-pair units); D % 64 == 0
 ESP_API int esp_conv2_dgrad_bf16(const void* dz2_16, const float* W, const float* z1, float* dz1, int B, int T1,
                                  int F1, int D, const float* zeros16, float* wc_work, long work_bytes, void* stream) {
   ESP_ARG_CHECK(D % 64 == 0, "esp_conv2_dgrad_bf16: D %% 64 == 0 needed");
-  return conv2_dgrad_impl(nullptr, dz2_16, W, z1, dz1, B, T1, F1, D, zeros16, wc_work, work_bytes, stream);
+  return conv2_dgrad_impl(nullptr, dz2_16, W, z1, nullptr, dz1, B, T1, F1, D, zeros16, wc_work, work_bytes, stream);
 }
-static int conv2_dgrad_impl(const float* dz2, const void* dz2_16, const float* W, const float* z1, float* dz1, int B,
-                            int T1, int F1, int D, const float* zeros16, float* wc_work, long work_bytes,
-                            void* stream) {
+static int conv2_dgrad_impl(const float* dz2, const void* dz2_16, const float* W, const float* z1,
+                            const unsigned* z1bits, float* dz1, int B, int T1, int F1, int D, const float* zeros16,
+                            float* wc_work, long work_bytes, void* stream) {
   const bool b16 = dz2_16 != nullptr;
   if (b16) dz2 = (const float*)dz2_16;  // bf16 pairs viewed as fp32 elements
   const int T2 = (T1 - 3) / 2 + 1, F2 = (F1 - 3) / 2 + 1;
   const long need__ = esp_conv2_dgrad_workspace_bytes(D);
   ESP_ARG_CHECK(work_bytes >= need__, "esp_conv2_dgrad: workspace %ld B < %ld B required (esp_conv2_dgrad_workspace_bytes)", work_bytes, need__);
   ESP_ARG_CHECK(B >= 1 && T2 >= 1 && F2 >= 1 && D % 32 == 0, "esp_conv2_dgrad: bad sizes (D %% 32 == 0 needed)");
-  ESP_ARG_CHECK(aligned16(dz2) && aligned16(z1) && aligned16(dz1) && aligned16(zeros16) && aligned16(wc_work),
+  ESP_ARG_CHECK(aligned16(dz2) && (z1bits || aligned16(z1)) && aligned16(dz1) && aligned16(zeros16) &&
+                    aligned16(wc_work),
                 "esp_conv2_dgrad: operands must be 16-B aligned");
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(conv2_class_weights_kernel, dim3(1024), dim3(256), 0, st, W, wc_work, D);
@@ -853,7 +864,8 @@ static int conv2_dgrad_impl(const float* dz2, const void* dz2_16, const float* W
     g.a = Operand{dz2, 0, 0, 0, 1, {}, 1};
     g.b = Operand{wc_work + (long)slot0[cls] * D * D, D, 0, 0, 1, {}, 1};
     g.c = dz1; g.ldc = D; g.alpha = 1.f; g.beta = 0.f;
-    g.bwd_act = ACT_RELU; g.pre = z1;
+    g.bwd_act = ACT_RELU; g.pre = z1bits ? dz1 : z1;  // (bits: pre is never read; any aligned pointer)
+    g.cm_bits = reinterpret_cast<const uint32_t*>(z1bits); g.cm_bw = D / 32;
     g.bf16 = g_compute;  // bf16 MFMA in the reduced-precision mode, as every other GEMM of the step
     if (bp) {
       g.b = Operand{reinterpret_cast<const float*>(planes + (long)slot0[cls] * D * D), D, 0, 0, 1, {}, 1};

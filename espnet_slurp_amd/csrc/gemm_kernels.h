@@ -130,6 +130,10 @@ struct GemmArgs {
   int cmap;
   FastDiv cm_hw, cm_w;
   int cm_T1, cm_F1, cm_ph, cm_pw;
+  // EPI_RMASKMAP's ReLU mask as the conv1 map's packed bit map (esp_conv1_fwd_bits: bit c % 32 of word
+  // pixel * cm_bw + c / 32 = (z1[pixel][c] > 0)) instead of the fp32 map in pre; NULL: pre
+  const uint32_t* cm_bits;
+  int cm_bw;
   // EPI_SMB (esp_attn_dscores): the dP = dctx V^T GEMM of rel-pos attention finishes the softmax
   // and rel_shift adjoints in its epilogue; pre = the attention probabilities (C's layout)
   int smb_rel;           // 0 off, 1 latest, 2 legacy rel_shift adjoint
@@ -145,12 +149,15 @@ struct GemmArgs {
   int band_c0, band_w;
 };
 
-__device__ __forceinline__ long row_off(const GemmArgs& g, int m) {
-  if (!g.cmap) return (long)m * g.ldc;
+__device__ __forceinline__ long row_pix(const GemmArgs& g, int m) {
   const int b = (int)fdiv((uint32_t)m, g.cm_hw);
   const int rem = m - b * (int)g.cm_hw.d;
   const int a = (int)fdiv((uint32_t)rem, g.cm_w), e = rem - a * (int)g.cm_w.d;
-  return (((long)b * g.cm_T1 + 2 * a + g.cm_ph) * g.cm_F1 + 2 * e + g.cm_pw) * g.ldc;
+  return ((long)b * g.cm_T1 + 2 * a + g.cm_ph) * g.cm_F1 + 2 * e + g.cm_pw;
+}
+__device__ __forceinline__ long row_off(const GemmArgs& g, int m) {
+  if (!g.cmap) return (long)m * g.ldc;
+  return row_pix(g, m) * g.ldc;
 }
 
 // Fused epilogue for output element (m, n) of batch z with raw accumulator `acc`.  The kind is
@@ -528,12 +535,23 @@ __device__ __forceinline__ void store_spec(const GemmArgs& g, int z, int mrow0, 
       }
       float4 x4[4];  // residual (BDR) or local derivative (BMUL)
       long roff[4];  // row offsets (EPI_RMASKMAP: through the class -> pixel row map)
+      long pix[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int m = mrow0 + i * 32 + 8 * q + 4 * h + (l32 & 3);
-        roff[q] = S::rmap ? row_off(g, min(m, g.M - 1)) : (long)m * g.ldc;
+        pix[q] = S::rmap ? row_pix(g, min(m, g.M - 1)) : 0;
+        roff[q] = S::rmap ? pix[q] * g.ldc : (long)m * g.ldc;
       }
-      if constexpr (S::res || S::mul) {
+      if (S::rmap && g.cm_bits) {
+        // the mask from the packed bit map: one word per 32 channels, the same word for the 8 lanes
+        // of a row (columns n .. n+3 of one 32-column sub-tile): 1/32 of the fp32 map's bytes
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int m = mrow0 + i * 32 + 8 * q + 4 * h + (l32 & 3);
+          const uint32_t w = (FULL || (nok && m < g.M)) ? g.cm_bits[pix[q] * g.cm_bw + (n >> 5)] >> (n & 31) : 0u;
+          x4[q] = make_float4((float)(w & 1u), (float)((w >> 1) & 1u), (float)((w >> 2) & 1u), (float)((w >> 3) & 1u));
+        }
+      } else if constexpr (S::res || S::mul) {
         const float* src = S::res ? g.r : g.pre;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {

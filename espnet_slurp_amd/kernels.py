@@ -1199,8 +1199,14 @@ def relshift_bwd(dS, dbd, relpos, Z, T, P, lds=None, ldp=None):
 
 
 # ----------------------------------------------------------------------------- subsampling
-def conv1_fwd(x, W, b, z, B, T, F, D, z16=None):
-    """z16 (bf16, optional): the output's bf16 copy too (esp_conv1_fwd_bf16)."""
+def conv1_fwd(x, W, b, z, B, T, F, D, z16=None, zbits=None):
+    """z16 (bf16, optional): the output's bf16 copy too (esp_conv1_fwd_bf16); zbits (int32, B*T1*F1*D/32,
+    optional): the ReLU mask as a packed bit map too (esp_conv1_fwd_bits)."""
+    if zbits is not None:
+        assert zbits.dtype == torch.int32 and zbits.is_contiguous()
+        _native.call("esp_conv1_fwd_bits", _p(x), _p(W), _p(b), _p(z), _p(z16) if z16 is not None else None,
+                     _p(zbits), B, T, F, D, _st())
+        return
     if z16 is not None:
         _native.call("esp_conv1_fwd_bf16", _p(x), _p(W), _p(b), _p(z), _p(z16), B, T, F, D, _st())
         return
@@ -1372,6 +1378,10 @@ _ZEROS = {}
 # col2im at C2 B=128 (tools/conv2_dgrad_bench.py), bench 1067 vs 1050 utt/s.  CONV2_IMPLICIT_DGRAD = False:
 # the column path.
 CONV2_IMPLICIT_DGRAD = True
+# training: conv1 also writes its ReLU mask as a packed bit map (esp_conv1_fwd_bits) and the implicit input
+# gradient's epilogue reads it (esp_conv2_dgrad_bits) instead of the fp32 map -- 1/32 of the mask bytes
+# (ESP_CONV2_BITS=0: the fp32 map, an A/B switch)
+CONV2_DGRAD_BITS = os.environ.get("ESP_CONV2_BITS", "1") != "0"
 
 
 def conv2_wgrad_bf16(dz2_16, z1_16, dw, db, B, T1, F1, D):
@@ -1391,10 +1401,12 @@ def conv2_wgrad_bf16(dz2_16, z1_16, dw, db, B, T1, F1, D):
         _PROF.append((2.0 * D * 9 * D * npix, ev0, ev1, (RC, I2C_RC, D, 9 * D, npix, 1, "bf16"), 0.0))
 
 
-def conv2_dgrad(dz2, W, z1, dz1, B, T1, F1, D, dz2_16=None):
+def conv2_dgrad(dz2, W, z1, dz1, B, T1, F1, D, dz2_16=None, z1bits=None):
     """Conv2d(D, D, 3, 2) input gradient x conv1 ReLU mask as 4 implicit parity-class GEMMs; dz2_16 (the
-    bf16 mode): dz2 as bf16, the class GEMMs on bf16 operands (esp_conv2_dgrad_bf16; dz2 may then be None)."""
+    bf16 mode): dz2 as bf16, the class GEMMs on bf16 operands (esp_conv2_dgrad_bf16; dz2 may then be None);
+    z1bits (conv1_fwd's bit map): the mask from it instead of z1 (esp_conv2_dgrad_bits; z1 may be None)."""
     assert dz2 is not None or dz2_16 is not None
+    assert z1 is not None or z1bits is not None
     _f32(dz2, W, z1, dz1)
     key = str(W.device)
     if key not in _ZEROS:
@@ -1405,7 +1417,12 @@ def conv2_dgrad(dz2, W, z1, dz1, B, T1, F1, D, dz2_16=None):
         ev0 = torch.cuda.Event(enable_timing=True)
         ev1 = torch.cuda.Event(enable_timing=True)
         ev0.record()
-    if dz2_16 is not None:
+    if z1bits is not None:
+        assert z1bits.dtype == torch.int32
+        _native.call("esp_conv2_dgrad_bits", None if dz2_16 is not None else _p(dz2),
+                     _p(dz2_16) if dz2_16 is not None else None, _p(W), _p(z1bits), _p(dz1), B, T1, F1, D,
+                     _p(_ZEROS[key]), _p(wc), n, _st())
+    elif dz2_16 is not None:
         _native.call("esp_conv2_dgrad_bf16", _p(dz2_16), _p(W), _p(z1), _p(dz1), B, T1, F1, D, _p(_ZEROS[key]), _p(wc),
                      n, _st())
     else:

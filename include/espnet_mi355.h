@@ -402,12 +402,22 @@ int esp_conv1_fwd(const float* x, const float* W, const float* bias, float* z, i
 /* esp_conv1_fwd writing z's bf16 copy (RNE) to z16 too (8-B aligned): the bf16 mode's conv2 operand. */
 int esp_conv1_fwd_bf16(const float* x, const float* W, const float* bias, float* z, void* z16, int B, int T, int F,
                        int D, void* stream);
+/* ABI 32: esp_conv1_fwd (z16 optional, as esp_conv1_fwd_bf16) also writing the ReLU mask as a packed bit map:
+ * bit c % 32 of zbits[p * D/32 + c / 32] = (z[p][c] > 0), D % 32 == 0, 4-B aligned (replaces the fp32 map
+ * as the conv2 input gradient's mask operand: esp_conv2_dgrad_bits reads 1/32 of the bytes). */
+int esp_conv1_fwd_bits(const float* x, const float* W, const float* bias, float* z, void* z16, unsigned* zbits, int B,
+                       int T, int F, int D, void* stream);
 /* conv2 input gradient as 4 implicit GEMMs (one per parity class of the conv1 output grid):
  * dz1 = relu'(z1) * conv_transpose(dz2, W), W = Conv2d(D,D,3,2).weight (o,c,kt,kf) as the
  * reference stores it; no 9x column buffer.  zeros16: >= 16 B of zeros (device); wc_work:
  * 9*D*D floats (the per-class weight re-layout).  D % 32 == 0. */
 int esp_conv2_dgrad(const float* dz2, const float* W, const float* z1, float* dz1, int B, int T1, int F1,
                     int D, const float* zeros16, float* wc_work, long work_bytes, void* stream);
+/* ABI 32: esp_conv2_dgrad / esp_conv2_dgrad_bf16 with the conv1 ReLU mask from esp_conv1_fwd_bits' bit map
+ * (z1bits) instead of the fp32 map; exactly one of dz2 (fp32) / dz2_16 (bf16, D % 64 == 0) non-NULL. */
+int esp_conv2_dgrad_bits(const float* dz2, const void* dz2_16, const float* W, const unsigned* z1bits, float* dz1,
+                         int B, int T1, int F1, int D, const float* zeros16, float* wc_work, long work_bytes,
+                         void* stream);
 int esp_col2im_relu(const float* dcol, const float* z1, float* dz1, int B, int T1, int F1, int D,
                     void* stream);
 int esp_conv1_wgrad(const float* x, const float* dz1, float* dW, float* db, int B, int T, int F,

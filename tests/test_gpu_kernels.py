@@ -857,6 +857,45 @@ def test_conv2_dgrad_parity_classes_vs_column_path(dev, T1, F1):
     assert rel_err(got.cpu(), ref.cpu()) < 1e-5
 
 
+@pytest.mark.parametrize("T1,F1,D", [(31, 39, 64), (32, 40, 128), (9, 7, 256)])
+def test_conv2_dgrad_bits_mask_bit_exact(dev, T1, F1, D):
+    """esp_conv1_fwd_bits' packed ReLU bit map is (z1 > 0) bit for bit (the same launch also writes z1 and
+    its bf16 copy unchanged), and esp_conv2_dgrad_bits (the mask from the bit map) equals esp_conv2_dgrad
+    (the mask from the fp32 map) exactly -- fp32 and bf16 dz2 -- at ragged grids and a padded C2 batch
+    whose conv1 map has exact zeros."""
+    B = 3
+    T, F = 2 * T1 + 1, 2 * F1 + 1
+    T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
+    g = torch.Generator().manual_seed(41)
+    x = torch.randn(B, T, F, generator=g)
+    x[1, T // 2:] = 0.0  # padded frames: conv1 = relu(bias) there, exact zeros where the bias is <= 0
+    x = x.to(dev)
+    w0, b0 = (torch.randn(D, 1, 3, 3, generator=g) * 0.3).to(dev), (torch.randn(D, generator=g) * 0.1).to(dev)
+    W = (torch.randn(D, D, 3, 3, generator=g) * 0.05).to(dev)
+    npx = B * T1 * F1
+    z1, z1b = torch.empty(npx * D, device=dev), torch.empty(npx * D, device=dev)
+    z16 = torch.empty(npx * D, dtype=torch.bfloat16, device=dev)
+    bits = torch.full((npx * D // 32,), -1, dtype=torch.int32, device=dev)
+    K.conv1_fwd(x, w0, b0, z1, B, T, F, D)
+    K.conv1_fwd(x, w0, b0, z1b, B, T, F, D, z16=z16, zbits=bits)
+    torch.cuda.synchronize()
+    assert torch.equal(z1, z1b)
+    assert torch.equal(z16.view(torch.int16), z1.bfloat16().view(torch.int16))
+    pos = (z1.view(npx, D // 32, 32) > 0).cpu().to(torch.int64)
+    want = (pos << torch.arange(32, dtype=torch.int64)).sum(-1)
+    assert torch.equal(bits.cpu().to(torch.int64) & 0xFFFFFFFF, want.view(-1))
+    dz2 = torch.randn(B * T2 * F2, D, generator=g).to(dev)
+    forms = [dict()] + ([dict(dz2_16=K.to_bf16(dz2, B * T2 * F2, D, D))] if D % 64 == 0 else [])
+    for kw in forms:
+        ref = torch.empty(npx * D, device=dev)
+        got = torch.full((npx * D,), float("nan"), device=dev)
+        with K.gemm_compute("bf16" if kw else "fp32"):
+            K.conv2_dgrad(dz2, W, z1, ref, B, T1, F1, D, **kw)
+            K.conv2_dgrad(None if kw else dz2, W, None, got, B, T1, F1, D, z1bits=bits, **kw)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref), kw.keys()
+
+
 @pytest.mark.parametrize("T1,F1", [(31, 39), (9, 7), (33, 40)])
 def test_conv2_bf16_operands_match_staged_rounding(dev, T1, F1):
     """The bf16 mode's conv2 forward (esp_conv2_fwd_bf16: implicit im2col over conv1's bf16 copy of z1,
