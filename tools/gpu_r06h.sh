@@ -1,0 +1,11 @@
+#!/bin/bash
+# round 6 (h): HEAD record -- the full GPU suite (-s: the LOSS_GATE / TRAINRUN_GATE lines), smoke, the default
+# bench line (cpu_baseline leg included) and a C2 B=256 kernel trace
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+rm -rf gpurun_out/prof_h
+bash gpurun_steps.sh \
+  "timeout -k 10 1100 python -u -m pytest tests -m gpu -v -s -rf --timeout 350 --timeout-method thread > gpurun_out/r06h_pytest_gpu.log 2>&1" \
+  "timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/r06h_smoke.log 2>&1" \
+  "timeout -k 10 500 python -u bench.py > gpurun_out/r06h_bench.log 2>&1" \
+  "timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_h -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --feed-steps 0 > gpurun_out/prof_h.log 2>&1"
