@@ -99,6 +99,8 @@ SIGNATURES = {
     "esp_conv1_fwd": [P, P, P, P, I, I, I, I, P],
     "esp_conv1_fwd_bits": [P, P, P, P, P, P, I, I, I, I, P],
     "esp_conv2_dgrad_bits": [P, P, P, P, P, I, I, I, I, P, P, L, P],
+    "esp_conv2_dgrad_c1fold": [P, P, P, P, P, I, I, P, P, I, I, I, I, P, P, L, P, L, P],
+    "esp_conv2_c1fold_workspace_bytes": [],
     "esp_col2im_relu": [P, P, P, I, I, I, I, P],
     "esp_conv1_wgrad": [P, P, P, P, I, I, I, I, P, L, P],
     "esp_permute3": [P, P, I, I, I, I, P],

@@ -647,11 +647,17 @@ class Conv2dSubsampling(nn.Module):
             K.gemm(D, 9 * D, npix2, dz2p, c.z1, dw2r, mode_a=K.RC, lda=D, mode_b=K.I2C_RC, ldb=0, ldc=9 * D, ic_b=ic,
                    rowsum=c2.bias.grad)
         K.permute3(dw2r, c2.weight.grad, D, 9, D, accumulate=True)  # (o, kk, c) -> (o, c, kk)
+        z1bits = c.get("z1bits")
+        if z1bits is not None and K.conv2_c1fold_ok(D):
+            # conv1's weight gradient in the input gradient's epilogue: the conv1-map gradient is never stored
+            K.conv2_dgrad_c1fold(dz2p, c2.weight, z1bits, c.feats, c.T, c.F, c0.weight.grad.view(D, 9), c0.bias.grad,
+                                 B, T1, F1, D, dz2_16=dz2_16)
+            return
         dz1 = empty(B * T1 * F1 * D, like=dx)
         # 4 implicit parity-class GEMMs with the ReLU mask in the epilogue (no 9x column buffer,
         # 8.4 GB at C2 B=128): 10.2 ms against 12.4 ms for column GEMM + col2im (kernels.py)
         if K.CONV2_IMPLICIT_DGRAD and D % 32 == 0:
-            K.conv2_dgrad(dz2p, c2.weight, c.z1, dz1, B, T1, F1, D, dz2_16=dz2_16, z1bits=c.get("z1bits"))
+            K.conv2_dgrad(dz2p, c2.weight, c.z1, dz1, B, T1, F1, D, dz2_16=dz2_16, z1bits=z1bits)
             del dz2_16
         else:
             dcol = empty(npix2, 9 * D, like=dx)

@@ -120,6 +120,7 @@ long persist_blocks(int per_cu) {
 }
 
 int g_compute = 0;  // 0: fp32 MFMA (exact f32 fma chain), 1: bf16-input MFMA with fp32 accumulate
+int g_last_grid = 0;  // the grid of the last LDS-DMA launch (EPI_C1FOLD: its per-block records)
 
 // split-K combine: 0 the reduction launch (default), 1 in-kernel (last-arriving unit per tile;
 // measured slower, kept for esp_set_splitk_mode and its parity test)
@@ -195,7 +196,9 @@ bool launch_glds(int MA, int MB, const GemmArgs& g, int batch, hipStream_t st, c
   x.ntiles = (int)((long)x.ntx * x.nty * batch * g.splits);
   const bool rs = can_rs && g.rowsum;
   if (rs) kind = EPI_PLAIN;
+  if (kind == EPI_C1FOLD && !(MA == I2CT_KC && MB == RC && BNT == 128 && bm == 128 && x.ntx <= C1NT)) return false;
   const dim3 grid((unsigned)std::min<long>(x.ntiles, persist_blocks(glds_occupancy_rt(BNT, kind, bm, g.bf16))));
+  g_last_grid = (int)grid.x;
   x.fd_grid = make_fastdiv(grid.x);
   x.fd_ntx = make_fastdiv((uint32_t)x.ntx);
   x.fd_nty = make_fastdiv((uint32_t)x.nty);
@@ -784,15 +787,64 @@ __global__ void conv2_class_weights_kernel(const float* __restrict__ W, float* _
     Wc[i] = W[(((long)o * D + c) * 3 + kt) * 3 + kf];
   }
 }
+// EPI_C1FOLD records -> conv1 weight / bias gradient, in fixed order (deterministic).  c1fold_reduce: block
+// (combo = tn * 4 + wave, chunk) sums element e (0..639: lane * 10 + slot) of its chunk of the records (the
+// class launches' blocks in order) -> red[combo][chunk][640]
+constexpr int C1_NCH = 32;
+struct C1Regions {
+  long off[4];  // record region of class launch i (floats)
+  int grid[4];  // its grid
+  int ncls;
+};
+__global__ __launch_bounds__(640) void c1fold_reduce_kernel(const float* __restrict__ part, C1Regions r,
+                                                            float* __restrict__ red) {
+  const int combo = blockIdx.x, chunk = blockIdx.y, e = threadIdx.x;
+  const int tn = combo >> 2, wave = combo & 3;
+  int total = 0;
+  for (int i = 0; i < r.ncls; ++i) total += r.grid[i];
+  const int r0 = (int)((long)total * chunk / C1_NCH), r1 = (int)((long)total * (chunk + 1) / C1_NCH);
+  float acc = 0.f;
+  int cls = 0, base = 0;
+  for (int rec = r0; rec < r1; ++rec) {
+    while (rec - base >= r.grid[cls]) base += r.grid[cls++];
+    const long b = rec - base;
+    acc += part[r.off[cls] + ((b * C1NT + tn) * 4 + wave) * 640 + e];
+  }
+  red[((long)combo * C1_NCH + chunk) * 640 + e] = acc;
+}
+// c1fold_finalize: output (c, k): column c = 128 tn + 64 wn + 32 j + 4 grp + col, sum v = 10 col + k held by lane
+// (h, l32) = (s >> 2, 4 grp + (s & 3)), s = v / 5, slot 5 j + v % 5 of waves wn and 2 + wn (store_c1fold)
+__global__ void c1fold_finalize_kernel(const float* __restrict__ red, int D, float* __restrict__ dW,
+                                       float* __restrict__ db) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= D * 10) return;
+  const int c = o / 10, k = o - c * 10;
+  const int tn = c >> 7, cc = c & 127, wn = cc >> 6, j = (cc >> 5) & 1, grp = (cc & 31) >> 2, col = cc & 3;
+  const int v = col * 10 + k, sl = v / 5, u = v - 5 * sl;
+  const int lane = (sl >> 2) * 32 + grp * 4 + (sl & 3), slot = 5 * j + u;
+  float acc = 0.f;
+  for (int wm = 0; wm < 2; ++wm) {
+    const int combo = tn * 4 + wm * 2 + wn;
+    for (int ch = 0; ch < C1_NCH; ++ch) acc += red[((long)combo * C1_NCH + ch) * 640 + lane * 10 + slot];
+  }
+  if (k < 9) dW[c * 9 + k] += acc;
+  else db[c] += acc;
+}
 }  // namespace
 
 // wc_work: the four parity classes' re-laid weights, 9 * D * D floats, then their three bf16 split
 // planes (the B-planes class GEMMs of the fp32 split build), 3 * 9 * D * D bf16
 // (esp_conv2_dgrad_workspace_bytes)
 ESP_API long esp_conv2_dgrad_workspace_bytes(int D) { return D <= 0 ? 0 : 4L * 9 * D * D + 6L * 9 * D * D; }
+struct C1FoldArgs {  // esp_conv2_dgrad_c1fold: the conv1 weight gradient folded into the class GEMMs
+  const float* x;
+  int T, F;
+  float *dW, *db, *work;
+  long work_bytes;
+};
 static int conv2_dgrad_impl(const float* dz2, const void* dz2_16, const float* W, const float* z1,
                             const unsigned* z1bits, float* dz1, int B, int T1, int F1, int D, const float* zeros16,
-                            float* wc_work, long work_bytes, void* stream);
+                            float* wc_work, long work_bytes, void* stream, const C1FoldArgs* c1 = nullptr);
 ESP_API int esp_conv2_dgrad(const float* dz2, const float* W, const float* z1, float* dz1, int B, int T1, int F1,
                             int D, const float* zeros16, float* wc_work, long work_bytes, void* stream) {
   return conv2_dgrad_impl(dz2, nullptr, W, z1, nullptr, dz1, B, T1, F1, D, zeros16, wc_work, work_bytes, stream);
@@ -814,16 +866,40 @@ ESP_API int esp_conv2_dgrad_bf16(const void* dz2_16, const float* W, const float
   ESP_ARG_CHECK(D % 64 == 0, "esp_conv2_dgrad_bf16: D %% 64 == 0 needed");
   return conv2_dgrad_impl(nullptr, dz2_16, W, z1, nullptr, dz1, B, T1, F1, D, zeros16, wc_work, work_bytes, stream);
 }
+// the records of the four class launches (<= C1NT column tiles of 128, <= 4 resident blocks per CU) + the
+// reduction's chunk sums (esp_conv2_dgrad_c1fold)
+ESP_API long esp_conv2_c1fold_workspace_bytes(void) {
+  return 4L * (4L * persist_blocks(4) * C1NT * 256 * 10 + (long)C1NT * 4 * C1_NCH * 640);
+}
+// esp_conv2_dgrad_bits with conv1's weight / bias gradient folded into the class GEMMs' epilogue (EPI_C1FOLD):
+// dW (D x 9) += sum over the conv1 map of dz1 * x-patch, db (D) += sum dz1, and dz1 itself is never written
+// (no 7.7 GB store at C2 B=256, no esp_conv1_wgrad pass over it).  x: the conv1 input (B, T, F), as esp_conv1_fwd
+// took it.  D % 128 == 0, D <= 512.
+ESP_API int esp_conv2_dgrad_c1fold(const float* dz2, const void* dz2_16, const float* W, const unsigned* z1bits,
+                                   const float* x, int T, int F, float* dW, float* db, int B, int T1, int F1, int D,
+                                   const float* zeros16, float* wc_work, long work_bytes, float* c1_work,
+                                   long c1_work_bytes, void* stream) {
+  ESP_ARG_CHECK(z1bits && ((uintptr_t)z1bits & 3) == 0 && (dz2 == nullptr) != (dz2_16 == nullptr) &&
+                    (!dz2_16 || D % 64 == 0) && D % 128 == 0 && D <= 128 * C1NT && x && dW && db && c1_work,
+                "esp_conv2_dgrad_c1fold: z1bits, x, dW, db, c1_work, exactly one of dz2 / dz2_16, D %% 128 == 0 and "
+                "D <= 512 needed");
+  ESP_ARG_CHECK(T1 == (T - 3) / 2 + 1 && F1 == (F - 3) / 2 + 1, "esp_conv2_dgrad_c1fold: T1 / F1 do not match T / F");
+  const long need = esp_conv2_c1fold_workspace_bytes();
+  ESP_ARG_CHECK(c1_work_bytes >= need, "esp_conv2_dgrad_c1fold: c1 workspace %ld B < %ld B", c1_work_bytes, need);
+  const C1FoldArgs c1{x, T, F, dW, db, c1_work, c1_work_bytes};
+  return conv2_dgrad_impl(dz2, dz2_16, W, nullptr, z1bits, nullptr, B, T1, F1, D, zeros16, wc_work, work_bytes, stream,
+                          &c1);
+}
 static int conv2_dgrad_impl(const float* dz2, const void* dz2_16, const float* W, const float* z1,
                             const unsigned* z1bits, float* dz1, int B, int T1, int F1, int D, const float* zeros16,
-                            float* wc_work, long work_bytes, void* stream) {
+                            float* wc_work, long work_bytes, void* stream, const C1FoldArgs* c1) {
   const bool b16 = dz2_16 != nullptr;
   if (b16) dz2 = (const float*)dz2_16;  // bf16 pairs viewed as fp32 elements
   const int T2 = (T1 - 3) / 2 + 1, F2 = (F1 - 3) / 2 + 1;
   const long need__ = esp_conv2_dgrad_workspace_bytes(D);
   ESP_ARG_CHECK(work_bytes >= need__, "esp_conv2_dgrad: workspace %ld B < %ld B required (esp_conv2_dgrad_workspace_bytes)", work_bytes, need__);
   ESP_ARG_CHECK(B >= 1 && T2 >= 1 && F2 >= 1 && D % 32 == 0, "esp_conv2_dgrad: bad sizes (D %% 32 == 0 needed)");
-  ESP_ARG_CHECK(aligned16(dz2) && (z1bits || aligned16(z1)) && aligned16(dz1) && aligned16(zeros16) &&
+  ESP_ARG_CHECK(aligned16(dz2) && (z1bits || aligned16(z1)) && (c1 || aligned16(dz1)) && aligned16(zeros16) &&
                     aligned16(wc_work),
                 "esp_conv2_dgrad: operands must be 16-B aligned");
   hipStream_t st = (hipStream_t)stream;
@@ -845,6 +921,8 @@ static int conv2_dgrad_impl(const float* dz2, const void* dz2_16, const float* W
     ESP_CHECK_LAUNCH("esp_conv2_dgrad (planes)");
   }
   const int slot0[4] = {0, 4, 6, 8};
+  C1Regions c1r{};
+  long c1off = 0;
   for (int cls = 0; cls < 4; ++cls) {
     const int ph = cls >> 1, pw = cls & 1;
     const int Ha = (T1 - ph + 1) / 2, We = (F1 - pw + 1) / 2;
@@ -864,8 +942,13 @@ static int conv2_dgrad_impl(const float* dz2, const void* dz2_16, const float* W
     g.a = Operand{dz2, 0, 0, 0, 1, {}, 1};
     g.b = Operand{wc_work + (long)slot0[cls] * D * D, D, 0, 0, 1, {}, 1};
     g.c = dz1; g.ldc = D; g.alpha = 1.f; g.beta = 0.f;
-    g.bwd_act = ACT_RELU; g.pre = z1bits ? dz1 : z1;  // (bits: pre is never read; any aligned pointer)
+    g.bwd_act = ACT_RELU; g.pre = z1bits ? zeros16 : z1;  // (bits: pre is never read; any aligned pointer)
     g.cm_bits = reinterpret_cast<const uint32_t*>(z1bits); g.cm_bw = D / 32;
+    if (c1) {  // no C: the conv1 gradient records of this class launch
+      g.c = wc_work;  // (never written by EPI_C1FOLD)
+      g.c1_x = c1->x; g.c1_T = c1->T; g.c1_F = c1->F;
+      g.c1_part = c1->work + c1off;
+    }
     g.bf16 = g_compute;  // bf16 MFMA in the reduced-precision mode, as every other GEMM of the step
     if (bp) {
       g.b = Operand{reinterpret_cast<const float*>(planes + (long)slot0[cls] * D * D), D, 0, 0, 1, {}, 1};
@@ -888,6 +971,18 @@ static int conv2_dgrad_impl(const float* dz2, const void* dz2_16, const float* W
       return -1;
     }
     ESP_CHECK_LAUNCH("esp_conv2_dgrad");
+    if (c1) {
+      c1r.off[cls] = c1off;
+      c1r.grid[cls] = g_last_grid;
+      c1off += (long)g_last_grid * C1NT * 256 * 10;
+    }
+  }
+  if (c1) {
+    c1r.ncls = 4;
+    float* red = c1->work + 4L * persist_blocks(4) * C1NT * 256 * 10;
+    hipLaunchKernelGGL(c1fold_reduce_kernel, dim3((D / 128) * 4, C1_NCH), dim3(640), 0, st, c1->work, c1r, red);
+    hipLaunchKernelGGL(c1fold_finalize_kernel, dim3((D * 10 + 255) / 256), dim3(256), 0, st, red, D, c1->dW, c1->db);
+    ESP_CHECK_LAUNCH("esp_conv2_dgrad_c1fold (reduce)");
   }
   return 0;
 }

@@ -4,7 +4,8 @@
 // and KC x KC, EPI_BMUL for the FFN input gradient and EPI_RMASK for the gradient through conv2's
 // ReLU (KC x RC) and its row-mapped form for the implicit conv2 input gradient (I2CT_KC x RC); the
 // FFN w_1 kinds with the hidden state written as bf16 planes (EPI_FFN_*_PL), the FFN and ReLU-mask input
-// gradients as planes (EPI_BMUL_PL, EPI_RMASK_PL).
+// gradients as planes (EPI_BMUL_PL, EPI_RMASK_PL); EPI_C1FOLD (the implicit conv2 input gradient with the conv1
+// weight gradient folded in, 128 x 128 tiles).
 // See store_spec.
 #include "gemm_kernels.h"
 
@@ -38,6 +39,7 @@ bool glds_launch_spec(int ma, int mb, int bnt, int prec, int epi, dim3 grid, hip
       ESP_SPEC(EPI_RMASK_PL)
     } else if constexpr (MA == I2CT_KC && MB == RC) {
       ESP_SPEC(EPI_RMASKMAP)
+      if constexpr (BNT == 128 && BMT == 128) ESP_SPEC(EPI_C1FOLD)
     }
 #undef ESP_SPEC
   });

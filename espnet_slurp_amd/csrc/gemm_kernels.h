@@ -134,6 +134,12 @@ struct GemmArgs {
   // pixel * cm_bw + c / 32 = (z1[pixel][c] > 0)) instead of the fp32 map in pre; NULL: pre
   const uint32_t* cm_bits;
   int cm_bw;
+  // EPI_C1FOLD: the masked input gradient of the conv1 map is not stored; its conv1 weight / bias gradient
+  // partials (x = the conv1 input, T x F per utterance) accumulate per wave in registers across the block's
+  // tiles and land in c1_part, [grid][tn C1NT][wave 4][lane 64][10] (c1fold_reduce / c1fold_finalize)
+  const float* c1_x;
+  int c1_T, c1_F;
+  float* c1_part;
   // EPI_SMB (esp_attn_dscores): the dP = dctx V^T GEMM of rel-pos attention finishes the softmax
   // and rel_shift adjoints in its epilogue; pre = the attention probabilities (C's layout)
   int smb_rel;           // 0 off, 1 latest, 2 legacy rel_shift adjoint
@@ -149,6 +155,14 @@ struct GemmArgs {
   int band_c0, band_w;
 };
 
+// the class-grid row m as (utterance b, conv1-map row t1, column f1)
+__device__ __forceinline__ void row_btf(const GemmArgs& g, int m, int& b, int& t1, int& f1) {
+  b = (int)fdiv((uint32_t)m, g.cm_hw);
+  const int rem = m - b * (int)g.cm_hw.d;
+  const int a = (int)fdiv((uint32_t)rem, g.cm_w), e = rem - a * (int)g.cm_w.d;
+  t1 = 2 * a + g.cm_ph;
+  f1 = 2 * e + g.cm_pw;
+}
 __device__ __forceinline__ long row_pix(const GemmArgs& g, int m) {
   const int b = (int)fdiv((uint32_t)m, g.cm_hw);
   const int rem = m - b * (int)g.cm_hw.d;
@@ -173,7 +187,9 @@ enum { EPI_PLAIN = 0, EPI_FWD = 1, EPI_BWD = 2, EPI_BIAS = 3, EPI_BDR = 4, EPI_F
        // ... and the FFN's input gradient through the stored derivative (its only readers: w_1's GEMMs)
        EPI_BMUL_PL = 17,
        // ... and the gradient through a ReLU output (the subsampling's dz2: its readers are conv2's GEMMs)
-       EPI_RMASK_PL = 18 };
+       EPI_RMASK_PL = 18,
+       // EPI_RMASKMAP (bit-map mask) that writes no C: the conv1 weight gradient folded in (store_c1fold)
+       EPI_C1FOLD = 19 };
 // the fp32-output kind a planes-output kind computes
 constexpr int epi_base(int e) {
   return e == EPI_FFN_SWISH_PL ? EPI_FFN_SWISH
@@ -204,7 +220,7 @@ __host__ inline int epi_kind_spec(const GemmArgs& g) {
   if (g.cmap)
     return (g.wide && k == EPI_BWD && g.bwd_act == ACT_RELU && !g.drop_thresh && !g.r && !g.bias && g.alpha == 1.0f &&
             g.splits == 1)
-               ? EPI_RMASKMAP
+               ? (g.c1_part && g.cm_bits ? EPI_C1FOLD : EPI_RMASKMAP)
                : k;
   if (!g.wide) {
     if (g.ragged4 && k == EPI_PLAIN && g.splits == 1 && !g.rowsum) return g.r ? EPI_PR : EPI_P0;
@@ -743,6 +759,73 @@ __device__ __forceinline__ void store_spec_tiles(const GemmArgs& g, int z, int m
   } else {
     if (full) store_spec<EPI, TM, TN, true>(g, z, mrow0, ncol0, lane, acc);
     else store_spec<EPI, TM, TN, false>(g, z, mrow0, ncol0, lane, acc);
+  }
+}
+// EPI_C1FOLD records per block: C1NT column tiles (N <= 512 at 128-wide tiles)
+constexpr int C1NT = 4;
+// EPI_C1FOLD: conv1's weight / bias gradient folded into the implicit conv2 input-gradient tile (the conv1-map
+// gradient dz1 itself is never stored).  Per 32-column sub-tile j a lane holds, after the quad transpose, rows
+// m (4 per 32-row tile) x columns n..n+3; dz1 = mask(bit map) * acc, and for every such value the 9 conv1
+// taps x[b, 2 t1 + kt, 2 f1 + kf] and 1 (bias) are accumulated: 40 sums over the lane's 8 rows.  A
+// reduce-scatter over the 8 lanes sharing the columns (lane bits 5, 1, 0) leaves lane s = (l32 & 3) + 4 h with
+// sums 5 s .. 5 s + 4 (sum v: column n + v / 10, tap v % 10) over the wave's 64 rows, added into k[5 j ..].
+// Host: N % 128 == 0 and 128 x 128 tiles (TM = TN = 2), the mask as a bit map (cm_bits).
+template <int TM, int TN>
+__device__ __forceinline__ void store_c1fold(const GemmArgs& g, int mrow0, int ncol0, int lane, f32x16 (&acc)[TM][TN],
+                                             float (&k)[5 * TN]) {
+  const int h = lane >> 5, l32 = lane & 31, b1 = (l32 >> 1) & 1, b0 = l32 & 1;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = ncol0 + j * 32 + 4 * (l32 >> 2);
+    float a[40];
+#pragma unroll
+    for (int v = 0; v < 40; ++v) a[v] = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      quad_transpose(acc[i][j], lane);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int m = mrow0 + i * 32 + 8 * q + 4 * h + (l32 & 3);
+        if (m >= g.M) continue;
+        int b, t1, f1;
+        row_btf(g, m, b, t1, f1);
+        const long pix = ((long)b * g.cm_T1 + t1) * g.cm_F1 + f1;
+        const uint32_t w = g.cm_bits[pix * g.cm_bw + (n >> 5)] >> (n & 31);
+        const float* xp = g.c1_x + ((long)b * g.c1_T + 2 * t1) * g.c1_F + 2 * f1;
+        float pt[9];
+#pragma unroll
+        for (int kt = 0; kt < 3; ++kt)
+#pragma unroll
+          for (int kf = 0; kf < 3; ++kf) pt[kt * 3 + kf] = xp[kt * g.c1_F + kf];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float d = (w >> e) & 1u ? acc[i][j][4 * q + e] : 0.f;
+#pragma unroll
+          for (int t = 0; t < 9; ++t) a[e * 10 + t] = fmaf(d, pt[t], a[e * 10 + t]);
+          a[e * 10 + 9] += d;
+        }
+      }
+    }
+    // reduce-scatter: lane bit 5 (h) keeps sums [20 h, 20 h + 20), bit 1 [10 b1, +10) of those, bit 0 [5 b0, +5)
+    float r20[20];
+#pragma unroll
+    for (int u = 0; u < 20; ++u) {
+      const float send = h ? a[u] : a[20 + u];
+      r20[u] = (h ? a[20 + u] : a[u]) + __shfl_xor(send, 32, 64);
+    }
+    float r10[10];
+#pragma unroll
+    for (int u = 0; u < 10; ++u) {
+      const float send = b1 ? r20[u] : r20[10 + u];
+      r10[u] = (b1 ? r20[10 + u] : r20[u]) +
+               __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0x4E, 0xF, 0xF, false));
+    }
+#pragma unroll
+    for (int u = 0; u < 5; ++u) {
+      const float send = b0 ? r10[u] : r10[5 + u];
+      k[5 * j + u] += (b0 ? r10[5 + u] : r10[u]) +
+                      __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1, 0xF, 0xF, false));
+    }
   }
 }
 template <int TM, int TN>
@@ -1821,7 +1904,13 @@ __global__ __launch_bounds__(glds_threads(BMT), (glds_occupancy<BNT, EPI, BMT, P
 
   const int G = gridDim.x;
   int t = blockIdx.x;
-  if (t >= x.ntiles) return;
+  if (t >= x.ntiles) {
+    if constexpr (EPI == EPI_C1FOLD) {  // a block without tiles: zero records (c1fold_reduce reads every block's)
+      float* dst = g.c1_part + (long)blockIdx.x * C1NT * NTK * 10;
+      for (int e = threadIdx.x; e < x.ntx * NTK * 10; e += NTK) dst[e] = 0.f;
+    }
+    return;
+  }
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1878,6 +1967,28 @@ __global__ __launch_bounds__(glds_threads(BMT), (glds_occupancy<BNT, EPI, BMT, P
   wait_vm0();
   raw_barrier();
   int buf = 0;
+
+  // EPI_C1FOLD: this wave's conv1-gradient sums over its tiles of one column tile tn (store_c1fold), written
+  // (first time) or added (the block returns to tn) to its record when the column tile changes, and at the end
+  constexpr int C1K = EPI == EPI_C1FOLD ? 5 * TN : 1;
+  float c1k[C1K];
+  int c1tn = -1;
+  bool c1seen[C1NT] = {false, false, false, false};
+  auto c1rec = [&](int tn) { return g.c1_part + ((((long)blockIdx.x * C1NT + tn) * NW + wave) * 64 + lane) * 10; };
+  auto c1flush = [&]() {
+    if constexpr (EPI == EPI_C1FOLD) {
+      if (c1tn < 0) return;
+      float* dst = c1rec(c1tn);
+#pragma unroll
+      for (int u = 0; u < C1K; ++u) {
+        dst[u] = c1seen[c1tn] ? dst[u] + c1k[u] : c1k[u];
+        c1k[u] = 0.f;
+      }
+      c1seen[c1tn] = true;
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < C1K; ++u) c1k[u] = 0.f;
 
   for (;;) {
     f32x16 acc[TM][TN];
@@ -2246,7 +2357,13 @@ __global__ __launch_bounds__(glds_threads(BMT), (glds_occupancy<BNT, EPI, BMT, P
       splitk_combine<BMT, BNT>(g, c.z, c.m0 / BMT, c.tn, x.ntx, x.nty, reinterpret_cast<int*>(smem + ST * BUF));
     } else {
       float* W = g.splits > 1 ? g.work + ((long)c.split * g.batch + c.z) * (long)g.M * g.N : nullptr;
-      if constexpr (EPI >= EPI_BIAS) {  // specialised kinds: never split-K, always wide
+      if constexpr (EPI == EPI_C1FOLD) {
+        if (c.tn != c1tn) {
+          c1flush();
+          c1tn = c.tn;
+        }
+        if constexpr (TM == 2 && TN == 2) store_c1fold<TM, TN>(g, c.m0 + wm * TM * 32, c.n0 + wn * TN * 32, lane, acc, c1k);
+      } else if constexpr (EPI >= EPI_BIAS) {  // specialised kinds: never split-K, always wide
         const int mr0 = c.m0 + wm * TM * 32, nc0 = c.n0 + wn * TN * 32;
         if (col_epi_ok<EPI>() && mr0 + TM * 32 <= g.M && nc0 + TN * 32 <= g.N) {
           const long cb = c_base(g, c.z);
@@ -2268,6 +2385,16 @@ __global__ __launch_bounds__(glds_threads(BMT), (glds_occupancy<BNT, EPI, BMT, P
     if (!has_next) break;
     t = tnext;
     c = cn;
+  }
+  if constexpr (EPI == EPI_C1FOLD) {
+    c1flush();
+#pragma unroll
+    for (int tn = 0; tn < C1NT; ++tn)
+      if (tn < x.ntx && !c1seen[tn]) {
+        float* dst = c1rec(tn);
+#pragma unroll
+        for (int u = 0; u < 10; ++u) dst[u] = 0.f;
+      }
   }
 }
 

@@ -58,6 +58,7 @@ class _Workspace:
 
 WS = _Workspace()
 _WS2 = _Workspace()
+_WS_C1 = _Workspace()  # esp_conv2_dgrad_c1fold's per-block records
 _GEMM_WS = _Workspace(zero=True)  # split-K partials (stream-ordered reuse) + arrival tickets (last 64 KB)
 _GEMM_WS_BYTES = 64 << 20
 
@@ -1382,6 +1383,10 @@ CONV2_IMPLICIT_DGRAD = True
 # gradient's epilogue reads it (esp_conv2_dgrad_bits) instead of the fp32 map -- 1/32 of the mask bytes
 # (ESP_CONV2_BITS=0: the fp32 map, an A/B switch)
 CONV2_DGRAD_BITS = os.environ.get("ESP_CONV2_BITS", "1") != "0"
+# training: conv1's weight gradient folded into the conv2 input gradient's epilogue (esp_conv2_dgrad_c1fold: the
+# 7.7 GB conv1-map gradient of C2 B=256 is never stored nor re-read); ESP_CONV1_FOLD=0: esp_conv2_dgrad_bits +
+# esp_conv1_wgrad (an A/B switch)
+CONV1_FOLD = os.environ.get("ESP_CONV1_FOLD", "1") != "0"
 
 
 def conv2_wgrad_bf16(dz2_16, z1_16, dw, db, B, T1, F1, D):
@@ -1399,6 +1404,30 @@ def conv2_wgrad_bf16(dz2_16, z1_16, dw, db, B, T1, F1, D):
         T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
         npix = B * T2 * F2
         _PROF.append((2.0 * D * 9 * D * npix, ev0, ev1, (RC, I2C_RC, D, 9 * D, npix, 1, "bf16"), 0.0))
+
+
+def conv2_dgrad_c1fold(dz2, W, z1bits, x, T, F, dW1, db1, B, T1, F1, D, dz2_16=None):
+    """The implicit conv2 input gradient with conv1's weight / bias gradient folded into its epilogue
+    (esp_conv2_dgrad_c1fold): dW1 (D x 9) and db1 (D) accumulate sum dz1 * x-patch and sum dz1 over the conv1
+    map; dz1 is never materialised.  The mask comes from conv1_fwd's bit map; x is the conv1 input."""
+    assert dz2 is not None or dz2_16 is not None
+    assert z1bits.dtype == torch.int32
+    _f32(dz2, W, x, dW1, db1)
+    key = str(W.device)
+    if key not in _ZEROS:
+        _ZEROS[key] = torch.zeros(64, dtype=torch.float32, device=W.device)
+    n = _wsize("esp_conv2_dgrad", D)
+    wc = _ws(_WS2, "esp_conv2_dgrad", n, W.device)
+    n1 = _wsize("esp_conv2_c1fold")
+    w1 = _ws(_WS_C1, "esp_conv2_c1fold", n1, W.device)
+    _native.call("esp_conv2_dgrad_c1fold", None if dz2_16 is not None else _p(dz2), _p(dz2_16), _p(W), _p(z1bits),
+                 _p(x), T, F, _p(dW1), _p(db1), B, T1, F1, D, _p(_ZEROS[key]), _p(wc), n, _p(w1), n1, _st())
+    _guard_post("esp_conv2_dgrad", wc, n)
+
+
+def conv2_c1fold_ok(D: int) -> bool:
+    """esp_conv2_dgrad_c1fold takes D % 128 == 0, D <= 512 (CONV1_FOLD: off -> esp_conv2_dgrad_bits + esp_conv1_wgrad)."""
+    return CONV1_FOLD and CONV2_DGRAD_BITS and CONV2_IMPLICIT_DGRAD and D % 128 == 0 and D <= 512
 
 
 def conv2_dgrad(dz2, W, z1, dz1, B, T1, F1, D, dz2_16=None, z1bits=None):

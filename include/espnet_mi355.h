@@ -418,6 +418,16 @@ int esp_conv2_dgrad(const float* dz2, const float* W, const float* z1, float* dz
 int esp_conv2_dgrad_bits(const float* dz2, const void* dz2_16, const float* W, const unsigned* z1bits, float* dz1,
                          int B, int T1, int F1, int D, const float* zeros16, float* wc_work, long work_bytes,
                          void* stream);
+/* ABI 32: esp_conv2_dgrad_bits with conv1's weight / bias gradient folded into the class GEMMs' epilogue
+ * (replaces esp_conv2_dgrad_bits + esp_conv1_wgrad, subsampling.py:53-87 backward): dW (D x 9) += sum over the
+ * conv1 map of dz1 * x-patch, db (D) += sum of dz1, dz1 never materialised.  x: the conv1 input (B, T, F) as
+ * esp_conv1_fwd took it; c1_work: esp_conv2_c1fold_workspace_bytes() (per-block partial records + their
+ * fixed-order reduction: deterministic).  D % 128 == 0, D <= 512. */
+int esp_conv2_dgrad_c1fold(const float* dz2, const void* dz2_16, const float* W, const unsigned* z1bits,
+                           const float* x, int T, int F, float* dW, float* db, int B, int T1, int F1, int D,
+                           const float* zeros16, float* wc_work, long work_bytes, float* c1_work,
+                           long c1_work_bytes, void* stream);
+long esp_conv2_c1fold_workspace_bytes(void);
 int esp_col2im_relu(const float* dcol, const float* z1, float* dz1, int B, int T1, int F1, int D,
                     void* stream);
 int esp_conv1_wgrad(const float* x, const float* dz1, float* dW, float* db, int B, int T, int F,

@@ -896,6 +896,44 @@ def test_conv2_dgrad_bits_mask_bit_exact(dev, T1, F1, D):
         assert torch.equal(got, ref), kw.keys()
 
 
+@pytest.mark.parametrize("T1,F1,D,bf16", [(31, 39, 128, False), (20, 13, 256, False), (9, 7, 128, False),
+                                           (31, 39, 128, True), (13, 17, 512, False)])
+def test_conv2_dgrad_c1fold_matches_two_pass(dev, T1, F1, D, bf16):
+    """esp_conv2_dgrad_c1fold (conv1's weight / bias gradient folded into the implicit conv2 input gradient's
+    epilogue, dz1 never stored) against the two-pass form it replaces (esp_conv2_dgrad_bits -> dz1 ->
+    esp_conv1_wgrad) and against the fp64 sums over that dz1; the fold sums in a different (fixed) order, so
+    the gate is fp32 rounding.  bf16: dz2 in bf16 (the bf16 mode's class GEMMs)."""
+    B = 3
+    T, F = 2 * T1 + 2, 2 * F1 + 1
+    T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
+    g = torch.Generator().manual_seed(43)
+    x = torch.randn(B, T, F, generator=g).to(dev)
+    w0, b0 = (torch.randn(D, 1, 3, 3, generator=g) * 0.3).to(dev), (torch.randn(D, generator=g) * 0.1).to(dev)
+    W = (torch.randn(D, D, 3, 3, generator=g) * 0.05).to(dev)
+    npx = B * T1 * F1
+    z1 = torch.empty(npx * D, device=dev)
+    bits = torch.empty(npx * D // 32, dtype=torch.int32, device=dev)
+    K.conv1_fwd(x, w0, b0, z1, B, T, F, D, zbits=bits)
+    dz2 = torch.randn(B * T2 * F2, D, generator=g).to(dev)
+    kw = dict(dz2_16=K.to_bf16(dz2, B * T2 * F2, D, D)) if bf16 else {}
+    dWa, dba = torch.full((D, 9), 0.25, device=dev), torch.full((D,), -0.5, device=dev)
+    dWb, dbb = dWa.clone(), dba.clone()
+    dz1 = torch.empty(npx * D, device=dev)
+    with K.gemm_compute("bf16" if bf16 else "fp32"):
+        K.conv2_dgrad(None if bf16 else dz2, W, None, dz1, B, T1, F1, D, z1bits=bits, **kw)
+        K.conv1_wgrad(x, dz1, dWa, dba, B, T, F, D)
+        K.conv2_dgrad_c1fold(None if bf16 else dz2, W, bits, x, T, F, dWb, dbb, B, T1, F1, D, **kw)
+    torch.cuda.synchronize()
+    # fp64 sums over the same dz1
+    xd = x.double().cpu()
+    pt = torch.stack([xd[:, kt:kt + 2 * T1 - 1:2, kf:kf + 2 * F1 - 1:2] for kt in range(3) for kf in range(3)], -1)
+    dzd = dz1.double().cpu().view(B, T1, F1, D)
+    wref = 0.25 + torch.einsum("btfc,btfk->ck", dzd, pt)
+    bref = -0.5 + dzd.sum((0, 1, 2))
+    assert rel_err(dWb.cpu(), wref) < 5e-6 and rel_err(dbb.cpu(), bref) < 5e-6
+    assert rel_err(dWb.cpu(), dWa.cpu().double()) < 1e-5 and rel_err(dbb.cpu(), dba.cpu().double()) < 1e-5
+
+
 @pytest.mark.parametrize("T1,F1", [(31, 39), (9, 7), (33, 40)])
 def test_conv2_bf16_operands_match_staged_rounding(dev, T1, F1):
     """The bf16 mode's conv2 forward (esp_conv2_fwd_bf16: implicit im2col over conv1's bf16 copy of z1,
