@@ -923,15 +923,7 @@ __device__ __forceinline__ f32x4 mfma_np(const Frag16& a, const Frag16& b, f32x4
 #ifndef ESP_ATTN_PREFETCH
 #define ESP_ATTN_PREFETCH 3
 #endif
-#ifndef ESP_ATTN_PREFETCH_LEGACY
-#define ESP_ATTN_PREFETCH_LEGACY ESP_ATTN_PREFETCH
-#endif
-// legacy rel_shift in relpos_probs_lds_kernel: how band blocks past the diagonal get the shifted A rows
-// q_v[i+1] (split once into LDS in the prologue): 1 a second register fragment and a per-step select, 2 the
-// fragment re-read from LDS every step and selected at step g
-#ifndef ESP_ATTN_LEGACY_SEL
-#define ESP_ATTN_LEGACY_SEL 1
-#endif
+
 constexpr int RW_ROWS = 16, RW_PITCH = 37;
 // store-transpose rows: 64 floats, so the float4 read-back (ds_read_b128 lane groups of 16 lanes over
 // two rows, bank (a/4) mod 64) is conflict-free, with the column XOR-ed by 16 in rows 4..7 and 12..15
@@ -1449,13 +1441,13 @@ __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
   // the block's last 16 rows at key tile 0)
   __syncthreads();
 
-  FragPl<NPL> xv2;  // legacy (ESP_ATTN_LEGACY_SEL 1): the shifted rows' fragment, from the stage image
-  if constexpr (LEGACY && ESP_ATTN_LEGACY_SEL == 1)
-    read_frag_pl(reinterpret_cast<const uint8_t*>(stage[wave]), PLB, li, q4, xv2);
+  FragPl<NPL> xv2;  // legacy: the shifted rows' fragment, from the stage image
+  if constexpr (LEGACY) read_frag_pl(reinterpret_cast<const uint8_t*>(stage[wave]), PLB, li, q4, xv2);
   f32x4 sc[NTA];
   // key tiles / band blocks PF steps ahead in registers (slot s % PF holds step s's): a step's loads
   // have PF steps of work to arrive before they are split into LDS
-  constexpr int PF = LEGACY ? ESP_ATTN_PREFETCH_LEGACY : ESP_ATTN_PREFETCH;
+  // (legacy at depth 2: 651 vs 618 us with the spilling loop, profiles/r06f_kernel_summary_legacy_b256_pf2_nobits.txt)
+  constexpr int PF = ESP_ATTN_PREFETCH;
   float4 nk[PF], np[PF];
 #pragma unroll
   for (int s = 1; s < PF; ++s)
@@ -1465,17 +1457,6 @@ __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
     }
 #pragma unroll
   for (int t = 0; t < NTA; ++t) {
-#if ESP_ATTN_LEGACY_SEL == 2
-    if constexpr (LEGACY) {  // the shifted fragment re-read every step, selected from step g on
-      FragPl<NPL> nv;
-      read_frag_pl(reinterpret_cast<const uint8_t*>(stage[wave]), PLB, li, q4, nv);
-      const bool sw = t == g;
-#pragma unroll
-      for (int p_ = 0; p_ < NPL; ++p_)
-#pragma unroll
-        for (int m_ = 0; m_ < 2; ++m_) xv.v[p_][m_] = sw ? nv.v[p_][m_] : xv.v[p_][m_];
-    }
-#endif
     if (t + PF < NTA) {
       nk[t % PF] = *k_src(t + PF);
       np[t % PF] = *p_src(t + PF);
@@ -1489,9 +1470,11 @@ __global__ __launch_bounds__(256, 2) void relpos_probs_lds_kernel(
     ESP_SLOT_CHECK(pgen[pslot(t - wave)], t - wave, 5);
     const f32x4 a = mfma_pl(xu, kf, f32x4{0.f, 0.f, 0.f, 0.f});
     f32x4 s;
-    if constexpr (LEGACY && ESP_ATTN_LEGACY_SEL == 1) {
+    if constexpr (LEGACY) {
       // band blocks t+1 >= g+1 (the shifted part) take the A rows q_v[i+1]: a per-step select, branch-free
-      // (a branch at t == g in the unrolled loop split it into 24 scheduling regions: 42 VGPRs spilled)
+      // (a branch at t == g in the unrolled loop split it into 24 scheduling regions: 42 VGPRs spilled, 618
+      // vs 521 us; re-reading the fragment from LDS every step and selecting it: 596 vs 581 us microbench,
+      // profiles/r06g_probs.log)
       FragPl<NPL> xa;
       const bool sw = t >= g;
 #pragma unroll
