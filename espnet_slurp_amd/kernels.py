@@ -1380,13 +1380,13 @@ _ZEROS = {}
 # the column path.
 CONV2_IMPLICIT_DGRAD = True
 # training: conv1 also writes its ReLU mask as a packed bit map (esp_conv1_fwd_bits) and the implicit input
-# gradient's epilogue reads it (esp_conv2_dgrad_bits) instead of the fp32 map -- 1/32 of the mask bytes
-# (ESP_CONV2_BITS=0: the fp32 map, an A/B switch)
-CONV2_DGRAD_BITS = os.environ.get("ESP_CONV2_BITS", "1") != "0"
+# gradient's epilogue reads it (esp_conv2_dgrad_bits) instead of the fp32 map -- 1/32 of the mask bytes; about
+# neutral alone (class GEMMs -58 us each, conv1 +0.1-0.2 ms), needed by CONV1_FOLD
+CONV2_DGRAD_BITS = True
 # training: conv1's weight gradient folded into the conv2 input gradient's epilogue (esp_conv2_dgrad_c1fold: the
-# 7.7 GB conv1-map gradient of C2 B=256 is never stored nor re-read); ESP_CONV1_FOLD=0: esp_conv2_dgrad_bits +
-# esp_conv1_wgrad (an A/B switch)
-CONV1_FOLD = os.environ.get("ESP_CONV1_FOLD", "1") != "0"
+# 7.7 GB conv1-map gradient of C2 B=256 is never stored nor re-read): 1470.4 vs 1458.0 utt/s with False
+# (esp_conv2_dgrad_bits + esp_conv1_wgrad; profiles/r06i_bench*.log; A/B: tools/bench_with.py kernels.CONV1_FOLD=0)
+CONV1_FOLD = True
 
 
 def conv2_wgrad_bf16(dz2_16, z1_16, dw, db, B, T1, F1, D):

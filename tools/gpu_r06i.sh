@@ -1,4 +1,5 @@
 #!/bin/bash
+# (the ESP_CONV1_FOLD environment switch this ran with is now kernels.CONV1_FOLD: tools/bench_with.py kernels.CONV1_FOLD=0)
 # round 6 (i): conv1's weight gradient folded into the conv2 input gradient (esp_conv2_dgrad_c1fold) -- its
 # kernel parity test, then the full GPU suite, a C2 B=256 kernel trace with the fold on and off
 # (ESP_CONV1_FOLD=0), bench lines
