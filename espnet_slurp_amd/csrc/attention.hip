@@ -1288,7 +1288,10 @@ __device__ __forceinline__ f32x4 mfma_pl(const FragPl<NPL>& a, const FragPl<NPL>
 //            into pslot(-4), which wave 3 read in the prologue -- the block barrier after the prologue's
 //            band read orders it (round-5 fix).
 //   ring[w], stage[w]: per wave (LDS is in order within a wave; asm memory fences keep the compiler from
-//            reordering the ring writes / reads).
+//            reordering the ring writes / reads).  Legacy: the block writes every wave's shifted-row plane
+//            image into stage[w] in the prologue (thread -> row sr of all four images), the block barrier after
+//            the prologue orders those writes before wave w reads its image into xv2 (before the key loop);
+//            after that only wave w touches stage[w] (the store transpose after the loop).
 // ESP_ATTN_SLOT_CHECK=1 (a separate build: make VARIANT=_slotchk EXTRA=-DESP_ATTN_SLOT_CHECK=1, loaded with
 // ESP_LIB_VARIANT=_slotchk) checks this at run time: each slot carries a per-wave generation word in LDS --
 // set to BUSY before a wave writes its rows of the slot and to the block / tile index after -- and every
