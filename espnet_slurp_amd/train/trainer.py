@@ -36,7 +36,8 @@ class TrainerOptions:
     # reduced-precision training (trainer.py:181-195,554 offer fp16 autocast + GradScaler under
     # `use_amp`): here every GEMM takes bf16 operands with fp32 accumulate (esp_set_gemm_compute);
     # parameters, gradients, optimizer state and all non-GEMM kernels stay fp32.  bf16 has the
-    # fp32 exponent range, so no loss scaler is needed.  SURVEY §8(d) C5.
+    # fp32 exponent range, so the loss is never multiplied by a scale; the GradScaler's state is
+    # still kept as the reference keeps it (Trainer.set_scaler).  SURVEY §8(d) C5.
     use_amp: bool = False
     # HIP-graph mode with variable-length data: pad each batch's frame axis up to a multiple of
     # graph_buckets[0] frames and its target axis to a multiple of graph_buckets[1] tokens, so
@@ -103,6 +104,30 @@ class Trainer:
         self._flag_event = torch.cuda.Event() if cuda else None
         self._pending = False
         self._last_weight = None  # the (all-reduced) weight of the last step, for the reporter
+        self.scaler = None
+        self._found_inf = None
+
+    def set_scaler(self, scaler):
+        """use_amp's loss-scaler state (trainer.py:181-195, 613-682): a torch GradScaler whose scale and
+        growth tracker evolve as the reference's do -- after every optimizer step, x growth_factor once
+        growth_interval consecutive steps were finite, x backoff_factor (and the step skipped) when the
+        gradient norm was not -- updated on device from the step's finite flag (torch._amp_update_scale_,
+        the op GradScaler.update runs; captured with the step in graph mode, so set it before the first
+        step).  The bf16 arithmetic never multiplies the loss by the scale (bf16 has the fp32 exponent
+        range: the unscaled gradients are the ones the reference unscales to), so the scale only travels in
+        checkpoint.pth's "scaler" entry, which resumes either way."""
+        self.scaler = scaler
+        if scaler is not None and scaler.is_enabled():
+            scaler._lazy_init_scale_growth_tracker(self._clip.device)
+            self._found_inf = torch.zeros(1, dtype=torch.float32, device=self._clip.device)
+
+    def _scaler_update(self):
+        s = self.scaler
+        if s is None or not s.is_enabled():
+            return
+        self._found_inf.fill_(1.0).sub_(self._clip[2:3])  # 1 where the step's gradient norm was non-finite
+        torch._amp_update_scale_(s._scale, s._growth_tracker, self._found_inf, s._growth_factor,
+                                 s._backoff_factor, s._growth_interval)
 
     @staticmethod
     def resume(checkpoint, model, reporter, optimizers, schedulers, scaler=None, ngpu: int = 0):
@@ -150,6 +175,7 @@ class Trainer:
             clip_grad_norm_(model.flat, opts.grad_clip, self._clip)
             # the Adam kernel itself skips a non-finite update on device (trainer.py:651-667)
             self.optimizer.step(clip=self._clip)
+            self._scaler_update()
             if check_finite:
                 self._flag_host.copy_(self._clip[2:3], non_blocking=True)
                 if self._flag_event is not None:
@@ -231,6 +257,7 @@ class Trainer:
     def _opt_tail(self):
         clip_grad_norm_(self.model.flat, self.options.grad_clip, self._clip)
         self.optimizer.step_device(self._clip, self.scheduler)  # counts itself only if finite
+        self._scaler_update()
         self.model.flat.grad.zero_()
 
     # ---------------------------------------------------------------- DDP + HIP graph
@@ -534,6 +561,11 @@ class Trainer:
         schedulers = [self.scheduler]
         if out is not None and rank0:
             out.mkdir(parents=True, exist_ok=True)
+        if scaler is None and o.use_amp and self.model.flat.flat.is_cuda and self.scaler is None:
+            scaler = torch.amp.GradScaler("cuda")  # trainer.py:190-193 (use_amp)
+        if scaler is not None:
+            self.set_scaler(scaler)
+        scaler = self.scaler
         if o.resume and out is not None and (out / "checkpoint.pth").exists():
             CK.resume(out / "checkpoint.pth", self.model, reporter, [self.optimizer], schedulers, scaler,
                       ngpu=1 if self.model.flat.flat.is_cuda else 0)

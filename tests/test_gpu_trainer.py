@@ -94,3 +94,45 @@ def test_reference_style_loop_on_flat_parameters(dev):
     _check_params(model, g)
     # the parameters are still views of the flat buffer the kernels read
     assert all(p.data_ptr() == model.flat.view(p).data_ptr() for p in model.parameters())
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_trainer_amp_scaler_state(dev, graph):
+    """use_amp's GradScaler state (trainer.py:181-195, 613-682): after every optimizer step the scale grows by
+    growth_factor once growth_interval consecutive steps were finite and backs off (the step skipped) on a
+    non-finite gradient norm -- the reference's scaler.update() sequence, here driven on device by the step's
+    finite flag (eager and inside the captured step).  Its state_dict is torch's, so checkpoint.pth's
+    "scaler" entry round-trips."""
+    from espnet_slurp_amd.optimizers.fused_adam import FusedAdam
+    from espnet_slurp_amd.train.trainer import Trainer, TrainerOptions
+    cfg = small_cfg("latest")
+    model = build_model(cfg, dev, dropout=0.0)
+    load_seeded(model, cfg, 11)
+    model.train()
+    opt = FusedAdam(model.parameters(), model.flat, lr=1e-3)
+    tr = Trainer(model, opt, None, TrainerOptions(grad_clip=5.0, use_amp=True), cuda_graph=graph)
+    scaler = torch.amp.GradScaler("cuda", init_scale=1024.0, growth_interval=2)
+    tr.set_scaler(scaler)
+    speech, slen, text, tlen = O.synthetic_batch(3, 96, 80, 32, [96, 80, 71], [6, 5, 4], 12)
+    good = dict(speech=speech.to(dev), speech_lengths=slen, text=text, text_lengths=tlen)
+    finite = [True, True, False, True, True, True]
+    want_scale, tracker = 1024.0, 0
+    for step, ok in enumerate(finite):
+        b = dict(good, speech=good["speech"].clone(), text=good["text"].clone())
+        if not ok:
+            b["speech"][0, 3, 5] = float("nan")
+        tr.train_one_step(b)
+        tr.resolve_pending()
+        tr.sync_host_state()
+        if ok:
+            tracker += 1
+            if tracker == 2:
+                want_scale, tracker = want_scale * 2.0, 0
+        else:
+            want_scale, tracker = want_scale * 0.5, 0
+        st = scaler.state_dict()
+        assert st["scale"] == want_scale and st["_growth_tracker"] == tracker, (step, st)
+    assert tr.n_skipped == 1 and tr.n_updates == len(finite)
+    again = torch.amp.GradScaler("cuda")
+    again.load_state_dict(scaler.state_dict())
+    assert again.state_dict() == scaler.state_dict()
