@@ -288,9 +288,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     # B per GPU ("tune; report B"): measured at C2 64 -> 848, 96 -> 875, 128 -> 906,
     # 192 -> 917, 256 -> 932 utt/s in round 1 (profiles/r01g_batch_sweep.txt); at the round-4 HEAD on one
-    # box 128 -> 1299, 192 -> 1297, 256 -> 1342 (profiles/r04i_batch_sweep.txt).  256 (8-GPU global
-    # batch 2048); tests/test_gpu_bench_shape.py checks B=128 against the oracle and B=256 against B=128
-    ap.add_argument("--batch", type=int, default=256, help="utterances per GPU")
+    # box 128 -> 1299, 192 -> 1297, 256 -> 1342 (profiles/r04i_batch_sweep.txt).  Round 6: 384 (8-GPU global
+    # batch 3072): 1471.4 / 1477.8 vs 1461.9 / 1464.3 utt/s at 256, alternating on one box, 211 GiB peak HBM on
+    # the 1-GPU and the DP path (profiles/r06q_*); tests/test_gpu_bench_shape.py checks B=128 against the
+    # oracle and B=256 / B=384 against B=128
+    ap.add_argument("--batch", type=int, default=384, help="utterances per GPU")
     ap.add_argument("--d", type=int, default=256)
     ap.add_argument("--heads", type=int, default=4)
     ap.add_argument("--ff", type=int, default=1024)
