@@ -188,7 +188,8 @@ def gemm_algorithmic_bytes(shapes) -> float:
     tot = 0.0
     for key, (n, _ms, _f, extra) in shapes.items():
         ma, mb, M, N, Kd, batch = key[:6]  # (+ a tag for the bf16-operand / score-gradient GEMMs)
-        if key[6:] == ("conv2_dgrad",):  # the implicit conv2 input gradient: its entry holds the whole count
+        if key[6:] in (("conv2_dgrad",), ("conv2_dgrad_c1fold",)):  # the implicit conv2 input gradient: its entry
+            # holds the whole count
             tot += extra
             continue
         a = M * Kd * (4 / 9 if ma >= 2 else 1.0)

@@ -1420,9 +1420,21 @@ def conv2_dgrad_c1fold(dz2, W, z1bits, x, T, F, dW1, db1, B, T1, F1, D, dz2_16=N
     wc = _ws(_WS2, "esp_conv2_dgrad", n, W.device)
     n1 = _wsize("esp_conv2_c1fold")
     w1 = _ws(_WS_C1, "esp_conv2_c1fold", n1, W.device)
+    if _PROF is not None:
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record()
     _native.call("esp_conv2_dgrad_c1fold", None if dz2_16 is not None else _p(dz2), _p(dz2_16), _p(W), _p(z1bits),
                  _p(x), T, F, _p(dW1), _p(db1), B, T1, F1, D, _p(_ZEROS[key]), _p(wc), n, _p(w1), n1, _st())
     _guard_post("esp_conv2_dgrad", wc, n)
+    if _PROF is not None:  # the 4 class GEMMs (+ the records' two small reductions) as one family entry
+        ev1.record()
+        T2, F2 = (T1 - 3) // 2 + 1, (F1 - 3) // 2 + 1
+        npix2 = B * T2 * F2
+        # algorithmic bytes: dz2 (4 B, or 2 B as bf16) and W read, the bit map and the conv1 input read; no dz1
+        eb = 2.0 if dz2_16 is not None else 4.0
+        _PROF.append((2.0 * npix2 * 9 * D * D, ev0, ev1, (4, RC, B * T1 * F1, D, 9 * D, 1, "conv2_dgrad_c1fold"),
+                      eb * npix2 * D + 4.0 * 9 * D * D + B * T1 * F1 * D / 8.0 + 4.0 * B * T * F))
 
 
 def conv2_c1fold_ok(D: int) -> bool:

@@ -26,7 +26,7 @@ def main():
     for line in open(order):
         fl, ev_ms, key = line.rstrip("\n").split("\t")
         launches.append((float(fl), float(ev_ms), ast.literal_eval(key)))
-    need = sum(4 if k[-1] == "conv2_dgrad" else 1 for _, _, k in launches)
+    need = sum(4 if k[-1] in ("conv2_dgrad", "conv2_dgrad_c1fold") else 1 for _, _, k in launches)
     # GEMM dispatches, each with the split-K reduction(s) that follow it
     gem = []
     for s, e, name in rows:
@@ -40,7 +40,7 @@ def main():
     shapes = collections.OrderedDict()
     i = 0
     for fl, ev_ms, key in launches:
-        k = 4 if key[-1] == "conv2_dgrad" else 1
+        k = 4 if key[-1] in ("conv2_dgrad", "conv2_dgrad_c1fold") else 1
         ns = sum(sum(g) for g in gem[i:i + k])
         nk = sum(g[0] for g in gem[i:i + k])
         i += k
