@@ -769,14 +769,29 @@ constexpr int C1NT = 4;
 // taps x[b, 2 t1 + kt, 2 f1 + kf] and 1 (bias) are accumulated: 40 sums over the lane's 8 rows.  A
 // reduce-scatter over the 8 lanes sharing the columns (lane bits 5, 1, 0) leaves lane s = (l32 & 3) + 4 h with
 // sums 5 s .. 5 s + 4 (sum v: column n + v / 10, tap v % 10) over the wave's 64 rows, added into k[5 j ..].
+// The lane's 8 rows are decomposed once for both sub-tiles (14.57 -> 14.27 ms per C2 B=256 call, r06v; with the
+// accumulators kept live and no fold the class GEMMs take 12.0 ms: the fold epilogue is ~2.3 ms of VALU + loads).
 // Host: N % 128 == 0 and 128 x 128 tiles (TM = TN = 2), the mask as a bit map (cm_bits).
 template <int TM, int TN>
 __device__ __forceinline__ void store_c1fold(const GemmArgs& g, int mrow0, int ncol0, int lane, f32x16 (&acc)[TM][TN],
                                              float (&k)[5 * TN]) {
   const int h = lane >> 5, l32 = lane & 31, b1 = (l32 >> 1) & 1, b0 = l32 & 1;
+  // the lane's 8 rows decomposed once for both 32-column sub-tiles: mask-word and conv1-input addresses
+  const uint32_t* wrow[TM][4];
+  const float* xrow[TM][4];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int m = min(mrow0 + i * 32 + 8 * q + 4 * h + (l32 & 3), g.M - 1);
+      int b, t1, f1;
+      row_btf(g, m, b, t1, f1);
+      wrow[i][q] = g.cm_bits + (((long)b * g.cm_T1 + t1) * g.cm_F1 + f1) * g.cm_bw + (ncol0 >> 5);
+      xrow[i][q] = g.c1_x + ((long)b * g.c1_T + 2 * t1) * g.c1_F + 2 * f1;
+    }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int n = ncol0 + j * 32 + 4 * (l32 >> 2);
+    const int sh = 4 * (l32 >> 2);
     float a[40];
 #pragma unroll
     for (int v = 0; v < 40; ++v) a[v] = 0.f;
@@ -787,16 +802,14 @@ __device__ __forceinline__ void store_c1fold(const GemmArgs& g, int mrow0, int n
       for (int q = 0; q < 4; ++q) {
         const int m = mrow0 + i * 32 + 8 * q + 4 * h + (l32 & 3);
         if (m >= g.M) continue;
-        int b, t1, f1;
-        row_btf(g, m, b, t1, f1);
-        const long pix = ((long)b * g.cm_T1 + t1) * g.cm_F1 + f1;
-        const uint32_t w = g.cm_bits[pix * g.cm_bw + (n >> 5)] >> (n & 31);
-        const float* xp = g.c1_x + ((long)b * g.c1_T + 2 * t1) * g.c1_F + 2 * f1;
+        const uint32_t w = wrow[i][q][j] >> sh;
+        const float* xp = xrow[i][q];
         float pt[9];
 #pragma unroll
         for (int kt = 0; kt < 3; ++kt)
 #pragma unroll
-          for (int kf = 0; kf < 3; ++kf) pt[kt * 3 + kf] = xp[kt * g.c1_F + kf];
+          for (int kf = 0; kf < 3; ++kf)
+            pt[kt * 3 + kf] = xp[kt * g.c1_F + kf];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float d = (w >> e) & 1u ? acc[i][j][4 * q + e] : 0.f;
